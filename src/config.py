@@ -1,0 +1,137 @@
+"""
+Configuration objects shared by every layer of the engine.
+
+`ModelConfig` keeps the reference's six leading fields and their order
+(`/root/reference/src/config.py:12-20`) so `ModelConfig("m", "/path", 8, 32)`
+keeps working; everything after them is new and describes how a real model
+session is placed on MI355X GPUs (architecture preset, dtype, tensor-parallel
+degree, prefill/decode role, paged-KV geometry, HBM budget).
+
+`EngineConfig` collects the continuous-batching scheduler knobs and
+`DeploymentConfig` is the coordinator topology that `examples/demo_config.yaml`
+(promised at `/root/reference/README.md:39`) is parsed into.
+"""
+
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field, asdict
+from typing import Any, Dict, List, Optional
+
+
+@dataclass
+class ModelConfig:
+    """Configuration for a model served by a worker.
+
+    The first six fields are the reference contract. `arch` selects the
+    backend: ``"mock"`` (FakeModel echo, CPU), ``"llama"`` or ``"mixtral"``
+    (GPU engine). `preset` names an architecture preset from
+    :mod:`src.models.presets` (e.g. ``"llama3-8b"``); `model_path` may point at
+    a safetensors directory, otherwise weights are random-initialised on device.
+    """
+
+    model_name: str
+    model_path: str
+    batch_size: int = 1
+    max_batch_size: int = 32
+    input_schema: Optional[Dict[str, Any]] = None
+    output_schema: Optional[Dict[str, Any]] = None
+    # --- MI355X engine extensions -------------------------------------------
+    arch: str = "mock"
+    preset: Optional[str] = None
+    dtype: str = "bfloat16"
+    tp_size: int = 1
+    role: str = "both"                 # "prefill" | "decode" | "both"
+    kv_block_size: int = 16
+    max_model_len: int = 4096
+    max_num_batched_tokens: int = 16384
+    gpu_memory_fraction: float = 0.90
+    num_kv_blocks: Optional[int] = None  # override the HBM-derived block count
+    enable_prefix_caching: bool = True
+    use_cuda_graph: bool = True        # hipGraph capture of decode steps
+    max_latency_ms: float = 10.0
+    seed: int = 0
+    overrides: Dict[str, Any] = field(default_factory=dict)
+
+    def to_dict(self) -> Dict[str, Any]:
+        return asdict(self)
+
+    @classmethod
+    def from_dict(cls, d: Dict[str, Any]) -> "ModelConfig":
+        known = {f for f in cls.__dataclass_fields__}  # type: ignore[attr-defined]
+        kwargs = {k: v for k, v in d.items() if k in known}
+        extra = {k: v for k, v in d.items() if k not in known}
+        cfg = cls(**kwargs)
+        if extra:
+            cfg.overrides.update(extra)
+        return cfg
+
+
+@dataclass
+class EngineConfig:
+    """Continuous-batching scheduler configuration (one engine per worker)."""
+
+    max_num_seqs: int = 32
+    max_num_batched_tokens: int = 16384
+    max_latency_ms: float = 10.0       # admission wait bound (the reference Batcher knob)
+    block_size: int = 16
+    num_kv_blocks: Optional[int] = None
+    gpu_memory_fraction: float = 0.90
+    enable_prefix_caching: bool = True
+    kv_block_ttl_s: Optional[float] = None  # TTL for cached (unreferenced) KV blocks
+    use_cuda_graph: bool = True
+    graph_batch_sizes: List[int] = field(default_factory=lambda: [1, 2, 4, 8, 16, 24, 32])
+    decode_partition_size: int = 256
+
+
+@dataclass
+class WorkerSpec:
+    worker_id: str
+    address: str
+    shard_id: int = 0
+    gpu: Optional[int] = None
+    role: str = "both"
+
+
+@dataclass
+class DeploymentConfig:
+    """Coordinator topology (models, shards, workers, strategies)."""
+
+    listen_host: str = "127.0.0.1"
+    listen_port: int = 9000
+    strategy: str = "round_robin"
+    batch_max_size: int = 32
+    batch_max_latency_ms: float = 10.0
+    cache_size: int = 10000
+    cache_policy: str = "lru"
+    cache_ttl_s: Optional[float] = None
+    max_retries: int = 2
+    request_timeout_s: float = 600.0
+    health_check_interval: float = 5.0
+    models: List[ModelConfig] = field(default_factory=list)
+    workers: List[WorkerSpec] = field(default_factory=list)
+
+    @classmethod
+    def from_dict(cls, d: Dict[str, Any]) -> "DeploymentConfig":
+        d = dict(d)
+        models = [ModelConfig.from_dict(m) for m in d.pop("models", [])]
+        workers = [WorkerSpec(**w) for w in d.pop("workers", [])]
+        known = {f for f in cls.__dataclass_fields__}  # type: ignore[attr-defined]
+        cfg = cls(**{k: v for k, v in d.items() if k in known})
+        cfg.models, cfg.workers = models, workers
+        return cfg
+
+    @classmethod
+    def from_yaml(cls, path: str) -> "DeploymentConfig":
+        import yaml
+
+        with open(path) as f:
+            data = yaml.safe_load(f) or {}
+        return cls.from_dict(data)
+
+
+def env_flag(name: str, default: bool = False) -> bool:
+    v = os.environ.get(name)
+    if v is None:
+        return default
+    return v.strip().lower() in ("1", "true", "yes", "on")

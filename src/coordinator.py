@@ -1,0 +1,442 @@
+"""
+Coordinator: the serving front door.
+
+The reference documents it (`/root/reference/README.md:27,56-60,109`,
+`docs/router_vs_load_balancer.md:41-57`) but never ships it. Request flow:
+
+    client ──framed JSON──▶ Coordinator.handle_request
+       ├─ validate {"model", "inputs", ["version"], ["request_key"], ["cache"]}
+       ├─ response cache (KVCache) hit → reply            (README.md:57-60)
+       ├─ shard  = Router.route_request(model, version, request_key)   (hash affinity + failover)
+       ├─ fut    = Batcher.add_request(model, "version#shard", inputs)  (max_batch / max_latency admission)
+       │     batch_callback → LoadBalancer.pick(group=shard) → RPC to the worker
+       │       "batch"  dispatch: one infer_batch RPC per flushed batch (coalesced; mock models)
+       │       "stream" dispatch: one infer RPC per request, all in flight at once; the worker's
+       │                 continuous-batching engine re-batches them per token step (LLMs)
+       │     failure → LB.record(failure) + Router.mark_worker_failure → retry on another
+       │               worker of the shard, then on another healthy shard (README.md:60 retries)
+       ├─ await fut → cache.set → reply, or ``op:"submit"`` returns a request_id to poll
+       └─ Tracer marks every stage (TTFT/TPOT come back in the LLM outputs)
+
+Workers join through ``{"op":"register"}`` (the handshake of README.md:85) or
+are listed statically (``--worker host:port``, or ``examples/demo_config.yaml``).
+"""
+
+from __future__ import annotations
+
+import asyncio
+import contextlib
+import hashlib
+import json
+import logging
+import os
+import sys
+import time
+from typing import Any, Dict, List, Optional, Tuple
+
+if __package__ in (None, ""):  # `python src/coordinator.py`
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from src.batcher import Batcher  # noqa: E402
+from src.config import DeploymentConfig  # noqa: E402
+from src.kvstore import KVCache  # noqa: E402
+from src.load_balancer import LoadBalancer, LoadBalancerStrategy  # noqa: E402
+from src.model_registry import ModelRegistry, rendezvous_score  # noqa: E402
+from src.router import Router, WorkerHealth  # noqa: E402
+from src.rpc import RPCClient, RPCError  # noqa: E402
+from src.utils import (  # noqa: E402
+    GLOBAL_TRACER,
+    ProtocolError,
+    new_request_id,
+    pack_frame,
+    read_message,
+    setup_logging,
+)
+
+logger = logging.getLogger(__name__)
+
+DEFAULT_VERSION = "1.0"
+
+
+class Coordinator:
+    def __init__(
+        self,
+        host: str = "127.0.0.1",
+        port: int = 9000,
+        strategy: str = "round_robin",
+        max_batch_size: int = 32,
+        max_latency_ms: float = 10.0,
+        cache_size: int = 10000,
+        cache_policy: str = "lru",
+        cache_ttl_s: Optional[float] = None,
+        max_retries: int = 2,
+        request_timeout_s: float = 600.0,
+        health_check_interval: float = 5.0,
+        dispatch: Optional[str] = None,
+    ):
+        self.host, self.port = host, port
+        self.strategy = LoadBalancerStrategy(strategy)
+        self.max_retries = max_retries
+        self.request_timeout_s = request_timeout_s
+        self.health_check_interval = health_check_interval
+        self.dispatch_override = dispatch
+        self.registry = ModelRegistry()
+        self.router = Router(self.registry, health_check_interval=health_check_interval)
+        self.lbs: Dict[str, LoadBalancer] = {}
+        self.cache = KVCache(max_size=cache_size, eviction_policy=cache_policy, default_ttl=cache_ttl_s)
+        self.batcher = Batcher(max_batch_size=max_batch_size, max_latency_ms=max_latency_ms,
+                               batch_callback=self._batch_callback)
+        self.rpc = RPCClient(max_idle_per_host=512)
+        self.tracer = GLOBAL_TRACER
+        self.server: Optional[asyncio.AbstractServer] = None
+        self._pending: Dict[str, asyncio.Task] = {}
+        self._results: KVCache = KVCache(max_size=100000, default_ttl=3600)
+        self._model_arch: Dict[str, str] = {}
+        self._shard_ids: Dict[str, int] = {}
+        self.stats = {"requests": 0, "errors": 0, "cache_hits": 0, "retries": 0, "registrations": 0}
+
+    @classmethod
+    def from_config(cls, cfg: DeploymentConfig) -> "Coordinator":
+        return cls(host=cfg.listen_host, port=cfg.listen_port, strategy=cfg.strategy,
+                   max_batch_size=cfg.batch_max_size, max_latency_ms=cfg.batch_max_latency_ms,
+                   cache_size=cfg.cache_size, cache_policy=cfg.cache_policy, cache_ttl_s=cfg.cache_ttl_s,
+                   max_retries=cfg.max_retries, request_timeout_s=cfg.request_timeout_s,
+                   health_check_interval=cfg.health_check_interval)
+
+    # ----------------------------------------------------------- lifecycle
+    async def start(self) -> int:
+        await self.batcher.start()
+        await self.router.start()
+        for lb in self.lbs.values():
+            await lb.start()
+        self.server = await asyncio.start_server(self._handle_connection, self.host, self.port, limit=1 << 26)
+        self.port = self.server.sockets[0].getsockname()[1]
+        logger.info("Coordinator listening on %s:%d", self.host, self.port)
+        return self.port
+
+    async def stop(self) -> None:
+        if self.server:
+            self.server.close()
+            with contextlib.suppress(Exception):
+                await asyncio.wait_for(self.server.wait_closed(), 2.0)
+        await self.batcher.stop()
+        await self.router.stop()
+        for lb in self.lbs.values():
+            await lb.stop()
+        for t in self._pending.values():
+            t.cancel()
+        self.rpc.close()
+
+    # -------------------------------------------------------- membership
+    def _lb(self, model: str, version: str) -> LoadBalancer:
+        key = f"{model}:{version}"
+        lb = self.lbs.get(key)
+        if lb is None:
+            lb = self.lbs[key] = LoadBalancer(strategy=self.strategy,
+                                              health_check_interval=self.health_check_interval)
+            if self.server is not None:
+                asyncio.get_event_loop().create_task(lb.start())
+        return lb
+
+    def register_worker(self, worker_id: str, address: str, models: Dict[str, Dict[str, Any]],
+                        metadata: Optional[Dict[str, Any]] = None, healthy: bool = True) -> None:
+        """Add a worker and the models it serves. ``metadata["shard_id"]``
+        puts it into an existing shard (replica); otherwise it forms a new one."""
+        metadata = dict(metadata or {})
+        self.router.register_worker(worker_id, address, metadata, healthy=healthy)
+        for name, mcfg in models.items():
+            mcfg = mcfg or {}
+            version = str(mcfg.get("overrides", {}).get("version", mcfg.get("version", DEFAULT_VERSION)))
+            if self.registry.get_model_version(name, version) is None:
+                self.registry.register_model(
+                    name, version, mcfg.get("model_path", ""), mcfg.get("input_schema") or {},
+                    mcfg.get("output_schema") or {}, batch_size=mcfg.get("batch_size", 1),
+                    max_batch_size=mcfg.get("max_batch_size", 32),
+                    metadata={"arch": mcfg.get("arch", "mock"), "preset": mcfg.get("preset")})
+            self._model_arch[name] = mcfg.get("arch", "mock")
+            shard_id = metadata.get("shard_id")
+            if shard_id is None:
+                key = f"{name}:{version}"
+                shard_id = self._shard_ids.get(key, 0)
+                self._shard_ids[key] = shard_id + 1
+            self.registry.add_shard(name, version, int(shard_id), worker_id, metadata)
+            self._lb(name, version).register_worker(worker_id, address, group=str(shard_id))
+        self.stats["registrations"] += 1
+
+    def unregister_worker(self, worker_id: str) -> None:
+        self.router.unregister_worker(worker_id)
+        for lb in self.lbs.values():
+            lb.unregister_worker(worker_id)
+
+    async def add_static_worker(self, address: str, attempts: int = 100) -> bool:
+        """Discover a worker listed on the command line via its health RPC."""
+        for _ in range(attempts):
+            ok, _, rep = await self.rpc.probe(address, 2.0)
+            if ok and rep:
+                wid = rep.get("worker_id", address)
+                self.register_worker(wid, address, {m: {} for m in rep.get("models", [])})
+                return True
+            await asyncio.sleep(0.2)
+        logger.error("static worker %s never answered", address)
+        return False
+
+    # --------------------------------------------------------------- serve
+    async def _handle_connection(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
+        try:
+            while True:
+                try:
+                    msg, mode, codec = await read_message(reader)
+                except (asyncio.IncompleteReadError, ConnectionError):
+                    break
+                except (ProtocolError, ValueError) as e:
+                    with contextlib.suppress(Exception):
+                        writer.write(pack_frame({"error": f"bad request: {e}", "success": False}))
+                        await writer.drain()
+                    break
+                if mode == "eof":
+                    break
+                resp = await self.handle_message(msg)
+                if mode == "legacy":
+                    writer.write(json.dumps(resp).encode())
+                    await writer.drain()
+                    break
+                writer.write(pack_frame(resp, codec))
+                await writer.drain()
+        finally:
+            with contextlib.suppress(Exception):
+                writer.close()
+
+    async def handle_message(self, msg: Any) -> Dict[str, Any]:
+        if not isinstance(msg, dict):
+            return {"error": "Request must be a JSON object", "success": False}
+        op = msg.get("op", "infer")
+        if op == "infer":
+            return await self.handle_request(msg)
+        if op == "submit":
+            rid = msg.get("request_id") or new_request_id()
+            msg = dict(msg, request_id=rid)
+            task = asyncio.create_task(self.handle_request(msg))
+            self._pending[rid] = task
+            task.add_done_callback(lambda t, r=rid: self._finish_async(r, t))
+            return {"success": True, "request_id": rid, "status": "pending"}
+        if op == "result":
+            rid = msg.get("request_id")
+            res = self._results.get(rid)
+            if res is not None:
+                return res
+            if rid in self._pending:
+                return {"success": True, "request_id": rid, "status": "pending"}
+            return {"error": f"unknown request_id {rid!r}", "success": False}
+        if op == "register":
+            self.register_worker(msg["worker_id"], msg["address"], msg.get("models", {}), msg.get("metadata"))
+            return {"success": True}
+        if op == "unregister":
+            self.unregister_worker(msg["worker_id"])
+            return {"success": True}
+        if op == "health":
+            return {"success": True, "role": "coordinator", "workers": len(self.router.workers)}
+        if op == "stats":
+            return {"success": True, "stats": await self.get_stats()}
+        return {"error": f"unknown op {op!r}", "success": False}
+
+    def _finish_async(self, rid: str, task: asyncio.Task) -> None:
+        self._pending.pop(rid, None)
+        if task.cancelled():
+            return
+        exc = task.exception()
+        res = {"error": str(exc), "success": False} if exc else task.result()
+        res = dict(res, request_id=rid, status="done")
+        self._results.set(rid, res)
+
+    @staticmethod
+    def _cache_key(model: str, version: str, inputs: Any) -> Optional[str]:
+        try:
+            blob = json.dumps([model, version, inputs], sort_keys=True, separators=(",", ":"))
+        except (TypeError, ValueError):
+            return None
+        return hashlib.blake2b(blob.encode(), digest_size=16).hexdigest()
+
+    def _cacheable(self, model: str, msg: Dict[str, Any]) -> bool:
+        if not msg.get("cache", True):
+            return False
+        if self._model_arch.get(model, "mock") == "mock":
+            return True
+        inp = msg.get("inputs")
+        # Only deterministic (greedy) generations are safe to serve from cache.
+        return isinstance(inp, dict) and float(inp.get("temperature", 0.0)) == 0.0
+
+    async def handle_request(self, msg: Dict[str, Any]) -> Dict[str, Any]:
+        self.stats["requests"] += 1
+        rid = msg.get("request_id") or new_request_id()
+        tr = self.tracer
+        tr.mark(rid, "coord.recv")
+        model = msg.get("model")
+        inputs = msg.get("inputs")
+        if not model or inputs is None:
+            self.stats["errors"] += 1
+            return {"error": "Missing required fields: model and inputs are required", "success": False}
+        version = str(msg.get("version") or self.registry.latest_version(model) or DEFAULT_VERSION)
+        if self.registry.get_model_version(model, version) is None:
+            self.stats["errors"] += 1
+            return {"error": f"Model '{model}' version '{version}' not registered", "success": False}
+        ckey = self._cache_key(model, version, inputs) if self._cacheable(model, msg) else None
+        if ckey is not None:
+            hit = self.cache.get(ckey)
+            if hit is not None:
+                self.stats["cache_hits"] += 1
+                tr.mark(rid, "coord.reply")
+                return dict(hit, cached=True, request_id=rid)
+        key = str(msg.get("request_key") or rid)
+        shard = self.router.route_request(model, version, key)
+        if shard is None:
+            self.stats["errors"] += 1
+            return {"error": f"no healthy shard for {model}:{version}", "success": False}
+        tr.mark(rid, "coord.routed")
+        try:
+            fut = await self.batcher.add_request(model, f"{version}#{shard.shard_id}",
+                                                 {"inputs": inputs, "request_id": rid, "key": key})
+            resp = await asyncio.wait_for(fut, self.request_timeout_s)
+        except Exception as e:
+            self.stats["errors"] += 1
+            return {"error": str(e) or type(e).__name__, "success": False, "request_id": rid}
+        tr.mark(rid, "coord.reply")
+        if resp.get("success") and ckey is not None:
+            self.cache.set(ckey, {k: v for k, v in resp.items() if k != "request_id"})
+        if not resp.get("success"):
+            self.stats["errors"] += 1
+        resp.setdefault("request_id", rid)
+        return resp
+
+    # ------------------------------------------------------------ dispatch
+    def _dispatch_mode(self, model: str) -> str:
+        if self.dispatch_override:
+            return self.dispatch_override
+        return "batch" if self._model_arch.get(model, "mock") == "mock" else "stream"
+
+    def _candidates(self, model: str, version: str, shard_id: int, key: str) -> List[Tuple[str, str]]:
+        """Ordered worker candidates: LB choice in the routed shard first, then
+        the shard's other healthy workers, then other healthy shards by key affinity."""
+        lb = self._lb(model, version)
+        out: List[Tuple[str, str]] = []
+        first = lb.pick(group=str(shard_id))
+        if first:
+            out.append(first)
+        for w, addr in lb.workers.items():
+            if lb.groups.get(w) == str(shard_id) and lb.is_healthy(w) and (w, addr) not in out:
+                out.append((w, addr))
+        others = [s for s in self.router.healthy_shards(model, version) if s.shard_id != shard_id]
+        others.sort(key=lambda s: -rendezvous_score(key, s.shard_id))
+        for s in others:
+            p = lb.pick(group=str(s.shard_id))
+            if p and p not in out:
+                out.append(p)
+        return out
+
+    async def _send(self, model: str, version: str, shard_id: int, key: str, msg: Dict[str, Any]) -> Dict[str, Any]:
+        lb = self._lb(model, version)
+        last_err = "no worker available"
+        tried = 0
+        for wid, addr in self._candidates(model, version, shard_id, key):
+            if tried > self.max_retries:
+                break
+            if tried:
+                self.stats["retries"] += 1
+            tried += 1
+            try:
+                async with lb.track(wid):
+                    rep = await self.rpc.call(addr, msg, timeout=self.request_timeout_s)
+                    if not isinstance(rep, dict):
+                        raise RPCError("malformed reply")
+                    if not rep.get("success") and rep.get("retryable"):
+                        raise RPCError(rep.get("error", "worker error"))
+                self.router.mark_worker_success(wid)
+                return rep
+            except (RPCError, OSError, asyncio.TimeoutError) as e:
+                last_err = f"{wid}: {e}"
+                self.router.mark_worker_failure(wid)
+                logger.warning("dispatch to %s failed (%s); retrying", wid, e)
+        return {"error": last_err, "success": False}
+
+    async def _batch_callback(self, model: str, vkey: str, items: List[Dict[str, Any]]) -> List[Any]:
+        version, _, sid = vkey.partition("#")
+        shard_id = int(sid)
+        key = items[0]["key"]
+        for it in items:
+            self.tracer.mark(it["request_id"], "coord.dispatch")
+        if self._dispatch_mode(model) == "batch":
+            rep = await self._send(model, version, shard_id, key,
+                                   {"op": "infer_batch", "model": model,
+                                    "inputs_list": [it["inputs"] for it in items]})
+            if not rep.get("success"):
+                return [dict(rep) for _ in items]
+            outs = rep["outputs_list"]
+            return [{"model": model, "outputs": o, "worker_id": rep.get("worker_id"), "success": True}
+                    for o in outs]
+        return [self._send(model, version, shard_id, it["key"],
+                           {"op": "infer", "model": model, "inputs": it["inputs"], "request_id": it["request_id"]})
+                for it in items]
+
+    # ---------------------------------------------------------------- stats
+    async def get_stats(self) -> Dict[str, Any]:
+        return {
+            "coordinator": dict(self.stats),
+            "cache": self.cache.get_stats(),
+            "batcher": await self.batcher.get_stats(),
+            "router": self.router.get_stats(),
+            "load_balancers": {k: lb.get_all_stats() for k, lb in self.lbs.items()},
+            "latency": self.tracer.summary("coord.recv", "coord.reply"),
+            "workers": {w: self.router.get_worker_info(w) for w in self.router.workers},
+        }
+
+    def healthy_worker_count(self) -> int:
+        return sum(1 for w in self.router.workers.values() if w.health == WorkerHealth.HEALTHY)
+
+
+def build_arg_parser():
+    import argparse
+
+    p = argparse.ArgumentParser(description="Coordinator (front door)")
+    p.add_argument("--listen-host", default="127.0.0.1")
+    p.add_argument("--listen-port", type=int, default=9000)
+    p.add_argument("--worker", action="append", default=[], help="host:port of a worker (repeatable)")
+    p.add_argument("--config", default=None, help="YAML deployment config (examples/demo_config.yaml)")
+    p.add_argument("--strategy", default=None,
+                   choices=[s.value for s in LoadBalancerStrategy])
+    p.add_argument("--max-batch-size", type=int, default=None)
+    p.add_argument("--max-latency-ms", type=float, default=None)
+    p.add_argument("--dispatch", default=None, choices=["batch", "stream"])
+    p.add_argument("--port-file", default=None)
+    return p
+
+
+async def main(argv=None) -> None:
+    setup_logging()
+    args = build_arg_parser().parse_args(argv)
+    cfg = DeploymentConfig.from_yaml(args.config) if args.config else DeploymentConfig()
+    cfg.listen_host = args.listen_host or cfg.listen_host
+    cfg.listen_port = args.listen_port if args.listen_port is not None else cfg.listen_port
+    if args.strategy:
+        cfg.strategy = args.strategy
+    if args.max_batch_size:
+        cfg.batch_max_size = args.max_batch_size
+    if args.max_latency_ms:
+        cfg.batch_max_latency_ms = args.max_latency_ms
+    coord = Coordinator.from_config(cfg)
+    coord.dispatch_override = args.dispatch
+    port = await coord.start()
+    addrs = list(args.worker) + [w.address for w in cfg.workers]
+    await asyncio.gather(*(coord.add_static_worker(a) for a in addrs))
+    if args.port_file:
+        with open(args.port_file + ".tmp", "w") as f:
+            f.write(str(port))
+        os.replace(args.port_file + ".tmp", args.port_file)
+    print(f"Coordinator listening on {cfg.listen_host}:{port}", flush=True)
+    try:
+        await asyncio.Event().wait()
+    finally:
+        await coord.stop()
+
+
+if __name__ == "__main__":
+    with contextlib.suppress(KeyboardInterrupt):
+        asyncio.run(main())

@@ -1,0 +1,164 @@
+"""
+Pre-processing: request normalisation and tokenisation
+(promised at `/root/reference/README.md:34,96-98`, absent from the reference).
+
+* :class:`ByteTokenizer` — a deterministic byte-level tokenizer that needs no
+  files (no network for HF downloads): ids 0/1/2 are pad/bos/eos, byte ``b``
+  is id ``b + 3``. A local HF tokenizer directory can be used instead through
+  :func:`load_tokenizer`.
+* :func:`normalize_request` — validates an LLM request's ``inputs`` and turns
+  it into :class:`GenerationInputs`.
+* :class:`PreprocPool` — pushes CPU-bound tokenisation to a separate process
+  pool ("disaggregated inference": pre/post-processing out of the worker's
+  event loop, `README.md:15,96-98`).
+"""
+
+from __future__ import annotations
+
+import asyncio
+import concurrent.futures as cf
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence
+
+PAD_ID, BOS_ID, EOS_ID = 0, 1, 2
+_BYTE_OFFSET = 3
+
+
+class ByteTokenizer:
+    """Byte-level tokenizer. Any id ≥ 259 (a random-init model emits them)
+    decodes to a byte by folding it into range, so detokenisation is total."""
+
+    def __init__(self, vocab_size: int = 128256):
+        self.vocab_size = vocab_size
+        self.pad_token_id, self.bos_token_id, self.eos_token_id = PAD_ID, BOS_ID, EOS_ID
+
+    def encode(self, text: str, add_bos: bool = True) -> List[int]:
+        ids = [b + _BYTE_OFFSET for b in text.encode("utf-8")]
+        return ([BOS_ID] + ids) if add_bos else ids
+
+    def decode(self, ids: Sequence[int], skip_special: bool = True) -> str:
+        out = bytearray()
+        for i in ids:
+            if i < _BYTE_OFFSET:
+                if not skip_special:
+                    out += b"<" + str(i).encode() + b">"
+                continue
+            out.append((i - _BYTE_OFFSET) % 256)
+        return out.decode("utf-8", errors="replace")
+
+
+def load_tokenizer(path: Optional[str] = None, vocab_size: int = 128256):
+    """A local HuggingFace tokenizer when ``path`` holds one, else ByteTokenizer."""
+    if path:
+        try:
+            from transformers import AutoTokenizer  # type: ignore
+
+            return AutoTokenizer.from_pretrained(path, local_files_only=True)
+        except Exception:
+            pass
+    return ByteTokenizer(vocab_size)
+
+
+@dataclass
+class SamplingParams:
+    max_tokens: int = 16
+    temperature: float = 0.0          # 0 → greedy
+    top_k: int = 0                    # 0 → disabled
+    top_p: float = 1.0
+    seed: Optional[int] = None
+    ignore_eos: bool = False
+    stop_token_ids: List[int] = field(default_factory=list)
+
+    def __post_init__(self):
+        if self.max_tokens < 1:
+            raise ValueError("max_tokens must be >= 1")
+        if self.temperature < 0:
+            raise ValueError("temperature must be >= 0")
+        if not (0.0 < self.top_p <= 1.0):
+            raise ValueError("top_p must be in (0, 1]")
+        if self.top_k < 0:
+            raise ValueError("top_k must be >= 0")
+
+    @property
+    def greedy(self) -> bool:
+        return self.temperature == 0.0 or self.top_k == 1
+
+
+@dataclass
+class GenerationInputs:
+    prompt_token_ids: List[int]
+    sampling: SamplingParams
+    prompt: Optional[str] = None
+    return_text: bool = True
+
+
+_SAMPLING_KEYS = ("max_tokens", "temperature", "top_k", "top_p", "seed", "ignore_eos", "stop_token_ids")
+
+
+def normalize_request(inputs: Any, tokenizer=None, max_model_len: Optional[int] = None) -> GenerationInputs:
+    """Accepts a prompt string, a token-id list, or a dict with ``prompt`` /
+    ``prompt_token_ids`` plus sampling fields."""
+    tok = tokenizer or ByteTokenizer()
+    if isinstance(inputs, str):
+        inputs = {"prompt": inputs}
+    elif isinstance(inputs, (list, tuple)) and all(isinstance(x, int) for x in inputs):
+        inputs = {"prompt_token_ids": list(inputs)}
+    if not isinstance(inputs, dict):
+        raise ValueError("LLM inputs must be a prompt string, a token id list, or an object")
+    prompt = inputs.get("prompt")
+    ids = inputs.get("prompt_token_ids")
+    if ids is None:
+        if not isinstance(prompt, str):
+            raise ValueError("inputs need 'prompt' (str) or 'prompt_token_ids' (list[int])")
+        ids = tok.encode(prompt)
+    if not ids:
+        raise ValueError("empty prompt")
+    ids = [int(x) for x in ids]
+    vs = getattr(tok, "vocab_size", None)
+    if vs and any(x < 0 or x >= vs for x in ids):
+        raise ValueError("prompt token id out of vocabulary range")
+    sp = SamplingParams(**{k: inputs[k] for k in _SAMPLING_KEYS if k in inputs})
+    if max_model_len is not None and len(ids) + sp.max_tokens > max_model_len:
+        raise ValueError(f"prompt ({len(ids)}) + max_tokens ({sp.max_tokens}) exceeds max_model_len {max_model_len}")
+    return GenerationInputs(prompt_token_ids=ids, sampling=sp, prompt=prompt,
+                            return_text=bool(inputs.get("return_text", True)))
+
+
+def _encode_batch(texts: List[str], vocab_size: int) -> List[List[int]]:
+    tok = ByteTokenizer(vocab_size)
+    return [tok.encode(t) for t in texts]
+
+
+def _decode_batch(seqs: List[List[int]], vocab_size: int) -> List[str]:
+    tok = ByteTokenizer(vocab_size)
+    return [tok.decode(s) for s in seqs]
+
+
+class PreprocPool:
+    """Tokenise / detokenise in worker processes so the serving loop never
+    spends its own time on it."""
+
+    def __init__(self, processes: int = 2, vocab_size: int = 128256):
+        self.vocab_size = vocab_size
+        self._pool = cf.ProcessPoolExecutor(max_workers=processes)
+
+    async def encode(self, texts: List[str]) -> List[List[int]]:
+        loop = asyncio.get_running_loop()
+        return await loop.run_in_executor(self._pool, _encode_batch, texts, self.vocab_size)
+
+    async def decode(self, seqs: List[List[int]]) -> List[str]:
+        loop = asyncio.get_running_loop()
+        return await loop.run_in_executor(self._pool, _decode_batch, seqs, self.vocab_size)
+
+    def close(self) -> None:
+        self._pool.shutdown(wait=False, cancel_futures=True)
+
+
+def preprocess(inputs: Dict[str, Any]) -> Dict[str, Any]:
+    """Generic (non-LLM) normalisation used by the mock path: strip strings,
+    lower-case keys."""
+    if isinstance(inputs, dict):
+        return {str(k).lower(): (v.strip() if isinstance(v, str) else v) for k, v in inputs.items()}
+    if isinstance(inputs, str):
+        return inputs.strip()  # type: ignore[return-value]
+    return inputs

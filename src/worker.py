@@ -1,0 +1,396 @@
+"""
+Worker: one serving process, owning one GPU (or one TP rank group entry) and
+the model sessions on it.
+
+Public API kept from `/root/reference/src/worker.py:26-209`: ``Worker(worker_id,
+host, port)``, ``await start() -> port``, ``await shutdown()``,
+``load_model(ModelConfig)``, ``unload_model(name)``, ``get_metrics()`` and the
+in-process ``await _process_request(dict)`` the reference demos call. The wire
+request is still ``{"model", "inputs", ...}`` and the reply
+``{"model","outputs","worker_id","success"}`` / ``{"error","success":false}``
+(`worker.py:135-162`).
+
+What is new:
+
+* the model behind ``predict`` is either the reference's mock
+  (:class:`FakeModel`, ``arch="mock"``) or a real MI355X session
+  (:class:`src.engine.backend.LLMBackend`: Llama-3 / Mixtral on PyTorch-ROCm
+  with hand-written HIP kernels, paged KV in HBM, continuous batching);
+* framed messages on persistent connections (legacy unframed JSON still served);
+* an ``op`` verb: ``infer`` (default), ``infer_batch``, ``health``, ``metrics``,
+  ``load_model``, ``unload_model``, ``kv_export``/``kv_import`` (disaggregated
+  prefill → decode), ``stats``; a health probe is answered cheaply and not
+  counted as a request (the reference counted probes, `worker.py:87`);
+* a registration handshake with the coordinator (`README.md:85`);
+* ``python src/worker.py`` works as well as ``python -m src.worker``, and
+  ``--model`` / ``--arch`` / ``--preset`` select what to serve (`README.md:108`).
+"""
+
+from __future__ import annotations
+
+import asyncio
+import contextlib
+import logging
+import os
+import signal
+import sys
+import time
+from typing import Any, Dict, Optional
+
+if __package__ in (None, ""):  # `python src/worker.py`
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import psutil  # noqa: E402
+
+from src.config import ModelConfig  # noqa: E402
+from src.mock_models import FakeModel  # noqa: E402
+from src.rpc import RPCClient  # noqa: E402
+from src.utils import (  # noqa: E402
+    GLOBAL_TRACER,
+    ProtocolError,
+    pack_frame,
+    read_message,
+    setup_logging,
+)
+
+logger = logging.getLogger(__name__)
+
+
+def make_backend(config: ModelConfig):
+    """Instantiate the backend for ``config.arch``."""
+    if config.arch in ("mock", "fake", "echo"):
+        return FakeModel(config)
+    if config.arch in ("llama", "mixtral"):
+        from src.engine.backend import LLMBackend
+
+        return LLMBackend(config)
+    raise ValueError(f"unknown model arch {config.arch!r}")
+
+
+class Worker:
+    def __init__(self, worker_id: str, host: str = "0.0.0.0", port: int = 0,
+                 coordinator: Optional[str] = None, metadata: Optional[Dict[str, Any]] = None,
+                 install_signal_handlers: bool = True):
+        self.worker_id = worker_id
+        self.host = host
+        self.port = port
+        self.coordinator = coordinator
+        self.metadata = metadata or {}
+        self.install_signal_handlers = install_signal_handlers
+        self.models: Dict[str, Any] = {}
+        self.server: Optional[asyncio.AbstractServer] = None
+        self._stop_event = asyncio.Event()
+        self._start_time = time.time()
+        self._request_count = 0
+        self._error_count = 0
+        self._probe_count = 0
+        self._active = 0
+        self._conns: set = set()
+        self._tracer = GLOBAL_TRACER
+        self._process = psutil.Process()
+
+    # ------------------------------------------------------------ lifecycle
+    async def start(self) -> int:
+        loop = asyncio.get_running_loop()
+        if self.install_signal_handlers:
+            for sig in (signal.SIGTERM, signal.SIGINT):
+                with contextlib.suppress(NotImplementedError, RuntimeError, ValueError):
+                    loop.add_signal_handler(sig, lambda s=sig: asyncio.create_task(self.shutdown(s)))
+        for m in self.models.values():
+            if hasattr(m, "start"):
+                await m.start()
+        self.server = await asyncio.start_server(self._handle_connection, host=self.host, port=self.port,
+                                                 limit=1 << 26)
+        self.port = self.server.sockets[0].getsockname()[1]
+        logger.info("Worker %s listening on %s:%d", self.worker_id, self.host, self.port)
+        if self.coordinator:
+            asyncio.create_task(self._register_with_coordinator())
+        return self.port
+
+    @property
+    def address(self) -> str:
+        host = "127.0.0.1" if self.host in ("0.0.0.0", "") else self.host
+        return f"{host}:{self.port}"
+
+    async def _register_with_coordinator(self, attempts: int = 60) -> bool:
+        client = RPCClient(max_idle_per_host=1)
+        msg = {
+            "op": "register",
+            "worker_id": self.worker_id,
+            "address": self.address,
+            "models": {name: getattr(m, "config", ModelConfig(name, "")).to_dict()
+                       for name, m in self.models.items()},
+            "metadata": self.metadata,
+        }
+        try:
+            for i in range(attempts):
+                try:
+                    rep = await client.call(self.coordinator, msg, timeout=5.0)
+                    if isinstance(rep, dict) and rep.get("success"):
+                        logger.info("Registered with coordinator %s", self.coordinator)
+                        return True
+                except Exception as e:  # coordinator not up yet
+                    logger.debug("registration attempt %d failed: %s", i, e)
+                await asyncio.sleep(min(0.25 * (i + 1), 2.0))
+            return False
+        finally:
+            client.close()
+
+    async def shutdown(self, sig=None) -> None:
+        if sig:
+            logger.info("Received signal %s, shutting down", getattr(sig, "name", sig))
+        if self.server:
+            self.server.close()
+            for w in list(self._conns):
+                with contextlib.suppress(Exception):
+                    w.close()
+            with contextlib.suppress(Exception):
+                await asyncio.wait_for(self.server.wait_closed(), 2.0)
+            self.server = None
+        for name in list(self.models):
+            m = self.models[name]
+            if hasattr(m, "stop"):
+                with contextlib.suppress(Exception):
+                    await m.stop()
+            self.unload_model(name)
+        self._stop_event.set()
+        if sig:
+            sys.exit(0)
+
+    async def wait_closed(self) -> None:
+        await self._stop_event.wait()
+
+    # -------------------------------------------------------------- network
+    async def _handle_connection(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
+        self._conns.add(writer)
+        try:
+            while True:
+                try:
+                    msg, mode, codec = await asyncio.wait_for(read_message(reader), timeout=3600)
+                except (asyncio.IncompleteReadError, ConnectionError, asyncio.TimeoutError):
+                    break
+                except (ProtocolError, ValueError) as e:
+                    self._error_count += 1
+                    with contextlib.suppress(Exception):
+                        writer.write(pack_frame({"error": f"bad request: {e}", "success": False}))
+                        await writer.drain()
+                    break
+                if mode == "eof":
+                    break  # TCP-connect probe: not a request
+                t0 = time.perf_counter()
+                resp = await self.handle_message(msg)
+                if mode == "legacy":
+                    import json
+
+                    writer.write(json.dumps(resp).encode())
+                    await writer.drain()
+                    break
+                writer.write(pack_frame(resp, codec))
+                await writer.drain()
+                logger.debug("request done in %.2f ms", (time.perf_counter() - t0) * 1e3)
+        finally:
+            self._conns.discard(writer)
+            with contextlib.suppress(Exception):
+                writer.close()
+
+    async def handle_message(self, msg: Any) -> Dict[str, Any]:
+        if not isinstance(msg, dict):
+            self._request_count += 1
+            self._error_count += 1
+            return {"error": "Request must be a JSON object", "success": False}
+        op = msg.get("op", "infer")
+        if op == "health":
+            self._probe_count += 1
+            return {"success": True, "worker_id": self.worker_id, "load": self.load(),
+                    "models": list(self.models)}
+        if op == "metrics":
+            return {"success": True, "metrics": self.get_metrics()}
+        if op == "load_model":
+            try:
+                ok = await asyncio.get_running_loop().run_in_executor(
+                    None, self.load_model, ModelConfig.from_dict(msg["config"]))
+                m = self.models.get(msg["config"]["model_name"])
+                if ok and m is not None and hasattr(m, "start"):
+                    await m.start()
+                return {"success": ok}
+            except Exception as e:
+                return {"error": str(e), "success": False}
+        if op == "unload_model":
+            name = msg.get("model")
+            m = self.models.get(name)
+            if m is not None and hasattr(m, "stop"):
+                await m.stop()
+            return {"success": self.unload_model(name)}
+        if op in ("infer", "infer_batch"):
+            self._request_count += 1
+            self._active += 1
+            try:
+                resp = await (self._process_batch(msg) if op == "infer_batch" else self._process_request(msg))
+            finally:
+                self._active -= 1
+            if not resp.get("success"):
+                self._error_count += 1
+            return resp
+        if op in ("kv_export", "kv_import", "engine_stats"):
+            m = self.models.get(msg.get("model"))
+            if m is None or not hasattr(m, "handle_op"):
+                return {"error": f"op {op} unsupported for model {msg.get('model')!r}", "success": False}
+            try:
+                return await m.handle_op(op, msg)
+            except Exception as e:
+                return {"error": str(e), "success": False}
+        return {"error": f"unknown op {op!r}", "success": False}
+
+    # ------------------------------------------------------------ inference
+    async def _process_request(self, request: Dict[str, Any]) -> Dict[str, Any]:
+        if not isinstance(request, dict):
+            return {"error": "Request must be a JSON object", "success": False}
+        model_name = request.get("model")
+        inputs = request.get("inputs")
+        if not model_name or inputs is None:
+            return {"error": "Missing required fields: model and inputs are required", "success": False}
+        model = self.models.get(model_name)
+        if model is None:
+            return {"error": f"Model '{model_name}' not found", "success": False}
+        rid = request.get("request_id")
+        try:
+            if rid:
+                self._tracer.mark(rid, "worker.recv")
+            outputs = await model.predict(inputs)
+            if rid:
+                self._tracer.mark(rid, "worker.done")
+            resp = {"model": model_name, "outputs": outputs, "worker_id": self.worker_id, "success": True}
+            if rid:
+                resp["request_id"] = rid
+            return resp
+        except Exception as e:
+            logger.error("Error processing request: %s", e)
+            return {"error": str(e), "success": False}
+
+    async def _process_batch(self, request: Dict[str, Any]) -> Dict[str, Any]:
+        model_name = request.get("model")
+        inputs_list = request.get("inputs_list")
+        if not model_name or not isinstance(inputs_list, list):
+            return {"error": "infer_batch needs model and inputs_list", "success": False}
+        model = self.models.get(model_name)
+        if model is None:
+            return {"error": f"Model '{model_name}' not found", "success": False}
+        try:
+            if hasattr(model, "predict_batch"):
+                outs = await model.predict_batch(inputs_list)
+            else:
+                outs = await asyncio.gather(*(model.predict(x) for x in inputs_list))
+            return {"model": model_name, "outputs_list": outs, "worker_id": self.worker_id, "success": True}
+        except Exception as e:
+            logger.error("Error processing batch: %s", e)
+            return {"error": str(e), "success": False}
+
+    # --------------------------------------------------------------- models
+    def load_model(self, config: ModelConfig) -> bool:
+        if config.model_name in self.models:
+            logger.warning("Model '%s' is already loaded", config.model_name)
+            return True
+        try:
+            self.models[config.model_name] = make_backend(config)
+            logger.info("Loaded model '%s' (%s) on worker %s", config.model_name, config.arch, self.worker_id)
+            return True
+        except Exception as e:
+            logger.error("Error loading model '%s': %s", config.model_name, e)
+            return False
+
+    def unload_model(self, model_name: str) -> bool:
+        m = self.models.pop(model_name, None)
+        if m is None:
+            return False
+        with contextlib.suppress(Exception):
+            m.close()
+        return True
+
+    # -------------------------------------------------------------- metrics
+    def load(self) -> float:
+        loads = [m.load() for m in self.models.values() if hasattr(m, "load")]
+        return max(loads) if loads else float(self._active)
+
+    def get_metrics(self) -> Dict[str, Any]:
+        mem = self._process.memory_info()
+        try:
+            conns = len(self._process.net_connections())
+        except Exception:
+            conns = -1
+        out = {
+            "worker_id": self.worker_id,
+            "start_time": self._start_time,
+            "uptime": time.time() - self._start_time,
+            "request_count": self._request_count,
+            "error_count": self._error_count,
+            "probe_count": self._probe_count,
+            "active_requests": self._active,
+            "loaded_models": list(self.models.keys()),
+            "model_metrics": {n: m.get_metrics() for n, m in self.models.items()},
+            "memory_usage_mb": mem.rss / (1024 * 1024),
+            "cpu_percent": self._process.cpu_percent(),
+            "thread_count": self._process.num_threads(),
+            "connections": conns,
+        }
+        out.update(self.metadata)
+        return out
+
+
+def build_arg_parser():
+    import argparse
+
+    p = argparse.ArgumentParser(description="MI355X inference worker")
+    p.add_argument("--worker-id", default=None, help="Unique worker ID (default: worker-<port>)")
+    p.add_argument("--host", default="0.0.0.0")
+    p.add_argument("--port", type=int, default=0, help="0 = OS-assigned")
+    p.add_argument("--model", default="test-model", help="name to serve the model under")
+    p.add_argument("--arch", default="mock", choices=["mock", "llama", "mixtral"])
+    p.add_argument("--preset", default=None, help="architecture preset, e.g. llama3-8b")
+    p.add_argument("--model-path", default="")
+    p.add_argument("--max-batch-size", type=int, default=32)
+    p.add_argument("--max-latency-ms", type=float, default=10.0)
+    p.add_argument("--max-model-len", type=int, default=4096)
+    p.add_argument("--tp-size", type=int, default=1)
+    p.add_argument("--role", default="both", choices=["both", "prefill", "decode"])
+    p.add_argument("--mock-latency-ms", type=float, default=None,
+                   help="FakeModel latency; default = reference 50-150 ms")
+    p.add_argument("--no-graph", action="store_true", help="disable hipGraph decode capture")
+    p.add_argument("--coordinator", default=None, help="host:port to register with")
+    p.add_argument("--port-file", default=None, help="write the bound port here once listening")
+    return p
+
+
+async def main(argv=None) -> None:
+    setup_logging()
+    args = build_arg_parser().parse_args(argv)
+    overrides: Dict[str, Any] = {}
+    if args.mock_latency_ms is not None:
+        overrides["latency_s"] = args.mock_latency_ms / 1000.0
+    cfg = ModelConfig(
+        model_name=args.model, model_path=args.model_path, batch_size=min(8, args.max_batch_size),
+        max_batch_size=args.max_batch_size, arch=args.arch, preset=args.preset, tp_size=args.tp_size,
+        role=args.role, max_model_len=args.max_model_len, max_latency_ms=args.max_latency_ms,
+        use_cuda_graph=not args.no_graph, overrides=overrides,
+    )
+    worker = Worker(worker_id=args.worker_id or f"worker-{os.getpid()}", host=args.host, port=args.port,
+                    coordinator=args.coordinator,
+                    metadata={"role": args.role, "gpu": os.environ.get("HIP_VISIBLE_DEVICES")})
+    if not worker.load_model(cfg):
+        raise SystemExit(f"failed to load model {cfg.model_name}")
+    port = await worker.start()
+    if args.port_file:
+        with open(args.port_file + ".tmp", "w") as f:
+            f.write(str(port))
+        os.replace(args.port_file + ".tmp", args.port_file)
+    print(f"Worker {worker.worker_id} started on port {port}", flush=True)
+    try:
+        await worker.wait_closed()
+    except asyncio.CancelledError:
+        pass
+    finally:
+        if worker.server is not None:
+            await worker.shutdown()
+
+
+if __name__ == "__main__":
+    asyncio.run(main())

@@ -1,0 +1,130 @@
+"""End-to-end control plane on CPU (BASELINE config 1): coordinator + 2 mock
+workers as separate processes, framed and legacy wire formats, caching,
+batching, polling, registration handshake and failover when a worker dies."""
+
+import asyncio
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import pytest
+
+from src.client import InferenceClient, legacy_request
+from src.coordinator import Coordinator
+from src.utils import deserialize, pack_frame, serialize, CODEC_MSGPACK, ProtocolError
+from src.worker import Worker
+from src.config import ModelConfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def spawn_worker(wid, coordinator=None, latency_ms=5):
+    fd, pf = tempfile.mkstemp()
+    os.close(fd)
+    os.unlink(pf)
+    cmd = [sys.executable, "-m", "src.worker", "--worker-id", wid, "--host", "127.0.0.1", "--port", "0",
+           "--model", "echo", "--arch", "mock", "--mock-latency-ms", str(latency_ms), "--port-file", pf]
+    if coordinator:
+        cmd += ["--coordinator", coordinator]
+    p = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    for _ in range(200):
+        if os.path.exists(pf):
+            with open(pf) as f:
+                port = int(f.read())
+            os.unlink(pf)
+            return p, f"127.0.0.1:{port}"
+        time.sleep(0.05)
+    p.kill()
+    raise RuntimeError("worker did not start")
+
+
+def test_framing_roundtrip():
+    obj = {"a": [1, 2, {"b": "x" * 10000}]}
+    assert deserialize(serialize(obj)) == obj
+    assert deserialize(serialize(obj, CODEC_MSGPACK)) == obj
+    with pytest.raises(ProtocolError):
+        deserialize(b"P" + b"junk")           # pickle refused by default
+    assert pack_frame(obj)[:4] == len(serialize(obj)).to_bytes(4, "big")
+
+
+def test_in_process_worker_api():
+    async def main():
+        w = Worker("w", host="127.0.0.1", install_signal_handlers=False)
+        assert w.load_model(ModelConfig("echo", "/x", arch="mock", overrides={"latency_s": 0}))
+        r = await w._process_request({"model": "echo", "inputs": {"x": 1}})
+        assert r["success"] and r["outputs"]["output"] == {"x": 1} and r["worker_id"] == "w"
+        assert not (await w._process_request({"model": "nope", "inputs": 1}))["success"]
+        assert not (await w._process_request({"inputs": 1}))["success"]
+        port = await w.start()
+        big = "y" * 100_000                       # > 4 KiB: the reference's read(4096) broke here
+        r = await legacy_request(f"127.0.0.1:{port}", {"model": "echo", "inputs": big})
+        assert r["success"] and r["outputs"]["output"] == big
+        c = InferenceClient(f"127.0.0.1:{port}")
+        for i in range(5):                        # persistent framed connection
+            r = await c.call({"model": "echo", "inputs": i})
+            assert r["outputs"]["output"] == i
+        h = await c.call({"op": "health"})
+        assert h["success"] and h["models"] == ["echo"]
+        m = (await c.call({"op": "metrics"}))["metrics"]
+        assert m["request_count"] == 6 and m["probe_count"] == 1
+        c.close()
+        await w.shutdown()
+    asyncio.run(main())
+
+
+def test_coordinator_two_workers_end_to_end():
+    async def main():
+        coord = Coordinator(port=0, max_batch_size=8, max_latency_ms=5, health_check_interval=0.2)
+        cport = await coord.start()
+        caddr = f"127.0.0.1:{cport}"
+        procs = []
+        try:
+            for i in range(2):
+                procs.append(spawn_worker(f"w{i}", coordinator=caddr))
+            for _ in range(200):
+                if coord.healthy_worker_count() == 2:
+                    break
+                await asyncio.sleep(0.05)
+            assert coord.healthy_worker_count() == 2
+            client = InferenceClient(caddr)
+            rs = await asyncio.gather(*(client.infer("echo", {"i": i}, cache=False) for i in range(64)))
+            assert all(r["success"] for r in rs)
+            assert [r["outputs"]["output"]["i"] for r in rs] == list(range(64))
+            assert {r["worker_id"] for r in rs} == {"w0", "w1"}       # both shards used
+            # cache: second identical request is a hit
+            a = await client.infer("echo", "same")
+            b = await client.infer("echo", "same")
+            assert not a.get("cached") and b.get("cached")
+            # request_key affinity
+            ws = {(await client.infer("echo", j, request_key="user-42", cache=False))["worker_id"] for j in range(5)}
+            assert len(ws) == 1
+            # polling mode
+            rid = await client.submit("echo", "later")
+            res = await client.result(rid, timeout=10)
+            assert res["success"] and res["outputs"]["output"] == "later"
+            # unknown model
+            assert not (await client.infer("nope", 1))["success"]
+            # legacy unframed client against the coordinator
+            r = await legacy_request(caddr, {"model": "echo", "inputs": "legacy"})
+            assert r["success"]
+            st = (await client.stats())["stats"]
+            assert st["batcher"]["avg_batch_size"] > 1.0
+            # kill the worker that owns user-42: requests fail over to the survivor
+            victim = next(iter(ws))
+            idx = int(victim[1:])
+            procs[idx][0].kill()
+            procs[idx][0].wait()
+            rs = await asyncio.gather(*(client.infer("echo", k, request_key="user-42", cache=False)
+                                        for k in range(10)))
+            assert all(r["success"] for r in rs)
+            assert {r["worker_id"] for r in rs} == {f"w{1 - idx}"}
+            client.close()
+        finally:
+            for p, _ in procs:
+                p.kill()
+                p.wait()
+            await coord.stop()
+    asyncio.run(main())
