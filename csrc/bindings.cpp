@@ -1,0 +1,296 @@
+// Torch bindings of the gfx950 kernels (module `src._C`). Each entry point
+// validates device/dtype/shape up front and throws on mismatch — a wrong shape
+// never reaches a kernel (a faulting kernel can take down every GPU on the
+// host) — then launches on the current HIP stream (graph-capture safe).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include "kernels/launchers.h"
+
+using torch::Tensor;
+
+namespace {
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+inline die::bf16_t* bf(const Tensor& t) { return reinterpret_cast<die::bf16_t*>(t.data_ptr()); }
+
+#define DIE_CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define DIE_CHECK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bfloat16")
+#define DIE_CHECK_DTYPE(x, d) TORCH_CHECK((x).scalar_type() == (d), #x " has wrong dtype")
+#define DIE_CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+#define DIE_HIP(call)                                                                 \
+  do {                                                                                \
+    hipError_t e_ = (call);                                                           \
+    TORCH_CHECK(e_ == hipSuccess, "HIP launch failed: ", hipGetErrorString(e_), " (", \
+                #call, ")");                                                          \
+  } while (0)
+
+inline void check_rows(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 2, name, " must be 2-D [rows, hidden]");
+  TORCH_CHECK(t.stride(1) == 1, name, " rows must be contiguous");
+  TORCH_CHECK(t.stride(0) % 8 == 0, name, " row stride must be a multiple of 8 elements");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+void rms_norm(Tensor out, Tensor x, Tensor w, double eps) {
+  DIE_CHECK_CUDA(x);
+  DIE_CHECK_BF16(x);
+  DIE_CHECK_BF16(out);
+  DIE_CHECK_BF16(w);
+  check_rows(x, "x");
+  check_rows(out, "out");
+  TORCH_CHECK(out.size(0) == x.size(0) && out.size(1) == x.size(1) && w.numel() == x.size(1), "rms_norm shapes");
+  TORCH_CHECK(x.size(1) <= 8 * 256 * 8, "hidden too large");
+  DIE_HIP(die::launch_rms_norm(bf(out), bf(x), bf(w), (float)eps, (int)x.size(0), (int)x.size(1), x.stride(0),
+                               out.stride(0), cur_stream()));
+}
+
+void fused_add_rms_norm(Tensor out, Tensor x, Tensor residual, Tensor w, double eps) {
+  DIE_CHECK_CUDA(x);
+  DIE_CHECK_BF16(x);
+  DIE_CHECK_BF16(out);
+  DIE_CHECK_BF16(residual);
+  DIE_CHECK_BF16(w);
+  check_rows(x, "x");
+  check_rows(out, "out");
+  DIE_CHECK_CONTIG(residual);
+  TORCH_CHECK(residual.size(0) == x.size(0) && residual.size(1) == x.size(1), "residual shape");
+  TORCH_CHECK(out.size(0) == x.size(0) && out.size(1) == x.size(1) && w.numel() == x.size(1), "norm shapes");
+  TORCH_CHECK(x.size(1) <= 8 * 256 * 8, "hidden too large");
+  DIE_HIP(die::launch_fused_add_rms_norm(bf(out), bf(x), bf(residual), bf(w), (float)eps, (int)x.size(0),
+                                         (int)x.size(1), x.stride(0), out.stride(0), cur_stream()));
+}
+
+void silu_and_mul(Tensor out, Tensor x) {
+  DIE_CHECK_CUDA(x);
+  DIE_CHECK_BF16(x);
+  DIE_CHECK_BF16(out);
+  DIE_CHECK_CONTIG(x);
+  DIE_CHECK_CONTIG(out);
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.size(1) == 2 * out.size(1) && x.size(0) == out.size(0),
+              "silu_and_mul: x [T, 2I], out [T, I]");
+  TORCH_CHECK(out.size(1) % 8 == 0, "intermediate size must be a multiple of 8");
+  DIE_HIP(die::launch_silu_and_mul(bf(out), bf(x), (int)x.size(0), (int)out.size(1), cur_stream()));
+}
+
+void check_cache(const Tensor& c, int64_t hkv, int64_t head_dim, const char* name) {
+  DIE_CHECK_CUDA(c);
+  DIE_CHECK_BF16(c);
+  DIE_CHECK_CONTIG(c);
+  TORCH_CHECK(c.dim() == 4 && c.size(1) == hkv && c.size(3) == head_dim, name,
+              " must be [num_blocks, num_kv_heads, block_size, head_dim]");
+}
+
+void rope_and_cache(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor slot_mapping, Tensor k_cache,
+                    Tensor v_cache, int64_t hq, int64_t hkv, int64_t head_dim) {
+  DIE_CHECK_CUDA(qkv);
+  DIE_CHECK_BF16(qkv);
+  check_rows(qkv, "qkv");
+  TORCH_CHECK(qkv.size(1) >= (hq + 2 * hkv) * head_dim, "qkv width < (hq + 2*hkv) * head_dim");
+  DIE_CHECK_DTYPE(positions, at::kLong);
+  DIE_CHECK_DTYPE(slot_mapping, at::kLong);
+  DIE_CHECK_DTYPE(cos_sin, at::kFloat);
+  DIE_CHECK_CONTIG(cos_sin);
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == head_dim, "cos_sin must be [max_pos, head_dim]");
+  TORCH_CHECK(positions.numel() >= qkv.size(0) && slot_mapping.numel() >= qkv.size(0), "positions/slots too short");
+  check_cache(k_cache, hkv, head_dim, "k_cache");
+  check_cache(v_cache, hkv, head_dim, "v_cache");
+  TORCH_CHECK(k_cache.sizes() == v_cache.sizes(), "k/v cache shapes differ");
+  DIE_HIP(die::launch_rope_and_cache(bf(qkv), qkv.stride(0), positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
+                                     slot_mapping.data_ptr<int64_t>(), bf(k_cache), bf(v_cache), (int)qkv.size(0),
+                                     (int)hq, (int)hkv, (int)head_dim, (int)k_cache.size(2), cur_stream()));
+}
+
+void attn_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor cu_q,
+                  Tensor ctx_lens, int64_t max_q_len, int64_t hq, int64_t hkv, double scale) {
+  DIE_CHECK_CUDA(q);
+  DIE_CHECK_BF16(q);
+  DIE_CHECK_BF16(out);
+  check_rows(q, "q");
+  DIE_CHECK_CONTIG(out);
+  const int64_t D = 128;
+  TORCH_CHECK(q.size(1) >= hq * D, "q width < hq*128 (head_dim must be 128)");
+  TORCH_CHECK(out.numel() >= q.size(0) * hq * D, "out too small");
+  TORCH_CHECK(hq % hkv == 0 && (hq / hkv) <= 32 && (32 % (hq / hkv)) == 0, "hq/hkv must divide 32");
+  check_cache(k_cache, hkv, D, "k_cache");
+  check_cache(v_cache, hkv, D, "v_cache");
+  DIE_CHECK_DTYPE(block_tables, at::kInt);
+  DIE_CHECK_DTYPE(cu_q, at::kInt);
+  DIE_CHECK_DTYPE(ctx_lens, at::kInt);
+  DIE_CHECK_CONTIG(block_tables);
+  const int64_t nseq = ctx_lens.numel();
+  TORCH_CHECK(cu_q.numel() >= nseq + 1 && block_tables.dim() == 2 && block_tables.size(0) >= nseq,
+              "cu_q / block_tables sizes");
+  DIE_HIP(die::launch_attn_prefill(bf(out), bf(q), q.stride(0), bf(k_cache), bf(v_cache),
+                                   block_tables.data_ptr<int>(), (int)block_tables.size(1), cu_q.data_ptr<int>(),
+                                   ctx_lens.data_ptr<int>(), (int)nseq, (int)max_q_len, (int)hq, (int)hkv, (int)D,
+                                   (int)k_cache.size(2), (float)scale, cur_stream()));
+}
+
+void attn_decode(Tensor out, Tensor part_o, Tensor part_ml, Tensor q, Tensor k_cache, Tensor v_cache,
+                 Tensor block_tables, Tensor ctx_lens, int64_t max_ctx, int64_t hq, int64_t hkv, double scale) {
+  DIE_CHECK_CUDA(q);
+  DIE_CHECK_BF16(q);
+  DIE_CHECK_BF16(out);
+  check_rows(q, "q");
+  DIE_CHECK_CONTIG(out);
+  const int64_t D = 128;
+  const int64_t nseq = ctx_lens.numel();
+  TORCH_CHECK(q.size(0) >= nseq && q.size(1) >= hq * D, "q shape");
+  TORCH_CHECK(out.numel() >= nseq * hq * D, "out too small");
+  TORCH_CHECK(hq % hkv == 0 && (hq / hkv) <= 32, "hq/hkv <= 32");
+  check_cache(k_cache, hkv, D, "k_cache");
+  check_cache(v_cache, hkv, D, "v_cache");
+  DIE_CHECK_DTYPE(block_tables, at::kInt);
+  DIE_CHECK_DTYPE(ctx_lens, at::kInt);
+  DIE_CHECK_CONTIG(block_tables);
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= nseq, "block_tables shape");
+  TORCH_CHECK(block_tables.size(1) * k_cache.size(2) >= max_ctx, "block table narrower than max_ctx");
+  const int maxp = die::attn_decode_max_partials((int)max_ctx);
+  DIE_CHECK_DTYPE(part_o, at::kFloat);
+  DIE_CHECK_DTYPE(part_ml, at::kFloat);
+  TORCH_CHECK(part_o.numel() >= nseq * hq * maxp * D && part_ml.numel() >= nseq * hq * maxp * 2,
+              "partial buffers too small for max_ctx");
+  DIE_HIP(die::launch_attn_decode(bf(out), part_o.data_ptr<float>(), part_ml.data_ptr<float>(), bf(q), q.stride(0),
+                                  bf(k_cache), bf(v_cache), block_tables.data_ptr<int>(), (int)block_tables.size(1),
+                                  ctx_lens.data_ptr<int>(), (int)nseq, (int)max_ctx, (int)hq, (int)hkv, (int)D,
+                                  (int)k_cache.size(2), (float)scale, cur_stream()));
+}
+
+int64_t decode_partials(int64_t max_ctx) { return die::attn_decode_max_partials((int)max_ctx); }
+
+void sample(Tensor out, Tensor logits, c10::optional<Tensor> temperature, c10::optional<Tensor> top_k,
+            c10::optional<Tensor> top_p, c10::optional<Tensor> seeds, c10::optional<Tensor> steps) {
+  DIE_CHECK_CUDA(logits);
+  DIE_CHECK_BF16(logits);
+  check_rows(logits, "logits");
+  DIE_CHECK_DTYPE(out, at::kLong);
+  const int64_t rows = logits.size(0);
+  TORCH_CHECK(out.numel() >= rows, "out too small");
+  TORCH_CHECK(logits.size(1) % 8 == 0, "vocab must be a multiple of 8");
+  auto opt = [&](const c10::optional<Tensor>& t, at::ScalarType d, const char* n) -> const void* {
+    if (!t.has_value()) return nullptr;
+    TORCH_CHECK(t->scalar_type() == d && t->is_cuda() && t->numel() >= rows, n, ": wrong dtype/device/size");
+    return t->data_ptr();
+  };
+  DIE_HIP(die::launch_sample(out.data_ptr<int64_t>(), bf(logits), logits.stride(0), (int)rows, (int)logits.size(1),
+                             (const float*)opt(temperature, at::kFloat, "temperature"),
+                             (const int*)opt(top_k, at::kInt, "top_k"), (const float*)opt(top_p, at::kFloat, "top_p"),
+                             (const int64_t*)opt(seeds, at::kLong, "seeds"),
+                             (const int64_t*)opt(steps, at::kLong, "steps"), cur_stream()));
+}
+
+// pool viewed as [planes, num_blocks, slab]
+void copy_blocks(Tensor pool, Tensor pairs) {
+  DIE_CHECK_CUDA(pool);
+  DIE_CHECK_BF16(pool);
+  DIE_CHECK_CONTIG(pool);
+  DIE_CHECK_DTYPE(pairs, at::kLong);
+  TORCH_CHECK(pool.dim() >= 3, "pool must be [planes, num_blocks, ...]");
+  TORCH_CHECK(pairs.dim() == 2 && pairs.size(1) == 2, "pairs must be [n, 2]");
+  const int64_t planes = pool.size(0), nb = pool.size(1), slab = pool.numel() / (planes * nb);
+  DIE_HIP(die::launch_copy_blocks(bf(pool), pairs.data_ptr<int64_t>(), (int)pairs.size(0), (int)planes, nb, slab,
+                                  cur_stream()));
+}
+
+void move_blocks(Tensor pool, Tensor buf, Tensor ids, bool gather) {
+  DIE_CHECK_CUDA(pool);
+  DIE_CHECK_BF16(pool);
+  DIE_CHECK_BF16(buf);
+  DIE_CHECK_CONTIG(pool);
+  DIE_CHECK_CONTIG(buf);
+  DIE_CHECK_DTYPE(ids, at::kLong);
+  const int64_t planes = pool.size(0), nb = pool.size(1), slab = pool.numel() / (planes * nb);
+  TORCH_CHECK(buf.numel() >= ids.numel() * planes * slab, "staging buffer too small");
+  DIE_HIP(die::launch_move_blocks(bf(pool), bf(buf), ids.data_ptr<int64_t>(), (int)ids.numel(), (int)planes, nb, slab,
+                                  gather, cur_stream()));
+}
+
+void topk_softmax(Tensor w, Tensor ids, Tensor gating, bool renorm) {
+  DIE_CHECK_CUDA(gating);
+  DIE_CHECK_BF16(gating);
+  DIE_CHECK_CONTIG(gating);
+  DIE_CHECK_DTYPE(w, at::kFloat);
+  DIE_CHECK_DTYPE(ids, at::kInt);
+  TORCH_CHECK(w.sizes() == ids.sizes() && w.size(0) == gating.size(0), "topk_softmax shapes");
+  DIE_HIP(die::launch_topk_softmax(w.data_ptr<float>(), ids.data_ptr<int>(), bf(gating), (int)gating.size(0),
+                                   (int)gating.size(1), (int)w.size(1), renorm, cur_stream()));
+}
+
+void moe_align(Tensor offsets, Tensor sorted, Tensor pos, Tensor ids, int64_t num_experts) {
+  DIE_CHECK_DTYPE(offsets, at::kInt);
+  DIE_CHECK_DTYPE(sorted, at::kInt);
+  DIE_CHECK_DTYPE(pos, at::kInt);
+  DIE_CHECK_DTYPE(ids, at::kInt);
+  TORCH_CHECK(offsets.numel() >= num_experts + 1 && sorted.numel() >= ids.numel() && pos.numel() >= ids.numel(),
+              "moe_align buffers");
+  DIE_HIP(die::launch_moe_align(offsets.data_ptr<int>(), sorted.data_ptr<int>(), pos.data_ptr<int>(),
+                                ids.data_ptr<int>(), (int)ids.numel(), (int)num_experts, cur_stream()));
+}
+
+void moe_gather(Tensor xs, Tensor x, Tensor sorted, int64_t topk) {
+  DIE_CHECK_BF16(xs);
+  DIE_CHECK_BF16(x);
+  DIE_CHECK_CONTIG(xs);
+  DIE_CHECK_CONTIG(x);
+  DIE_CHECK_DTYPE(sorted, at::kInt);
+  TORCH_CHECK(xs.size(0) == sorted.numel() && xs.size(1) == x.size(1) && sorted.numel() == x.size(0) * topk,
+              "moe_gather shapes");
+  DIE_HIP(die::launch_moe_gather(bf(xs), bf(x), sorted.data_ptr<int>(), (int)xs.size(0), (int)topk, (int)x.size(1),
+                                 cur_stream()));
+}
+
+void moe_combine(Tensor out, Tensor ys, Tensor pos, Tensor w) {
+  DIE_CHECK_BF16(out);
+  DIE_CHECK_BF16(ys);
+  DIE_CHECK_CONTIG(out);
+  DIE_CHECK_CONTIG(ys);
+  DIE_CHECK_DTYPE(pos, at::kInt);
+  DIE_CHECK_DTYPE(w, at::kFloat);
+  const int64_t T = out.size(0), K = w.size(1);
+  TORCH_CHECK(w.size(0) == T && pos.numel() == T * K && ys.size(0) == T * K && ys.size(1) == out.size(1),
+              "moe_combine shapes");
+  DIE_HIP(die::launch_moe_combine(bf(out), bf(ys), pos.data_ptr<int>(), w.data_ptr<float>(), (int)T, (int)K,
+                                  (int)out.size(1), cur_stream()));
+}
+
+void moe_grouped_gemm(Tensor y, Tensor x, Tensor w, Tensor offsets) {
+  DIE_CHECK_BF16(y);
+  DIE_CHECK_BF16(x);
+  DIE_CHECK_BF16(w);
+  DIE_CHECK_CONTIG(y);
+  DIE_CHECK_CONTIG(x);
+  DIE_CHECK_CONTIG(w);
+  DIE_CHECK_DTYPE(offsets, at::kInt);
+  TORCH_CHECK(w.dim() == 3 && x.dim() == 2 && y.dim() == 2, "w [E,N,K], x [M,K], y [M,N]");
+  const int64_t E = w.size(0), N = w.size(1), K = w.size(2);
+  TORCH_CHECK(x.size(1) == K && y.size(1) == N && y.size(0) == x.size(0) && offsets.numel() >= E + 1,
+              "moe_grouped_gemm shapes");
+  TORCH_CHECK(N % 64 == 0 && K % 32 == 0, "N % 64 and K % 32 required");
+  DIE_HIP(die::launch_moe_grouped_gemm(bf(y), bf(x), bf(w), offsets.data_ptr<int>(), (int)x.size(0), (int)E,
+                                       (int)N, (int)K, cur_stream()));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "Hand-written gfx950 (MI355X) HIP kernels";
+  m.def("rms_norm", &rms_norm);
+  m.def("fused_add_rms_norm", &fused_add_rms_norm);
+  m.def("silu_and_mul", &silu_and_mul);
+  m.def("rope_and_cache", &rope_and_cache);
+  m.def("attn_prefill", &attn_prefill);
+  m.def("attn_decode", &attn_decode);
+  m.def("decode_partials", &decode_partials);
+  m.def("sample", &sample, py::arg("out"), py::arg("logits"), py::arg("temperature") = py::none(),
+        py::arg("top_k") = py::none(), py::arg("top_p") = py::none(), py::arg("seeds") = py::none(),
+        py::arg("steps") = py::none());
+  m.def("copy_blocks", &copy_blocks);
+  m.def("move_blocks", &move_blocks);
+  m.def("topk_softmax", &topk_softmax);
+  m.def("moe_align", &moe_align);
+  m.def("moe_gather", &moe_gather);
+  m.def("moe_combine", &moe_combine);
+  m.def("moe_grouped_gemm", &moe_grouped_gemm);
+}

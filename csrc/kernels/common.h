@@ -1,0 +1,93 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels.
+//
+// Conventions used by every kernel in this directory:
+//  * wave = 64 lanes; block sizes are multiples of 64;
+//  * bf16 tensors are moved as 16-byte vectors (8 x bf16, `uint4`) — hipcc does
+//    not vectorise scalar bf16 accesses (cdna_hip_programming.md Guideline 13);
+//  * all arithmetic is fp32, rounded to bf16 only on store (v_cvt_pk_bf16_f32);
+//  * launches take an explicit hipStream_t so everything is hipGraph-capturable
+//    (no allocation / sync inside a launcher, Guideline 9).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace die {
+
+typedef uint16_t bf16_t;  // storage type for bfloat16
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;   // MFMA A/B fragment
+typedef __attribute__((ext_vector_type(4))) short short4_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;   // 32x32 MFMA accumulator
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;     // 16x16 MFMA accumulator
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(bf16_t x) { return __uint_as_float(((uint32_t)x) << 16); }
+
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32 on gfx950 (round-to-nearest-even, NaN-preserving)
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+// 8 bf16 packed in a uint4 <-> 8 floats
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = pack2(f[0], f[1]);
+  v.y = pack2(f[2], f[3]);
+  v.z = pack2(f[4], f[5]);
+  v.w = pack2(f[6], f[7]);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x = NT (multiple of 64). `red` is LDS scratch of NT/64 floats.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t += red[i];
+  __syncthreads();
+  return t;
+}
+
+// Counter-based RNG (splitmix64 finaliser) -> uniform in (0,1).
+__device__ __forceinline__ float hash_uniform(uint64_t seed, uint64_t a, uint64_t b) {
+  uint64_t z = seed ^ (a * 0x9E3779B97F4A7C15ull) ^ (b * 0xD1B54A32D192ED03ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return ((float)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+}  // namespace die

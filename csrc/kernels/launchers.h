@@ -1,0 +1,50 @@
+// Host launchers for the gfx950 kernels. Raw pointers + an explicit stream;
+// no allocation and no synchronisation, so every launcher is safe inside a
+// hipGraph capture. Shape/dtype validation happens in csrc/bindings.cpp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace die {
+
+typedef uint16_t bf16_t;
+
+hipError_t launch_rms_norm(bf16_t* out, const bf16_t* in, const bf16_t* w, float eps, int rows, int hidden,
+                           int64_t in_stride, int64_t out_stride, hipStream_t s);
+hipError_t launch_fused_add_rms_norm(bf16_t* out, const bf16_t* in, bf16_t* residual, const bf16_t* w, float eps,
+                                     int rows, int hidden, int64_t in_stride, int64_t out_stride, hipStream_t s);
+hipError_t launch_silu_and_mul(bf16_t* out, const bf16_t* in, int rows, int inter, hipStream_t s);
+
+hipError_t launch_rope_and_cache(bf16_t* qkv, int64_t qkv_stride, const int64_t* positions, const float* cos_sin,
+                                 const int64_t* slot_mapping, bf16_t* k_cache, bf16_t* v_cache, int num_tokens,
+                                 int hq, int hkv, int head_dim, int block_size, hipStream_t s);
+hipError_t launch_copy_blocks(bf16_t* pool, const int64_t* pairs, int num_pairs, int planes, int64_t num_blocks,
+                              int64_t slab, hipStream_t s);
+hipError_t launch_move_blocks(bf16_t* pool, bf16_t* buf, const int64_t* ids, int n, int planes, int64_t num_blocks,
+                              int64_t slab, bool gather, hipStream_t s);
+
+hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, const bf16_t* k_cache,
+                               const bf16_t* v_cache, const int* block_tables, int bt_stride, const int* cu_q,
+                               const int* ctx_lens, int num_seqs, int max_q_len, int hq, int hkv, int head_dim,
+                               int block_size, float scale, hipStream_t s);
+hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, const bf16_t* q, int64_t q_stride,
+                              const bf16_t* k_cache, const bf16_t* v_cache, const int* block_tables, int bt_stride,
+                              const int* ctx_lens, int num_seqs, int max_ctx, int hq, int hkv, int head_dim,
+                              int block_size, float scale, hipStream_t s);
+int attn_decode_max_partials(int max_ctx);
+
+hipError_t launch_sample(int64_t* out, const bf16_t* logits, int64_t stride, int rows, int vocab,
+                         const float* temperature, const int* top_k, const float* top_p, const int64_t* seeds,
+                         const int64_t* steps, hipStream_t s);
+
+hipError_t launch_topk_softmax(float* w, int* ids, const bf16_t* gating, int T, int E, int K, bool renorm,
+                               hipStream_t s);
+hipError_t launch_moe_align(int* offsets, int* sorted, int* pos, const int* ids, int n, int E, hipStream_t s);
+hipError_t launch_moe_gather(bf16_t* xs, const bf16_t* x, const int* sorted, int n, int K, int H, hipStream_t s);
+hipError_t launch_moe_combine(bf16_t* out, const bf16_t* ys, const int* pos, const float* w, int T, int K, int H,
+                              hipStream_t s);
+hipError_t launch_moe_grouped_gemm(bf16_t* Y, const bf16_t* X, const bf16_t* W, const int* offsets, int max_rows,
+                                   int E, int N, int K, hipStream_t s);
+
+}  // namespace die

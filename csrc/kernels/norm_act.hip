@@ -1,0 +1,127 @@
+// RMSNorm, fused residual-add + RMSNorm, and SiLU(gate) * up for gfx950.
+//
+// All three are HBM-bound elementwise/reduction ops (Appendix B of
+// cdna_hip_programming.md): one 16-byte vector per lane per access, fp32 math,
+// the row held in registers between the reduction and the scale pass so every
+// byte is read once and written once.
+#include "common.h"
+#include "launchers.h"
+
+namespace die {
+
+// One workgroup (NT threads) per row; NC 16-byte chunks per thread.
+// hidden = NT * NC * 8 at most (host picks NC = ceil(hidden / (8*NT))).
+template <int NT, int NC, bool FUSED_ADD>
+__global__ void __launch_bounds__(NT) rmsnorm_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ in,
+                                                     bf16_t* __restrict__ residual, const bf16_t* __restrict__ w,
+                                                     float eps, int hidden, int64_t in_stride,
+                                                     int64_t out_stride) {
+  __shared__ float red[NT / 64];
+  const int64_t row = blockIdx.x;
+  const uint4* src = reinterpret_cast<const uint4*>(in + row * in_stride);
+  uint4* dst = reinterpret_cast<uint4*>(out + row * out_stride);
+  uint4* res = FUSED_ADD ? reinterpret_cast<uint4*>(residual + row * (int64_t)hidden) : nullptr;
+  const int nchunk = hidden >> 3;
+  float x[NC][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int idx = threadIdx.x + c * NT;
+    if (idx < nchunk) {
+      unpack8(src[idx], x[c]);
+      if (FUSED_ADD) {
+        float r[8];
+        unpack8(res[idx], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[c][j] += r[j];
+        // the residual stream is kept in bf16: round once, normalise the rounded value
+        uint4 packed = pack8(x[c]);
+        res[idx] = packed;
+        unpack8(packed, x[c]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += x[c][j] * x[c][j];
+    }
+  }
+  const float var = block_sum<NT>(ss, red) / (float)hidden;
+  const float inv = rsqrtf(var + eps);
+  const uint4* wv = reinterpret_cast<const uint4*>(w);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int idx = threadIdx.x + c * NT;
+    if (idx < nchunk) {
+      float g[8], y[8];
+      unpack8(wv[idx], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] = x[c][j] * inv * g[j];
+      dst[idx] = pack8(y);
+    }
+  }
+}
+
+template <int NT, bool FUSED>
+static hipError_t rms_dispatch(bf16_t* out, const bf16_t* in, bf16_t* residual, const bf16_t* w, float eps,
+                               int rows, int hidden, int64_t in_stride, int64_t out_stride, hipStream_t s) {
+  const int nc = (hidden / 8 + NT - 1) / NT;
+  dim3 grid(rows), block(NT);
+#define DIE_RMS_CASE(N)                                                                               \
+  case N:                                                                                             \
+    hipLaunchKernelGGL((rmsnorm_kernel<NT, N, FUSED>), grid, block, 0, s, out, in, residual, w, eps, \
+                       hidden, in_stride, out_stride);                                                \
+    break;
+  switch (nc) {
+    DIE_RMS_CASE(1)
+    DIE_RMS_CASE(2)
+    DIE_RMS_CASE(3)
+    DIE_RMS_CASE(4)
+    DIE_RMS_CASE(5)
+    DIE_RMS_CASE(6)
+    DIE_RMS_CASE(7)
+    DIE_RMS_CASE(8)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef DIE_RMS_CASE
+  return hipGetLastError();
+}
+
+hipError_t launch_rms_norm(bf16_t* out, const bf16_t* in, const bf16_t* w, float eps, int rows, int hidden,
+                           int64_t in_stride, int64_t out_stride, hipStream_t s) {
+  if (hidden % 8 != 0 || rows <= 0) return rows == 0 ? hipSuccess : hipErrorInvalidValue;
+  return rms_dispatch<256, false>(out, in, nullptr, w, eps, rows, hidden, in_stride, out_stride, s);
+}
+
+hipError_t launch_fused_add_rms_norm(bf16_t* out, const bf16_t* in, bf16_t* residual, const bf16_t* w, float eps,
+                                     int rows, int hidden, int64_t in_stride, int64_t out_stride,
+                                     hipStream_t s) {
+  if (hidden % 8 != 0 || rows <= 0) return rows == 0 ? hipSuccess : hipErrorInvalidValue;
+  return rms_dispatch<256, true>(out, in, residual, w, eps, rows, hidden, in_stride, out_stride, s);
+}
+
+// ----------------------------------------------------------------------------
+// silu(gate) * up. Input row = [gate(I) | up(I)], output row = I.
+// grid = (rows, ceil(I/8 / 256)); one 16-byte chunk of gate and of up per lane.
+__global__ void __launch_bounds__(256) silu_mul_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ in,
+                                                       int inter) {
+  const int64_t row = blockIdx.x;
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= (inter >> 3)) return;
+  const uint4* g = reinterpret_cast<const uint4*>(in + row * 2 * (int64_t)inter);
+  const uint4* u = reinterpret_cast<const uint4*>(in + row * 2 * (int64_t)inter + inter);
+  float a[8], b[8], y[8];
+  unpack8(g[c], a);
+  unpack8(u[c], b);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) y[j] = a[j] / (1.f + __expf(-a[j])) * b[j];
+  reinterpret_cast<uint4*>(out + row * (int64_t)inter)[c] = pack8(y);
+}
+
+hipError_t launch_silu_and_mul(bf16_t* out, const bf16_t* in, int rows, int inter, hipStream_t s) {
+  if (inter % 8 != 0) return hipErrorInvalidValue;
+  if (rows == 0) return hipSuccess;
+  dim3 grid(rows, (inter / 8 + 255) / 256), block(256);
+  hipLaunchKernelGGL(silu_mul_kernel, grid, block, 0, s, out, in, inter);
+  return hipGetLastError();
+}
+
+}  // namespace die

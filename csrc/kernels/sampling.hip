@@ -1,0 +1,181 @@
+// Token sampling for gfx950: greedy argmax, temperature, top-k and top-p in
+// ONE kernel (one 1024-thread workgroup per sequence), exact and sort-free:
+//
+//  * top-k / top-p thresholds by 4-pass radix select over order-preserving
+//    32-bit keys of the scaled logits (8-bit digit histograms in LDS; counts
+//    for top-k, probability mass for top-p) — no sort of the 128K vocabulary;
+//  * the draw is Gumbel-max, argmax(z_i + G_i) over the kept set with
+//    G_i = -log(-log(u_i)), u from a counter-based hash of
+//    (request seed, generation step, token id): reproducible per request and
+//    independent of batch composition, and needs no prefix sum.
+// Rows stream from L2 (a 128256-entry bf16 row is 250 KiB), 16 B per lane.
+#include "common.h"
+#include "launchers.h"
+
+namespace die {
+
+constexpr int SNT = 1024;
+
+__device__ __forceinline__ uint32_t f2key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+  const uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __uint_as_float(u);
+}
+
+struct ArgMax {
+  float v;
+  int i;
+};
+__device__ __forceinline__ ArgMax better(ArgMax a, ArgMax b) {
+  return (b.v > a.v || (b.v == a.v && b.i < a.i)) ? b : a;
+}
+
+__device__ ArgMax block_argmax(ArgMax x, ArgMax* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ArgMax y;
+    y.v = __shfl_xor(x.v, o, 64);
+    y.i = __shfl_xor(x.i, o, 64);
+    x = better(x, y);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = x;
+  __syncthreads();
+  ArgMax r = red[0];
+  for (int w = 1; w < SNT / 64; ++w) r = better(r, red[w]);
+  __syncthreads();
+  return r;
+}
+
+__device__ float block_sumf(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int w = 0; w < SNT / 64; ++w) t += red[w];
+  __syncthreads();
+  return t;
+}
+
+// Radix-select the threshold key. MASS=false: the k-th largest key among
+// keys >= floor_key (target = k). MASS=true: the largest key t such that the
+// probability mass of {z >= t, z >= floor} reaches `target` (weights exp(z - m)).
+template <bool MASS>
+__device__ uint32_t radix_threshold(const bf16_t* row, int vocab, float inv_t, float m, uint32_t floor_key,
+                                    float target, float* hist, uint32_t* sh) {
+  uint32_t prefix = 0, pmask = 0;
+  float remaining = target;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int b = threadIdx.x; b < 256; b += SNT) hist[b] = 0.f;
+    __syncthreads();
+    for (int i = threadIdx.x * 8; i < vocab; i += SNT * 8) {
+      float z[8];
+      unpack8(*reinterpret_cast<const uint4*>(row + i), z);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float zz = z[j] * inv_t;
+        const uint32_t k = f2key(zz);
+        if (k >= floor_key && (k & pmask) == prefix)
+          atomicAdd(&hist[(k >> shift) & 255u], MASS ? __expf(zz - m) : 1.f);
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float cum = 0.f;
+      int b = 255;
+      for (; b > 0; --b) {
+        if (cum + hist[b] >= remaining) break;
+        cum += hist[b];
+      }
+      sh[0] = (uint32_t)b;
+      reinterpret_cast<float*>(sh)[1] = remaining - cum;
+    }
+    __syncthreads();
+    prefix |= sh[0] << shift;
+    pmask |= 255u << shift;
+    remaining = reinterpret_cast<float*>(sh)[1];
+    __syncthreads();
+  }
+  return prefix;
+}
+
+__global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, const bf16_t* __restrict__ logits,
+                                                     int64_t stride, int vocab, const float* __restrict__ temperature,
+                                                     const int* __restrict__ top_k, const float* __restrict__ top_p,
+                                                     const int64_t* __restrict__ seeds,
+                                                     const int64_t* __restrict__ steps) {
+  __shared__ ArgMax red[SNT / 64];
+  __shared__ float redf[SNT / 64];
+  __shared__ float hist[256];
+  __shared__ uint32_t sh[2];
+  const int r = blockIdx.x;
+  const bf16_t* row = logits + (int64_t)r * stride;
+  const float temp = temperature ? temperature[r] : 0.f;
+  const int k = top_k ? top_k[r] : 0;
+  const float p = top_p ? top_p[r] : 1.f;
+
+  ArgMax best{-INFINITY, 0x7fffffff};
+  for (int i = threadIdx.x * 8; i < vocab; i += SNT * 8) {
+    float z[8];
+    unpack8(*reinterpret_cast<const uint4*>(row + i), z);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) best = better(best, ArgMax{z[j], i + j});
+  }
+  best = block_argmax(best, red);
+  if (temp <= 0.f || k == 1) {
+    if (threadIdx.x == 0) out[r] = best.i;
+    return;
+  }
+  const float inv_t = 1.f / temp;
+  const float m = best.v * inv_t;
+  uint32_t floor_key = 0;
+  if (k > 0 && k < vocab) floor_key = radix_threshold<false>(row, vocab, inv_t, m, 0u, (float)k, hist, sh);
+  if (p < 1.f) {
+    float z_mass = 0.f;
+    for (int i = threadIdx.x * 8; i < vocab; i += SNT * 8) {
+      float z[8];
+      unpack8(*reinterpret_cast<const uint4*>(row + i), z);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float zz = z[j] * inv_t;
+        if (f2key(zz) >= floor_key) z_mass += __expf(zz - m);
+      }
+    }
+    z_mass = block_sumf(z_mass, redf);
+    const uint32_t pk = radix_threshold<true>(row, vocab, inv_t, m, floor_key, p * z_mass, hist, sh);
+    floor_key = pk > floor_key ? pk : floor_key;
+  }
+  const uint64_t seed = seeds ? (uint64_t)seeds[r] : 0x5eedull;
+  const uint64_t step = steps ? (uint64_t)steps[r] : 0ull;
+  ArgMax g{-INFINITY, 0x7fffffff};
+  for (int i = threadIdx.x * 8; i < vocab; i += SNT * 8) {
+    float z[8];
+    unpack8(*reinterpret_cast<const uint4*>(row + i), z);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float zz = z[j] * inv_t;
+      if (f2key(zz) >= floor_key) {
+        const float u = hash_uniform(seed, step, (uint64_t)(i + j));
+        g = better(g, ArgMax{zz - __logf(-__logf(u)), i + j});
+      }
+    }
+  }
+  g = block_argmax(g, red);
+  if (threadIdx.x == 0) out[r] = g.i <= vocab ? g.i : best.i;
+}
+
+hipError_t launch_sample(int64_t* out, const bf16_t* logits, int64_t stride, int rows, int vocab,
+                         const float* temperature, const int* top_k, const float* top_p, const int64_t* seeds,
+                         const int64_t* steps, hipStream_t s) {
+  if (rows == 0) return hipSuccess;
+  if (vocab % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sample_kernel, dim3(rows), dim3(SNT), 0, s, out, logits, stride, vocab, temperature, top_k,
+                     top_p, seeds, steps);
+  return hipGetLastError();
+}
+
+}  // namespace die

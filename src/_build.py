@@ -1,0 +1,125 @@
+"""
+In-tree native build (no hipify, no JIT cache): compiles the gfx950 HIP
+kernels and the torch bindings into ``src/_C*.so`` and the host runtime
+(block manager, step builder) into ``src/_runtime*.so``.
+
+    python -m src._build            # incremental
+    python -m src._build --force
+
+The kernels are compiled once here with ``hipcc --offload-arch=gfx950`` and the
+``.so`` files travel with the repo snapshot to the GPU box.
+"""
+
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+OBJ = os.path.join(ROOT, "build", "obj")
+EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+ARCH = os.environ.get("DIE_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+KERNELS = ["norm_act", "rope_cache", "attention", "sampling", "moe"]
+
+
+def _torch_paths():
+    import torch
+    from torch.utils.cpp_extension import include_paths
+
+    return include_paths(), os.path.join(os.path.dirname(torch.__file__), "lib"), int(torch._C._GLIBCXX_USE_CXX11_ABI)
+
+
+def _newer(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}")
+    return r.stdout
+
+
+def _headers(d: str):
+    return [os.path.join(d, f) for f in os.listdir(d) if f.endswith(".h")]
+
+
+def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    out = os.path.join(ROOT, "src", "_C" + EXT_SUFFIX)
+    kdir = os.path.join(CSRC, "kernels")
+    hdrs = _headers(kdir)
+    incs, torch_lib, abi = _torch_paths()
+    jobs_list = []
+    objs = []
+    for k in KERNELS:
+        src = os.path.join(kdir, k + ".hip")
+        obj = os.path.join(OBJ, k + ".o")
+        objs.append(obj)
+        if force or _newer(obj, [src] + hdrs):
+            jobs_list.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", CSRC,
+                              "-c", src, "-o", obj])
+    bsrc = os.path.join(CSRC, "bindings.cpp")
+    bobj = os.path.join(OBJ, "bindings.o")
+    objs.append(bobj)
+    if force or _newer(bobj, [bsrc] + hdrs):
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__=1",
+               "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+               "-I", CSRC, "-I", "/opt/rocm/include", "-I", sysconfig.get_paths()["include"]]
+        for i in incs:
+            cmd += ["-isystem", i]
+        cmd += ["-c", bsrc, "-o", bobj]
+        jobs_list.append(cmd)
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        for res in ex.map(_run, jobs_list):
+            if verbose and res:
+                print(res)
+    if force or _newer(out, objs):
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out,
+              "-L", torch_lib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+              f"-Wl,-rpath,{torch_lib}"])
+    return out
+
+
+def build_runtime(force: bool = False) -> str:
+    out = os.path.join(ROOT, "src", "_runtime" + EXT_SUFFIX)
+    rdir = os.path.join(CSRC, "runtime")
+    srcs = [os.path.join(rdir, "runtime_bindings.cpp")] + _headers(rdir)
+    if force or _newer(out, srcs):
+        import pybind11
+
+        _run(["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-I", pybind11.get_include(),
+              "-I", sysconfig.get_paths()["include"], "-I", rdir,
+              os.path.join(rdir, "runtime_bindings.cpp"), "-o", out])
+    return out
+
+
+def build_all(force: bool = False, verbose: bool = False) -> None:
+    build_runtime(force)
+    build_kernels(force, verbose=verbose)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--runtime-only", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    print(build_runtime(a.force))
+    if not a.runtime_only:
+        print(build_kernels(a.force, verbose=a.verbose))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

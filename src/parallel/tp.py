@@ -1,0 +1,99 @@
+"""
+Tensor parallelism over RCCL (torch.distributed ``"nccl"`` backend = RCCL on
+ROCm), one process per GPU.
+
+Megatron-style split, chosen for xGMI's point-to-point links: per decoder layer
+exactly two all-reduces (after the row-parallel ``o_proj`` and ``down_proj``),
+each of ``tokens x hidden`` bf16 — for 70B TP=8 decode at batch 32 that is
+512 KiB, small enough that RCCL picks its low-latency one-shot/LL protocols
+over the 7 xGMI links. QKV and gate/up are column-parallel (each rank owns
+whole heads / a contiguous slice of the FFN), the LM head is vocab-parallel
+with one all-gather of the logits, the embedding is replicated (2 GiB for
+70B — trivial against 288 GB of HBM, and it saves a collective per step).
+On CPU the same code runs on ``gloo`` for tests.
+"""
+
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class TPContext:
+    rank: int = 0
+    world_size: int = 1
+    group: Optional[object] = None
+
+    @property
+    def enabled(self) -> bool:
+        return self.world_size > 1
+
+    def shard(self, n: int) -> int:
+        if n % self.world_size:
+            raise ValueError(f"{n} not divisible by tp={self.world_size}")
+        return n // self.world_size
+
+    def kv_heads(self, n_kv: int) -> int:
+        """KV heads per rank: split when divisible, replicate when tp > n_kv."""
+        if n_kv >= self.world_size:
+            return self.shard(n_kv)
+        if self.world_size % n_kv:
+            raise ValueError("tp must be a multiple of num_kv_heads when tp > num_kv_heads")
+        return 1
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        if self.enabled:
+            dist.all_reduce(t, group=self.group)
+        return t
+
+    def all_gather_last(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenate the per-rank shards along the last dim."""
+        if not self.enabled:
+            return t
+        parts = [torch.empty_like(t) for _ in range(self.world_size)]
+        dist.all_gather(parts, t.contiguous(), group=self.group)
+        return torch.cat(parts, dim=-1)
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.enabled:
+            dist.broadcast(t, src=src, group=self.group)
+        return t
+
+
+_TP: Optional[TPContext] = None
+
+
+def init_tp(tp_size: Optional[int] = None, backend: Optional[str] = None) -> TPContext:
+    """Initialise (or reuse) the default process group and return the TP
+    context. Reads RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* from the
+    environment (torchrun)."""
+    global _TP
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    tp = tp_size or world
+    if tp == 1:
+        _TP = TPContext()
+        return _TP
+    if not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        dist.init_process_group(backend=backend)
+    rank = dist.get_rank()
+    if dist.get_world_size() == tp:
+        group = None
+    else:
+        # consecutive ranks form a TP group (GPUs of one xGMI-connected node)
+        groups = [dist.new_group(list(range(s, s + tp))) for s in range(0, dist.get_world_size(), tp)]
+        group = groups[rank // tp]
+    _TP = TPContext(rank=rank % tp, world_size=tp, group=group)
+    return _TP
+
+
+def get_tp() -> TPContext:
+    return _TP or TPContext()

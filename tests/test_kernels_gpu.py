@@ -1,0 +1,220 @@
+"""Numerics of every hand-written gfx950 kernel against the plain PyTorch fp32
+reference of the same op (src/ops/reference.py). GPU only."""
+
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from src import ops  # noqa: E402
+from src.ops import reference as ref  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert ops.native_available(), "HIP extension must be built for GPU tests"
+    torch.manual_seed(0)
+    return torch.device("cuda:0")
+
+
+def close(a, b, atol, rtol=0.0):
+    d = (a.float() - b.float()).abs()
+    lim = atol + rtol * b.float().abs()
+    bad = (d > lim).sum().item()
+    assert bad == 0, f"{bad} elements off; max abs err {d.max().item():.4g}"
+
+
+@pytest.mark.parametrize("hidden", [4096, 8192, 1024])
+def test_rms_norm(dev, hidden):
+    x = torch.randn(37, hidden, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(hidden, device=dev, dtype=torch.bfloat16)
+    close(ops.rms_norm(x, w, 1e-5), ref.rms_norm(x, w, 1e-5), atol=2e-2, rtol=1e-2)
+
+
+def test_rms_norm_strided_input(dev):
+    big = torch.randn(9, 6144, device=dev, dtype=torch.bfloat16)
+    x = big[:, :4096]
+    w = torch.randn(4096, device=dev, dtype=torch.bfloat16)
+    close(ops.rms_norm(x, w, 1e-5), ref.rms_norm(x.contiguous(), w, 1e-5), atol=2e-2, rtol=1e-2)
+
+
+def test_fused_add_rms_norm(dev):
+    x = torch.randn(33, 4096, device=dev, dtype=torch.bfloat16)
+    r = torch.randn(33, 4096, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(4096, device=dev, dtype=torch.bfloat16)
+    y_ref, r_ref = ref.fused_add_rms_norm(x, r.clone(), w, 1e-5)
+    r2 = r.clone()
+    y = ops.fused_add_rms_norm(x, r2, w, 1e-5)
+    close(r2, r_ref, atol=1e-2, rtol=1e-2)
+    close(y, y_ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("inter", [14336, 3584, 64])
+def test_silu_and_mul(dev, inter):
+    x = torch.randn(19, 2 * inter, device=dev, dtype=torch.bfloat16)
+    close(ops.silu_and_mul(x), ref.silu_and_mul(x), atol=2e-2, rtol=1e-2)
+
+
+def _paged(num_blocks, hkv, bs, dev):
+    k = torch.zeros(num_blocks, hkv, bs, 128, device=dev, dtype=torch.bfloat16)
+    return k, torch.zeros_like(k)
+
+
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1), (16, 16)])
+def test_rope_and_cache(dev, hq, hkv):
+    t, bs, nb = 45, 16, 16
+    qkv = torch.randn(t, (hq + 2 * hkv) * 128, device=dev, dtype=torch.bfloat16)
+    pos = torch.randint(0, 4000, (t,), device=dev)
+    slots = torch.randperm(nb * bs, device=dev)[:t]
+    slots[3] = -1
+    cs = ref.rope_cos_sin(4096, 128, 500000.0, dev)
+    kc, vc = _paged(nb, hkv, bs, dev)
+    kr, vr = _paged(nb, hkv, bs, dev)
+    q1 = qkv.clone()
+    q2 = qkv.clone()
+    ops.rope_and_cache(q1, pos, cs, slots, kc, vc, hq, hkv, 128)
+    ref.rope_and_cache(q2, pos.cpu(), cs, slots.cpu(), kr, vr, hq, hkv, 128)
+    close(q1, q2, atol=2e-2, rtol=1e-2)
+    close(kc, kr, atol=2e-2, rtol=1e-2)
+    close(vc, vr, atol=0)
+
+
+def _make_seqs(qlens, ctxs, hkv, bs, dev, g):
+    hq = hkv * g
+    nseq = len(qlens)
+    max_blocks = max((c + bs - 1) // bs for c in ctxs) + 1
+    total = sum((c + bs - 1) // bs for c in ctxs) + 4
+    perm = torch.randperm(total).tolist()
+    bt = torch.zeros(nseq, max_blocks, dtype=torch.int32)
+    p = 0
+    for i, c in enumerate(ctxs):
+        nb = (c + bs - 1) // bs
+        bt[i, :nb] = torch.tensor(perm[p:p + nb], dtype=torch.int32)
+        p += nb
+    kc = torch.randn(total, hkv, bs, 128, device=dev, dtype=torch.bfloat16)
+    vc = torch.randn(total, hkv, bs, 128, device=dev, dtype=torch.bfloat16)
+    cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0).tolist()), dtype=torch.int32)
+    t = int(cu[-1])
+    # q rows embedded in a wider qkv-like buffer (strided rows, as in the model)
+    qkv = torch.randn(t, (hq + 2 * hkv) * 128, device=dev, dtype=torch.bfloat16)
+    q = qkv[:, : hq * 128]
+    return q, kc, vc, bt.to(dev), cu.to(dev), torch.tensor(ctxs, dtype=torch.int32, device=dev), hq
+
+
+@pytest.mark.parametrize("g", [4, 8, 1])
+def test_attn_prefill(dev, g):
+    hkv = 8 if g != 8 else 1
+    if g == 1:
+        hkv = 4
+    qlens = [1, 37, 128, 200, 64]
+    ctxs = [1, 37, 300, 200, 1000]          # ctx > qlen: chunked prefill over cached prefix
+    q, kc, vc, bt, cu, ctx, hq = _make_seqs(qlens, ctxs, hkv, 16, dev, g)
+    scale = 1 / math.sqrt(128)
+    out = ops.attn_prefill(q, kc, vc, bt, cu, ctx, max(qlens), hq, hkv, scale)
+    r = ref.attention(q, kc, vc, bt, cu, ctx, hq, hkv, scale).reshape(q.shape[0], -1)
+    close(out, r, atol=2.5e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("g,bs", [(4, 16), (8, 16), (4, 32), (1, 16)])
+def test_attn_decode(dev, g, bs):
+    hkv = 8 if g == 4 else (1 if g == 8 else 4)
+    ctxs = [1, 17, 64, 65, 300, 1000, 2049]
+    q, kc, vc, bt, _, ctx, hq = _make_seqs([1] * len(ctxs), ctxs, hkv, bs, dev, g)
+    scale = 1 / math.sqrt(128)
+    max_ctx = 4096
+    bt_wide = torch.zeros(bt.shape[0], max_ctx // bs, dtype=torch.int32, device=dev)
+    bt_wide[:, : bt.shape[1]] = bt
+    out = ops.attn_decode(q, kc, vc, bt_wide, ctx, max_ctx, hq, hkv, scale)
+    cu = torch.arange(len(ctxs) + 1, dtype=torch.int32, device=dev)
+    r = ref.attention(q, kc, vc, bt, cu, ctx, hq, hkv, scale).reshape(q.shape[0], -1)
+    close(out, r, atol=2.5e-2, rtol=2e-2)
+
+
+def test_attn_softmax_spike(dev):
+    """Force the online-softmax rescale branch: one key with a huge score late in the sequence."""
+    g, hkv = 4, 2
+    q, kc, vc, bt, cu, ctx, hq = _make_seqs([100], [700], hkv, 16, dev, g)
+    # make key 650 align strongly with every query of head group 0
+    blk, off = bt[0, 650 // 16].item(), 650 % 16
+    kc[blk, 0, off] = (q[0, :128].float() * 8).to(torch.bfloat16)
+    scale = 1 / math.sqrt(128)
+    out = ops.attn_prefill(q, kc, vc, bt, cu, ctx, 100, hq, hkv, scale)
+    r = ref.attention(q, kc, vc, bt, cu, ctx, hq, hkv, scale).reshape(q.shape[0], -1)
+    close(out, r, atol=3e-2, rtol=2e-2)
+    bt_wide = torch.zeros(1, 256, dtype=torch.int32, device=dev)
+    bt_wide[:, : bt.shape[1]] = bt
+    ctx1 = torch.tensor([700], dtype=torch.int32, device=dev)
+    qd = q[99:100]
+    out_d = ops.attn_decode(qd, kc, vc, bt_wide, ctx1, 4096, hq, hkv, scale)
+    close(out_d, r[99:100], atol=3e-2, rtol=2e-2)
+
+
+def test_sampling_greedy_and_filters(dev):
+    v = 128256
+    logits = torch.randn(6, v, device=dev, dtype=torch.bfloat16) * 3
+    out = ops.sample(logits)
+    assert torch.equal(out.cpu(), logits.float().argmax(-1).cpu())
+    temp = torch.full((6,), 0.8, device=dev)
+    topk = torch.tensor([1, 5, 5, 0, 0, 50], dtype=torch.int32, device=dev)
+    topp = torch.tensor([1.0, 1.0, 0.5, 1e-6, 0.9, 0.9], device=dev)
+    seeds = torch.arange(6, device=dev, dtype=torch.long)
+    top5 = torch.topk(logits.float(), 5, -1).indices.cpu()
+    for step in range(20):
+        steps = torch.full((6,), step, device=dev, dtype=torch.long)
+        s = ops.sample(logits, temp, topk, topp, seeds, steps).cpu()
+        assert s[0] == top5[0, 0]                 # top_k = 1 → greedy
+        assert s[1] in top5[1] and s[2] in top5[2]
+        assert s[3] == top5[3, 0]                 # tiny top_p → argmax
+    # reproducible per (seed, step)
+    a = ops.sample(logits, temp, topk, topp, seeds, steps)
+    b = ops.sample(logits, temp, topk, topp, seeds, steps)
+    assert torch.equal(a, b)
+
+
+def test_sampling_distribution(dev):
+    v = 1024
+    probs = torch.zeros(v)
+    probs[:4] = torch.tensor([0.4, 0.3, 0.2, 0.1])
+    logits = torch.log(probs.clamp_min(1e-30)).to(torch.bfloat16)
+    n = 4000
+    rows = logits[None].repeat(n, 1).to(dev)
+    temp = torch.ones(n, device=dev)
+    seeds = torch.arange(n, device=dev, dtype=torch.long) * 7919
+    steps = torch.zeros(n, device=dev, dtype=torch.long)
+    s = ops.sample(rows, temp, None, None, seeds, steps).cpu()
+    freq = torch.bincount(s, minlength=v)[:4].float() / n
+    assert (freq - probs[:4]).abs().max() < 0.03, freq
+
+
+def test_block_movers(dev):
+    pool = torch.randn(6, 10, 2, 16, 128, device=dev, dtype=torch.bfloat16)
+    ref_pool = pool.clone()
+    pairs = torch.tensor([[1, 7], [3, 8]], device=dev)
+    ops.copy_blocks(pool, pairs)
+    ref_pool[:, 7] = ref_pool[:, 1]
+    ref_pool[:, 8] = ref_pool[:, 3]
+    assert torch.equal(pool, ref_pool)
+    ids = torch.tensor([2, 5, 9], device=dev)
+    buf = ops.gather_blocks(pool, ids)
+    assert torch.equal(buf.view(3, 6, -1)[1], pool[:, 5].reshape(6, -1))
+    other = torch.zeros_like(pool)
+    ops.scatter_blocks(other, ids, buf)
+    assert torch.equal(other[:, ids], pool[:, ids])
+
+
+def test_moe(dev):
+    t, h, inter, e, k = 77, 512, 256, 8, 2
+    x = torch.randn(t, h, device=dev, dtype=torch.bfloat16)
+    gating = torch.randn(t, e, device=dev, dtype=torch.bfloat16)
+    w13 = torch.randn(e, 2 * inter, h, device=dev, dtype=torch.bfloat16) / math.sqrt(h)
+    w2 = torch.randn(e, h, inter, device=dev, dtype=torch.bfloat16) / math.sqrt(inter)
+    w, ids = ops.topk_softmax(gating, k)
+    wr, idr = ref.topk_softmax(gating, k)
+    # bf16 router logits can tie: compare the selected sets and the weights in sorted order
+    assert torch.equal(ids.sort(-1).values.cpu(), idr.sort(-1).values.cpu())
+    close(w.sort(-1).values, wr.sort(-1).values, atol=1e-4)
+    close(ops.moe_forward(x, w13, w2, gating, k), ref.moe_forward(x, w13, w2, gating, k), atol=3e-2, rtol=3e-2)
