@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""
+Headline benchmark (BASELINE.json): req/s + p50 end-to-end latency of
+Llama-3-8B batched serving on 1/2/4/8 MI355X.
+
+Each rank (one per GPU, launched by torch.distributed.run for N > 1) runs a
+full serving replica — data parallel, the right layout for an 8B model that
+fits one 288 GB GPU many times over — and the whole serving path minus TCP:
+
+    Batcher(max_batch=32, max_latency=10 ms)  →  AsyncLLMEngine (engine thread)
+      → continuous-batching scheduler → paged-KV Llama-3-8B (random-init bf16)
+      → hand-written gfx950 kernels + hipBLASLt GEMMs, hipGraph decode.
+
+One "step" = one wave of ``--batch`` (32) synthetic requests per GPU, each a
+distinct random 512-token prompt generating 128 tokens (ignore_eos), submitted
+together and served to completion (prefill + 128 decode iterations, sampling
+included). Weak scaling: per-GPU work is fixed as N grows. ``value`` is the
+whole-job request rate (all GPUs); ``p50_latency_ms`` is the median
+submit→finish latency over every timed request.
+
+    python bench.py                      # 1 GPU, 3 timed steps, 1 warmup
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8 --steps 3 --warmup 1
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import random
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+METRIC = "req/sec + p50 end-to-end latency, Llama-3-8B batched serving at 1/2/4/8 MI355X"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=None)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--batch", type=int, default=32, help="requests per GPU per step (= max_batch)")
+    p.add_argument("--prompt-len", type=int, default=512)
+    p.add_argument("--gen-len", type=int, default=128)
+    p.add_argument("--preset", default="llama3-8b")
+    p.add_argument("--max-latency-ms", type=float, default=10.0)
+    p.add_argument("--max-model-len", type=int, default=2048)
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--temperature", type=float, default=0.0)
+    p.add_argument("--verbose", action="store_true")
+    return p.parse_args()
+
+
+async def serve_wave(batcher, n, prompt_len, gen_len, temperature, rng, tag):
+    prompts = [[rng.randrange(3, 128000) for _ in range(prompt_len)] for _ in range(n)]
+    t0 = [0.0] * n
+    lat = [0.0] * n
+
+    async def one(i):
+        t0[i] = time.perf_counter()
+        fut = await batcher.add_request("llama", "1", {
+            "prompt_token_ids": prompts[i], "max_tokens": gen_len, "ignore_eos": True,
+            "temperature": temperature, "seed": i})
+        seq = await fut
+        lat[i] = time.perf_counter() - t0[i]
+        assert len(seq.output_ids) == gen_len, (len(seq.output_ids), seq.finish_reason)
+
+    await asyncio.gather(*(one(i) for i in range(n)))
+    return lat
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n_gpus = args.gpus or world
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device(f"cuda:{local}")
+
+    from src.batcher import Batcher
+    from src.config import EngineConfig
+    from src.engine import LLMEngine
+    from src.engine.async_engine import AsyncLLMEngine
+    from src.preproc import normalize_request
+
+    cfg = EngineConfig(max_num_seqs=args.batch, max_num_batched_tokens=max(16384, args.prompt_len),
+                       max_latency_ms=args.max_latency_ms, use_cuda_graph=not args.no_graph,
+                       graph_batch_sizes=[1, 2, 4, 8, 16, 24, 32, args.batch])
+    t_init = time.perf_counter()
+    engine = LLMEngine.from_preset(args.preset, device=dev, cfg=cfg, max_model_len=args.max_model_len,
+                                   seed=1234, capture=not args.no_graph)
+    init_s = time.perf_counter() - t_init
+    aeng = AsyncLLMEngine(engine)
+    aeng.start()
+
+    async def callback(model, version, inputs_list):
+        loop = asyncio.get_running_loop()
+        futs = []
+        for x in inputs_list:
+            gi = normalize_request(x, None, engine.max_model_len)
+            futs.append(aeng.submit(os.urandom(8).hex(), gi.prompt_token_ids, gi.sampling, loop))
+        return futs
+
+    rng = random.Random(1000 + rank)
+
+    async def run():
+        batcher = Batcher(max_batch_size=args.batch, max_latency_ms=args.max_latency_ms, batch_callback=callback)
+        await batcher.start()
+        for w in range(args.warmup):
+            await serve_wave(batcher, args.batch, args.prompt_len, args.gen_len, args.temperature, rng, f"w{w}")
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        stats0 = dict(engine.stats)
+        t0 = time.perf_counter()
+        lats = []
+        for s in range(args.steps):
+            lats += await serve_wave(batcher, args.batch, args.prompt_len, args.gen_len, args.temperature, rng,
+                                     f"s{s}")
+            if args.verbose and rank == 0:
+                print(f"step {s}: {time.perf_counter() - t0:.2f}s", file=sys.stderr, flush=True)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        await batcher.stop()
+        return elapsed, lats, stats0
+
+    elapsed, lats, stats0 = asyncio.run(run())
+    aeng.stop()
+    st = engine.stats
+    gen_tok = st["generated_tokens"] - stats0["generated_tokens"]
+    prefill_s = st["prefill_time"] - stats0["prefill_time"]
+    decode_s = st["decode_time"] - stats0["decode_time"]
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        gathered = [None] * world
+        dist.all_gather_object(gathered, lats)
+        lats = [x for g in gathered for x in g]
+    total_req = args.steps * args.batch * n_gpus
+    rps = total_req / elapsed
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": round(rps, 3),
+            "unit": "req/s",
+            "n_gpus": n_gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic",
+            "p50_latency_ms": round(1e3 * statistics.median(lats), 2),
+            "p99_latency_ms": round(1e3 * sorted(lats)[max(0, int(0.99 * len(lats)) - 1)], 2),
+            "output_tok_per_s": round(gen_tok * n_gpus / elapsed, 1),
+            "config": {
+                "model": args.preset.replace("llama3", "Llama-3").replace("-8b", "-8B").replace("-70b", "-70B"),
+                "global_batch": args.batch * n_gpus,
+                "seq_len": args.prompt_len + args.gen_len,
+                "prompt_len": args.prompt_len,
+                "gen_len": args.gen_len,
+                "parallelism": f"dp{n_gpus}",
+                "max_batch": args.batch,
+                "max_latency_ms": args.max_latency_ms,
+                "weights": "random-init",
+                "hip_graph_decode": not args.no_graph,
+            },
+            "notes": {
+                "baseline": "reference publishes no numbers and has no GPU path (BASELINE.md); vs_baseline=null",
+                "rank0_prefill_s": round(prefill_s, 3),
+                "rank0_decode_s": round(decode_s, 3),
+                "engine_init_s": round(init_s, 1),
+            },
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

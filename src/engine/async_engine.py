@@ -1,0 +1,144 @@
+"""
+AsyncLLMEngine: runs the LLMEngine step loop on a dedicated thread and hands
+results back to asyncio.
+
+The reference runs "inference" on the event loop itself (an ``asyncio.sleep``
+inside the RPC handler, `/root/reference/src/worker.py:152`). A real GPU step
+loop must never share the event-loop thread: here the RPC side calls
+:meth:`submit` (thread-safe, returns an ``asyncio.Future``), the engine thread
+drains the submission queue between steps, and each finished sequence resolves
+its future via ``loop.call_soon_threadsafe``. No lock is held across an await
+or across a GPU step.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import logging
+import queue
+import threading
+import time
+from typing import Any, Dict, List, Optional
+
+from src.engine.llm_engine import LLMEngine
+from src.engine.sequence import Sequence
+from src.preproc import SamplingParams
+
+logger = logging.getLogger(__name__)
+
+
+class AsyncLLMEngine:
+    def __init__(self, engine: LLMEngine, name: str = "engine"):
+        self.engine = engine
+        self.name = name
+        self._q: "queue.Queue" = queue.Queue()
+        self._wake = threading.Event()
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self.error: Optional[BaseException] = None
+
+    def start(self) -> None:
+        if self._thread is not None:
+            return
+        self._stop.clear()
+        self._thread = threading.Thread(target=self._loop, name=f"{self.name}-loop", daemon=True)
+        self._thread.start()
+
+    def stop(self, timeout: float = 30.0) -> None:
+        self._stop.set()
+        self._wake.set()
+        if self._thread is not None:
+            self._thread.join(timeout)
+            self._thread = None
+
+    @property
+    def running(self) -> bool:
+        return self._thread is not None and self._thread.is_alive()
+
+    def submit(self, request_id: str, prompt_ids: List[int], sampling: SamplingParams,
+               loop: Optional[asyncio.AbstractEventLoop] = None, user_data: Any = None) -> asyncio.Future:
+        """Thread-safe; call from the event loop. The future resolves to the
+        finished :class:`Sequence` (or raises if the engine failed)."""
+        loop = loop or asyncio.get_running_loop()
+        fut = loop.create_future()
+        if self.error is not None:
+            fut.set_exception(RuntimeError(f"engine failed: {self.error!r}"))
+            return fut
+        self._q.put((request_id, prompt_ids, sampling, fut, loop, user_data))
+        self._wake.set()
+        return fut
+
+    def submit_sync(self, request_id: str, prompt_ids: List[int], sampling: SamplingParams,
+                    callback) -> None:
+        """Non-asyncio submission: ``callback(seq_or_exception)`` runs on the engine thread."""
+        self._q.put((request_id, prompt_ids, sampling, callback, None, None))
+        self._wake.set()
+
+    def _drain(self) -> None:
+        while True:
+            try:
+                rid, ids, sp, fut, loop, ud = self._q.get_nowait()
+            except queue.Empty:
+                return
+
+            def done(seq: Sequence, fut=fut, loop=loop):
+                if loop is None:
+                    fut(seq)
+                else:
+                    loop.call_soon_threadsafe(_resolve, fut, seq)
+
+            try:
+                self.engine.add_request(rid, ids, sp, on_finish=done, user_data=ud)
+            except Exception as e:
+                if loop is None:
+                    fut(e)
+                else:
+                    loop.call_soon_threadsafe(_fail, fut, e)
+
+    def _loop(self) -> None:
+        eng = self.engine
+        try:
+            while not self._stop.is_set():
+                self._drain()
+                if not eng.has_work():
+                    self._wake.wait(0.05)
+                    self._wake.clear()
+                    continue
+                finished = eng.step()
+                if not finished and not eng.scheduler.running:
+                    # admission is being held for batching (max_latency): sleep until due
+                    w = eng.scheduler.next_wakeup()
+                    if w:
+                        self._wake.wait(min(w, 0.01))
+                        self._wake.clear()
+        except BaseException as e:  # surface GPU/HIP faults to every waiter
+            logger.exception("engine loop crashed")
+            self.error = e
+            for seq in list(eng.seqs.values()):
+                if seq.on_finish is not None:
+                    seq.finish_reason = "error"
+                    try:
+                        seq.on_finish(seq)
+                    except Exception:
+                        pass
+
+    def stats(self) -> Dict[str, Any]:
+        s = self.engine.get_stats()
+        s["queue"] = self._q.qsize()
+        s["alive"] = self.running
+        s["error"] = repr(self.error) if self.error else None
+        return s
+
+
+def _resolve(fut: asyncio.Future, seq: Sequence) -> None:
+    if fut.done():
+        return
+    if seq.finish_reason == "error":
+        fut.set_exception(RuntimeError("engine failed"))
+    else:
+        fut.set_result(seq)
+
+
+def _fail(fut: asyncio.Future, e: BaseException) -> None:
+    if not fut.done():
+        fut.set_exception(e)

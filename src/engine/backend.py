@@ -1,0 +1,120 @@
+"""
+LLMBackend: the worker-side model session for ``arch in {"llama","mixtral"}``
+(the GPU replacement of the reference's ``FakeModel``,
+`/root/reference/src/mock_models/fake_model.py:33-67`).
+
+``predict(inputs)`` accepts the LLM request format documented in
+:func:`src.preproc.normalize_request` and returns
+``{"token_ids", "text", "num_prompt_tokens", "num_output_tokens",
+"finish_reason", "ttft_ms", "latency_ms", "tpot_ms"}``.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import time
+import uuid
+from typing import Any, Dict, List, Optional
+
+import torch
+
+from src.config import EngineConfig, ModelConfig
+from src.engine.async_engine import AsyncLLMEngine
+from src.engine.llm_engine import LLMEngine
+from src.postproc import build_llm_output
+from src.preproc import ByteTokenizer, load_tokenizer, normalize_request
+
+logger = logging.getLogger(__name__)
+
+_DEFAULT_PRESET = {"llama": "llama3-8b", "mixtral": "mixtral-8x7b"}
+
+
+def engine_config_from(config: ModelConfig) -> EngineConfig:
+    ov = config.overrides or {}
+    return EngineConfig(
+        max_num_seqs=config.max_batch_size,
+        max_num_batched_tokens=config.max_num_batched_tokens,
+        max_latency_ms=config.max_latency_ms,
+        block_size=config.kv_block_size,
+        num_kv_blocks=config.num_kv_blocks,
+        gpu_memory_fraction=config.gpu_memory_fraction,
+        enable_prefix_caching=config.enable_prefix_caching,
+        kv_block_ttl_s=ov.get("kv_block_ttl_s"),
+        use_cuda_graph=config.use_cuda_graph,
+    )
+
+
+class LLMBackend:
+    def __init__(self, config: ModelConfig, engine: Optional[LLMEngine] = None):
+        self.config = config
+        preset = config.preset or _DEFAULT_PRESET[config.arch]
+        device = config.overrides.get("device") if config.overrides else None
+        if device is None:
+            device = "cuda:0" if torch.cuda.is_available() else "cpu"
+        if engine is None:
+            ecfg = engine_config_from(config)
+            engine = LLMEngine.from_preset(preset, device=device, cfg=ecfg, max_model_len=config.max_model_len,
+                                           seed=config.seed, capture=config.use_cuda_graph)
+        self.engine = engine
+        self.tokenizer = load_tokenizer(config.model_path or None, engine.arch.vocab_size)
+        if not isinstance(self.tokenizer, ByteTokenizer):
+            engine.eos_token_id = getattr(self.tokenizer, "eos_token_id", engine.eos_token_id)
+        self.async_engine = AsyncLLMEngine(engine, name=config.model_name)
+        self.request_count = 0
+        self.error_count = 0
+        self.total_latency = 0.0
+
+    async def start(self) -> None:
+        self.async_engine.start()
+
+    async def stop(self) -> None:
+        self.async_engine.stop()
+
+    def close(self) -> None:
+        self.async_engine.stop()
+
+    def load(self) -> float:
+        s = self.engine.scheduler
+        return (len(s.running) + len(s.waiting)) / max(1, self.engine.cfg.max_num_seqs)
+
+    async def predict(self, inputs: Any) -> Dict[str, Any]:
+        if not self.async_engine.running:
+            self.async_engine.start()
+        self.request_count += 1
+        try:
+            gi = normalize_request(inputs, self.tokenizer, self.engine.max_model_len)
+        except ValueError:
+            self.error_count += 1
+            raise
+        rid = uuid.uuid4().hex
+        t0 = time.perf_counter()
+        seq = await self.async_engine.submit(rid, gi.prompt_token_ids, gi.sampling)
+        lat = (time.perf_counter() - t0) * 1e3
+        self.total_latency += lat / 1e3
+        return build_llm_output(seq.output_ids, self.tokenizer, prompt_len=seq.prompt_len,
+                                finish_reason=seq.finish_reason or "length", ttft_ms=seq.ttft_ms(),
+                                latency_ms=seq.latency_ms(), return_text=gi.return_text)
+
+    async def predict_batch(self, inputs_list: List[Any]) -> List[Dict[str, Any]]:
+        return list(await asyncio.gather(*(self.predict(x) for x in inputs_list)))
+
+    async def handle_op(self, op: str, msg: Dict[str, Any]) -> Dict[str, Any]:
+        if op == "engine_stats":
+            return {"success": True, "stats": self.async_engine.stats()}
+        raise ValueError(f"unsupported op {op}")
+
+    def get_metrics(self) -> Dict[str, Any]:
+        m = {
+            "model_name": self.config.model_name,
+            "request_count": self.request_count,
+            "error_count": self.error_count,
+            "avg_latency": self.total_latency / self.request_count if self.request_count else 0.0,
+            "engine": self.engine.get_stats(),
+        }
+        if self.engine.device.type == "cuda":
+            free, total = torch.cuda.mem_get_info(self.engine.device)
+            m["hbm_used_gib"] = (total - free) / 2**30
+            m["hbm_total_gib"] = total / 2**30
+        return m

@@ -1,0 +1,195 @@
+"""
+LLMEngine: model + paged KV pool + scheduler + runner for one worker (one GPU,
+or one TP group driven from its rank 0).
+
+    engine = LLMEngine.from_preset("llama3-8b", device="cuda:0")
+    engine.add_request("r1", prompt_ids, SamplingParams(max_tokens=128))
+    while engine.has_work(): finished = engine.step()
+
+HBM budget (288 GB per MI355X): weights are created first, then the KV pool
+takes ``gpu_memory_fraction`` of what is left after an activation reserve
+sized from ``max_num_batched_tokens`` — for Llama-3-8B that is ≈1.9 M tokens of
+KV (128 KiB/token), so prefix blocks stay cached long after their requests
+finish and LRU/TTL eviction only starts under real memory pressure.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+import logging
+import time
+from typing import Callable, Dict, List, Optional
+
+import torch
+
+from src.config import EngineConfig
+from src.engine.block_manager import KVBlockManager
+from src.engine.model_runner import KVPool, ModelRunner
+from src.engine.scheduler import Scheduler, SchedulerOutput
+from src.engine.sequence import Sequence, SeqStatus
+from src.models.llama import CausalLM
+from src.models.presets import ArchConfig, get_preset
+from src.parallel.tp import TPContext
+from src.preproc import SamplingParams
+
+logger = logging.getLogger(__name__)
+
+
+def plan_kv_blocks(arch: ArchConfig, model: CausalLM, cfg: EngineConfig, device: torch.device) -> int:
+    if cfg.num_kv_blocks:
+        return cfg.num_kv_blocks
+    per_block = KVPool.bytes_per_block(arch.num_layers, model.hkv, cfg.block_size, arch.head_dim)
+    if device.type != "cuda":
+        return 512
+    free, total = torch.cuda.mem_get_info(device)
+    h = arch.hidden_size
+    inter = model.inter * (arch.top_k if arch.is_moe else 1)
+    t = cfg.max_num_batched_tokens
+    # activations of one prefill step (qkv, attn, gate_up, act, residual ...) + logits + slack
+    act = t * (3 * h + (model.hq + 2 * model.hkv) * arch.head_dim + 3 * inter) * 2
+    act += cfg.max_num_seqs * arch.vocab_size * 4 + (2 << 30)
+    budget = min(free - act, cfg.gpu_memory_fraction * total - (total - free) - act)
+    return max(16, int(budget // per_block))
+
+
+class LLMEngine:
+    def __init__(self, model: CausalLM, cfg: EngineConfig, max_model_len: int, eos_token_id: Optional[int] = 2):
+        self.model = model
+        self.arch = model.arch
+        self.cfg = cfg
+        self.device = model.device
+        self.max_model_len = min(max_model_len, model.max_position)
+        self.eos_token_id = eos_token_id
+        nblocks = plan_kv_blocks(self.arch, model, cfg, self.device)
+        self.pool = KVPool(self.arch.num_layers, nblocks, model.hkv, cfg.block_size, self.arch.head_dim,
+                           self.device, dtype=model.dtype)
+        self.blocks = KVBlockManager(nblocks, cfg.block_size, cfg.enable_prefix_caching, cfg.kv_block_ttl_s)
+        self.scheduler = Scheduler(cfg, self.blocks, self.max_model_len)
+        self.runner = ModelRunner(model, self.pool, cfg, self.max_model_len)
+        self.seqs: Dict[str, Sequence] = {}
+        self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "finished": 0, "prefill_time": 0.0,
+                      "decode_time": 0.0, "steps": 0, "prefix_hit_tokens": 0}
+        logger.info("KV pool: %d blocks x %d tokens = %.1f GiB (%d tokens)", nblocks, cfg.block_size,
+                    self.pool.nbytes / 2**30, nblocks * cfg.block_size)
+
+    @classmethod
+    def from_preset(cls, preset: str, device="cuda:0", cfg: Optional[EngineConfig] = None, max_model_len: int = 4096,
+                    tp: Optional[TPContext] = None, seed: int = 0, capture: bool = True, dtype=torch.bfloat16,
+                    **arch_overrides):
+        arch = get_preset(preset, **arch_overrides)
+        cfg = cfg or EngineConfig()
+        model = CausalLM(arch, device, dtype=dtype, tp=tp, seed=seed, max_position=max(max_model_len, 16))
+        eng = cls(model, cfg, max_model_len)
+        if capture:
+            eng.runner.capture_graphs()
+        return eng
+
+    # ------------------------------------------------------------ requests
+    def add_request(self, request_id: str, prompt_ids: List[int], sampling: SamplingParams,
+                    on_finish: Optional[Callable[[Sequence], None]] = None, user_data=None) -> Sequence:
+        if request_id in self.seqs:
+            raise ValueError(f"duplicate request id {request_id}")
+        if len(prompt_ids) + sampling.max_tokens > self.max_model_len:
+            raise ValueError(f"prompt + max_tokens exceeds max_model_len={self.max_model_len}")
+        seq = Sequence(request_id, list(prompt_ids), dataclasses.replace(sampling), on_finish=on_finish,
+                       user_data=user_data)
+        self.seqs[request_id] = seq
+        self.scheduler.add(seq)
+        self.stats["prompt_tokens"] += len(prompt_ids)
+        return seq
+
+    def abort(self, request_id: str) -> None:
+        seq = self.scheduler.abort(request_id)
+        if seq is not None:
+            self._complete(seq)
+
+    def has_work(self) -> bool:
+        return self.scheduler.has_work()
+
+    # ----------------------------------------------------------------- step
+    def step(self) -> List[Sequence]:
+        """One engine iteration. Returns the sequences that finished in it."""
+        out: SchedulerOutput = self.scheduler.schedule()
+        finished: List[Sequence] = []
+        for s in out.preempted:
+            if s.status == SeqStatus.FINISHED:  # rejected at admission
+                s.finish_time = time.perf_counter()
+                finished.append(s)
+                self._complete(s)
+        if out.empty:
+            return finished
+        t0 = time.perf_counter()
+        now = t0
+        if out.prefill:
+            toks = self.runner.prefill(out.prefill)
+            now = time.perf_counter()
+            self.stats["prefill_time"] += now - t0
+            for c, tok in zip(out.prefill, toks):
+                seq = c.seq
+                seq.num_computed = c.start + c.length
+                if tok is None:
+                    continue
+                self.blocks.register_prompt_blocks(seq)
+                self.stats["prefix_hit_tokens"] += seq.num_prefix_hit
+                if seq.first_token_time is None:
+                    seq.first_token_time = now
+                self._append(seq, tok, finished)
+        else:
+            toks = self.runner.decode(out.decode)
+            now = time.perf_counter()
+            self.stats["decode_time"] += now - t0
+            for seq, tok in zip(out.decode, toks):
+                seq.num_computed += 1
+                self._append(seq, tok, finished)
+        self.stats["steps"] += 1
+        if self.cfg.kv_block_ttl_s:
+            self.blocks.evict_expired()
+        return finished
+
+    def _append(self, seq: Sequence, tok: int, finished: List[Sequence]) -> None:
+        seq.output_ids.append(int(tok))
+        self.stats["generated_tokens"] += 1
+        sp = seq.sampling
+        reason = None
+        if not sp.ignore_eos and self.eos_token_id is not None and tok == self.eos_token_id:
+            reason = "stop"
+        elif tok in sp.stop_token_ids:
+            reason = "stop"
+        elif len(seq.output_ids) >= sp.max_tokens:
+            reason = "length"
+        elif len(seq) >= self.max_model_len:
+            reason = "length"
+        if reason:
+            self.scheduler.finish(seq, reason)
+            finished.append(seq)
+            self._complete(seq)
+
+    def _complete(self, seq: Sequence) -> None:
+        self.seqs.pop(seq.request_id, None)
+        self.stats["finished"] += 1
+        prev = getattr(seq, "_preempted_outputs", None)
+        if prev:
+            seq.output_ids = prev + seq.output_ids
+            seq.prompt_ids = seq.prompt_ids[: len(seq.prompt_ids) - len(prev)]
+            seq._preempted_outputs = []  # type: ignore[attr-defined]
+        if seq.on_finish is not None:
+            seq.on_finish(seq)
+
+    # ------------------------------------------------------------- helpers
+    def generate(self, prompts: List[List[int]], sampling: SamplingParams) -> List[List[int]]:
+        """Offline batch generation (blocking)."""
+        res: Dict[str, List[int]] = {}
+        for i, p in enumerate(prompts):
+            self.add_request(f"gen-{i}-{time.monotonic_ns()}", p, sampling,
+                             on_finish=lambda s, i=i: res.__setitem__(i, list(s.output_ids)))
+        while self.has_work():
+            self.step()
+        return [res[i] for i in range(len(prompts))]
+
+    def get_stats(self) -> dict:
+        s = dict(self.stats)
+        s.update(self.scheduler.stats())
+        s["kv"] = self.blocks.stats()
+        s["kv_pool_gib"] = self.pool.nbytes / 2**30
+        s["graphs"] = list(self.runner.graph_sizes)
+        return s

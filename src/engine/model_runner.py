@@ -1,0 +1,271 @@
+"""
+Model runner: turns a scheduled step into GPU work on one HIP stream.
+
+* Step inputs are assembled by the native step builder
+  (``csrc/runtime/step_builder.h``) straight into pinned host buffers and
+  shipped with one async H2D copy per buffer.
+* Prefill steps run eagerly (ragged shapes; their GEMMs dominate anyway).
+* Decode steps replay a **hipGraph** captured per padded batch size
+  (``EngineConfig.graph_batch_sizes``): embedding → 32 layers of
+  norm/GEMM/RoPE+KV-write/paged-attention → LM head → sampling is one graph
+  launch, so host launch overhead (≈10 launches × 32 layers) disappears.
+  The graph reads everything from static buffers; the decode attention grid
+  is sized for ``max_model_len`` and idle workgroups exit immediately.
+* Only the token ids (8 B per sequence) come back to the host each step.
+"""
+
+from __future__ import annotations
+
+import bisect
+import logging
+from typing import Dict, List, Optional, Sequence as Seq
+
+import torch
+
+from src import ops
+from src.config import EngineConfig
+from src.engine.block_manager import native_runtime
+from src.engine.scheduler import PrefillChunk
+from src.engine.sequence import Sequence
+from src.models.llama import AttnMetadata, CausalLM
+
+logger = logging.getLogger(__name__)
+
+
+class KVPool:
+    """One HBM tensor for the whole KV cache:
+    [layers, 2 (K,V), num_blocks, kv_heads, block_size, head_dim] (bf16)."""
+
+    def __init__(self, num_layers: int, num_blocks: int, kv_heads: int, block_size: int, head_dim: int, device,
+                 dtype=torch.bfloat16):
+        self.shape = (num_layers, 2, num_blocks, kv_heads, block_size, head_dim)
+        self.tensor = torch.empty(self.shape, dtype=dtype, device=device)
+        self.num_blocks = num_blocks
+        self.block_size = block_size
+
+    @property
+    def nbytes(self) -> int:
+        return self.tensor.numel() * self.tensor.element_size()
+
+    def planes(self) -> torch.Tensor:
+        """[layers*2, num_blocks, ...] view used by the block movers."""
+        s = self.shape
+        return self.tensor.view(s[0] * s[1], s[2], s[3], s[4], s[5])
+
+    @staticmethod
+    def bytes_per_block(num_layers: int, kv_heads: int, block_size: int, head_dim: int, dtype_bytes: int = 2) -> int:
+        return num_layers * 2 * kv_heads * block_size * head_dim * dtype_bytes
+
+
+class ModelRunner:
+    def __init__(self, model: CausalLM, pool: KVPool, cfg: EngineConfig, max_model_len: int):
+        self.model = model
+        self.pool = pool
+        self.cfg = cfg
+        self.device = model.device
+        self.is_cuda = self.device.type == "cuda"
+        self.bs = pool.block_size
+        self.max_model_len = max_model_len
+        self.bt_width = (max_model_len + self.bs - 1) // self.bs
+        self.rt = native_runtime()
+        self.max_seqs = cfg.max_num_seqs
+        self.max_tokens = max(cfg.max_num_batched_tokens, self.max_seqs)
+        pin = self.is_cuda
+        i64, i32 = torch.int64, torch.int32
+        # pinned host staging
+        self.h_ids = torch.zeros(self.max_tokens, dtype=i64, pin_memory=pin)
+        self.h_pos = torch.zeros(self.max_tokens, dtype=i64, pin_memory=pin)
+        self.h_slots = torch.zeros(self.max_tokens, dtype=i64, pin_memory=pin)
+        self.h_cu = torch.zeros(self.max_seqs + 1, dtype=i32, pin_memory=pin)
+        self.h_ctx = torch.zeros(self.max_seqs, dtype=i32, pin_memory=pin)
+        self.h_bt = torch.zeros(self.max_seqs, self.bt_width, dtype=i32, pin_memory=pin)
+        self.h_last = torch.zeros(self.max_seqs, dtype=i64, pin_memory=pin)
+        self.h_temp = torch.zeros(self.max_seqs, dtype=torch.float32, pin_memory=pin)
+        self.h_topk = torch.zeros(self.max_seqs, dtype=i32, pin_memory=pin)
+        self.h_topp = torch.ones(self.max_seqs, dtype=torch.float32, pin_memory=pin)
+        self.h_seed = torch.zeros(self.max_seqs, dtype=i64, pin_memory=pin)
+        self.h_step = torch.zeros(self.max_seqs, dtype=i64, pin_memory=pin)
+        self.h_out = torch.zeros(self.max_seqs, dtype=i64, pin_memory=pin)
+        # numpy views over the pinned buffers (zero-copy) for cheap bulk writes
+        self.n_ids, self.n_temp, self.n_topk = self.h_ids.numpy(), self.h_temp.numpy(), self.h_topk.numpy()
+        self.n_topp, self.n_seed, self.n_step = self.h_topp.numpy(), self.h_seed.numpy(), self.h_step.numpy()
+        self._samp_key = None
+        dev = self.device
+        # device-side static buffers (graph inputs)
+        self.d_ids = torch.zeros(self.max_tokens, dtype=i64, device=dev)
+        self.d_pos = torch.zeros(self.max_tokens, dtype=i64, device=dev)
+        self.d_slots = torch.zeros(self.max_tokens, dtype=i64, device=dev)
+        self.d_cu = torch.zeros(self.max_seqs + 1, dtype=i32, device=dev)
+        self.d_ctx = torch.ones(self.max_seqs, dtype=i32, device=dev)
+        self.d_bt = torch.zeros(self.max_seqs, self.bt_width, dtype=i32, device=dev)
+        self.d_last = torch.zeros(self.max_seqs, dtype=i64, device=dev)
+        self.d_temp = torch.zeros(self.max_seqs, dtype=torch.float32, device=dev)
+        self.d_topk = torch.zeros(self.max_seqs, dtype=i32, device=dev)
+        self.d_topp = torch.ones(self.max_seqs, dtype=torch.float32, device=dev)
+        self.d_seed = torch.zeros(self.max_seqs, dtype=i64, device=dev)
+        self.d_step = torch.zeros(self.max_seqs, dtype=i64, device=dev)
+        self.d_out = torch.zeros(self.max_seqs, dtype=i64, device=dev)
+        if self.is_cuda:
+            maxp = ops.decode_partials(max_model_len)
+            hq = model.hq
+            self.part_o = torch.empty(self.max_seqs * hq * maxp * 128, dtype=torch.float32, device=dev)
+            self.part_ml = torch.empty(self.max_seqs * hq * maxp * 2, dtype=torch.float32, device=dev)
+        else:
+            self.part_o = self.part_ml = None
+        self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.graph_sizes: List[int] = []
+        self._graph_pool = None
+        self.stream = torch.cuda.current_stream(dev) if self.is_cuda else None
+
+    # ------------------------------------------------------------ helpers
+    def _h2d(self, n_tok: int, n_seq: int, with_cu: bool) -> None:
+        nb = self.is_cuda
+        self.d_ids[:n_tok].copy_(self.h_ids[:n_tok], non_blocking=nb)
+        self.d_pos[:n_tok].copy_(self.h_pos[:n_tok], non_blocking=nb)
+        self.d_slots[:n_tok].copy_(self.h_slots[:n_tok], non_blocking=nb)
+        self.d_ctx[:n_seq].copy_(self.h_ctx[:n_seq], non_blocking=nb)
+        self.d_bt[:n_seq].copy_(self.h_bt[:n_seq], non_blocking=nb)
+        if with_cu:
+            self.d_cu[: n_seq + 1].copy_(self.h_cu[: n_seq + 1], non_blocking=nb)
+            self.d_last[:n_seq].copy_(self.h_last[:n_seq], non_blocking=nb)
+
+    def _fill_sampling(self, seqs: Seq[Sequence], n_pad: int) -> bool:
+        """Write per-row sampling params; returns True when every row is greedy.
+        Skips the H2D copies when the rows are all greedy (the kernel's greedy
+        path ignores them) — the common decode case costs nothing here."""
+        greedy = all(s.sampling.greedy for s in seqs)
+        if greedy:
+            key = ("greedy", n_pad)
+            if self._samp_key == key:
+                return True
+            self.n_temp[:n_pad] = 0.0
+            self.n_topk[:n_pad] = 0
+            self.n_topp[:n_pad] = 1.0
+            self._samp_key = key
+        else:
+            n = len(seqs)
+            self.n_temp[:n] = [s.sampling.temperature for s in seqs]
+            self.n_topk[:n] = [s.sampling.top_k for s in seqs]
+            self.n_topp[:n] = [s.sampling.top_p for s in seqs]
+            self.n_seed[:n] = [s.sampling.seed if s.sampling.seed is not None else s.seq_id for s in seqs]
+            self.n_step[:n] = [len(s.output_ids) + len(getattr(s, "_preempted_outputs", ())) for s in seqs]
+            self.n_temp[n:n_pad] = 0.0
+            self.n_topk[n:n_pad] = 0
+            self.n_topp[n:n_pad] = 1.0
+            self._samp_key = None
+        nb = self.is_cuda
+        for h, d in ((self.h_temp, self.d_temp), (self.h_topk, self.d_topk), (self.h_topp, self.d_topp),
+                     (self.h_seed, self.d_seed), (self.h_step, self.d_step)):
+            d[:n_pad].copy_(h[:n_pad], non_blocking=nb)
+        return greedy
+
+    def _sample(self, logits: torch.Tensor, n: int, greedy: bool, out: torch.Tensor) -> torch.Tensor:
+        if greedy:
+            return ops.sample(logits, out=out[:n]) if self.is_cuda else ops.sample(logits)
+        args = (self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n], self.d_step[:n])
+        return ops.sample(logits, *args, out=out[:n]) if self.is_cuda else ops.sample(logits, *args)
+
+    def _to_host(self, ids: torch.Tensor, n: int) -> List[int]:
+        if self.is_cuda:
+            self.h_out[:n].copy_(ids[:n], non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            return self.h_out[:n].tolist()
+        return ids[:n].tolist()
+
+    # ------------------------------------------------------------ prefill
+    @torch.inference_mode()
+    def prefill(self, chunks: List[PrefillChunk]) -> List[Optional[int]]:
+        """Run one ragged prefill batch; returns the sampled token for every
+        chunk that completes its prompt (None for partial chunks)."""
+        toks = [c.seq.prompt_ids[c.start: c.start + c.length] for c in chunks]
+        starts = [c.start for c in chunks]
+        tables = [c.seq.block_table for c in chunks]
+        n = len(chunks)
+        t = self.rt.build_prefill_inputs(toks, starts, tables, self.bs, self.h_ids.data_ptr(),
+                                         self.h_pos.data_ptr(), self.h_slots.data_ptr(), self.h_cu.data_ptr(),
+                                         self.h_ctx.data_ptr(), self.h_bt.data_ptr(), self.bt_width,
+                                         self.h_last.data_ptr())
+        self._h2d(t, n, with_cu=True)
+        meta = AttnMetadata(is_prefill=True, slot_mapping=self.d_slots[:t], block_tables=self.d_bt[:n],
+                            ctx_lens=self.d_ctx[:n], cu_q=self.d_cu[: n + 1],
+                            max_q_len=max(c.length for c in chunks))
+        hidden = self.model.forward(self.d_ids[:t], self.d_pos[:t], meta, self.pool.tensor)
+        done = [i for i, c in enumerate(chunks) if c.completes_prompt]
+        if not done:
+            if self.is_cuda:
+                torch.cuda.current_stream(self.device).synchronize()
+            return [None] * n
+        sel = [c.seq for c in chunks if c.completes_prompt]
+        greedy = self._fill_sampling(sel, len(sel))
+        if len(done) == n:
+            last = self.d_last[:n]
+        else:
+            last = self.d_last[torch.tensor(done, device=self.device)]
+        logits = self.model.compute_logits(hidden.index_select(0, last))
+        ids = self._sample(logits, len(sel), greedy, self.d_out)
+        vals = self._to_host(ids, len(sel))
+        res: List[Optional[int]] = [None] * n
+        for j, i in enumerate(done):
+            res[i] = vals[j]
+        return res
+
+    # ------------------------------------------------------------- decode
+    def _decode_forward(self, n: int) -> torch.Tensor:
+        meta = AttnMetadata(is_prefill=False, slot_mapping=self.d_slots[:n], block_tables=self.d_bt[:n],
+                            ctx_lens=self.d_ctx[:n], max_ctx=self.max_model_len, part_o=self.part_o,
+                            part_ml=self.part_ml)
+        hidden = self.model.forward(self.d_ids[:n], self.d_pos[:n], meta, self.pool.tensor)
+        logits = self.model.compute_logits(hidden)
+        return ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
+                          self.d_step[:n], out=self.d_out[:n])
+
+    @torch.inference_mode()
+    def capture_graphs(self) -> None:
+        if not self.is_cuda or not self.cfg.use_cuda_graph:
+            return
+        sizes = sorted({min(b, self.max_seqs) for b in self.cfg.graph_batch_sizes} | {self.max_seqs})
+        self._graph_pool = torch.cuda.graph_pool_handle()
+        # warm up (hipBLASLt heuristics, kernel loads) outside capture
+        for b in sizes:
+            self.d_slots[:b].fill_(-1)
+            self.d_ctx[:b].fill_(1)
+            self._decode_forward(b)
+        torch.cuda.synchronize(self.device)
+        for b in reversed(sizes):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self._graph_pool):
+                self._decode_forward(b)
+            self.graphs[b] = g
+        torch.cuda.synchronize(self.device)
+        self.graph_sizes = sizes
+        logger.info("captured decode hipGraphs for batch sizes %s", sizes)
+
+    @torch.inference_mode()
+    def decode(self, seqs: List[Sequence]) -> List[int]:
+        n = len(seqs)
+        pad = n
+        if self.graphs:
+            k = bisect.bisect_left(self.graph_sizes, n)
+            pad = self.graph_sizes[k] if k < len(self.graph_sizes) else n
+        self.n_ids[:n] = [s.last_token for s in seqs]
+        self.n_ids[n:pad] = 0
+        self.rt.build_decode_inputs([s.block_table for s in seqs], [len(s) for s in seqs], self.bs,
+                                    self.h_pos.data_ptr(), self.h_slots.data_ptr(), self.h_ctx.data_ptr(),
+                                    self.h_bt.data_ptr(), self.bt_width, pad)
+        self._fill_sampling(seqs, pad)
+        self._h2d(pad, pad, with_cu=False)
+        g = self.graphs.get(pad)
+        if g is not None:
+            g.replay()
+            ids = self.d_out
+        else:
+            ids = self._decode_forward(n) if self.is_cuda else self._decode_cpu(n)
+        return self._to_host(ids, n)
+
+    def _decode_cpu(self, n: int) -> torch.Tensor:
+        meta = AttnMetadata(is_prefill=False, slot_mapping=self.d_slots[:n], block_tables=self.d_bt[:n],
+                            ctx_lens=self.d_ctx[:n], max_ctx=self.max_model_len)
+        hidden = self.model.forward(self.d_ids[:n], self.d_pos[:n], meta, self.pool.tensor)
+        logits = self.model.compute_logits(hidden)
+        return ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
+                          self.d_step[:n])

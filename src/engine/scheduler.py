@@ -1,0 +1,209 @@
+"""
+Continuous-batching scheduler (iteration-level): the reference Batcher's
+max-batch / max-latency flush (`/root/reference/src/batcher.py:144-166`)
+re-cast for token generation.
+
+Every engine step is either
+
+* a **prefill step** — new prompts (and chunks of long prompts: chunked
+  prefill) packed into one ragged batch of at most ``max_num_batched_tokens``
+  tokens, or
+* a **decode step** — one token for every running sequence (≤ ``max_num_seqs``),
+  replayed from a captured hipGraph.
+
+Sequences join the running batch as soon as their prompt is done and leave it
+the step they finish, so the batch never waits for its slowest member.
+``max_latency_ms`` bounds how long an idle engine waits to accumulate a fuller
+first prefill batch. When the KV pool runs dry during decode the most recently
+admitted sequence is preempted (blocks freed, recomputed later; its cached
+prefix blocks usually make the recompute cheap).
+"""
+
+from __future__ import annotations
+
+import time
+from collections import deque
+from dataclasses import dataclass, field
+from typing import Deque, List, Optional, Tuple
+
+from src.config import EngineConfig
+from src.engine.block_manager import KVBlockManager
+from src.engine.sequence import Sequence, SeqStatus
+
+
+@dataclass
+class PrefillChunk:
+    seq: Sequence
+    start: int        # first position computed in this step
+    length: int       # tokens computed in this step
+
+    @property
+    def completes_prompt(self) -> bool:
+        return self.start + self.length >= self.seq.prompt_len
+
+
+@dataclass
+class SchedulerOutput:
+    prefill: List[PrefillChunk] = field(default_factory=list)
+    decode: List[Sequence] = field(default_factory=list)
+    preempted: List[Sequence] = field(default_factory=list)
+
+    @property
+    def empty(self) -> bool:
+        return not self.prefill and not self.decode
+
+    @property
+    def num_tokens(self) -> int:
+        return sum(c.length for c in self.prefill) + len(self.decode)
+
+
+class Scheduler:
+    def __init__(self, cfg: EngineConfig, blocks: KVBlockManager, max_model_len: int):
+        self.cfg = cfg
+        self.blocks = blocks
+        self.max_model_len = max_model_len
+        self.waiting: Deque[Sequence] = deque()
+        self.running: List[Sequence] = []
+        self.num_preemptions = 0
+        self.steps_prefill = 0
+        self.steps_decode = 0
+
+    def add(self, seq: Sequence) -> None:
+        seq.status = SeqStatus.WAITING
+        self.waiting.append(seq)
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    def abort(self, request_id: str) -> Optional[Sequence]:
+        for q in (self.waiting, self.running):
+            for s in list(q):
+                if s.request_id == request_id:
+                    q.remove(s)
+                    self.blocks.free(s)
+                    s.status = SeqStatus.FINISHED
+                    s.finish_reason = "abort"
+                    return s
+        return None
+
+    # ------------------------------------------------------------- policy
+    def _hold_for_batching(self, now: float) -> bool:
+        """Idle engine + a partial first batch younger than max_latency: wait."""
+        if self.running or not self.waiting:
+            return False
+        if len(self.waiting) >= self.cfg.max_num_seqs:
+            return False
+        tokens = sum(s.prompt_len for s in self.waiting)
+        if tokens >= self.cfg.max_num_batched_tokens:
+            return False
+        oldest = self.waiting[0].arrival
+        return (now - oldest) * 1e3 < self.cfg.max_latency_ms
+
+    def next_wakeup(self) -> Optional[float]:
+        """Seconds until a held batch must be released (for the engine loop)."""
+        if not self.waiting or self.running:
+            return None
+        return max(0.0, self.cfg.max_latency_ms / 1e3 - (time.perf_counter() - self.waiting[0].arrival))
+
+    def schedule(self, now: Optional[float] = None) -> SchedulerOutput:
+        now = time.perf_counter() if now is None else now
+        out = SchedulerOutput()
+        budget = self.cfg.max_num_batched_tokens
+        # 1) continue chunked prefills already running
+        for seq in self.running:
+            if budget <= 0:
+                break
+            if seq.in_prefill:
+                n = min(seq.prompt_len - seq.num_computed, budget)
+                out.prefill.append(PrefillChunk(seq, seq.num_computed, n))
+                budget -= n
+        # 2) admit new prompts
+        if not self._hold_for_batching(now):
+            while self.waiting and budget > 0 and len(self.running) < self.cfg.max_num_seqs:
+                seq = self.waiting[0]
+                if len(seq) > self.max_model_len:
+                    self.waiting.popleft()
+                    seq.status = SeqStatus.FINISHED
+                    seq.finish_reason = "length_exceeds_max_model_len"
+                    out.preempted.append(seq)  # reported back as failed
+                    continue
+                # reserve one block of headroom per running sequence for decode growth
+                if not self.blocks.can_allocate(seq, reserve=len(self.running) // 4):
+                    break
+                self.waiting.popleft()
+                self.blocks.allocate(seq)
+                seq.status = SeqStatus.RUNNING
+                self.running.append(seq)
+                remaining = len(seq) - seq.num_computed
+                if seq.imported_kv:
+                    continue  # KV shipped from a prefill worker: goes straight to decode
+                n = min(seq.prompt_len - seq.num_computed, budget) if seq.in_prefill else remaining
+                out.prefill.append(PrefillChunk(seq, seq.num_computed, n))
+                budget -= n
+        if out.prefill:
+            self.steps_prefill += 1
+            return out
+        # 3) decode everything that is past its prompt
+        ready = [s for s in self.running if not s.in_prefill and s.num_computed == len(s) - 1]
+        ready.sort(key=lambda s: s.arrival)
+        decode: List[Sequence] = []
+        for seq in ready:
+            if seq.status != SeqStatus.RUNNING:
+                continue
+            while not self.blocks.ensure_slots(seq, len(seq)):
+                victim = self._pick_victim(exclude=seq)
+                if victim is None:
+                    break
+                self._preempt(victim)
+                out.preempted.append(victim)
+                if victim in decode:
+                    decode.remove(victim)
+            else:
+                decode.append(seq)
+                continue
+            # could not find room even after preempting everyone else
+            self._preempt(seq)
+            out.preempted.append(seq)
+        out.decode = decode
+        if decode:
+            self.steps_decode += 1
+        return out
+
+    def _pick_victim(self, exclude: Sequence) -> Optional[Sequence]:
+        cands = [s for s in self.running if s is not exclude and s.status == SeqStatus.RUNNING]
+        return max(cands, key=lambda s: s.arrival) if cands else None
+
+    def _preempt(self, seq: Sequence) -> None:
+        """Recompute-style preemption: drop the KV, requeue at the front."""
+        self.blocks.free(seq)
+        if seq in self.running:
+            self.running.remove(seq)
+        seq.num_computed = 0
+        seq.num_preemptions += 1
+        seq.status = SeqStatus.WAITING
+        # the generated tokens become part of the prompt for the recompute
+        seq.prompt_ids = seq.prompt_ids + seq.output_ids
+        seq.sampling.max_tokens -= len(seq.output_ids)
+        seq._preempted_outputs = getattr(seq, "_preempted_outputs", []) + seq.output_ids  # type: ignore[attr-defined]
+        seq.output_ids = []
+        seq.block_hashes = None
+        self.waiting.appendleft(seq)
+        self.num_preemptions += 1
+
+    # ------------------------------------------------------------ results
+    def finish(self, seq: Sequence, reason: str) -> None:
+        seq.status = SeqStatus.FINISHED
+        seq.finish_reason = reason
+        seq.finish_time = time.perf_counter()
+        if seq in self.running:
+            self.running.remove(seq)
+        self.blocks.free(seq)
+
+    def stats(self) -> dict:
+        return {
+            "waiting": len(self.waiting),
+            "running": len(self.running),
+            "preemptions": self.num_preemptions,
+            "steps_prefill": self.steps_prefill,
+            "steps_decode": self.steps_decode,
+        }

@@ -1,0 +1,94 @@
+"""The full engine on the MI355X: HIP kernels + hipBLASLt + paged KV +
+continuous batching + hipGraph decode, checked against a no-cache recompute."""
+
+import random
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from src import ops  # noqa: E402
+from src.config import EngineConfig  # noqa: E402
+from src.engine import LLMEngine  # noqa: E402
+from src.models.llama import AttnMetadata  # noqa: E402
+from src.preproc import SamplingParams  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def engine():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert ops.native_available()
+    cfg = EngineConfig(max_num_seqs=8, max_num_batched_tokens=512, num_kv_blocks=512, max_latency_ms=0.0,
+                       graph_batch_sizes=[1, 2, 4, 8])
+    return LLMEngine.from_preset("llama-mini", device="cuda:0", cfg=cfg, max_model_len=1024)
+
+
+@torch.inference_mode()
+def reference_with_margins(model, prompt, n):
+    """Greedy no-cache recompute; also returns the top1-top2 logit margin per step."""
+    dev = model.device
+    ids, toks, margins = list(prompt), [], []
+    nb = (len(prompt) + n + 15) // 16
+    pool = torch.zeros(model.arch.num_layers, 2, nb, model.hkv, 16, 128, dtype=model.dtype, device=dev)
+    for _ in range(n):
+        t = len(ids)
+        pos = torch.arange(t, device=dev)
+        meta = AttnMetadata(True, pos.clone(), torch.arange(nb, dtype=torch.int32, device=dev)[None],
+                            torch.tensor([t], dtype=torch.int32, device=dev),
+                            torch.tensor([0, t], dtype=torch.int32, device=dev), t)
+        h = model.forward(torch.tensor(ids, device=dev), pos, meta, pool)
+        lg = model.compute_logits(h[-1:])[0].float()
+        top = torch.topk(lg, 2)
+        toks.append(int(top.indices[0]))
+        margins.append(float(top.values[0] - top.values[1]))
+        ids.append(toks[-1])
+    return toks, margins
+
+
+def agree(out, ref, margins, thr=0.25):
+    """Tokens must agree up to the first near-tie of the reference."""
+    for o, r, m in zip(out, ref, margins):
+        if m < thr:
+            return True
+        if o != r:
+            return False
+    return True
+
+
+def test_engine_matches_reference(engine):
+    rng = random.Random(0)
+    prompts = [[rng.randrange(3, 32000) for _ in range(rng.randrange(3, 300))] for _ in range(7)]
+    outs = engine.generate(prompts, SamplingParams(max_tokens=12))
+    assert engine.runner.graphs, "decode hipGraphs should be captured"
+    for p, o in zip(prompts, outs):
+        r, m = reference_with_margins(engine.model, p, 12)
+        assert agree(o, r, m), (o, r, m)
+
+
+def test_prefix_cache_and_long_prompt_chunking(engine):
+    rng = random.Random(1)
+    shared = [rng.randrange(3, 32000) for _ in range(400)]
+    ps = [shared + [5, 6], shared + [7, 8, 9]]
+    hits0 = engine.stats["prefix_hit_tokens"]
+    outs = engine.generate(ps, SamplingParams(max_tokens=6))   # 402 tokens > budget 512? no; two prompts chunk
+    outs2 = engine.generate(ps, SamplingParams(max_tokens=6))
+    assert engine.stats["prefix_hit_tokens"] > hits0
+    assert outs == outs2
+    for p, o in zip(ps, outs):
+        r, m = reference_with_margins(engine.model, p, 6)
+        assert agree(o, r, m)
+
+
+def test_sampling_modes(engine):
+    sp = SamplingParams(max_tokens=10, temperature=0.9, top_k=50, top_p=0.95, seed=7)
+    a = engine.generate([[1, 2, 3, 4]], sp)[0]
+    b = engine.generate([[1, 2, 3, 4]], sp)[0]
+    assert a == b and len(a) == 10
+
+
+def test_kv_pool_accounting(engine):
+    st = engine.get_stats()
+    assert st["kv"]["used"] == 0
+    assert st["running"] == 0 and st["waiting"] == 0
