@@ -57,6 +57,7 @@ def parse():
     p.add_argument("--max-model-len", type=int, default=2048)
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--temperature", type=float, default=0.0)
+    p.add_argument("--tp", type=int, default=1, help="tensor-parallel degree per replica (70B: --tp 8)")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args()
 
@@ -100,8 +101,33 @@ def main():
                        max_latency_ms=args.max_latency_ms, use_cuda_graph=not args.no_graph,
                        graph_batch_sizes=[1, 2, 4, 8, 16, 24, 32, args.batch])
     t_init = time.perf_counter()
-    engine = LLMEngine.from_preset(args.preset, device=dev, cfg=cfg, max_model_len=args.max_model_len,
-                                   seed=1234, capture=not args.no_graph)
+    tp = None
+    if args.tp > 1:
+        from src.parallel.tp import init_tp
+        from src.parallel.tp_runner import build_tp_engine
+
+        tp = init_tp(args.tp)
+        obj = build_tp_engine(args.preset, tp, dev, cfg=cfg, max_model_len=args.max_model_len, seed=1234,
+                              capture=not args.no_graph)
+        if tp.rank != 0:  # follower: mirror the leader through warmup and the timed waves
+            obj.follower_loop()
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            obj.follower_loop()
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            t = torch.zeros(1, device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dist.all_gather_object([None] * world, [])
+            dist.barrier()
+            dist.destroy_process_group()
+            return
+        engine = obj
+    else:
+        engine = LLMEngine.from_preset(args.preset, device=dev, cfg=cfg, max_model_len=args.max_model_len,
+                                       seed=1234, capture=not args.no_graph)
+    engine.eos_token_id = None
+    replicas = n_gpus // args.tp
     init_s = time.perf_counter() - t_init
     aeng = AsyncLLMEngine(engine)
     aeng.start()
@@ -122,6 +148,8 @@ def main():
         for w in range(args.warmup):
             await serve_wave(batcher, args.batch, args.prompt_len, args.gen_len, args.temperature, rng, f"w{w}")
         torch.cuda.synchronize(dev)
+        if tp is not None:
+            engine.runner.stop_followers()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -134,6 +162,8 @@ def main():
             if args.verbose and rank == 0:
                 print(f"step {s}: {time.perf_counter() - t0:.2f}s", file=sys.stderr, flush=True)
         torch.cuda.synchronize(dev)
+        if tp is not None:
+            engine.runner.stop_followers()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -154,7 +184,7 @@ def main():
         gathered = [None] * world
         dist.all_gather_object(gathered, lats)
         lats = [x for g in gathered for x in g]
-    total_req = args.steps * args.batch * n_gpus
+    total_req = args.steps * args.batch * replicas
     rps = total_req / elapsed
     if rank == 0:
         res = {
@@ -172,14 +202,14 @@ def main():
             "data": "synthetic",
             "p50_latency_ms": round(1e3 * statistics.median(lats), 2),
             "p99_latency_ms": round(1e3 * sorted(lats)[max(0, int(0.99 * len(lats)) - 1)], 2),
-            "output_tok_per_s": round(gen_tok * n_gpus / elapsed, 1),
+            "output_tok_per_s": round(gen_tok * replicas / elapsed, 1),
             "config": {
                 "model": args.preset.replace("llama3", "Llama-3").replace("-8b", "-8B").replace("-70b", "-70B"),
-                "global_batch": args.batch * n_gpus,
+                "global_batch": args.batch * replicas,
                 "seq_len": args.prompt_len + args.gen_len,
                 "prompt_len": args.prompt_len,
                 "gen_len": args.gen_len,
-                "parallelism": f"dp{n_gpus}",
+                "parallelism": f"dp{replicas}" + (f"-tp{args.tp}" if args.tp > 1 else ""),
                 "max_batch": args.batch,
                 "max_latency_ms": args.max_latency_ms,
                 "weights": "random-init",

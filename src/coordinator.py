@@ -174,7 +174,8 @@ class Coordinator:
             ok, _, rep = await self.rpc.probe(address, 2.0)
             if ok and rep:
                 wid = rep.get("worker_id", address)
-                self.register_worker(wid, address, {m: {} for m in rep.get("models", [])})
+                archs = rep.get("archs", {})
+                self.register_worker(wid, address, {m: {"arch": archs.get(m, "mock")} for m in rep.get("models", [])})
                 return True
             await asyncio.sleep(0.2)
         logger.error("static worker %s never answered", address)

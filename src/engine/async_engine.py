@@ -74,12 +74,28 @@ class AsyncLLMEngine:
         self._q.put((request_id, prompt_ids, sampling, callback, None, None))
         self._wake.set()
 
+    def call(self, fn, loop: Optional[asyncio.AbstractEventLoop] = None) -> asyncio.Future:
+        """Run ``fn(engine)`` on the engine thread between steps; the future
+        gets its return value (used for KV import/export and stats)."""
+        loop = loop or asyncio.get_running_loop()
+        fut = loop.create_future()
+        self._q.put(("__call__", fn, None, fut, loop, None))
+        self._wake.set()
+        return fut
+
     def _drain(self) -> None:
         while True:
             try:
                 rid, ids, sp, fut, loop, ud = self._q.get_nowait()
             except queue.Empty:
                 return
+            if rid == "__call__":
+                try:
+                    res = ids(self.engine)
+                    loop.call_soon_threadsafe(_set, fut, res)
+                except Exception as e:
+                    loop.call_soon_threadsafe(_fail, fut, e)
+                continue
 
             def done(seq: Sequence, fut=fut, loop=loop):
                 if loop is None:
@@ -88,7 +104,11 @@ class AsyncLLMEngine:
                     loop.call_soon_threadsafe(_resolve, fut, seq)
 
             try:
-                self.engine.add_request(rid, ids, sp, on_finish=done, user_data=ud)
+                if isinstance(ud, dict) and ud.get("import_packet") is not None:
+                    self.engine.add_imported(ud["import_packet"], sp, on_finish=done)
+                else:
+                    self.engine.add_request(rid, ids, sp, on_finish=done, user_data=ud,
+                                            export_kv=isinstance(ud, dict) and bool(ud.get("export_kv")))
             except Exception as e:
                 if loop is None:
                     fut(e)
@@ -137,6 +157,11 @@ def _resolve(fut: asyncio.Future, seq: Sequence) -> None:
         fut.set_exception(RuntimeError("engine failed"))
     else:
         fut.set_result(seq)
+
+
+def _set(fut: asyncio.Future, v) -> None:
+    if not fut.done():
+        fut.set_result(v)
 
 
 def _fail(fut: asyncio.Future, e: BaseException) -> None:

@@ -62,6 +62,14 @@ class LLMBackend:
         if not isinstance(self.tokenizer, ByteTokenizer):
             engine.eos_token_id = getattr(self.tokenizer, "eos_token_id", engine.eos_token_id)
         self.async_engine = AsyncLLMEngine(engine, name=config.model_name)
+        self.role = config.role
+        self._decode_link = None
+        if self.role == "prefill":
+            from src.engine.disagg import RemoteDecodeLink
+
+            addr = (config.overrides or {}).get("decode_worker")
+            if addr:
+                self._decode_link = RemoteDecodeLink(addr, config.model_name)
         self.request_count = 0
         self.error_count = 0
         self.total_latency = 0.0
@@ -90,6 +98,8 @@ class LLMBackend:
             raise
         rid = uuid.uuid4().hex
         t0 = time.perf_counter()
+        if self._decode_link is not None and gi.sampling.max_tokens > 1:
+            return await self._prefill_then_ship(rid, gi, t0)
         seq = await self.async_engine.submit(rid, gi.prompt_token_ids, gi.sampling)
         lat = (time.perf_counter() - t0) * 1e3
         self.total_latency += lat / 1e3
@@ -97,12 +107,48 @@ class LLMBackend:
                                 finish_reason=seq.finish_reason or "length", ttft_ms=seq.ttft_ms(),
                                 latency_ms=seq.latency_ms(), return_text=gi.return_text)
 
+    async def _prefill_then_ship(self, rid: str, gi, t0: float) -> Dict[str, Any]:
+        from src.engine.disagg import sampling_to_dict
+        from src.parallel.kv_transfer import KVPacket
+
+        pseq = await self.async_engine.submit(rid, gi.prompt_token_ids, gi.sampling,
+                                              user_data={"export_kv": True})
+        if pseq.finish_reason == "stop":
+            return build_llm_output(pseq.output_ids, self.tokenizer, prompt_len=pseq.prompt_len,
+                                    finish_reason="stop", ttft_ms=pseq.ttft_ms(), latency_ms=pseq.latency_ms(),
+                                    return_text=gi.return_text)
+        packet = KVPacket(rid, gi.prompt_token_ids, pseq.output_ids[0], pseq.kv_export, self.engine.cfg.block_size,
+                          sampling_to_dict(gi.sampling), ttft_ms=pseq.ttft_ms())
+        pseq.kv_export = None
+        rep = await self._decode_link.send(packet)
+        if not rep.get("success"):
+            raise RuntimeError(f"decode worker failed: {rep.get('error')}")
+        out = rep["outputs"]
+        out["latency_ms"] = (time.perf_counter() - t0) * 1e3
+        out["disaggregated"] = True
+        return out
+
+    async def _kv_import(self, msg: Dict[str, Any]) -> Dict[str, Any]:
+        from src.engine.disagg import packet_for_import
+        from src.preproc import SamplingParams
+
+        packet = packet_for_import(msg["packet"], self.engine.device)
+        sp = SamplingParams(**packet.sampling) if packet.sampling else SamplingParams()
+        if not self.async_engine.running:
+            self.async_engine.start()
+        seq = await self.async_engine.submit(packet.request_id, [], sp, user_data={"import_packet": packet})
+        return {"success": True, "outputs": build_llm_output(
+            seq.output_ids, self.tokenizer, prompt_len=seq.prompt_len, finish_reason=seq.finish_reason or "length",
+            ttft_ms=packet.ttft_ms, latency_ms=seq.latency_ms())}
+
     async def predict_batch(self, inputs_list: List[Any]) -> List[Dict[str, Any]]:
         return list(await asyncio.gather(*(self.predict(x) for x in inputs_list)))
 
     async def handle_op(self, op: str, msg: Dict[str, Any]) -> Dict[str, Any]:
         if op == "engine_stats":
             return {"success": True, "stats": self.async_engine.stats()}
+        if op == "kv_import":
+            return await self._kv_import(msg)
         raise ValueError(f"unsupported op {op}")
 
     def get_metrics(self) -> Dict[str, Any]:

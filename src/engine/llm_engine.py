@@ -53,7 +53,8 @@ def plan_kv_blocks(arch: ArchConfig, model: CausalLM, cfg: EngineConfig, device:
 
 
 class LLMEngine:
-    def __init__(self, model: CausalLM, cfg: EngineConfig, max_model_len: int, eos_token_id: Optional[int] = 2):
+    def __init__(self, model: CausalLM, cfg: EngineConfig, max_model_len: int, eos_token_id: Optional[int] = 2,
+                 runner_cls=ModelRunner):
         self.model = model
         self.arch = model.arch
         self.cfg = cfg
@@ -65,7 +66,7 @@ class LLMEngine:
                            self.device, dtype=model.dtype)
         self.blocks = KVBlockManager(nblocks, cfg.block_size, cfg.enable_prefix_caching, cfg.kv_block_ttl_s)
         self.scheduler = Scheduler(cfg, self.blocks, self.max_model_len)
-        self.runner = ModelRunner(model, self.pool, cfg, self.max_model_len)
+        self.runner = runner_cls(model, self.pool, cfg, self.max_model_len)
         self.seqs: Dict[str, Sequence] = {}
         self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "finished": 0, "prefill_time": 0.0,
                       "decode_time": 0.0, "steps": 0, "prefix_hit_tokens": 0}
@@ -86,16 +87,55 @@ class LLMEngine:
 
     # ------------------------------------------------------------ requests
     def add_request(self, request_id: str, prompt_ids: List[int], sampling: SamplingParams,
-                    on_finish: Optional[Callable[[Sequence], None]] = None, user_data=None) -> Sequence:
+                    on_finish: Optional[Callable[[Sequence], None]] = None, user_data=None,
+                    export_kv: bool = False) -> Sequence:
         if request_id in self.seqs:
             raise ValueError(f"duplicate request id {request_id}")
         if len(prompt_ids) + sampling.max_tokens > self.max_model_len:
             raise ValueError(f"prompt + max_tokens exceeds max_model_len={self.max_model_len}")
         seq = Sequence(request_id, list(prompt_ids), dataclasses.replace(sampling), on_finish=on_finish,
                        user_data=user_data)
+        if export_kv:  # disaggregated prefill: stop after the first token and hand the prompt KV over
+            seq.sampling.max_tokens = 1
+            seq.export_kv = True  # type: ignore[attr-defined]
         self.seqs[request_id] = seq
         self.scheduler.add(seq)
         self.stats["prompt_tokens"] += len(prompt_ids)
+        return seq
+
+    def add_imported(self, packet, sampling: SamplingParams,
+                     on_finish: Optional[Callable[[Sequence], None]] = None) -> Sequence:
+        """Resume a sequence whose prompt KV was computed by a prefill worker:
+        allocate blocks, scatter the shipped KV into them, join the decode batch."""
+        from src.parallel.kv_transfer import import_blocks
+
+        if packet.block_size != self.cfg.block_size:
+            raise ValueError("block size mismatch between prefill and decode workers")
+        seq = Sequence(packet.request_id, list(packet.prompt_ids), dataclasses.replace(sampling),
+                       on_finish=on_finish, imported_kv=True)
+        seq.output_ids = [int(packet.first_token)]
+        seq.first_token_time = time.perf_counter()
+        if packet.ttft_ms is not None:
+            seq.arrival = seq.first_token_time - packet.ttft_ms / 1e3
+        if len(seq) + sampling.max_tokens > self.max_model_len + 1:
+            raise ValueError("imported sequence exceeds max_model_len")
+        self.blocks.allocate(seq)
+        nb = self.blocks.blocks_needed(seq.prompt_len)
+        if packet.kv.shape[0] != nb:
+            self.blocks.free(seq)
+            raise ValueError(f"packet has {packet.kv.shape[0]} blocks, prompt needs {nb}")
+        import_blocks(self.pool.planes(), seq.block_table[:nb], packet.kv)
+        seq.num_computed = seq.prompt_len
+        self.seqs[seq.request_id] = seq
+        self.stats["prompt_tokens"] += seq.prompt_len
+        if len(seq.output_ids) >= seq.sampling.max_tokens:
+            seq.status = SeqStatus.RUNNING
+            self.scheduler.running.append(seq)
+            self.scheduler.finish(seq, "length")
+            self._complete(seq)
+            return seq
+        seq.status = SeqStatus.RUNNING
+        self.scheduler.running.append(seq)
         return seq
 
     def abort(self, request_id: str) -> None:
@@ -160,6 +200,11 @@ class LLMEngine:
         elif len(seq) >= self.max_model_len:
             reason = "length"
         if reason:
+            if getattr(seq, "export_kv", False):
+                from src.parallel.kv_transfer import export_blocks
+
+                nb = self.blocks.blocks_needed(seq.prompt_len)
+                seq.kv_export = export_blocks(self.pool.planes(), seq.block_table[:nb])  # type: ignore[attr-defined]
             self.scheduler.finish(seq, reason)
             finished.append(seq)
             self._complete(seq)

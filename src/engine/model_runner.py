@@ -173,6 +173,12 @@ class ModelRunner:
         return ids[:n].tolist()
 
     # ------------------------------------------------------------ prefill
+    KIND_STOP, KIND_PREFILL, KIND_DECODE = 0, 1, 2
+
+    def _sync_step(self, kind: int, a: int = 0, b: int = 0, c: int = 0, d: int = 0) -> None:
+        """Hook for tensor parallelism: rank 0 publishes the step to followers
+        (see :class:`src.parallel.tp_runner.TPModelRunner`). No-op at TP=1."""
+
     @torch.inference_mode()
     def prefill(self, chunks: List[PrefillChunk]) -> List[Optional[int]]:
         """Run one ragged prefill batch; returns the sampled token for every
@@ -185,29 +191,33 @@ class ModelRunner:
                                          self.h_pos.data_ptr(), self.h_slots.data_ptr(), self.h_cu.data_ptr(),
                                          self.h_ctx.data_ptr(), self.h_bt.data_ptr(), self.bt_width,
                                          self.h_last.data_ptr())
-        self._h2d(t, n, with_cu=True)
-        meta = AttnMetadata(is_prefill=True, slot_mapping=self.d_slots[:t], block_tables=self.d_bt[:n],
-                            ctx_lens=self.d_ctx[:n], cu_q=self.d_cu[: n + 1],
-                            max_q_len=max(c.length for c in chunks))
-        hidden = self.model.forward(self.d_ids[:t], self.d_pos[:t], meta, self.pool.tensor)
         done = [i for i, c in enumerate(chunks) if c.completes_prompt]
-        if not done:
-            if self.is_cuda:
-                torch.cuda.current_stream(self.device).synchronize()
-            return [None] * n
-        sel = [c.seq for c in chunks if c.completes_prompt]
-        greedy = self._fill_sampling(sel, len(sel))
-        if len(done) == n:
-            last = self.d_last[:n]
-        else:
-            last = self.d_last[torch.tensor(done, device=self.device)]
-        logits = self.model.compute_logits(hidden.index_select(0, last))
-        ids = self._sample(logits, len(sel), greedy, self.d_out)
-        vals = self._to_host(ids, len(sel))
+        nd = len(done)
+        if nd and nd != n:
+            nl = self.h_last.numpy()
+            nl[:nd] = nl[done]
+        greedy = self._fill_sampling([chunks[i].seq for i in done], nd) if nd else True
+        self._h2d(t, n, with_cu=True)
+        max_q = max(c.length for c in chunks)
+        self._sync_step(self.KIND_PREFILL, t, n, max_q, nd)
+        ids = self._exec_prefill(t, n, max_q, nd, greedy)
         res: List[Optional[int]] = [None] * n
-        for j, i in enumerate(done):
-            res[i] = vals[j]
+        if nd:
+            vals = self._to_host(ids, nd)
+            for j, i in enumerate(done):
+                res[i] = vals[j]
+        elif self.is_cuda:
+            torch.cuda.current_stream(self.device).synchronize()
         return res
+
+    def _exec_prefill(self, t: int, n: int, max_q: int, nd: int, greedy: bool) -> Optional[torch.Tensor]:
+        meta = AttnMetadata(is_prefill=True, slot_mapping=self.d_slots[:t], block_tables=self.d_bt[:n],
+                            ctx_lens=self.d_ctx[:n], cu_q=self.d_cu[: n + 1], max_q_len=max_q)
+        hidden = self.model.forward(self.d_ids[:t], self.d_pos[:t], meta, self.pool.tensor)
+        if not nd:
+            return None
+        logits = self.model.compute_logits(hidden.index_select(0, self.d_last[:nd]))
+        return self._sample(logits, nd, greedy, self.d_out)
 
     # ------------------------------------------------------------- decode
     def _decode_forward(self, n: int) -> torch.Tensor:
@@ -216,6 +226,9 @@ class ModelRunner:
                             part_ml=self.part_ml)
         hidden = self.model.forward(self.d_ids[:n], self.d_pos[:n], meta, self.pool.tensor)
         logits = self.model.compute_logits(hidden)
+        if not self.is_cuda:
+            return ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
+                              self.d_step[:n])
         return ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
                           self.d_step[:n], out=self.d_out[:n])
 
@@ -240,13 +253,17 @@ class ModelRunner:
         self.graph_sizes = sizes
         logger.info("captured decode hipGraphs for batch sizes %s", sizes)
 
+    def _pad_for(self, n: int) -> int:
+        if self.graphs:
+            k = bisect.bisect_left(self.graph_sizes, n)
+            if k < len(self.graph_sizes):
+                return self.graph_sizes[k]
+        return n
+
     @torch.inference_mode()
     def decode(self, seqs: List[Sequence]) -> List[int]:
         n = len(seqs)
-        pad = n
-        if self.graphs:
-            k = bisect.bisect_left(self.graph_sizes, n)
-            pad = self.graph_sizes[k] if k < len(self.graph_sizes) else n
+        pad = self._pad_for(n)
         self.n_ids[:n] = [s.last_token for s in seqs]
         self.n_ids[n:pad] = 0
         self.rt.build_decode_inputs([s.block_table for s in seqs], [len(s) for s in seqs], self.bs,
@@ -254,18 +271,13 @@ class ModelRunner:
                                     self.h_bt.data_ptr(), self.bt_width, pad)
         self._fill_sampling(seqs, pad)
         self._h2d(pad, pad, with_cu=False)
+        self._sync_step(self.KIND_DECODE, n, pad)
+        ids = self._exec_decode(n, pad)
+        return self._to_host(ids, n)
+
+    def _exec_decode(self, n: int, pad: int) -> torch.Tensor:
         g = self.graphs.get(pad)
         if g is not None:
             g.replay()
-            ids = self.d_out
-        else:
-            ids = self._decode_forward(n) if self.is_cuda else self._decode_cpu(n)
-        return self._to_host(ids, n)
-
-    def _decode_cpu(self, n: int) -> torch.Tensor:
-        meta = AttnMetadata(is_prefill=False, slot_mapping=self.d_slots[:n], block_tables=self.d_bt[:n],
-                            ctx_lens=self.d_ctx[:n], max_ctx=self.max_model_len)
-        hidden = self.model.forward(self.d_ids[:n], self.d_pos[:n], meta, self.pool.tensor)
-        logits = self.model.compute_logits(hidden)
-        return ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
-                          self.d_step[:n])
+            return self.d_out
+        return self._decode_forward(n)

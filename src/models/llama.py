@@ -60,7 +60,12 @@ class CausalLM:
     """A TP-sharded decoder-only LM (no nn.Module overhead on the hot path)."""
 
     def __init__(self, arch: ArchConfig, device, dtype=torch.bfloat16, tp: Optional[TPContext] = None,
-                 seed: int = 0, init_std: float = 0.02, max_position: Optional[int] = None):
+                 seed: int = 0, init_std: float = 0.02, max_position: Optional[int] = None,
+                 full_init: bool = False):
+        """``full_init=True`` draws every weight at full (unsharded) size from a
+        rank-independent generator and slices this rank's shard — identical to
+        the TP=1 model, used by the TP equivalence tests. The default draws
+        only the local shard (never materialises a 70B tensor)."""
         self.arch = arch
         self.device = torch.device(device)
         self.dtype = dtype
@@ -74,6 +79,7 @@ class CausalLM:
         self.head_dim = a.head_dim
         self.scale = 1.0 / math.sqrt(a.head_dim)
         self.max_position = max_position or a.max_position
+        self.full_init = full_init
         self.layers: List[LayerWeights] = []
         self._init_random(seed, init_std)
         self.cos_sin = rope_cos_sin(self.max_position, a.head_dim, a.rope_theta, self.device, a.rope_scaling)
@@ -84,31 +90,71 @@ class CausalLM:
         t.normal_(0.0, std, generator=gen)
         return t
 
+    # TP slicing of full-size tensors (Megatron layout, see src/parallel/tp.py)
+    def shard_qkv(self, full: torch.Tensor) -> torch.Tensor:
+        a, r, d = self.arch, self.tp.rank, self.head_dim
+        hq, hkv = self.hq, self.hkv
+        kv_idx = (r * hkv) if a.num_kv_heads >= self.tp.world_size else r // (self.tp.world_size // a.num_kv_heads)
+        q = full[r * hq * d:(r + 1) * hq * d]
+        k0 = a.num_heads * d + kv_idx * d
+        v0 = (a.num_heads + a.num_kv_heads) * d + kv_idx * d
+        return torch.cat([q, full[k0:k0 + hkv * d], full[v0:v0 + hkv * d]], 0)
+
+    def shard_cols(self, full: torch.Tensor, n_local: int) -> torch.Tensor:
+        r = self.tp.rank
+        return full[..., r * n_local:(r + 1) * n_local]
+
+    def shard_gate_up(self, full: torch.Tensor) -> torch.Tensor:
+        r, i = self.tp.rank, self.inter
+        big = self.arch.intermediate_size
+        g = full[..., r * i:(r + 1) * i, :]
+        u = full[..., big + r * i:big + (r + 1) * i, :]
+        return torch.cat([g, u], -2)
+
+    def shard_rows(self, full: torch.Tensor, n_local: int) -> torch.Tensor:
+        r = self.tp.rank
+        return full[r * n_local:(r + 1) * n_local]
+
+    def _param(self, local_shape, full_shape, shard, std, gen_local, gen_full):
+        if self.full_init and self.tp.enabled:
+            return shard(self._randn(*full_shape, std=std, gen=gen_full)).contiguous()
+        return self._randn(*local_shape, std=std, gen=gen_full if not self.tp.enabled else gen_local)
+
     def _init_random(self, seed: int, std: float) -> None:
         a = self.arch
         gen = torch.Generator(device=self.device)
         gen.manual_seed(seed * 7919 + self.tp.rank)
-        h, d = a.hidden_size, a.head_dim
+        genf = torch.Generator(device=self.device)   # rank-independent stream
+        genf.manual_seed(seed * 7919 + 104729)
+        h, d, L = a.hidden_size, a.head_dim, a.num_layers
+        ostd = std / math.sqrt(2 * L)
         # Embedding replicated on every rank: identical across ranks.
         gen_e = torch.Generator(device=self.device)
         gen_e.manual_seed(seed)
         self.embed = self._randn(a.vocab_size, h, std=1.0, gen=gen_e)
-        for _ in range(a.num_layers):
+        nq, nkv, big = a.num_heads, a.num_kv_heads, a.intermediate_size
+        for _ in range(L):
             lw = LayerWeights()
             lw.ln1 = torch.ones(h, dtype=self.dtype, device=self.device)
             lw.ln2 = torch.ones(h, dtype=self.dtype, device=self.device)
-            lw.qkv = self._randn((self.hq + 2 * self.hkv) * d, h, std=std, gen=gen)
-            lw.o = self._randn(h, self.hq * d, std=std / math.sqrt(2 * a.num_layers), gen=gen)
+            lw.qkv = self._param(((self.hq + 2 * self.hkv) * d, h), ((nq + 2 * nkv) * d, h), self.shard_qkv,
+                                 std, gen, genf)
+            lw.o = self._param((h, self.hq * d), (h, nq * d), lambda t: self.shard_cols(t, self.hq * d), ostd,
+                               gen, genf)
             if a.is_moe:
                 lw.router = self._randn(a.num_experts, h, std=std, gen=gen_e)  # replicated router
-                lw.w13 = self._randn(a.num_experts, 2 * self.inter, h, std=std, gen=gen)
-                lw.w2 = self._randn(a.num_experts, h, self.inter, std=std / math.sqrt(2 * a.num_layers), gen=gen)
+                lw.w13 = self._param((a.num_experts, 2 * self.inter, h), (a.num_experts, 2 * big, h),
+                                     self.shard_gate_up, std, gen, genf)
+                lw.w2 = self._param((a.num_experts, h, self.inter), (a.num_experts, h, big),
+                                    lambda t: self.shard_cols(t, self.inter), ostd, gen, genf)
             else:
-                lw.gate_up = self._randn(2 * self.inter, h, std=std, gen=gen)
-                lw.down = self._randn(h, self.inter, std=std / math.sqrt(2 * a.num_layers), gen=gen)
+                lw.gate_up = self._param((2 * self.inter, h), (2 * big, h), self.shard_gate_up, std, gen, genf)
+                lw.down = self._param((h, self.inter), (h, big), lambda t: self.shard_cols(t, self.inter), ostd,
+                                      gen, genf)
             self.layers.append(lw)
         self.norm = torch.ones(h, dtype=self.dtype, device=self.device)
-        self.lm_head = self._randn(self.vocab_local, h, std=std, gen=gen)
+        self.lm_head = self._param((self.vocab_local, h), (a.vocab_size, h),
+                                   lambda t: self.shard_rows(t, self.vocab_local), std, gen, genf)
 
     def load_state_dict(self, tensors: Dict[str, torch.Tensor]) -> int:
         """Load HF-named Llama/Mixtral weights (already TP-sliced by the caller

@@ -1,0 +1,114 @@
+"""
+KV-block transfer for disaggregated prefill → decode (BASELINE config 3).
+
+A prefill worker computes a prompt's KV into its paged pool, packs the
+sequence's blocks (every layer, K and V) into one contiguous staging tensor
+with the ``move_blocks`` HIP kernel, and ships it to the decode worker's GPU:
+
+* same process, other GPU  → ``tensor.to(dst)`` = ``hipMemcpyPeerAsync`` over
+  xGMI (SDMA engines; compute keeps running);
+* other process, same node → RCCL point-to-point (``dist.send/recv``), which
+  also rides xGMI (:class:`RCCLChannel`);
+* anywhere else            → framed bytes over the control-plane TCP socket
+  (:func:`packet_to_wire` / :func:`packet_from_wire`), the CPU fallback.
+
+The decode worker allocates fresh blocks, scatters the staging tensor into
+them (``move_blocks`` again) and resumes the sequence as a running decode —
+no prompt recompute. For Llama-3-8B a 512-token prompt is 64 MiB of KV.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from src import ops
+
+
+@dataclass
+class KVPacket:
+    request_id: str
+    prompt_ids: List[int]
+    first_token: int
+    kv: torch.Tensor                 # [n_blocks, planes, slab] (bf16)
+    block_size: int
+    sampling: Dict[str, Any] = field(default_factory=dict)
+    ttft_ms: Optional[float] = None
+
+    @property
+    def nbytes(self) -> int:
+        return self.kv.numel() * self.kv.element_size()
+
+
+def export_blocks(pool_planes: torch.Tensor, block_ids: List[int]) -> torch.Tensor:
+    """Gather ``block_ids`` of every (layer, K/V) plane into a staging tensor."""
+    ids = torch.tensor(block_ids, dtype=torch.int64, device=pool_planes.device)
+    return ops.gather_blocks(pool_planes, ids)
+
+
+def import_blocks(pool_planes: torch.Tensor, block_ids: List[int], buf: torch.Tensor) -> None:
+    ids = torch.tensor(block_ids, dtype=torch.int64, device=pool_planes.device)
+    if buf.device != pool_planes.device:
+        buf = buf.to(pool_planes.device, non_blocking=True)
+    ops.scatter_blocks(pool_planes, ids, buf.contiguous())
+
+
+def ship(buf: torch.Tensor, device) -> torch.Tensor:
+    """Peer copy to another GPU (hipMemcpyPeerAsync over xGMI) or a no-op."""
+    device = torch.device(device)
+    if buf.device == device:
+        return buf
+    out = buf.to(device, non_blocking=True)
+    if device.type == "cuda":
+        torch.cuda.current_stream(device).synchronize()
+    return out
+
+
+def packet_to_wire(p: KVPacket) -> Dict[str, Any]:
+    kv = p.kv.detach().to("cpu").contiguous()
+    raw = kv.view(torch.int16).numpy().tobytes()
+    return {"request_id": p.request_id, "prompt_ids": p.prompt_ids, "first_token": p.first_token,
+            "shape": list(kv.shape), "block_size": p.block_size, "sampling": p.sampling, "kv": raw,
+            "ttft_ms": p.ttft_ms}
+
+
+def packet_from_wire(d: Dict[str, Any], device="cpu") -> KVPacket:
+    arr = np.frombuffer(d["kv"], dtype=np.int16).reshape(d["shape"])
+    kv = torch.from_numpy(arr.copy()).view(torch.bfloat16).to(device)
+    return KVPacket(d["request_id"], list(d["prompt_ids"]), int(d["first_token"]), kv, int(d["block_size"]),
+                    dict(d.get("sampling") or {}), d.get("ttft_ms"))
+
+
+class RCCLChannel:
+    """Point-to-point KV shipping between two ranks of one process group
+    (RCCL over xGMI on MI355X; gloo on CPU). A small int64 header carries the
+    packet metadata, then the staging tensor follows."""
+
+    HDR = 8
+
+    def __init__(self, peer: int, device, group=None):
+        self.peer = peer
+        self.device = torch.device(device)
+        self.group = group
+
+    def send(self, p: KVPacket) -> None:
+        n_ids = len(p.prompt_ids)
+        hdr = torch.tensor([n_ids, p.first_token, p.block_size, *p.kv.shape, 0, 0][: self.HDR],
+                           dtype=torch.int64, device=self.device)
+        dist.send(hdr, self.peer, group=self.group)
+        dist.send(torch.tensor(p.prompt_ids, dtype=torch.int64, device=self.device), self.peer, group=self.group)
+        dist.send(p.kv.contiguous(), self.peer, group=self.group)
+
+    def recv(self, request_id: str = "") -> KVPacket:
+        hdr = torch.empty(self.HDR, dtype=torch.int64, device=self.device)
+        dist.recv(hdr, self.peer, group=self.group)
+        n_ids, first, bs, nb, planes, slab = (int(x) for x in hdr.tolist()[:6])
+        ids = torch.empty(n_ids, dtype=torch.int64, device=self.device)
+        dist.recv(ids, self.peer, group=self.group)
+        kv = torch.empty(nb, planes, slab, dtype=torch.bfloat16, device=self.device)
+        dist.recv(kv, self.peer, group=self.group)
+        return KVPacket(request_id, ids.tolist(), first, kv, bs)

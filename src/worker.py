@@ -202,7 +202,8 @@ class Worker:
         if op == "health":
             self._probe_count += 1
             return {"success": True, "worker_id": self.worker_id, "load": self.load(),
-                    "models": list(self.models)}
+                    "models": list(self.models),
+                    "archs": {n: getattr(getattr(m, "config", None), "arch", "mock") for n, m in self.models.items()}}
         if op == "metrics":
             return {"success": True, "metrics": self.get_metrics()}
         if op == "load_model":
@@ -355,6 +356,10 @@ def build_arg_parser():
     p.add_argument("--mock-latency-ms", type=float, default=None,
                    help="FakeModel latency; default = reference 50-150 ms")
     p.add_argument("--no-graph", action="store_true", help="disable hipGraph decode capture")
+    p.add_argument("--decode-worker", default=None,
+                   help="(role=prefill) host:port of the decode worker that receives the prompt KV")
+    p.add_argument("--device", default=None, help="torch device for LLM backends (default cuda:0 / cpu)")
+    p.add_argument("--num-kv-blocks", type=int, default=None)
     p.add_argument("--coordinator", default=None, help="host:port to register with")
     p.add_argument("--port-file", default=None, help="write the bound port here once listening")
     return p
@@ -366,11 +371,15 @@ async def main(argv=None) -> None:
     overrides: Dict[str, Any] = {}
     if args.mock_latency_ms is not None:
         overrides["latency_s"] = args.mock_latency_ms / 1000.0
+    if args.decode_worker:
+        overrides["decode_worker"] = args.decode_worker
+    if args.device:
+        overrides["device"] = args.device
     cfg = ModelConfig(
         model_name=args.model, model_path=args.model_path, batch_size=min(8, args.max_batch_size),
         max_batch_size=args.max_batch_size, arch=args.arch, preset=args.preset, tp_size=args.tp_size,
         role=args.role, max_model_len=args.max_model_len, max_latency_ms=args.max_latency_ms,
-        use_cuda_graph=not args.no_graph, overrides=overrides,
+        use_cuda_graph=not args.no_graph, num_kv_blocks=args.num_kv_blocks, overrides=overrides,
     )
     worker = Worker(worker_id=args.worker_id or f"worker-{os.getpid()}", host=args.host, port=args.port,
                     coordinator=args.coordinator,

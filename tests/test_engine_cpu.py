@@ -20,8 +20,10 @@ def make_engine(**kw):
     cfg = EngineConfig(max_num_seqs=kw.pop("max_num_seqs", 4), max_num_batched_tokens=kw.pop("budget", 64),
                        num_kv_blocks=kw.pop("blocks", 64), max_latency_ms=0.0, block_size=16,
                        enable_prefix_caching=kw.pop("prefix", True))
-    return LLMEngine.from_preset(kw.pop("preset", "llama-tiny"), device="cpu", cfg=cfg, max_model_len=256,
-                                 capture=False, dtype=torch.float32, **kw)
+    eng = LLMEngine.from_preset(kw.pop("preset", "llama-tiny"), device="cpu", cfg=cfg, max_model_len=256,
+                                capture=False, dtype=torch.float32, **kw)
+    eng.eos_token_id = None   # random weights may emit any id; lengths are asserted
+    return eng
 
 
 def prompts(n, seed=0):

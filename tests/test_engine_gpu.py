@@ -22,7 +22,9 @@ def engine():
     assert ops.native_available()
     cfg = EngineConfig(max_num_seqs=8, max_num_batched_tokens=512, num_kv_blocks=512, max_latency_ms=0.0,
                        graph_batch_sizes=[1, 2, 4, 8])
-    return LLMEngine.from_preset("llama-mini", device="cuda:0", cfg=cfg, max_model_len=1024)
+    eng = LLMEngine.from_preset("llama-mini", device="cuda:0", cfg=cfg, max_model_len=1024)
+    eng.eos_token_id = None
+    return eng
 
 
 @torch.inference_mode()

@@ -1,0 +1,72 @@
+"""The LLM serving path end to end on CPU (tiny Llama, reference ops):
+client → coordinator (cache, router, batcher 'stream' dispatch) → worker →
+LLMBackend → AsyncLLMEngine; and prefill-worker → decode-worker KV shipping
+over the RPC socket (op kv_import)."""
+
+import asyncio
+
+from src.client import InferenceClient
+from src.config import ModelConfig
+from src.coordinator import Coordinator
+from src.worker import Worker
+
+
+def llm_cfg(name="tiny", **kw):
+    return ModelConfig(model_name=name, model_path="", arch="llama", preset="llama-tiny", max_batch_size=4,
+                       max_model_len=256, max_num_batched_tokens=128, num_kv_blocks=128, use_cuda_graph=False,
+                       max_latency_ms=1.0, overrides=dict({"device": "cpu"}, **kw.pop("overrides", {})), **kw)
+
+
+def test_llm_through_coordinator():
+    async def main():
+        w = Worker("llm0", host="127.0.0.1", install_signal_handlers=False)
+        assert w.load_model(llm_cfg())
+        wport = await w.start()
+        coord = Coordinator(port=0, max_batch_size=4, max_latency_ms=2)
+        cport = await coord.start()
+        await coord.add_static_worker(f"127.0.0.1:{wport}")
+        assert coord._model_arch["tiny"] == "llama"
+        c = InferenceClient(f"127.0.0.1:{cport}")
+        reqs = [{"prompt": f"hello {i}", "max_tokens": 5, "ignore_eos": True} for i in range(6)]
+        rs = await asyncio.wait_for(asyncio.gather(*(c.infer("tiny", r) for r in reqs)), 120)
+        assert all(r["success"] for r in rs), rs
+        for r in rs:
+            o = r["outputs"]
+            assert o["num_output_tokens"] == 5 and len(o["token_ids"]) == 5
+            assert o["ttft_ms"] <= o["latency_ms"]
+        # greedy requests are cacheable
+        again = await c.infer("tiny", reqs[0])
+        assert again.get("cached") and again["outputs"]["token_ids"] == rs[0]["outputs"]["token_ids"]
+        m = await c.call({"op": "stats"})
+        assert m["success"]
+        c.close()
+        await coord.stop()
+        await w.shutdown()
+    asyncio.run(main())
+
+
+def test_disaggregated_workers_over_rpc():
+    async def main():
+        dec = Worker("dec", host="127.0.0.1", install_signal_handlers=False)
+        assert dec.load_model(llm_cfg(role="decode"))
+        dport = await dec.start()
+        pre = Worker("pre", host="127.0.0.1", install_signal_handlers=False)
+        assert pre.load_model(llm_cfg(role="prefill", overrides={"decode_worker": f"127.0.0.1:{dport}"}))
+        pport = await pre.start()
+        solo = Worker("solo", host="127.0.0.1", install_signal_handlers=False)
+        assert solo.load_model(llm_cfg())
+        sport = await solo.start()
+        cp, cs = InferenceClient(f"127.0.0.1:{pport}"), InferenceClient(f"127.0.0.1:{sport}")
+        req = {"prompt_token_ids": list(range(3, 40)), "max_tokens": 6, "ignore_eos": True}
+        a = await asyncio.wait_for(cp.call({"model": "tiny", "inputs": req}), 120)
+        b = await asyncio.wait_for(cs.call({"model": "tiny", "inputs": req}), 120)
+        assert a["success"] and b["success"], (a, b)
+        assert a["outputs"]["disaggregated"]
+        assert a["outputs"]["token_ids"] == b["outputs"]["token_ids"]
+        dm = (await InferenceClient(f"127.0.0.1:{dport}").call({"op": "engine_stats", "model": "tiny"}))
+        assert dm["stats"]["prompt_tokens"] == 37          # decode worker imported, never prefilled
+        for x in (cp, cs):
+            x.close()
+        for w in (pre, dec, solo):
+            await w.shutdown()
+    asyncio.run(main())
