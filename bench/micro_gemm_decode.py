@@ -1,0 +1,84 @@
+"""Microbenchmark: decode-shaped GEMMs (M = batch <= 32) — hipBLASLt (F.linear)
+vs the hand-written weight-streaming kernel in every (mode, wr, sk) config.
+
+Cold-cache protocol: the kernel cycles through enough distinct weight copies
+(>= 1.5 GiB) that nothing is served from the 256 MiB Infinity Cache, as in the
+real decode step where each layer's weights are read once. Prints one JSON
+line per (shape, variant) with time per call and effective HBM GB/s."""
+
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from src import ops  # noqa: E402
+
+SHAPES = {  # name: (N_out, K, silu)
+    "qkv_8b": (6144, 4096, False),
+    "o_8b": (4096, 4096, False),
+    "gate_up_8b": (14336, 4096, True),
+    "down_8b": (4096, 14336, False),
+    "lm_head_8b": (128256, 4096, False),
+    "qkv_70b_tp8": (1280, 8192, False),
+    "o_70b_tp8": (8192, 1024, False),
+    "gate_up_70b_tp8": (3584, 8192, True),
+    "down_70b_tp8": (8192, 3584, False),
+}
+
+
+def timeit(fn, ws, iters=None):
+    n = len(ws)
+    iters = iters or max(n, 8)
+    for i in range(3):
+        fn(ws[i % n])
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for i in range(iters):
+            fn(ws[i % n])
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = 1e9
+    for _ in range(3):
+        s.record()
+        g.replay()
+        e.record()
+        torch.cuda.synchronize()
+        best = min(best, s.elapsed_time(e) * 1e3 / iters)
+    return best
+
+
+def main():
+    m = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+    dev = torch.device("cuda:0")
+    for name, (n, k, silu) in SHAPES.items():
+        wrows = 2 * n if silu else n
+        x = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
+        wbytes = wrows * k * 2
+        copies = max(2, int(1.5 * 2**30 // wbytes) + 1)
+        ws = [torch.randn(wrows, k, device=dev, dtype=torch.bfloat16) / 64 for _ in range(copies)]
+        res = []
+        if silu:
+            res.append(("hipblaslt+silu", timeit(lambda w: ops.silu_and_mul(torch.nn.functional.linear(x, w)), ws)))
+        else:
+            res.append(("hipblaslt", timeit(lambda w: torch.nn.functional.linear(x, w), ws)))
+        for wr in (32, 64):
+            if silu:
+                if n % (wr // 2) == 0:
+                    res.append((f"gd_silu_wr{wr}", timeit(lambda w: ops.gemm_decode(x, w, 1, wr, 1), ws)))
+                continue
+            if n % wr == 0:
+                res.append((f"gd_bf16_wr{wr}", timeit(lambda w: ops.gemm_decode(x, w, 0, wr, 1), ws)))
+            for sk in (2, 4, 8):
+                if k % (256 * sk) == 0 and n % wr == 0:
+                    res.append((f"gd_slab_wr{wr}_sk{sk}", timeit(lambda w: ops.gemm_decode(x, w, 2, wr, sk), ws)))
+        for v, us in res:
+            print(json.dumps({"shape": name, "M": m, "N": n, "K": k, "variant": v, "us": round(us, 2),
+                              "GBps": round(wbytes / us / 1e3, 1)}), flush=True)
+        del ws
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -272,6 +272,81 @@ void moe_grouped_gemm(Tensor y, Tensor x, Tensor w, Tensor offsets) {
                                        (int)N, (int)K, cur_stream()));
 }
 
+// Decode GEMM (M <= 32): x[M, K] @ w^T.
+//   mode 0: y bf16 [M, N], w [N, K]
+//   mode 1: y bf16 [M, N] = silu(x gate^T) * (x up^T), w = [gate; up] [2N, K]
+//   mode 2: y fp32 split-K slabs [sk, M, N], w [N, K]
+void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t sk) {
+  DIE_CHECK_CUDA(x);
+  DIE_CHECK_BF16(x);
+  DIE_CHECK_BF16(w);
+  DIE_CHECK_CONTIG(w);
+  check_rows(x, "x");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(M >= 1 && M <= 32, "gemm_decode: 1 <= M <= 32");
+  TORCH_CHECK(wr == 32 || wr == 64, "wr must be 32 or 64");
+  TORCH_CHECK(K % (256 * sk) == 0, "gemm_decode: K must be a multiple of 256*sk");
+  int64_t N, ldy;
+  if (mode == 2) {
+    DIE_CHECK_DTYPE(y, at::kFloat);
+    DIE_CHECK_CONTIG(y);
+    TORCH_CHECK(y.dim() == 3 && y.size(0) == sk && y.size(1) == M, "slab y must be [sk, M, N]");
+    N = y.size(2);
+    ldy = N;
+  } else {
+    DIE_CHECK_BF16(y);
+    check_rows(y, "y");
+    TORCH_CHECK(sk == 1 && y.size(0) == M, "bf16 output: sk == 1, y [M, N]");
+    N = y.size(1);
+    ldy = y.stride(0);
+  }
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K && w.size(0) == (mode == 1 ? 2 * N : N), "gemm_decode w shape");
+  TORCH_CHECK(N % (mode == 1 ? wr / 2 : wr) == 0, "N not a multiple of the column tile");
+  DIE_HIP(die::launch_gemm_decode(y.data_ptr(), ldy, bf(x), x.stride(0), bf(w), (int)M, (int)N, (int)K, (int)mode,
+                                  (int)wr, (int)sk, cur_stream()));
+}
+
+void fused_add_rms_norm_slab(Tensor out, Tensor slab, Tensor residual, Tensor w, double eps) {
+  DIE_CHECK_CUDA(slab);
+  DIE_CHECK_DTYPE(slab, at::kFloat);
+  DIE_CHECK_CONTIG(slab);
+  DIE_CHECK_BF16(out);
+  DIE_CHECK_BF16(residual);
+  DIE_CHECK_CONTIG(residual);
+  check_rows(out, "out");
+  TORCH_CHECK(slab.dim() == 3 && slab.size(1) == residual.size(0) && slab.size(2) == residual.size(1),
+              "slab [sk, rows, hidden] must match residual");
+  TORCH_CHECK(out.size(0) == residual.size(0) && out.size(1) == residual.size(1) && w.numel() == residual.size(1),
+              "shapes");
+  TORCH_CHECK(residual.size(1) <= 8 * 256 * 8 && residual.size(1) % 8 == 0, "hidden");
+  DIE_HIP(die::launch_fused_add_rms_norm_slab(bf(out), slab.data_ptr<float>(), (int)slab.size(0), bf(residual), bf(w),
+                                              (float)eps, (int)residual.size(0), (int)residual.size(1),
+                                              out.stride(0), cur_stream()));
+}
+
+void rope_and_cache_slab(Tensor q_out, Tensor slab, Tensor positions, Tensor cos_sin, Tensor slot_mapping,
+                         Tensor k_cache, Tensor v_cache, int64_t hq, int64_t hkv, int64_t head_dim) {
+  DIE_CHECK_CUDA(slab);
+  DIE_CHECK_DTYPE(slab, at::kFloat);
+  DIE_CHECK_CONTIG(slab);
+  DIE_CHECK_BF16(q_out);
+  DIE_CHECK_CONTIG(q_out);
+  const int64_t T = slab.size(1);
+  TORCH_CHECK(slab.dim() == 3 && slab.size(2) == (hq + 2 * hkv) * head_dim, "slab [sk, T, (hq+2hkv)*D]");
+  TORCH_CHECK(q_out.numel() >= T * hq * head_dim, "q_out too small");
+  DIE_CHECK_DTYPE(positions, at::kLong);
+  DIE_CHECK_DTYPE(slot_mapping, at::kLong);
+  DIE_CHECK_DTYPE(cos_sin, at::kFloat);
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == head_dim, "cos_sin must be [max_pos, head_dim]");
+  TORCH_CHECK(positions.numel() >= T && slot_mapping.numel() >= T, "positions/slots too short");
+  check_cache(k_cache, hkv, head_dim, "k_cache");
+  check_cache(v_cache, hkv, head_dim, "v_cache");
+  DIE_HIP(die::launch_rope_and_cache_slab(bf(q_out), slab.data_ptr<float>(), (int)slab.size(0),
+                                          positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
+                                          slot_mapping.data_ptr<int64_t>(), bf(k_cache), bf(v_cache), (int)T,
+                                          (int)hq, (int)hkv, (int)head_dim, (int)k_cache.size(2), cur_stream()));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -293,4 +368,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_gather", &moe_gather);
   m.def("moe_combine", &moe_combine);
   m.def("moe_grouped_gemm", &moe_grouped_gemm);
+  m.def("gemm_decode", &gemm_decode);
+  m.def("fused_add_rms_norm_slab", &fused_add_rms_norm_slab);
+  m.def("rope_and_cache_slab", &rope_and_cache_slab);
 }

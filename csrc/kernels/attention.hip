@@ -38,8 +38,6 @@ constexpr int K_TILE = KT * K_PITCH;      // 8704
 constexpr int V_TILE = KT * V_PITCH;      // 10240
 constexpr int KV_TILE = K_TILE + V_TILE;  // 18944
 constexpr float NEG_BIG = -1.0e30f;       // finite running-max sentinel
-constexpr int DECODE_WAVE_KEYS = 64;      // keys per wave in decode (2 tiles)
-constexpr int DECODE_BLOCK_KEYS = 4 * DECODE_WAVE_KEYS;
 
 typedef __attribute__((address_space(3))) short4_t lds_short4;
 
@@ -261,88 +259,185 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(bf16_t* __restrict
   }
 }
 
-// grid = (num_seqs, hkv, max_blocks_per_seq); block = 256; dynamic LDS = 4 * V_TILE.
-// Partial slot of a wave = blockIdx.z * 4 + wave; part_o [S][hq][maxp][D], part_ml [S][hq][maxp][2].
+// ---------------------------------------------------------------------------
+// Decode (flash-decoding). grid = (num_seqs, hkv, ceil(max_ctx / 128)); block = 256.
+// One workgroup owns 128 keys of one (sequence, kv head):
+//  1. every lane issues 16 LDS-DMA loads (global_load_lds_dwordx4: 8 for K, 8 for
+//     V) for the whole 128-key chunk up front — 64 KiB in flight per workgroup
+//     and no VGPRs spent on staging. The LDS images are lane-linear, so the
+//     bank-conflict swizzles are applied to the per-lane SOURCE address
+//     (cdna_hip_programming.md rule 21): K chunk c of row r lands at c^(r&15)
+//     (ds_read_b128 A-fragments conflict-free), V chunk c at c^((r&3)<<2)
+//     (ds_read_b64_tr_b16 V^T fragments conflict-free);
+//  2. wave w computes keys [32w, 32w+32) for the G query heads of the group;
+//  3. the 4 waves' (m, l, O) are merged through LDS and ONE partial per
+//     workgroup is written; attn_decode_reduce merges the partials.
+// Keys past the context are clamped to a valid row (never NaN garbage) and
+// masked to -inf in the softmax.
+constexpr int DEC_KEYS = 128;
+constexpr int DEC_ROW = 256;                       // bytes per K/V row (128 x bf16), unpadded
+constexpr int DEC_LDS = 2 * DEC_KEYS * DEC_ROW;    // 64 KiB
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void global_cvoid;
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((global_cvoid*)src, (lds_void*)lds_wave_base, 16, 0, 0);
+}
+
+// S^T tile from a swizzled K image (row r, logical chunk c at physical c ^ (r & 15)).
+__device__ __forceinline__ f32x16_t qk_lds_swz(const char* kimg, const bf16x8_t qf[8], int lane) {
+  f32x16_t s;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s[r] = 0.f;
+  const int row = lane & 31, h = lane >> 5;
+  const char* base = kimg + row * DEC_ROW;
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    const int pc = (2 * kk + h) ^ (row & 15);
+    const bf16x8_t a = as_frag(*reinterpret_cast<const uint4*>(base + 16 * pc));
+    s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[kk], s, 0, 0, 0);
+  }
+  return s;
+}
+
+// O^T += V^T * P^T from a swizzled V image (logical chunk c of row r at c ^ ((r&3)<<2)).
+__device__ __forceinline__ void pv_lds_swz(const char* vimg, const f32x16_t& p, State& st, int lane) {
+  bf16x8_t pf[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    uint4 w;
+    w.x = pack2(p[8 * s2 + 0], p[8 * s2 + 1]);
+    w.y = pack2(p[8 * s2 + 2], p[8 * s2 + 3]);
+    w.z = pack2(p[8 * s2 + 4], p[8 * s2 + 5]);
+    w.w = pack2(p[8 * s2 + 6], p[8 * s2 + 7]);
+    pf[s2] = as_frag(w);
+  }
+  const int g = lane >> 4, i = lane & 15, h = lane >> 5;
+  const int q4 = i >> 2, p4 = i & 3;
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    const int lch = 4 * db + 2 * (g & 1) + (p4 >> 1);
+    const int off = 16 * (lch ^ (q4 << 2)) + 8 * (p4 & 1);  // rows below are all == q4 (mod 4)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int r0 = 16 * s2 + 4 * h + q4;
+      const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(vimg + r0 * DEC_ROW + off));
+      const short4_t hi =
+          __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(vimg + (r0 + 8) * DEC_ROW + off));
+      typedef __attribute__((ext_vector_type(8))) short short8_t;
+      const short8_t a8 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      st.o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a8), pf[s2], st.o[db], 0,
+                                                         0, 0);
+    }
+  }
+}
+
 template <int G>
 __global__ void __launch_bounds__(256, 2) attn_decode_kernel(float* __restrict__ part_o, float* __restrict__ part_ml,
-                                                          const bf16_t* __restrict__ q, int64_t q_stride,
-                                                          const bf16_t* __restrict__ k_cache,
-                                                          const bf16_t* __restrict__ v_cache,
-                                                          const int* __restrict__ block_tables, int bt_stride,
-                                                          const int* __restrict__ ctx_lens, int hq, int hkv,
-                                                          int block_size, float scale_log2, int maxp) {
+                                                             const bf16_t* __restrict__ q, int64_t q_stride,
+                                                             const bf16_t* __restrict__ k_cache,
+                                                             const bf16_t* __restrict__ v_cache,
+                                                             const int* __restrict__ block_tables, int bt_stride,
+                                                             const int* __restrict__ ctx_lens, int num_seqs, int hq,
+                                                             int hkv, int block_size, float scale_log2, int maxp) {
+  // Persistent: the grid is sized for the hardware (2 workgroups per CU), not for
+  // max_model_len, and walks (part, kv head, seq) tasks up to the batch's actual
+  // longest context — no wave of empty workgroups under hipGraph replay.
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int seq = blockIdx.x, kvh = blockIdx.y;
-  const int ctx = ctx_lens[seq];
+  int& sh_parts = *reinterpret_cast<int*>(smem + DEC_LDS);  // keep all LDS dynamic (Guideline 17)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const int pidx = blockIdx.z * 4 + wave;
-  const int kbeg = pidx * DECODE_WAVE_KEYS;
-  if (kbeg >= ctx) return;  // no barrier below: per-wave exit is safe
+  if (wave == 0) {
+    int m = 0;
+    for (int s = lane; s < num_seqs; s += 64) m = max(m, (ctx_lens[s] + DEC_KEYS - 1) / DEC_KEYS);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+    if (lane == 0) sh_parts = min(m, maxp);
+  }
+  __syncthreads();
+  const int n_tasks = num_seqs * hkv * sh_parts;
+  char* kimg = smem;
+  char* vimg = smem + DEC_KEYS * DEC_ROW;
+#pragma unroll 1
+  for (int task = blockIdx.x; task < n_tasks; task += gridDim.x) {
+  const int part = task / (num_seqs * hkv);
+  const int rem = task - part * num_seqs * hkv;
+  const int seq = rem % num_seqs, kvh = rem / num_seqs;
+  const int ctx = ctx_lens[seq];
+  const int kbeg = part * DEC_KEYS;
+  if (kbeg >= ctx) continue;  // uniform over the workgroup
+  const int* bt = block_tables + (int64_t)seq * bt_stride;
+
+  // 1) LDS-DMA the 128-key chunk: instruction i of wave w fills rows 4(8w+i) .. +3.
+  {
+    const int pch = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = (wave * 8 + i) * 4 + (lane >> 4);
+      const int key = min(kbeg + row, ctx - 1);
+      const int64_t blk = bt[key / block_size];
+      const int64_t roff = ((blk * hkv + kvh) * block_size + key % block_size) * D;
+      const int kc = pch ^ (row & 15), vc = pch ^ ((row & 3) << 2);
+      glds16(k_cache + roff + kc * 8, kimg + (wave * 8 + i) * 1024);
+      glds16(v_cache + roff + vc * 8, vimg + (wave * 8 + i) * 1024);
+    }
+  }
   const int row = lane & 31;
   const bool row_valid = row < G;
   const int head = kvh * G + (row_valid ? row : 0);
-  const int* bt = block_tables + (int64_t)seq * bt_stride;
-  char* vl = smem + wave * V_TILE;
-
   bf16x8_t qf[8];
   load_q(qf, row_valid ? q + (int64_t)seq * q_stride + (int64_t)head * D : nullptr, h);
   State st;
   init_state(st);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
-#pragma unroll 1
-  for (int t = 0; t < DECODE_WAVE_KEYS / KT; ++t) {
-    const int kb = kbeg + t * KT;
-    if (kb >= ctx) break;
-    // K: this lane's key row straight into MFMA A fragments.
-    bf16x8_t kf[8];
-    {
-      const int key = kb + row;
-      if (key < ctx) {
-        const bf16_t* kp = kv_row(k_cache, bt, key, block_size, hkv, kvh) + 8 * h;
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) kf[kk] = as_frag(*reinterpret_cast<const uint4*>(kp + 16 * kk));
-      } else {
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) kf[kk] = zero_frag();
-      }
-    }
-    // V: tile into the wave-private LDS image (8 x 16 B per lane).
-    {
-      const int vr = lane >> 4, vc = lane & 15;
-      uint4 vv[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int key = kb + vr + 4 * i;
-        vv[i] = key < ctx ? *reinterpret_cast<const uint4*>(kv_row(v_cache, bt, key, block_size, hkv, kvh) + vc * 8)
-                          : make_uint4(0, 0, 0, 0);
-      }
-      // previous tile's transposed reads must have retired before overwriting
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int i = 0; i < 8; ++i) *reinterpret_cast<uint4*>(vl + (vr + 4 * i) * V_PITCH + vc * 16) = vv[i];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-    }
-    f32x16_t s = qk_regs(kf, qf);
+  // 2) this wave's 32 keys
+  const int kb = kbeg + 32 * wave;
+  if (kb < ctx) {
+    f32x16_t s = qk_lds_swz(kimg + 32 * wave * DEC_ROW, qf, lane);
     softmax_tile(s, st, kb, ctx, scale_log2, h);
-    pv_lds(vl, s, st, lane);
+    pv_lds_swz(vimg + 32 * wave * DEC_ROW, s, st, lane);
   }
+  __syncthreads();  // K/V images are dead: reuse LDS for the merge
 
+  // 3) merge the 4 waves: ml[w][row][2], o[w][row][128] (rows < G)
+  float* ml = reinterpret_cast<float*>(smem);
+  float* ob = ml + 4 * 32 * 2;
   if (row_valid) {
-    const int64_t slot = ((int64_t)seq * hq + head) * maxp + pidx;
     if (h == 0) {
-      part_ml[slot * 2 + 0] = st.m;
-      part_ml[slot * 2 + 1] = st.l;
+      ml[(wave * 32 + row) * 2 + 0] = st.m;
+      ml[(wave * 32 + row) * 2 + 1] = st.l;
     }
-    float* po = part_o + slot * D;
+    float* o = ob + (wave * G + row) * D;
 #pragma unroll
     for (int db = 0; db < 4; ++db)
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = 32 * db + 8 * g4 + 4 * h;
-        *reinterpret_cast<float4*>(po + d) =
+      for (int g4 = 0; g4 < 4; ++g4)
+        *reinterpret_cast<float4*>(o + 32 * db + 8 * g4 + 4 * h) =
             make_float4(st.o[db][4 * g4], st.o[db][4 * g4 + 1], st.o[db][4 * g4 + 2], st.o[db][4 * g4 + 3]);
-      }
+  }
+  __syncthreads();
+  for (int e = tid; e < G * D; e += 256) {
+    const int r = e / D, d = e % D;
+    float M = NEG_BIG;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, ml[(w * 32 + r) * 2]);
+    float L = 0.f, acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float f = exp2f(ml[(w * 32 + r) * 2] - M);
+      L += f * ml[(w * 32 + r) * 2 + 1];
+      acc += f * ob[(w * G + r) * D + d];
+    }
+    const int64_t slot = ((int64_t)seq * hq + kvh * G + r) * maxp + part;
+    part_o[slot * D + d] = acc;
+    if (d == 0) {
+      part_ml[slot * 2 + 0] = M;
+      part_ml[slot * 2 + 1] = L;
+    }
+  }
+  __syncthreads();  // merge buffers are read before the next task's DMA overwrites LDS
   }
 }
 
@@ -353,7 +448,7 @@ __global__ void __launch_bounds__(128) attn_decode_reduce_kernel(bf16_t* __restr
                                                                  const int* __restrict__ ctx_lens, int hq, int maxp) {
   const int seq = blockIdx.x, head = blockIdx.y, d = threadIdx.x;
   const int ctx = ctx_lens[seq];
-  const int np = (ctx + DECODE_WAVE_KEYS - 1) / DECODE_WAVE_KEYS;
+  const int np = (ctx + DEC_KEYS - 1) / DEC_KEYS;
   const int64_t base = ((int64_t)seq * hq + head) * maxp;
   float M = NEG_BIG;
   for (int i = 0; i < np; ++i) M = fmaxf(M, part_ml[(base + i) * 2]);
@@ -403,16 +498,15 @@ hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, const 
   if (num_seqs == 0) return hipSuccess;
   if (head_dim != D || hq % hkv) return hipErrorInvalidValue;
   const int G = hq / hkv;
-  if (G > 32) return hipErrorInvalidValue;
+  if (G > 32 || G * D * 4 * 4 + 4 * 32 * 2 * 4 > DEC_LDS) return hipErrorInvalidValue;
   const float sl2 = scale * 1.4426950408889634f;
-  const int nblk = (max_ctx + DECODE_BLOCK_KEYS - 1) / DECODE_BLOCK_KEYS;
-  const int maxp = nblk * 4;
-  dim3 grid(num_seqs, hkv, nblk), block(256);
-  const size_t lds = 4 * V_TILE;
+  const int maxp = (max_ctx + DEC_KEYS - 1) / DEC_KEYS;
+  const int tasks = num_seqs * hkv * maxp;
+  dim3 grid(tasks < 512 ? tasks : 512), block(256);
 #define DIE_DC(GG)                                                                                          \
   case GG:                                                                                                  \
-    hipLaunchKernelGGL(attn_decode_kernel<GG>, grid, block, lds, s, part_o, part_ml, q, q_stride, k_cache, \
-                       v_cache, block_tables, bt_stride, ctx_lens, hq, hkv, block_size, sl2, maxp);         \
+    hipLaunchKernelGGL(attn_decode_kernel<GG>, grid, block, DEC_LDS + 16, s, part_o, part_ml, q, q_stride,      \
+                       k_cache, v_cache, block_tables, bt_stride, ctx_lens, num_seqs, hq, hkv, block_size, sl2, maxp); \
     break;
   switch (G) {
     DIE_DC(1)
@@ -432,8 +526,6 @@ hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, const 
   return hipGetLastError();
 }
 
-int attn_decode_max_partials(int max_ctx) {
-  return ((max_ctx + DECODE_BLOCK_KEYS - 1) / DECODE_BLOCK_KEYS) * 4;
-}
+int attn_decode_max_partials(int max_ctx) { return (max_ctx + DEC_KEYS - 1) / DEC_KEYS; }
 
 }  // namespace die

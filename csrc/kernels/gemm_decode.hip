@@ -1,0 +1,208 @@
+// Weight-streaming GEMM for decode steps: Y[M, N] = X[M, K] · W[N, K]^T with
+// M <= 32 (one token per running sequence), bf16 in, fp32 accumulate.
+//
+// At M <= 32 a projection is a pure HBM stream of W (Llama-3-8B gate/up: 235 MB
+// per layer-step) — the arithmetic is free. What decides speed is how many
+// bytes each CU keeps in flight, whether every CU is busy, and how much of the
+// per-CU load path the (re-read) activations steal from the weight stream:
+//  * a workgroup owns WR weight rows (32 or 64) and a 1/SK slice of K
+//    (split-K), so even N = 4096 projections spread over >= 256 workgroups;
+//  * K is streamed in 256-wide chunks through a ring of S LDS slots filled by
+//    LDS-DMA (global_load_lds_dwordx4): S-1 chunks (64-96 KiB) in flight per
+//    CU while the 4 waves run MFMAs on the landed chunk. Counted
+//    `s_waitcnt vmcnt(N)` + raw s_barrier, never a drain-to-zero in the loop
+//    (cdna_hip_programming.md "Pipelining across barriers", T3/T4);
+//  * X (the 32 activation rows) rides the same ring; at WR = 64 it is a third
+//    of the DMA bytes (half at WR = 32);
+//  * the LDS images are lane-linear; bank conflicts are removed by XOR-ing the
+//    16-byte chunk index with the row on the SOURCE address and on the read
+//    (rule 21), so A/B fragments are conflict-free ds_read_b128;
+//  * v_mfma_f32_16x16x32_bf16, 2 m-tiles x (WR/16) n-tiles per k-step;
+//  * epilogues: bf16 store; SiLU(gate)*up for the fused gate/up projection
+//    (the silu_and_mul kernel disappears); or an fp32 split-K slab
+//    [SK][M][N] that the CONSUMER kernel (fused residual-add RMSNorm, RoPE)
+//    sums in its prologue — split-K without atomics or an extra launch.
+#include "common.h"
+#include "launchers.h"
+
+namespace die {
+namespace gd {
+
+constexpr int KC = 256;             // K elements per chunk
+constexpr int ROWB = KC * 2;        // bytes per image row (512)
+constexpr int MR = 32;              // activation rows (max M)
+constexpr int NTH = 256;            // threads per workgroup
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void global_cvoid;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f4;
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((global_cvoid*)src, (lds_void*)lds_wave_base, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+}  // namespace gd
+
+using namespace gd;
+
+// EPI 0: bf16 Y = XW^T. EPI 1: bf16 Y[:, j] = silu(g_j) * u_j, W = [gate(N_out rows); up(N_out rows)].
+// EPI 2: fp32 slab Y[blockIdx.y][m][n] (split-K partial).
+// WR = weight rows in the workgroup's image; output columns per workgroup = WR (EPI 0/2) or WR/2 (EPI 1).
+template <int WR, int EPI, int S>
+__global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv, int64_t ldy,
+                                                          const bf16_t* __restrict__ X, int64_t ldx,
+                                                          const bf16_t* __restrict__ W, int M, int N_out, int K) {
+  constexpr int NO = EPI == 1 ? WR / 2 : WR;   // output columns per workgroup
+  constexpr int SLOT = (WR + MR) * ROWB;       // bytes per ring slot
+  constexpr int INSTR = (WR + MR) / 2;         // 1-KiB DMA pieces per chunk (2 rows each)
+  constexpr int PER_WAVE = INSTR / 4;          // pieces issued per wave per chunk
+  constexpr int NTILE = WR / 16;               // 16-column MFMA tiles
+  static_assert(INSTR % 4 == 0, "pieces must split over 4 waves");
+  static_assert((S - 1) * PER_WAVE <= 63, "vmcnt field is 6 bits");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * NO;
+  const int kper = K / gridDim.y;
+  const int k0 = blockIdx.y * kper;
+  const int nch = kper / KC;
+
+  // Per-lane source rows for this wave's DMA pieces (fixed across chunks).
+  const bf16_t* src[PER_WAVE];
+#pragma unroll
+  for (int p = 0; p < PER_WAVE; ++p) {
+    const int piece = wave + 4 * p;
+    const int row = 2 * piece + (lane >> 5);  // image row: [0, WR) = W, [WR, WR+32) = X
+    const int lch = (lane & 31) ^ (row & 15);
+    const bf16_t* base;
+    if (row < WR) {
+      int grow = n0 + row;
+      if (EPI == 1 && row >= NO) grow = N_out + n0 + (row - NO);
+      base = W + (int64_t)grow * K;
+    } else {
+      base = X + (int64_t)min(row - WR, M - 1) * ldx;
+    }
+    src[p] = base + k0 + lch * 8;
+  }
+  auto issue = [&](int c) {
+    char* slot = smem + (c % S) * SLOT;
+#pragma unroll
+    for (int p = 0; p < PER_WAVE; ++p) glds16(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);
+  };
+
+  f4 acc[2][NTILE];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < NTILE; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int c = 0; c < S - 1; ++c)
+    if (c < nch) issue(c);
+
+  const int fr = lane & 15, kg = lane >> 4;
+#pragma unroll 1
+  for (int c = 0; c < nch; ++c) {
+    if (c + S - 1 < nch) issue(c + S - 1);
+    const int after = min(S - 1, nch - 1 - c);  // chunks issued after c
+    if (after >= 4) wait_vm<4 * PER_WAVE>();
+    else if (after == 3) wait_vm<3 * PER_WAVE>();
+    else if (after == 2) wait_vm<2 * PER_WAVE>();
+    else if (after == 1) wait_vm<PER_WAVE>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    const char* slot = smem + (c % S) * SLOT;
+    const char* ximg = slot + WR * ROWB;
+    // 8 k-steps of 32 per chunk, 2 per wave
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ks = wave * 2 + kk;
+      const int lch = 4 * ks + kg;
+      bf16x8 a[2], b[NTILE];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int r = 16 * mt + fr;
+        a[mt] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ximg + r * ROWB + 16 * (lch ^ (r & 15))));
+      }
+#pragma unroll
+      for (int nt = 0; nt < NTILE; ++nt) {
+        const int r = 16 * nt + fr;
+        b[nt] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(slot + r * ROWB + 16 * (lch ^ (r & 15))));
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NTILE; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // slot c%S is refilled next iteration
+  }
+
+  // Cross-wave reduction through LDS (the ring is idle now): red[wave][m][WR] fp32.
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NTILE; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * mt + 4 * kg + r, n = 16 * nt + fr;  // C: col = lane&15, row = (lane>>4)*4 + r
+        red[(wave * MR + m) * WR + n] = acc[mt][nt][r];
+      }
+  __syncthreads();
+  for (int e = tid; e < MR * NO; e += NTH) {
+    const int m = e / NO, j = e % NO;
+    if (m >= M) continue;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) v += red[(w * MR + m) * WR + j];
+    if (EPI == 1) {
+      float u = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) u += red[(w * MR + m) * WR + NO + j];
+      v = v / (1.f + __expf(-v)) * u;
+    }
+    if (EPI == 2)
+      reinterpret_cast<float*>(Yv)[((int64_t)blockIdx.y * M + m) * ldy + n0 + j] = v;
+    else
+      reinterpret_cast<bf16_t*>(Yv)[(int64_t)m * ldy + n0 + j] = f2bf(v);
+  }
+}
+
+template <int WR, int EPI, int S>
+static hipError_t launch_gd(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N_out,
+                            int K, int sk, hipStream_t s) {
+  constexpr int NO = EPI == 1 ? WR / 2 : WR;
+  if (N_out % NO || (K / sk) % KC || K % sk) return hipErrorInvalidValue;
+  const size_t lds = (size_t)S * (WR + MR) * ROWB;
+  hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S>), dim3(N_out / NO, sk), dim3(NTH), lds, s, Y, ldy, X, ldx, W,
+                     M, N_out, K);
+  return hipGetLastError();
+}
+
+// mode 0: bf16 Y [M, N]; mode 1: bf16 silu(gate)*up, W = [2N, K]; mode 2: fp32 slabs [sk, M, N].
+// wr: weight rows per workgroup (32 or 64).
+hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,
+                              int K, int mode, int wr, int sk, hipStream_t s) {
+  if (M <= 0) return hipSuccess;
+  if (M > MR || sk < 1 || (mode != 2 && sk != 1)) return hipErrorInvalidValue;
+  if (wr == 32) {
+    if (mode == 0) return launch_gd<32, 0, 4>(Y, ldy, X, ldx, W, M, N, K, sk, s);
+    if (mode == 1) return launch_gd<32, 1, 4>(Y, ldy, X, ldx, W, M, N, K, sk, s);
+    return launch_gd<32, 2, 4>(Y, ldy, X, ldx, W, M, N, K, sk, s);
+  }
+  if (wr == 64) {
+    if (mode == 0) return launch_gd<64, 0, 3>(Y, ldy, X, ldx, W, M, N, K, sk, s);
+    if (mode == 1) return launch_gd<64, 1, 3>(Y, ldy, X, ldx, W, M, N, K, sk, s);
+    return launch_gd<64, 2, 3>(Y, ldy, X, ldx, W, M, N, K, sk, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace die

@@ -47,4 +47,14 @@ hipError_t launch_moe_combine(bf16_t* out, const bf16_t* ys, const int* pos, con
 hipError_t launch_moe_grouped_gemm(bf16_t* Y, const bf16_t* X, const bf16_t* W, const int* offsets, int max_rows,
                                    int E, int N, int K, hipStream_t s);
 
+hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,
+                              int K, int mode, int wr, int sk, hipStream_t s);
+// consumers of fp32 split-K slabs [sk][rows][width]
+hipError_t launch_fused_add_rms_norm_slab(bf16_t* out, const float* slab, int sk, bf16_t* residual, const bf16_t* w,
+                                          float eps, int rows, int hidden, int64_t out_stride, hipStream_t s);
+hipError_t launch_rope_and_cache_slab(bf16_t* q_out, const float* slab, int sk, const int64_t* positions,
+                                      const float* cos_sin, const int64_t* slot_mapping, bf16_t* k_cache,
+                                      bf16_t* v_cache, int num_tokens, int hq, int hkv, int head_dim, int block_size,
+                                      hipStream_t s);
+
 }  // namespace die

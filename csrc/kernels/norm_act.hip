@@ -99,6 +99,83 @@ hipError_t launch_fused_add_rms_norm(bf16_t* out, const bf16_t* in, bf16_t* resi
 }
 
 // ----------------------------------------------------------------------------
+// residual += sum_s slab[s]; out = rmsnorm(residual) * w. The slab is the fp32
+// split-K output of gemm_decode (mode 2): the split-K reduction happens here,
+// in the prologue of a kernel that runs anyway.
+template <int NT, int NC>
+__global__ void __launch_bounds__(NT) rmsnorm_slab_kernel(bf16_t* __restrict__ out, const float* __restrict__ slab,
+                                                          int sk, bf16_t* __restrict__ residual,
+                                                          const bf16_t* __restrict__ w, float eps, int rows,
+                                                          int hidden, int64_t out_stride) {
+  __shared__ float red[NT / 64];
+  const int64_t row = blockIdx.x;
+  const int nchunk = hidden >> 3;
+  uint4* res = reinterpret_cast<uint4*>(residual + row * (int64_t)hidden);
+  const int64_t sstride = (int64_t)rows * hidden;
+  float x[NC][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int idx = threadIdx.x + c * NT;
+    if (idx < nchunk) {
+      unpack8(res[idx], x[c]);
+      for (int s = 0; s < sk; ++s) {
+        const float4* p = reinterpret_cast<const float4*>(slab + s * sstride + row * hidden + idx * 8);
+        const float4 a = p[0], b = p[1];
+        x[c][0] += a.x; x[c][1] += a.y; x[c][2] += a.z; x[c][3] += a.w;
+        x[c][4] += b.x; x[c][5] += b.y; x[c][6] += b.z; x[c][7] += b.w;
+      }
+      uint4 packed = pack8(x[c]);
+      res[idx] = packed;
+      unpack8(packed, x[c]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += x[c][j] * x[c][j];
+    }
+  }
+  const float inv = rsqrtf(block_sum<NT>(ss, red) / (float)hidden + eps);
+  const uint4* wv = reinterpret_cast<const uint4*>(w);
+  uint4* dst = reinterpret_cast<uint4*>(out + row * out_stride);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int idx = threadIdx.x + c * NT;
+    if (idx < nchunk) {
+      float g[8], y[8];
+      unpack8(wv[idx], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] = x[c][j] * inv * g[j];
+      dst[idx] = pack8(y);
+    }
+  }
+}
+
+hipError_t launch_fused_add_rms_norm_slab(bf16_t* out, const float* slab, int sk, bf16_t* residual, const bf16_t* w,
+                                          float eps, int rows, int hidden, int64_t out_stride, hipStream_t s) {
+  if (rows == 0) return hipSuccess;
+  if (hidden % 8) return hipErrorInvalidValue;
+  const int nc = (hidden / 8 + 255) / 256;
+  dim3 grid(rows), block(256);
+  switch (nc) {
+#define DIE_RS(N)                                                                                              \
+  case N:                                                                                                      \
+    hipLaunchKernelGGL((rmsnorm_slab_kernel<256, N>), grid, block, 0, s, out, slab, sk, residual, w, eps, rows, \
+                       hidden, out_stride);                                                                    \
+    break;
+    DIE_RS(1)
+    DIE_RS(2)
+    DIE_RS(3)
+    DIE_RS(4)
+    DIE_RS(5)
+    DIE_RS(6)
+    DIE_RS(7)
+    DIE_RS(8)
+#undef DIE_RS
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------
 // silu(gate) * up. Input row = [gate(I) | up(I)], output row = I.
 // grid = (rows, ceil(I/8 / 256)); one 16-byte chunk of gate and of up per lane.
 __global__ void __launch_bounds__(256) silu_mul_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ in,

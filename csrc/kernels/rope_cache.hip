@@ -87,6 +87,98 @@ hipError_t launch_rope_and_cache(bf16_t* qkv, int64_t qkv_stride, const int64_t*
   return hipGetLastError();
 }
 
+// Same op fed by fp32 split-K slabs [sk][T][(hq+2hkv)*D] of the decode QKV
+// GEMM: the slabs are summed here, q is written (bf16) to q_out [T][hq*D].
+template <int D>
+__global__ void __launch_bounds__(256) rope_cache_slab_kernel(bf16_t* __restrict__ q_out,
+                                                              const float* __restrict__ slab, int sk,
+                                                              const int64_t* __restrict__ positions,
+                                                              const float* __restrict__ cos_sin,
+                                                              const int64_t* __restrict__ slot_mapping,
+                                                              bf16_t* __restrict__ k_cache,
+                                                              bf16_t* __restrict__ v_cache, int T, int hq, int hkv,
+                                                              int block_size) {
+  constexpr int HALF = D / 2;
+  constexpr int RC = HALF / 8;
+  constexpr int VC = D / 8;
+  const int64_t tok = blockIdx.x;
+  const int width = (hq + 2 * hkv) * D;
+  const int64_t sstride = (int64_t)T * width;
+  const float* row = slab + tok * width;
+  const int64_t pos = positions[tok];
+  const int64_t slot = slot_mapping ? slot_mapping[tok] : -1;
+  const float* cs = cos_sin + pos * D;
+  const int n_rot = (hq + hkv) * RC;
+  const int n_items = n_rot + hkv * VC;
+  auto sum8 = [&](int off, float* v) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    for (int s = 0; s < sk; ++s) {
+      const float4* p = reinterpret_cast<const float4*>(row + s * sstride + off);
+      const float4 a = p[0], b = p[1];
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+      v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+  };
+  for (int it = threadIdx.x; it < n_items; it += blockDim.x) {
+    if (it < n_rot) {
+      const int head = it / RC, c = it % RC;
+      float a[8], b[8], co[8], si[8], ya[8], yb[8];
+      sum8(head * D + c * 8, a);
+      sum8(head * D + c * 8 + HALF, b);
+      *reinterpret_cast<float4*>(co) = *reinterpret_cast<const float4*>(cs + c * 8);
+      *reinterpret_cast<float4*>(co + 4) = *reinterpret_cast<const float4*>(cs + c * 8 + 4);
+      *reinterpret_cast<float4*>(si) = *reinterpret_cast<const float4*>(cs + HALF + c * 8);
+      *reinterpret_cast<float4*>(si + 4) = *reinterpret_cast<const float4*>(cs + HALF + c * 8 + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ya[j] = a[j] * co[j] - b[j] * si[j];
+        yb[j] = b[j] * co[j] + a[j] * si[j];
+      }
+      const uint4 pa = pack8(ya), pb = pack8(yb);
+      if (head < hq) {
+        bf16_t* x = q_out + tok * hq * D + head * D + c * 8;
+        *reinterpret_cast<uint4*>(x) = pa;
+        *reinterpret_cast<uint4*>(x + HALF) = pb;
+      } else if (slot >= 0) {
+        const int kh = head - hq;
+        const int64_t blk = slot / block_size, off = slot % block_size;
+        bf16_t* dst = k_cache + ((blk * hkv + kh) * block_size + off) * D + c * 8;
+        *reinterpret_cast<uint4*>(dst) = pa;
+        *reinterpret_cast<uint4*>(dst + HALF) = pb;
+      }
+    } else if (slot >= 0) {
+      const int v = it - n_rot;
+      const int kh = v / VC, c = v % VC;
+      float val[8];
+      sum8((hq + hkv + kh) * D + c * 8, val);
+      const int64_t blk = slot / block_size, off = slot % block_size;
+      *reinterpret_cast<uint4*>(v_cache + ((blk * hkv + kh) * block_size + off) * D + c * 8) = pack8(val);
+    }
+  }
+}
+
+hipError_t launch_rope_and_cache_slab(bf16_t* q_out, const float* slab, int sk, const int64_t* positions,
+                                      const float* cos_sin, const int64_t* slot_mapping, bf16_t* k_cache,
+                                      bf16_t* v_cache, int num_tokens, int hq, int hkv, int head_dim, int block_size,
+                                      hipStream_t s) {
+  if (num_tokens == 0) return hipSuccess;
+  dim3 grid(num_tokens), block(256);
+  switch (head_dim) {
+    case 64:
+      hipLaunchKernelGGL(rope_cache_slab_kernel<64>, grid, block, 0, s, q_out, slab, sk, positions, cos_sin,
+                         slot_mapping, k_cache, v_cache, num_tokens, hq, hkv, block_size);
+      break;
+    case 128:
+      hipLaunchKernelGGL(rope_cache_slab_kernel<128>, grid, block, 0, s, q_out, slab, sk, positions, cos_sin,
+                         slot_mapping, k_cache, v_cache, num_tokens, hq, hkv, block_size);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 // ----------------------------------------------------------------------------
 // Block movers. `slab` = elements of one (layer, kv, block) = hkv*block_size*D.
 // The pool is viewed as [planes = layers*2][num_blocks][slab].

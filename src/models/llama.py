@@ -224,12 +224,14 @@ class CausalLM:
         d = self.head_dim
         hq, hkv = self.hq, self.hkv
         residual = F.embedding(input_ids, self.embed)
+        if self._slab_path(input_ids):
+            return self._forward_decode_slab(residual, positions, meta, kv_pool)
         x = ops.rms_norm(residual, self.layers[0].ln1, eps)
         h = None
         for li, lw in enumerate(self.layers):
             if li > 0:
                 x = ops.fused_add_rms_norm(h, residual, lw.ln1, eps)
-            qkv = F.linear(x, lw.qkv)
+            qkv = ops.linear(x, lw.qkv)
             k_cache, v_cache = kv_pool[li, 0], kv_pool[li, 1]
             ops.rope_and_cache(qkv, positions, self.cos_sin, meta.slot_mapping, k_cache, v_cache, hq, hkv, d)
             q = qkv[:, : hq * d]
@@ -239,18 +241,50 @@ class CausalLM:
             else:
                 attn = ops.attn_decode(q, k_cache, v_cache, meta.block_tables, meta.ctx_lens, meta.max_ctx, hq,
                                        hkv, self.scale, part_o=meta.part_o, part_ml=meta.part_ml)
-            o = self.tp.all_reduce(F.linear(attn, lw.o))
+            o = self.tp.all_reduce(ops.linear(attn, lw.o))
             x = ops.fused_add_rms_norm(o, residual, lw.ln2, eps)
             if a.is_moe:
                 gating = F.linear(x, lw.router)
                 h = ops.moe_forward(x, lw.w13, lw.w2, gating, a.top_k)
             else:
-                h = F.linear(ops.silu_and_mul(F.linear(x, lw.gate_up)), lw.down)
+                h = ops.linear(ops.linear_silu_mul(x, lw.gate_up), lw.down)
             h = self.tp.all_reduce(h)
         return ops.fused_add_rms_norm(h, residual, self.norm, eps)
 
+    # ------------------------------------------------- decode fast path (M <= 32)
+    def _slab_path(self, input_ids: torch.Tensor) -> bool:
+        """Decode-sized steps on the GPU at TP=1 run every projection on the
+        weight-streaming kernel with split-K fp32 slabs reduced inside the
+        consumer kernels (no separate reduction or SiLU launches)."""
+        if not (input_ids.is_cuda and ops.native_available()) or self.tp.enabled or self.arch.is_moe:
+            return False
+        m, h = input_ids.shape[0], self.arch.hidden_size
+        return (1 <= m <= ops.DECODE_GEMM_MAX_M and h % 256 == 0 and self.inter % 256 == 0
+                and (self.hq * self.head_dim) % 256 == 0 and self.layers[0].qkv.shape[0] % 32 == 0)
+
+    def _forward_decode_slab(self, residual, positions, meta: AttnMetadata, kv_pool):
+        a, eps, d = self.arch, self.arch.rms_eps, self.head_dim
+        hq, hkv = self.hq, self.hkv
+        x = ops.rms_norm(residual, self.layers[0].ln1, eps)
+        slab = None
+        for li, lw in enumerate(self.layers):
+            if li > 0:
+                x = ops.fused_add_rms_norm_slab(slab, residual, lw.ln1, eps)
+            k_cache, v_cache = kv_pool[li, 0], kv_pool[li, 1]
+            q = ops.rope_and_cache_slab(ops.linear_slab(x, lw.qkv), positions, self.cos_sin, meta.slot_mapping,
+                                        k_cache, v_cache, hq, hkv, d)
+            if meta.is_prefill:
+                attn = ops.attn_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_q, meta.ctx_lens,
+                                        meta.max_q_len, hq, hkv, self.scale)
+            else:
+                attn = ops.attn_decode(q, k_cache, v_cache, meta.block_tables, meta.ctx_lens, meta.max_ctx, hq,
+                                       hkv, self.scale, part_o=meta.part_o, part_ml=meta.part_ml)
+            x = ops.fused_add_rms_norm_slab(ops.linear_slab(attn, lw.o), residual, lw.ln2, eps)
+            slab = ops.linear_slab(ops.linear_silu_mul(x, lw.gate_up), lw.down)
+        return ops.fused_add_rms_norm_slab(slab, residual, self.norm, eps)
+
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
-        logits = F.linear(hidden, self.lm_head)
+        logits = ops.linear(hidden, self.lm_head)
         if self.vocab_parallel:
             logits = self.tp.all_gather_last(logits)
         return logits

@@ -152,6 +152,119 @@ def scatter_blocks(pool: torch.Tensor, ids: torch.Tensor, buf: torch.Tensor) -> 
     _kern().move_blocks(pool, buf, ids, False)
 
 
+DECODE_GEMM_MAX_M = 32
+
+
+def _decode_gemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return (x.is_cuda and 1 <= x.shape[0] <= DECODE_GEMM_MAX_M and x.shape[1] % 256 == 0
+            and w.shape[0] % 16 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0)
+
+
+def gemm_decode(x: torch.Tensor, w: torch.Tensor, mode: int = 0, wr: int = 64, sk: int = 1,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Raw access to the decode GEMM kernel (see csrc/kernels/gemm_decode.hip).
+    mode 0: bf16 x@w^T; mode 1: bf16 silu(gate)*up (w = [gate; up]);
+    mode 2: fp32 split-K slabs [sk, M, N]."""
+    m = x.shape[0]
+    n = w.shape[0] // 2 if mode == 1 else w.shape[0]
+    if out is None:
+        if mode == 2:
+            out = torch.empty(sk, m, n, dtype=torch.float32, device=x.device)
+        else:
+            out = torch.empty(m, n, dtype=x.dtype, device=x.device)
+    _kern().gemm_decode(out, x, w, mode, wr, sk)
+    return out
+
+
+# (N, K, mode) -> (wr, sk), measured with bench/micro_gemm_decode.py on MI355X (cold
+# weights, M = 32; profiles/micro_gemm_decode_m32_r1.jsonl). Fastest configs put
+# ~(N/wr)*sk ≈ 256 workgroups (one per CU) on the chip.
+DECODE_GEMM_CFG = {
+    (6144, 4096, 2): (64, 2),    # Llama-3-8B / Mixtral qkv  (13.5 us vs hipBLASLt 15.3)
+    (4096, 4096, 2): (64, 4),    # 8B o_proj                  (9.8 vs 13.3)
+    (14336, 4096, 1): (64, 1),   # 8B gate/up + SiLU          (49.2 vs 55.1)
+    (4096, 14336, 2): (64, 4),   # 8B down_proj               (24.5 vs 33.9)
+    (1280, 8192, 2): (64, 8),    # 70B TP=8 qkv               (8.3 vs 15.3)
+    (8192, 1024, 0): (32, 1),    # 70B TP=8 o_proj            (6.3 vs 11.4)
+    (3584, 8192, 1): (32, 1),    # 70B TP=8 gate/up + SiLU    (27.5 vs 29.4)
+    (8192, 3584, 0): (32, 1),    # 70B TP=8 down_proj         (14.8 vs 15.9)
+}
+
+
+def _cfg_for(n: int, k: int, mode: int):
+    c = DECODE_GEMM_CFG.get((n, k, mode))
+    if c is not None:
+        return c
+    import math
+
+    best, score = (64, 1), 1e9
+    for wr in (64, 32):
+        cols = wr // 2 if mode == 1 else wr
+        if n % cols:
+            continue
+        for sk in ((1, 2, 4, 8) if mode == 2 else (1,)):
+            if k % (256 * sk):
+                continue
+            s = abs(math.log2((n // cols) * sk / 256.0))
+            if s < score - 1e-9:
+                best, score = (wr, sk), s
+    return best
+
+
+def decode_slab_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return _decode_gemm_ok(x, w) and w.shape[0] % 32 == 0 and w.shape[0] <= 32768
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x @ w^T. Decode-sized M (<= 32 rows) runs on the weight-streaming
+    gfx950 kernel (gemm_decode.hip); larger M goes to hipBLASLt."""
+    # the LM head (N ~ 128K) streams at the same rate on hipBLASLt: keep it there
+    if _decode_gemm_ok(x, w) and w.shape[0] % 32 == 0 and w.shape[0] <= 32768:
+        wr, _ = _cfg_for(w.shape[0], x.shape[1], 0)
+        return gemm_decode(x, w, 0, wr, 1, out)
+    return torch.nn.functional.linear(x, w, out=out) if out is not None else torch.nn.functional.linear(x, w)
+
+
+def linear_slab(x: torch.Tensor, w: torch.Tensor, sk: Optional[int] = None, wr: Optional[int] = None) -> torch.Tensor:
+    """fp32 split-K slabs [sk, M, N] of x @ w^T (decode sizes only); the
+    consumer (fused_add_rms_norm_slab / rope_and_cache_slab) reduces them."""
+    if sk is None or wr is None:
+        wr0, sk0 = _cfg_for(w.shape[0], x.shape[1], 2)
+        wr, sk = wr or wr0, sk or sk0
+    return gemm_decode(x, w, 2, wr, sk)
+
+
+def linear_silu_mul(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
+    """silu(x @ gate^T) * (x @ up^T) with w_gate_up = [gate; up] (fused epilogue
+    in the decode kernel; GEMM + silu_and_mul kernel otherwise)."""
+    if _decode_gemm_ok(x, w_gate_up) and (w_gate_up.shape[0] // 2) % 32 == 0:
+        wr, _ = _cfg_for(w_gate_up.shape[0] // 2, x.shape[1], 1)
+        return gemm_decode(x, w_gate_up, 1, wr, 1)
+    return silu_and_mul(torch.nn.functional.linear(x, w_gate_up))
+
+
+def fused_add_rms_norm_slab(slab: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """residual += slab.sum(0) (bf16, in place); returns rms_norm(residual) * w."""
+    if not slab.is_cuda:
+        return fused_add_rms_norm(slab.sum(0).to(residual.dtype), residual, w, eps, out)
+    if out is None:
+        out = torch.empty(residual.shape, dtype=residual.dtype, device=residual.device)
+    _kern().fused_add_rms_norm_slab(out, slab, residual, w, eps)
+    return out
+
+
+def rope_and_cache_slab(slab, positions, cos_sin, slot_mapping, k_cache, v_cache, hq: int, hkv: int,
+                        head_dim: int, q_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Sum the QKV split-K slabs, rotate q/k, write k/v into the paged cache;
+    returns q [T, hq*D] (bf16)."""
+    t = slab.shape[1]
+    if q_out is None:
+        q_out = torch.empty(t, hq * head_dim, dtype=torch.bfloat16, device=slab.device)
+    _kern().rope_and_cache_slab(q_out, slab, positions, cos_sin, slot_mapping, k_cache, v_cache, hq, hkv, head_dim)
+    return q_out
+
+
 def topk_softmax(gating: torch.Tensor, k: int, renorm: bool = True):
     if not gating.is_cuda:
         return ref.topk_softmax(gating, k, renorm)

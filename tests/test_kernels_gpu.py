@@ -218,3 +218,64 @@ def test_moe(dev):
     assert torch.equal(ids.sort(-1).values.cpu(), idr.sort(-1).values.cpu())
     close(w.sort(-1).values, wr.sort(-1).values, atol=1e-4)
     close(ops.moe_forward(x, w13, w2, gating, k), ref.moe_forward(x, w13, w2, gating, k), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("m,n,k", [(1, 4096, 4096), (7, 6144, 4096), (32, 4096, 14336), (32, 1024, 256),
+                                   (20, 128256, 4096)])
+def test_gemm_decode(dev, m, n, k):
+    x = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(n, k, device=dev, dtype=torch.bfloat16) / math.sqrt(k)
+    y = ops.linear(x, w)
+    r = (x.float() @ w.float().t())
+    close(y, r, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("m,inter,k", [(32, 14336, 4096), (5, 2048, 1024)])
+def test_gemm_decode_silu(dev, m, inter, k):
+    x = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(2 * inter, k, device=dev, dtype=torch.bfloat16) / math.sqrt(k)
+    y = ops.linear_silu_mul(x, w)
+    h = x.float() @ w.float().t()
+    r = torch.nn.functional.silu(h[:, :inter]) * h[:, inter:]
+    close(y, r, atol=2e-2, rtol=2e-2)
+
+
+def test_gemm_decode_strided_input(dev):
+    big = torch.randn(16, 6144, device=dev, dtype=torch.bfloat16)
+    x = big[:, :4096]
+    w = torch.randn(512, 4096, device=dev, dtype=torch.bfloat16) / 64
+    close(ops.linear(x, w), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("wr,sk", [(32, 1), (64, 4), (64, 2)])
+def test_gemm_decode_slab_and_consumers(dev, wr, sk):
+    m, h = 11, 4096
+    x = torch.randn(m, 4096, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(h, 4096, device=dev, dtype=torch.bfloat16) / 64
+    slab = ops.linear_slab(x, w, sk, wr)
+    assert slab.shape == (sk, m, h)
+    close(slab.sum(0), x.float() @ w.float().t(), atol=1e-2, rtol=1e-2)
+    res = torch.randn(m, h, device=dev, dtype=torch.bfloat16)
+    g = torch.randn(h, device=dev, dtype=torch.bfloat16)
+    y_ref, r_ref = ref.fused_add_rms_norm(slab.sum(0).to(torch.bfloat16), res.clone(), g, 1e-5)
+    r2 = res.clone()
+    y = ops.fused_add_rms_norm_slab(slab, r2, g, 1e-5)
+    close(r2, r_ref, atol=2e-2, rtol=1e-2)
+    close(y, y_ref, atol=5e-2, rtol=3e-2)
+
+
+def test_rope_and_cache_slab(dev):
+    hq, hkv, t, sk, bs, nb = 32, 8, 13, 2, 16, 8
+    width = (hq + 2 * hkv) * 128
+    slab = torch.randn(sk, t, width, device=dev)
+    pos = torch.randint(0, 2000, (t,), device=dev)
+    slots = torch.randperm(nb * bs, device=dev)[:t]
+    cs = ref.rope_cos_sin(4096, 128, 500000.0, dev)
+    kc, vc = _paged(nb, hkv, bs, dev)
+    kr, vr = _paged(nb, hkv, bs, dev)
+    q = ops.rope_and_cache_slab(slab, pos, cs, slots, kc, vc, hq, hkv, 128)
+    qkv = slab.sum(0).to(torch.bfloat16)
+    ref.rope_and_cache(qkv, pos.cpu(), cs, slots.cpu(), kr, vr, hq, hkv, 128)
+    close(q, qkv[:, : hq * 128], atol=3e-2, rtol=2e-2)
+    close(kc, kr, atol=3e-2, rtol=2e-2)
+    close(vc, vr, atol=2e-2, rtol=1e-2)
