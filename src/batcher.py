@@ -69,6 +69,7 @@ class Batcher:
         coalesce: Optional[Callable[[List[Any]], Any]] = None,
         split: Optional[Callable[[Any, int], List[Any]]] = None,
         max_inflight_batches: Optional[int] = None,
+        eager_when_idle: bool = False,
     ):
         if max_batch_size < 1:
             raise ValueError("max_batch_size must be at least 1")
@@ -83,6 +84,10 @@ class Batcher:
         self._flush_tasks: Dict[str, asyncio.Task] = {}
         self._inflight: set = set()
         self._sem = asyncio.Semaphore(max_inflight_batches) if max_inflight_batches else None
+        # eager_when_idle: a request for a key with nothing in flight is dispatched at once
+        # (no max_latency wait when the backend is idle); later arrivals batch up behind it.
+        self.eager_when_idle = eager_when_idle
+        self._inflight_by_key: Dict[str, int] = {}
         self._running = False
         self._lock = asyncio.Lock()
         self.total_batches = 0
@@ -146,6 +151,11 @@ class Batcher:
         to_flush: Optional[List[BatchedRequest]] = None
         async with self._lock:
             batch = self._batches.get(key)
+            if batch is None and self.eager_when_idle and not self._inflight_by_key.get(key):
+                self.total_requests += 1
+                eager = Batch(model_name, version, [req], time.time(), self.max_batch_size, self.max_latency)
+                self._spawn(key, eager, [req])
+                return req.future
             if batch is None:
                 batch = Batch(model_name, version, [], time.time(), self.max_batch_size, self.max_latency)
                 self._batches[key] = batch
@@ -172,7 +182,13 @@ class Batcher:
     def _spawn(self, key: str, batch: Batch, reqs: List[BatchedRequest]) -> None:
         task = asyncio.create_task(self._process_batch(key, batch, reqs))
         self._inflight.add(task)
-        task.add_done_callback(self._inflight.discard)
+        self._inflight_by_key[key] = self._inflight_by_key.get(key, 0) + 1
+
+        def done(t, key=key):
+            self._inflight.discard(t)
+            self._inflight_by_key[key] -= 1
+
+        task.add_done_callback(done)
 
     async def _timer(self, key: str, batch: Batch) -> None:
         try:

@@ -84,8 +84,10 @@ class Coordinator:
         self.router = Router(self.registry, health_check_interval=health_check_interval)
         self.lbs: Dict[str, LoadBalancer] = {}
         self.cache = KVCache(max_size=cache_size, eviction_policy=cache_policy, default_ttl=cache_ttl_s)
+        # eager_when_idle: an idle shard gets a request immediately; max_latency only
+        # applies while a previous batch for that shard is still in flight.
         self.batcher = Batcher(max_batch_size=max_batch_size, max_latency_ms=max_latency_ms,
-                               batch_callback=self._batch_callback)
+                               batch_callback=self._batch_callback, eager_when_idle=True)
         self.rpc = RPCClient(max_idle_per_host=512)
         self.tracer = GLOBAL_TRACER
         self.server: Optional[asyncio.AbstractServer] = None
@@ -109,7 +111,9 @@ class Coordinator:
         await self.router.start()
         for lb in self.lbs.values():
             await lb.start()
-        self.server = await asyncio.start_server(self._handle_connection, self.host, self.port, limit=1 << 26)
+        # backlog: a burst of >100 new client connections must not hit SYN retransmits (1 s stalls)
+        self.server = await asyncio.start_server(self._handle_connection, self.host, self.port, limit=1 << 26,
+                                                 backlog=4096)
         self.port = self.server.sockets[0].getsockname()[1]
         logger.info("Coordinator listening on %s:%d", self.host, self.port)
         return self.port

@@ -99,7 +99,7 @@ class Worker:
         for m in self.models.values():
             if hasattr(m, "start"):
                 await m.start()
-        self.server = await asyncio.start_server(self._handle_connection, host=self.host, port=self.port,
+        self.server = await asyncio.start_server(self._handle_connection, host=self.host, port=self.port, backlog=4096,
                                                  limit=1 << 26)
         self.port = self.server.sockets[0].getsockname()[1]
         logger.info("Worker %s listening on %s:%d", self.worker_id, self.host, self.port)
