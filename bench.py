@@ -62,8 +62,8 @@ def parse():
     return p.parse_args()
 
 
-async def serve_wave(batcher, n, prompt_len, gen_len, temperature, rng, tag):
-    prompts = [[rng.randrange(3, 128000) for _ in range(prompt_len)] for _ in range(n)]
+async def serve_wave(batcher, n, prompt_len, gen_len, temperature, rng, tag, vocab=128000):
+    prompts = [[rng.randrange(3, vocab) for _ in range(prompt_len)] for _ in range(n)]
     t0 = [0.0] * n
     lat = [0.0] * n
 
@@ -146,7 +146,7 @@ def main():
         batcher = Batcher(max_batch_size=args.batch, max_latency_ms=args.max_latency_ms, batch_callback=callback)
         await batcher.start()
         for w in range(args.warmup):
-            await serve_wave(batcher, args.batch, args.prompt_len, args.gen_len, args.temperature, rng, f"w{w}")
+            await serve_wave(batcher, args.batch, args.prompt_len, args.gen_len, args.temperature, rng, f"w{w}", engine.arch.vocab_size)
         torch.cuda.synchronize(dev)
         if tp is not None:
             engine.runner.stop_followers()
@@ -157,7 +157,7 @@ def main():
         t0 = time.perf_counter()
         lats = []
         for s in range(args.steps):
-            lats += await serve_wave(batcher, args.batch, args.prompt_len, args.gen_len, args.temperature, rng,
+            lats += await serve_wave(batcher, args.batch, args.prompt_len, args.gen_len, args.temperature, rng, vocab=engine.arch.vocab_size, tag=
                                      f"s{s}")
             if args.verbose and rank == 0:
                 print(f"step {s}: {time.perf_counter() - t0:.2f}s", file=sys.stderr, flush=True)
