@@ -11,7 +11,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from src import ops  # noqa: E402
 
 SHAPES = {  # name: (N_out, K, silu)
@@ -51,6 +51,8 @@ def timeit(fn, ws, iters=None):
 
 def main():
     m = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+    if len(sys.argv) > 2 and sys.argv[2] == "nt":
+        return main_nt(m)
     dev = torch.device("cuda:0")
     for name, (n, k, silu) in SHAPES.items():
         wrows = 2 * n if silu else n
@@ -75,6 +77,27 @@ def main():
                     res.append((f"gd_slab_wr{wr}_sk{sk}", timeit(lambda w: ops.gemm_decode(x, w, 2, wr, sk), ws)))
         for v, us in res:
             print(json.dumps({"shape": name, "M": m, "N": n, "K": k, "variant": v, "us": round(us, 2),
+                              "GBps": round(wbytes / us / 1e3, 1)}), flush=True)
+        del ws
+        torch.cuda.empty_cache()
+
+
+def main_nt(m):
+    """Tuned config per shape, non-temporal vs default-policy weight loads."""
+    dev = torch.device("cuda:0")
+    for name, (n, k, silu) in SHAPES.items():
+        if name.startswith("lm_head"):
+            continue
+        mode = 1 if silu else (0 if (n, k, 0) in ops.DECODE_GEMM_CFG else 2)
+        wr, sk = ops._cfg_for(n, k, mode)
+        wrows = 2 * n if silu else n
+        x = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
+        wbytes = wrows * k * 2
+        copies = max(2, int(1.5 * 2**30 // wbytes) + 1)
+        ws = [torch.randn(wrows, k, device=dev, dtype=torch.bfloat16) / 64 for _ in range(copies)]
+        for nt in (False, True):
+            us = timeit(lambda w: ops.gemm_decode(x, w, mode, wr, sk, nt=nt), ws)
+            print(json.dumps({"shape": name, "M": m, "mode": mode, "wr": wr, "sk": sk, "nt": nt, "us": round(us, 2),
                               "GBps": round(wbytes / us / 1e3, 1)}), flush=True)
         del ws
         torch.cuda.empty_cache()

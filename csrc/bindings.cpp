@@ -128,7 +128,9 @@ void attn_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor b
                                    (int)k_cache.size(2), (float)scale, cur_stream()));
 }
 
-void attn_decode(Tensor out, Tensor part_o, Tensor part_ml, Tensor q, Tensor k_cache, Tensor v_cache,
+// counters: int32 [>= num_seqs * hkv], zero before first use (the kernel re-arms them); an empty tensor
+// selects the two-kernel path (partials + merge launch).
+void attn_decode(Tensor out, Tensor part_o, Tensor part_ml, Tensor counters, Tensor q, Tensor k_cache, Tensor v_cache,
                  Tensor block_tables, Tensor ctx_lens, int64_t max_ctx, int64_t hq, int64_t hkv, double scale) {
   DIE_CHECK_CUDA(q);
   DIE_CHECK_BF16(q);
@@ -152,7 +154,13 @@ void attn_decode(Tensor out, Tensor part_o, Tensor part_ml, Tensor q, Tensor k_c
   DIE_CHECK_DTYPE(part_ml, at::kFloat);
   TORCH_CHECK(part_o.numel() >= nseq * hq * maxp * D && part_ml.numel() >= nseq * hq * maxp * 2,
               "partial buffers too small for max_ctx");
-  DIE_HIP(die::launch_attn_decode(bf(out), part_o.data_ptr<float>(), part_ml.data_ptr<float>(), bf(q), q.stride(0),
+  int* cnt = nullptr;
+  if (counters.numel() > 0) {
+    DIE_CHECK_DTYPE(counters, at::kInt);
+    TORCH_CHECK(counters.is_cuda() && counters.numel() >= nseq * hkv, "attn counters: int32 [>= num_seqs*hkv]");
+    cnt = counters.data_ptr<int>();
+  }
+  DIE_HIP(die::launch_attn_decode(bf(out), part_o.data_ptr<float>(), part_ml.data_ptr<float>(), cnt, bf(q), q.stride(0),
                                   bf(k_cache), bf(v_cache), block_tables.data_ptr<int>(), (int)block_tables.size(1),
                                   ctx_lens.data_ptr<int>(), (int)nseq, (int)max_ctx, (int)hq, (int)hkv, (int)D,
                                   (int)k_cache.size(2), (float)scale, cur_stream()));
@@ -276,7 +284,7 @@ void moe_grouped_gemm(Tensor y, Tensor x, Tensor w, Tensor offsets) {
 //   mode 0: y bf16 [M, N], w [N, K]
 //   mode 1: y bf16 [M, N] = silu(x gate^T) * (x up^T), w = [gate; up] [2N, K]
 //   mode 2: y fp32 split-K slabs [sk, M, N], w [N, K]
-void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t sk) {
+void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t sk, bool nt) {
   DIE_CHECK_CUDA(x);
   DIE_CHECK_BF16(x);
   DIE_CHECK_BF16(w);
@@ -303,7 +311,7 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
   TORCH_CHECK(w.dim() == 2 && w.size(1) == K && w.size(0) == (mode == 1 ? 2 * N : N), "gemm_decode w shape");
   TORCH_CHECK(N % (mode == 1 ? wr / 2 : wr) == 0, "N not a multiple of the column tile");
   DIE_HIP(die::launch_gemm_decode(y.data_ptr(), ldy, bf(x), x.stride(0), bf(w), (int)M, (int)N, (int)K, (int)mode,
-                                  (int)wr, (int)sk, cur_stream()));
+                                  (int)wr, (int)sk, nt, cur_stream()));
 }
 
 void fused_add_rms_norm_slab(Tensor out, Tensor slab, Tensor residual, Tensor w, double eps) {

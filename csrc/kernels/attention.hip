@@ -24,6 +24,8 @@
 //    a wave-private LDS tile), writes an unnormalised partial; a second kernel
 //    merges partials (flash-decoding). Grid sized by the max context so the
 //    launch is hipGraph-capturable; surplus workgroups exit immediately.
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -441,6 +443,348 @@ __global__ void __launch_bounds__(256, 2) attn_decode_kernel(float* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------
+// Decode v3 (block_size 16, G <= 8): persistent, prefetching, self-merging.
+//
+// * Grid = one workgroup per CU. The (sequence, kv head) pairs' contexts are cut
+//   into parts of C 128-key chunks, C = ceil(maxp * pairs / grid) from the static
+//   max_ctx (no device pre-pass: it would put a dependent HBM read in front of every
+//   workgroup), so pairs x parts ~ the grid (Llama-3-8B, 32 seqs x 8 kv heads: one
+//   part per pair, one pair per CU).
+// * A task streams its chunks through two 64 KiB LDS buffers: chunk c+1 is issued by
+//   LDS-DMA (global_load_lds_dwordx4, lane-linear images, XOR swizzle on the source
+//   address) before chunk c is computed; the wait is a counted `s_waitcnt vmcnt(16)`
+//   + raw s_barrier (cdna_hip_programming.md "Pipelining across barriers"). The
+//   chunk loop has no data-dependent branches (keys past the context are clamped on
+//   load and masked in the softmax), so the O accumulators stay put in registers.
+// * Block ids and context lengths are wave-uniform scalar loads (one 16-key block
+//   per LDS-DMA instruction): no vector load forces a vmcnt(0) drain.
+// * The 4 waves merge once per task. A task covering the whole context writes the
+//   normalised bf16 output directly (no second kernel). Otherwise it writes an
+//   fp32 partial with write-through (sc1) stores, draws a ticket from a per-pair
+//   agent-scope counter and the last arriver merges all parts with sc1 loads and
+//   re-arms the counter (MI355X_MICROARCH.md inter-workgroup visibility table,
+//   "ONE lane of each storing workgroup ... agent-scope atomic add" row).
+constexpr int V3_CHUNK = 2 * DEC_KEYS * DEC_ROW;               // K + V images of one chunk: 64 KiB
+constexpr int V3_QIMG = 2048;                                  // G <= 8 query rows x 256 B
+constexpr int V3_BUF = V3_CHUNK + V3_QIMG;
+constexpr int V3_ML = 4 * 32 * 2 * 4;                          // per-wave (m, l): 1 KiB
+constexpr int V3_MERGE = V3_ML + 4 * 8 * D * 4;                // + per-wave O for G <= 8: 16 KiB
+constexpr int V3_LDS = 2 * V3_BUF + V3_MERGE + 16;             // 152,592 B
+
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// pv_lds_swz with the transposed reads in inline asm: the ds_read_b64_tr_b16 builtin carries no
+// memory operand, so hipcc's waitcnt pass assumes it may alias the LDS-DMA prefetch of the OTHER
+// buffer and drains it (vmcnt(0)) before every PV step. The 16 reads are issued back to back and
+// retired by one explicit lgkmcnt(0) that is tied to their results.
+__device__ __forceinline__ void pv_lds_swz_v3(const char* vimg, const f32x16_t& p, State& st, int lane) {
+  bf16x8_t pf[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    uint4 w;
+    w.x = pack2(p[8 * s2 + 0], p[8 * s2 + 1]);
+    w.y = pack2(p[8 * s2 + 2], p[8 * s2 + 3]);
+    w.z = pack2(p[8 * s2 + 4], p[8 * s2 + 5]);
+    w.w = pack2(p[8 * s2 + 6], p[8 * s2 + 7]);
+    pf[s2] = as_frag(w);
+  }
+  const int g = lane >> 4, i = lane & 15, h = lane >> 5;
+  const int q4 = i >> 2, p4 = i & 3;
+  const uint32_t vb = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)vimg);
+  short4_t t[4][2][2];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    const int lch = 4 * db + 2 * (g & 1) + (p4 >> 1);
+    const int off = 16 * (lch ^ (q4 << 2)) + 8 * (p4 & 1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int r0 = 16 * s2 + 4 * h + q4;
+      const uint32_t a0 = vb + r0 * DEC_ROW + off;
+      asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(t[db][s2][0]) : "v"(a0));
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:2048" : "=v"(t[db][s2][1]) : "v"(a0));
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(t[0][0][0]), "+v"(t[0][0][1]), "+v"(t[0][1][0]), "+v"(t[0][1][1]), "+v"(t[1][0][0]),
+                 "+v"(t[1][0][1]), "+v"(t[1][1][0]), "+v"(t[1][1][1]), "+v"(t[2][0][0]), "+v"(t[2][0][1]),
+                 "+v"(t[2][1][0]), "+v"(t[2][1][1]), "+v"(t[3][0][0]), "+v"(t[3][0][1]), "+v"(t[3][1][0]),
+                 "+v"(t[3][1][1]));
+  typedef __attribute__((ext_vector_type(8))) short short8_t;
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const short8_t a8 = __builtin_shufflevector(t[db][s2][0], t[db][s2][1], 0, 1, 2, 3, 4, 5, 6, 7);
+      st.o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a8), pf[s2], st.o[db], 0,
+                                                         0, 0);
+    }
+}
+
+// Online softmax for decode with a lazy rescale: the running max is only moved (and O, l
+// rescaled) when a tile's max exceeds it by more than 8 in log2 units, so P <= 2^8 stays
+// exact in fp32/bf16 and the 64-accumulator rescale (AGPR read-multiply-write) runs a few
+// times per sequence instead of every 32 keys. v_exp_f32 directly (exp2(-inf) = 0).
+__device__ __forceinline__ void softmax_tile_lazy(f32x16_t& s, State& st, int kbase, int kv_len, float scale_log2,
+                                                  int h) {
+  float mx = -INFINITY;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int key = kbase + (r & 3) + 8 * (r >> 2) + 4 * h;
+    const float v = key < kv_len ? s[r] * scale_log2 : -INFINITY;
+    s[r] = v;
+    mx = fmaxf(mx, v);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  const bool need = mx > st.m + 8.f;
+  if (__any(need)) {
+    const float m_use = need ? mx : st.m;
+    const float alpha = __builtin_amdgcn_exp2f(st.m - m_use);
+    st.l *= alpha;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st.o[db][r] *= alpha;
+    st.m = m_use;
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float p = __builtin_amdgcn_exp2f(s[r] - st.m);
+    s[r] = p;
+    sum += p;
+  }
+  sum += __shfl_xor(sum, 32, 64);
+  st.l += sum;
+}
+
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+// Merge-area LDS traffic in inline asm, for the same reason as pv_lds_swz_v3: hipcc cannot tell
+// these accesses from the in-flight LDS-DMA ring and would drain it (vmcnt(0)) first.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)p);
+}
+__device__ __forceinline__ void lds_st128(uint32_t a, f32x4_t v) {
+  asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ f32x4_t lds_ld128(uint32_t a) {
+  f32x4_t v;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+__device__ __forceinline__ float lds_ld32(uint32_t a) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+__device__ __forceinline__ void lds_st32(uint32_t a, float v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+
+template <int G>
+__global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
+    bf16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters,
+    const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
+    const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ ctx_lens, int num_seqs, int hq, int hkv, float scale_log2, int maxp, int dbg) {
+  constexpr int QI = (G * 256 + 1023) / 1024;  // LDS-DMA instructions for the query rows
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* ml = reinterpret_cast<float*>(smem + 2 * V3_BUF);
+  float* ob = reinterpret_cast<float*>(smem + 2 * V3_BUF + V3_ML);
+  int* ctl = reinterpret_cast<int*>(smem + 2 * V3_BUF + V3_MERGE);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, row = lane & 31;
+  const int pairs = num_seqs * hkv;
+  const int C = max(1, min(maxp, (maxp * pairs + (int)gridDim.x - 1) / (int)gridDim.x));
+  const int np = (maxp + C - 1) / C;
+  const int n_tasks = pairs * np;
+  const int pch = lane & 15;
+
+#pragma unroll 1
+  for (int t = blockIdx.x; t < n_tasks; t += gridDim.x) {
+    const int pair = t % pairs, part = t / pairs;
+    const int seq = pair / hkv, kvh = pair - seq * hkv;
+    const int ctx = __builtin_amdgcn_readfirstlane(ctx_lens[seq]);
+    const int nch = (ctx + DEC_KEYS - 1) / DEC_KEYS;
+    const int c0 = part * C;
+    if (c0 >= nch) continue;  // uniform
+    const int c1 = min(c0 + C, nch);
+    const int* bt = block_tables + (int64_t)seq * bt_stride;
+    const int last_blk = (ctx - 1) >> 4;
+
+    // LDS-DMA chunk c (K and V rows of 128 keys) into buffer b: 16 instructions per lane.
+    auto issue = [&](int c, int b) {
+      if (dbg & 2) return;
+      char* base = smem + b * V3_BUF;
+      // this wave's two 16-key blocks of the chunk; the table row is read speculatively
+      // (clamped to the row, not to the context) so the loads do not wait for ctx
+      const int j0 = c * 8 + 2 * wave;
+      const int e0 = bt[__builtin_amdgcn_readfirstlane(min(j0, bt_stride - 1))];
+      const int e1 = bt[__builtin_amdgcn_readfirstlane(min(j0 + 1, bt_stride - 1))];
+      const int el = j0 + 1 > last_blk ? bt[last_blk] : 0;  // only the context's last chunk needs it
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = (wave * 8 + i) * 4 + (lane >> 4);            // image row = key in chunk
+        const int j = j0 + (i >> 2);
+        const int64_t blk = j <= last_blk ? (i < 4 ? e0 : e1) : el; // past the context: last block
+        const int key = min(c * DEC_KEYS + r, ctx - 1);            // clamp: never read past the context
+        const int64_t roff = ((blk * hkv + kvh) * 16 + (key & 15)) * D;
+        glds16(k_cache + roff + (pch ^ (r & 15)) * 8, base + (wave * 8 + i) * 1024);
+        glds16(v_cache + roff + (pch ^ ((r & 3) << 2)) * 8, base + DEC_KEYS * DEC_ROW + (wave * 8 + i) * 1024);
+      }
+    };
+
+    issue(c0, 0);
+    if (wave == 0 && !(dbg & 2)) {  // the G query rows of this (seq, kv head), 256 B each
+      const bf16_t* qb = q + (int64_t)seq * q_stride + (int64_t)kvh * G * D;
+#pragma unroll
+      for (int i = 0; i < QI; ++i) {
+        const int qr = min(4 * i + (lane >> 4), G - 1);
+        glds16(qb + qr * D + (lane & 15) * 8, smem + V3_CHUNK + i * 1024);
+      }
+    }
+    State st;
+    init_state(st);
+    bf16x8_t qf[8];
+#pragma unroll 1
+    for (int c = c0; c < c1; ++c) {
+      const int b = (c - c0) & 1;
+      if (c + 1 < c1) {
+        issue(c + 1, b ^ 1);
+        wait_vm<16>();  // chunk c (and the query rows) landed; chunk c+1 stays in flight
+      } else {
+        wait_vm<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      const char* base = smem + b * V3_BUF;
+      if (c == c0) {
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+          qf[kk] = row < G ? as_frag(*reinterpret_cast<const uint4*>(smem + V3_CHUNK + row * 256 + (2 * kk + h) * 16))
+                           : zero_frag();
+      }
+      if (!(dbg & 1)) {
+        const int kb = c * DEC_KEYS + 32 * wave;  // keys >= ctx: clamped rows, masked to -inf
+        f32x16_t s = qk_lds_swz(base + 32 * wave * DEC_ROW, qf, lane);
+        softmax_tile_lazy(s, st, kb, ctx, scale_log2, h);
+        pv_lds_swz_v3(base + DEC_KEYS * DEC_ROW + 32 * wave * DEC_ROW, s, st, lane);
+      }
+      lds_barrier();  // buffer b is refilled by the next iteration
+    }
+    if (dbg & 32) continue;
+
+    // merge the 4 waves' (m, l, O) through LDS
+    if (row < G) {
+      if (h == 0) {
+        lds_st32(lds_addr(ml + (wave * 32 + row) * 2 + 0), st.m);
+        lds_st32(lds_addr(ml + (wave * 32 + row) * 2 + 1), st.l);
+      }
+      const uint32_t o = lds_addr(ob + (wave * G + row) * D);
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4)
+          lds_st128(o + 4 * (32 * db + 8 * g4 + 4 * h),
+                    f32x4_t{st.o[db][4 * g4], st.o[db][4 * g4 + 1], st.o[db][4 * g4 + 2], st.o[db][4 * g4 + 3]});
+    }
+    lds_barrier();
+    const int nparts = (nch + C - 1) / C;  // parts of THIS pair
+    for (int e = tid; e < G * (D / 4); e += 256) {
+      const int r = e / (D / 4), d = 4 * (e % (D / 4));
+      float mw[4], lw[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        mw[w] = lds_ld32(lds_addr(ml + (w * 32 + r) * 2));
+        lw[w] = lds_ld32(lds_addr(ml + (w * 32 + r) * 2 + 1));
+      }
+      float M = NEG_BIG;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) M = fmaxf(M, mw[w]);
+      float L = 0.f;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float f = exp2f(mw[w] - M);
+        L += f * lw[w];
+        const f32x4_t v = lds_ld128(lds_addr(ob + (w * G + r) * D + d));
+        acc.x += f * v.x;
+        acc.y += f * v.y;
+        acc.z += f * v.z;
+        acc.w += f * v.w;
+      }
+      const int head = kvh * G + r;
+      if (nparts == 1) {
+        const float inv = L > 0.f ? 1.f / L : 0.f;
+        uint2 pk;
+        pk.x = pack2(acc.x * inv, acc.y * inv);
+        pk.y = pack2(acc.z * inv, acc.w * inv);
+        *reinterpret_cast<uint2*>(out + ((int64_t)seq * hq + head) * D + d) = pk;
+      } else {
+        const int64_t slot = ((int64_t)seq * hq + head) * maxp + part;
+        __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(part_o, 0, 0x7fffffff, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, acc),
+                                               ro, (int)(slot * D + d) * 4, 0, 16);
+        if (d == 0) {
+          __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(part_ml, 0, 0x7fffffff, 0x00020000);
+          const float2 mlv = make_float2(M, L);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, mlv),
+                                                rm, (int)(slot * 2) * 4, 0, 16);
+        }
+      }
+    }
+    if (nparts > 1) {
+      wait_vm<0>();  // this wave's write-through partial stores are done
+      lds_barrier();
+      if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(counters + pair, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ctl[1] = old == nparts - 1;
+      }
+      lds_barrier();
+      if (ctl[1]) {  // last arriver: merge every part of this pair
+        __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(part_o, 0, 0x7fffffff, 0x00020000);
+        __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(part_ml, 0, 0x7fffffff, 0x00020000);
+        for (int e = tid; e < G * (D / 4); e += 256) {
+          const int r = e / (D / 4), d = 4 * (e % (D / 4));
+          const int head = kvh * G + r;
+          const int64_t s0 = ((int64_t)seq * hq + head) * maxp;
+          float M = NEG_BIG, L = 0.f;
+          float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+          for (int p = 0; p < nparts; ++p) {
+            const auto mv =
+                __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rm, (int)((s0 + p) * 2) * 4, 0, 16));
+            const auto ov = __builtin_bit_cast(
+                float4, __builtin_amdgcn_raw_buffer_load_b128(ro, (int)((s0 + p) * D + d) * 4, 0, 16));
+            const float Mn = fmaxf(M, mv.x);
+            const float a = exp2f(M - Mn), bb = exp2f(mv.x - Mn);
+            L = L * a + mv.y * bb;
+            acc.x = acc.x * a + ov.x * bb;
+            acc.y = acc.y * a + ov.y * bb;
+            acc.z = acc.z * a + ov.z * bb;
+            acc.w = acc.w * a + ov.w * bb;
+            M = Mn;
+          }
+          const float inv = L > 0.f ? 1.f / L : 0.f;
+          uint2 pk;
+          pk.x = pack2(acc.x * inv, acc.y * inv);
+          pk.y = pack2(acc.z * inv, acc.w * inv);
+          *reinterpret_cast<uint2*>(out + ((int64_t)seq * hq + head) * D + d) = pk;
+        }
+        if (tid == 0) __hip_atomic_store(counters + pair, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    lds_barrier();  // merge area and buffers are reused by the next task
+  }
+}
+
+
 // grid = (num_seqs, hq); block = 128 (one lane per head-dim element).
 __global__ void __launch_bounds__(128) attn_decode_reduce_kernel(bf16_t* __restrict__ out,
                                                                  const float* __restrict__ part_o,
@@ -491,13 +835,49 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
   return hipGetLastError();
 }
 
-hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, const bf16_t* q, int64_t q_stride,
-                              const bf16_t* k_cache, const bf16_t* v_cache, const int* block_tables, int bt_stride,
-                              const int* ctx_lens, int num_seqs, int max_ctx, int hq, int hkv, int head_dim,
-                              int block_size, float scale, hipStream_t s) {
+static int num_cus() {
+  static int n[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (n[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    n[dev] = v;
+  }
+  return n[dev];
+}
+
+hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* counters, const bf16_t* q,
+                              int64_t q_stride, const bf16_t* k_cache, const bf16_t* v_cache, const int* block_tables,
+                              int bt_stride, const int* ctx_lens, int num_seqs, int max_ctx, int hq, int hkv,
+                              int head_dim, int block_size, float scale, hipStream_t s) {
   if (num_seqs == 0) return hipSuccess;
   if (head_dim != D || hq % hkv) return hipErrorInvalidValue;
   const int G = hq / hkv;
+  const int maxp3 = (max_ctx + DEC_KEYS - 1) / DEC_KEYS;
+  const int64_t part_bytes = (int64_t)num_seqs * hq * maxp3 * D * 4;
+  if (counters != nullptr && block_size == 16 && (G == 1 || G == 2 || G == 4 || G == 8) &&
+      part_bytes < ((int64_t)1 << 31)) {
+    const float sl2 = scale * 1.4426950408889634f;
+    const int tasks = num_seqs * hkv * maxp3;
+    const int ncu = num_cus();
+    static const int dbg = getenv("DIE_ATTN_DBG") ? atoi(getenv("DIE_ATTN_DBG")) : 0;  // perf experiments only
+    dim3 grid(tasks < ncu ? tasks : ncu), block(256);
+#define DIE_D3(GG)                                                                                           \
+  case GG:                                                                                                   \
+    hipLaunchKernelGGL(attn_decode_v3_kernel<GG>, grid, block, V3_LDS, s, out, part_o, part_ml, counters, q, \
+                       q_stride, k_cache, v_cache, block_tables, bt_stride, ctx_lens, num_seqs, hq, hkv, sl2,    \
+                       maxp3, dbg);                                                                          \
+    break;
+    switch (G) {
+      DIE_D3(1)
+      DIE_D3(2)
+      DIE_D3(4)
+      DIE_D3(8)
+    }
+#undef DIE_D3
+    return hipGetLastError();
+  }
   if (G > 32 || G * D * 4 * 4 + 4 * 32 * 2 * 4 > DEC_LDS) return hipErrorInvalidValue;
   const float sl2 = scale * 1.4426950408889634f;
   const int maxp = (max_ctx + DEC_KEYS - 1) / DEC_KEYS;

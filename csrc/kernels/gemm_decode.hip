@@ -38,8 +38,9 @@ typedef __attribute__((address_space(1))) const void global_cvoid;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f4;
 
+template <int AUX = 0>
 __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((global_cvoid*)src, (lds_void*)lds_wave_base, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds((global_cvoid*)src, (lds_void*)lds_wave_base, 16, 0, AUX);
 }
 
 template <int N>
@@ -54,7 +55,9 @@ using namespace gd;
 // EPI 0: bf16 Y = XW^T. EPI 1: bf16 Y[:, j] = silu(g_j) * u_j, W = [gate(N_out rows); up(N_out rows)].
 // EPI 2: fp32 slab Y[blockIdx.y][m][n] (split-K partial).
 // WR = weight rows in the workgroup's image; output columns per workgroup = WR (EPI 0/2) or WR/2 (EPI 1).
-template <int WR, int EPI, int S>
+// NT: weight pieces are loaded non-temporal (aux = 2): each weight byte is read once per step by one CU,
+// so it should not displace the activations / KV in L2 and MALL (MI355X_MICROARCH.md "nt-weights").
+template <int WR, int EPI, int S, bool NT>
 __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv, int64_t ldy,
                                                           const bf16_t* __restrict__ X, int64_t ldx,
                                                           const bf16_t* __restrict__ W, int M, int N_out, int K) {
@@ -74,6 +77,7 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
 
   // Per-lane source rows for this wave's DMA pieces (fixed across chunks).
   const bf16_t* src[PER_WAVE];
+  bool isw[PER_WAVE];
 #pragma unroll
   for (int p = 0; p < PER_WAVE; ++p) {
     const int piece = wave + 4 * p;
@@ -88,11 +92,18 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
       base = X + (int64_t)min(row - WR, M - 1) * ldx;
     }
     src[p] = base + k0 + lch * 8;
+    isw[p] = row < WR;
   }
   auto issue = [&](int c) {
     char* slot = smem + (c % S) * SLOT;
 #pragma unroll
-    for (int p = 0; p < PER_WAVE; ++p) glds16(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);
+    for (int p = 0; p < PER_WAVE; ++p) {
+      // piece p of a wave is all-weight or all-activation (2 rows per piece, WR even): wave-uniform branch
+      if (NT && isw[p])
+        glds16<2>(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);
+      else
+        glds16<0>(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);
+    }
   };
 
   f4 acc[2][NTILE];
@@ -177,30 +188,34 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
 
 template <int WR, int EPI, int S>
 static hipError_t launch_gd(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N_out,
-                            int K, int sk, hipStream_t s) {
+                            int K, int sk, bool nt, hipStream_t s) {
   constexpr int NO = EPI == 1 ? WR / 2 : WR;
   if (N_out % NO || (K / sk) % KC || K % sk) return hipErrorInvalidValue;
   const size_t lds = (size_t)S * (WR + MR) * ROWB;
-  hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S>), dim3(N_out / NO, sk), dim3(NTH), lds, s, Y, ldy, X, ldx, W,
-                     M, N_out, K);
+  if (nt)
+    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, true>), dim3(N_out / NO, sk), dim3(NTH), lds, s, Y, ldy, X,
+                       ldx, W, M, N_out, K);
+  else
+    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, false>), dim3(N_out / NO, sk), dim3(NTH), lds, s, Y, ldy, X,
+                       ldx, W, M, N_out, K);
   return hipGetLastError();
 }
 
 // mode 0: bf16 Y [M, N]; mode 1: bf16 silu(gate)*up, W = [2N, K]; mode 2: fp32 slabs [sk, M, N].
 // wr: weight rows per workgroup (32 or 64).
 hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,
-                              int K, int mode, int wr, int sk, hipStream_t s) {
+                              int K, int mode, int wr, int sk, bool nt, hipStream_t s) {
   if (M <= 0) return hipSuccess;
   if (M > MR || sk < 1 || (mode != 2 && sk != 1)) return hipErrorInvalidValue;
   if (wr == 32) {
-    if (mode == 0) return launch_gd<32, 0, 4>(Y, ldy, X, ldx, W, M, N, K, sk, s);
-    if (mode == 1) return launch_gd<32, 1, 4>(Y, ldy, X, ldx, W, M, N, K, sk, s);
-    return launch_gd<32, 2, 4>(Y, ldy, X, ldx, W, M, N, K, sk, s);
+    if (mode == 0) return launch_gd<32, 0, 4>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
+    if (mode == 1) return launch_gd<32, 1, 4>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
+    return launch_gd<32, 2, 4>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
   }
   if (wr == 64) {
-    if (mode == 0) return launch_gd<64, 0, 3>(Y, ldy, X, ldx, W, M, N, K, sk, s);
-    if (mode == 1) return launch_gd<64, 1, 3>(Y, ldy, X, ldx, W, M, N, K, sk, s);
-    return launch_gd<64, 2, 3>(Y, ldy, X, ldx, W, M, N, K, sk, s);
+    if (mode == 0) return launch_gd<64, 0, 3>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
+    if (mode == 1) return launch_gd<64, 1, 3>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
+    return launch_gd<64, 2, 3>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
   }
   return hipErrorInvalidValue;
 }

@@ -28,10 +28,10 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
                                const bf16_t* v_cache, const int* block_tables, int bt_stride, const int* cu_q,
                                const int* ctx_lens, int num_seqs, int max_q_len, int hq, int hkv, int head_dim,
                                int block_size, float scale, hipStream_t s);
-hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, const bf16_t* q, int64_t q_stride,
-                              const bf16_t* k_cache, const bf16_t* v_cache, const int* block_tables, int bt_stride,
-                              const int* ctx_lens, int num_seqs, int max_ctx, int hq, int hkv, int head_dim,
-                              int block_size, float scale, hipStream_t s);
+hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* counters, const bf16_t* q,
+                              int64_t q_stride, const bf16_t* k_cache, const bf16_t* v_cache, const int* block_tables,
+                              int bt_stride, const int* ctx_lens, int num_seqs, int max_ctx, int hq, int hkv,
+                              int head_dim, int block_size, float scale, hipStream_t s);
 int attn_decode_max_partials(int max_ctx);
 
 hipError_t launch_sample(int64_t* out, const bf16_t* logits, int64_t stride, int rows, int vocab,
@@ -48,7 +48,7 @@ hipError_t launch_moe_grouped_gemm(bf16_t* Y, const bf16_t* X, const bf16_t* W, 
                                    int E, int N, int K, hipStream_t s);
 
 hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,
-                              int K, int mode, int wr, int sk, hipStream_t s);
+                              int K, int mode, int wr, int sk, bool nt, hipStream_t s);
 // consumers of fp32 split-K slabs [sk][rows][width]
 hipError_t launch_fused_add_rms_norm_slab(bf16_t* out, const float* slab, int sk, bf16_t* residual, const bf16_t* w,
                                           float eps, int rows, int hidden, int64_t out_stride, hipStream_t s);

@@ -46,6 +46,7 @@ class AttnMetadata:
     max_ctx: int = 0                # decode grid bound (static under hipGraph)
     part_o: Optional[torch.Tensor] = None
     part_ml: Optional[torch.Tensor] = None
+    attn_cnt: Optional[torch.Tensor] = None  # decode attention merge tickets (int32, zeroed once)
 
 
 class LayerWeights:
@@ -240,7 +241,8 @@ class CausalLM:
                                         meta.max_q_len, hq, hkv, self.scale)
             else:
                 attn = ops.attn_decode(q, k_cache, v_cache, meta.block_tables, meta.ctx_lens, meta.max_ctx, hq,
-                                       hkv, self.scale, part_o=meta.part_o, part_ml=meta.part_ml)
+                                       hkv, self.scale, part_o=meta.part_o, part_ml=meta.part_ml,
+                                       counters=meta.attn_cnt)
             o = self.tp.all_reduce(ops.linear(attn, lw.o))
             x = ops.fused_add_rms_norm(o, residual, lw.ln2, eps)
             if a.is_moe:
@@ -278,7 +280,8 @@ class CausalLM:
                                         meta.max_q_len, hq, hkv, self.scale)
             else:
                 attn = ops.attn_decode(q, k_cache, v_cache, meta.block_tables, meta.ctx_lens, meta.max_ctx, hq,
-                                       hkv, self.scale, part_o=meta.part_o, part_ml=meta.part_ml)
+                                       hkv, self.scale, part_o=meta.part_o, part_ml=meta.part_ml,
+                                       counters=meta.attn_cnt)
             x = ops.fused_add_rms_norm_slab(ops.linear_slab(attn, lw.o), residual, lw.ln2, eps)
             slab = ops.linear_slab(ops.linear_silu_mul(x, lw.gate_up), lw.down)
         return ops.fused_add_rms_norm_slab(slab, residual, self.norm, eps)

@@ -95,7 +95,11 @@ def decode_partials(max_ctx: int) -> int:
 
 def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, max_ctx: int, hq: int, hkv: int, scale: float,
                 part_o: Optional[torch.Tensor] = None, part_ml: Optional[torch.Tensor] = None,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, counters: Optional[torch.Tensor] = None,
+                merge_kernel: bool = False) -> torch.Tensor:
+    """Paged decode attention. `counters` (int32, >= num_seqs * hkv, zeroed once) are the
+    per-(sequence, kv head) tickets of the self-merging kernel; they are re-armed by the kernel,
+    so a runner allocates them once. merge_kernel=True forces the two-launch path."""
     if not q.is_cuda:
         n = ctx_lens.numel()
         cu = torch.arange(n + 1, dtype=torch.int32)
@@ -107,7 +111,12 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, max_ctx: int, hq: i
         maxp = decode_partials(max_ctx)
         part_o = torch.empty(n * hq * maxp * 128, dtype=torch.float32, device=q.device)
         part_ml = torch.empty(n * hq * maxp * 2, dtype=torch.float32, device=q.device)
-    _kern().attn_decode(out, part_o, part_ml, q, k_cache, v_cache, block_tables, ctx_lens, max_ctx, hq, hkv, scale)
+    if merge_kernel:
+        counters = torch.empty(0, dtype=torch.int32, device=q.device)
+    elif counters is None:
+        counters = torch.zeros(n * hkv, dtype=torch.int32, device=q.device)
+    _kern().attn_decode(out, part_o, part_ml, counters, q, k_cache, v_cache, block_tables, ctx_lens, max_ctx, hq,
+                        hkv, scale)
     return out
 
 
@@ -160,8 +169,11 @@ def _decode_gemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
             and w.shape[0] % 16 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0)
 
 
+DECODE_GEMM_NT = True  # non-temporal weight loads (read-once stream)
+
+
 def gemm_decode(x: torch.Tensor, w: torch.Tensor, mode: int = 0, wr: int = 64, sk: int = 1,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, nt: Optional[bool] = None) -> torch.Tensor:
     """Raw access to the decode GEMM kernel (see csrc/kernels/gemm_decode.hip).
     mode 0: bf16 x@w^T; mode 1: bf16 silu(gate)*up (w = [gate; up]);
     mode 2: fp32 split-K slabs [sk, M, N]."""
@@ -172,7 +184,7 @@ def gemm_decode(x: torch.Tensor, w: torch.Tensor, mode: int = 0, wr: int = 64, s
             out = torch.empty(sk, m, n, dtype=torch.float32, device=x.device)
         else:
             out = torch.empty(m, n, dtype=x.dtype, device=x.device)
-    _kern().gemm_decode(out, x, w, mode, wr, sk)
+    _kern().gemm_decode(out, x, w, mode, wr, sk, DECODE_GEMM_NT if nt is None else nt)
     return out
 
 

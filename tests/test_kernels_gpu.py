@@ -119,19 +119,40 @@ def test_attn_prefill(dev, g):
     close(out, r, atol=2.5e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("g,bs", [(4, 16), (8, 16), (4, 32), (1, 16)])
-def test_attn_decode(dev, g, bs):
+@pytest.mark.parametrize("g,bs,merge", [(4, 16, False), (8, 16, False), (4, 32, False), (1, 16, False),
+                                         (2, 16, False), (4, 16, True)])
+def test_attn_decode(dev, g, bs, merge):
     hkv = 8 if g == 4 else (1 if g == 8 else 4)
-    ctxs = [1, 17, 64, 65, 300, 1000, 2049]
+    ctxs = [1, 17, 64, 65, 300, 1000, 2049]   # one-part pairs (direct output) and multi-part pairs (ticket merge)
     q, kc, vc, bt, _, ctx, hq = _make_seqs([1] * len(ctxs), ctxs, hkv, bs, dev, g)
     scale = 1 / math.sqrt(128)
     max_ctx = 4096
     bt_wide = torch.zeros(bt.shape[0], max_ctx // bs, dtype=torch.int32, device=dev)
     bt_wide[:, : bt.shape[1]] = bt
-    out = ops.attn_decode(q, kc, vc, bt_wide, ctx, max_ctx, hq, hkv, scale)
+    cnt = torch.zeros(len(ctxs) * hkv, dtype=torch.int32, device=dev)
+    out = ops.attn_decode(q, kc, vc, bt_wide, ctx, max_ctx, hq, hkv, scale, counters=cnt, merge_kernel=merge)
     cu = torch.arange(len(ctxs) + 1, dtype=torch.int32, device=dev)
     r = ref.attention(q, kc, vc, bt, cu, ctx, hq, hkv, scale).reshape(q.shape[0], -1)
     close(out, r, atol=2.5e-2, rtol=2e-2)
+    # the merge tickets are re-armed: a second launch on the same counters gives the same answer
+    out2 = ops.attn_decode(q, kc, vc, bt_wide, ctx, max_ctx, hq, hkv, scale, counters=cnt, merge_kernel=merge)
+    assert torch.equal(out, out2)
+    assert int(cnt.abs().sum()) == 0
+
+
+def test_attn_decode_batch32(dev):
+    """The serving shape: 32 sequences x 8 kv heads (one task per CU, no partials), plus a
+    single long sequence (every CU on one pair, all-partials merge)."""
+    hkv, g = 8, 4
+    scale = 1 / math.sqrt(128)
+    for ctxs in ([512 + 7 * i for i in range(32)], [8000]):
+        q, kc, vc, bt, _, ctx, hq = _make_seqs([1] * len(ctxs), ctxs, hkv, 16, dev, g)
+        bt_wide = torch.zeros(bt.shape[0], 8192 // 16, dtype=torch.int32, device=dev)
+        bt_wide[:, : bt.shape[1]] = bt
+        out = ops.attn_decode(q, kc, vc, bt_wide, ctx, 8192, hq, hkv, scale)
+        cu = torch.arange(len(ctxs) + 1, dtype=torch.int32, device=dev)
+        r = ref.attention(q, kc, vc, bt, cu, ctx, hq, hkv, scale).reshape(q.shape[0], -1)
+        close(out, r, atol=2.5e-2, rtol=2e-2)
 
 
 def test_attn_softmax_spike(dev):
