@@ -65,7 +65,8 @@ def main():
             res.append(("hipblaslt+silu", timeit(lambda w: ops.silu_and_mul(torch.nn.functional.linear(x, w)), ws)))
         else:
             res.append(("hipblaslt", timeit(lambda w: torch.nn.functional.linear(x, w), ws)))
-        for wr in (32, 64):
+        for wr in (32, 48, 64, 96, 112, 128):
+            kc = 128 if wr >= 96 else 256
             if silu:
                 if n % (wr // 2) == 0:
                     res.append((f"gd_silu_wr{wr}", timeit(lambda w: ops.gemm_decode(x, w, 1, wr, 1), ws)))
@@ -73,7 +74,7 @@ def main():
             if n % wr == 0:
                 res.append((f"gd_bf16_wr{wr}", timeit(lambda w: ops.gemm_decode(x, w, 0, wr, 1), ws)))
             for sk in (2, 4, 8):
-                if k % (256 * sk) == 0 and n % wr == 0:
+                if k % (kc * sk) == 0 and n % wr == 0 and (n // wr) * sk <= 1024:
                     res.append((f"gd_slab_wr{wr}_sk{sk}", timeit(lambda w: ops.gemm_decode(x, w, 2, wr, sk), ws)))
         for v, us in res:
             print(json.dumps({"shape": name, "M": m, "N": n, "K": k, "variant": v, "us": round(us, 2),

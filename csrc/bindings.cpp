@@ -292,8 +292,10 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
   check_rows(x, "x");
   const int64_t M = x.size(0), K = x.size(1);
   TORCH_CHECK(M >= 1 && M <= 32, "gemm_decode: 1 <= M <= 32");
-  TORCH_CHECK(wr == 32 || wr == 64, "wr must be 32 or 64");
-  TORCH_CHECK(K % (256 * sk) == 0, "gemm_decode: K must be a multiple of 256*sk");
+  TORCH_CHECK(wr == 32 || wr == 48 || wr == 64 || wr == 96 || wr == 112 || wr == 128,
+              "wr must be one of 32, 48, 64, 96, 112, 128");
+  const int64_t kc = wr >= 96 ? 128 : 256;
+  TORCH_CHECK(K % (kc * sk) == 0, "gemm_decode: K must be a multiple of the K slot (256, or 128 for wr >= 96) * sk");
   int64_t N, ldy;
   if (mode == 2) {
     DIE_CHECK_DTYPE(y, at::kFloat);

@@ -28,8 +28,6 @@
 namespace die {
 namespace gd {
 
-constexpr int KC = 256;             // K elements per chunk
-constexpr int ROWB = KC * 2;        // bytes per image row (512)
 constexpr int MR = 32;              // activation rows (max M)
 constexpr int NTH = 256;            // threads per workgroup
 
@@ -55,18 +53,23 @@ using namespace gd;
 // EPI 0: bf16 Y = XW^T. EPI 1: bf16 Y[:, j] = silu(g_j) * u_j, W = [gate(N_out rows); up(N_out rows)].
 // EPI 2: fp32 slab Y[blockIdx.y][m][n] (split-K partial).
 // WR = weight rows in the workgroup's image; output columns per workgroup = WR (EPI 0/2) or WR/2 (EPI 1).
+// KC = K elements per ring slot (256, or 128 for the wide tiles so that 4 slots fit in LDS).
 // NT: weight pieces are loaded non-temporal (aux = 2): each weight byte is read once per step by one CU,
 // so it should not displace the activations / KV in L2 and MALL (MI355X_MICROARCH.md "nt-weights").
-template <int WR, int EPI, int S, bool NT>
+template <int WR, int EPI, int S, bool NT, int KC>
 __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv, int64_t ldy,
                                                           const bf16_t* __restrict__ X, int64_t ldx,
                                                           const bf16_t* __restrict__ W, int M, int N_out, int K) {
+  constexpr int ROWB = KC * 2;                 // bytes per image row
+  constexpr int CPR = KC / 8;                  // 16-byte chunks per row (32 or 16)
+  constexpr int RPP = 64 / CPR;                // rows per 1-KiB DMA piece (2 or 4)
   constexpr int NO = EPI == 1 ? WR / 2 : WR;   // output columns per workgroup
   constexpr int SLOT = (WR + MR) * ROWB;       // bytes per ring slot
-  constexpr int INSTR = (WR + MR) / 2;         // 1-KiB DMA pieces per chunk (2 rows each)
+  constexpr int INSTR = (WR + MR) / RPP;       // 1-KiB DMA pieces per chunk
   constexpr int PER_WAVE = INSTR / 4;          // pieces issued per wave per chunk
   constexpr int NTILE = WR / 16;               // 16-column MFMA tiles
-  static_assert(INSTR % 4 == 0, "pieces must split over 4 waves");
+  constexpr int KSW = KC / 128;                // 32-deep k-steps per wave per chunk
+  static_assert(INSTR % 4 == 0 && WR % RPP == 0, "pieces must split over 4 waves, W/X pieces unmixed");
   static_assert((S - 1) * PER_WAVE <= 63, "vmcnt field is 6 bits");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -81,8 +84,8 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
 #pragma unroll
   for (int p = 0; p < PER_WAVE; ++p) {
     const int piece = wave + 4 * p;
-    const int row = 2 * piece + (lane >> 5);  // image row: [0, WR) = W, [WR, WR+32) = X
-    const int lch = (lane & 31) ^ (row & 15);
+    const int row = RPP * piece + lane / CPR;  // image row: [0, WR) = W, [WR, WR+32) = X
+    const int lch = (lane % CPR) ^ (row & 15);
     const bf16_t* base;
     if (row < WR) {
       int grow = n0 + row;
@@ -98,7 +101,7 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
     char* slot = smem + (c % S) * SLOT;
 #pragma unroll
     for (int p = 0; p < PER_WAVE; ++p) {
-      // piece p of a wave is all-weight or all-activation (2 rows per piece, WR even): wave-uniform branch
+      // a piece is all-weight or all-activation rows: wave-uniform branch
       if (NT && isw[p])
         glds16<2>(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);
       else
@@ -129,10 +132,10 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
     __builtin_amdgcn_s_barrier();
     const char* slot = smem + (c % S) * SLOT;
     const char* ximg = slot + WR * ROWB;
-    // 8 k-steps of 32 per chunk, 2 per wave
+    // KC/32 k-steps of 32 per chunk, KSW per wave
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int ks = wave * 2 + kk;
+    for (int kk = 0; kk < KSW; ++kk) {
+      const int ks = wave * KSW + kk;
       const int lch = 4 * ks + kg;
       bf16x8 a[2], b[NTILE];
 #pragma unroll
@@ -186,38 +189,46 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
   }
 }
 
-template <int WR, int EPI, int S>
+template <int WR, int EPI, int S, int KC>
 static hipError_t launch_gd(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N_out,
                             int K, int sk, bool nt, hipStream_t s) {
   constexpr int NO = EPI == 1 ? WR / 2 : WR;
-  if (N_out % NO || (K / sk) % KC || K % sk) return hipErrorInvalidValue;
-  const size_t lds = (size_t)S * (WR + MR) * ROWB;
+  if (N_out % NO || K % sk || (K / sk) % KC) return hipErrorInvalidValue;
+  const size_t lds = (size_t)S * (WR + MR) * KC * 2;
   if (nt)
-    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, true>), dim3(N_out / NO, sk), dim3(NTH), lds, s, Y, ldy, X,
-                       ldx, W, M, N_out, K);
+    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, true, KC>), dim3(N_out / NO, sk), dim3(NTH), lds, s, Y, ldy,
+                       X, ldx, W, M, N_out, K);
   else
-    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, false>), dim3(N_out / NO, sk), dim3(NTH), lds, s, Y, ldy, X,
-                       ldx, W, M, N_out, K);
+    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, false, KC>), dim3(N_out / NO, sk), dim3(NTH), lds, s, Y, ldy,
+                       X, ldx, W, M, N_out, K);
   return hipGetLastError();
 }
 
+template <int WR, int S, int KC>
+static hipError_t launch_modes(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,
+                               int K, int mode, int sk, bool nt, hipStream_t s) {
+  if (mode == 0) return launch_gd<WR, 0, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
+  if (mode == 1) return launch_gd<WR, 1, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
+  return launch_gd<WR, 2, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
+}
+
 // mode 0: bf16 Y [M, N]; mode 1: bf16 silu(gate)*up, W = [2N, K]; mode 2: fp32 slabs [sk, M, N].
-// wr: weight rows per workgroup (32 or 64).
+// wr: weight rows per workgroup: 32 / 48 / 64 (256-wide K slots) or 96 / 112 / 128 (128-wide K slots),
+// so that (N / columns) * sk can be made a multiple of the CU count for the model's shapes
+// (e.g. 8B gate/up: 14336 / 56 = 256 workgroups at wr = 112).
 hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,
                               int K, int mode, int wr, int sk, bool nt, hipStream_t s) {
   if (M <= 0) return hipSuccess;
   if (M > MR || sk < 1 || (mode != 2 && sk != 1)) return hipErrorInvalidValue;
-  if (wr == 32) {
-    if (mode == 0) return launch_gd<32, 0, 4>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
-    if (mode == 1) return launch_gd<32, 1, 4>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
-    return launch_gd<32, 2, 4>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
+  switch (wr) {
+    case 32: return launch_modes<32, 4, 256>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, s);
+    case 48: return launch_modes<48, 3, 256>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, s);
+    case 64: return launch_modes<64, 3, 256>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, s);
+    case 96: return launch_modes<96, 4, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, s);
+    case 112: return launch_modes<112, 4, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, s);
+    case 128: return launch_modes<128, 3, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, s);
+    default: return hipErrorInvalidValue;
   }
-  if (wr == 64) {
-    if (mode == 0) return launch_gd<64, 0, 3>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
-    if (mode == 1) return launch_gd<64, 1, 3>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
-    return launch_gd<64, 2, 3>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
-  }
-  return hipErrorInvalidValue;
 }
 
 }  // namespace die

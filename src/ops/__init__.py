@@ -189,18 +189,20 @@ def gemm_decode(x: torch.Tensor, w: torch.Tensor, mode: int = 0, wr: int = 64, s
 
 
 # (N, K, mode) -> (wr, sk), measured with bench/micro_gemm_decode.py on MI355X (cold
-# weights, M = 32; profiles/micro_gemm_decode_m32_r1.jsonl). Fastest configs put
-# ~(N/wr)*sk ≈ 256 workgroups (one per CU) on the chip.
+# weights, M = 32, nt weight loads; profiles/micro_gemm_decode_m32_r1b.jsonl). Fastest
+# configs put (N/cols)*sk at (a multiple of) ~256 workgroups, one per CU.
 DECODE_GEMM_CFG = {
-    (6144, 4096, 2): (64, 2),    # Llama-3-8B / Mixtral qkv  (13.5 us vs hipBLASLt 15.3)
-    (4096, 4096, 2): (64, 4),    # 8B o_proj                  (9.8 vs 13.3)
-    (14336, 4096, 1): (64, 1),   # 8B gate/up + SiLU          (49.2 vs 55.1)
-    (4096, 14336, 2): (64, 4),   # 8B down_proj               (24.5 vs 33.9)
-    (1280, 8192, 2): (64, 8),    # 70B TP=8 qkv               (8.3 vs 15.3)
-    (8192, 1024, 0): (32, 1),    # 70B TP=8 o_proj            (6.3 vs 11.4)
-    (3584, 8192, 1): (32, 1),    # 70B TP=8 gate/up + SiLU    (27.5 vs 29.4)
-    (8192, 3584, 0): (32, 1),    # 70B TP=8 down_proj         (14.8 vs 15.9)
+    (6144, 4096, 2): (48, 2),      # Llama-3-8B / Mixtral qkv  (11.6 us vs hipBLASLt 15.3)
+    (4096, 4096, 2): (64, 4),      # 8B o_proj                  (9.3 vs 13.3)
+    (14336, 4096, 1): (112, 1),    # 8B gate/up + SiLU          (46.4 vs 53.4)
+    (4096, 14336, 2): (64, 4),     # 8B down_proj               (22.2 vs 33.9)
+    (128256, 4096, 0): (64, 1),    # Llama-3 LM head            (177 vs 190, 5.9 TB/s)
+    (1280, 8192, 2): (64, 8),      # 70B TP=8 qkv               (7.8 vs 15.3)
+    (8192, 1024, 0): (32, 1),      # 70B TP=8 o_proj            (6.3 vs 11.4)
+    (3584, 8192, 1): (32, 1),      # 70B TP=8 gate/up + SiLU    (26.6 vs 29.7)
+    (8192, 3584, 0): (32, 1),      # 70B TP=8 down_proj         (13.3 vs 15.6)
 }
+DECODE_GEMM_MAX_N = 262144
 
 
 def _cfg_for(n: int, k: int, mode: int):
@@ -224,14 +226,13 @@ def _cfg_for(n: int, k: int, mode: int):
 
 
 def decode_slab_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    return _decode_gemm_ok(x, w) and w.shape[0] % 32 == 0 and w.shape[0] <= 32768
+    return _decode_gemm_ok(x, w) and w.shape[0] % 32 == 0 and w.shape[0] <= DECODE_GEMM_MAX_N
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = x @ w^T. Decode-sized M (<= 32 rows) runs on the weight-streaming
     gfx950 kernel (gemm_decode.hip); larger M goes to hipBLASLt."""
-    # the LM head (N ~ 128K) streams at the same rate on hipBLASLt: keep it there
-    if _decode_gemm_ok(x, w) and w.shape[0] % 32 == 0 and w.shape[0] <= 32768:
+    if _decode_gemm_ok(x, w) and w.shape[0] % 32 == 0 and w.shape[0] <= DECODE_GEMM_MAX_N:
         wr, _ = _cfg_for(w.shape[0], x.shape[1], 0)
         return gemm_decode(x, w, 0, wr, 1, out)
     return torch.nn.functional.linear(x, w, out=out) if out is not None else torch.nn.functional.linear(x, w)
