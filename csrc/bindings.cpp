@@ -163,7 +163,69 @@ void attn_decode(Tensor out, Tensor part_o, Tensor part_ml, Tensor counters, Ten
   DIE_HIP(die::launch_attn_decode(bf(out), part_o.data_ptr<float>(), part_ml.data_ptr<float>(), cnt, bf(q), q.stride(0),
                                   bf(k_cache), bf(v_cache), block_tables.data_ptr<int>(), (int)block_tables.size(1),
                                   ctx_lens.data_ptr<int>(), (int)nseq, (int)max_ctx, (int)hq, (int)hkv, (int)D,
-                                  (int)k_cache.size(2), (float)scale, cur_stream()));
+                                  (int)k_cache.size(2), (float)scale, nullptr, cur_stream()));
+}
+
+// Decode attention with the fused prologue: q / new K,V built from the qkv projection's
+// fp32 split-K slabs [sk, M, (hq+2hkv)*128] (RMSNorm row scale from ssp [T, 32], RoPE from
+// cos_sin [max_pos, 128] at positions [M]); the new K/V go to the paged cache at slot_mapping.
+void attn_decode_fused(Tensor out, Tensor part_o, Tensor part_ml, Tensor counters, Tensor slab, Tensor ssp,
+                       Tensor positions, Tensor cos_sin, Tensor slot_mapping, Tensor k_cache, Tensor v_cache,
+                       Tensor block_tables, Tensor ctx_lens, int64_t max_ctx, int64_t hq, int64_t hkv, double scale,
+                       double eps, int64_t hidden) {
+  DIE_CHECK_CUDA(slab);
+  DIE_CHECK_DTYPE(slab, at::kFloat);
+  DIE_CHECK_CONTIG(slab);
+  DIE_CHECK_BF16(out);
+  DIE_CHECK_CONTIG(out);
+  const int64_t D = 128;
+  const int64_t nseq = ctx_lens.numel();
+  TORCH_CHECK(slab.dim() == 3 && slab.size(1) >= nseq && slab.size(2) == (hq + 2 * hkv) * D, "slab [sk, M, width]");
+  TORCH_CHECK(out.numel() >= nseq * hq * D, "out too small");
+  TORCH_CHECK(hq % hkv == 0, "hq % hkv");
+  const int64_t G = hq / hkv;
+  TORCH_CHECK(G == 1 || G == 2 || G == 4 || G == 8, "fused decode attention: G in {1, 2, 4, 8}");
+  check_cache(k_cache, hkv, D, "k_cache");
+  check_cache(v_cache, hkv, D, "v_cache");
+  TORCH_CHECK(k_cache.size(2) == 16, "fused decode attention: block_size 16");
+  DIE_CHECK_DTYPE(block_tables, at::kInt);
+  DIE_CHECK_DTYPE(ctx_lens, at::kInt);
+  DIE_CHECK_CONTIG(block_tables);
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= nseq, "block_tables shape");
+  TORCH_CHECK(block_tables.size(1) * 16 >= max_ctx, "block table narrower than max_ctx");
+  DIE_CHECK_DTYPE(ssp, at::kFloat);
+  DIE_CHECK_CONTIG(ssp);
+  TORCH_CHECK(ssp.dim() == 2 && ssp.size(1) == 32 && ssp.size(0) >= 1 && ssp.size(0) <= 128, "ssp [T <= 128, 32]");
+  DIE_CHECK_DTYPE(positions, at::kLong);
+  DIE_CHECK_DTYPE(slot_mapping, at::kLong);
+  DIE_CHECK_DTYPE(cos_sin, at::kFloat);
+  DIE_CHECK_CONTIG(cos_sin);
+  TORCH_CHECK(cos_sin.size(1) == D, "cos_sin [max_pos, 128]");
+  TORCH_CHECK(positions.numel() >= nseq && slot_mapping.numel() >= nseq, "positions / slot_mapping");
+  // decode: every sequence's new token sits at position ctx_len - 1 (the kernel uses that)
+  const int maxp = die::attn_decode_max_partials((int)max_ctx);
+  DIE_CHECK_DTYPE(part_o, at::kFloat);
+  DIE_CHECK_DTYPE(part_ml, at::kFloat);
+  TORCH_CHECK(part_o.numel() >= nseq * hq * maxp * D && part_ml.numel() >= nseq * hq * maxp * 2,
+              "partial buffers too small for max_ctx");
+  DIE_CHECK_DTYPE(counters, at::kInt);
+  TORCH_CHECK(counters.is_cuda() && counters.numel() >= nseq * hkv, "attn counters: int32 [>= num_seqs*hkv]");
+  die::AttnDecodeFuse fz;
+  fz.slab = slab.data_ptr<float>();
+  fz.sk = (int)slab.size(0);
+  fz.slab_stride = slab.size(1) * slab.size(2);
+  fz.width = (int)slab.size(2);
+  fz.ssp = ssp.data_ptr<float>();
+  fz.ssp_tiles = (int)ssp.size(0);
+  fz.inv_n = 1.f / (float)hidden;
+  fz.eps = (float)eps;
+  fz.cos_sin = cos_sin.data_ptr<float>();
+  fz.slot_mapping = slot_mapping.data_ptr<int64_t>();
+  DIE_HIP(die::launch_attn_decode(bf(out), part_o.data_ptr<float>(), part_ml.data_ptr<float>(),
+                                  counters.data_ptr<int>(), nullptr, 0, bf(k_cache), bf(v_cache),
+                                  block_tables.data_ptr<int>(), (int)block_tables.size(1), ctx_lens.data_ptr<int>(),
+                                  (int)nseq, (int)max_ctx, (int)hq, (int)hkv, (int)D, 16, (float)scale, &fz,
+                                  cur_stream()));
 }
 
 int64_t decode_partials(int64_t max_ctx) { return die::attn_decode_max_partials((int)max_ctx); }
@@ -284,7 +346,13 @@ void moe_grouped_gemm(Tensor y, Tensor x, Tensor w, Tensor offsets) {
 //   mode 0: y bf16 [M, N], w [N, K]
 //   mode 1: y bf16 [M, N] = silu(x gate^T) * (x up^T), w = [gate; up] [2N, K]
 //   mode 2: y fp32 split-K slabs [sk, M, N], w [N, K]
-void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t sk, bool nt) {
+// Decode GEMM (gemm_decode.hip). mode 0 bf16, 1 silu*up, 2 fp32 split-K slabs [sk, M, N],
+// 3 slabs + residual update of `resid` [M, N] and row sums of squares `ssp_out` [N/wr, 32]
+// (tickets `counters` [N/wr], zeroed once), 4 = mode 1 with rows scaled by the RMSNorm
+// statistics `ssp_in` [T, 32] (eps; the norm weight is folded into w). Unused fusion tensors
+// may be empty.
+void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t sk, bool nt, Tensor resid,
+                 Tensor ssp_out, Tensor counters, Tensor ssp_in, double eps) {
   DIE_CHECK_CUDA(x);
   DIE_CHECK_BF16(x);
   DIE_CHECK_BF16(w);
@@ -294,10 +362,12 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
   TORCH_CHECK(M >= 1 && M <= 32, "gemm_decode: 1 <= M <= 32");
   TORCH_CHECK(wr == 32 || wr == 48 || wr == 64 || wr == 96 || wr == 112 || wr == 128,
               "wr must be one of 32, 48, 64, 96, 112, 128");
+  TORCH_CHECK(mode >= 0 && mode <= 4, "mode");
   const int64_t kc = wr >= 96 ? 128 : 256;
   TORCH_CHECK(K % (kc * sk) == 0, "gemm_decode: K must be a multiple of the K slot (256, or 128 for wr >= 96) * sk");
+  const bool silu = mode == 1 || mode == 4;
   int64_t N, ldy;
-  if (mode == 2) {
+  if (mode == 2 || mode == 3) {
     DIE_CHECK_DTYPE(y, at::kFloat);
     DIE_CHECK_CONTIG(y);
     TORCH_CHECK(y.dim() == 3 && y.size(0) == sk && y.size(1) == M, "slab y must be [sk, M, N]");
@@ -310,10 +380,50 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
     N = y.size(1);
     ldy = y.stride(0);
   }
-  TORCH_CHECK(w.dim() == 2 && w.size(1) == K && w.size(0) == (mode == 1 ? 2 * N : N), "gemm_decode w shape");
-  TORCH_CHECK(N % (mode == 1 ? wr / 2 : wr) == 0, "N not a multiple of the column tile");
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K && w.size(0) == (silu ? 2 * N : N), "gemm_decode w shape");
+  TORCH_CHECK(N % (silu ? wr / 2 : wr) == 0, "N not a multiple of the column tile");
+  TORCH_CHECK((int64_t)sk * M * N * 4 < ((int64_t)1 << 31) || mode != 3, "slab too large");
+  die::GemmDecodeFuse fz;
+  if (mode == 3) {
+    TORCH_CHECK(wr == 32 || wr == 64 || wr == 128, "mode 3: wr in {32, 64, 128}");
+    DIE_CHECK_BF16(resid);
+    check_rows(resid, "resid");
+    TORCH_CHECK(resid.size(0) >= M && resid.size(1) == N, "resid [M, N]");
+    DIE_CHECK_DTYPE(ssp_out, at::kFloat);
+    DIE_CHECK_CONTIG(ssp_out);
+    TORCH_CHECK(ssp_out.numel() >= (N / wr) * 32, "ssp_out [N/wr, 32]");
+    fz.resid = bf(resid);
+    fz.ld_resid = resid.stride(0);
+    fz.ssp_out = ssp_out.data_ptr<float>();
+    if (sk > 1) {
+      DIE_CHECK_DTYPE(counters, at::kInt);
+      TORCH_CHECK(counters.is_cuda() && counters.numel() >= N / wr, "counters [N/wr] int32");
+      fz.counters = counters.data_ptr<int>();
+    }
+  }
+  if (mode == 4) {
+    DIE_CHECK_DTYPE(ssp_in, at::kFloat);
+    DIE_CHECK_CONTIG(ssp_in);
+    TORCH_CHECK(ssp_in.dim() == 2 && ssp_in.size(1) == 32 && ssp_in.size(0) >= 1 && ssp_in.size(0) <= 128,
+                "ssp_in [T <= 128, 32]");
+    fz.ssp_in = ssp_in.data_ptr<float>();
+    fz.ssp_tiles = (int)ssp_in.size(0);
+    fz.inv_n = 1.f / (float)K;
+    fz.eps = (float)eps;
+  }
   DIE_HIP(die::launch_gemm_decode(y.data_ptr(), ldy, bf(x), x.stride(0), bf(w), (int)M, (int)N, (int)K, (int)mode,
-                                  (int)wr, (int)sk, nt, cur_stream()));
+                                  (int)wr, (int)sk, nt, fz, cur_stream()));
+}
+
+void row_sumsq(Tensor ssp, Tensor x) {
+  DIE_CHECK_CUDA(x);
+  DIE_CHECK_BF16(x);
+  check_rows(x, "x");
+  DIE_CHECK_DTYPE(ssp, at::kFloat);
+  DIE_CHECK_CONTIG(ssp);
+  TORCH_CHECK(x.size(0) <= 32 && ssp.numel() >= 32, "row_sumsq: x [<= 32, H], ssp [1, 32]");
+  DIE_HIP(die::launch_row_sumsq(ssp.data_ptr<float>(), bf(x), (int)x.size(0), (int)x.size(1), x.stride(0),
+                                cur_stream()));
 }
 
 void fused_add_rms_norm_slab(Tensor out, Tensor slab, Tensor residual, Tensor w, double eps) {
@@ -367,6 +477,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("rope_and_cache", &rope_and_cache);
   m.def("attn_prefill", &attn_prefill);
   m.def("attn_decode", &attn_decode);
+  m.def("attn_decode_fused", &attn_decode_fused);
   m.def("decode_partials", &decode_partials);
   m.def("sample", &sample, py::arg("out"), py::arg("logits"), py::arg("temperature") = py::none(),
         py::arg("top_k") = py::none(), py::arg("top_p") = py::none(), py::arg("seeds") = py::none(),
@@ -379,6 +490,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_combine", &moe_combine);
   m.def("moe_grouped_gemm", &moe_grouped_gemm);
   m.def("gemm_decode", &gemm_decode);
+  m.def("row_sumsq", &row_sumsq);
   m.def("fused_add_rms_norm_slab", &fused_add_rms_norm_slab);
   m.def("rope_and_cache_slab", &rope_and_cache_slab);
 }

@@ -589,13 +589,27 @@ __device__ __forceinline__ float lds_ld32(uint32_t a) {
 __device__ __forceinline__ void lds_st32(uint32_t a, float v) {
   asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
+__device__ __forceinline__ void lds_st16(uint32_t a, uint32_t v) {
+  asm volatile("ds_write_b16 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
 
-template <int G>
+__device__ __forceinline__ void glds4(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((global_cvoid*)src, (lds_void*)lds_wave_base, 4, 0, 0);
+}
+
+// FUSED: the query rows and the new token's K/V are not read from a rotated qkv tensor but built
+// here from the qkv projection's fp32 split-K slabs: sum the slabs, scale by the input RMSNorm's
+// rsqrt (its weight is folded into Wqkv; statistics = the previous layer's per-tile sums of
+// squares), apply RoPE, write K/V to the paged cache (for later steps) and patch the new token's
+// row straight into this step's LDS image. The separate RoPE/KV-write and RMSNorm kernels of
+// the decode layer disappear. Everything the prologue needs arrives by LDS-DMA, staged in the
+// merge area (idle at a task start), so no ordinary load stalls the chunk stream.
+template <int G, bool FUSED>
 __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters,
-    const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
-    const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
-    const int* __restrict__ ctx_lens, int num_seqs, int hq, int hkv, float scale_log2, int maxp, int dbg) {
+    const bf16_t* __restrict__ q, int64_t q_stride, bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, int num_seqs, int hq,
+    int hkv, float scale_log2, int maxp, int dbg, AttnDecodeFuse fz, const int64_t* __restrict__ slot_mapping) {
   constexpr int QI = (G * 256 + 1023) / 1024;  // LDS-DMA instructions for the query rows
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* ml = reinterpret_cast<float*>(smem + 2 * V3_BUF);
@@ -643,7 +657,28 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
     };
 
     issue(c0, 0);
-    if (wave == 0 && !(dbg & 2)) {  // the G query rows of this (seq, kv head), 256 B each
+    const bool has_new = FUSED && c1 == nch;  // this part holds the step's new token (key ctx-1)
+    char* fa = smem + 2 * V3_BUF;            // FUSED staging (merge area, idle at a task start)
+    const int frows = fz.sk * (G + 2);       // slab rows: [s][q heads..., k, v] x 128 fp32
+    const int fs_off = ((frows + 1) / 2) * 1024;
+    if constexpr (FUSED) {
+      if (!(dbg & 2)) {
+        const float* srow = fz.slab + (int64_t)seq * fz.width;
+        for (int i = wave; i < (frows + 1) / 2; i += 4) {
+          const int ri = min(2 * i + (lane >> 5), frows - 1);
+          const int sl = ri / (G + 2), j = ri - sl * (G + 2);
+          const int col = j < G ? (kvh * G + j) * D : (j == G ? (hq + kvh) * D : (hq + hkv + kvh) * D);
+          glds16(srow + sl * fz.slab_stride + col + (lane & 31) * 4, fa + i * 1024);
+        }
+        if (wave == 0) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            glds4(fz.ssp + min(lane + 64 * i, fz.ssp_tiles - 1) * 32 + seq, fa + fs_off + i * 256);
+        }
+        if (wave == 1)  // decode: the new token sits at position ctx - 1
+          glds16(fz.cos_sin + (int64_t)(ctx - 1) * D + (lane & 31) * 4, fa + fs_off + 512);
+      }
+    } else if (wave == 0 && !(dbg & 2)) {  // the G query rows of this (seq, kv head), 256 B each
       const bf16_t* qb = q + (int64_t)seq * q_stride + (int64_t)kvh * G * D;
 #pragma unroll
       for (int i = 0; i < QI; ++i) {
@@ -654,6 +689,7 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
     State st;
     init_state(st);
     bf16x8_t qf[8];
+    bf16_t nk0 = 0, nk1 = 0, nv = 0;  // FUSED: the new token's rotated key pair / value element
 #pragma unroll 1
     for (int c = c0; c < c1; ++c) {
       const int b = (c - c0) & 1;
@@ -665,6 +701,65 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
       }
       __builtin_amdgcn_s_barrier();
       const char* base = smem + b * V3_BUF;
+      if constexpr (FUSED) {
+        if (c == c0) {
+          // r = rsqrt(mean(h^2) + eps) of this sequence's row
+          float ssum = 0.f;
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            ssum += lane + 64 * i < fz.ssp_tiles ? lds_ld32(lds_addr(fa + fs_off + 4 * (lane + 64 * i))) : 0.f;
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) ssum += __shfl_xor(ssum, o, 64);
+          const float rn = rsqrtf(ssum * fz.inv_n + fz.eps);
+          const uint32_t cs = lds_addr(fa + fs_off + 512);
+          auto slab_sum = [&](int j, int d) {
+            float v = 0.f;
+            for (int sl = 0; sl < fz.sk; ++sl) v += lds_ld32(lds_addr(fa + ((sl * (G + 2) + j) * D + d) * 4));
+            return v * rn;
+          };
+          for (int it = tid; it < G * 64; it += 256) {  // rotated query rows -> q image (bf16)
+            const int j = it >> 6, p = it & 63;
+            const float a = slab_sum(j, p), bq = slab_sum(j, p + 64);
+            const float co = lds_ld32(cs + 4 * p), si = lds_ld32(cs + 4 * (p + 64));
+            const uint32_t qa = lds_addr(smem + V3_CHUNK + j * 256);
+            lds_st16(qa + 2 * p, f2bf(a * co - bq * si));
+            lds_st16(qa + 2 * (p + 64), f2bf(bq * co + a * si));
+          }
+          if (tid < 64) {  // new key, rotated
+            const float a = slab_sum(G, tid), bq = slab_sum(G, tid + 64);
+            const float co = lds_ld32(cs + 4 * tid), si = lds_ld32(cs + 4 * (tid + 64));
+            nk0 = f2bf(a * co - bq * si);
+            nk1 = f2bf(bq * co + a * si);
+          } else if (tid < 192) {
+            nv = f2bf(slab_sum(G + 1, tid - 64));
+          }
+          if (has_new) {
+            const int64_t slot = slot_mapping[seq];  // -1: padded graph row, no write
+            if (slot >= 0) {  // the paged cache, for later steps (this step reads the LDS patch)
+              const int64_t base_kv = ((slot >> 4) * hkv + kvh) * 16 * D + (slot & 15) * D;
+              if (tid < 64) {
+                k_cache[base_kv + tid] = nk0;
+                k_cache[base_kv + tid + 64] = nk1;
+              } else if (tid < 192) {
+                v_cache[base_kv + tid - 64] = nv;
+              }
+            }
+          }
+          lds_barrier();
+        }
+        if (has_new && c + 1 == c1) {  // patch key ctx-1 into this chunk's K / V images
+          const int rr = (ctx - 1) - c * DEC_KEYS;
+          const uint32_t kimg = lds_addr(base) + rr * DEC_ROW, vimg = kimg + DEC_KEYS * DEC_ROW;
+          if (tid < 64) {
+            lds_st16(kimg + 16 * ((tid >> 3) ^ (rr & 15)) + 2 * (tid & 7), nk0);
+            lds_st16(kimg + 16 * (((tid + 64) >> 3) ^ (rr & 15)) + 2 * (tid & 7), nk1);
+          } else if (tid < 192) {
+            const int d = tid - 64;
+            lds_st16(vimg + 16 * ((d >> 3) ^ ((rr & 3) << 2)) + 2 * (d & 7), nv);
+          }
+          lds_barrier();
+        }
+      }
       if (c == c0) {
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk)
@@ -848,26 +943,38 @@ static int num_cus() {
 }
 
 hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* counters, const bf16_t* q,
-                              int64_t q_stride, const bf16_t* k_cache, const bf16_t* v_cache, const int* block_tables,
+                              int64_t q_stride, bf16_t* k_cache, bf16_t* v_cache, const int* block_tables,
                               int bt_stride, const int* ctx_lens, int num_seqs, int max_ctx, int hq, int hkv,
-                              int head_dim, int block_size, float scale, hipStream_t s) {
+                              int head_dim, int block_size, float scale, const AttnDecodeFuse* fz, hipStream_t s) {
   if (num_seqs == 0) return hipSuccess;
   if (head_dim != D || hq % hkv) return hipErrorInvalidValue;
   const int G = hq / hkv;
   const int maxp3 = (max_ctx + DEC_KEYS - 1) / DEC_KEYS;
   const int64_t part_bytes = (int64_t)num_seqs * hq * maxp3 * D * 4;
-  if (counters != nullptr && block_size == 16 && (G == 1 || G == 2 || G == 4 || G == 8) &&
-      part_bytes < ((int64_t)1 << 31)) {
+  const bool v3_ok = counters != nullptr && block_size == 16 && (G == 1 || G == 2 || G == 4 || G == 8) &&
+                     part_bytes < ((int64_t)1 << 31);
+  if (fz != nullptr) {  // fused prologue: only the v3 kernel has it
+    if (!v3_ok || fz->sk < 1 || fz->ssp_tiles < 1 || fz->ssp_tiles > 128 ||
+        ((fz->sk * (G + 2) + 1) / 2) * 1024 + 1536 > V3_MERGE)
+      return hipErrorInvalidValue;
+  }
+  if (v3_ok) {
     const float sl2 = scale * 1.4426950408889634f;
     const int tasks = num_seqs * hkv * maxp3;
     const int ncu = num_cus();
     static const int dbg = getenv("DIE_ATTN_DBG") ? atoi(getenv("DIE_ATTN_DBG")) : 0;  // perf experiments only
     dim3 grid(tasks < ncu ? tasks : ncu), block(256);
-#define DIE_D3(GG)                                                                                           \
-  case GG:                                                                                                   \
-    hipLaunchKernelGGL(attn_decode_v3_kernel<GG>, grid, block, V3_LDS, s, out, part_o, part_ml, counters, q, \
-                       q_stride, k_cache, v_cache, block_tables, bt_stride, ctx_lens, num_seqs, hq, hkv, sl2,    \
-                       maxp3, dbg);                                                                          \
+    const AttnDecodeFuse none{};
+#define DIE_D3(GG)                                                                                              \
+  case GG:                                                                                                      \
+    if (fz)                                                                                                     \
+      hipLaunchKernelGGL((attn_decode_v3_kernel<GG, true>), grid, block, V3_LDS, s, out, part_o, part_ml,       \
+                         counters, q, q_stride, k_cache, v_cache, block_tables, bt_stride, ctx_lens, num_seqs, hq, \
+                         hkv, sl2, maxp3, dbg, *fz, fz->slot_mapping);                                          \
+    else                                                                                                        \
+      hipLaunchKernelGGL((attn_decode_v3_kernel<GG, false>), grid, block, V3_LDS, s, out, part_o, part_ml,      \
+                         counters, q, q_stride, k_cache, v_cache, block_tables, bt_stride, ctx_lens, num_seqs, hq, \
+                         hkv, sl2, maxp3, dbg, none, nullptr);                                                  \
     break;
     switch (G) {
       DIE_D3(1)

@@ -59,11 +59,13 @@ using namespace gd;
 template <int WR, int EPI, int S, bool NT, int KC>
 __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv, int64_t ldy,
                                                           const bf16_t* __restrict__ X, int64_t ldx,
-                                                          const bf16_t* __restrict__ W, int M, int N_out, int K) {
+                                                          const bf16_t* __restrict__ W, int M, int N_out, int K,
+                                                          GemmDecodeFuse fz) {
   constexpr int ROWB = KC * 2;                 // bytes per image row
   constexpr int CPR = KC / 8;                  // 16-byte chunks per row (32 or 16)
   constexpr int RPP = 64 / CPR;                // rows per 1-KiB DMA piece (2 or 4)
-  constexpr int NO = EPI == 1 ? WR / 2 : WR;   // output columns per workgroup
+  constexpr bool SILU = EPI == 1 || EPI == 4;
+  constexpr int NO = SILU ? WR / 2 : WR;       // output columns per workgroup
   constexpr int SLOT = (WR + MR) * ROWB;       // bytes per ring slot
   constexpr int INSTR = (WR + MR) / RPP;       // 1-KiB DMA pieces per chunk
   constexpr int PER_WAVE = INSTR / 4;          // pieces issued per wave per chunk
@@ -89,7 +91,7 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
     const bf16_t* base;
     if (row < WR) {
       int grow = n0 + row;
-      if (EPI == 1 && row >= NO) grow = N_out + n0 + (row - NO);
+      if (SILU && row >= NO) grow = N_out + n0 + (row - NO);
       base = W + (int64_t)grow * K;
     } else {
       base = X + (int64_t)min(row - WR, M - 1) * ldx;
@@ -108,6 +110,16 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
         glds16<0>(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);
     }
   };
+
+  // EPI 4: this thread's share of the producer's per-tile sums of squares (row tid & 31,
+  // tiles (tid >> 5) + 8i), loaded before any LDS-DMA and first used in the epilogue, so
+  // no wait lands inside the weight stream. Index clamped, masked later (no branches).
+  float ssv[EPI == 4 ? 16 : 1];
+  if constexpr (EPI == 4) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      ssv[i] = fz.ssp_in[min((tid >> 5) + 8 * i, fz.ssp_tiles - 1) * 32 + (tid & 31)];
+  }
 
   f4 acc[2][NTILE];
 #pragma unroll
@@ -170,16 +182,97 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
         red[(wave * MR + m) * WR + n] = acc[mt][nt][r];
       }
   __syncthreads();
+  if constexpr (EPI == 3) {
+    // split-K partial -> last arriver: h += sum of partials (bf16), per-tile row sums of squares
+    constexpr int Q = WR / 4;  // float4 column groups per row (8, 16 or 32 lanes: one row per lane group)
+    static_assert(Q == 8 || Q == 16 || Q == 32, "EPI 3 needs wr in {32, 64, 128}");
+    int* ctl = reinterpret_cast<int*>(smem + 4 * MR * WR * 4);
+    const bool single = gridDim.y == 1;
+    if (!single) {
+      __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(Yv, 0, 0x7fffffff, 0x00020000);
+      for (int e = tid; e < MR * Q; e += NTH) {
+        const int m = e / Q, j = 4 * (e % Q);
+        if (m >= M) continue;
+        f4 v = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int w = 0; w < 4; ++w) v += *reinterpret_cast<const f4*>(red + (w * MR + m) * WR + j);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                               ry, (int)((((int64_t)blockIdx.y * M + m) * ldy + n0 + j) * 4), 0,
+                                               16);  // write-through (sc1): no release fence needed
+      }
+      wait_vm<0>();
+      __syncthreads();
+      if (tid == 0)
+        ctl[0] = __hip_atomic_fetch_add(fz.counters + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 (int)gridDim.y - 1;
+      __syncthreads();
+      if (!ctl[0]) return;
+    }
+    __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(Yv, 0, 0x7fffffff, 0x00020000);
+    for (int e = tid; e < MR * Q; e += NTH) {  // Q | 64 and NTH % Q == 0: a row's lanes share a wave
+      const int m = e / Q, j = 4 * (e % Q);
+      float ss = 0.f;
+      if (m < M) {
+        f4 v = f4{0.f, 0.f, 0.f, 0.f};
+        if (single) {
+#pragma unroll
+          for (int w = 0; w < 4; ++w) v += *reinterpret_cast<const f4*>(red + (w * MR + m) * WR + j);
+        } else {
+          for (int k = 0; k < (int)gridDim.y; ++k)
+            v += __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            ry, (int)((((int64_t)k * M + m) * ldy + n0 + j) * 4), 0, 16));
+        }
+        bf16_t* hp = fz.resid + (int64_t)m * fz.ld_resid + n0 + j;
+        const uint2 hr = *reinterpret_cast<const uint2*>(hp);
+        float hv[4] = {bf2f((bf16_t)(hr.x & 0xffff)) + v[0], bf2f((bf16_t)(hr.x >> 16)) + v[1],
+                       bf2f((bf16_t)(hr.y & 0xffff)) + v[2], bf2f((bf16_t)(hr.y >> 16)) + v[3]};
+        uint2 hw;
+        hw.x = pack2(hv[0], hv[1]);
+        hw.y = pack2(hv[2], hv[3]);
+        *reinterpret_cast<uint2*>(hp) = hw;
+        const float r0 = bf2f((bf16_t)(hw.x & 0xffff)), r1 = bf2f((bf16_t)(hw.x >> 16));
+        const float r2 = bf2f((bf16_t)(hw.y & 0xffff)), r3 = bf2f((bf16_t)(hw.y >> 16));
+        ss = r0 * r0 + r1 * r1 + r2 * r2 + r3 * r3;
+      }
+#pragma unroll
+      for (int o = Q / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+      if (e % Q == 0) fz.ssp_out[blockIdx.x * 32 + m] = m < M ? ss : 0.f;
+    }
+    if (!single && tid == 0) __hip_atomic_store(fz.counters + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if constexpr (EPI == 4) {
+    // row scale r[m] = rsqrt(sum_t ssp[t][m] / n + eps) (the RMSNorm whose weight is folded into W)
+    float* part = reinterpret_cast<float*>(smem + 4 * MR * WR * 4);  // [8][32]
+    float* rs = part + 8 * 32;
+    float acc_ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc_ss += (tid >> 5) + 8 * i < fz.ssp_tiles ? ssv[i] : 0.f;
+    part[tid] = acc_ss;  // tid = slice * 32 + row
+    __syncthreads();
+    if (tid < 32) {
+      float t = 0.f;
+#pragma unroll
+      for (int sl = 0; sl < 8; ++sl) t += part[sl * 32 + tid];
+      rs[tid] = rsqrtf(t * fz.inv_n + fz.eps);
+    }
+    __syncthreads();
+  }
   for (int e = tid; e < MR * NO; e += NTH) {
     const int m = e / NO, j = e % NO;
     if (m >= M) continue;
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) v += red[(w * MR + m) * WR + j];
-    if (EPI == 1) {
+    if (SILU) {
       float u = 0.f;
 #pragma unroll
       for (int w = 0; w < 4; ++w) u += red[(w * MR + m) * WR + NO + j];
+      if constexpr (EPI == 4) {
+        const float r = reinterpret_cast<const float*>(smem + 4 * MR * WR * 4)[8 * 32 + m];
+        v *= r;
+        u *= r;
+      }
       v = v / (1.f + __expf(-v)) * u;
     }
     if (EPI == 2)
@@ -191,42 +284,56 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
 
 template <int WR, int EPI, int S, int KC>
 static hipError_t launch_gd(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N_out,
-                            int K, int sk, bool nt, hipStream_t s) {
-  constexpr int NO = EPI == 1 ? WR / 2 : WR;
+                            int K, int sk, bool nt, const GemmDecodeFuse& fz, hipStream_t s) {
+  constexpr int NO = (EPI == 1 || EPI == 4) ? WR / 2 : WR;
   if (N_out % NO || K % sk || (K / sk) % KC) return hipErrorInvalidValue;
   const size_t lds = (size_t)S * (WR + MR) * KC * 2;
   if (nt)
     hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, true, KC>), dim3(N_out / NO, sk), dim3(NTH), lds, s, Y, ldy,
-                       X, ldx, W, M, N_out, K);
+                       X, ldx, W, M, N_out, K, fz);
   else
     hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, false, KC>), dim3(N_out / NO, sk), dim3(NTH), lds, s, Y, ldy,
-                       X, ldx, W, M, N_out, K);
+                       X, ldx, W, M, N_out, K, fz);
   return hipGetLastError();
 }
 
 template <int WR, int S, int KC>
 static hipError_t launch_modes(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,
-                               int K, int mode, int sk, bool nt, hipStream_t s) {
-  if (mode == 0) return launch_gd<WR, 0, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
-  if (mode == 1) return launch_gd<WR, 1, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
-  return launch_gd<WR, 2, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, s);
+                               int K, int mode, int sk, bool nt, const GemmDecodeFuse& fz, hipStream_t s) {
+  switch (mode) {
+    case 0: return launch_gd<WR, 0, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
+    case 1: return launch_gd<WR, 1, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
+    case 2: return launch_gd<WR, 2, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
+    case 4: return launch_gd<WR, 4, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
+    case 3:
+      if constexpr (WR == 32 || WR == 64 || WR == 128) return launch_gd<WR, 3, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
+      return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;
+  }
 }
 
-// mode 0: bf16 Y [M, N]; mode 1: bf16 silu(gate)*up, W = [2N, K]; mode 2: fp32 slabs [sk, M, N].
+// mode 0: bf16 Y [M, N]; mode 1: bf16 silu(gate)*up, W = [2N, K]; mode 2: fp32 slabs [sk, M, N];
+// mode 3: fp32 slabs + last-arriver residual update (fz.resid += sum of slabs, bf16) and per-tile
+//         row sums of squares fz.ssp_out [N / wr][32] (the next RMSNorm's statistics);
+// mode 4: mode 1 with the rows scaled by rsqrt(sum_t fz.ssp_in[t][m] * inv_n + eps) (RMSNorm with
+//         its weight folded into W).
 // wr: weight rows per workgroup: 32 / 48 / 64 (256-wide K slots) or 96 / 112 / 128 (128-wide K slots),
 // so that (N / columns) * sk can be made a multiple of the CU count for the model's shapes
 // (e.g. 8B gate/up: 14336 / 56 = 256 workgroups at wr = 112).
 hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,
-                              int K, int mode, int wr, int sk, bool nt, hipStream_t s) {
+                              int K, int mode, int wr, int sk, bool nt, const GemmDecodeFuse& fz, hipStream_t s) {
   if (M <= 0) return hipSuccess;
-  if (M > MR || sk < 1 || (mode != 2 && sk != 1)) return hipErrorInvalidValue;
+  if (M > MR || sk < 1 || (mode != 2 && mode != 3 && sk != 1)) return hipErrorInvalidValue;
+  if (mode == 4 && (fz.ssp_in == nullptr || fz.ssp_tiles < 1 || fz.ssp_tiles > 128)) return hipErrorInvalidValue;
+  if (mode == 3 && (fz.resid == nullptr || fz.ssp_out == nullptr || (sk > 1 && fz.counters == nullptr)))
+    return hipErrorInvalidValue;
   switch (wr) {
-    case 32: return launch_modes<32, 4, 256>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, s);
-    case 48: return launch_modes<48, 3, 256>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, s);
-    case 64: return launch_modes<64, 3, 256>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, s);
-    case 96: return launch_modes<96, 4, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, s);
-    case 112: return launch_modes<112, 4, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, s);
-    case 128: return launch_modes<128, 3, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, s);
+    case 32: return launch_modes<32, 4, 256>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, fz, s);
+    case 48: return launch_modes<48, 3, 256>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, fz, s);
+    case 64: return launch_modes<64, 3, 256>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, fz, s);
+    case 96: return launch_modes<96, 4, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, fz, s);
+    case 112: return launch_modes<112, 4, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, fz, s);
+    case 128: return launch_modes<128, 3, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, fz, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -28,10 +28,22 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
                                const bf16_t* v_cache, const int* block_tables, int bt_stride, const int* cu_q,
                                const int* ctx_lens, int num_seqs, int max_q_len, int hq, int hkv, int head_dim,
                                int block_size, float scale, hipStream_t s);
+// Fused decode-attention prologue (attention.hip, attn_decode_v3_kernel<G, true>).
+struct AttnDecodeFuse {
+  const float* slab = nullptr;      // qkv projection split-K slabs [sk][M][width] fp32
+  int sk = 0;
+  int64_t slab_stride = 0;          // M * width
+  int width = 0;                    // (hq + 2 hkv) * 128
+  const float* ssp = nullptr;       // input-norm statistics [ssp_tiles][32]
+  int ssp_tiles = 0;
+  float inv_n = 0.f, eps = 0.f;     // 1 / hidden, RMSNorm eps
+  const float* cos_sin = nullptr;   // [max_pos][128]: cos | sin, read at position ctx - 1
+  const int64_t* slot_mapping = nullptr;
+};
 hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* counters, const bf16_t* q,
-                              int64_t q_stride, const bf16_t* k_cache, const bf16_t* v_cache, const int* block_tables,
+                              int64_t q_stride, bf16_t* k_cache, bf16_t* v_cache, const int* block_tables,
                               int bt_stride, const int* ctx_lens, int num_seqs, int max_ctx, int hq, int hkv,
-                              int head_dim, int block_size, float scale, hipStream_t s);
+                              int head_dim, int block_size, float scale, const AttnDecodeFuse* fz, hipStream_t s);
 int attn_decode_max_partials(int max_ctx);
 
 hipError_t launch_sample(int64_t* out, const bf16_t* logits, int64_t stride, int rows, int vocab,
@@ -47,8 +59,20 @@ hipError_t launch_moe_combine(bf16_t* out, const bf16_t* ys, const int* pos, con
 hipError_t launch_moe_grouped_gemm(bf16_t* Y, const bf16_t* X, const bf16_t* W, const int* offsets, int max_rows,
                                    int E, int N, int K, hipStream_t s);
 
+// Fusion operands of the decode GEMM (modes 3 and 4, see gemm_decode.hip).
+hipError_t launch_row_sumsq(float* ssp, const bf16_t* x, int rows, int hidden, int64_t stride, hipStream_t s);
+struct GemmDecodeFuse {
+  bf16_t* resid = nullptr;       // mode 3: residual stream [M][ld_resid], updated in place
+  int64_t ld_resid = 0;
+  float* ssp_out = nullptr;      // mode 3: [N / wr][32] row sums of squares per column tile
+  int* counters = nullptr;       // mode 3: [N / wr] split-K tickets (zero, re-armed by the kernel)
+  const float* ssp_in = nullptr; // mode 4: producer's [ssp_tiles][32] sums of squares
+  int ssp_tiles = 0;
+  float inv_n = 0.f;             // 1 / hidden size
+  float eps = 0.f;
+};
 hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,
-                              int K, int mode, int wr, int sk, bool nt, hipStream_t s);
+                              int K, int mode, int wr, int sk, bool nt, const GemmDecodeFuse& fz, hipStream_t s);
 // consumers of fp32 split-K slabs [sk][rows][width]
 hipError_t launch_fused_add_rms_norm_slab(bf16_t* out, const float* slab, int sk, bf16_t* residual, const bf16_t* w,
                                           float eps, int rows, int hidden, int64_t out_stride, hipStream_t s);

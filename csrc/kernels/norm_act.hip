@@ -176,6 +176,34 @@ hipError_t launch_fused_add_rms_norm_slab(bf16_t* out, const float* slab, int sk
 }
 
 // ----------------------------------------------------------------------------
+// Row sums of squares of x [rows <= 32][hidden] into ssp[row] (the [1][32] statistics
+// block that the norm-folded decode consumers read). grid = rows, block = 256.
+__global__ void __launch_bounds__(256) row_sumsq_kernel(float* __restrict__ ssp, const bf16_t* __restrict__ x,
+                                                        int hidden, int64_t stride) {
+  __shared__ float red[4];
+  const uint4* src = reinterpret_cast<const uint4*>(x + blockIdx.x * stride);
+  float ss = 0.f;
+  for (int c = threadIdx.x; c < (hidden >> 3); c += 256) {
+    float v[8];
+    unpack8(src[c], v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  if (threadIdx.x == 0) ssp[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+hipError_t launch_row_sumsq(float* ssp, const bf16_t* x, int rows, int hidden, int64_t stride, hipStream_t s) {
+  if (rows == 0) return hipSuccess;
+  if (hidden % 8 || rows > 32) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(row_sumsq_kernel, dim3(rows), dim3(256), 0, s, ssp, x, hidden, stride);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------
 // silu(gate) * up. Input row = [gate(I) | up(I)], output row = I.
 // grid = (rows, ceil(I/8 / 256)); one 16-byte chunk of gate and of up per lane.
 __global__ void __launch_bounds__(256) silu_mul_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ in,

@@ -111,8 +111,9 @@ class ModelRunner:
             self.part_o = torch.empty(self.max_seqs * hq * maxp * 128, dtype=torch.float32, device=dev)
             self.part_ml = torch.empty(self.max_seqs * hq * maxp * 2, dtype=torch.float32, device=dev)
             self.attn_cnt = torch.zeros(self.max_seqs * model.hkv, dtype=i32, device=dev)
+            self.dec_scratch = model.alloc_decode_scratch() if hasattr(model, "alloc_decode_scratch") else None
         else:
-            self.part_o = self.part_ml = self.attn_cnt = None
+            self.part_o = self.part_ml = self.attn_cnt = self.dec_scratch = None
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_sizes: List[int] = []
         self._graph_pool = None
@@ -224,7 +225,7 @@ class ModelRunner:
     def _decode_forward(self, n: int) -> torch.Tensor:
         meta = AttnMetadata(is_prefill=False, slot_mapping=self.d_slots[:n], block_tables=self.d_bt[:n],
                             ctx_lens=self.d_ctx[:n], max_ctx=self.max_model_len, part_o=self.part_o,
-                            part_ml=self.part_ml, attn_cnt=self.attn_cnt)
+                            part_ml=self.part_ml, attn_cnt=self.attn_cnt, scratch=self.dec_scratch)
         hidden = self.model.forward(self.d_ids[:n], self.d_pos[:n], meta, self.pool.tensor)
         logits = self.model.compute_logits(hidden)
         if not self.is_cuda:

@@ -47,6 +47,7 @@ class AttnMetadata:
     part_o: Optional[torch.Tensor] = None
     part_ml: Optional[torch.Tensor] = None
     attn_cnt: Optional[torch.Tensor] = None  # decode attention merge tickets (int32, zeroed once)
+    scratch: Optional[dict] = None  # fused decode path buffers (CausalLM.alloc_decode_scratch)
 
 
 class LayerWeights:
@@ -156,6 +157,28 @@ class CausalLM:
         self.norm = torch.ones(h, dtype=self.dtype, device=self.device)
         self.lm_head = self._param((self.vocab_local, h), (a.vocab_size, h),
                                    lambda t: self.shard_rows(t, self.vocab_local), std, gen, genf)
+        self.norms_folded = False
+        self.fold_norm_weights()
+
+    def fold_norm_weights(self, layers: Optional[List[int]] = None) -> None:
+        """Fold each dense layer's RMSNorm weights into the projection that consumes the
+        normalised activations: Wqkv <- Wqkv * ln1 (per input feature), Wgate_up <- Wgate_up *
+        ln2, and the norm weights become ones. Mathematically a no-op (rmsnorm(x) * g @ W^T ==
+        rmsnorm(x) @ (W * g)^T); it lets the decode fast path apply the norm as a per-row
+        scale inside the GEMM / attention kernels (no norm kernels in the decode layer).
+        Mixtral keeps its norms (the router also consumes the normalised activations)."""
+        if self.arch.is_moe:
+            return
+        for i, lw in enumerate(self.layers):
+            if layers is not None and i not in layers:
+                continue
+            if not bool((lw.ln1 == 1).all()):
+                lw.qkv.mul_(lw.ln1.to(lw.qkv.dtype)[None, :])
+                lw.ln1.fill_(1)
+            if not bool((lw.ln2 == 1).all()):
+                lw.gate_up.mul_(lw.ln2.to(lw.gate_up.dtype)[None, :])
+                lw.ln2.fill_(1)
+        self.norms_folded = True
 
     def load_state_dict(self, tensors: Dict[str, torch.Tensor]) -> int:
         """Load HF-named Llama/Mixtral weights (already TP-sliced by the caller
@@ -204,6 +227,7 @@ class CausalLM:
         t = take("lm_head.weight")
         if t is not None:
             self.lm_head.copy_(t)
+        self.fold_norm_weights()  # checkpoint norm weights -> folded into Wqkv / Wgate_up
         return n
 
     def weight_bytes(self) -> int:
@@ -226,6 +250,8 @@ class CausalLM:
         hq, hkv = self.hq, self.hkv
         residual = F.embedding(input_ids, self.embed)
         if self._slab_path(input_ids):
+            if meta.scratch is not None and not meta.is_prefill and self._fused_decode_ok(kv_pool):
+                return self._forward_decode_fused(residual, positions, meta, kv_pool)
             return self._forward_decode_slab(residual, positions, meta, kv_pool)
         x = ops.rms_norm(residual, self.layers[0].ln1, eps)
         h = None
@@ -285,6 +311,65 @@ class CausalLM:
             x = ops.fused_add_rms_norm_slab(ops.linear_slab(attn, lw.o), residual, lw.ln2, eps)
             slab = ops.linear_slab(ops.linear_silu_mul(x, lw.gate_up), lw.down)
         return ops.fused_add_rms_norm_slab(slab, residual, self.norm, eps)
+
+    # ----------------------------------------- fused decode path (norms folded, M <= 32)
+    def decode_plan(self) -> dict:
+        """Decode-GEMM tiles of the fused path: (wr, sk) of the qkv slab projection and of the
+        residual-updating o / down projections (wr in {32, 64, 128}: one norm-statistics tile
+        per wr output columns)."""
+        h, d = self.arch.hidden_size, self.head_dim
+        wq, sq = ops._cfg_for(self.layers[0].qkv.shape[0], h, 2)
+
+        def resid_cfg(k):
+            wr, sk = ops._cfg_for(h, k, 2)
+            if wr not in (32, 64, 128) or h % wr:
+                wr = 64 if h % 64 == 0 else 32
+            while sk > 1 and k % (256 * sk):
+                sk //= 2
+            return wr, sk
+
+        return {"qkv": (wq, sq), "o": resid_cfg(self.hq * d), "down": resid_cfg(self.inter)}
+
+    def alloc_decode_scratch(self) -> Optional[dict]:
+        if not (self.device.type == "cuda" and ops.native_available()) or self.tp.enabled or self.arch.is_moe:
+            return None
+        p, h = self.decode_plan(), self.arch.hidden_size
+        f32, i32 = torch.float32, torch.int32
+        to, td = h // p["o"][0], h // p["down"][0]
+        if max(to, td) > 128:
+            return None
+        dev = self.device
+        return {"plan": p, "ssp0": torch.zeros(1, 32, dtype=f32, device=dev),
+                "ssp_a": torch.zeros(to, 32, dtype=f32, device=dev), "cnt_a": torch.zeros(to, dtype=i32, device=dev),
+                "ssp_b": torch.zeros(td, 32, dtype=f32, device=dev), "cnt_b": torch.zeros(td, dtype=i32, device=dev)}
+
+    def _fused_decode_ok(self, kv_pool: torch.Tensor) -> bool:
+        g = self.hq // self.hkv
+        sq = self.decode_plan()["qkv"][1]
+        return (self.norms_folded and self.head_dim == 128 and kv_pool.shape[4] == 16 and g in (1, 2, 4, 8)
+                and ((sq * (g + 2) + 1) // 2) * 1024 + 1536 <= 17408)
+
+    def _forward_decode_fused(self, h: torch.Tensor, positions: torch.Tensor, meta: AttnMetadata,
+                              kv_pool: torch.Tensor) -> torch.Tensor:
+        """Decode layer = 5 launches: qkv (split-K slabs) -> attention (norm scale + slab sum + RoPE
+        + KV write in its prologue) -> o (slabs, last arriver adds into the residual and writes the
+        next norm's row statistics) -> gate/up (norm as a row scale, SiLU*mul) -> down (as o).
+        The residual stream `h` is updated in place; norm weights are folded into Wqkv / Wgate_up."""
+        a, eps = self.arch, self.arch.rms_eps
+        sc, plan = meta.scratch, meta.scratch["plan"]
+        hq, hkv, hid = self.hq, self.hkv, a.hidden_size
+        ssp_prev = ops.row_sumsq(h, out=sc["ssp0"])
+        for li, lw in enumerate(self.layers):
+            k_cache, v_cache = kv_pool[li, 0], kv_pool[li, 1]
+            slab = ops.linear_slab(h, lw.qkv, sk=plan["qkv"][1], wr=plan["qkv"][0])
+            attn = ops.attn_decode_fused(slab, ssp_prev, positions, self.cos_sin, meta.slot_mapping,
+                                         k_cache, v_cache, meta.block_tables, meta.ctx_lens, meta.max_ctx, hq, hkv,
+                                         self.scale, eps, hid, meta.part_o, meta.part_ml, meta.attn_cnt)
+            ops.linear_slab_residual(attn, lw.o, h, sc["ssp_a"], sc["cnt_a"], *plan["o"])
+            act = ops.linear_silu_mul_rownorm(h, lw.gate_up, sc["ssp_a"], eps)
+            ops.linear_slab_residual(act, lw.down, h, sc["ssp_b"], sc["cnt_b"], *plan["down"])
+            ssp_prev = sc["ssp_b"]
+        return ops.rms_norm(h, self.norm, eps)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         logits = ops.linear(hidden, self.lm_head)

@@ -120,6 +120,22 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, max_ctx: int, hq: i
     return out
 
 
+def attn_decode_fused(qkv_slab: torch.Tensor, ssp: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor,
+                      slot_mapping: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                      block_tables: torch.Tensor, ctx_lens: torch.Tensor, max_ctx: int, hq: int, hkv: int,
+                      scale: float, eps: float, hidden: int, part_o: torch.Tensor, part_ml: torch.Tensor,
+                      counters: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Decode attention whose prologue does the input RMSNorm row scale (statistics ssp [T, 32],
+    weight folded into Wqkv), the split-K reduction of the qkv slabs [sk, M, width], RoPE at
+    position ctx-1 and the paged KV write of the new token (attention.hip, FUSED)."""
+    n = ctx_lens.numel()
+    if out is None:
+        out = torch.empty(n, hq * 128, dtype=torch.bfloat16, device=qkv_slab.device)
+    _kern().attn_decode_fused(out, part_o, part_ml, counters, qkv_slab, ssp, positions, cos_sin, slot_mapping,
+                              k_cache, v_cache, block_tables, ctx_lens, max_ctx, hq, hkv, scale, eps, hidden)
+    return out
+
+
 def sample(logits, temperature=None, top_k=None, top_p=None, seeds=None, steps=None,
            out: Optional[torch.Tensor] = None) -> torch.Tensor:
     if not logits.is_cuda:
@@ -184,7 +200,56 @@ def gemm_decode(x: torch.Tensor, w: torch.Tensor, mode: int = 0, wr: int = 64, s
             out = torch.empty(sk, m, n, dtype=torch.float32, device=x.device)
         else:
             out = torch.empty(m, n, dtype=x.dtype, device=x.device)
-    _kern().gemm_decode(out, x, w, mode, wr, sk, DECODE_GEMM_NT if nt is None else nt)
+    e = _empty(x.device)
+    _kern().gemm_decode(out, x, w, mode, wr, sk, DECODE_GEMM_NT if nt is None else nt, e, e, e, e, 0.0)
+    return out
+
+
+_EMPTY: dict = {}
+
+
+def _empty(dev) -> torch.Tensor:
+    t = _EMPTY.get(dev)
+    if t is None:
+        t = _EMPTY[dev] = torch.empty(0, device=dev)
+    return t
+
+
+def linear_slab_residual(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, ssp_out: torch.Tensor,
+                         counters: torch.Tensor, wr: int = 64, sk: int = 4) -> torch.Tensor:
+    """resid += x @ w^T (bf16, in place) with split-K reduced by the last-arriving workgroup of
+    each column tile, which also writes the tile's row sums of squares of the new residual to
+    ssp_out [N/wr, 32] — the statistics of the next RMSNorm (whose weight is folded into the
+    consuming projection). counters [N/wr] int32, zeroed once. Returns the slab scratch."""
+    m, n = x.shape[0], w.shape[0]
+    slab = torch.empty(sk, m, n, dtype=torch.float32, device=x.device)
+    e = _empty(x.device)
+    _kern().gemm_decode(slab, x, w, 3, wr, sk, DECODE_GEMM_NT, resid, ssp_out, counters, e, 0.0)
+    return slab
+
+
+def linear_silu_mul_rownorm(x: torch.Tensor, w_gate_up: torch.Tensor, ssp_in: torch.Tensor, eps: float,
+                            wr: Optional[int] = None) -> torch.Tensor:
+    """silu(r * x @ gate^T) * (r * x @ up^T) with r = rsqrt(sum_t ssp_in[t] / K + eps) per row:
+    RMSNorm (weight folded into w_gate_up) + gate/up + SiLU*mul in one weight stream."""
+    n = w_gate_up.shape[0] // 2
+    if wr is None:
+        wr, _ = _cfg_for(n, x.shape[1], 1)
+    out = torch.empty(x.shape[0], n, dtype=x.dtype, device=x.device)
+    e = _empty(x.device)
+    _kern().gemm_decode(out, x, w_gate_up, 4, wr, 1, DECODE_GEMM_NT, e, e, e, ssp_in, float(eps))
+    return out
+
+
+def row_sumsq(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[1, 32] fp32 per-row sums of squares of x [M <= 32, H] (RMSNorm statistics)."""
+    if out is None:
+        out = torch.zeros(1, 32, dtype=torch.float32, device=x.device)
+    if not x.is_cuda:
+        out.zero_()
+        out[0, : x.shape[0]] = x.float().pow(2).sum(-1)
+        return out
+    _kern().row_sumsq(out, x)
     return out
 
 

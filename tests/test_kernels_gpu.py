@@ -300,3 +300,91 @@ def test_rope_and_cache_slab(dev):
     close(q, qkv[:, : hq * 128], atol=3e-2, rtol=2e-2)
     close(kc, kr, atol=3e-2, rtol=2e-2)
     close(vc, vr, atol=2e-2, rtol=1e-2)
+
+
+# ---------------------------------------------------------------- fused decode path pieces
+@pytest.mark.parametrize("wr,sk,k", [(64, 4, 4096), (64, 4, 14336), (32, 1, 2048), (128, 2, 4096)])
+def test_gemm_decode_residual_mode(dev, wr, sk, k):
+    """mode 3: resid += x @ w^T with the split-K reduced by the last-arriving workgroup, which
+    also writes the per-tile row sums of squares of the new residual."""
+    m, h = 27, 4096
+    x = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(h, k, device=dev, dtype=torch.bfloat16) / math.sqrt(k)
+    res = torch.randn(m, h, device=dev, dtype=torch.bfloat16)
+    t = h // wr
+    ssp = torch.full((t, 32), -1.0, device=dev)
+    cnt = torch.zeros(t, dtype=torch.int32, device=dev)
+    for it in range(2):  # tickets are re-armed: a second launch works too
+        r0 = res.clone()
+        ops.linear_slab_residual(x, w, res, ssp, cnt, wr, sk)
+        expect = (r0.float() + x.float() @ w.float().t()).to(torch.bfloat16)
+        close(res, expect, atol=3e-2, rtol=1e-2)
+        ss_ref = res.float().pow(2).view(m, t, wr).sum(-1).t()       # [t, m]
+        close(ssp[:, :m], ss_ref, atol=1e-2, rtol=1e-3)
+        assert torch.all(ssp[:, m:] == 0)
+        assert int(cnt.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("m,inter,k,wr", [(32, 14336, 4096, 112), (7, 2048, 1024, 64)])
+def test_gemm_decode_rownorm_silu(dev, m, inter, k, wr):
+    """mode 4: RMSNorm (weight folded into W) as a per-row scale + gate/up + SiLU*mul."""
+    x = torch.randn(m, k, device=dev, dtype=torch.bfloat16) * 3
+    w = torch.randn(2 * inter, k, device=dev, dtype=torch.bfloat16) / math.sqrt(k)
+    ss = x.float().pow(2)
+    t = 64 if k % 64 == 0 else 1
+    ssp = torch.zeros(t, 32, device=dev)
+    ssp[:, :m] = ss.view(m, t, -1).sum(-1).t()
+    y = ops.linear_silu_mul_rownorm(x, w, ssp, 1e-5, wr)
+    xn = x.float() * torch.rsqrt(ss.mean(-1, keepdim=True) + 1e-5)
+    hh = xn @ w.float().t()
+    r = torch.nn.functional.silu(hh[:, :inter]) * hh[:, inter:]
+    close(y, r, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("g,hkv", [(4, 8), (8, 1), (1, 4)])
+def test_attn_decode_fused(dev, g, hkv):
+    """Fused prologue: norm scale + qkv slab sum + RoPE at ctx-1 + KV write, then attention."""
+    hq, sk, bs, d = hkv * g, 2, 16, 128
+    hid = 1024
+    ctxs = [1, 17, 200, 777, 2049]
+    n = len(ctxs)
+    width = (hq + 2 * hkv) * d
+    _, kc, vc, bt, _, ctx, _ = _make_seqs([1] * n, ctxs, hkv, bs, dev, g)
+    max_ctx = 4096
+    bt_wide = torch.zeros(n, max_ctx // bs, dtype=torch.int32, device=dev)
+    bt_wide[:, : bt.shape[1]] = bt
+    slab = torch.randn(sk, n, width, device=dev) * 0.7   # normalised q/k/v ~ N(0, 1): realistic scores
+    ssv = (torch.rand(n, device=dev) + 0.5) * hid
+    ssp = torch.zeros(4, 32, device=dev)
+    ssp[:, :n] = (ssv / 4)[None, :]                     # 4 tiles summing to ssv
+    slots = torch.tensor([int(bt[i, (c - 1) // bs]) * bs + (c - 1) % bs for i, c in enumerate(ctxs)],
+                         dtype=torch.long, device=dev)
+    slots[1] = -1                                        # a padded row: no cache write
+    pos = (ctx - 1).long()
+    cs = ref.rope_cos_sin(8192, d, 500000.0, dev)
+    maxp = ops.decode_partials(max_ctx)
+    po = torch.empty(n * hq * maxp * d, device=dev)
+    pm = torch.empty(n * hq * maxp * 2, device=dev)
+    cnt = torch.zeros(n * hkv, dtype=torch.int32, device=dev)
+    kr, vr = kc.clone(), vc.clone()
+    scale = 1 / math.sqrt(d)
+    out = ops.attn_decode_fused(slab, ssp, pos, cs, slots, kc, vc, bt_wide, ctx, max_ctx, hq, hkv, scale, 1e-5,
+                                hid, po, pm, cnt)
+    # reference: normalise the summed projection, rope + cache, attention
+    rn = torch.rsqrt(ssv / hid + 1e-5)
+    qkv = (slab.sum(0) * rn[:, None]).to(torch.bfloat16)
+    slots_ref = slots.clone()
+    ref.rope_and_cache(qkv, pos.cpu(), cs, slots_ref.cpu(), kr, vr, hq, hkv, d)
+    # row 1 is "padded": its new token is not written; the kernel still attends to it via LDS
+    blk, off = int(bt[1, (ctxs[1] - 1) // bs]), (ctxs[1] - 1) % bs
+    k1 = ref.apply_rope(qkv[1:2, hq * d:(hq + hkv) * d].view(1, hkv, d), pos[1:2].cpu(), cs)
+    kr2, vr2 = kr.clone(), vr.clone()
+    kr2[blk, :, off] = k1[0]
+    vr2[blk, :, off] = qkv[1, (hq + hkv) * d:].view(hkv, d)
+    cu = torch.arange(n + 1, dtype=torch.int32, device=dev)
+    r = ref.attention(qkv[:, : hq * d], kr2, vr2, bt, cu, ctx, hq, hkv, scale).reshape(n, -1)
+    close(out, r, atol=3e-2, rtol=3e-2)
+    # the cache got the new tokens (except the padded row); the kernel rotates before rounding
+    close(kc, kr, atol=3e-2, rtol=2e-2)
+    close(vc, vr, atol=3e-2, rtol=2e-2)
+    assert int(cnt.abs().sum()) == 0
