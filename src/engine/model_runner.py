@@ -68,6 +68,10 @@ class ModelRunner:
         self.max_model_len = max_model_len
         self.bt_width = (max_model_len + self.bs - 1) // self.bs
         self.rt = native_runtime()
+        if self.is_cuda:
+            from src.ops.gemm_tuning import enable_tuned_gemms
+
+            enable_tuned_gemms()  # prefill GEMM solutions measured on MI355X (configs/)
         self.max_seqs = cfg.max_num_seqs
         self.max_tokens = max(cfg.max_num_batched_tokens, self.max_seqs)
         pin = self.is_cuda
