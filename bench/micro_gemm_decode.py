@@ -53,6 +53,8 @@ def main():
     m = int(sys.argv[1]) if len(sys.argv) > 1 else 32
     if len(sys.argv) > 2 and sys.argv[2] == "nt":
         return main_nt(m)
+    if len(sys.argv) > 2 and sys.argv[2] == "resid":
+        return main_resid(m)
     dev = torch.device("cuda:0")
     for name, (n, k, silu) in SHAPES.items():
         wrows = 2 * n if silu else n
@@ -100,6 +102,30 @@ def main_nt(m):
             us = timeit(lambda w: ops.gemm_decode(x, w, mode, wr, sk, nt=nt), ws)
             print(json.dumps({"shape": name, "M": m, "mode": mode, "wr": wr, "sk": sk, "nt": nt, "us": round(us, 2),
                               "GBps": round(wbytes / us / 1e3, 1)}), flush=True)
+        del ws
+        torch.cuda.empty_cache()
+
+
+
+def main_resid(m):
+    """Mode 3 (split-K + last-arriver residual update + norm statistics) tile sweep."""
+    dev = torch.device("cuda:0")
+    for name, (n, k) in {"o_8b": (4096, 4096), "down_8b": (4096, 14336)}.items():
+        x = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
+        wbytes = n * k * 2
+        copies = max(2, int(1.5 * 2**30 // wbytes) + 1)
+        ws = [torch.randn(n, k, device=dev, dtype=torch.bfloat16) / 64 for _ in range(copies)]
+        res = torch.randn(m, n, device=dev, dtype=torch.bfloat16)
+        for wr in (32, 64, 128):
+            for sk in (1, 2, 4, 8):
+                kc = 128 if wr >= 96 else 256
+                if k % (kc * sk) or (n // wr) * sk > 1024:
+                    continue
+                ssp = torch.zeros(n // wr, 32, device=dev)
+                cnt = torch.zeros(n // wr, dtype=torch.int32, device=dev)
+                us = timeit(lambda w: ops.linear_slab_residual(x, w, res, ssp, cnt, wr, sk), ws)
+                print(json.dumps({"shape": name, "M": m, "mode": 3, "wr": wr, "sk": sk, "us": round(us, 2),
+                                  "GBps": round(wbytes / us / 1e3, 1)}), flush=True)
         del ws
         torch.cuda.empty_cache()
 

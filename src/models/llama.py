@@ -321,6 +321,9 @@ class CausalLM:
         wq, sq = ops._cfg_for(self.layers[0].qkv.shape[0], h, 2)
 
         def resid_cfg(k):
+            c = ops.DECODE_GEMM_RESID_CFG.get((h, k))
+            if c is not None:
+                return c
             wr, sk = ops._cfg_for(h, k, 2)
             if wr not in (32, 64, 128) or h % wr:
                 wr = 64 if h % 64 == 0 else 32

@@ -268,6 +268,11 @@ DECODE_GEMM_CFG = {
     (8192, 3584, 0): (32, 1),      # 70B TP=8 down_proj         (13.3 vs 15.6)
 }
 DECODE_GEMM_MAX_N = 262144
+# mode 3 (split-K + last-arriver residual update), (N, K) -> (wr, sk); micro_gemm_decode.py resid
+DECODE_GEMM_RESID_CFG = {
+    (4096, 4096): (32, 2),     # 8B o_proj   11.5 us (64/4: 12.8)
+    (4096, 14336): (32, 2),    # 8B down     26.6 us (64/4: 27.3)
+}
 
 
 def _cfg_for(n: int, k: int, mode: int):
