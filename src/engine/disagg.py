@@ -53,12 +53,12 @@ class DisaggregatedServer:
             pseq.sampling = sampling
             return pseq
         t0 = time.perf_counter()
-        kv = ship(pseq.kv_export, self.decode.engine.device)
-        self.transfer_s += time.perf_counter() - t0
+        kv, ready = ship(pseq.kv_export, self.decode.engine.device, getattr(pseq, "kv_export_ready", None))
+        self.transfer_s += time.perf_counter() - t0   # issue time: the copy itself is asynchronous
         self.transfers += 1
         self.bytes_moved += kv.numel() * kv.element_size()
         packet = KVPacket(rid, list(prompt_ids), pseq.output_ids[0], kv, self.prefill.engine.cfg.block_size,
-                          ttft_ms=pseq.ttft_ms())
+                          ttft_ms=pseq.ttft_ms(), ready=ready)
         pseq.kv_export = None
         return await self.decode.submit(rid, [], sampling, user_data={"import_packet": packet})
 

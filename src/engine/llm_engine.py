@@ -124,6 +124,10 @@ class LLMEngine:
         if packet.kv.shape[0] != nb:
             self.blocks.free(seq)
             raise ValueError(f"packet has {packet.kv.shape[0]} blocks, prompt needs {nb}")
+        if getattr(packet, "ready", None) is not None:  # shipped on a transfer stream
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_event(packet.ready)
+            packet.kv.record_stream(cur)
         import_blocks(self.pool.planes(), seq.block_table[:nb], packet.kv)
         seq.num_computed = seq.prompt_len
         self.seqs[seq.request_id] = seq
@@ -205,6 +209,10 @@ class LLMEngine:
 
                 nb = self.blocks.blocks_needed(seq.prompt_len)
                 seq.kv_export = export_blocks(self.pool.planes(), seq.block_table[:nb])  # type: ignore[attr-defined]
+                if seq.kv_export.is_cuda:  # consumers wait on this instead of a host sync
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    seq.kv_export_ready = ev  # type: ignore[attr-defined]
             self.scheduler.finish(seq, reason)
             finished.append(seq)
             self._complete(seq)

@@ -38,6 +38,7 @@ class KVPacket:
     block_size: int
     sampling: Dict[str, Any] = field(default_factory=dict)
     ttft_ms: Optional[float] = None
+    ready: Any = None                # HIP event: kv is complete on its device (None = already complete)
 
     @property
     def nbytes(self) -> int:
@@ -57,15 +58,38 @@ def import_blocks(pool_planes: torch.Tensor, block_ids: List[int], buf: torch.Te
     ops.scatter_blocks(pool_planes, ids, buf.contiguous())
 
 
-def ship(buf: torch.Tensor, device) -> torch.Tensor:
-    """Peer copy to another GPU (hipMemcpyPeerAsync over xGMI) or a no-op."""
+_XFER_STREAMS: Dict[Any, Any] = {}
+
+
+def _transfer_stream(device: torch.device):
+    s = _XFER_STREAMS.get(device)
+    if s is None:
+        s = _XFER_STREAMS[device] = torch.cuda.Stream(device=device)
+    return s
+
+
+def ship(buf: torch.Tensor, device, ready=None):
+    """Move a staging tensor to ``device`` without a host sync: peer copy
+    (hipMemcpyPeerAsync over xGMI) on a dedicated per-device transfer stream that
+    first waits for ``ready`` (the prefill engine's gather); returns ``(tensor, event)``
+    where the event marks the copy's completion — the decode engine makes its
+    stream wait on it before scattering the blocks. Same device: no copy."""
     device = torch.device(device)
     if buf.device == device:
-        return buf
-    out = buf.to(device, non_blocking=True)
-    if device.type == "cuda":
-        torch.cuda.current_stream(device).synchronize()
-    return out
+        return buf, ready
+    if device.type != "cuda" or buf.device.type != "cuda":
+        if ready is not None:
+            ready.synchronize()
+        return buf.to(device), None
+    s = _transfer_stream(device)
+    with torch.cuda.stream(s):
+        if ready is not None:
+            s.wait_event(ready)
+        out = buf.to(device, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record(s)
+    buf.record_stream(s)   # the source block may not be reused before the copy has read it
+    return out, done
 
 
 def packet_to_wire(p: KVPacket) -> Dict[str, Any]:
