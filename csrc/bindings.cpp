@@ -415,6 +415,36 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
                                   (int)wr, (int)sk, nt, fz, cur_stream()));
 }
 
+// Grouped (MoE) decode GEMM: x [R, K] token-sorted activations (expert e owns rows
+// [offsets[e], offsets[e+1]), at most 32 of them — one decode step), w [E, rows, K] stacked
+// expert weights, y [R, N] bf16. mode 1: w[e] = [gate; up] -> silu(gate)*up (N = rows/2);
+// mode 0: plain. Experts with no rows stream no weights.
+void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t mode, int64_t wr) {
+  DIE_CHECK_CUDA(x);
+  DIE_CHECK_BF16(x);
+  DIE_CHECK_BF16(w);
+  DIE_CHECK_BF16(y);
+  DIE_CHECK_CONTIG(w);
+  check_rows(x, "x");
+  check_rows(y, "y");
+  DIE_CHECK_DTYPE(offsets, at::kInt);
+  TORCH_CHECK(mode == 0 || mode == 1, "grouped: mode 0 or 1");
+  TORCH_CHECK(w.dim() == 3 && w.size(2) == x.size(1), "w [E, rows, K]");
+  const int64_t E = w.size(0), K = x.size(1);
+  TORCH_CHECK(offsets.numel() >= E + 1, "offsets [E+1]");
+  const int64_t N = mode == 1 ? w.size(1) / 2 : w.size(1);
+  TORCH_CHECK(y.size(0) == x.size(0) && y.size(1) == N, "y [R, N]");
+  TORCH_CHECK(wr == 32 || wr == 48 || wr == 64 || wr == 96 || wr == 112 || wr == 128, "wr");
+  const int64_t kc = wr >= 96 ? 128 : 256;
+  TORCH_CHECK(K % kc == 0 && N % (mode == 1 ? wr / 2 : wr) == 0, "tile shape");
+  die::GemmDecodeFuse fz;
+  fz.grp_off = offsets.data_ptr<int>();
+  fz.grp_wstride = w.size(1) * K;
+  fz.grp_n = (int)E;
+  DIE_HIP(die::launch_gemm_decode(y.data_ptr(), y.stride(0), bf(x), x.stride(0), bf(w), 32, (int)N, (int)K, (int)mode,
+                                  (int)wr, 1, true, fz, cur_stream()));
+}
+
 void row_sumsq(Tensor ssp, Tensor x) {
   DIE_CHECK_CUDA(x);
   DIE_CHECK_BF16(x);
@@ -491,6 +521,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_grouped_gemm", &moe_grouped_gemm);
   m.def("gemm_decode", &gemm_decode);
   m.def("row_sumsq", &row_sumsq);
+  m.def("gemm_decode_grouped", &gemm_decode_grouped);
   m.def("fused_add_rms_norm_slab", &fused_add_rms_norm_slab);
   m.def("rope_and_cache_slab", &rope_and_cache_slab);
 }

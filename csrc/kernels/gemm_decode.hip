@@ -75,6 +75,17 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
   static_assert((S - 1) * PER_WAVE <= 63, "vmcnt field is 6 bits");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (fz.grp_off != nullptr) {
+    // grouped (MoE) form: blockIdx.z = expert; its rows of X/Y are [off[e], off[e+1]) of the
+    // token-sorted activations, its weights W + e * grp_wstride. Unused experts cost nothing.
+    const int e = blockIdx.z;
+    const int r0 = fz.grp_off[e];
+    M = min(fz.grp_off[e + 1] - r0, MR);
+    if (M <= 0) return;
+    X += (int64_t)r0 * ldx;
+    W += (int64_t)e * fz.grp_wstride;
+    Yv = reinterpret_cast<char*>(Yv) + (int64_t)r0 * ldy * (EPI == 2 || EPI == 3 ? 4 : 2);
+  }
   const int n0 = blockIdx.x * NO;
   const int kper = K / gridDim.y;
   const int k0 = blockIdx.y * kper;
@@ -289,11 +300,11 @@ static hipError_t launch_gd(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, 
   if (N_out % NO || K % sk || (K / sk) % KC) return hipErrorInvalidValue;
   const size_t lds = (size_t)S * (WR + MR) * KC * 2;
   if (nt)
-    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, true, KC>), dim3(N_out / NO, sk), dim3(NTH), lds, s, Y, ldy,
-                       X, ldx, W, M, N_out, K, fz);
+    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, true, KC>), dim3(N_out / NO, sk, fz.grp_n), dim3(NTH), lds,
+                       s, Y, ldy, X, ldx, W, M, N_out, K, fz);
   else
-    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, false, KC>), dim3(N_out / NO, sk), dim3(NTH), lds, s, Y, ldy,
-                       X, ldx, W, M, N_out, K, fz);
+    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, false, KC>), dim3(N_out / NO, sk, fz.grp_n), dim3(NTH), lds,
+                       s, Y, ldy, X, ldx, W, M, N_out, K, fz);
   return hipGetLastError();
 }
 

@@ -70,6 +70,9 @@ struct GemmDecodeFuse {
   int ssp_tiles = 0;
   float inv_n = 0.f;             // 1 / hidden size
   float eps = 0.f;
+  const int* grp_off = nullptr;  // grouped (MoE) form: expert row offsets [grp_n + 1] (device)
+  int64_t grp_wstride = 0;       //   elements between experts' weight matrices
+  int grp_n = 1;                 //   number of experts (grid z)
 };
 hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,
                               int K, int mode, int wr, int sk, bool nt, const GemmDecodeFuse& fz, hipStream_t s);

@@ -379,15 +379,44 @@ def moe_forward(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, gating: to
     kern = _kern()
     t, hdim = x.shape
     e = w13.shape[0]
+    inter = w13.shape[1] // 2
     w, ids = topk_softmax(gating, k, renorm)
     offsets, sorted_idx, pos = moe_align(ids, e)
     xs = torch.empty(t * k, hdim, dtype=x.dtype, device=x.device)
     kern.moe_gather(xs, x, sorted_idx, k)
-    h = torch.empty(t * k, w13.shape[1], dtype=x.dtype, device=x.device)
-    kern.moe_grouped_gemm(h, xs, w13, offsets)
-    a = silu_and_mul(h)
     ys = torch.empty(t * k, hdim, dtype=x.dtype, device=x.device)
-    kern.moe_grouped_gemm(ys, a, w2, offsets)
+    if t <= DECODE_GEMM_MAX_M and _moe_decode_ok(hdim, inter):
+        # decode: every expert's weights streamed once by the weight-streaming kernel, its
+        # (<= 32) routed tokens riding along; SiLU*mul fused; idle experts read nothing
+        a = torch.empty(t * k, inter, dtype=x.dtype, device=x.device)
+        kern.gemm_decode_grouped(a, xs, w13, offsets, 1, _cfg_for(inter, hdim, 1)[0])
+        kern.gemm_decode_grouped(ys, a, w2, offsets, 0, _moe_down_wr(hdim, inter))
+    elif t >= MOE_LIBRARY_MIN_TOKENS and not torch.cuda.is_current_stream_capturing():
+        # prefill: the per-expert groups are thousands of rows — hipBLASLt GEMMs per expert at
+        # ~1.5 PF/s beat the device-offset grouped kernel; costs one host read of the offsets
+        off = offsets.tolist()
+        for ei in range(e):
+            a0, a1 = off[ei], off[ei + 1]
+            if a1 > a0:
+                act = silu_and_mul(torch.nn.functional.linear(xs[a0:a1], w13[ei]))
+                torch.nn.functional.linear(act, w2[ei], out=ys[a0:a1])
+    else:
+        h = torch.empty(t * k, w13.shape[1], dtype=x.dtype, device=x.device)
+        kern.moe_grouped_gemm(h, xs, w13, offsets)
+        a = silu_and_mul(h)
+        kern.moe_grouped_gemm(ys, a, w2, offsets)
     out = torch.empty_like(x)
     kern.moe_combine(out, ys, pos, w)
     return out
+
+
+MOE_LIBRARY_MIN_TOKENS = 256
+
+
+def _moe_decode_ok(hdim: int, inter: int) -> bool:
+    wr1 = _cfg_for(inter, hdim, 1)[0]
+    return hdim % 256 == 0 and inter % 256 == 0 and inter % (wr1 // 2) == 0 and hdim % 64 == 0
+
+
+def _moe_down_wr(hdim: int, inter: int) -> int:
+    return 64 if hdim % 64 == 0 else 32

@@ -227,8 +227,9 @@ def test_block_movers(dev):
     assert torch.equal(other[:, ids], pool[:, ids])
 
 
-def test_moe(dev):
-    t, h, inter, e, k = 77, 512, 256, 8, 2
+@pytest.mark.parametrize("t", [5, 32, 77, 600])  # decode streaming / grouped kernel / per-expert hipBLASLt
+def test_moe(dev, t):
+    h, inter, e, k = 512, 256, 8, 2
     x = torch.randn(t, h, device=dev, dtype=torch.bfloat16)
     gating = torch.randn(t, e, device=dev, dtype=torch.bfloat16)
     w13 = torch.randn(e, 2 * inter, h, device=dev, dtype=torch.bfloat16) / math.sqrt(h)
