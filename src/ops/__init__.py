@@ -268,10 +268,12 @@ DECODE_GEMM_CFG = {
     (8192, 3584, 0): (32, 1),      # 70B TP=8 down_proj         (13.3 vs 15.6)
 }
 DECODE_GEMM_MAX_N = 262144
-# mode 3 (split-K + last-arriver residual update), (N, K) -> (wr, sk); micro_gemm_decode.py resid
+# mode 3 (split-K + last-arriver residual update), (N, K) -> (wr, sk). In isolation
+# (micro_gemm_decode.py resid) wr32/sk2 wins by ~1 us, but inside the decode graph wr64/sk4
+# is faster (bench decode 4.07 -> 3.93 ms/step): keep what the real step measures.
 DECODE_GEMM_RESID_CFG = {
-    (4096, 4096): (32, 2),     # 8B o_proj   11.5 us (64/4: 12.8)
-    (4096, 14336): (32, 2),    # 8B down     26.6 us (64/4: 27.3)
+    (4096, 4096): (64, 4),     # 8B o_proj
+    (4096, 14336): (64, 4),    # 8B down
 }
 
 
