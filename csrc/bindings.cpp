@@ -445,6 +445,25 @@ void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t m
                                   (int)wr, 1, true, fz, cur_stream()));
 }
 
+// Decode-step input advance (decode_step.hip), for multi-step decode windows.
+void decode_advance(Tensor out, Tensor ids, Tensor pos, Tensor ctx, Tensor slots, Tensor bt, Tensor step,
+                    Tensor tokens, Tensor cnt, Tensor n_real, int64_t rows, int64_t block_size) {
+  DIE_CHECK_CUDA(out);
+  for (const Tensor* t : {&out, &ids, &pos, &slots, &step, &tokens}) DIE_CHECK_DTYPE((*t), at::kLong);
+  for (const Tensor* t : {&ctx, &bt, &cnt, &n_real}) DIE_CHECK_DTYPE((*t), at::kInt);
+  DIE_CHECK_CONTIG(bt);
+  DIE_CHECK_CONTIG(tokens);
+  TORCH_CHECK(rows <= out.numel() && rows <= ids.numel() && rows <= pos.numel() && rows <= ctx.numel() &&
+                  rows <= slots.numel() && rows <= step.numel() && rows <= bt.size(0) && rows <= tokens.size(1),
+              "decode_advance: buffers smaller than rows");
+  TORCH_CHECK(tokens.dim() == 2 && bt.dim() == 2, "tokens [K, S], bt [S, W]");
+  DIE_HIP(die::launch_decode_advance(out.data_ptr<int64_t>(), ids.data_ptr<int64_t>(), pos.data_ptr<int64_t>(),
+                                     ctx.data_ptr<int>(), slots.data_ptr<int64_t>(), bt.data_ptr<int>(),
+                                     (int)bt.size(1), step.data_ptr<int64_t>(), tokens.data_ptr<int64_t>(),
+                                     (int)tokens.size(1), cnt.data_ptr<int>(), n_real.data_ptr<int>(), (int)rows,
+                                     (int)block_size, (int)tokens.size(0), cur_stream()));
+}
+
 void row_sumsq(Tensor ssp, Tensor x) {
   DIE_CHECK_CUDA(x);
   DIE_CHECK_BF16(x);
@@ -521,6 +540,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_grouped_gemm", &moe_grouped_gemm);
   m.def("gemm_decode", &gemm_decode);
   m.def("row_sumsq", &row_sumsq);
+  m.def("decode_advance", &decode_advance);
   m.def("gemm_decode_grouped", &gemm_decode_grouped);
   m.def("fused_add_rms_norm_slab", &fused_add_rms_norm_slab);
   m.def("rope_and_cache_slab", &rope_and_cache_slab);

@@ -82,6 +82,9 @@ class EngineConfig:
     use_cuda_graph: bool = True
     graph_batch_sizes: List[int] = field(default_factory=lambda: [1, 2, 4, 8, 16, 24, 32])
     decode_partition_size: int = 256
+    # decode steps replayed back to back on the GPU per host round trip when nothing is waiting
+    # for admission (inputs advanced on the device; see src/engine/model_runner.py decode_multi)
+    decode_window: int = 8
 
 
 @dataclass

@@ -179,16 +179,38 @@ class LLMEngine:
                     seq.first_token_time = now
                 self._append(seq, tok, finished)
         else:
-            toks = self.runner.decode(out.decode)
+            k = self._decode_window(out.decode)
+            toks_k = self.runner.decode_multi(out.decode, k) if k > 1 else [self.runner.decode(out.decode)]
             now = time.perf_counter()
             self.stats["decode_time"] += now - t0
-            for seq, tok in zip(out.decode, toks):
-                seq.num_computed += 1
-                self._append(seq, tok, finished)
+            for toks in toks_k:
+                for seq, tok in zip(out.decode, toks):
+                    if seq.status == SeqStatus.FINISHED:  # stopped earlier in the window: discard
+                        continue
+                    seq.num_computed += 1
+                    self._append(seq, tok, finished)
+            self.stats["decode_windows"] = self.stats.get("decode_windows", 0) + 1
         self.stats["steps"] += 1
         if self.cfg.kv_block_ttl_s:
             self.blocks.evict_expired()
         return finished
+
+    def _decode_window(self, seqs: List[Sequence]) -> int:
+        """How many decode steps to run before the host looks again: 1 while requests wait for
+        admission (they must not sit behind a window), otherwise up to cfg.decode_window, no
+        further than the longest remaining generation and the context limit, and only if KV
+        slots for the whole window can be reserved now."""
+        kmax = int(getattr(self.cfg, "decode_window", 1))
+        if kmax <= 1 or not getattr(self.runner, "supports_multistep", False) or self.scheduler.waiting:
+            return 1
+        k = min(kmax, max(s.sampling.max_tokens - len(s.output_ids) for s in seqs),
+                min(self.max_model_len - len(s) + 1 for s in seqs))
+        if k <= 1:
+            return 1
+        for s in seqs:
+            if not self.blocks.ensure_slots(s, len(s) + k - 1):
+                return 1
+        return k
 
     def _append(self, seq: Sequence, tok: int, finished: List[Sequence]) -> None:
         seq.output_ids.append(int(tok))

@@ -90,6 +90,9 @@ class ModelRunner:
         self.h_seed = torch.zeros(self.max_seqs, dtype=i64, pin_memory=pin)
         self.h_step = torch.zeros(self.max_seqs, dtype=i64, pin_memory=pin)
         self.h_out = torch.zeros(self.max_seqs, dtype=i64, pin_memory=pin)
+        self.k_max = max(1, int(getattr(cfg, "decode_window", 1)))
+        self.h_tokens = torch.zeros(self.k_max, self.max_seqs, dtype=i64, pin_memory=pin)
+        self.h_ctl = torch.zeros(2, dtype=i32, pin_memory=pin)   # [window step counter, real rows]
         # numpy views over the pinned buffers (zero-copy) for cheap bulk writes
         self.n_ids, self.n_temp, self.n_topk = self.h_ids.numpy(), self.h_temp.numpy(), self.h_topk.numpy()
         self.n_topp, self.n_seed, self.n_step = self.h_topp.numpy(), self.h_seed.numpy(), self.h_step.numpy()
@@ -109,6 +112,8 @@ class ModelRunner:
         self.d_seed = torch.zeros(self.max_seqs, dtype=i64, device=dev)
         self.d_step = torch.zeros(self.max_seqs, dtype=i64, device=dev)
         self.d_out = torch.zeros(self.max_seqs, dtype=i64, device=dev)
+        self.d_tokens = torch.zeros(self.k_max, self.max_seqs, dtype=i64, device=dev)
+        self.d_ctl = torch.zeros(2, dtype=i32, device=dev)
         if self.is_cuda:
             maxp = ops.decode_partials(max_model_len)
             hq = model.hq
@@ -118,6 +123,7 @@ class ModelRunner:
             self.dec_scratch = model.alloc_decode_scratch() if hasattr(model, "alloc_decode_scratch") else None
         else:
             self.part_o = self.part_ml = self.attn_cnt = self.dec_scratch = None
+        self.supports_multistep = self.is_cuda and self.k_max > 1 and type(self)._sync_step is ModelRunner._sync_step
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_sizes: List[int] = []
         self._graph_pool = None
@@ -235,8 +241,13 @@ class ModelRunner:
         if not self.is_cuda:
             return ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
                               self.d_step[:n])
-        return ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
-                          self.d_step[:n], out=self.d_out[:n])
+        out = ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
+                         self.d_step[:n], out=self.d_out[:n])
+        if self.supports_multistep:
+            # next step's inputs from this step's samples, on the device (multi-step windows)
+            ops.decode_advance(self.d_out, self.d_ids, self.d_pos, self.d_ctx, self.d_slots, self.d_bt, self.d_step,
+                               self.d_tokens, self.d_ctl[0:1], self.d_ctl[1:2], n, self.bs)
+        return out
 
     @torch.inference_mode()
     def capture_graphs(self) -> None:
@@ -280,6 +291,35 @@ class ModelRunner:
         self._sync_step(self.KIND_DECODE, n, pad)
         ids = self._exec_decode(n, pad)
         return self._to_host(ids, n)
+
+    @torch.inference_mode()
+    def decode_multi(self, seqs: List[Sequence], k: int) -> List[List[int]]:
+        """k decode steps for the same batch in one host round trip: the step's hipGraph ends
+        with a device-side input advance (sampled ids -> next ids, positions/context/step + 1,
+        next slot from the block table), so the graph is replayed k times back to back and the
+        k x n sampled tokens come back in one copy. The caller has reserved KV slots for the
+        k positions. Falls back to single steps where no graph covers the batch."""
+        n = len(seqs)
+        pad = self._pad_for(n)
+        g = self.graphs.get(pad)
+        if k <= 1 or g is None or not self.supports_multistep:
+            return [self.decode(seqs)]
+        k = min(k, self.k_max)
+        self.n_ids[:n] = [s.last_token for s in seqs]
+        self.n_ids[n:pad] = 0
+        self.rt.build_decode_inputs([s.block_table for s in seqs], [len(s) for s in seqs], self.bs,
+                                    self.h_pos.data_ptr(), self.h_slots.data_ptr(), self.h_ctx.data_ptr(),
+                                    self.h_bt.data_ptr(), self.bt_width, pad)
+        self._fill_sampling(seqs, pad)
+        self._h2d(pad, pad, with_cu=False)
+        self.h_ctl[0] = 0
+        self.h_ctl[1] = n
+        self.d_ctl.copy_(self.h_ctl, non_blocking=True)
+        for _ in range(k):
+            g.replay()
+        self.h_tokens[:k].copy_(self.d_tokens[:k], non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        return self.h_tokens[:k, :n].tolist()
 
     def _exec_decode(self, n: int, pad: int) -> torch.Tensor:
         g = self.graphs.get(pad)

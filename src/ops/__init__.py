@@ -136,6 +136,11 @@ def attn_decode_fused(qkv_slab: torch.Tensor, ssp: torch.Tensor, positions: torc
     return out
 
 
+def decode_advance(out, ids, pos, ctx, slots, bt, step, tokens, cnt, n_real, rows: int, block_size: int) -> None:
+    """Device-side advance of the decode inputs (decode_step.hip); see ModelRunner.decode_multi."""
+    _kern().decode_advance(out, ids, pos, ctx, slots, bt, step, tokens, cnt, n_real, rows, block_size)
+
+
 def sample(logits, temperature=None, top_k=None, top_p=None, seeds=None, steps=None,
            out: Optional[torch.Tensor] = None) -> torch.Tensor:
     if not logits.is_cuda:
