@@ -55,6 +55,10 @@ def main():
         return main_nt(m)
     if len(sys.argv) > 2 and sys.argv[2] == "resid":
         return main_resid(m)
+    if len(sys.argv) > 2 and sys.argv[2] == "warm":
+        return main_warm(m)
+    if len(sys.argv) > 2 and sys.argv[2] == "deep":
+        return main_deep(m)
     dev = torch.device("cuda:0")
     for name, (n, k, silu) in SHAPES.items():
         wrows = 2 * n if silu else n
@@ -126,6 +130,54 @@ def main_resid(m):
                 us = timeit(lambda w: ops.linear_slab_residual(x, w, res, ssp, cnt, wr, sk), ws)
                 print(json.dumps({"shape": name, "M": m, "mode": 3, "wr": wr, "sk": sk, "us": round(us, 2),
                                   "GBps": round(wbytes / us / 1e3, 1)}), flush=True)
+        del ws
+        torch.cuda.empty_cache()
+
+
+def main_warm(m):
+    """Same weights every call (Infinity-Cache resident when they fit in 256 MB) vs cold copies:
+    what a weight prefetch into the MALL could buy each decode projection."""
+    dev = torch.device("cuda:0")
+    for name, (n, k, silu) in SHAPES.items():
+        if name.startswith("lm_head") or "70b" in name:
+            continue
+        mode = 1 if silu else 2
+        wr, sk = ops._cfg_for(n, k, mode)
+        wrows = 2 * n if silu else n
+        x = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
+        wbytes = wrows * k * 2
+        copies = max(2, int(1.5 * 2**30 // wbytes) + 1)
+        ws = [torch.randn(wrows, k, device=dev, dtype=torch.bfloat16) / 64 for _ in range(copies)]
+        for nt in (True, False):
+            cold = timeit(lambda w: ops.gemm_decode(x, w, mode, wr, sk, nt=nt), ws)
+            warm = timeit(lambda w: ops.gemm_decode(x, w, mode, wr, sk, nt=nt), ws[:1], iters=max(8, copies))
+            print(json.dumps({"shape": name, "MB": round(wbytes / 2**20, 1), "nt": nt, "cold_us": round(cold, 2),
+                              "warm_us": round(warm, 2)}), flush=True)
+        del ws
+        torch.cuda.empty_cache()
+
+
+def main_deep(m):
+    """Deep-ring variants (wr code rows+1: 128-wide K slots, 5-7 slots in flight) vs the tuned configs."""
+    dev = torch.device("cuda:0")
+    cand = {
+        "qkv_8b": [(2, 48, 2), (2, 49, 2), (2, 49, 4), (2, 65, 2), (2, 65, 4), (2, 33, 2)],
+        "o_8b": [(2, 64, 4), (2, 65, 4), (2, 65, 2), (2, 33, 2), (2, 49, 4)],
+        "gate_up_8b": [(1, 112, 1), (1, 65, 1), (1, 33, 1), (1, 64, 1)],
+        "down_8b": [(2, 64, 4), (2, 65, 4), (2, 65, 2), (2, 33, 2), (2, 49, 4)],
+        "lm_head_8b": [(0, 64, 1), (0, 65, 1)],
+    }
+    for name, cfgs in cand.items():
+        n, k, silu = SHAPES[name]
+        wrows = 2 * n if silu else n
+        x = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
+        wbytes = wrows * k * 2
+        copies = max(2, int(1.5 * 2**30 // wbytes) + 1)
+        ws = [torch.randn(wrows, k, device=dev, dtype=torch.bfloat16) / 64 for _ in range(copies)]
+        for mode, wr, sk in cfgs:
+            us = timeit(lambda w: ops.gemm_decode(x, w, mode, wr, sk), ws)
+            print(json.dumps({"shape": name, "mode": mode, "wr": wr, "sk": sk, "us": round(us, 2),
+                              "GBps": round(wbytes / us / 1e3, 1)}), flush=True)
         del ws
         torch.cuda.empty_cache()
 

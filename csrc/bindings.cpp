@@ -360,10 +360,12 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
   check_rows(x, "x");
   const int64_t M = x.size(0), K = x.size(1);
   TORCH_CHECK(M >= 1 && M <= 32, "gemm_decode: 1 <= M <= 32");
-  TORCH_CHECK(wr == 32 || wr == 48 || wr == 64 || wr == 96 || wr == 112 || wr == 128,
-              "wr must be one of 32, 48, 64, 96, 112, 128");
+  TORCH_CHECK(wr == 32 || wr == 48 || wr == 64 || wr == 96 || wr == 112 || wr == 128 || wr == 33 || wr == 49 ||
+                  wr == 65,
+              "wr must be one of 32, 48, 64, 96, 112, 128 (or 33 / 49 / 65: the deep-ring variants)");
   TORCH_CHECK(mode >= 0 && mode <= 4, "mode");
-  const int64_t kc = wr >= 96 ? 128 : 256;
+  const int64_t kc = (wr >= 96 || (wr & 1)) ? 128 : 256;
+  const int64_t wrr = wr & ~1;  // rows per workgroup
   TORCH_CHECK(K % (kc * sk) == 0, "gemm_decode: K must be a multiple of the K slot (256, or 128 for wr >= 96) * sk");
   const bool silu = mode == 1 || mode == 4;
   int64_t N, ldy;
@@ -381,23 +383,23 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
     ldy = y.stride(0);
   }
   TORCH_CHECK(w.dim() == 2 && w.size(1) == K && w.size(0) == (silu ? 2 * N : N), "gemm_decode w shape");
-  TORCH_CHECK(N % (silu ? wr / 2 : wr) == 0, "N not a multiple of the column tile");
+  TORCH_CHECK(N % (silu ? wrr / 2 : wrr) == 0, "N not a multiple of the column tile");
   TORCH_CHECK((int64_t)sk * M * N * 4 < ((int64_t)1 << 31) || mode != 3, "slab too large");
   die::GemmDecodeFuse fz;
   if (mode == 3) {
-    TORCH_CHECK(wr == 32 || wr == 64 || wr == 128, "mode 3: wr in {32, 64, 128}");
+    TORCH_CHECK(wrr == 32 || wrr == 64 || wrr == 128, "mode 3: wr in {32, 64, 128}");
     DIE_CHECK_BF16(resid);
     check_rows(resid, "resid");
     TORCH_CHECK(resid.size(0) >= M && resid.size(1) == N, "resid [M, N]");
     DIE_CHECK_DTYPE(ssp_out, at::kFloat);
     DIE_CHECK_CONTIG(ssp_out);
-    TORCH_CHECK(ssp_out.numel() >= (N / wr) * 32, "ssp_out [N/wr, 32]");
+    TORCH_CHECK(ssp_out.numel() >= (N / wrr) * 32, "ssp_out [N/wr, 32]");
     fz.resid = bf(resid);
     fz.ld_resid = resid.stride(0);
     fz.ssp_out = ssp_out.data_ptr<float>();
     if (sk > 1) {
       DIE_CHECK_DTYPE(counters, at::kInt);
-      TORCH_CHECK(counters.is_cuda() && counters.numel() >= N / wr, "counters [N/wr] int32");
+      TORCH_CHECK(counters.is_cuda() && counters.numel() >= N / wrr, "counters [N/wr] int32");
       fz.counters = counters.data_ptr<int>();
     }
   }

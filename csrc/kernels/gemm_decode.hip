@@ -147,11 +147,16 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
   for (int c = 0; c < nch; ++c) {
     if (c + S - 1 < nch) issue(c + S - 1);
     const int after = min(S - 1, nch - 1 - c);  // chunks issued after c
-    if (after >= 4) wait_vm<4 * PER_WAVE>();
-    else if (after == 3) wait_vm<3 * PER_WAVE>();
-    else if (after == 2) wait_vm<2 * PER_WAVE>();
-    else if (after == 1) wait_vm<PER_WAVE>();
-    else wait_vm<0>();
+    switch (after) {  // counted wait: the younger chunks stay in flight
+      case 7: wait_vm<(S > 7 ? 7 : 0) * PER_WAVE>(); break;
+      case 6: wait_vm<(S > 6 ? 6 : 0) * PER_WAVE>(); break;
+      case 5: wait_vm<(S > 5 ? 5 : 0) * PER_WAVE>(); break;
+      case 4: wait_vm<(S > 4 ? 4 : 0) * PER_WAVE>(); break;
+      case 3: wait_vm<3 * PER_WAVE>(); break;
+      case 2: wait_vm<2 * PER_WAVE>(); break;
+      case 1: wait_vm<PER_WAVE>(); break;
+      default: wait_vm<0>();
+    }
     __builtin_amdgcn_s_barrier();
     const char* slot = smem + (c % S) * SLOT;
     const char* ximg = slot + WR * ROWB;
@@ -317,7 +322,8 @@ static hipError_t launch_modes(void* Y, int64_t ldy, const bf16_t* X, int64_t ld
     case 2: return launch_gd<WR, 2, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
     case 4: return launch_gd<WR, 4, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
     case 3:
-      if constexpr (WR == 32 || WR == 64 || WR == 128) return launch_gd<WR, 3, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
+      if constexpr (WR == 32 || WR == 64 || WR == 128)
+        return launch_gd<WR, 3, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
       return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
@@ -345,6 +351,10 @@ hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx
     case 96: return launch_modes<96, 4, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, fz, s);
     case 112: return launch_modes<112, 4, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, fz, s);
     case 128: return launch_modes<128, 3, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, fz, s);
+    // deep rings (128-wide K slots, 5-7 slots in flight): wr code = rows + 1
+    case 33: return launch_modes<32, 8, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, fz, s);
+    case 49: return launch_modes<48, 6, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, fz, s);
+    case 65: return launch_modes<64, 6, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, fz, s);
     default: return hipErrorInvalidValue;
   }
 }
