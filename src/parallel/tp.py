@@ -46,22 +46,42 @@ class TPContext:
             raise ValueError("tp must be a multiple of num_kv_heads when tp > num_kv_heads")
         return 1
 
+    def _staged(self, t: torch.Tensor) -> bool:
+        """GPU tensors over a gloo group (e.g. several ranks validating TP on one GPU): stage the
+        collective through host memory in fp32. The RCCL path never takes this branch."""
+        return t.is_cuda and dist.get_backend(self.group) == "gloo"
+
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.enabled:
-            dist.all_reduce(t, group=self.group)
+            if self._staged(t):
+                c = t.float().cpu()
+                dist.all_reduce(c, group=self.group)
+                t.copy_(c)
+            else:
+                dist.all_reduce(t, group=self.group)
         return t
 
     def all_gather_last(self, t: torch.Tensor) -> torch.Tensor:
         """Concatenate the per-rank shards along the last dim."""
         if not self.enabled:
             return t
+        if self._staged(t):
+            c = t.float().cpu().contiguous()
+            parts = [torch.empty_like(c) for _ in range(self.world_size)]
+            dist.all_gather(parts, c, group=self.group)
+            return torch.cat(parts, dim=-1).to(t.device, t.dtype)
         parts = [torch.empty_like(t) for _ in range(self.world_size)]
         dist.all_gather(parts, t.contiguous(), group=self.group)
         return torch.cat(parts, dim=-1)
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.enabled:
-            dist.broadcast(t, src=src, group=self.group)
+            if self._staged(t):
+                c = t.cpu()
+                dist.broadcast(c, src=src, group=self.group)
+                t.copy_(c)
+            else:
+                dist.broadcast(t, src=src, group=self.group)
         return t
 
 

@@ -34,7 +34,7 @@ class TPModelRunner(ModelRunner):
         self.h_hdr = torch.zeros(6, dtype=torch.int64, pin_memory=self.is_cuda)
 
     def _bcast(self, t: torch.Tensor) -> None:
-        dist.broadcast(t, src=0, group=self.tp.group) if self.tp.group is not None else dist.broadcast(t, src=0)
+        self.tp.broadcast(t, src=0)
 
     def _sync_step(self, kind: int, a: int = 0, b: int = 0, c: int = 0, d: int = 0) -> None:
         if not self.tp.enabled:

@@ -164,3 +164,63 @@ def test_kv_export_import_exact(engine):
     back = planes.reshape(planes.shape[0], nb, slab)[:, ids].transpose(0, 1)
     assert torch.equal(back, s_.kv_export)
     dec.abort("kvx")
+
+
+def _tp_gpu_worker(rank, world, port, q, preset):
+    import os
+
+    import torch.distributed as dist
+
+    from src.parallel.tp import TPContext
+    from src.parallel.tp_runner import build_tp_engine
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tp = TPContext(rank=rank, world_size=world)
+        cfg = EngineConfig(max_num_seqs=4, max_num_batched_tokens=256, num_kv_blocks=128, max_latency_ms=0.0,
+                           use_cuda_graph=False)
+        obj = build_tp_engine(preset, tp, "cuda:0", cfg=cfg, max_model_len=512, capture=False,
+                              full_init=True, seed=3)
+        if rank == 0:
+            obj.eos_token_id = None
+            q.put(obj.generate(TP_PROMPTS, SamplingParams(max_tokens=8)))
+            obj.runner.stop_followers()
+        else:
+            obj.follower_loop()
+    finally:
+        dist.destroy_process_group()
+
+
+TP_PROMPTS = [[5, 9, 33, 12, 7] * 9, [100, 200, 300], list(range(3, 140))]
+
+
+@pytest.mark.parametrize("preset", ["llama-mini", "mixtral-tiny"])
+def test_tensor_parallel_tp2_on_one_gpu(preset):
+    """The TP=2 code path on real kernels: two ranks share the GPU (gloo, collectives staged
+    through the host), Megatron-split weights drawn from the same stream as the TP=1 model;
+    greedy tokens must agree with the TP=1 fp32 reference up to near-ties."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from src.models.llama import CausalLM
+    from src.models.presets import get_preset
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_tp_gpu_worker, args=(r, 2, port, q, preset)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=600)
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    m = CausalLM(get_preset(preset), "cuda:0", seed=3, max_position=512, full_init=True)
+    for p, o in zip(TP_PROMPTS, got):
+        r, mg = reference_with_margins(m, p, 8)
+        assert agree(o, r, mg), (o, r, mg)
