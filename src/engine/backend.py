@@ -54,9 +54,16 @@ class LLMBackend:
         if device is None:
             device = "cuda:0" if torch.cuda.is_available() else "cpu"
         if engine is None:
+            from src.models.loader import is_hf_checkpoint
+
             ecfg = engine_config_from(config)
-            engine = LLMEngine.from_preset(preset, device=device, cfg=ecfg, max_model_len=config.max_model_len,
-                                           seed=config.seed, capture=config.use_cuda_graph)
+            if is_hf_checkpoint(config.model_path):  # real weights from a local checkpoint directory
+                engine = LLMEngine.from_pretrained(config.model_path, device=device, cfg=ecfg,
+                                                   max_model_len=config.max_model_len,
+                                                   capture=config.use_cuda_graph)
+            else:
+                engine = LLMEngine.from_preset(preset, device=device, cfg=ecfg, max_model_len=config.max_model_len,
+                                               seed=config.seed, capture=config.use_cuda_graph)
         self.engine = engine
         self.tokenizer = load_tokenizer(config.model_path or None, engine.arch.vocab_size)
         if not isinstance(self.tokenizer, ByteTokenizer):

@@ -85,6 +85,22 @@ class LLMEngine:
             eng.runner.capture_graphs()
         return eng
 
+    @classmethod
+    def from_pretrained(cls, path: str, device="cuda:0", cfg: Optional[EngineConfig] = None,
+                        max_model_len: int = 4096, tp: Optional[TPContext] = None, capture: bool = True,
+                        dtype=torch.bfloat16, **arch_overrides):
+        """A local HF-format checkpoint directory (config.json + *.safetensors)."""
+        from src.models.loader import arch_from_hf_config, load_checkpoint
+
+        arch = arch_from_hf_config(path, **arch_overrides)
+        cfg = cfg or EngineConfig()
+        model = CausalLM(arch, device, dtype=dtype, tp=tp, max_position=max(max_model_len, 16))
+        load_checkpoint(model, path)
+        eng = cls(model, cfg, max_model_len)
+        if capture:
+            eng.runner.capture_graphs()
+        return eng
+
     # ------------------------------------------------------------ requests
     def add_request(self, request_id: str, prompt_ids: List[int], sampling: SamplingParams,
                     on_finish: Optional[Callable[[Sequence], None]] = None, user_data=None,

@@ -180,54 +180,71 @@ class CausalLM:
                 lw.ln2.fill_(1)
         self.norms_folded = True
 
-    def load_state_dict(self, tensors: Dict[str, torch.Tensor]) -> int:
-        """Load HF-named Llama/Mixtral weights (already TP-sliced by the caller
-        when tp > 1). Returns the number of tensors consumed."""
+    def load_state_dict(self, tensors: Dict[str, torch.Tensor], fold: bool = True) -> int:
+        """Load HuggingFace-named Llama / Mixtral tensors at their FULL (unsharded) shapes; this
+        rank's Megatron slice is cut here, so a checkpoint shard file can be streamed in as is and
+        q / k / v (gate / up, w1 / w3) may arrive in different calls. Returns the number of
+        tensors consumed. ``fold``: fold the norm weights into Wqkv / Wgate_up afterwards (pass
+        False while streaming several files, then call :meth:`fold_norm_weights` once)."""
+        a, d, r, ws = self.arch, self.head_dim, self.tp.rank, self.tp.world_size
+        hq, hkv, inter = self.hq, self.hkv, self.inter
+        kv_idx = (r * hkv) if a.num_kv_heads >= ws else r // (ws // a.num_kv_heads)
         n = 0
-        a = self.arch
 
-        def take(name):
+        def put(dst: torch.Tensor, src: torch.Tensor) -> None:
             nonlocal n
-            t = tensors.get(name)
-            if t is not None:
-                n += 1
-            return t
+            dst.copy_(src.to(dst.device, dst.dtype))
+            n += 1
 
-        e = take("model.embed_tokens.weight")
-        if e is not None:
-            self.embed.copy_(e)
-        for i, lw in enumerate(self.layers):
-            p = f"model.layers.{i}."
-            q, k, v = take(p + "self_attn.q_proj.weight"), take(p + "self_attn.k_proj.weight"), take(p + "self_attn.v_proj.weight")
-            if q is not None:
-                lw.qkv.copy_(torch.cat([q, k, v], 0))
-                lw.o.copy_(take(p + "self_attn.o_proj.weight"))
-            for nm, dst in (("input_layernorm.weight", lw.ln1), ("post_attention_layernorm.weight", lw.ln2)):
-                t = take(p + nm)
-                if t is not None:
-                    dst.copy_(t)
-            if not a.is_moe:
-                g, u = take(p + "mlp.gate_proj.weight"), take(p + "mlp.up_proj.weight")
-                if g is not None:
-                    lw.gate_up.copy_(torch.cat([g, u], 0))
-                    lw.down.copy_(take(p + "mlp.down_proj.weight"))
-            else:
-                r = take(p + "block_sparse_moe.gate.weight")
-                if r is not None:
-                    lw.router.copy_(r)
-                for x in range(a.num_experts):
-                    q2 = p + f"block_sparse_moe.experts.{x}."
-                    w1, w3, w2 = take(q2 + "w1.weight"), take(q2 + "w3.weight"), take(q2 + "w2.weight")
-                    if w1 is not None:
-                        lw.w13[x].copy_(torch.cat([w1, w3], 0))
-                        lw.w2[x].copy_(w2)
-        t = take("model.norm.weight")
-        if t is not None:
-            self.norm.copy_(t)
-        t = take("lm_head.weight")
-        if t is not None:
-            self.lm_head.copy_(t)
-        self.fold_norm_weights()  # checkpoint norm weights -> folded into Wqkv / Wgate_up
+        def rows(t, lo, cnt):
+            return t[lo:lo + cnt]
+
+        for name, t in tensors.items():
+            if name == "model.embed_tokens.weight":
+                put(self.embed, t)
+                if a.tie_embeddings and "lm_head.weight" not in tensors:
+                    put(self.lm_head, rows(t, r * self.vocab_local, self.vocab_local) if self.vocab_parallel else t)
+                    n -= 1
+            elif name == "model.norm.weight":
+                put(self.norm, t)
+            elif name == "lm_head.weight":
+                put(self.lm_head, rows(t, r * self.vocab_local, self.vocab_local) if self.vocab_parallel else t)
+            elif name.startswith("model.layers."):
+                parts = name.split(".")
+                li, rest = int(parts[2]), ".".join(parts[3:])
+                if li >= len(self.layers):
+                    continue
+                lw = self.layers[li]
+                if rest == "self_attn.q_proj.weight":
+                    put(lw.qkv[: hq * d], rows(t, r * hq * d, hq * d))
+                elif rest == "self_attn.k_proj.weight":
+                    put(lw.qkv[hq * d:(hq + hkv) * d], rows(t, kv_idx * d, hkv * d))
+                elif rest == "self_attn.v_proj.weight":
+                    put(lw.qkv[(hq + hkv) * d:], rows(t, kv_idx * d, hkv * d))
+                elif rest == "self_attn.o_proj.weight":
+                    put(lw.o, t[:, r * hq * d:(r + 1) * hq * d])
+                elif rest == "input_layernorm.weight":
+                    put(lw.ln1, t)
+                elif rest == "post_attention_layernorm.weight":
+                    put(lw.ln2, t)
+                elif rest == "mlp.gate_proj.weight" and not a.is_moe:
+                    put(lw.gate_up[:inter], rows(t, r * inter, inter))
+                elif rest == "mlp.up_proj.weight" and not a.is_moe:
+                    put(lw.gate_up[inter:], rows(t, r * inter, inter))
+                elif rest == "mlp.down_proj.weight" and not a.is_moe:
+                    put(lw.down, t[:, r * inter:(r + 1) * inter])
+                elif rest == "block_sparse_moe.gate.weight" and a.is_moe:
+                    put(lw.router, t)
+                elif rest.startswith("block_sparse_moe.experts.") and a.is_moe:
+                    x, wname = int(parts[5]), parts[6]
+                    if wname == "w1":
+                        put(lw.w13[x, :inter], rows(t, r * inter, inter))
+                    elif wname == "w3":
+                        put(lw.w13[x, inter:], rows(t, r * inter, inter))
+                    elif wname == "w2":
+                        put(lw.w2[x], t[:, r * inter:(r + 1) * inter])
+        if fold:
+            self.fold_norm_weights()  # checkpoint norm weights -> folded into Wqkv / Wgate_up
         return n
 
     def weight_bytes(self) -> int:

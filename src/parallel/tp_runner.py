@@ -97,12 +97,16 @@ def build_tp_engine(preset: str, tp, device, cfg: Optional[EngineConfig] = None,
     (scheduler + RPC-facing API) whose runner broadcasts steps; other ranks get
     a :class:`TPModelRunner` on which to call :meth:`follower_loop`."""
     from src.engine.llm_engine import LLMEngine, plan_kv_blocks
+    from src.models.loader import arch_from_hf_config, is_hf_checkpoint, load_checkpoint
     from src.models.presets import get_preset
 
-    arch = get_preset(preset, **arch_overrides)
+    ckpt = is_hf_checkpoint(preset)  # `preset` may be a local HF checkpoint directory
+    arch = arch_from_hf_config(preset, **arch_overrides) if ckpt else get_preset(preset, **arch_overrides)
     cfg = cfg or EngineConfig()
     model = CausalLM(arch, device, dtype=dtype, tp=tp, seed=seed, max_position=max(max_model_len, 16),
                      full_init=full_init)
+    if ckpt:
+        load_checkpoint(model, preset)  # every rank streams the shards and keeps its own slice
     nblocks = agree_num_blocks(plan_kv_blocks(arch, model, cfg, model.device), tp)
     cfg = EngineConfig(**{**cfg.__dict__, "num_kv_blocks": nblocks})
     if tp.rank == 0:
