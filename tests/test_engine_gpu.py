@@ -224,3 +224,30 @@ def test_tensor_parallel_tp2_on_one_gpu(preset):
     for p, o in zip(TP_PROMPTS, got):
         r, mg = reference_with_margins(m, p, 8)
         assert agree(o, r, mg), (o, r, mg)
+
+
+def test_from_pretrained_checkpoint_on_gpu(tmp_path):
+    """A local HF checkpoint with non-trivial norm weights: loaded, norms folded into the
+    projections, served by the fused decode path; tokens agree with the unfolded source model."""
+    from src.models.llama import CausalLM
+    from src.models.loader import save_hf_checkpoint
+    from src.models.presets import get_preset
+
+    src = CausalLM(get_preset("llama-mini"), "cuda:0", seed=5, max_position=1024)
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    for lw in src.layers:
+        lw.ln1.copy_(torch.rand(lw.ln1.shape, generator=g, device="cuda:0") + 0.5)
+        lw.ln2.copy_(torch.rand(lw.ln2.shape, generator=g, device="cuda:0") + 0.5)
+    src.norms_folded = False
+    path = str(tmp_path / "ckpt")
+    save_hf_checkpoint(src, path, shards=2)
+    cfg = EngineConfig(max_num_seqs=4, max_num_batched_tokens=512, num_kv_blocks=256, max_latency_ms=0.0,
+                       graph_batch_sizes=[1, 2, 4])
+    eng = LLMEngine.from_pretrained(path, device="cuda:0", cfg=cfg, max_model_len=1024)
+    eng.eos_token_id = None
+    assert eng.model.norms_folded and eng.runner.dec_scratch is not None
+    prompts = [[7, 8, 9] * 30, list(range(40, 300))]
+    outs = eng.generate(prompts, SamplingParams(max_tokens=10))
+    for p, o in zip(prompts, outs):
+        r, m = reference_with_margins(src, p, 10)
+        assert agree(o, r, m), (o, r, m)
