@@ -210,9 +210,14 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(bf16_t* __restrict
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int key = kt * KT + kr + 16 * i;
+      // keys 16i .. 16i+15 of the tile share one block (block_size is a multiple of 16): the
+      // block id is wave-uniform, read by a scalar load instead of a per-lane dependent load
+      const int kb = __builtin_amdgcn_readfirstlane(min(kt * KT + 16 * i, kv_end - 1) / block_size);
+      const int64_t blk = bt[kb];
+      const int64_t roff = ((blk * hkv + kvh) * block_size + key % block_size) * D + c * 8;
       if (key < kv_end) {
-        kreg[i] = *reinterpret_cast<const uint4*>(kv_row(k_cache, bt, key, block_size, hkv, kvh) + c * 8);
-        vreg[i] = *reinterpret_cast<const uint4*>(kv_row(v_cache, bt, key, block_size, hkv, kvh) + c * 8);
+        kreg[i] = *reinterpret_cast<const uint4*>(k_cache + roff);
+        vreg[i] = *reinterpret_cast<const uint4*>(v_cache + roff);
       } else {
         kreg[i] = make_uint4(0, 0, 0, 0);
         vreg[i] = make_uint4(0, 0, 0, 0);
@@ -905,7 +910,7 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
                                const int* ctx_lens, int num_seqs, int max_q_len, int hq, int hkv, int head_dim,
                                int block_size, float scale, hipStream_t s) {
   if (num_seqs == 0 || max_q_len == 0) return hipSuccess;
-  if (head_dim != D || hq % hkv) return hipErrorInvalidValue;
+  if (head_dim != D || hq % hkv || block_size % 16) return hipErrorInvalidValue;
   const int G = hq / hkv;
   const float sl2 = scale * 1.4426950408889634f;
   const int tpb = 4 * (32 / (G > 32 ? 32 : G));
