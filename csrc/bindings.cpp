@@ -466,6 +466,19 @@ void decode_advance(Tensor out, Tensor ids, Tensor pos, Tensor ctx, Tensor slots
                                      (int)block_size, (int)tokens.size(0), cur_stream()));
 }
 
+void residual_add_sumsq(Tensor ssp, Tensor resid, Tensor x) {
+  DIE_CHECK_CUDA(x);
+  DIE_CHECK_BF16(x);
+  DIE_CHECK_BF16(resid);
+  check_rows(x, "x");
+  check_rows(resid, "resid");
+  DIE_CHECK_DTYPE(ssp, at::kFloat);
+  DIE_CHECK_CONTIG(ssp);
+  TORCH_CHECK(x.sizes() == resid.sizes() && x.size(0) <= 32 && ssp.numel() >= 32, "residual_add_sumsq shapes");
+  DIE_HIP(die::launch_residual_add_sumsq(ssp.data_ptr<float>(), bf(resid), bf(x), (int)x.size(0), (int)x.size(1),
+                                         resid.stride(0), x.stride(0), cur_stream()));
+}
+
 void row_sumsq(Tensor ssp, Tensor x) {
   DIE_CHECK_CUDA(x);
   DIE_CHECK_BF16(x);
@@ -542,6 +555,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_grouped_gemm", &moe_grouped_gemm);
   m.def("gemm_decode", &gemm_decode);
   m.def("row_sumsq", &row_sumsq);
+  m.def("residual_add_sumsq", &residual_add_sumsq);
   m.def("decode_advance", &decode_advance);
   m.def("gemm_decode_grouped", &gemm_decode_grouped);
   m.def("fused_add_rms_norm_slab", &fused_add_rms_norm_slab);

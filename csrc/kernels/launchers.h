@@ -63,6 +63,8 @@ hipError_t launch_moe_grouped_gemm(bf16_t* Y, const bf16_t* X, const bf16_t* W, 
 hipError_t launch_decode_advance(const int64_t* out, int64_t* ids, int64_t* pos, int* ctx, int64_t* slots,
                                  const int* bt, int bt_width, int64_t* step, int64_t* tokens, int tok_stride,
                                  int* cnt, const int* n_real, int rows, int bs, int k_max, hipStream_t s);
+hipError_t launch_residual_add_sumsq(float* ssp, bf16_t* resid, const bf16_t* x, int rows, int hidden,
+                                     int64_t rstride, int64_t xstride, hipStream_t s);
 hipError_t launch_row_sumsq(float* ssp, const bf16_t* x, int rows, int hidden, int64_t stride, hipStream_t s);
 struct GemmDecodeFuse {
   bf16_t* resid = nullptr;       // mode 3: residual stream [M][ld_resid], updated in place

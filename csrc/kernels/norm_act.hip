@@ -196,6 +196,43 @@ __global__ void __launch_bounds__(256) row_sumsq_kernel(float* __restrict__ ssp,
   if (threadIdx.x == 0) ssp[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
+// resid[row] += x[row] (bf16, in place) and ssp[row] = sum of squares of the new residual:
+// the tensor-parallel form of the decode GEMM's residual epilogue (mode 3), run after the
+// row-parallel projection's all-reduce. grid = rows (<= 32), block = 256.
+__global__ void __launch_bounds__(256) residual_add_sumsq_kernel(float* __restrict__ ssp, bf16_t* __restrict__ resid,
+                                                                 const bf16_t* __restrict__ x, int hidden,
+                                                                 int64_t rstride, int64_t xstride) {
+  __shared__ float red[4];
+  uint4* r = reinterpret_cast<uint4*>(resid + blockIdx.x * rstride);
+  const uint4* src = reinterpret_cast<const uint4*>(x + blockIdx.x * xstride);
+  float ss = 0.f;
+  for (int c = threadIdx.x; c < (hidden >> 3); c += 256) {
+    float a[8], b[8];
+    unpack8(r[c], a);
+    unpack8(src[c], b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += b[j];
+    const uint4 p = pack8(a);
+    r[c] = p;
+    unpack8(p, a);  // statistics of the rounded residual, as the next norm sees it
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += a[j] * a[j];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  if (threadIdx.x == 0) ssp[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+hipError_t launch_residual_add_sumsq(float* ssp, bf16_t* resid, const bf16_t* x, int rows, int hidden,
+                                     int64_t rstride, int64_t xstride, hipStream_t s) {
+  if (rows == 0) return hipSuccess;
+  if (hidden % 8 || rows > 32) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(residual_add_sumsq_kernel, dim3(rows), dim3(256), 0, s, ssp, resid, x, hidden, rstride, xstride);
+  return hipGetLastError();
+}
+
 hipError_t launch_row_sumsq(float* ssp, const bf16_t* x, int rows, int hidden, int64_t stride, hipStream_t s) {
   if (rows == 0) return hipSuccess;
   if (hidden % 8 || rows > 32) return hipErrorInvalidValue;

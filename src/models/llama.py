@@ -269,7 +269,8 @@ class CausalLM:
         if self._slab_path(input_ids):
             if meta.scratch is not None and not meta.is_prefill and self._fused_decode_ok(kv_pool):
                 return self._forward_decode_fused(residual, positions, meta, kv_pool)
-            return self._forward_decode_slab(residual, positions, meta, kv_pool)
+            if not self.tp.enabled:
+                return self._forward_decode_slab(residual, positions, meta, kv_pool)
         x = ops.rms_norm(residual, self.layers[0].ln1, eps)
         h = None
         for li, lw in enumerate(self.layers):
@@ -298,10 +299,10 @@ class CausalLM:
 
     # ------------------------------------------------- decode fast path (M <= 32)
     def _slab_path(self, input_ids: torch.Tensor) -> bool:
-        """Decode-sized steps on the GPU at TP=1 run every projection on the
-        weight-streaming kernel with split-K fp32 slabs reduced inside the
-        consumer kernels (no separate reduction or SiLU launches)."""
-        if not (input_ids.is_cuda and ops.native_available()) or self.tp.enabled or self.arch.is_moe:
+        """Decode-sized steps on the GPU run every projection on the weight-streaming kernel
+        (split-K fp32 slabs reduced inside the consumer kernels; no separate reduction or SiLU
+        launches). The slab fallback is TP=1 only; the fused path also serves TP."""
+        if not (input_ids.is_cuda and ops.native_available()) or self.arch.is_moe:
             return False
         m, h = input_ids.shape[0], self.arch.hidden_size
         return (1 <= m <= ops.DECODE_GEMM_MAX_M and h % 256 == 0 and self.inter % 256 == 0
@@ -335,7 +336,9 @@ class CausalLM:
         residual-updating o / down projections (wr in {32, 64, 128}: one norm-statistics tile
         per wr output columns)."""
         h, d = self.arch.hidden_size, self.head_dim
-        wq, sq = ops._cfg_for(self.layers[0].qkv.shape[0], h, 2)
+        # the fused attention stages sk x (G + 2) slab rows of 512 B in its 17 KiB merge area
+        g = max(1, self.hq // self.hkv)
+        wq, sq = ops._cfg_for(self.layers[0].qkv.shape[0], h, 2, max_sk=max(1, 30 // (g + 2)))
 
         def resid_cfg(k):
             c = ops.DECODE_GEMM_RESID_CFG.get((h, k))
@@ -351,11 +354,13 @@ class CausalLM:
         return {"qkv": (wq, sq), "o": resid_cfg(self.hq * d), "down": resid_cfg(self.inter)}
 
     def alloc_decode_scratch(self) -> Optional[dict]:
-        if not (self.device.type == "cuda" and ops.native_available()) or self.tp.enabled or self.arch.is_moe:
+        if not (self.device.type == "cuda" and ops.native_available()) or self.arch.is_moe:
             return None
         p, h = self.decode_plan(), self.arch.hidden_size
         f32, i32 = torch.float32, torch.int32
-        to, td = h // p["o"][0], h // p["down"][0]
+        # TP: the row-parallel projections are all-reduced first, then one kernel adds into the
+        # residual and writes a single statistics tile
+        to, td = (1, 1) if self.tp.enabled else (h // p["o"][0], h // p["down"][0])
         if max(to, td) > 128:
             return None
         dev = self.device
@@ -385,9 +390,14 @@ class CausalLM:
             attn = ops.attn_decode_fused(slab, ssp_prev, positions, self.cos_sin, meta.slot_mapping,
                                          k_cache, v_cache, meta.block_tables, meta.ctx_lens, meta.max_ctx, hq, hkv,
                                          self.scale, eps, hid, meta.part_o, meta.part_ml, meta.attn_cnt)
-            ops.linear_slab_residual(attn, lw.o, h, sc["ssp_a"], sc["cnt_a"], *plan["o"])
-            act = ops.linear_silu_mul_rownorm(h, lw.gate_up, sc["ssp_a"], eps)
-            ops.linear_slab_residual(act, lw.down, h, sc["ssp_b"], sc["cnt_b"], *plan["down"])
+            if self.tp.enabled:  # row-parallel partial sums -> all-reduce (RCCL) -> residual + statistics
+                ops.residual_add_sumsq(h, self.tp.all_reduce(ops.linear(attn, lw.o)), sc["ssp_a"])
+                act = ops.linear_silu_mul_rownorm(h, lw.gate_up, sc["ssp_a"], eps)
+                ops.residual_add_sumsq(h, self.tp.all_reduce(ops.linear(act, lw.down)), sc["ssp_b"])
+            else:
+                ops.linear_slab_residual(attn, lw.o, h, sc["ssp_a"], sc["cnt_a"], *plan["o"])
+                act = ops.linear_silu_mul_rownorm(h, lw.gate_up, sc["ssp_a"], eps)
+                ops.linear_slab_residual(act, lw.down, h, sc["ssp_b"], sc["cnt_b"], *plan["down"])
             ssp_prev = sc["ssp_b"]
         return ops.rms_norm(h, self.norm, eps)
 

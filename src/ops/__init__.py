@@ -246,6 +246,17 @@ def linear_silu_mul_rownorm(x: torch.Tensor, w_gate_up: torch.Tensor, ssp_in: to
     return out
 
 
+def residual_add_sumsq(resid: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """resid += x (bf16, in place); out [1, 32] = per-row sums of squares of the new residual."""
+    if not x.is_cuda:
+        resid.copy_((resid.float() + x.float()).to(resid.dtype))
+        out.zero_()
+        out[0, : x.shape[0]] = resid.float().pow(2).sum(-1)
+        return out
+    _kern().residual_add_sumsq(out, resid, x)
+    return out
+
+
 def row_sumsq(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[1, 32] fp32 per-row sums of squares of x [M <= 32, H] (RMSNorm statistics)."""
     if out is None:
@@ -282,9 +293,9 @@ DECODE_GEMM_RESID_CFG = {
 }
 
 
-def _cfg_for(n: int, k: int, mode: int):
+def _cfg_for(n: int, k: int, mode: int, max_sk: int = 8):
     c = DECODE_GEMM_CFG.get((n, k, mode))
-    if c is not None:
+    if c is not None and c[1] <= max_sk:
         return c
     import math
 
@@ -294,6 +305,8 @@ def _cfg_for(n: int, k: int, mode: int):
         if n % cols:
             continue
         for sk in ((1, 2, 4, 8) if mode == 2 else (1,)):
+            if sk > max_sk:
+                continue
             if k % (256 * sk):
                 continue
             s = abs(math.log2((n // cols) * sk / 256.0))

@@ -389,3 +389,14 @@ def test_attn_decode_fused(dev, g, hkv):
     close(kc, kr, atol=3e-2, rtol=2e-2)
     close(vc, vr, atol=3e-2, rtol=2e-2)
     assert int(cnt.abs().sum()) == 0
+
+
+def test_residual_add_sumsq(dev):
+    m, h = 13, 8192
+    res = torch.randn(m, h, device=dev, dtype=torch.bfloat16)
+    x = torch.randn(m, h, device=dev, dtype=torch.bfloat16)
+    expect = (res.float() + x.float()).to(torch.bfloat16)
+    ssp = torch.full((1, 32), -1.0, device=dev)
+    ops.residual_add_sumsq(res, x, ssp)
+    assert torch.equal(res, expect)
+    close(ssp[0, :m], expect.float().pow(2).sum(-1), atol=1e-2, rtol=1e-4)
