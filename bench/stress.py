@@ -68,7 +68,7 @@ async def main():
     st = await InferenceClient(f"127.0.0.1:{wport}").call({"op": "engine_stats", "model": "m"})
     print(json.dumps({"bench": "stress", "preset": a.preset, "requests": a.requests, "failed": len(bad),
                       "elapsed_s": round(el, 1), "req_per_s": round(a.requests / el, 1),
-                      "engine": {k: st["stats"].get(k) for k in ("preemptions", "prefix_hit_tokens", "steps",
+                      "engine": {k: st["stats"].get(k) for k in ("preemptions", "swaps_out", "prefix_hit_tokens", "steps",
                                                                  "decode_windows", "generated_tokens")}}),
           flush=True)
     for b in bad[:5]:

@@ -85,6 +85,13 @@ class EngineConfig:
     # decode steps replayed back to back on the GPU per host round trip when nothing is waiting
     # for admission (inputs advanced on the device; see src/engine/model_runner.py decode_multi)
     decode_window: int = 8
+    # KV-pool exhaustion during decode: "recompute" drops the victim's KV and re-prefills it later;
+    # "swap" copies its blocks to pinned host memory and scatters them back on resume (no
+    # recompute); "auto" swaps sequences with at least `swap_min_tokens` of context and recomputes
+    # shorter ones (prefix-cached prompt blocks make those cheap). Swap space is host RAM.
+    preemption_mode: str = "auto"
+    swap_space_gib: float = 16.0
+    swap_min_tokens: int = 256
 
 
 @dataclass

@@ -87,6 +87,12 @@ class KVBlockManager:
         seq.num_computed = len(matched) * self.block_size
         seq.num_prefix_hit = seq.num_computed
 
+    def allocate_fresh(self, seq: Sequence, n_blocks: int) -> List[int]:
+        """A table of ``n_blocks`` new blocks (no prefix matching): swap-in target."""
+        assert not seq.block_table
+        seq.block_table = list(self.bm.allocate(n_blocks))
+        return list(seq.block_table)
+
     def ensure_slots(self, seq: Sequence, n_tokens: int) -> bool:
         """Grow the table to hold ``n_tokens`` tokens. False if out of blocks."""
         need = self.blocks_needed(n_tokens) - len(seq.block_table)

@@ -65,8 +65,14 @@ class LLMEngine:
         self.pool = KVPool(self.arch.num_layers, nblocks, model.hkv, cfg.block_size, self.arch.head_dim,
                            self.device, dtype=model.dtype)
         self.blocks = KVBlockManager(nblocks, cfg.block_size, cfg.enable_prefix_caching, cfg.kv_block_ttl_s)
-        self.scheduler = Scheduler(cfg, self.blocks, self.max_model_len)
         self.runner = runner_cls(model, self.pool, cfg, self.max_model_len)
+        # host swap space for preempted sequences (single-process runners only: a TP group would
+        # have to mirror every swap on its followers, so it always recomputes)
+        per_block = KVPool.bytes_per_block(self.arch.num_layers, model.hkv, cfg.block_size, self.arch.head_dim)
+        swap_blocks = 0
+        if cfg.preemption_mode != "recompute" and getattr(self.runner, "supports_swap", False):
+            swap_blocks = int(cfg.swap_space_gib * 2**30 // per_block)
+        self.scheduler = Scheduler(cfg, self.blocks, self.max_model_len, swap_capacity_blocks=swap_blocks)
         self.seqs: Dict[str, Sequence] = {}
         self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "finished": 0, "prefill_time": 0.0,
                       "decode_time": 0.0, "steps": 0, "prefix_hit_tokens": 0}
@@ -176,6 +182,8 @@ class LLMEngine:
                 s.finish_time = time.perf_counter()
                 finished.append(s)
                 self._complete(s)
+        if out.swap_out or out.swap_in:
+            self._run_swaps(out)
         if out.empty:
             return finished
         t0 = time.perf_counter()
@@ -210,6 +218,26 @@ class LLMEngine:
         if self.cfg.kv_block_ttl_s:
             self.blocks.evict_expired()
         return finished
+
+    def _run_swaps(self, out: SchedulerOutput) -> None:
+        """Queue the step's KV swaps on the compute stream ahead of its forward: swap-outs pack
+        the victim's blocks (move_blocks kernel) and copy them to pinned host memory without a
+        host sync; swap-ins copy back and scatter into the freshly allocated blocks. Stream
+        order makes the gathers read before any later kernel reuses the freed blocks."""
+        from src.parallel.kv_transfer import export_blocks, import_blocks
+
+        planes = self.pool.planes()
+        for seq, ids in out.swap_out:
+            buf = export_blocks(planes, ids)
+            if buf.is_cuda:
+                host = torch.empty(buf.shape, dtype=buf.dtype, pin_memory=True)
+                host.copy_(buf, non_blocking=True)
+                buf = host
+            seq.swap_buf = buf
+            self.stats["swap_out_bytes"] = self.stats.get("swap_out_bytes", 0) + buf.numel() * buf.element_size()
+        for seq, ids in out.swap_in:
+            import_blocks(planes, ids, seq.swap_buf)
+            seq.swap_buf = None
 
     def _decode_window(self, seqs: List[Sequence]) -> int:
         """How many decode steps to run before the host looks again: 1 while requests wait for

@@ -123,6 +123,7 @@ class ModelRunner:
             self.dec_scratch = model.alloc_decode_scratch() if hasattr(model, "alloc_decode_scratch") else None
         else:
             self.part_o = self.part_ml = self.attn_cnt = self.dec_scratch = None
+        self.supports_swap = type(self)._sync_step is ModelRunner._sync_step
         self.supports_multistep = self.is_cuda and self.k_max > 1 and type(self)._sync_step is ModelRunner._sync_step
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_sizes: List[int] = []

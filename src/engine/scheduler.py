@@ -15,8 +15,16 @@ Sequences join the running batch as soon as their prompt is done and leave it
 the step they finish, so the batch never waits for its slowest member.
 ``max_latency_ms`` bounds how long an idle engine waits to accumulate a fuller
 first prefill batch. When the KV pool runs dry during decode the most recently
-admitted sequence is preempted (blocks freed, recomputed later; its cached
-prefix blocks usually make the recompute cheap).
+admitted sequence is preempted. Two preemption modes (``EngineConfig.preemption_mode``):
+
+* **recompute** — blocks freed, the sequence re-prefills later (prompt + the
+  tokens generated so far); its cached prefix blocks usually make that cheap;
+* **swap** — its blocks are packed (``move_blocks`` HIP kernel) and copied to
+  pinned host memory; on resume fresh blocks are allocated and the KV is
+  scattered back, so nothing is recomputed. ``auto`` swaps long contexts
+  (≥ ``swap_min_tokens``) and recomputes short ones.
+
+Swapped sequences resume (FIFO) before any new prompt is admitted.
 """
 
 from __future__ import annotations
@@ -47,6 +55,9 @@ class SchedulerOutput:
     prefill: List[PrefillChunk] = field(default_factory=list)
     decode: List[Sequence] = field(default_factory=list)
     preempted: List[Sequence] = field(default_factory=list)
+    # (sequence, block ids) to copy out to host / back in from host before this step's forward
+    swap_out: List[Tuple[Sequence, List[int]]] = field(default_factory=list)
+    swap_in: List[Tuple[Sequence, List[int]]] = field(default_factory=list)
 
     @property
     def empty(self) -> bool:
@@ -58,12 +69,18 @@ class SchedulerOutput:
 
 
 class Scheduler:
-    def __init__(self, cfg: EngineConfig, blocks: KVBlockManager, max_model_len: int):
+    def __init__(self, cfg: EngineConfig, blocks: KVBlockManager, max_model_len: int,
+                 swap_capacity_blocks: int = 0):
         self.cfg = cfg
         self.blocks = blocks
         self.max_model_len = max_model_len
         self.waiting: Deque[Sequence] = deque()
         self.running: List[Sequence] = []
+        self.swapped: Deque[Sequence] = deque()
+        self.swap_capacity = swap_capacity_blocks   # host swap space, in KV blocks
+        self.swap_used = 0
+        self.num_swaps_out = 0
+        self.num_swaps_in = 0
         self.num_preemptions = 0
         self.steps_prefill = 0
         self.steps_decode = 0
@@ -73,14 +90,15 @@ class Scheduler:
         self.waiting.append(seq)
 
     def has_work(self) -> bool:
-        return bool(self.waiting or self.running)
+        return bool(self.waiting or self.running or self.swapped)
 
     def abort(self, request_id: str) -> Optional[Sequence]:
-        for q in (self.waiting, self.running):
+        for q in (self.waiting, self.running, self.swapped):
             for s in list(q):
                 if s.request_id == request_id:
                     q.remove(s)
                     self.blocks.free(s)
+                    self._drop_swap(s)
                     s.status = SeqStatus.FINISHED
                     s.finish_reason = "abort"
                     return s
@@ -109,6 +127,20 @@ class Scheduler:
         now = time.perf_counter() if now is None else now
         out = SchedulerOutput()
         budget = self.cfg.max_num_batched_tokens
+        # 0) resume swapped-out sequences first (FIFO); while one is still parked, admit nothing new
+        while self.swapped and len(self.running) < self.cfg.max_num_seqs:
+            seq = self.swapped[0]
+            nb = self.blocks.blocks_needed(seq.num_computed)
+            if nb + len(self.running) // 4 > self.blocks.num_available():
+                break
+            self.swapped.popleft()
+            ids = self.blocks.allocate_fresh(seq, nb)
+            out.swap_in.append((seq, ids))
+            self.swap_used -= nb
+            self.num_swaps_in += 1
+            seq.status = SeqStatus.RUNNING
+            self.running.append(seq)
+        blocked = bool(self.swapped)
         # 1) continue chunked prefills already running
         for seq in self.running:
             if budget <= 0:
@@ -118,7 +150,7 @@ class Scheduler:
                 out.prefill.append(PrefillChunk(seq, seq.num_computed, n))
                 budget -= n
         # 2) admit new prompts
-        if not self._hold_for_batching(now):
+        if not blocked and not self._hold_for_batching(now):
             while self.waiting and budget > 0 and len(self.running) < self.cfg.max_num_seqs:
                 seq = self.waiting[0]
                 if len(seq) > self.max_model_len:
@@ -154,7 +186,7 @@ class Scheduler:
                 victim = self._pick_victim(exclude=seq)
                 if victim is None:
                     break
-                self._preempt(victim)
+                self._preempt(victim, out)
                 out.preempted.append(victim)
                 if victim in decode:
                     decode.remove(victim)
@@ -162,7 +194,7 @@ class Scheduler:
                 decode.append(seq)
                 continue
             # could not find room even after preempting everyone else
-            self._preempt(seq)
+            self._preempt(seq, out)
             out.preempted.append(seq)
         out.decode = decode
         if decode:
@@ -173,13 +205,37 @@ class Scheduler:
         cands = [s for s in self.running if s is not exclude and s.status == SeqStatus.RUNNING]
         return max(cands, key=lambda s: s.arrival) if cands else None
 
-    def _preempt(self, seq: Sequence) -> None:
-        """Recompute-style preemption: drop the KV, requeue at the front."""
-        self.blocks.free(seq)
+    def _swap_ok(self, seq: Sequence) -> bool:
+        mode = self.cfg.preemption_mode
+        if self.swap_capacity <= 0 or mode == "recompute" or seq.in_prefill or seq.num_computed == 0:
+            return False
+        if mode == "auto" and seq.num_computed < self.cfg.swap_min_tokens:
+            return False
+        return self.swap_used + self.blocks.blocks_needed(seq.num_computed) <= self.swap_capacity
+
+    def _drop_swap(self, seq: Sequence) -> None:
+        if seq.status == SeqStatus.SWAPPED:
+            self.swap_used -= self.blocks.blocks_needed(seq.num_computed)
+            seq.swap_buf = None
+
+    def _preempt(self, seq: Sequence, out: Optional[SchedulerOutput] = None) -> None:
+        """Preempt ``seq``: swap its KV to host (see module doc) or drop it for recompute."""
         if seq in self.running:
             self.running.remove(seq)
-        seq.num_computed = 0
+        self.num_preemptions += 1
         seq.num_preemptions += 1
+        if out is not None and self._swap_ok(seq):
+            nb = self.blocks.blocks_needed(seq.num_computed)
+            out.swap_out.append((seq, list(seq.block_table[:nb])))
+            # freed now; the engine gathers them before this step's forward can overwrite any
+            self.blocks.free(seq)
+            self.swap_used += nb
+            self.num_swaps_out += 1
+            seq.status = SeqStatus.SWAPPED
+            self.swapped.append(seq)
+            return
+        self.blocks.free(seq)
+        seq.num_computed = 0
         seq.status = SeqStatus.WAITING
         # the generated tokens become part of the prompt for the recompute
         seq.prompt_ids = seq.prompt_ids + seq.output_ids
@@ -188,7 +244,6 @@ class Scheduler:
         seq.output_ids = []
         seq.block_hashes = None
         self.waiting.appendleft(seq)
-        self.num_preemptions += 1
 
     # ------------------------------------------------------------ results
     def finish(self, seq: Sequence, reason: str) -> None:
@@ -203,7 +258,10 @@ class Scheduler:
         return {
             "waiting": len(self.waiting),
             "running": len(self.running),
+            "swapped": len(self.swapped),
             "preemptions": self.num_preemptions,
+            "swaps_out": self.num_swaps_out,
+            "swaps_in": self.num_swaps_in,
             "steps_prefill": self.steps_prefill,
             "steps_decode": self.steps_decode,
         }

@@ -17,6 +17,7 @@ class SeqStatus(enum.Enum):
     WAITING = 0
     RUNNING = 1
     FINISHED = 2
+    SWAPPED = 3       # preempted with its KV parked in host memory
 
 
 @dataclass
@@ -40,6 +41,7 @@ class Sequence:
     user_data: Any = None
     # Disaggregation: a sequence whose prompt KV arrives from a prefill worker
     imported_kv: bool = False
+    swap_buf: Any = None             # host copy of the KV blocks while SWAPPED
 
     def __len__(self) -> int:
         return len(self.prompt_ids) + len(self.output_ids)

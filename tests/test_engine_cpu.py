@@ -19,7 +19,8 @@ from tests.engine_reference import greedy_reference
 def make_engine(**kw):
     cfg = EngineConfig(max_num_seqs=kw.pop("max_num_seqs", 4), max_num_batched_tokens=kw.pop("budget", 64),
                        num_kv_blocks=kw.pop("blocks", 64), max_latency_ms=0.0, block_size=16,
-                       enable_prefix_caching=kw.pop("prefix", True))
+                       enable_prefix_caching=kw.pop("prefix", True),
+                       preemption_mode=kw.pop("preemption", "recompute"), swap_min_tokens=kw.pop("swap_min", 256))
     eng = LLMEngine.from_preset(kw.pop("preset", "llama-tiny"), device="cpu", cfg=cfg, max_model_len=256,
                                 capture=False, dtype=torch.float32, **kw)
     eng.eos_token_id = None   # random weights may emit any id; lengths are asserted
@@ -62,6 +63,34 @@ def test_preemption_under_kv_pressure():
     for p, o in zip(ps, outs):
         assert len(o) == 30
         assert o == greedy_reference(eng.model, p, 30)
+
+
+@pytest.mark.parametrize("mode", ["swap", "auto"])
+def test_swap_preemption_under_kv_pressure(mode):
+    """Preempted sequences park their KV in host memory and resume without recompute
+    (auto: only contexts of >= swap_min tokens swap); tokens must not change."""
+    eng = make_engine(blocks=12, max_num_seqs=4, budget=256, prefix=False, preemption=mode, swap_min=48)
+    ps = [p[:40] for p in prompts(4, seed=3)]
+    outs = eng.generate(ps, SamplingParams(max_tokens=30))
+    st = eng.get_stats()
+    assert st["swaps_out"] > 0 and st["swaps_in"] == st["swaps_out"]
+    assert st["swapped"] == 0 and st["kv"]["used"] == 0 and eng.scheduler.swap_used == 0
+    for p, o in zip(ps, outs):
+        assert o == greedy_reference(eng.model, p, 30)
+
+
+def test_swap_abort_releases_swap_space():
+    eng = make_engine(blocks=12, max_num_seqs=4, budget=256, prefix=False, preemption="swap")
+    for i, p in enumerate(prompts(4, seed=3)):
+        eng.add_request(f"r{i}", p[:40], SamplingParams(max_tokens=30))
+    while not eng.scheduler.swapped:
+        eng.step()
+    victim = eng.scheduler.swapped[0]
+    eng.abort(victim.request_id)
+    assert eng.scheduler.swap_used == 0 or eng.scheduler.swapped
+    while eng.has_work():
+        eng.step()
+    assert eng.scheduler.swap_used == 0 and eng.get_stats()["kv"]["used"] == 0
 
 
 def test_moe_engine():

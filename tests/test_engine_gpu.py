@@ -251,3 +251,20 @@ def test_from_pretrained_checkpoint_on_gpu(tmp_path):
     for p, o in zip(prompts, outs):
         r, m = reference_with_margins(src, p, 10)
         assert agree(o, r, m), (o, r, m)
+
+
+def test_swap_preemption_on_gpu():
+    """KV pool too small for the batch: preempted sequences' blocks go to pinned host memory
+    (move_blocks kernel + async D2H) and come back (H2D + scatter); tokens unchanged."""
+    cfg = EngineConfig(max_num_seqs=4, max_num_batched_tokens=512, num_kv_blocks=24, max_latency_ms=0.0,
+                       graph_batch_sizes=[1, 2, 4], preemption_mode="swap", decode_window=1)
+    eng = LLMEngine.from_preset("llama-mini", device="cuda:0", cfg=cfg, max_model_len=512)
+    eng.eos_token_id = None
+    rng = random.Random(4)
+    prompts = [[rng.randrange(3, 32000) for _ in range(70)] for _ in range(4)]
+    outs = eng.generate(prompts, SamplingParams(max_tokens=40))
+    st = eng.get_stats()
+    assert st["swaps_out"] > 0 and st["swaps_in"] == st["swaps_out"] and st["kv"]["used"] == 0
+    for p, o in zip(prompts, outs):
+        r, m = reference_with_margins(eng.model, p, 40)
+        assert agree(o, r, m), (o, r, m)
