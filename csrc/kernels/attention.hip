@@ -935,18 +935,6 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
   return hipGetLastError();
 }
 
-static int num_cus() {
-  static int n[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (n[dev] == 0) {
-    int v = 0;
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-    n[dev] = v;
-  }
-  return n[dev];
-}
-
 hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* counters, const bf16_t* q,
                               int64_t q_stride, bf16_t* k_cache, bf16_t* v_cache, const int* block_tables,
                               int bt_stride, const int* ctx_lens, int num_seqs, int max_ctx, int hq, int hkv,

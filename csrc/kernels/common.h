@@ -90,4 +90,18 @@ __device__ __forceinline__ float hash_uniform(uint64_t seed, uint64_t a, uint64_
   return ((float)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);
 }
 
+// Compute units of the current device (256 on MI355X), cached per device: persistent and
+// self-merging kernels size their grids by it.
+static inline int num_cus() {
+  static int n[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (n[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    n[dev] = v;
+  }
+  return n[dev];
+}
+
 }  // namespace die

@@ -56,11 +56,17 @@ using namespace gd;
 // KC = K elements per ring slot (256, or 128 for the wide tiles so that 4 slots fit in LDS).
 // NT: weight pieces are loaded non-temporal (aux = 2): each weight byte is read once per step by one CU,
 // so it should not displace the activations / KV in L2 and MALL (MI355X_MICROARCH.md "nt-weights").
-template <int WR, int EPI, int S, bool NT, int KC>
-__global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv, int64_t ldy,
-                                                          const bf16_t* __restrict__ X, int64_t ldx,
-                                                          const bf16_t* __restrict__ W, int M, int N_out, int K,
-                                                          GemmDecodeFuse fz) {
+//
+// The body is a device function so that a persistent launch can chain two of them (mlp_decode_kernel):
+// (bx, by, ny) stand for (blockIdx.x, blockIdx.y, gridDim.y). XWAIT: the activations X are produced
+// inside the same launch — the first S-1 weight chunks are issued, then the workgroup waits until
+// *xflag reaches xtarget, then X is read with device-coherent (sc1) loads. WT: the output is stored
+// write-through (sc1) so that workgroups on other XCDs can read it in the same launch.
+template <int WR, int EPI, int S, bool NT, int KC, bool XWAIT = false, bool WT = false>
+__device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const bf16_t* __restrict__ X, int64_t ldx,
+                                        const bf16_t* __restrict__ W, int M, int N_out, int K,
+                                        const GemmDecodeFuse& fz, const int bx, const int by, const int ny,
+                                        const int* xflag = nullptr, int xtarget = 0, int* err = nullptr) {
   constexpr int ROWB = KC * 2;                 // bytes per image row
   constexpr int CPR = KC / 8;                  // 16-byte chunks per row (32 or 16)
   constexpr int RPP = 64 / CPR;                // rows per 1-KiB DMA piece (2 or 4)
@@ -73,7 +79,8 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
   constexpr int KSW = KC / 128;                // 32-deep k-steps per wave per chunk
   static_assert(INSTR % 4 == 0 && WR % RPP == 0, "pieces must split over 4 waves, W/X pieces unmixed");
   static_assert((S - 1) * PER_WAVE <= 63, "vmcnt field is 6 bits");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int PX = MR / RPP / 4;             // activation pieces per wave per chunk
+  static_assert((MR / RPP) % 4 == 0, "activation pieces must split over 4 waves");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (fz.grp_off != nullptr) {
     // grouped (MoE) form: blockIdx.z = expert; its rows of X/Y are [off[e], off[e+1]) of the
@@ -86,9 +93,9 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
     W += (int64_t)e * fz.grp_wstride;
     Yv = reinterpret_cast<char*>(Yv) + (int64_t)r0 * ldy * (EPI == 2 || EPI == 3 ? 4 : 2);
   }
-  const int n0 = blockIdx.x * NO;
-  const int kper = K / gridDim.y;
-  const int k0 = blockIdx.y * kper;
+  const int n0 = bx * NO;
+  const int kper = K / ny;
+  const int k0 = by * kper;
   const int nch = kper / KC;
 
   // Per-lane source rows for this wave's DMA pieces (fixed across chunks).
@@ -110,15 +117,25 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
     src[p] = base + k0 + lch * 8;
     isw[p] = row < WR;
   }
-  auto issue = [&](int c) {
+  // part: 3 = whole chunk, 1 = weight pieces only, 2 = activation pieces only
+  auto issue = [&](int c, int part = 3) {
     char* slot = smem + (c % S) * SLOT;
 #pragma unroll
     for (int p = 0; p < PER_WAVE; ++p) {
       // a piece is all-weight or all-activation rows: wave-uniform branch
-      if (NT && isw[p])
-        glds16<2>(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);
-      else
-        glds16<0>(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);
+      if (isw[p]) {
+        if (!(part & 1)) continue;
+        if (NT)
+          glds16<2>(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);
+        else
+          glds16<0>(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);
+      } else {
+        if (!(part & 2)) continue;
+        if (XWAIT)
+          glds16<16>(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);  // sc1: other XCDs wrote X
+        else
+          glds16<0>(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);
+      }
     }
   };
 
@@ -138,15 +155,42 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
 #pragma unroll
     for (int b = 0; b < NTILE; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
 
+  if constexpr (XWAIT) {
+    // weights do not depend on X: put S-1 chunks of them in flight, then wait for the producers
+    // (nch >= S is checked by the launcher)
 #pragma unroll
-  for (int c = 0; c < S - 1; ++c)
-    if (c < nch) issue(c);
+    for (int c = 0; c < S - 1; ++c) issue(c, 1);
+    if (tid == 0) {
+      int it = 0;
+      while (__hip_atomic_load(xflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < xtarget) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++it > (1 << 20)) {  // bounded: a broken hand-off reports instead of hanging the GPU
+          *err = 1;
+          break;
+        }
+      }
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int c = 0; c < S - 1; ++c) issue(c, 2);
+  } else {
+#pragma unroll
+    for (int c = 0; c < S - 1; ++c)
+      if (c < nch) issue(c);
+  }
 
   const int fr = lane & 15, kg = lane >> 4;
 #pragma unroll 1
   for (int c = 0; c < nch; ++c) {
     if (c + S - 1 < nch) issue(c + S - 1);
     const int after = min(S - 1, nch - 1 - c);  // chunks issued after c
+    if (XWAIT && c == 0) {
+      // issue order was W(0..S-2), X(0..S-2), chunk S-1: chunk 0 is complete once only
+      // X(1..S-2) and chunk S-1 remain
+      wait_vm<(S - 2) * PX + PER_WAVE>();
+    } else
     switch (after) {  // counted wait: the younger chunks stay in flight
       case 7: wait_vm<(S > 7 ? 7 : 0) * PER_WAVE>(); break;
       case 6: wait_vm<(S > 6 ? 6 : 0) * PER_WAVE>(); break;
@@ -203,7 +247,7 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
     constexpr int Q = WR / 4;  // float4 column groups per row (8, 16 or 32 lanes: one row per lane group)
     static_assert(Q == 8 || Q == 16 || Q == 32, "EPI 3 needs wr in {32, 64, 128}");
     int* ctl = reinterpret_cast<int*>(smem + 4 * MR * WR * 4);
-    const bool single = gridDim.y == 1;
+    const bool single = ny == 1;
     if (!single) {
       __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(Yv, 0, 0x7fffffff, 0x00020000);
       for (int e = tid; e < MR * Q; e += NTH) {
@@ -213,14 +257,13 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
 #pragma unroll
         for (int w = 0; w < 4; ++w) v += *reinterpret_cast<const f4*>(red + (w * MR + m) * WR + j);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
-                                               ry, (int)((((int64_t)blockIdx.y * M + m) * ldy + n0 + j) * 4), 0,
+                                               ry, (int)((((int64_t)by * M + m) * ldy + n0 + j) * 4), 0,
                                                16);  // write-through (sc1): no release fence needed
       }
       wait_vm<0>();
       __syncthreads();
       if (tid == 0)
-        ctl[0] = __hip_atomic_fetch_add(fz.counters + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                 (int)gridDim.y - 1;
+        ctl[0] = __hip_atomic_fetch_add(fz.counters + bx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ny - 1;
       __syncthreads();
       if (!ctl[0]) return;
     }
@@ -234,7 +277,7 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
 #pragma unroll
           for (int w = 0; w < 4; ++w) v += *reinterpret_cast<const f4*>(red + (w * MR + m) * WR + j);
         } else {
-          for (int k = 0; k < (int)gridDim.y; ++k)
+          for (int k = 0; k < ny; ++k)
             v += __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
                                             ry, (int)((((int64_t)k * M + m) * ldy + n0 + j) * 4), 0, 16));
         }
@@ -252,9 +295,9 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
       }
 #pragma unroll
       for (int o = Q / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
-      if (e % Q == 0) fz.ssp_out[blockIdx.x * 32 + m] = m < M ? ss : 0.f;
+      if (e % Q == 0) fz.ssp_out[bx * 32 + m] = m < M ? ss : 0.f;
     }
-    if (!single && tid == 0) __hip_atomic_store(fz.counters + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!single && tid == 0) __hip_atomic_store(fz.counters + bx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   if constexpr (EPI == 4) {
@@ -291,10 +334,65 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
       }
       v = v / (1.f + __expf(-v)) * u;
     }
-    if (EPI == 2)
-      reinterpret_cast<float*>(Yv)[((int64_t)blockIdx.y * M + m) * ldy + n0 + j] = v;
-    else
+    if (EPI == 2) {
+      reinterpret_cast<float*>(Yv)[((int64_t)by * M + m) * ldy + n0 + j] = v;
+    } else if (WT) {
+      __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(Yv, 0, 0x7fffffff, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), ry, (int)(((int64_t)m * ldy + n0 + j) * 2), 0, 16);
+    } else {
       reinterpret_cast<bf16_t*>(Yv)[(int64_t)m * ldy + n0 + j] = f2bf(v);
+    }
+  }
+}
+
+template <int WR, int EPI, int S, bool NT, int KC>
+__global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv, int64_t ldy,
+                                                          const bf16_t* __restrict__ X, int64_t ldx,
+                                                          const bf16_t* __restrict__ W, int M, int N_out, int K,
+                                                          GemmDecodeFuse fz) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  gd_body<WR, EPI, S, NT, KC>(smem, Yv, ldy, X, ldx, W, M, N_out, K, fz, blockIdx.x, blockIdx.y, gridDim.y);
+}
+
+// Persistent decode MLP (one launch instead of two): every workgroup first computes gate/up column
+// tiles (mode 4: norm row scale + SiLU*mul, 56 outputs per tile, written through to memory), then
+// down-projection tiles (mode 3: 64 columns x 1/4 of K, split-K slabs + last-arriver residual update
+// and next-norm statistics). Down tile (n, s) needs only the activation columns of k-slice s, i.e. the
+// gate/up tiles [s * P, (s + 1) * P): each producer bumps flags[s], and the consumer streams its first
+// weight chunks into the LDS ring BEFORE waiting for flags[s] == P, so the down weight stream starts
+// while the last gate/up tiles drain (no launch boundary, no pipeline refill; cf.
+// cdna_hip_programming.md §5.6: the MLP half of a decode layer at batch 16-32 is faster in one launch).
+// flags[s + 4] counts consumers past the wait; the last one re-arms both words for the next layer.
+// The grid never exceeds the CU count and one workgroup fills a CU's LDS, so every workgroup is
+// resident and the waits cannot deadlock; every spin is bounded (err = 1 on give-up).
+constexpr int MLP_NO1 = 56, MLP_WR2 = 64, MLP_SK2 = 4;
+
+template <bool NT>
+__global__ void __launch_bounds__(NTH) mlp_decode_kernel(bf16_t* __restrict__ act, const bf16_t* __restrict__ X,
+                                                         int64_t ldx, const bf16_t* __restrict__ Wgu,
+                                                         const bf16_t* __restrict__ Wd, float* __restrict__ slab,
+                                                         int M, int H, int I, GemmDecodeFuse fz1, GemmDecodeFuse fz2,
+                                                         int* __restrict__ flags, int* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tiles1 = I / MLP_NO1, per_slice = tiles1 / MLP_SK2;
+  const int ntile2 = H / MLP_WR2, tiles2 = ntile2 * MLP_SK2;
+  const int tid = threadIdx.x;
+  for (int t = blockIdx.x; t < tiles1; t += gridDim.x) {
+    gd_body<112, 4, 4, NT, 128, false, true>(smem, act, I, X, ldx, Wgu, M, I, H, fz1, t, 0, 1);
+    wait_vm<0>();     // this thread's write-through stores are acknowledged
+    __syncthreads();  // ... and everyone's; the LDS is free again
+    if (tid == 0) __hip_atomic_fetch_add(flags + t / per_slice, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (int t = blockIdx.x; t < tiles2; t += gridDim.x) {
+    const int s = t % MLP_SK2, n = t / MLP_SK2;
+    gd_body<MLP_WR2, 3, 3, NT, 256, true, false>(smem, slab, H, act, I, Wd, M, H, I, fz2, n, s, MLP_SK2, flags + s,
+                                                  per_slice, err);
+    __syncthreads();
+    if (tid == 0 &&
+        __hip_atomic_fetch_add(flags + MLP_SK2 + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ntile2 - 1) {
+      __hip_atomic_store(flags + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(flags + MLP_SK2 + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -357,6 +455,32 @@ hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx
     case 65: return launch_modes<64, 6, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, fz, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+// act [M, I] bf16 scratch (row stride I); slab [4, M, H] fp32 scratch; flags int[8] zeroed once;
+// fz1: ssp_in / ssp_tiles / inv_n / eps of the gate/up norm; fz2: resid / ld_resid / ssp_out /
+// counters [H / 64] of the down projection (as mode 3).
+hipError_t launch_mlp_decode(bf16_t* act, const bf16_t* X, int64_t ldx, const bf16_t* Wgu, const bf16_t* Wd,
+                             float* slab, int M, int H, int I, const GemmDecodeFuse& fz1, const GemmDecodeFuse& fz2,
+                             int* flags, int* err, bool nt, hipStream_t s) {
+  if (M <= 0) return hipSuccess;
+  if (M > MR || H % 128 || H % MLP_WR2 || I % (MLP_NO1 * MLP_SK2) || (I / MLP_SK2) % 256 || (I / MLP_SK2) / 256 < 3)
+    return hipErrorInvalidValue;
+  if (fz1.ssp_in == nullptr || fz1.ssp_tiles < 1 || fz1.ssp_tiles > 128 || fz2.resid == nullptr ||
+      fz2.ssp_out == nullptr || fz2.counters == nullptr || flags == nullptr || err == nullptr)
+    return hipErrorInvalidValue;
+  const int tiles = min(I / MLP_NO1, (H / MLP_WR2) * MLP_SK2);
+  const int grid = min(tiles, num_cus());
+  constexpr size_t lds1 = (size_t)4 * (112 + MR) * 128 * 2, lds2 = (size_t)3 * (MLP_WR2 + MR) * 256 * 2;
+  constexpr size_t lds = lds1 > lds2 ? lds1 : lds2;
+  static_assert(lds > 80 * 1024, "one workgroup per CU (residency of the persistent grid)");
+  if (nt)
+    hipLaunchKernelGGL(mlp_decode_kernel<true>, dim3(grid), dim3(NTH), lds, s, act, X, ldx, Wgu, Wd, slab, M, H, I,
+                       fz1, fz2, flags, err);
+  else
+    hipLaunchKernelGGL(mlp_decode_kernel<false>, dim3(grid), dim3(NTH), lds, s, act, X, ldx, Wgu, Wd, slab, M, H, I,
+                       fz1, fz2, flags, err);
+  return hipGetLastError();
 }
 
 }  // namespace die

@@ -351,7 +351,11 @@ class CausalLM:
                 sk //= 2
             return wr, sk
 
-        return {"qkv": (wq, sq), "o": resid_cfg(self.hq * d), "down": resid_cfg(self.inter)}
+        plan = {"qkv": (wq, sq), "o": resid_cfg(self.hq * d), "down": resid_cfg(self.inter), "mlp_fused": False}
+        if ops.MLP_DECODE_FUSED and not self.tp.enabled and ops.mlp_decode_ok(h, self.inter):
+            # gate/up + down in one persistent launch; its down tiles are 64 columns x 4 k-slices
+            plan["mlp_fused"], plan["down"] = True, (64, 4)
+        return plan
 
     def alloc_decode_scratch(self) -> Optional[dict]:
         if not (self.device.type == "cuda" and ops.native_available()) or self.arch.is_moe:
@@ -364,9 +368,14 @@ class CausalLM:
         if max(to, td) > 128:
             return None
         dev = self.device
-        return {"plan": p, "ssp0": torch.zeros(1, 32, dtype=f32, device=dev),
-                "ssp_a": torch.zeros(to, 32, dtype=f32, device=dev), "cnt_a": torch.zeros(to, dtype=i32, device=dev),
-                "ssp_b": torch.zeros(td, 32, dtype=f32, device=dev), "cnt_b": torch.zeros(td, dtype=i32, device=dev)}
+        sc = {"plan": p, "ssp0": torch.zeros(1, 32, dtype=f32, device=dev),
+              "ssp_a": torch.zeros(to, 32, dtype=f32, device=dev), "cnt_a": torch.zeros(to, dtype=i32, device=dev),
+              "ssp_b": torch.zeros(td, 32, dtype=f32, device=dev), "cnt_b": torch.zeros(td, dtype=i32, device=dev)}
+        if p["mlp_fused"]:
+            sc.update(mlp_flags=torch.zeros(8, dtype=i32, device=dev), mlp_err=torch.zeros(1, dtype=i32, device=dev),
+                      mlp_act=torch.empty(32, self.inter, dtype=self.dtype, device=dev),
+                      mlp_slab=torch.empty(4 * 32 * h, dtype=f32, device=dev))
+        return sc
 
     def _fused_decode_ok(self, kv_pool: torch.Tensor) -> bool:
         g = self.hq // self.hkv
@@ -376,7 +385,7 @@ class CausalLM:
 
     def _forward_decode_fused(self, h: torch.Tensor, positions: torch.Tensor, meta: AttnMetadata,
                               kv_pool: torch.Tensor) -> torch.Tensor:
-        """Decode layer = 5 launches: qkv (split-K slabs) -> attention (norm scale + slab sum + RoPE
+        """Decode layer = 5 launches (4 with the persistent MLP): qkv (split-K slabs) -> attention (norm scale + slab sum + RoPE
         + KV write in its prologue) -> o (slabs, last arriver adds into the residual and writes the
         next norm's row statistics) -> gate/up (norm as a row scale, SiLU*mul) -> down (as o).
         The residual stream `h` is updated in place; norm weights are folded into Wqkv / Wgate_up."""
@@ -396,8 +405,12 @@ class CausalLM:
                 ops.residual_add_sumsq(h, self.tp.all_reduce(ops.linear(act, lw.down)), sc["ssp_b"])
             else:
                 ops.linear_slab_residual(attn, lw.o, h, sc["ssp_a"], sc["cnt_a"], *plan["o"])
-                act = ops.linear_silu_mul_rownorm(h, lw.gate_up, sc["ssp_a"], eps)
-                ops.linear_slab_residual(act, lw.down, h, sc["ssp_b"], sc["cnt_b"], *plan["down"])
+                if plan["mlp_fused"]:  # gate/up -> down hand-off inside one persistent launch
+                    ops.mlp_decode(h, lw.gate_up, lw.down, sc["ssp_a"], eps, h, sc["ssp_b"], sc["cnt_b"],
+                                   sc["mlp_flags"], sc["mlp_err"], sc["mlp_act"][: h.shape[0]], sc["mlp_slab"])
+                else:
+                    act = ops.linear_silu_mul_rownorm(h, lw.gate_up, sc["ssp_a"], eps)
+                    ops.linear_slab_residual(act, lw.down, h, sc["ssp_b"], sc["cnt_b"], *plan["down"])
             ssp_prev = sc["ssp_b"]
         return ops.rms_norm(h, self.norm, eps)
 

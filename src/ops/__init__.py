@@ -8,6 +8,7 @@ which lets the engine's control flow run in CPU-only tests.
 
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -190,7 +191,12 @@ def _decode_gemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
             and w.shape[0] % 16 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0)
 
 
-DECODE_GEMM_NT = True  # non-temporal weight loads (read-once stream)
+DECODE_GEMM_NT = True
+# decode MLP (gate/up + down) as one persistent launch where the shapes allow (opt-in, DIE_MLP_FUSED=1):
+# bit-identical to the two launches and measured equal in speed on MI355X (bench/micro_mlp_decode.py:
+# 78.3 vs 78.1 us per Llama-3-8B layer at batch 32, profiles/micro_mlp_decode_r1.jsonl), so the simpler
+# two-launch form stays the default
+MLP_DECODE_FUSED = os.environ.get("DIE_MLP_FUSED", "0") == "1"  # non-temporal weight loads (read-once stream)
 
 
 def gemm_decode(x: torch.Tensor, w: torch.Tensor, mode: int = 0, wr: int = 64, sk: int = 1,
@@ -244,6 +250,31 @@ def linear_silu_mul_rownorm(x: torch.Tensor, w_gate_up: torch.Tensor, ssp_in: to
     e = _empty(x.device)
     _kern().gemm_decode(out, x, w_gate_up, 4, wr, 1, DECODE_GEMM_NT, e, e, e, ssp_in, float(eps))
     return out
+
+
+def mlp_decode_ok(hidden: int, inter: int) -> bool:
+    """Shapes the persistent decode-MLP kernel takes (gate/up tiles of 56 columns, down tiles of
+    64 columns x 4 k-slices of whole 256-wide chunks), e.g. Llama-3-8B 4096 / 14336."""
+    return hidden % 128 == 0 and inter % 224 == 0 and (inter // 4) % 256 == 0 and inter // 4 >= 768
+
+
+def mlp_decode(x: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor, ssp_in: torch.Tensor, eps: float,
+               resid: torch.Tensor, ssp_out: torch.Tensor, counters: torch.Tensor, flags: torch.Tensor,
+               err: torch.Tensor, act: Optional[torch.Tensor] = None, slab: Optional[torch.Tensor] = None) -> None:
+    """resid += down(silu(r x Wg^T) * (r x Wu^T)) in ONE persistent launch (gate/up tiles hand their
+    activation columns to the down tiles through per-k-slice flags; see gemm_decode.hip
+    mlp_decode_kernel). r = rsqrt(sum_t ssp_in[t] / H + eps) per row; ssp_out [H/64, 32] receives the
+    next norm's statistics. counters [H/64] and flags [8] int32, zeroed once; err [1] int32 stays 0
+    unless a hand-off wait gave up. x may alias resid (the down tiles write it only after every
+    gate/up tile has finished reading)."""
+    m, h = x.shape
+    inter = w_down.shape[1]
+    if act is None:
+        act = torch.empty(m, inter, dtype=x.dtype, device=x.device)
+    if slab is None:
+        slab = torch.empty(4, m, h, dtype=torch.float32, device=x.device)
+    _kern().mlp_decode(act, slab, x, w_gate_up, w_down, ssp_in, resid, ssp_out, counters, flags, err, float(eps),
+                       DECODE_GEMM_NT)
 
 
 def residual_add_sumsq(resid: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:

@@ -342,6 +342,42 @@ def test_gemm_decode_rownorm_silu(dev, m, inter, k, wr):
     close(y, r, atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("m,h,inter", [(32, 4096, 14336), (1, 4096, 14336), (19, 2048, 7168)])
+def test_mlp_decode_persistent(dev, m, h, inter):
+    """gate/up -> down in one persistent launch (flag hand-off per k-slice) must equal the two-launch
+    path bit for bit (same tiles, same reduction order) and the fp32 reference; x aliases the
+    residual as in the model; flags re-arm across launches; no hand-off wait gives up."""
+    assert ops.mlp_decode_ok(h, inter)
+    x0 = torch.randn(m, h, device=dev, dtype=torch.bfloat16) * 2
+    wgu = torch.randn(2 * inter, h, device=dev, dtype=torch.bfloat16) / math.sqrt(h)
+    wd = torch.randn(h, inter, device=dev, dtype=torch.bfloat16) / math.sqrt(inter)
+    tin = h // 64
+    ssp_in = torch.zeros(tin, 32, device=dev)
+    ssp_in[:, :m] = x0.float().pow(2).view(m, tin, 64).sum(-1).t()
+    td = h // 64
+    flags = torch.zeros(8, dtype=torch.int32, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(td, dtype=torch.int32, device=dev)
+    cnt2 = torch.zeros(td, dtype=torch.int32, device=dev)
+    for it in range(3):
+        h1 = x0.clone()
+        ssp1 = torch.full((td, 32), -1.0, device=dev)
+        ops.mlp_decode(h1, wgu, wd, ssp_in, 1e-5, h1, ssp1, cnt, flags, err)
+        h2 = x0.clone()
+        ssp2 = torch.full((td, 32), -1.0, device=dev)
+        act = ops.linear_silu_mul_rownorm(h2, wgu, ssp_in, 1e-5, 112)
+        ops.linear_slab_residual(act, wd, h2, ssp2, cnt2, 64, 4)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0
+        assert int(flags.abs().sum()) == 0 and int(cnt.abs().sum()) == 0
+        assert torch.equal(h1, h2), (h1.float() - h2.float()).abs().max()
+        assert torch.equal(ssp1, ssp2)
+    xn = x0.float() * torch.rsqrt(x0.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    gu = xn @ wgu.float().t()
+    ref_h = x0.float() + (torch.nn.functional.silu(gu[:, :inter]) * gu[:, inter:]) @ wd.float().t()
+    close(h1, ref_h.to(torch.bfloat16), atol=6e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("g,hkv", [(4, 8), (8, 1), (1, 4)])
 def test_attn_decode_fused(dev, g, hkv):
     """Fused prologue: norm scale + qkv slab sum + RoPE at ctx-1 + KV write, then attention."""
