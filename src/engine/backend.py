@@ -90,6 +90,11 @@ class LLMBackend:
     def close(self) -> None:
         self.async_engine.stop()
 
+    def healthy(self) -> bool:
+        """False once the engine loop died (e.g. a HIP fault surfaced as an exception): the worker
+        then reports itself unhealthy and fails requests as retryable elsewhere."""
+        return self.async_engine.error is None
+
     def load(self) -> float:
         s = self.engine.scheduler
         return (len(s.running) + len(s.waiting)) / max(1, self.engine.cfg.max_num_seqs)

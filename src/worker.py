@@ -35,7 +35,7 @@ import os
 import signal
 import sys
 import time
-from typing import Any, Dict, Optional
+from typing import Any, Dict, List, Optional
 
 if __package__ in (None, ""):  # `python src/worker.py`
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -201,7 +201,8 @@ class Worker:
         op = msg.get("op", "infer")
         if op == "health":
             self._probe_count += 1
-            return {"success": True, "worker_id": self.worker_id, "load": self.load(),
+            failed = self.failed_models()
+            return {"success": not failed, "worker_id": self.worker_id, "load": self.load(), "failed_models": failed,
                     "models": list(self.models),
                     "archs": {n: getattr(getattr(m, "config", None), "arch", "mock") for n, m in self.models.items()}}
         if op == "metrics":
@@ -253,6 +254,9 @@ class Worker:
         model = self.models.get(model_name)
         if model is None:
             return {"error": f"Model '{model_name}' not found", "success": False}
+        if model_name in self.failed_models():
+            return {"error": f"model '{model_name}' engine failed on {self.worker_id}", "success": False,
+                    "retryable": True}
         rid = request.get("request_id")
         try:
             if rid:
@@ -266,7 +270,8 @@ class Worker:
             return resp
         except Exception as e:
             logger.error("Error processing request: %s", e)
-            return {"error": str(e), "success": False}
+            # an engine failure (not a bad input) may succeed on another replica
+            return {"error": str(e), "success": False, "retryable": model_name in self.failed_models()}
 
     async def _process_batch(self, request: Dict[str, Any]) -> Dict[str, Any]:
         model_name = request.get("model")
@@ -284,9 +289,13 @@ class Worker:
             return {"model": model_name, "outputs_list": outs, "worker_id": self.worker_id, "success": True}
         except Exception as e:
             logger.error("Error processing batch: %s", e)
-            return {"error": str(e), "success": False}
+            return {"error": str(e), "success": False, "retryable": model_name in self.failed_models()}
 
     # --------------------------------------------------------------- models
+    def failed_models(self) -> List[str]:
+        """Loaded models whose engine has died (GPU fault surfaced by the engine loop)."""
+        return [n for n, m in self.models.items() if hasattr(m, "healthy") and not m.healthy()]
+
     def load_model(self, config: ModelConfig) -> bool:
         if config.model_name in self.models:
             logger.warning("Model '%s' is already loaded", config.model_name)

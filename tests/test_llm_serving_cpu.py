@@ -70,3 +70,41 @@ def test_disaggregated_workers_over_rpc():
         for w in (pre, dec, solo):
             await w.shutdown()
     asyncio.run(main())
+
+
+def test_engine_failure_marks_worker_unhealthy_and_retries_elsewhere():
+    """A dead engine (as after a HIP fault: the engine loop raised) makes the worker fail its health
+    probe and answer requests with a retryable error; the coordinator retries them on the healthy
+    replica, so clients still succeed."""
+    async def main():
+        bad = Worker("bad", host="127.0.0.1", install_signal_handlers=False)
+        good = Worker("good", host="127.0.0.1", install_signal_handlers=False)
+        assert bad.load_model(llm_cfg()) and good.load_model(llm_cfg())
+        bport, gport = await bad.start(), await good.start()
+
+        coord = Coordinator(port=0, max_batch_size=4, max_latency_ms=2)
+        cport = await coord.start()
+        await coord.add_static_worker(f"127.0.0.1:{bport}")
+        await coord.add_static_worker(f"127.0.0.1:{gport}")
+
+        def boom():
+            raise RuntimeError("simulated HIP fault")
+
+        bad.models["tiny"].engine.step = boom  # dies on its next step, after passing registration
+        c = InferenceClient(f"127.0.0.1:{cport}")
+        reqs = [{"prompt": f"req {i}", "max_tokens": 3, "ignore_eos": True, "temperature": 0.5} for i in range(8)]
+        rs = await asyncio.wait_for(asyncio.gather(*(c.infer("tiny", q) for q in reqs)), 120)
+        assert all(x["success"] for x in rs), rs
+        assert coord.stats["retries"] > 0  # some requests hit the dead engine first and moved over
+        cb = InferenceClient(f"127.0.0.1:{bport}")
+        r = await asyncio.wait_for(cb.infer("tiny", {"prompt": "x", "max_tokens": 3}), 60)
+        assert not r["success"] and r.get("retryable"), r
+        h = await cb.call({"op": "health"})
+        assert not h["success"] and h["failed_models"] == ["tiny"]
+        assert all(x.get("worker_id") == "good" for x in rs)
+        c.close()
+        cb.close()
+        await coord.stop()
+        await bad.shutdown()
+        await good.shutdown()
+    asyncio.run(main())
