@@ -66,6 +66,8 @@ class AsyncLLMEngine:
             return fut
         self._q.put((request_id, prompt_ids, sampling, fut, loop, user_data))
         self._wake.set()
+        if self.error is not None:  # the loop died between the check above and the put
+            self._fail_pending()
         return fut
 
     def submit_sync(self, request_id: str, prompt_ids: List[int], sampling: SamplingParams,
@@ -73,6 +75,8 @@ class AsyncLLMEngine:
         """Non-asyncio submission: ``callback(seq_or_exception)`` runs on the engine thread."""
         self._q.put((request_id, prompt_ids, sampling, callback, None, None))
         self._wake.set()
+        if self.error is not None:
+            self._fail_pending()
 
     def call(self, fn, loop: Optional[asyncio.AbstractEventLoop] = None) -> asyncio.Future:
         """Run ``fn(engine)`` on the engine thread between steps; the future
@@ -81,7 +85,22 @@ class AsyncLLMEngine:
         fut = loop.create_future()
         self._q.put(("__call__", fn, None, fut, loop, None))
         self._wake.set()
+        if self.error is not None:
+            self._fail_pending()
         return fut
+
+    def _fail_pending(self) -> None:
+        """After the loop died: fail every queued submission (thread-safe, idempotent)."""
+        err = RuntimeError(f"engine failed: {self.error!r}")
+        while True:
+            try:
+                rid, _, _, fut, loop, _ = self._q.get_nowait()
+            except queue.Empty:
+                return
+            if loop is None:
+                fut(err)
+            else:
+                loop.call_soon_threadsafe(_fail, fut, err)
 
     def _drain(self) -> None:
         while True:
@@ -141,6 +160,7 @@ class AsyncLLMEngine:
                         seq.on_finish(seq)
                     except Exception:
                         pass
+            self._fail_pending()
 
     def stats(self) -> Dict[str, Any]:
         s = self.engine.get_stats()
