@@ -140,6 +140,7 @@ class AsyncLLMEngine:
             while not self._stop.is_set():
                 self._drain()
                 if not eng.has_work():
+                    eng.runner.idle_tick()
                     self._wake.wait(0.05)
                     self._wake.clear()
                     continue

@@ -186,7 +186,10 @@ class ModelRunner:
         return ids[:n].tolist()
 
     # ------------------------------------------------------------ prefill
-    KIND_STOP, KIND_PREFILL, KIND_DECODE = 0, 1, 2
+    KIND_STOP, KIND_PREFILL, KIND_DECODE, KIND_HEARTBEAT = 0, 1, 2, 3
+
+    def idle_tick(self) -> None:
+        """Called by the engine loop while it has no work (TP runners send heartbeats)."""
 
     def _sync_step(self, kind: int, a: int = 0, b: int = 0, c: int = 0, d: int = 0) -> None:
         """Hook for tensor parallelism: rank 0 publishes the step to followers

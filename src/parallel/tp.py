@@ -15,6 +15,7 @@ On CPU the same code runs on ``gloo`` for tests.
 
 from __future__ import annotations
 
+import datetime
 import os
 from dataclasses import dataclass
 from typing import Optional
@@ -88,10 +89,13 @@ class TPContext:
 _TP: Optional[TPContext] = None
 
 
-def init_tp(tp_size: Optional[int] = None, backend: Optional[str] = None) -> TPContext:
+def init_tp(tp_size: Optional[int] = None, backend: Optional[str] = None,
+            timeout_s: Optional[float] = None) -> TPContext:
     """Initialise (or reuse) the default process group and return the TP
     context. Reads RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* from the
-    environment (torchrun)."""
+    environment (torchrun). ``timeout_s`` bounds every collective (a dead rank
+    then fails its peers instead of hanging them; serving leaders send
+    heartbeats while idle, see tp_runner)."""
     global _TP
     world = int(os.environ.get("WORLD_SIZE", "1"))
     tp = tp_size or world
@@ -103,7 +107,8 @@ def init_tp(tp_size: Optional[int] = None, backend: Optional[str] = None) -> TPC
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-        dist.init_process_group(backend=backend)
+        kw = {"timeout": datetime.timedelta(seconds=timeout_s)} if timeout_s else {}
+        dist.init_process_group(backend=backend, **kw)
     rank = dist.get_rank()
     if dist.get_world_size() == tp:
         group = None

@@ -9,11 +9,19 @@ step rank 0 builds the inputs, copies them to its device and broadcasts a
 identical forward — including replaying the same captured decode hipGraph —
 and meet in the two per-layer all-reduces and the logits all-gather. Only
 rank 0 copies sampled token ids back to the host.
+
+Failure as a unit: the process group carries a finite collective timeout
+(``init_tp(timeout_s=...)``) so a dead rank turns every peer's next collective
+into an error (the leader's engine loop dies → its worker reports unhealthy →
+the coordinator routes elsewhere) instead of a hang. An idle leader therefore
+broadcasts a heartbeat step every ``HEARTBEAT_S`` so that followers parked in
+their header broadcast never hit that timeout.
 """
 
 from __future__ import annotations
 
 import logging
+import time
 from typing import Optional
 
 import torch
@@ -27,9 +35,12 @@ logger = logging.getLogger(__name__)
 
 
 class TPModelRunner(ModelRunner):
+    HEARTBEAT_S = 20.0
+
     def __init__(self, model: CausalLM, pool: KVPool, cfg: EngineConfig, max_model_len: int):
         super().__init__(model, pool, cfg, max_model_len)
         self.tp = model.tp
+        self._last_sync = time.monotonic()
         self.hdr = torch.zeros(6, dtype=torch.int64, device=self.device)
         self.h_hdr = torch.zeros(6, dtype=torch.int64, pin_memory=self.is_cuda)
 
@@ -39,6 +50,7 @@ class TPModelRunner(ModelRunner):
     def _sync_step(self, kind: int, a: int = 0, b: int = 0, c: int = 0, d: int = 0) -> None:
         if not self.tp.enabled:
             return
+        self._last_sync = time.monotonic()
         self.h_hdr.copy_(torch.tensor([kind, a, b, c, d, 0], dtype=torch.int64))
         self.hdr.copy_(self.h_hdr, non_blocking=self.is_cuda)
         self._bcast(self.hdr)
@@ -58,6 +70,10 @@ class TPModelRunner(ModelRunner):
                         self.d_bt[:pad]):
                 self._bcast(buf)
 
+    def idle_tick(self) -> None:
+        if self.tp.enabled and self.tp.rank == 0 and time.monotonic() - self._last_sync > self.HEARTBEAT_S:
+            self._sync_step(self.KIND_HEARTBEAT)
+
     def stop_followers(self) -> None:
         if self.tp.enabled and self.tp.rank == 0:
             self._sync_step(self.KIND_STOP)
@@ -71,6 +87,8 @@ class TPModelRunner(ModelRunner):
             kind, a, b, c, d, _ = (int(x) for x in self.hdr.tolist())
             if kind == self.KIND_STOP:
                 return
+            if kind == self.KIND_HEARTBEAT:
+                continue
             self._bcast_inputs(kind, a, b, c, d)
             if kind == self.KIND_PREFILL:
                 self._exec_prefill(a, b, c, d, True)

@@ -48,7 +48,7 @@ def main(argv=None) -> None:
     args = build_arg_parser().parse_args(argv)
     if args.arch == "mock":
         args.arch = "llama"
-    tp = init_tp(args.tp_size)
+    tp = init_tp(args.tp_size, timeout_s=300)  # idle leaders send heartbeats (tp_runner.HEARTBEAT_S)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     device = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
     from src.engine.backend import engine_config_from

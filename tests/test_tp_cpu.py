@@ -41,6 +41,9 @@ def _worker(rank, world, port, preset, q):
                               dtype=torch.float32, full_init=True, seed=3)
         if rank == 0:
             obj.eos_token_id = None
+            obj.runner.HEARTBEAT_S = 0.0  # idle heartbeats must be absorbed by the followers
+            for _ in range(3):
+                obj.runner.idle_tick()
             outs = obj.generate(PROMPTS, SamplingParams(max_tokens=6))
             obj.runner.stop_followers()
             q.put(outs)
