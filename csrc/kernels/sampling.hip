@@ -126,6 +126,9 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
     for (int j = 0; j < 8; ++j) best = better(best, ArgMax{z[j], i + j});
   }
   best = block_argmax(best, red);
+  // an all-NaN / all -inf row (e.g. a padded graph row over uninitialised KV) still yields a
+  // valid token id: an out-of-range id would turn into an out-of-bounds embedding read next step
+  if (best.i >= vocab) best.i = 0;
   if (temp <= 0.f || k == 1) {
     if (threadIdx.x == 0) out[r] = best.i;
     return;
@@ -165,7 +168,7 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
     }
   }
   g = block_argmax(g, red);
-  if (threadIdx.x == 0) out[r] = g.i <= vocab ? g.i : best.i;
+  if (threadIdx.x == 0) out[r] = g.i < vocab ? g.i : best.i;
 }
 
 hipError_t launch_sample(int64_t* out, const bf16_t* logits, int64_t stride, int rows, int vocab,

@@ -39,7 +39,9 @@ class KVPool:
     def __init__(self, num_layers: int, num_blocks: int, kv_heads: int, block_size: int, head_dim: int, device,
                  dtype=torch.bfloat16):
         self.shape = (num_layers, 2, num_blocks, kv_heads, block_size, head_dim)
-        self.tensor = torch.empty(self.shape, dtype=dtype, device=device)
+        # zeroed once: a padded graph row reads block 0 before anything was written there, and
+        # uninitialised bf16 can hold NaN bit patterns
+        self.tensor = torch.zeros(self.shape, dtype=dtype, device=device)
         self.num_blocks = num_blocks
         self.block_size = block_size
 
@@ -292,6 +294,10 @@ class ModelRunner:
                                     self.h_bt.data_ptr(), self.bt_width, pad)
         self._fill_sampling(seqs, pad)
         self._h2d(pad, pad, with_cu=False)
+        if self.supports_multistep:  # the graph's input advance must see this step's real rows
+            self.h_ctl[0] = 0
+            self.h_ctl[1] = n
+            self.d_ctl.copy_(self.h_ctl, non_blocking=True)
         self._sync_step(self.KIND_DECODE, n, pad)
         ids = self._exec_decode(n, pad)
         return self._to_host(ids, n)
