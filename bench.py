@@ -58,6 +58,8 @@ def parse():
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--temperature", type=float, default=0.0)
     p.add_argument("--tp", type=int, default=1, help="tensor-parallel degree per replica (70B: --tp 8)")
+    p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                   help="cpu: reference-op engine over gloo (tests the multi-rank plumbing, not a measurement)")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args()
 
@@ -86,10 +88,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     n_gpus = args.gpus or world
+    on_gpu = args.device == "cuda"
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    dev = torch.device(f"cuda:{local}")
+        if on_gpu:
+            torch.cuda.set_device(local)
+        dist.init_process_group("nccl" if on_gpu else "gloo")  # nccl = RCCL over xGMI
+    dev = torch.device(f"cuda:{local}" if on_gpu else "cpu")
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize(dev)
 
     from src.batcher import Batcher
     from src.config import EngineConfig
@@ -111,10 +119,10 @@ def main():
                               capture=not args.no_graph)
         if tp.rank != 0:  # follower: mirror the leader through warmup and the timed waves
             obj.follower_loop()
-            torch.cuda.synchronize(dev)
+            sync()
             dist.barrier()
             obj.follower_loop()
-            torch.cuda.synchronize(dev)
+            sync()
             dist.barrier()
             t = torch.zeros(1, device=dev, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -147,12 +155,12 @@ def main():
         await batcher.start()
         for w in range(args.warmup):
             await serve_wave(batcher, args.batch, args.prompt_len, args.gen_len, args.temperature, rng, f"w{w}", engine.arch.vocab_size)
-        torch.cuda.synchronize(dev)
+        sync()
         if tp is not None:
             engine.runner.stop_followers()
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize(dev)
+        sync()
         stats0 = dict(engine.stats)
         t0 = time.perf_counter()
         lats = []
@@ -161,12 +169,12 @@ def main():
                                      f"s{s}")
             if args.verbose and rank == 0:
                 print(f"step {s}: {time.perf_counter() - t0:.2f}s", file=sys.stderr, flush=True)
-        torch.cuda.synchronize(dev)
+        sync()
         if tp is not None:
             engine.runner.stop_followers()
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize(dev)
+        sync()
         elapsed = time.perf_counter() - t0
         await batcher.stop()
         return elapsed, lats, stats0
