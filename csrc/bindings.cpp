@@ -583,6 +583,64 @@ void rope_and_cache_slab(Tensor q_out, Tensor slab, Tensor positions, Tensor cos
                                           (int)hq, (int)hkv, (int)head_dim, (int)k_cache.size(2), cur_stream()));
 }
 
+// ---- one-shot all-reduce over IPC-mapped peer buffers (src/parallel/custom_allreduce.py)
+int64_t car_alloc(int64_t bytes) {
+  TORCH_CHECK(bytes > 0 && bytes % 256 == 0, "car_alloc: bytes must be a positive multiple of 256");
+  void* p = nullptr;
+  DIE_HIP(die::car_malloc(&p, (size_t)bytes));
+  return reinterpret_cast<int64_t>(p);
+}
+
+void car_release(int64_t ptr) { DIE_HIP(die::car_free(reinterpret_cast<void*>(ptr))); }
+
+py::bytes car_handle(int64_t ptr) {
+  char h[sizeof(hipIpcMemHandle_t)];
+  DIE_HIP(die::car_ipc_handle(reinterpret_cast<void*>(ptr), h));
+  return py::bytes(h, sizeof(h));
+}
+
+int64_t car_open(py::bytes handle) {
+  std::string s = handle;
+  TORCH_CHECK(s.size() == sizeof(hipIpcMemHandle_t), "bad IPC handle size");
+  void* p = nullptr;
+  DIE_HIP(die::car_ipc_open(s.data(), &p));
+  return reinterpret_cast<int64_t>(p);
+}
+
+void car_close(int64_t ptr) { DIE_HIP(die::car_ipc_close(reinterpret_cast<void*>(ptr))); }
+
+std::vector<int64_t> car_read_words(int64_t ptr, int64_t n) {  // synchronising host read of uint32 words
+  TORCH_CHECK(n > 0 && n <= 64, "car_read_words: 1..64 words");
+  std::vector<uint32_t> h((size_t)n);
+  DIE_HIP(hipDeviceSynchronize());
+  DIE_HIP(hipMemcpy(h.data(), reinterpret_cast<void*>(ptr), (size_t)n * 4, hipMemcpyDeviceToHost));
+  return std::vector<int64_t>(h.begin(), h.end());
+}
+
+void car_all_reduce(Tensor in, Tensor out, int64_t rank, std::vector<int64_t> bufs, std::vector<int64_t> sigs,
+                    int64_t ctl, int64_t cap_elems, int64_t blocks) {
+  DIE_CHECK_CUDA(in);
+  DIE_CHECK_BF16(in);
+  DIE_CHECK_BF16(out);
+  DIE_CHECK_CONTIG(in);
+  DIE_CHECK_CONTIG(out);
+  TORCH_CHECK(in.numel() == out.numel(), "all_reduce: in/out sizes differ");
+  TORCH_CHECK(in.numel() % 8 == 0 && in.numel() <= cap_elems, "all_reduce: numel must be a multiple of 8 <= cap");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(in.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "all_reduce: 16-byte alignment");
+  const int world = (int)bufs.size();
+  TORCH_CHECK(world >= 2 && world <= die::CAR_MAX_RANKS && (int)sigs.size() == world, "all_reduce: 2..8 ranks");
+  TORCH_CHECK(rank >= 0 && rank < world && ctl != 0, "all_reduce: bad rank / control word");
+  die::CarPeers peers;
+  for (int p = 0; p < world; ++p) {
+    TORCH_CHECK(bufs[p] != 0 && sigs[p] != 0, "all_reduce: null peer pointer");
+    peers.buf[p] = reinterpret_cast<die::bf16_t*>(bufs[p]);
+    peers.sig[p] = reinterpret_cast<uint32_t*>(sigs[p]);
+  }
+  DIE_HIP(die::launch_custom_all_reduce(bf(in), bf(out), in.numel(), (int)rank, world, peers,
+                                        reinterpret_cast<uint32_t*>(ctl), cap_elems, (int)blocks, cur_stream()));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -613,4 +671,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_decode_grouped", &gemm_decode_grouped);
   m.def("fused_add_rms_norm_slab", &fused_add_rms_norm_slab);
   m.def("rope_and_cache_slab", &rope_and_cache_slab);
+  m.def("car_alloc", &car_alloc);
+  m.def("car_release", &car_release);
+  m.def("car_handle", &car_handle);
+  m.def("car_open", &car_open);
+  m.def("car_close", &car_close);
+  m.def("car_all_reduce", &car_all_reduce);
+  m.def("car_read_words", &car_read_words);
 }

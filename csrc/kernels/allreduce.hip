@@ -1,0 +1,147 @@
+// One-shot all-reduce over xGMI for the small, latency-bound messages of tensor-parallel decode
+// (Llama-3-70B TP=8 at batch 32: two [32, 8192] bf16 = 512 KiB sums per layer, 160 per step).
+//
+// Why not only RCCL: its ring/tree algorithms move a message through W-1 hops, each paying an xGMI
+// round trip plus a protocol step; for sub-MiB messages the latency term dominates. On one
+// MI355X node every GPU has a direct xGMI link to each of the 7 others, so a ONE-SHOT exchange is a
+// single hop on all 7 links at once: every rank publishes its input in a buffer the peers have
+// IPC-mapped, and every rank reads all W inputs and sums them itself (in rank order, so the W
+// results are bit-identical — tensor-parallel ranks must stay in lockstep).
+//
+// Protocol per call (epoch e = 1, 2, ...; buffers and flags double-buffered by e & 1):
+//   1. workgroup b copies slice b of its input into its own IPC staging buffer (uncached memory:
+//      peers read it over xGMI without any cache of this GPU in the way);
+//   2. after a system-scope release, one lane per peer stores e into that peer's flag slot
+//      [e & 1][b][my rank] (a remote store over xGMI into the peer's uncached signal page);
+//   3. one lane per peer polls this rank's own slot [e & 1][b][peer] until it reads e (bounded
+//      spin: a dead peer sets the error word instead of hanging the GPU), system-scope acquire;
+//   4. slice b of the output = sum over ranks p = 0..W-1 of (p == me ? input : peer p's buffer).
+// Double buffering makes an end barrier unnecessary: call e + 2 overwrites the half that peers
+// read in call e only after every peer has signalled call e + 1, i.e. has finished call e
+// (its kernels are stream-ordered).
+// The epoch lives in device memory (the last workgroup to finish advances it), so the launch is
+// hipGraph-capturable and replays correctly.
+#include "common.h"
+#include "launchers.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace die {
+
+namespace car {
+constexpr int NTH = 512;
+
+__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+}  // namespace car
+
+__global__ void __launch_bounds__(car::NTH) custom_all_reduce_kernel(const bf16_t* __restrict__ in,
+                                                                     bf16_t* __restrict__ out, int64_t nvec,
+                                                                     int rank, int world, CarPeers peers,
+                                                                     uint32_t* __restrict__ ctl, int64_t cap_vec) {
+  using namespace car;
+  const int tid = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
+  const uint32_t epoch = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const int par = (int)(epoch & 1u);
+  const int64_t per = (nvec + nb - 1) / nb;
+  const int64_t v0 = min(nvec, (int64_t)b * per), v1 = min(nvec, v0 + per);
+
+  // 1. publish this rank's slice
+  const uint4* src = reinterpret_cast<const uint4*>(in);
+  uint4* mine = reinterpret_cast<uint4*>(peers.buf[rank]) + par * cap_vec;
+  for (int64_t i = v0 + tid; i < v1; i += NTH) mine[i] = src[i];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the stores reach memory first
+  __syncthreads();
+  // 2. signal every peer, 3. wait for every peer's signal
+  uint32_t* slots = peers.sig[rank] + ((int64_t)par * CAR_MAX_BLOCKS + b) * CAR_MAX_RANKS;
+  if (tid < world && tid != rank) {
+    st_sys(peers.sig[tid] + ((int64_t)par * CAR_MAX_BLOCKS + b) * CAR_MAX_RANKS + rank, epoch);
+    uint32_t it = 0;
+    while (ld_sys(slots + tid) != epoch) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++it > (1u << 25)) {  // ~2 s: a missing peer reports instead of hanging the GPU
+        __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // peers' slices are read after their flags
+
+  // 4. reduce in rank order (bit-identical on every rank)
+  const uint4* bufs[CAR_MAX_RANKS];
+#pragma unroll
+  for (int p = 0; p < CAR_MAX_RANKS; ++p)
+    bufs[p] = p < world ? reinterpret_cast<const uint4*>(peers.buf[p]) + par * cap_vec : nullptr;
+  uint4* dst = reinterpret_cast<uint4*>(out);
+  for (int64_t i = v0 + tid; i < v1; i += NTH) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < world; ++p) {
+      const uint4 v = p == rank ? src[i] : bufs[p][i];  // uncached: read from the peer over xGMI
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += f[j];
+    }
+    uint4 o;
+    o.x = pack2(acc[0], acc[1]);
+    o.y = pack2(acc[2], acc[3]);
+    o.z = pack2(acc[4], acc[5]);
+    o.w = pack2(acc[6], acc[7]);
+    dst[i] = o;
+  }
+  // 5. the last workgroup advances the epoch for the next call (every workgroup read it at entry)
+  __syncthreads();
+  if (tid == 0) {
+    if (__hip_atomic_fetch_add(ctl + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)nb - 1) {
+      __hip_atomic_store(ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+hipError_t launch_custom_all_reduce(const bf16_t* in, bf16_t* out, int64_t n, int rank, int world,
+                                    const CarPeers& peers, uint32_t* ctl, int64_t cap_elems, int blocks,
+                                    hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (n % 8 || world < 2 || world > CAR_MAX_RANKS || rank < 0 || rank >= world || n > cap_elems ||
+      blocks < 1 || blocks > CAR_MAX_BLOCKS)
+    return hipErrorInvalidValue;
+  for (int p = 0; p < world; ++p)
+    if (peers.buf[p] == nullptr || peers.sig[p] == nullptr) return hipErrorInvalidValue;
+  const int64_t nvec = n / 8;
+  blocks = (int)std::min<int64_t>(blocks, (nvec + 63) / 64);  // at least 64 vectors (1 KiB) per workgroup
+  hipLaunchKernelGGL(custom_all_reduce_kernel, dim3(blocks), dim3(car::NTH), 0, s, in, out, nvec, rank, world,
+                     peers, ctl, cap_elems / 8);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- IPC-shareable allocations
+// Staging buffers and flag pages are allocated uncached (hipDeviceMallocUncached): the peers'
+// loads and stores over xGMI then never meet a stale line in this GPU's L2.
+hipError_t car_malloc(void** p, size_t bytes) {
+  hipError_t e = hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return e;
+  return hipMemset(*p, 0, bytes);
+}
+
+hipError_t car_free(void* p) { return hipFree(p); }
+
+hipError_t car_ipc_handle(void* p, void* handle64) {
+  return hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(handle64), p);
+}
+
+hipError_t car_ipc_open(const void* handle64, void** p) {
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle64, sizeof(h));
+  return hipIpcOpenMemHandle(p, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+hipError_t car_ipc_close(void* p) { return hipIpcCloseMemHandle(p); }
+
+}  // namespace die

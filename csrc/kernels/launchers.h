@@ -93,4 +93,20 @@ hipError_t launch_rope_and_cache_slab(bf16_t* q_out, const float* slab, int sk, 
                                       bf16_t* v_cache, int num_tokens, int hq, int hkv, int head_dim, int block_size,
                                       hipStream_t s);
 
+// one-shot all-reduce over IPC-mapped peer buffers (allreduce.hip)
+constexpr int CAR_MAX_RANKS = 8;
+constexpr int CAR_MAX_BLOCKS = 64;
+struct CarPeers {
+  bf16_t* buf[CAR_MAX_RANKS] = {};    // per rank: staging [2][cap] (its own = local, others IPC-mapped)
+  uint32_t* sig[CAR_MAX_RANKS] = {};  // per rank: flag page [2][CAR_MAX_BLOCKS][CAR_MAX_RANKS]
+};
+hipError_t launch_custom_all_reduce(const bf16_t* in, bf16_t* out, int64_t n, int rank, int world,
+                                    const CarPeers& peers, uint32_t* ctl, int64_t cap_elems, int blocks,
+                                    hipStream_t s);
+hipError_t car_malloc(void** p, size_t bytes);
+hipError_t car_free(void* p);
+hipError_t car_ipc_handle(void* p, void* handle64);
+hipError_t car_ipc_open(const void* handle64, void** p);
+hipError_t car_ipc_close(void* p);
+
 }  // namespace die

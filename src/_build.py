@@ -26,7 +26,7 @@ EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 ARCH = os.environ.get("DIE_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-KERNELS = ["norm_act", "rope_cache", "attention", "sampling", "moe", "gemm_decode", "decode_step"]
+KERNELS = ["norm_act", "rope_cache", "attention", "sampling", "moe", "gemm_decode", "decode_step", "allreduce"]
 
 
 def _torch_paths():

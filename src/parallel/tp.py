@@ -10,6 +10,9 @@ over the 7 xGMI links. QKV and gate/up are column-parallel (each rank owns
 whole heads / a contiguous slice of the FFN), the LM head is vocab-parallel
 with one all-gather of the logits, the embedding is replicated (2 GiB for
 70B — trivial against 288 GB of HBM, and it saves a collective per step).
+Decode-sized all-reduces (<= 8 MiB bf16) take the one-shot IPC kernel of
+``custom_allreduce.py`` (one xGMI hop on all 7 links at once, bit-identical
+on every rank); prefill-sized ones stay on RCCL.
 On CPU the same code runs on ``gloo`` for tests.
 """
 
@@ -29,6 +32,20 @@ class TPContext:
     rank: int = 0
     world_size: int = 1
     group: Optional[object] = None
+    car: Optional[object] = None  # CustomAllReduce (one-shot IPC all-reduce) once enabled
+
+    def enable_custom_allreduce(self, max_bytes: int = 8 << 20) -> bool:
+        """Collective over the group: set up the one-shot IPC all-reduce (src/parallel/custom_allreduce.py)
+        for GPU tensors of up to ``max_bytes`` — the decode-sized messages; larger ones stay on RCCL.
+        ``DIE_CUSTOM_AR=0`` keeps everything on RCCL. Every rank must make the same call."""
+        if not self.enabled or self.car is not None:
+            return self.car is not None
+        if os.environ.get("DIE_CUSTOM_AR", "1") == "0" or not torch.cuda.is_available() or self.world_size > 8:
+            return False
+        from src.parallel.custom_allreduce import CustomAllReduce
+
+        self.car = CustomAllReduce(self.rank, self.world_size, self.group, max_bytes=max_bytes)
+        return True
 
     @property
     def enabled(self) -> bool:
@@ -54,7 +71,15 @@ class TPContext:
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.enabled:
-            if self._staged(t):
+            car = self.car
+            # the choice depends only on dtype and size, so every rank takes the same path
+            if car is not None and t.is_cuda and t.dtype == torch.bfloat16 and t.numel() % 8 == 0 \
+                    and 0 < 2 * t.numel() <= car.max_bytes:
+                if t.is_contiguous() and t.data_ptr() % 16 == 0:
+                    car.all_reduce(t)
+                else:
+                    t.copy_(car.all_reduce(t.contiguous().clone()))
+            elif self._staged(t):
                 c = t.float().cpu()
                 dist.all_reduce(c, group=self.group)
                 t.copy_(c)

@@ -121,6 +121,8 @@ def build_tp_engine(preset: str, tp, device, cfg: Optional[EngineConfig] = None,
     ckpt = is_hf_checkpoint(preset)  # `preset` may be a local HF checkpoint directory
     arch = arch_from_hf_config(preset, **arch_overrides) if ckpt else get_preset(preset, **arch_overrides)
     cfg = cfg or EngineConfig()
+    if torch.device(device).type == "cuda":
+        tp.enable_custom_allreduce()  # decode-sized all-reduces: one xGMI hop instead of RCCL's ring
     model = CausalLM(arch, device, dtype=dtype, tp=tp, seed=seed, max_position=max(max_model_len, 16),
                      full_init=full_init)
     if ckpt:

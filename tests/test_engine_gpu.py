@@ -184,7 +184,7 @@ def _tp_gpu_worker(rank, world, port, q, preset):
                               full_init=True, seed=3)
         if rank == 0:
             obj.eos_token_id = None
-            q.put(obj.generate(TP_PROMPTS, SamplingParams(max_tokens=8)))
+            q.put((obj.generate(TP_PROMPTS, SamplingParams(max_tokens=8)), tp.car is not None))
             obj.runner.stop_followers()
         else:
             obj.follower_loop()
@@ -216,10 +216,11 @@ def test_tensor_parallel_tp2_on_one_gpu(preset):
     procs = [ctx.Process(target=_tp_gpu_worker, args=(r, 2, port, q, preset)) for r in range(2)]
     for p in procs:
         p.start()
-    got = q.get(timeout=600)
+    got, used_car = q.get(timeout=600)
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
+    assert used_car  # decode/prefill all-reduces went through the one-shot IPC kernel (allreduce.hip)
     m = CausalLM(get_preset(preset), "cuda:0", seed=3, max_position=512, full_init=True)
     for p, o in zip(TP_PROMPTS, got):
         r, mg = reference_with_margins(m, p, 8)
