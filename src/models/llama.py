@@ -63,11 +63,18 @@ class CausalLM:
 
     def __init__(self, arch: ArchConfig, device, dtype=torch.bfloat16, tp: Optional[TPContext] = None,
                  seed: int = 0, init_std: float = 0.02, max_position: Optional[int] = None,
-                 full_init: bool = False):
+                 full_init: bool = False, moe_parallel: str = "tp"):
         """``full_init=True`` draws every weight at full (unsharded) size from a
         rank-independent generator and slices this rank's shard — identical to
         the TP=1 model, used by the TP equivalence tests. The default draws
-        only the local shard (never materialises a 70B tensor)."""
+        only the local shard (never materialises a 70B tensor).
+
+        ``moe_parallel`` (MoE models under TP): ``"tp"`` splits every expert's FFN dimension over
+        the ranks; ``"ep"`` (expert parallelism) gives each rank whole experts
+        ``[rank * E/tp, (rank + 1) * E/tp)`` — bigger per-expert GEMMs, no FFN-dim divisibility
+        constraint. Attention stays tensor-parallel, so every rank holds every token: the routed
+        assignments to remote experts are masked locally and the MoE's TP all-reduce is the combine
+        (no all-to-all, see ops.expert_parallel_local)."""
         self.arch = arch
         self.device = torch.device(device)
         self.dtype = dtype
@@ -75,7 +82,16 @@ class CausalLM:
         a, tpc = arch, self.tp
         self.hq = tpc.shard(a.num_heads)
         self.hkv = tpc.kv_heads(a.num_kv_heads)
-        self.inter = tpc.shard(a.intermediate_size)
+        self.ep = bool(a.is_moe and tpc.enabled and moe_parallel == "ep")
+        if moe_parallel not in ("tp", "ep"):
+            raise ValueError(f"moe_parallel must be 'tp' or 'ep', got {moe_parallel!r}")
+        if self.ep:
+            self.experts_local = tpc.shard(a.num_experts)
+            self.expert0 = tpc.rank * self.experts_local
+            self.inter = a.intermediate_size  # whole experts per rank
+        else:
+            self.experts_local, self.expert0 = a.num_experts, 0
+            self.inter = tpc.shard(a.intermediate_size)
         self.vocab_local = tpc.shard(a.vocab_size) if a.vocab_size % tpc.world_size == 0 else a.vocab_size
         self.vocab_parallel = self.vocab_local != a.vocab_size
         self.head_dim = a.head_dim
@@ -145,10 +161,17 @@ class CausalLM:
                                gen, genf)
             if a.is_moe:
                 lw.router = self._randn(a.num_experts, h, std=std, gen=gen_e)  # replicated router
-                lw.w13 = self._param((a.num_experts, 2 * self.inter, h), (a.num_experts, 2 * big, h),
-                                     self.shard_gate_up, std, gen, genf)
-                lw.w2 = self._param((a.num_experts, h, self.inter), (a.num_experts, h, big),
-                                    lambda t: self.shard_cols(t, self.inter), ostd, gen, genf)
+                if self.ep:  # whole experts [expert0, expert0 + experts_local)
+                    e0, el = self.expert0, self.experts_local
+                    lw.w13 = self._param((el, 2 * big, h), (a.num_experts, 2 * big, h), lambda t: t[e0:e0 + el],
+                                         std, gen, genf)
+                    lw.w2 = self._param((el, h, big), (a.num_experts, h, big), lambda t: t[e0:e0 + el], ostd,
+                                        gen, genf)
+                else:
+                    lw.w13 = self._param((a.num_experts, 2 * self.inter, h), (a.num_experts, 2 * big, h),
+                                         self.shard_gate_up, std, gen, genf)
+                    lw.w2 = self._param((a.num_experts, h, self.inter), (a.num_experts, h, big),
+                                        lambda t: self.shard_cols(t, self.inter), ostd, gen, genf)
             else:
                 lw.gate_up = self._param((2 * self.inter, h), (2 * big, h), self.shard_gate_up, std, gen, genf)
                 lw.down = self._param((h, self.inter), (h, big), lambda t: self.shard_cols(t, self.inter), ostd,
@@ -237,7 +260,17 @@ class CausalLM:
                     put(lw.router, t)
                 elif rest.startswith("block_sparse_moe.experts.") and a.is_moe:
                     x, wname = int(parts[5]), parts[6]
-                    if wname == "w1":
+                    if self.ep:  # whole experts: keep ours, rebased
+                        if not self.expert0 <= x < self.expert0 + self.experts_local:
+                            continue
+                        x -= self.expert0
+                        if wname == "w1":
+                            put(lw.w13[x, :inter], t)
+                        elif wname == "w3":
+                            put(lw.w13[x, inter:], t)
+                        elif wname == "w2":
+                            put(lw.w2[x], t)
+                    elif wname == "w1":
                         put(lw.w13[x, :inter], rows(t, r * inter, inter))
                     elif wname == "w3":
                         put(lw.w13[x, inter:], rows(t, r * inter, inter))
@@ -291,7 +324,7 @@ class CausalLM:
             x = ops.fused_add_rms_norm(o, residual, lw.ln2, eps)
             if a.is_moe:
                 gating = F.linear(x, lw.router)
-                h = ops.moe_forward(x, lw.w13, lw.w2, gating, a.top_k)
+                h = ops.moe_forward(x, lw.w13, lw.w2, gating, a.top_k, expert0=self.expert0 if self.ep else None)
             else:
                 h = ops.linear(ops.linear_silu_mul(x, lw.gate_up), lw.down)
             h = self.tp.all_reduce(h)

@@ -420,22 +420,51 @@ def moe_align(ids: torch.Tensor, num_experts: int):
     return offsets, sorted_idx, pos
 
 
+def expert_parallel_local(w: torch.Tensor, ids: torch.Tensor, expert0: int, n_local: int):
+    """Expert parallelism over replicated tokens: keep the (token, slot) assignments routed to the
+    local experts [expert0, expert0 + n_local) (ids rebased to 0..n_local-1) and send every other
+    one to a null group ``n_local`` with weight 0 — no rows are computed for it, and the TP
+    all-reduce after the MoE sums the experts' contributions across ranks. Plain tensor ops: no
+    host sync, hipGraph-capturable."""
+    local = (ids >= expert0) & (ids < expert0 + n_local)
+    ids_l = torch.where(local, ids - expert0, torch.full_like(ids, n_local))
+    return torch.where(local, w, torch.zeros_like(w)), ids_l.to(ids.dtype)
+
+
 def moe_forward(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, gating: torch.Tensor, k: int,
-                renorm: bool = True) -> torch.Tensor:
+                renorm: bool = True, expert0: Optional[int] = None) -> torch.Tensor:
     """Fused-routing MoE FFN on the HIP kernels: route → align → gather →
     grouped GEMM (gate/up) → SiLU·mul → grouped GEMM (down) → weighted combine.
-    No host synchronisation (hipGraph-capturable)."""
+    No host synchronisation (hipGraph-capturable). ``expert0``: expert parallelism — ``w13``/``w2``
+    hold experts [expert0, expert0 + E_local) of the ``gating.shape[1]`` routed experts, and the
+    output is this rank's partial sum (see :func:`expert_parallel_local`)."""
+    e = w13.shape[0]
+    w, ids = topk_softmax(gating, k, renorm)
+    if expert0 is not None:
+        w, ids = expert_parallel_local(w, ids, expert0, e)
+        return moe_apply(x, w13, w2, w, ids, e + 1)  # + the null group of remote assignments
+    return moe_apply(x, w13, w2, w, ids, e)
+
+
+def moe_apply(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, w: torch.Tensor, ids: torch.Tensor,
+              groups: int) -> torch.Tensor:
+    """out[t] = sum_j w[t, j] * expert_{ids[t, j]}(x[t]) for given routing (w [T, k] fp32, ids [T, k]
+    int32). ``groups`` may exceed the number of local experts ``w13.shape[0]``: assignments to those
+    extra groups are not computed (their weight must be 0)."""
+    e = w13.shape[0]
     if not x.is_cuda:
-        return ref.moe_forward(x, w13, w2, gating, k, renorm)
+        return ref.moe_experts(x, w13, w2, w, ids)
     kern = _kern()
     t, hdim = x.shape
-    e = w13.shape[0]
+    k = ids.shape[1]
     inter = w13.shape[1] // 2
-    w, ids = topk_softmax(gating, k, renorm)
-    offsets, sorted_idx, pos = moe_align(ids, e)
+    ids = ids.to(torch.int32).contiguous()
+    w = w.float().contiguous()
+    offsets, sorted_idx, pos = moe_align(ids, groups)
     xs = torch.empty(t * k, hdim, dtype=x.dtype, device=x.device)
     kern.moe_gather(xs, x, sorted_idx, k)
-    ys = torch.empty(t * k, hdim, dtype=x.dtype, device=x.device)
+    # rows of the extra groups are never computed: zero them so that weight 0 x row stays 0
+    ys = (torch.zeros if groups > e else torch.empty)(t * k, hdim, dtype=x.dtype, device=x.device)
     if t <= DECODE_GEMM_MAX_M and _moe_decode_ok(hdim, inter):
         # decode: every expert's weights streamed once by the weight-streaming kernel, its
         # (<= 32) routed tokens riding along; SiLU*mul fused; idle experts read nothing

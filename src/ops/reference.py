@@ -152,6 +152,11 @@ def topk_softmax(gating: torch.Tensor, k: int, renorm: bool = True):
 def moe_forward(x, w13, w2, gating, k: int, renorm: bool = True):
     """Reference MoE FFN: x [T,H], w13 [E, 2I, H], w2 [E, H, I]."""
     w, ids = topk_softmax(gating, k, renorm)
+    return moe_experts(x, w13, w2, w, ids)
+
+
+def moe_experts(x, w13, w2, w, ids):
+    """Experts' weighted sum for given routing (w [T,k], ids [T,k]); ids >= E are skipped."""
     out = torch.zeros(x.shape, dtype=torch.float32, device=x.device)
     inter = w2.shape[-1]
     for e in range(w13.shape[0]):
