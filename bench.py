@@ -58,6 +58,8 @@ def parse():
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--temperature", type=float, default=0.0)
     p.add_argument("--tp", type=int, default=1, help="tensor-parallel degree per replica (70B: --tp 8)")
+    p.add_argument("--moe-parallel", choices=["tp", "ep"], default="tp", help="MoE layout under --tp")
+    p.add_argument("--sequence-parallel", action="store_true", help="Megatron-SP prefill under --tp")
     p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                    help="cpu: reference-op engine over gloo (tests the multi-rank plumbing, not a measurement)")
     p.add_argument("--verbose", action="store_true")
@@ -116,7 +118,8 @@ def main():
 
         tp = init_tp(args.tp)
         obj = build_tp_engine(args.preset, tp, dev, cfg=cfg, max_model_len=args.max_model_len, seed=1234,
-                              capture=not args.no_graph)
+                              capture=not args.no_graph, moe_parallel=args.moe_parallel,
+                              sequence_parallel=args.sequence_parallel)
         if tp.rank != 0:  # follower: mirror the leader through warmup and the timed waves
             obj.follower_loop()
             sync()
@@ -217,7 +220,9 @@ def main():
                 "seq_len": args.prompt_len + args.gen_len,
                 "prompt_len": args.prompt_len,
                 "gen_len": args.gen_len,
-                "parallelism": f"dp{replicas}" + (f"-tp{args.tp}" if args.tp > 1 else ""),
+                "parallelism": f"dp{replicas}" + (f"-tp{args.tp}" if args.tp > 1 else "")
+                + ("-ep" if args.tp > 1 and args.moe_parallel == "ep" else "")
+                + ("-sp" if args.tp > 1 and args.sequence_parallel else ""),
                 "max_batch": args.batch,
                 "max_latency_ms": args.max_latency_ms,
                 "weights": "random-init",

@@ -63,7 +63,7 @@ class CausalLM:
 
     def __init__(self, arch: ArchConfig, device, dtype=torch.bfloat16, tp: Optional[TPContext] = None,
                  seed: int = 0, init_std: float = 0.02, max_position: Optional[int] = None,
-                 full_init: bool = False, moe_parallel: str = "tp"):
+                 full_init: bool = False, moe_parallel: str = "tp", sequence_parallel: bool = False):
         """``full_init=True`` draws every weight at full (unsharded) size from a
         rank-independent generator and slices this rank's shard — identical to
         the TP=1 model, used by the TP equivalence tests. The default draws
@@ -74,7 +74,12 @@ class CausalLM:
         ``[rank * E/tp, (rank + 1) * E/tp)`` — bigger per-expert GEMMs, no FFN-dim divisibility
         constraint. Attention stays tensor-parallel, so every rank holds every token: the routed
         assignments to remote experts are masked locally and the MoE's TP all-reduce is the combine
-        (no all-to-all, see ops.expert_parallel_local)."""
+        (no all-to-all, see ops.expert_parallel_local).
+
+        ``sequence_parallel`` (TP prefill): Megatron-SP — the residual stream and the norms are
+        sharded over the ranks by token; each layer's two all-reduces become a reduce-scatter into
+        the norm and an all-gather out of it (same bytes on the links, 1/W of the norm work and of
+        the residual's memory). Decode steps (<= 32 rows) keep the all-reduce path."""
         self.arch = arch
         self.device = torch.device(device)
         self.dtype = dtype
@@ -98,6 +103,7 @@ class CausalLM:
         self.scale = 1.0 / math.sqrt(a.head_dim)
         self.max_position = max_position or a.max_position
         self.full_init = full_init
+        self.sequence_parallel = bool(sequence_parallel and self.tp.enabled)
         self.layers: List[LayerWeights] = []
         self._init_random(seed, init_std)
         self.cos_sin = rope_cos_sin(self.max_position, a.head_dim, a.rope_theta, self.device, a.rope_scaling)
@@ -294,41 +300,72 @@ class CausalLM:
                 kv_pool: torch.Tensor) -> torch.Tensor:
         """Returns the final-norm hidden states [T, H]. ``kv_pool`` is
         [layers, 2, num_blocks, hkv, block_size, head_dim]."""
-        a = self.arch
-        eps = a.rms_eps
-        d = self.head_dim
-        hq, hkv = self.hq, self.hkv
+        eps = self.arch.rms_eps
         residual = F.embedding(input_ids, self.embed)
         if self._slab_path(input_ids):
             if meta.scratch is not None and not meta.is_prefill and self._fused_decode_ok(kv_pool):
                 return self._forward_decode_fused(residual, positions, meta, kv_pool)
             if not self.tp.enabled:
                 return self._forward_decode_slab(residual, positions, meta, kv_pool)
+        if self.sequence_parallel and meta.is_prefill:
+            return self._forward_sp(residual, positions, meta, kv_pool)
         x = ops.rms_norm(residual, self.layers[0].ln1, eps)
         h = None
         for li, lw in enumerate(self.layers):
             if li > 0:
                 x = ops.fused_add_rms_norm(h, residual, lw.ln1, eps)
-            qkv = ops.linear(x, lw.qkv)
-            k_cache, v_cache = kv_pool[li, 0], kv_pool[li, 1]
-            ops.rope_and_cache(qkv, positions, self.cos_sin, meta.slot_mapping, k_cache, v_cache, hq, hkv, d)
-            q = qkv[:, : hq * d]
-            if meta.is_prefill:
-                attn = ops.attn_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_q, meta.ctx_lens,
-                                        meta.max_q_len, hq, hkv, self.scale)
-            else:
-                attn = ops.attn_decode(q, k_cache, v_cache, meta.block_tables, meta.ctx_lens, meta.max_ctx, hq,
-                                       hkv, self.scale, part_o=meta.part_o, part_ml=meta.part_ml,
-                                       counters=meta.attn_cnt)
+            attn = self._attention(li, lw, x, positions, meta, kv_pool)
             o = self.tp.all_reduce(ops.linear(attn, lw.o))
             x = ops.fused_add_rms_norm(o, residual, lw.ln2, eps)
-            if a.is_moe:
-                gating = F.linear(x, lw.router)
-                h = ops.moe_forward(x, lw.w13, lw.w2, gating, a.top_k, expert0=self.expert0 if self.ep else None)
-            else:
-                h = ops.linear(ops.linear_silu_mul(x, lw.gate_up), lw.down)
-            h = self.tp.all_reduce(h)
+            h = self.tp.all_reduce(self._mlp(lw, x))
         return ops.fused_add_rms_norm(h, residual, self.norm, eps)
+
+    def _attention(self, li: int, lw: LayerWeights, x: torch.Tensor, positions: torch.Tensor, meta: AttnMetadata,
+                   kv_pool: torch.Tensor) -> torch.Tensor:
+        """qkv projection, RoPE + paged KV write, paged attention (prefill or decode) -> [T, hq*d]."""
+        d, hq, hkv = self.head_dim, self.hq, self.hkv
+        qkv = ops.linear(x, lw.qkv)
+        k_cache, v_cache = kv_pool[li, 0], kv_pool[li, 1]
+        ops.rope_and_cache(qkv, positions, self.cos_sin, meta.slot_mapping, k_cache, v_cache, hq, hkv, d)
+        q = qkv[:, : hq * d]
+        if meta.is_prefill:
+            return ops.attn_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_q, meta.ctx_lens,
+                                    meta.max_q_len, hq, hkv, self.scale)
+        return ops.attn_decode(q, k_cache, v_cache, meta.block_tables, meta.ctx_lens, meta.max_ctx, hq, hkv,
+                               self.scale, part_o=meta.part_o, part_ml=meta.part_ml, counters=meta.attn_cnt)
+
+    def _mlp(self, lw: LayerWeights, x: torch.Tensor) -> torch.Tensor:
+        """This rank's partial FFN / MoE output (summed over the TP group by the caller)."""
+        a = self.arch
+        if a.is_moe:
+            gating = F.linear(x, lw.router)
+            return ops.moe_forward(x, lw.w13, lw.w2, gating, a.top_k, expert0=self.expert0 if self.ep else None)
+        return ops.linear(ops.linear_silu_mul(x, lw.gate_up), lw.down)
+
+    def _forward_sp(self, residual_full: torch.Tensor, positions: torch.Tensor, meta: AttnMetadata,
+                    kv_pool: torch.Tensor) -> torch.Tensor:
+        """Sequence-parallel prefill: this rank keeps tokens [r*n, (r+1)*n) of the residual stream
+        (rows padded to a multiple of the TP size); projections and attention see all tokens."""
+        tp, eps = self.tp, self.arch.rms_eps
+        T = residual_full.shape[0]
+        W = tp.world_size
+        n = -(-T // W)
+        pad = n * W - T
+
+        def padded(t: torch.Tensor) -> torch.Tensor:
+            return F.pad(t, (0, 0, 0, pad)) if pad else t
+
+        residual = padded(residual_full)[tp.rank * n:(tp.rank + 1) * n].contiguous()
+        x_s = ops.rms_norm(residual, self.layers[0].ln1, eps)
+        h_s = None
+        for li, lw in enumerate(self.layers):
+            if li > 0:
+                x_s = ops.fused_add_rms_norm(h_s, residual, lw.ln1, eps)
+            attn = self._attention(li, lw, tp.all_gather_rows(x_s)[:T], positions, meta, kv_pool)
+            o_s = tp.reduce_scatter_rows(padded(ops.linear(attn, lw.o)))
+            x_s = ops.fused_add_rms_norm(o_s, residual, lw.ln2, eps)
+            h_s = tp.reduce_scatter_rows(padded(self._mlp(lw, tp.all_gather_rows(x_s)[:T])))
+        return tp.all_gather_rows(ops.fused_add_rms_norm(h_s, residual, self.norm, eps))[:T]
 
     # ------------------------------------------------- decode fast path (M <= 32)
     def _slab_path(self, input_ids: torch.Tensor) -> bool:

@@ -87,6 +87,33 @@ class TPContext:
                 dist.all_reduce(t, group=self.group)
         return t
 
+    # --- sequence parallelism (Megatron-SP): the all-reduce split into its two halves around the
+    # token-sharded norms. Rows = tokens, padded by the caller to a multiple of world_size.
+    def reduce_scatter_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """[T, H] partial sums -> this rank's [T / W, H] rows of the total."""
+        if not self.enabled:
+            return t
+        n = t.shape[0] // self.world_size
+        if dist.get_backend(self.group) == "gloo":  # gloo has no reduce-scatter: all-reduce + slice
+            full = self.all_reduce(t.clone())
+            return full[self.rank * n:(self.rank + 1) * n].contiguous()
+        out = torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.reduce_scatter_tensor(out, t.contiguous(), group=self.group)
+        return out
+
+    def all_gather_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """This rank's [T / W, H] rows -> [T, H] (rank-major)."""
+        if not self.enabled:
+            return t
+        if dist.get_backend(self.group) == "gloo":
+            c = t.float().cpu().contiguous() if t.is_cuda else t.contiguous()
+            parts = [torch.empty_like(c) for _ in range(self.world_size)]
+            dist.all_gather(parts, c, group=self.group)
+            return torch.cat(parts, 0).to(t.device, t.dtype)
+        out = torch.empty((t.shape[0] * self.world_size,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out
+
     def all_gather_last(self, t: torch.Tensor) -> torch.Tensor:
         """Concatenate the per-rank shards along the last dim."""
         if not self.enabled:

@@ -110,7 +110,7 @@ def agree_num_blocks(n: int, tp) -> int:
 
 def build_tp_engine(preset: str, tp, device, cfg: Optional[EngineConfig] = None, max_model_len: int = 4096,
                     seed: int = 0, capture: bool = True, dtype=torch.bfloat16, full_init: bool = False,
-                    moe_parallel: str = "tp", **arch_overrides):
+                    moe_parallel: str = "tp", sequence_parallel: bool = False, **arch_overrides):
     """Construct the per-rank pieces. Rank 0 gets an :class:`LLMEngine`
     (scheduler + RPC-facing API) whose runner broadcasts steps; other ranks get
     a :class:`TPModelRunner` on which to call :meth:`follower_loop`."""
@@ -124,7 +124,7 @@ def build_tp_engine(preset: str, tp, device, cfg: Optional[EngineConfig] = None,
     if torch.device(device).type == "cuda":
         tp.enable_custom_allreduce()  # decode-sized all-reduces: one xGMI hop instead of RCCL's ring
     model = CausalLM(arch, device, dtype=dtype, tp=tp, seed=seed, max_position=max(max_model_len, 16),
-                     full_init=full_init, moe_parallel=moe_parallel)
+                     full_init=full_init, moe_parallel=moe_parallel, sequence_parallel=sequence_parallel)
     if ckpt:
         load_checkpoint(model, preset)  # every rank streams the shards and keeps its own slice
     nblocks = agree_num_blocks(plan_kv_blocks(arch, model, cfg, model.device), tp)

@@ -57,7 +57,8 @@ def main(argv=None) -> None:
                        arch=args.arch, preset=args.preset, max_model_len=args.max_model_len,
                        max_latency_ms=args.max_latency_ms, use_cuda_graph=not args.no_graph)
     obj = build_tp_engine(args.preset or "llama3-70b", tp, device, cfg=engine_config_from(mcfg),
-                          max_model_len=args.max_model_len, capture=not args.no_graph)
+                          max_model_len=args.max_model_len, capture=not args.no_graph,
+                          moe_parallel=args.moe_parallel, sequence_parallel=args.sequence_parallel)
     if tp.rank == 0:
         try:
             asyncio.run(serve(args, obj))

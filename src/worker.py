@@ -361,6 +361,10 @@ def build_arg_parser():
     p.add_argument("--max-latency-ms", type=float, default=10.0)
     p.add_argument("--max-model-len", type=int, default=4096)
     p.add_argument("--tp-size", type=int, default=1)
+    p.add_argument("--moe-parallel", choices=["tp", "ep"], default="tp",
+                   help="MoE under TP: split each expert (tp) or give ranks whole experts (ep)")
+    p.add_argument("--sequence-parallel", action="store_true",
+                   help="TP prefill: token-sharded norms, reduce-scatter/all-gather instead of all-reduce")
     p.add_argument("--role", default="both", choices=["both", "prefill", "decode"])
     p.add_argument("--mock-latency-ms", type=float, default=None,
                    help="FakeModel latency; default = reference 50-150 ms")

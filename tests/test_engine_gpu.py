@@ -166,7 +166,7 @@ def test_kv_export_import_exact(engine):
     dec.abort("kvx")
 
 
-def _tp_gpu_worker(rank, world, port, q, preset, moe_parallel="tp"):
+def _tp_gpu_worker(rank, world, port, q, preset, moe_parallel="tp", sp=False):
     import os
 
     import torch.distributed as dist
@@ -181,7 +181,7 @@ def _tp_gpu_worker(rank, world, port, q, preset, moe_parallel="tp"):
         cfg = EngineConfig(max_num_seqs=4, max_num_batched_tokens=256, num_kv_blocks=128, max_latency_ms=0.0,
                            use_cuda_graph=False)
         obj = build_tp_engine(preset, tp, "cuda:0", cfg=cfg, max_model_len=512, capture=False,
-                              full_init=True, seed=3, moe_parallel=moe_parallel)
+                              full_init=True, seed=3, moe_parallel=moe_parallel, sequence_parallel=sp)
         if rank == 0:
             obj.eos_token_id = None
             q.put((obj.generate(TP_PROMPTS, SamplingParams(max_tokens=8)), tp.car is not None))
@@ -195,9 +195,9 @@ def _tp_gpu_worker(rank, world, port, q, preset, moe_parallel="tp"):
 TP_PROMPTS = [[5, 9, 33, 12, 7] * 9, [100, 200, 300], list(range(3, 140))]
 
 
-@pytest.mark.parametrize("preset,moe_parallel", [("llama-mini", "tp"), ("mixtral-tiny", "tp"),
-                                                 ("mixtral-tiny", "ep")])
-def test_tensor_parallel_tp2_on_one_gpu(preset, moe_parallel):
+@pytest.mark.parametrize("preset,moe_parallel,sp", [("llama-mini", "tp", False), ("mixtral-tiny", "tp", False),
+                                                    ("mixtral-tiny", "ep", False), ("llama-mini", "tp", True)])
+def test_tensor_parallel_tp2_on_one_gpu(preset, moe_parallel, sp):
     """The TP=2 code path on real kernels: two ranks share the GPU (gloo, collectives staged
     through the host), Megatron-split weights drawn from the same stream as the TP=1 model;
     greedy tokens must agree with the TP=1 fp32 reference up to near-ties."""
@@ -214,7 +214,7 @@ def test_tensor_parallel_tp2_on_one_gpu(preset, moe_parallel):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_tp_gpu_worker, args=(r, 2, port, q, preset, moe_parallel)) for r in range(2)]
+    procs = [ctx.Process(target=_tp_gpu_worker, args=(r, 2, port, q, preset, moe_parallel, sp)) for r in range(2)]
     for p in procs:
         p.start()
     got, used_car = q.get(timeout=600)

@@ -51,6 +51,9 @@ def _worker(rank, world, port, q):
         padded = ep_moe_forward(x, router, w13_l, w2_l, K, capacity=tmax * K)
         tight = ep_moe_forward(x, router, w13_l, w2_l, K, capacity=2)
         q.put((rank, exact, padded, tight))
+    except Exception as e:  # surface the failure in the parent instead of a queue timeout
+        q.put((rank, repr(e), None, None))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -71,6 +74,7 @@ def test_ep_all_to_all_matches_single_process(world):
         p.join(60)
         assert p.exitcode == 0
     for r in range(world):
+        assert not isinstance(got[r][0], str), got[r][0]
         x = _tokens(r)
         want = ref.moe_forward(x, w13, w2, x @ router.t(), K)
         exact, padded, tight = got[r]

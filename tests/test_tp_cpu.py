@@ -32,13 +32,14 @@ def _cfg():
     return EngineConfig(max_num_seqs=4, max_num_batched_tokens=48, num_kv_blocks=64, max_latency_ms=0.0)
 
 
-def _worker(rank, world, port, preset, q, moe_parallel="tp"):
+def _worker(rank, world, port, preset, q, moe_parallel="tp", sp=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     tp = TPContext(rank=rank, world_size=world)
     try:
         obj = build_tp_engine(preset, tp, "cpu", cfg=_cfg(), max_model_len=256, capture=False,
-                              dtype=torch.float32, full_init=True, seed=3, moe_parallel=moe_parallel)
+                              dtype=torch.float32, full_init=True, seed=3, moe_parallel=moe_parallel,
+                              sequence_parallel=sp)
         if rank == 0:
             obj.eos_token_id = None
             obj.runner.HEARTBEAT_S = 0.0  # idle heartbeats must be absorbed by the followers
@@ -53,10 +54,13 @@ def _worker(rank, world, port, preset, q, moe_parallel="tp"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("preset,moe_parallel", [("llama-tiny", "tp"), ("mixtral-tiny", "tp"),
-                                                 ("mixtral-tiny", "ep")])
-def test_tp2_matches_tp1(preset, moe_parallel):
-    """TP=2; for Mixtral also expert parallelism (each rank owns half the experts, whole)."""
+@pytest.mark.parametrize("preset,moe_parallel,sp", [("llama-tiny", "tp", False), ("mixtral-tiny", "tp", False),
+                                                    ("mixtral-tiny", "ep", False), ("llama-tiny", "tp", True),
+                                                    ("mixtral-tiny", "ep", True)])
+def test_tp2_matches_tp1(preset, moe_parallel, sp):
+    """TP=2; for Mixtral also expert parallelism (each rank owns half the experts, whole); with
+    sequence parallelism the prefill's residual stream and norms are token-sharded (odd token
+    counts exercise the padding)."""
     # TP=1 with full_init draws from the same rank-independent stream
     from src.models.llama import CausalLM
     from src.models.presets import get_preset
@@ -67,7 +71,7 @@ def test_tp2_matches_tp1(preset, moe_parallel):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, preset, q, moe_parallel)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, preset, q, moe_parallel, sp)) for r in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)
