@@ -422,7 +422,7 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
 // are scratch; counters [H / 64] and flags [8] int32 zeroed once (re-armed by the kernel); err [1] int32
 // is set to 1 if a hand-off wait gave up (never expected).
 void mlp_decode(Tensor act, Tensor slab, Tensor x, Tensor w_gate_up, Tensor w_down, Tensor ssp_in, Tensor resid,
-                Tensor ssp_out, Tensor counters, Tensor flags, Tensor err, double eps, bool nt) {
+                Tensor ssp_out, Tensor counters, Tensor flags, Tensor err, double eps, bool nt, int64_t xmode) {
   DIE_CHECK_CUDA(x);
   DIE_CHECK_BF16(x);
   DIE_CHECK_BF16(w_gate_up);
@@ -466,7 +466,7 @@ void mlp_decode(Tensor act, Tensor slab, Tensor x, Tensor w_gate_up, Tensor w_do
   fz2.counters = counters.data_ptr<int>();
   DIE_HIP(die::launch_mlp_decode(bf(act), bf(x), x.stride(0), bf(w_gate_up), bf(w_down), slab.data_ptr<float>(),
                                  (int)M, (int)H, (int)I, fz1, fz2, flags.data_ptr<int>(), err.data_ptr<int>(), nt,
-                                 cur_stream()));
+                                 (int)xmode, cur_stream()));
 }
 
 // Grouped (MoE) decode GEMM: x [R, K] token-sorted activations (expert e owns rows

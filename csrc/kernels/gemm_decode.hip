@@ -62,7 +62,9 @@ using namespace gd;
 // inside the same launch — the first S-1 weight chunks are issued, then the workgroup waits until
 // *xflag reaches xtarget, then X is read with device-coherent (sc1) loads. WT: the output is stored
 // write-through (sc1) so that workgroups on other XCDs can read it in the same launch.
-template <int WR, int EPI, int S, bool NT, int KC, bool XWAIT = false, bool WT = false>
+// XWAIT = 1: X read with sc1 loads; XWAIT = 2: one agent-scope acquire after the wait, then plain
+// (L2-cacheable) X loads (cdna_hip_programming.md Guideline 16 recipe R1).
+template <int WR, int EPI, int S, bool NT, int KC, int XWAIT = 0, bool WT = false>
 __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const bf16_t* __restrict__ X, int64_t ldx,
                                         const bf16_t* __restrict__ W, int M, int N_out, int K,
                                         const GemmDecodeFuse& fz, const int bx, const int by, const int ny,
@@ -131,7 +133,7 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
           glds16<0>(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);
       } else {
         if (!(part & 2)) continue;
-        if (XWAIT)
+        if (XWAIT == 1)
           glds16<16>(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);  // sc1: other XCDs wrote X
         else
           glds16<0>(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);
@@ -155,7 +157,7 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
 #pragma unroll
     for (int b = 0; b < NTILE; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (XWAIT) {
+  if constexpr (XWAIT != 0) {
     // weights do not depend on X: put S-1 chunks of them in flight, then wait for the producers
     // (nch >= S is checked by the launcher)
 #pragma unroll
@@ -168,6 +170,10 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
           *err = 1;
           break;
         }
+      }
+      if constexpr (XWAIT == 2) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // drop this CU's stale L1 lines of X
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
     asm volatile("" ::: "memory");
@@ -186,7 +192,7 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
   for (int c = 0; c < nch; ++c) {
     if (c + S - 1 < nch) issue(c + S - 1);
     const int after = min(S - 1, nch - 1 - c);  // chunks issued after c
-    if (XWAIT && c == 0) {
+    if (XWAIT != 0 && c == 0) {
       // issue order was W(0..S-2), X(0..S-2), chunk S-1: chunk 0 is complete once only
       // X(1..S-2) and chunk S-1 remain
       wait_vm<(S - 2) * PX + PER_WAVE>();
@@ -367,7 +373,7 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
 // resident and the waits cannot deadlock; every spin is bounded (err = 1 on give-up).
 constexpr int MLP_NO1 = 56, MLP_WR2 = 64, MLP_SK2 = 4;
 
-template <bool NT>
+template <bool NT, int XMODE>
 __global__ void __launch_bounds__(NTH) mlp_decode_kernel(bf16_t* __restrict__ act, const bf16_t* __restrict__ X,
                                                          int64_t ldx, const bf16_t* __restrict__ Wgu,
                                                          const bf16_t* __restrict__ Wd, float* __restrict__ slab,
@@ -385,7 +391,7 @@ __global__ void __launch_bounds__(NTH) mlp_decode_kernel(bf16_t* __restrict__ ac
   }
   for (int t = blockIdx.x; t < tiles2; t += gridDim.x) {
     const int s = t % MLP_SK2, n = t / MLP_SK2;
-    gd_body<MLP_WR2, 3, 3, NT, 256, true, false>(smem, slab, H, act, I, Wd, M, H, I, fz2, n, s, MLP_SK2, flags + s,
+    gd_body<MLP_WR2, 3, 3, NT, 256, XMODE, false>(smem, slab, H, act, I, Wd, M, H, I, fz2, n, s, MLP_SK2, flags + s,
                                                   per_slice, err);
     __syncthreads();
     if (tid == 0 &&
@@ -462,8 +468,9 @@ hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx
 // counters [H / 64] of the down projection (as mode 3).
 hipError_t launch_mlp_decode(bf16_t* act, const bf16_t* X, int64_t ldx, const bf16_t* Wgu, const bf16_t* Wd,
                              float* slab, int M, int H, int I, const GemmDecodeFuse& fz1, const GemmDecodeFuse& fz2,
-                             int* flags, int* err, bool nt, hipStream_t s) {
+                             int* flags, int* err, bool nt, int xmode, hipStream_t s) {
   if (M <= 0) return hipSuccess;
+  if (xmode != 1 && xmode != 2) return hipErrorInvalidValue;
   if (M > MR || H % 128 || H % MLP_WR2 || I % (MLP_NO1 * MLP_SK2) || (I / MLP_SK2) % 256 || (I / MLP_SK2) / 256 < 3)
     return hipErrorInvalidValue;
   if (fz1.ssp_in == nullptr || fz1.ssp_tiles < 1 || fz1.ssp_tiles > 128 || fz2.resid == nullptr ||
@@ -474,12 +481,15 @@ hipError_t launch_mlp_decode(bf16_t* act, const bf16_t* X, int64_t ldx, const bf
   constexpr size_t lds1 = (size_t)4 * (112 + MR) * 128 * 2, lds2 = (size_t)3 * (MLP_WR2 + MR) * 256 * 2;
   constexpr size_t lds = lds1 > lds2 ? lds1 : lds2;
   static_assert(lds > 80 * 1024, "one workgroup per CU (residency of the persistent grid)");
-  if (nt)
-    hipLaunchKernelGGL(mlp_decode_kernel<true>, dim3(grid), dim3(NTH), lds, s, act, X, ldx, Wgu, Wd, slab, M, H, I,
-                       fz1, fz2, flags, err);
-  else
-    hipLaunchKernelGGL(mlp_decode_kernel<false>, dim3(grid), dim3(NTH), lds, s, act, X, ldx, Wgu, Wd, slab, M, H, I,
-                       fz1, fz2, flags, err);
+#define DIE_MLP_LAUNCH(NTV, XM)                                                                               \
+  hipLaunchKernelGGL((mlp_decode_kernel<NTV, XM>), dim3(grid), dim3(NTH), lds, s, act, X, ldx, Wgu, Wd, slab, M, H, \
+                     I, fz1, fz2, flags, err)
+  if (nt) {
+    if (xmode == 2) DIE_MLP_LAUNCH(true, 2); else DIE_MLP_LAUNCH(true, 1);
+  } else {
+    if (xmode == 2) DIE_MLP_LAUNCH(false, 2); else DIE_MLP_LAUNCH(false, 1);
+  }
+#undef DIE_MLP_LAUNCH
   return hipGetLastError();
 }
 

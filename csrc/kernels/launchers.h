@@ -84,7 +84,7 @@ hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx
 // persistent decode MLP: gate/up (mode 4) then down (mode 3) in one launch (gemm_decode.hip)
 hipError_t launch_mlp_decode(bf16_t* act, const bf16_t* X, int64_t ldx, const bf16_t* Wgu, const bf16_t* Wd,
                              float* slab, int M, int H, int I, const GemmDecodeFuse& fz1, const GemmDecodeFuse& fz2,
-                             int* flags, int* err, bool nt, hipStream_t s);
+                             int* flags, int* err, bool nt, int xmode, hipStream_t s);
 // consumers of fp32 split-K slabs [sk][rows][width]
 hipError_t launch_fused_add_rms_norm_slab(bf16_t* out, const float* slab, int sk, bf16_t* residual, const bf16_t* w,
                                           float eps, int rows, int hidden, int64_t out_stride, hipStream_t s);

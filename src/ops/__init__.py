@@ -196,7 +196,10 @@ DECODE_GEMM_NT = True
 # bit-identical to the two launches and measured equal in speed on MI355X (bench/micro_mlp_decode.py:
 # 78.3 vs 78.1 us per Llama-3-8B layer at batch 32, profiles/micro_mlp_decode_r1.jsonl), so the simpler
 # two-launch form stays the default
-MLP_DECODE_FUSED = os.environ.get("DIE_MLP_FUSED", "0") == "1"  # non-temporal weight loads (read-once stream)
+MLP_DECODE_FUSED = os.environ.get("DIE_MLP_FUSED", "0") == "1"
+# hand-off of the gate/up activations to the down tiles: 1 = sc1 loads of X on every chunk,
+# 2 = one agent-scope acquire after the flag, then plain L2-cacheable loads
+MLP_XMODE = int(os.environ.get("DIE_MLP_XMODE", "2"))  # non-temporal weight loads (read-once stream)
 
 
 def gemm_decode(x: torch.Tensor, w: torch.Tensor, mode: int = 0, wr: int = 64, sk: int = 1,
@@ -274,7 +277,7 @@ def mlp_decode(x: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor, s
     if slab is None:
         slab = torch.empty(4, m, h, dtype=torch.float32, device=x.device)
     _kern().mlp_decode(act, slab, x, w_gate_up, w_down, ssp_in, resid, ssp_out, counters, flags, err, float(eps),
-                       DECODE_GEMM_NT)
+                       DECODE_GEMM_NT, MLP_XMODE)
 
 
 def residual_add_sumsq(resid: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
