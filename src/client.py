@@ -29,6 +29,24 @@ class InferenceClient:
         msg.update(extra)
         return await self._rpc.call(self.address, msg, self.timeout)
 
+    async def infer_stream(self, model: str, inputs: Any, version: Optional[str] = None,
+                           request_key: Optional[str] = None, **extra):
+        """Streamed generation: yields ``{"delta_token_ids": [...], "done": False}`` frames as tokens are
+        produced, then the final response (``"done": True``, same shape as :meth:`infer`'s reply)."""
+        inputs = dict(inputs, stream=True)
+        msg: Dict[str, Any] = {"op": "infer", "model": model, "inputs": inputs, "cache": False}
+        if version:
+            msg["version"] = version
+        if request_key:
+            msg["request_key"] = request_key
+        msg.update(extra)
+        async for frame in self._rpc.stream(self.address, msg, self.timeout):
+            yield frame
+
+    async def abort(self, model: str, request_id: str) -> Dict[str, Any]:
+        """Abort a running request on a worker (frees its batch slot and KV blocks)."""
+        return await self.call({"op": "abort", "model": model, "request_id": request_id})
+
     async def submit(self, model: str, inputs: Any, **kw) -> str:
         rep = await self._rpc.call(self.address, dict({"op": "submit", "model": model, "inputs": inputs}, **kw),
                                    self.timeout)

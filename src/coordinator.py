@@ -200,22 +200,32 @@ class Coordinator:
                     break
                 if mode == "eof":
                     break
-                resp = await self.handle_message(msg)
+                async def emit(frame, codec=codec):  # token deltas of a streamed request
+                    writer.write(pack_frame(frame, codec))
+                    await writer.drain()
+
+                resp = await self.handle_message(msg, emit=emit if mode != "legacy" else None)
                 if mode == "legacy":
                     writer.write(json.dumps(resp).encode())
                     await writer.drain()
                     break
-                writer.write(pack_frame(resp, codec))
-                await writer.drain()
+                try:
+                    writer.write(pack_frame(resp, codec))
+                    await writer.drain()
+                except ConnectionError:  # the client went away
+                    break
         finally:
             with contextlib.suppress(Exception):
                 writer.close()
 
-    async def handle_message(self, msg: Any) -> Dict[str, Any]:
+    async def handle_message(self, msg: Any, emit=None) -> Dict[str, Any]:
         if not isinstance(msg, dict):
             return {"error": "Request must be a JSON object", "success": False}
         op = msg.get("op", "infer")
         if op == "infer":
+            inp = msg.get("inputs")
+            if emit is not None and isinstance(inp, dict) and inp.get("stream"):
+                return await self.handle_stream(msg, emit)
             return await self.handle_request(msg)
         if op == "submit":
             rid = msg.get("request_id") or new_request_id()
@@ -311,6 +321,49 @@ class Coordinator:
             self.stats["errors"] += 1
         resp.setdefault("request_id", rid)
         return resp
+
+    async def handle_stream(self, msg: Dict[str, Any], emit) -> Dict[str, Any]:
+        """Streamed request: routed like any other (hash shard → LB), bypassing the batcher and the
+        response cache; the worker's token-delta frames are relayed as they arrive. A failed worker
+        is retried on the next candidate only while no token has been relayed."""
+        self.stats["requests"] += 1
+        rid = msg.get("request_id") or new_request_id()
+        model, inputs = msg.get("model"), msg.get("inputs")
+        version = str(msg.get("version") or self.registry.latest_version(model) or DEFAULT_VERSION)
+        if not model or self.registry.get_model_version(model, version) is None:
+            self.stats["errors"] += 1
+            return {"error": f"Model '{model}' version '{version}' not registered", "success": False}
+        key = str(msg.get("request_key") or rid)
+        shard = self.router.route_request(model, version, key)
+        if shard is None:
+            self.stats["errors"] += 1
+            return {"error": f"no healthy shard for {model}:{version}", "success": False}
+        lb = self._lb(model, version)
+        wmsg = {"op": "infer", "model": model, "inputs": inputs, "request_id": rid}
+        last_err = "no worker available"
+        for i, (wid, addr) in enumerate(self._candidates(model, version, shard.shard_id, key)):
+            if i > self.max_retries:
+                break
+            relayed = False
+            try:
+                async with lb.track(wid):
+                    async for frame in self.rpc.stream(addr, wmsg, timeout=self.request_timeout_s):
+                        if isinstance(frame, dict) and frame.get("done") is False:
+                            relayed = True
+                            await emit(frame)
+                            continue
+                        self.router.mark_worker_success(wid)
+                        if isinstance(frame, dict):
+                            frame.setdefault("request_id", rid)
+                        return frame
+            except (RPCError, OSError, asyncio.TimeoutError) as e:
+                last_err = f"{wid}: {e}"
+                self.router.mark_worker_failure(wid)
+                if relayed:
+                    break
+                self.stats["retries"] += 1
+        self.stats["errors"] += 1
+        return {"error": last_err, "success": False, "request_id": rid, "done": True}
 
     # ------------------------------------------------------------ dispatch
     def _dispatch_mode(self, model: str) -> str:

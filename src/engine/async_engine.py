@@ -18,7 +18,7 @@ import logging
 import queue
 import threading
 import time
-from typing import Any, Dict, List, Optional
+from typing import Any, Callable, Dict, List, Optional
 
 from src.engine.llm_engine import LLMEngine
 from src.engine.sequence import Sequence
@@ -32,6 +32,7 @@ class AsyncLLMEngine:
         self.engine = engine
         self.name = name
         self._q: "queue.Queue" = queue.Queue()
+        self._aborts: "queue.Queue" = queue.Queue()
         self._wake = threading.Event()
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
@@ -56,14 +57,18 @@ class AsyncLLMEngine:
         return self._thread is not None and self._thread.is_alive()
 
     def submit(self, request_id: str, prompt_ids: List[int], sampling: SamplingParams,
-               loop: Optional[asyncio.AbstractEventLoop] = None, user_data: Any = None) -> asyncio.Future:
+               loop: Optional[asyncio.AbstractEventLoop] = None, user_data: Any = None,
+               on_token: Optional[Callable[[int], None]] = None) -> asyncio.Future:
         """Thread-safe; call from the event loop. The future resolves to the
-        finished :class:`Sequence` (or raises if the engine failed)."""
+        finished :class:`Sequence` (or raises if the engine failed). ``on_token(tok)`` (streaming)
+        runs on the event loop for every generated token, in order, before the future resolves."""
         loop = loop or asyncio.get_running_loop()
         fut = loop.create_future()
         if self.error is not None:
             fut.set_exception(RuntimeError(f"engine failed: {self.error!r}"))
             return fut
+        if on_token is not None:
+            user_data = dict(user_data or {}, on_token=on_token)
         self._q.put((request_id, prompt_ids, sampling, fut, loop, user_data))
         self._wake.set()
         if self.error is not None:  # the loop died between the check above and the put
@@ -77,6 +82,12 @@ class AsyncLLMEngine:
         self._wake.set()
         if self.error is not None:
             self._fail_pending()
+
+    def abort(self, request_id: str) -> None:
+        """Thread-safe: drop a queued or running request (its KV blocks are freed between steps and its
+        future resolves with ``finish_reason == "abort"`` and the tokens generated so far)."""
+        self._aborts.put(request_id)
+        self._wake.set()
 
     def call(self, fn, loop: Optional[asyncio.AbstractEventLoop] = None) -> asyncio.Future:
         """Run ``fn(engine)`` on the engine thread between steps; the future
@@ -103,6 +114,15 @@ class AsyncLLMEngine:
                 loop.call_soon_threadsafe(_fail, fut, err)
 
     def _drain(self) -> None:
+        self._drain_submissions()
+        while True:  # aborts after submissions: an abort may follow its own submit in the same drain
+            try:
+                rid = self._aborts.get_nowait()
+            except queue.Empty:
+                return
+            self.engine.abort(rid)
+
+    def _drain_submissions(self) -> None:
         while True:
             try:
                 rid, ids, sp, fut, loop, ud = self._q.get_nowait()
@@ -122,12 +142,17 @@ class AsyncLLMEngine:
                 else:
                     loop.call_soon_threadsafe(_resolve, fut, seq)
 
+            on_tok = None
+            if isinstance(ud, dict) and ud.get("on_token") is not None and loop is not None:
+                def on_tok(seq: Sequence, tok: int, cb=ud["on_token"], loop=loop):
+                    loop.call_soon_threadsafe(cb, tok)
             try:
                 if isinstance(ud, dict) and ud.get("import_packet") is not None:
                     self.engine.add_imported(ud["import_packet"], sp, on_finish=done)
                 else:
                     self.engine.add_request(rid, ids, sp, on_finish=done, user_data=ud,
-                                            export_kv=isinstance(ud, dict) and bool(ud.get("export_kv")))
+                                            export_kv=isinstance(ud, dict) and bool(ud.get("export_kv")),
+                                            on_token=on_tok)
             except Exception as e:
                 if loop is None:
                     fut(e)

@@ -80,6 +80,7 @@ class LLMBackend:
         self.request_count = 0
         self.error_count = 0
         self.total_latency = 0.0
+        self._live: Dict[str, str] = {}  # client request_id -> engine request id (abort)
 
     async def start(self) -> None:
         self.async_engine.start()
@@ -99,7 +100,12 @@ class LLMBackend:
         s = self.engine.scheduler
         return (len(s.running) + len(s.waiting)) / max(1, self.engine.cfg.max_num_seqs)
 
-    async def predict(self, inputs: Any) -> Dict[str, Any]:
+    async def predict(self, inputs: Any, request_id: Optional[str] = None,
+                      on_token=None) -> Dict[str, Any]:
+        """One generation. ``inputs["timeout_s"]`` bounds it (the request is aborted in the engine and the
+        tokens so far come back with ``finish_reason="timeout"``); a cancelled caller (client gone) aborts
+        it too, so an abandoned request never keeps its batch slot and KV blocks. ``request_id`` names it
+        for :meth:`abort_request`; ``on_token(tok)`` streams tokens (event-loop thread)."""
         if not self.async_engine.running:
             self.async_engine.start()
         self.request_count += 1
@@ -112,12 +118,67 @@ class LLMBackend:
         t0 = time.perf_counter()
         if self._decode_link is not None and gi.sampling.max_tokens > 1:
             return await self._prefill_then_ship(rid, gi, t0)
-        seq = await self.async_engine.submit(rid, gi.prompt_token_ids, gi.sampling)
+        timeout = inputs.get("timeout_s") if isinstance(inputs, dict) else None
+        if request_id:
+            self._live[request_id] = rid
+        fut = self.async_engine.submit(rid, gi.prompt_token_ids, gi.sampling, on_token=on_token)
+        timed_out = False
+        try:
+            if timeout:
+                try:
+                    seq = await asyncio.wait_for(asyncio.shield(fut), float(timeout))
+                except asyncio.TimeoutError:
+                    timed_out = True
+                    self.async_engine.abort(rid)
+                    seq = await fut
+            else:
+                seq = await fut
+        except asyncio.CancelledError:
+            self.async_engine.abort(rid)
+            raise
+        finally:
+            if request_id:
+                self._live.pop(request_id, None)
         lat = (time.perf_counter() - t0) * 1e3
         self.total_latency += lat / 1e3
+        reason = "timeout" if timed_out and seq.finish_reason == "abort" else (seq.finish_reason or "length")
         return build_llm_output(seq.output_ids, self.tokenizer, prompt_len=seq.prompt_len,
-                                finish_reason=seq.finish_reason or "length", ttft_ms=seq.ttft_ms(),
+                                finish_reason=reason, ttft_ms=seq.ttft_ms(),
                                 latency_ms=seq.latency_ms(), return_text=gi.return_text)
+
+    async def predict_stream(self, inputs: Any, emit, request_id: Optional[str] = None) -> Dict[str, Any]:
+        """Streaming generation: ``await emit({"delta_token_ids": [...], "done": False})`` as tokens are
+        produced (bursts of up to ``decode_window`` per host round trip), then return the final output.
+        If ``emit`` fails (client gone) the request is aborted."""
+        q: asyncio.Queue = asyncio.Queue()
+        task = asyncio.ensure_future(self.predict(inputs, request_id, on_token=q.put_nowait))
+        try:
+            while True:
+                get = asyncio.ensure_future(q.get())
+                done, _ = await asyncio.wait({get, task}, return_when=asyncio.FIRST_COMPLETED)
+                if get not in done:
+                    get.cancel()
+                    break
+                toks = [get.result()]
+                while not q.empty():
+                    toks.append(q.get_nowait())
+                await emit({"delta_token_ids": toks, "done": False})
+            toks = []
+            while not q.empty():  # tokens delivered before the completion callback ran
+                toks.append(q.get_nowait())
+            if toks:
+                await emit({"delta_token_ids": toks, "done": False})
+            return await task
+        except BaseException:
+            task.cancel()
+            raise
+
+    def abort_request(self, request_id: str) -> bool:
+        rid = self._live.get(request_id)
+        if rid is None:
+            return False
+        self.async_engine.abort(rid)
+        return True
 
     async def _prefill_then_ship(self, rid: str, gi, t0: float) -> Dict[str, Any]:
         from src.engine.disagg import sampling_to_dict

@@ -110,13 +110,14 @@ class LLMEngine:
     # ------------------------------------------------------------ requests
     def add_request(self, request_id: str, prompt_ids: List[int], sampling: SamplingParams,
                     on_finish: Optional[Callable[[Sequence], None]] = None, user_data=None,
-                    export_kv: bool = False) -> Sequence:
+                    export_kv: bool = False,
+                    on_token: Optional[Callable[[Sequence, int], None]] = None) -> Sequence:
         if request_id in self.seqs:
             raise ValueError(f"duplicate request id {request_id}")
         if len(prompt_ids) + sampling.max_tokens > self.max_model_len:
             raise ValueError(f"prompt + max_tokens exceeds max_model_len={self.max_model_len}")
         seq = Sequence(request_id, list(prompt_ids), dataclasses.replace(sampling), on_finish=on_finish,
-                       user_data=user_data)
+                       user_data=user_data, on_token=on_token)
         if export_kv:  # disaggregated prefill: stop after the first token and hand the prompt KV over
             seq.sampling.max_tokens = 1
             seq.export_kv = True  # type: ignore[attr-defined]
@@ -259,6 +260,8 @@ class LLMEngine:
     def _append(self, seq: Sequence, tok: int, finished: List[Sequence]) -> None:
         seq.output_ids.append(int(tok))
         self.stats["generated_tokens"] += 1
+        if seq.on_token is not None:
+            seq.on_token(seq, int(tok))
         sp = seq.sampling
         reason = None
         if not sp.ignore_eos and self.eos_token_id is not None and tok == self.eos_token_id:

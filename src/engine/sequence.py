@@ -39,6 +39,7 @@ class Sequence:
     finish_reason: Optional[str] = None
     num_preemptions: int = 0
     user_data: Any = None
+    on_token: Optional[Callable[["Sequence", int], None]] = None  # streaming: called per new token
     # Disaggregation: a sequence whose prompt KV arrives from a prefill worker
     imported_kv: bool = False
     swap_buf: Any = None             # host copy of the KV blocks while SWAPPED

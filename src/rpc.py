@@ -73,6 +73,24 @@ class RPCClient:
             conn.close()
         return reply
 
+    async def stream(self, address: str, msg: Any, timeout: Optional[float] = 600.0):
+        """Send one request whose reply is streamed: yields every frame; intermediate frames carry
+        ``"done": False``, the last one does not. Uses a dedicated connection (closed at the end), so a
+        consumer that stops early simply drops the connection and the server aborts the request."""
+        conn = await self._open(address, timeout or 30.0)
+        try:
+            conn.writer.write(pack_frame(msg, self.codec))
+            await conn.writer.drain()
+            while True:
+                frame, _ = await asyncio.wait_for(read_frame(conn.reader), timeout)
+                yield frame
+                if not (isinstance(frame, dict) and frame.get("done") is False):
+                    return
+        except (ConnectionError, asyncio.IncompleteReadError, OSError) as e:
+            raise RPCError(f"stream from {address} failed: {e}") from e
+        finally:
+            conn.close()
+
     async def probe(self, address: str, timeout: float = 2.0) -> Tuple[bool, float, Optional[Dict[str, Any]]]:
         """Health RPC on a dedicated short-lived connection. Returns
         ``(ok, latency_s, reply)``; the latency is the probe's own round trip

@@ -178,22 +178,32 @@ class Worker:
                 if mode == "eof":
                     break  # TCP-connect probe: not a request
                 t0 = time.perf_counter()
-                resp = await self.handle_message(msg)
+
+                async def emit(frame, codec=codec):  # intermediate frames of a streamed reply
+                    writer.write(pack_frame(frame, codec))
+                    await writer.drain()
+
+                resp = await self.handle_message(msg, emit=emit if mode != "legacy" else None)
                 if mode == "legacy":
                     import json
 
                     writer.write(json.dumps(resp).encode())
                     await writer.drain()
                     break
-                writer.write(pack_frame(resp, codec))
-                await writer.drain()
+                try:
+                    writer.write(pack_frame(resp, codec))
+                    await writer.drain()
+                except ConnectionError:  # the client went away (e.g. a dropped stream)
+                    break
                 logger.debug("request done in %.2f ms", (time.perf_counter() - t0) * 1e3)
         finally:
             self._conns.discard(writer)
             with contextlib.suppress(Exception):
                 writer.close()
 
-    async def handle_message(self, msg: Any) -> Dict[str, Any]:
+    async def handle_message(self, msg: Any, emit=None) -> Dict[str, Any]:
+        """One RPC. ``emit``: writes an intermediate frame on the caller's connection — streamed
+        generations (``inputs["stream"]``) send token deltas through it before the final reply."""
         if not isinstance(msg, dict):
             self._request_count += 1
             self._error_count += 1
@@ -223,11 +233,15 @@ class Worker:
             if m is not None and hasattr(m, "stop"):
                 await m.stop()
             return {"success": self.unload_model(name)}
+        if op == "abort":
+            m = self.models.get(msg.get("model"))
+            ok = m is not None and hasattr(m, "abort_request") and m.abort_request(str(msg.get("request_id")))
+            return {"success": bool(ok), "request_id": msg.get("request_id")}
         if op in ("infer", "infer_batch"):
             self._request_count += 1
             self._active += 1
             try:
-                resp = await (self._process_batch(msg) if op == "infer_batch" else self._process_request(msg))
+                resp = await (self._process_batch(msg) if op == "infer_batch" else self._process_request(msg, emit))
             finally:
                 self._active -= 1
             if not resp.get("success"):
@@ -244,7 +258,7 @@ class Worker:
         return {"error": f"unknown op {op!r}", "success": False}
 
     # ------------------------------------------------------------ inference
-    async def _process_request(self, request: Dict[str, Any]) -> Dict[str, Any]:
+    async def _process_request(self, request: Dict[str, Any], emit=None) -> Dict[str, Any]:
         if not isinstance(request, dict):
             return {"error": "Request must be a JSON object", "success": False}
         model_name = request.get("model")
@@ -261,10 +275,22 @@ class Worker:
         try:
             if rid:
                 self._tracer.mark(rid, "worker.recv")
-            outputs = await model.predict(inputs)
+            stream = emit is not None and isinstance(inputs, dict) and inputs.get("stream") and \
+                hasattr(model, "predict_stream")
+            if stream:
+                async def emit_rid(frame):
+                    await emit(dict(frame, request_id=rid) if rid else frame)
+
+                outputs = await model.predict_stream(inputs, emit_rid, request_id=rid)
+            elif hasattr(model, "abort_request"):
+                outputs = await model.predict(inputs, request_id=rid)
+            else:
+                outputs = await model.predict(inputs)
             if rid:
                 self._tracer.mark(rid, "worker.done")
             resp = {"model": model_name, "outputs": outputs, "worker_id": self.worker_id, "success": True}
+            if stream:
+                resp["done"] = True
             if rid:
                 resp["request_id"] = rid
             return resp

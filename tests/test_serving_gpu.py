@@ -44,6 +44,37 @@ def test_gpu_worker_through_coordinator():
     asyncio.run(main())
 
 
+def test_gpu_streaming_matches_plain():
+    """Token streaming on the GPU engine (hipGraph decode, multi-step windows deliver bursts): the
+    streamed deltas concatenate to the non-streamed greedy output, through worker and coordinator."""
+    async def main():
+        w = Worker("gs", host="127.0.0.1", install_signal_handlers=False)
+        assert w.load_model(gpu_cfg())
+        wport = await w.start()
+        coord = Coordinator(port=0, max_batch_size=8, max_latency_ms=2)
+        cport = await coord.start()
+        await coord.add_static_worker(f"127.0.0.1:{wport}")
+        req = {"prompt_token_ids": list(range(5, 90)), "max_tokens": 40, "ignore_eos": True}
+        cw, cc = InferenceClient(f"127.0.0.1:{wport}"), InferenceClient(f"127.0.0.1:{cport}")
+        plain = await asyncio.wait_for(cw.call({"op": "infer", "model": "mini", "inputs": req}), 300)
+        assert plain["success"], plain
+        for client in (cw, cc):
+            deltas, frames, final = [], 0, None
+            async for fr in client.infer_stream("mini", req):
+                if fr.get("done") is False:
+                    deltas += fr["delta_token_ids"]
+                    frames += 1
+                else:
+                    final = fr
+            assert final["success"] and deltas == plain["outputs"]["token_ids"] == final["outputs"]["token_ids"]
+            assert frames >= 2
+        cw.close()
+        cc.close()
+        await coord.stop()
+        await w.shutdown()
+    asyncio.run(main())
+
+
 def test_gpu_disaggregated_workers_over_rpc():
     async def main():
         dec = Worker("dec", host="127.0.0.1", install_signal_handlers=False)

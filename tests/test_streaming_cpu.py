@@ -1,0 +1,100 @@
+"""Token streaming, abort and per-request timeouts on the LLM serving path (CPU, tiny Llama):
+client → coordinator → worker → LLMBackend → AsyncLLMEngine.
+
+* streamed deltas concatenate to exactly the non-streamed greedy output, through the worker and
+  through the coordinator relay;
+* ``{"op": "abort"}`` stops a running generation (partial tokens, ``finish_reason == "abort"``);
+* ``inputs["timeout_s"]`` returns the tokens so far with ``finish_reason == "timeout"``;
+* a streaming client that goes away mid-generation gets its request aborted — the engine frees the
+  batch slot and KV blocks instead of generating for nobody."""
+
+import asyncio
+
+from src.client import InferenceClient
+from src.config import ModelConfig
+from src.coordinator import Coordinator
+from src.worker import Worker
+
+
+def llm_cfg(name="tiny"):
+    return ModelConfig(model_name=name, model_path="", arch="llama", preset="llama-tiny", max_batch_size=4,
+                       max_model_len=1024, max_num_batched_tokens=128, num_kv_blocks=256, use_cuda_graph=False,
+                       max_latency_ms=1.0, overrides={"device": "cpu"})
+
+
+REQ = {"prompt_token_ids": list(range(3, 30)), "max_tokens": 12, "ignore_eos": True}
+
+
+async def _collect(it):
+    deltas, final = [], None
+    async for frame in it:
+        if frame.get("done") is False:
+            deltas.extend(frame["delta_token_ids"])
+        else:
+            final = frame
+    return deltas, final
+
+
+def test_stream_matches_plain_worker_and_coordinator():
+    async def main():
+        w = Worker("s0", host="127.0.0.1", install_signal_handlers=False)
+        assert w.load_model(llm_cfg())
+        wport = await w.start()
+        coord = Coordinator(port=0, max_batch_size=4, max_latency_ms=2)
+        cport = await coord.start()
+        await coord.add_static_worker(f"127.0.0.1:{wport}")
+        cw, cc = InferenceClient(f"127.0.0.1:{wport}"), InferenceClient(f"127.0.0.1:{cport}")
+        plain = await cw.call({"op": "infer", "model": "tiny", "inputs": REQ})
+        assert plain["success"]
+        want = plain["outputs"]["token_ids"]
+        for client in (cw, cc):
+            deltas, final = await asyncio.wait_for(_collect(client.infer_stream("tiny", REQ)), 120)
+            assert final["success"] and final["done"] is True, final
+            assert deltas == want == final["outputs"]["token_ids"]
+        cw.close()
+        cc.close()
+        await coord.stop()
+        await w.shutdown()
+    asyncio.run(main())
+
+
+def test_abort_timeout_and_client_disconnect():
+    async def main():
+        w = Worker("s1", host="127.0.0.1", install_signal_handlers=False)
+        assert w.load_model(llm_cfg())
+        wport = await w.start()
+        c = InferenceClient(f"127.0.0.1:{wport}")
+        backend = w.models["tiny"]
+        long = {"prompt_token_ids": list(range(3, 20)), "max_tokens": 900, "ignore_eos": True}
+        # explicit abort of a running request
+        task = asyncio.ensure_future(c.call({"op": "infer", "model": "tiny", "inputs": long, "request_id": "r1"}))
+        for _ in range(200):
+            await asyncio.sleep(0.02)
+            if backend.engine.stats["generated_tokens"] > 3:
+                break
+        rep = await c.abort("tiny", "r1")
+        assert rep["success"], rep
+        res = await asyncio.wait_for(task, 60)
+        assert res["success"] and res["outputs"]["finish_reason"] == "abort"
+        assert 0 < res["outputs"]["num_output_tokens"] < 900
+        # per-request timeout
+        res = await asyncio.wait_for(c.call({"op": "infer", "model": "tiny",
+                                             "inputs": dict(long, timeout_s=0.2)}), 60)
+        assert res["outputs"]["finish_reason"] == "timeout" and res["outputs"]["num_output_tokens"] < 900
+        # streaming client that disappears after two frames
+        gen = c.infer_stream("tiny", long)
+        n = 0
+        async for frame in gen:
+            n += 1
+            if n == 2:
+                break
+        await gen.aclose()
+        for _ in range(250):
+            await asyncio.sleep(0.02)
+            if not backend.engine.scheduler.running and not backend.engine.scheduler.waiting:
+                break
+        assert not backend.engine.scheduler.running and not backend.engine.scheduler.waiting
+        assert backend.engine.get_stats()["kv"]["used"] == 0
+        c.close()
+        await w.shutdown()
+    asyncio.run(main())
