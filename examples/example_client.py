@@ -4,6 +4,7 @@
     python examples/example_client.py --address 127.0.0.1:9000 --model echo --inputs '{"x": 1}'
     python examples/example_client.py --model llama --prompt "Hello" --max-tokens 32
     python examples/example_client.py --model llama --prompt "Hi" -n 64 --concurrency 32   # mini load test
+    python examples/example_client.py --model llama --prompt "Hello" --max-tokens 64 --stream  # token stream
 """
 
 import argparse
@@ -31,12 +32,22 @@ async def main():
     ap.add_argument("-n", type=int, default=1)
     ap.add_argument("--concurrency", type=int, default=1)
     ap.add_argument("--poll", action="store_true", help="submit + poll instead of waiting")
+    ap.add_argument("--stream", action="store_true", help="print token deltas as they are generated")
     a = ap.parse_args()
     if a.prompt is not None:
         inputs = {"prompt": a.prompt, "max_tokens": a.max_tokens, "temperature": a.temperature}
     else:
         inputs = json.loads(a.inputs) if a.inputs else {"text": "hello"}
     c = InferenceClient(a.address)
+    if a.stream:
+        t0 = time.perf_counter()
+        async for frame in c.infer_stream(a.model, inputs, request_key=a.request_key):
+            if frame.get("done") is False:
+                print(f"[{1e3 * (time.perf_counter() - t0):8.1f} ms] +{frame['delta_token_ids']}", flush=True)
+            else:
+                print(json.dumps(frame, indent=2)[:4000])
+        c.close()
+        return
     sem = asyncio.Semaphore(a.concurrency)
     lat = []
 
