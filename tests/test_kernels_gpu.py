@@ -140,19 +140,28 @@ def test_attn_decode(dev, g, bs, merge):
     assert int(cnt.abs().sum()) == 0
 
 
-def test_attn_decode_batch32(dev):
+@pytest.mark.parametrize("v4", ["0", "1"])
+def test_attn_decode_batch32(dev, v4, monkeypatch):
     """The serving shape: 32 sequences x 8 kv heads (one task per CU, no partials), plus a
     single long sequence (every CU on one pair, all-partials merge)."""
+    monkeypatch.setenv("DIE_ATTN_V4", v4)  # v4: opt-in variant of the self-merging kernel
     hkv, g = 8, 4
     scale = 1 / math.sqrt(128)
-    for ctxs in ([512 + 7 * i for i in range(32)], [8000]):
+    # 32 x 8 pairs fill the chip: the v4 kernel (two workgroups per CU, each context split in two
+    # halves); the mixed list has one-chunk contexts (one non-empty half: direct output) and 64-key
+    # chunk boundaries; a single long sequence takes v3's static split
+    mixed = [1, 17, 64, 65, 127, 128, 129] + [300 + 37 * i for i in range(25)]
+    for ctxs in ([512 + 7 * i for i in range(32)], mixed, [8000]):
         q, kc, vc, bt, _, ctx, hq = _make_seqs([1] * len(ctxs), ctxs, hkv, 16, dev, g)
         bt_wide = torch.zeros(bt.shape[0], 8192 // 16, dtype=torch.int32, device=dev)
         bt_wide[:, : bt.shape[1]] = bt
-        out = ops.attn_decode(q, kc, vc, bt_wide, ctx, 8192, hq, hkv, scale)
+        cnt = torch.zeros(len(ctxs) * hkv, dtype=torch.int32, device=dev)
+        out = ops.attn_decode(q, kc, vc, bt_wide, ctx, 8192, hq, hkv, scale, counters=cnt)
         cu = torch.arange(len(ctxs) + 1, dtype=torch.int32, device=dev)
         r = ref.attention(q, kc, vc, bt, cu, ctx, hq, hkv, scale).reshape(q.shape[0], -1)
         close(out, r, atol=2.5e-2, rtol=2e-2)
+        out2 = ops.attn_decode(q, kc, vc, bt_wide, ctx, 8192, hq, hkv, scale, counters=cnt)
+        assert torch.equal(out, out2) and int(cnt.abs().sum()) == 0  # tickets re-armed
 
 
 def test_attn_softmax_spike(dev):
@@ -378,12 +387,17 @@ def test_mlp_decode_persistent(dev, m, h, inter):
     close(h1, ref_h.to(torch.bfloat16), atol=6e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("g,hkv", [(4, 8), (8, 1), (1, 4)])
-def test_attn_decode_fused(dev, g, hkv):
-    """Fused prologue: norm scale + qkv slab sum + RoPE at ctx-1 + KV write, then attention."""
+@pytest.mark.parametrize("g,hkv,big", [(4, 8, False), (8, 1, False), (1, 4, False), (4, 8, True), (4, 8, "v4")])
+def test_attn_decode_fused(dev, g, hkv, big, monkeypatch):
+    """Fused prologue: norm scale + qkv slab sum + RoPE at ctx-1 + KV write, then attention.
+    big: 32 sequences x 8 kv heads; "v4": the same through the opt-in v4 kernel (two workgroups
+    per CU, context halves)."""
+    monkeypatch.setenv("DIE_ATTN_V4", "1" if big == "v4" else "0")
     hq, sk, bs, d = hkv * g, 2, 16, 128
     hid = 1024
     ctxs = [1, 17, 200, 777, 2049]
+    if big:
+        ctxs = [1, 17, 64, 65, 129, 200, 777, 2049] + [400 + 29 * i for i in range(24)]
     n = len(ctxs)
     width = (hq + 2 * hkv) * d
     _, kc, vc, bt, _, ctx, _ = _make_seqs([1] * n, ctxs, hkv, bs, dev, g)
