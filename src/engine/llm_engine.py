@@ -116,6 +116,9 @@ class LLMEngine:
             raise ValueError(f"duplicate request id {request_id}")
         if len(prompt_ids) + sampling.max_tokens > self.max_model_len:
             raise ValueError(f"prompt + max_tokens exceeds max_model_len={self.max_model_len}")
+        if prompt_ids and (min(prompt_ids) < 0 or max(prompt_ids) >= self.arch.vocab_size):
+            # an out-of-range id would be an out-of-bounds embedding read on the GPU
+            raise ValueError(f"prompt token id outside [0, {self.arch.vocab_size})")
         seq = Sequence(request_id, list(prompt_ids), dataclasses.replace(sampling), on_finish=on_finish,
                        user_data=user_data, on_token=on_token)
         if export_kv:  # disaggregated prefill: stop after the first token and hand the prompt KV over
