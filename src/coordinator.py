@@ -252,6 +252,8 @@ class Coordinator:
             return {"success": True, "role": "coordinator", "workers": len(self.router.workers)}
         if op == "stats":
             return {"success": True, "stats": await self.get_stats()}
+        if op == "models":
+            return {"success": True, "models": {m: self.registry.list_versions(m) for m in self.registry.list_models()}}
         return {"error": f"unknown op {op!r}", "success": False}
 
     def _finish_async(self, rid: str, task: asyncio.Task) -> None:

@@ -152,6 +152,22 @@ class LLMBackend:
         If ``emit`` fails (client gone) the request is aborted."""
         q: asyncio.Queue = asyncio.Queue()
         task = asyncio.ensure_future(self.predict(inputs, request_id, on_token=q.put_nowait))
+        with_text = not isinstance(inputs, dict) or bool(inputs.get("return_text", True))
+        so_far: List[int] = []
+        text_sent = 0
+
+        async def send(toks: List[int]) -> None:
+            nonlocal text_sent
+            frame: Dict[str, Any] = {"delta_token_ids": toks, "done": False}
+            so_far.extend(toks)
+            if with_text:  # incremental detokenisation: hold back a trailing partial character
+                text = self.tokenizer.decode(so_far)
+                if text.endswith("\ufffd"):
+                    text = text.rstrip("\ufffd")
+                frame["delta_text"] = text[text_sent:]
+                text_sent = max(text_sent, len(text))
+            await emit(frame)
+
         try:
             while True:
                 get = asyncio.ensure_future(q.get())
@@ -162,13 +178,16 @@ class LLMBackend:
                 toks = [get.result()]
                 while not q.empty():
                     toks.append(q.get_nowait())
-                await emit({"delta_token_ids": toks, "done": False})
+                await send(toks)
             toks = []
             while not q.empty():  # tokens delivered before the completion callback ran
                 toks.append(q.get_nowait())
             if toks:
-                await emit({"delta_token_ids": toks, "done": False})
-            return await task
+                await send(toks)
+            out = await task
+            if with_text and isinstance(out.get("text"), str) and len(out["text"]) > text_sent:
+                await emit({"delta_token_ids": [], "delta_text": out["text"][text_sent:], "done": False})
+            return out
         except BaseException:
             task.cancel()
             raise
