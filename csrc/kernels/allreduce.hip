@@ -25,6 +25,7 @@
 #include "launchers.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace die {
@@ -43,7 +44,8 @@ __device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
 __global__ void __launch_bounds__(car::NTH) custom_all_reduce_kernel(const bf16_t* __restrict__ in,
                                                                      bf16_t* __restrict__ out, int64_t nvec,
                                                                      int rank, int world, CarPeers peers,
-                                                                     uint32_t* __restrict__ ctl, int64_t cap_vec) {
+                                                                     uint32_t* __restrict__ ctl, int64_t cap_vec,
+                                                                     int mode) {
   using namespace car;
   const int tid = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
   const uint32_t epoch = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
@@ -55,10 +57,12 @@ __global__ void __launch_bounds__(car::NTH) custom_all_reduce_kernel(const bf16_
   const uint4* src = reinterpret_cast<const uint4*>(in);
   uint4* mine = reinterpret_cast<uint4*>(peers.buf[rank]) + par * cap_vec;
   for (int64_t i = v0 + tid; i < v1; i += NTH) mine[i] = src[i];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the stores reach memory first
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's staging stores are acknowledged
   __syncthreads();
-  // 2. signal every peer, 3. wait for every peer's signal
+  // 2. signal every peer, 3. wait for every peer's signal (wave 0 only: one release per workgroup,
+  // issued by the wave that then stores the flags, so program order covers them)
   uint32_t* slots = peers.sig[rank] + ((int64_t)par * CAR_MAX_BLOCKS + b) * CAR_MAX_RANKS;
+  if (tid < 64 && !(mode & 2)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
   if (tid < world && tid != rank) {
     st_sys(peers.sig[tid] + ((int64_t)par * CAR_MAX_BLOCKS + b) * CAR_MAX_RANKS + rank, epoch);
     uint32_t it = 0;
@@ -71,7 +75,10 @@ __global__ void __launch_bounds__(car::NTH) custom_all_reduce_kernel(const bf16_
     }
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // peers' slices are read after their flags
+  // mode bit 0: the peers' slices are read with system-coherent (sc0 sc1) loads of uncached memory,
+  // so no cache can hold a stale copy and no L2-invalidating acquire is needed (the loads issue
+  // only after the polls returned: control dependency + the barrier above)
+  if (!(mode & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 
   // 4. reduce in rank order (bit-identical on every rank)
   const uint4* bufs[CAR_MAX_RANKS];
@@ -82,7 +89,16 @@ __global__ void __launch_bounds__(car::NTH) custom_all_reduce_kernel(const bf16_
   for (int64_t i = v0 + tid; i < v1; i += NTH) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int p = 0; p < world; ++p) {
-      const uint4 v = p == rank ? src[i] : bufs[p][i];  // uncached: read from the peer over xGMI
+      uint4 v;
+      if (p == rank) {
+        v = src[i];
+      } else if (mode & 1) {
+        __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(bufs[p]), 0, 0x7fffffff,
+                                                                     0x00020000);
+        v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 16), 0, 17));
+      } else {
+        v = bufs[p][i];  // uncached: read from the peer over xGMI
+      }
       float f[8];
       unpack8(v, f);
 #pragma unroll
@@ -98,9 +114,10 @@ __global__ void __launch_bounds__(car::NTH) custom_all_reduce_kernel(const bf16_
   // 5. the last workgroup advances the epoch for the next call (every workgroup read it at entry)
   __syncthreads();
   if (tid == 0) {
-    if (__hip_atomic_fetch_add(ctl + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)nb - 1) {
+    // relaxed: only atomicity matters here; the next launch reads the epoch after a kernel boundary
+    if (__hip_atomic_fetch_add(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)nb - 1) {
       __hip_atomic_store(ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ctl, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -116,8 +133,9 @@ hipError_t launch_custom_all_reduce(const bf16_t* in, bf16_t* out, int64_t n, in
     if (peers.buf[p] == nullptr || peers.sig[p] == nullptr) return hipErrorInvalidValue;
   const int64_t nvec = n / 8;
   blocks = (int)std::min<int64_t>(blocks, (nvec + 63) / 64);  // at least 64 vectors (1 KiB) per workgroup
+  static const int mode = getenv("DIE_CAR_MODE") ? atoi(getenv("DIE_CAR_MODE")) : 1;
   hipLaunchKernelGGL(custom_all_reduce_kernel, dim3(blocks), dim3(car::NTH), 0, s, in, out, nvec, rank, world,
-                     peers, ctl, cap_elems / 8);
+                     peers, ctl, cap_elems / 8, mode);
   return hipGetLastError();
 }
 
