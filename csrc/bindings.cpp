@@ -609,6 +609,36 @@ int64_t car_open(py::bytes handle) {
 
 void car_close(int64_t ptr) { DIE_HIP(die::car_ipc_close(reinterpret_cast<void*>(ptr))); }
 
+void car_all_reduce_residual(Tensor x, Tensor resid, Tensor ssp, int64_t rank, std::vector<int64_t> bufs,
+                             std::vector<int64_t> sigs, int64_t ctl, int64_t cap_elems) {
+  DIE_CHECK_CUDA(x);
+  DIE_CHECK_BF16(x);
+  DIE_CHECK_BF16(resid);
+  DIE_CHECK_CONTIG(x);
+  DIE_CHECK_CONTIG(resid);
+  DIE_CHECK_DTYPE(ssp, at::kFloat);
+  DIE_CHECK_CONTIG(ssp);
+  TORCH_CHECK(x.dim() == 2 && resid.sizes() == x.sizes(), "x and resid must both be [rows, hidden]");
+  const int64_t rows = x.size(0), hidden = x.size(1);
+  TORCH_CHECK(hidden % 8 == 0 && rows <= die::CAR_MAX_BLOCKS && rows * hidden <= cap_elems,
+              "all_reduce_residual: hidden % 8, rows <= 64, size <= cap");
+  TORCH_CHECK(ssp.numel() >= rows, "ssp too small");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(resid.data_ptr()) % 16 == 0, "16-byte alignment");
+  const int world = (int)bufs.size();
+  TORCH_CHECK(world >= 2 && world <= die::CAR_MAX_RANKS && (int)sigs.size() == world, "2..8 ranks");
+  TORCH_CHECK(rank >= 0 && rank < world && ctl != 0, "bad rank / control word");
+  die::CarPeers peers;
+  for (int p = 0; p < world; ++p) {
+    TORCH_CHECK(bufs[p] != 0 && sigs[p] != 0, "null peer pointer");
+    peers.buf[p] = reinterpret_cast<die::bf16_t*>(bufs[p]);
+    peers.sig[p] = reinterpret_cast<uint32_t*>(sigs[p]);
+  }
+  DIE_HIP(die::launch_custom_all_reduce_residual(bf(x), bf(resid), ssp.data_ptr<float>(), (int)rows, (int)hidden,
+                                                 (int)rank, world, peers, reinterpret_cast<uint32_t*>(ctl), cap_elems,
+                                                 cur_stream()));
+}
+
 std::vector<int64_t> car_read_words(int64_t ptr, int64_t n) {  // synchronising host read of uint32 words
   TORCH_CHECK(n > 0 && n <= 64, "car_read_words: 1..64 words");
   std::vector<uint32_t> h((size_t)n);
@@ -678,4 +708,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("car_close", &car_close);
   m.def("car_all_reduce", &car_all_reduce);
   m.def("car_read_words", &car_read_words);
+  m.def("car_all_reduce_residual", &car_all_reduce_residual);
 }

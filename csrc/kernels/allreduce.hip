@@ -122,6 +122,108 @@ __global__ void __launch_bounds__(car::NTH) custom_all_reduce_kernel(const bf16_
   }
 }
 
+// Fused variant for the tensor-parallel decode layer: the row-parallel projection's partial sums are
+// all-reduced AND added into the residual stream, and the new residual's per-row sums of squares (the
+// next RMSNorm's statistics, consumed as a row scale by the gate/up or qkv kernels) are written — what
+// all_reduce + residual_add_sumsq did in two launches. One workgroup per row (M <= 64 decode rows), so
+// each row's statistics come from one deterministic block reduction. Same protocol as above.
+__global__ void __launch_bounds__(car::NTH) custom_all_reduce_residual_kernel(
+    const bf16_t* __restrict__ in, bf16_t* __restrict__ resid, float* __restrict__ ssp, int hidden, int rank,
+    int world, CarPeers peers, uint32_t* __restrict__ ctl, int64_t cap_vec, int mode) {
+  using namespace car;
+  __shared__ float red[NTH / 64];
+  const int tid = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
+  const uint32_t epoch = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const int par = (int)(epoch & 1u);
+  const int hv = hidden / 8;
+  const int64_t v0 = (int64_t)b * hv, v1 = v0 + hv;
+  const uint4* src = reinterpret_cast<const uint4*>(in);
+  uint4* mine = reinterpret_cast<uint4*>(peers.buf[rank]) + par * cap_vec;
+  for (int64_t i = v0 + tid; i < v1; i += NTH) mine[i] = src[i];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  uint32_t* slots = peers.sig[rank] + ((int64_t)par * CAR_MAX_BLOCKS + b) * CAR_MAX_RANKS;
+  if (tid < 64 && !(mode & 2)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (tid < world && tid != rank) {
+    st_sys(peers.sig[tid] + ((int64_t)par * CAR_MAX_BLOCKS + b) * CAR_MAX_RANKS + rank, epoch);
+    uint32_t it = 0;
+    while (ld_sys(slots + tid) != epoch) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++it > (1u << 25)) {
+        __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (!(mode & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  uint4* r = reinterpret_cast<uint4*>(resid);
+  float ss = 0.f;
+  for (int64_t i = v0 + tid; i < v1; i += NTH) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < world; ++p) {
+      uint4 v;
+      if (p == rank) {
+        v = src[i];
+      } else {
+        const uint4* pb = reinterpret_cast<const uint4*>(peers.buf[p]) + par * cap_vec;
+        if (mode & 1) {
+          __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(pb), 0, 0x7fffffff,
+                                                                        0x00020000);
+          v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * 16), 0, 17));
+        } else {
+          v = pb[i];
+        }
+      }
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += f[j];
+    }
+    // the all-reduced partial is rounded to bf16 first (as a separate all-reduce would store it),
+    // then added to the residual; the statistics are of the rounded new residual
+    float h[8], a8[8];
+    unpack8(r[i], h);
+    unpack8(pack8(acc), a8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) h[j] += a8[j];
+    const uint4 pk = pack8(h);
+    r[i] = pk;
+    unpack8(pk, h);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += h[j] * h[j];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  if (tid == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < NTH / 64; ++w) t += red[w];
+    ssp[b] = t;
+    if (__hip_atomic_fetch_add(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)nb - 1) {
+      __hip_atomic_store(ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+hipError_t launch_custom_all_reduce_residual(const bf16_t* in, bf16_t* resid, float* ssp, int rows, int hidden,
+                                             int rank, int world, const CarPeers& peers, uint32_t* ctl,
+                                             int64_t cap_elems, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  if (hidden % 8 || rows > CAR_MAX_BLOCKS || world < 2 || world > CAR_MAX_RANKS || rank < 0 || rank >= world ||
+      (int64_t)rows * hidden > cap_elems)
+    return hipErrorInvalidValue;
+  for (int p = 0; p < world; ++p)
+    if (peers.buf[p] == nullptr || peers.sig[p] == nullptr) return hipErrorInvalidValue;
+  static const int mode = getenv("DIE_CAR_MODE") ? atoi(getenv("DIE_CAR_MODE")) : 1;
+  hipLaunchKernelGGL(custom_all_reduce_residual_kernel, dim3(rows), dim3(car::NTH), 0, s, in, resid, ssp, hidden,
+                     rank, world, peers, ctl, cap_elems / 8, mode);
+  return hipGetLastError();
+}
+
 hipError_t launch_custom_all_reduce(const bf16_t* in, bf16_t* out, int64_t n, int rank, int world,
                                     const CarPeers& peers, uint32_t* ctl, int64_t cap_elems, int blocks,
                                     hipStream_t s) {

@@ -103,6 +103,10 @@ struct CarPeers {
 hipError_t launch_custom_all_reduce(const bf16_t* in, bf16_t* out, int64_t n, int rank, int world,
                                     const CarPeers& peers, uint32_t* ctl, int64_t cap_elems, int blocks,
                                     hipStream_t s);
+// fused: resid [rows, hidden] += all_reduce(in) (bf16), ssp[row] = sum of squares of the new residual row
+hipError_t launch_custom_all_reduce_residual(const bf16_t* in, bf16_t* resid, float* ssp, int rows, int hidden,
+                                             int rank, int world, const CarPeers& peers, uint32_t* ctl,
+                                             int64_t cap_elems, hipStream_t s);
 hipError_t car_malloc(void** p, size_t bytes);
 hipError_t car_free(void* p);
 hipError_t car_ipc_handle(void* p, void* handle64);

@@ -469,10 +469,11 @@ class CausalLM:
             attn = ops.attn_decode_fused(slab, ssp_prev, positions, self.cos_sin, meta.slot_mapping,
                                          k_cache, v_cache, meta.block_tables, meta.ctx_lens, meta.max_ctx, hq, hkv,
                                          self.scale, eps, hid, meta.part_o, meta.part_ml, meta.attn_cnt)
-            if self.tp.enabled:  # row-parallel partial sums -> all-reduce (RCCL) -> residual + statistics
-                ops.residual_add_sumsq(h, self.tp.all_reduce(ops.linear(attn, lw.o)), sc["ssp_a"])
+            if self.tp.enabled:  # row-parallel partial sums -> all-reduce -> residual + statistics (one launch
+                # on the one-shot IPC path, see TPContext.all_reduce_residual)
+                self.tp.all_reduce_residual(ops.linear(attn, lw.o), h, sc["ssp_a"])
                 act = ops.linear_silu_mul_rownorm(h, lw.gate_up, sc["ssp_a"], eps)
-                ops.residual_add_sumsq(h, self.tp.all_reduce(ops.linear(act, lw.down)), sc["ssp_b"])
+                self.tp.all_reduce_residual(ops.linear(act, lw.down), h, sc["ssp_b"])
             else:
                 ops.linear_slab_residual(attn, lw.o, h, sc["ssp_a"], sc["cnt_a"], *plan["o"])
                 if plan["mlp_fused"]:  # gate/up -> down hand-off inside one persistent launch

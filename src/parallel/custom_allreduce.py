@@ -81,6 +81,17 @@ class CustomAllReduce:
         _kern().car_all_reduce(t, out, self.rank, self.bufs, self.sigs, self.ctl, self.cap, self.blocks)
         return out
 
+    def can_run_residual(self, x: torch.Tensor, resid: torch.Tensor) -> bool:
+        return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and x.shape[0] <= MAX_BLOCKS
+                and x.shape[1] % 8 == 0 and 2 * x.numel() <= self.max_bytes and x.is_contiguous()
+                and resid.is_contiguous() and resid.shape == x.shape and x.data_ptr() % 16 == 0
+                and resid.data_ptr() % 16 == 0)
+
+    def all_reduce_residual(self, x: torch.Tensor, resid: torch.Tensor, ssp: torch.Tensor) -> None:
+        """resid += sum over the group of x (bf16, in place), ssp[row] = that row's sum of squares of the
+        new residual — all-reduce and residual_add_sumsq in one launch (decode rows, <= 64)."""
+        _kern().car_all_reduce_residual(x, resid, ssp, self.rank, self.bufs, self.sigs, self.ctl, self.cap)
+
     def read_ctl(self) -> List[int]:
         """[epoch, ticket, error] control words (synchronising host read)."""
         return list(_kern().car_read_words(self.ctl, 3))

@@ -87,6 +87,18 @@ class TPContext:
                 dist.all_reduce(t, group=self.group)
         return t
 
+    def all_reduce_residual(self, x: torch.Tensor, resid: torch.Tensor, ssp: torch.Tensor) -> None:
+        """resid += all_reduce(x); ssp[0, row] = sum of squares of the new residual row (the next norm's
+        statistics). One fused launch on the one-shot IPC path, else all-reduce + residual_add_sumsq.
+        The choice depends only on shapes, so every rank takes the same path."""
+        car = self.car
+        if self.enabled and car is not None and car.can_run_residual(x, resid):
+            car.all_reduce_residual(x, resid, ssp)
+            return
+        from src import ops
+
+        ops.residual_add_sumsq(resid, self.all_reduce(x), ssp)
+
     # --- sequence parallelism (Megatron-SP): the all-reduce split into its two halves around the
     # token-sharded norms. Rows = tokens, padded by the caller to a multiple of world_size.
     def reduce_scatter_rows(self, t: torch.Tensor) -> torch.Tensor:

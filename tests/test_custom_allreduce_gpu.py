@@ -65,6 +65,24 @@ def _worker(rank, world, port, q):
             torch.cuda.synchronize()
             want = float(sum(r + 1 + it for r in range(world)))
             replay_ok.append(bool((yout.float() == want).all()))
+        # fused all-reduce + residual add + row statistics (the TP decode layer's form)
+        m, h = 19, 8192
+        g = torch.Generator(device="cuda").manual_seed(7 + rank)
+        x = torch.randn(m, h, device="cuda", generator=g).to(torch.bfloat16)
+        g0 = torch.Generator(device="cuda").manual_seed(99)  # the residual stream is the same on every rank
+        resid = torch.randn(m, h, device="cuda", generator=g0).to(torch.bfloat16)
+        ssp = torch.full((32,), -1.0, device="cuda")
+        allx = [torch.empty(m, h) for _ in range(world)]
+        dist.all_gather(allx, x.float().cpu())
+        tot = torch.zeros(m, h)
+        for t in allx:
+            tot += t
+        want = (resid.float().cpu() + tot.to(torch.bfloat16).float()).to(torch.bfloat16)
+        car.all_reduce_residual(x, resid, ssp)
+        torch.cuda.synchronize()
+        fused_ok = torch.equal(resid.cpu(), want) and torch.allclose(
+            ssp[:m].cpu(), want.float().pow(2).sum(-1), rtol=1e-4, atol=1e-2)
+        replay_ok.append(fused_ok)
         err = car.error()
         ctl = car.read_ctl()
         dist.barrier()
@@ -97,7 +115,7 @@ def test_custom_allreduce_two_ranks_one_gpu():
         assert all(ok.values()), ok
         assert all(replay_ok), replay_ok
         assert not err
-        assert ctl[0] == len(SIZES) + 1 + 5 and ctl[1] == 0, ctl  # one epoch per executed call (not the capture)
+        assert ctl[0] == len(SIZES) + 1 + 5 + 1 and ctl[1] == 0, ctl  # one epoch per executed call (not the capture)
     for n in SIZES:
         assert torch.equal(res[0][2][n], res[1][2][n])  # bit-identical on every rank
     assert all(p.exitcode == 0 for p in procs)
