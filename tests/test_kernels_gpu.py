@@ -196,9 +196,11 @@ def test_sampling_greedy_and_filters(dev):
     for step in range(20):
         steps = torch.full((6,), step, device=dev, dtype=torch.long)
         s = ops.sample(logits, temp, topk, topp, seeds, steps).cpu()
-        assert s[0] == top5[0, 0]                 # top_k = 1 → greedy
-        assert s[1] in top5[1] and s[2] in top5[2]
-        assert s[3] == top5[3, 0]                 # tiny top_p → argmax
+        # bf16 logits tie often at the top (spacing 1/16 near 12): compare values, not indices
+        lc = logits.float().cpu()
+        assert lc[0, s[0]] == lc[0].max()         # top_k = 1 → greedy
+        assert lc[1, s[1]] >= lc[1, top5[1, 4]] and lc[2, s[2]] >= lc[2, top5[2, 4]]
+        assert lc[3, s[3]] == lc[3].max()         # tiny top_p → argmax
     # reproducible per (seed, step)
     a = ops.sample(logits, temp, topk, topp, seeds, steps)
     b = ops.sample(logits, temp, topk, topp, seeds, steps)
