@@ -584,11 +584,29 @@ void rope_and_cache_slab(Tensor q_out, Tensor slab, Tensor positions, Tensor cos
 }
 
 // ---- one-shot all-reduce over IPC-mapped peer buffers (src/parallel/custom_allreduce.py)
-int64_t car_alloc(int64_t bytes) {
+int64_t car_alloc(int64_t bytes, bool uncached) {
   TORCH_CHECK(bytes > 0 && bytes % 256 == 0, "car_alloc: bytes must be a positive multiple of 256");
   void* p = nullptr;
-  DIE_HIP(die::car_malloc(&p, (size_t)bytes));
+  DIE_HIP(die::car_malloc(&p, (size_t)bytes, uncached));
   return reinterpret_cast<int64_t>(p);
+}
+
+// dst_ptr (raw device pointer, e.g. an IPC-mapped peer buffer) <- src (contiguous GPU tensor), by a
+// copy kernel on the current stream
+void car_copy_to(int64_t dst_ptr, Tensor src) {
+  DIE_CHECK_CUDA(src);
+  DIE_CHECK_CONTIG(src);
+  const int64_t nbytes = src.numel() * src.element_size();
+  TORCH_CHECK(dst_ptr != 0 && nbytes % 16 == 0, "car_copy_to: null destination or size not a multiple of 16");
+  DIE_HIP(die::launch_ipc_copy(reinterpret_cast<void*>(dst_ptr), src.data_ptr(), nbytes, cur_stream()));
+}
+
+// A byte tensor over raw device memory we own or mapped (IPC landing zones); no deleter: the owner
+// frees it with car_release / car_close after the last view is gone.
+Tensor car_tensor(int64_t ptr, int64_t nbytes, int64_t device) {
+  TORCH_CHECK(ptr != 0 && nbytes > 0, "car_tensor: null pointer or empty");
+  return torch::from_blob(reinterpret_cast<void*>(ptr), {nbytes},
+                          torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, (int)device));
 }
 
 void car_release(int64_t ptr) { DIE_HIP(die::car_free(reinterpret_cast<void*>(ptr))); }
@@ -603,7 +621,11 @@ int64_t car_open(py::bytes handle) {
   std::string s = handle;
   TORCH_CHECK(s.size() == sizeof(hipIpcMemHandle_t), "bad IPC handle size");
   void* p = nullptr;
-  DIE_HIP(die::car_ipc_open(s.data(), &p));
+  const hipError_t e = die::car_ipc_open(s.data(), &p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();  // do not leave the error behind for the next (unrelated) HIP call
+    TORCH_CHECK(false, "hipIpcOpenMemHandle failed: ", hipGetErrorString(e));
+  }
   return reinterpret_cast<int64_t>(p);
 }
 
@@ -701,7 +723,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_decode_grouped", &gemm_decode_grouped);
   m.def("fused_add_rms_norm_slab", &fused_add_rms_norm_slab);
   m.def("rope_and_cache_slab", &rope_and_cache_slab);
-  m.def("car_alloc", &car_alloc);
+  m.def("car_alloc", &car_alloc, py::arg("bytes"), py::arg("uncached") = true);
+  m.def("car_tensor", &car_tensor);
+  m.def("car_copy_to", &car_copy_to);
   m.def("car_release", &car_release);
   m.def("car_handle", &car_handle);
   m.def("car_open", &car_open);

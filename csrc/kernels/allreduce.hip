@@ -241,11 +241,31 @@ hipError_t launch_custom_all_reduce(const bf16_t* in, bf16_t* out, int64_t n, in
   return hipGetLastError();
 }
 
+// Plain 16-byte vector copy by shader stores: the KV IPC path writes into a peer's landing zone this
+// way (stores from the CUs travel over xGMI like the all-reduce's; no DMA engine involved).
+__global__ void __launch_bounds__(256) ipc_copy_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src,
+                                                       int64_t n16) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+hipError_t launch_ipc_copy(void* dst, const void* src, int64_t nbytes, hipStream_t s) {
+  if (nbytes <= 0) return hipSuccess;
+  if (nbytes % 16 || reinterpret_cast<uintptr_t>(dst) % 16 || reinterpret_cast<uintptr_t>(src) % 16)
+    return hipErrorInvalidValue;
+  const int64_t n16 = nbytes / 16;
+  const int grid = (int)std::min<int64_t>((n16 + 255) / 256, 2048);
+  hipLaunchKernelGGL(ipc_copy_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<uint4*>(dst),
+                     reinterpret_cast<const uint4*>(src), n16);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- IPC-shareable allocations
 // Staging buffers and flag pages are allocated uncached (hipDeviceMallocUncached): the peers'
 // loads and stores over xGMI then never meet a stale line in this GPU's L2.
-hipError_t car_malloc(void** p, size_t bytes) {
-  hipError_t e = hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+hipError_t car_malloc(void** p, size_t bytes, bool uncached) {
+  // uncached: flag pages and all-reduce staging; cached (plain hipMalloc): bulk landing zones that
+  // a peer fills by DMA and this GPU then reads once (KV shipping, src/parallel/kv_transfer.py)
+  hipError_t e = uncached ? hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached) : hipMalloc(p, bytes);
   if (e != hipSuccess) return e;
   return hipMemset(*p, 0, bytes);
 }

@@ -81,6 +81,8 @@ class LLMBackend:
         self.error_count = 0
         self.total_latency = 0.0
         self._live: Dict[str, str] = {}  # client request_id -> engine request id (abort)
+        self._zone = None                # IPC landing zone for shipped KV (decode role, lazily)
+        self.ipc_imports = 0
 
     async def start(self) -> None:
         self.async_engine.start()
@@ -210,7 +212,8 @@ class LLMBackend:
                                     finish_reason="stop", ttft_ms=pseq.ttft_ms(), latency_ms=pseq.latency_ms(),
                                     return_text=gi.return_text)
         packet = KVPacket(rid, gi.prompt_token_ids, pseq.output_ids[0], pseq.kv_export, self.engine.cfg.block_size,
-                          sampling_to_dict(gi.sampling), ttft_ms=pseq.ttft_ms())
+                          sampling_to_dict(gi.sampling), ttft_ms=pseq.ttft_ms(),
+                          ready=getattr(pseq, "kv_export_ready", None))
         pseq.kv_export = None
         rep = await self._decode_link.send(packet)
         if not rep.get("success"):
@@ -220,11 +223,29 @@ class LLMBackend:
         out["disaggregated"] = True
         return out
 
+    def _landing_zone(self):
+        if self._zone is None:
+            from src.parallel.kv_transfer import IPCLandingZone
+
+            cap = int((self.config.overrides or {}).get("kv_landing_zone_bytes",
+                                                         os.environ.get("DIE_KV_ZONE_BYTES", 1 << 30)))
+            self._zone = IPCLandingZone(self.engine.device, cap,
+                                        uncached=os.environ.get("DIE_KV_ZONE_UNCACHED", "0") == "1")
+        return self._zone
+
     async def _kv_import(self, msg: Dict[str, Any]) -> Dict[str, Any]:
         from src.engine.disagg import packet_for_import
+        from src.parallel.kv_transfer import KVPacket
         from src.preproc import SamplingParams
 
-        packet = packet_for_import(msg["packet"], self.engine.device)
+        d = msg["packet"]
+        if d.get("ipc") is not None:  # payload already delivered by DMA into the landing zone
+            kv = self._landing_zone().take(int(d["ipc"]["offset"]), d["shape"])
+            packet = KVPacket(d["request_id"], list(d["prompt_ids"]), int(d["first_token"]), kv,
+                              int(d["block_size"]), dict(d.get("sampling") or {}), d.get("ttft_ms"))
+            self.ipc_imports += 1
+        else:
+            packet = packet_for_import(d, self.engine.device)
         sp = SamplingParams(**packet.sampling) if packet.sampling else SamplingParams()
         if not self.async_engine.running:
             self.async_engine.start()
@@ -241,6 +262,15 @@ class LLMBackend:
             return {"success": True, "stats": self.async_engine.stats()}
         if op == "kv_import":
             return await self._kv_import(msg)
+        if op == "kv_channel":  # same-node prefill workers map this GPU's landing zone (IPC)
+            if self.engine.device.type != "cuda":
+                return {"success": False, "error": "no GPU landing zone on a CPU engine"}
+            z = self._landing_zone()
+            return {"success": True, "handle": z.handle, "capacity": z.capacity, "device": str(z.device),
+                    "pid": os.getpid()}
+        if op == "kv_reserve":
+            off = self._landing_zone().reserve(int(msg["nbytes"]))
+            return {"success": off is not None, "offset": off}
         raise ValueError(f"unsupported op {op}")
 
     def get_metrics(self) -> Dict[str, Any]:

@@ -16,15 +16,19 @@ control-plane RPC (``op: kv_import``).
 
 from __future__ import annotations
 
+import logging
+import os
 import time
 import uuid
 from typing import Any, Dict, List, Optional
 
 from src.engine.async_engine import AsyncLLMEngine
 from src.engine.sequence import Sequence
-from src.parallel.kv_transfer import KVPacket, packet_from_wire, packet_to_wire, ship
+from src.parallel.kv_transfer import KVPacket, packet_from_wire, packet_meta, packet_to_wire, ship
 from src.preproc import SamplingParams
 from src.rpc import RPCClient
+
+logger = logging.getLogger(__name__)
 
 
 class DisaggregatedServer:
@@ -69,16 +73,53 @@ class DisaggregatedServer:
 
 
 class RemoteDecodeLink:
-    """Prefill worker side of a cross-process pair: sends the packet to a
-    decode worker (``op: kv_import``) and returns that worker's reply."""
+    """Prefill worker side of a cross-process pair: sends the packet to a decode worker
+    (``op: kv_import``) and returns that worker's reply. On one node the KV payload goes by DMA into
+    the decode worker's IPC landing zone (``kv_channel`` once, ``kv_reserve`` per packet; xGMI between
+    two GPUs) and only the metadata crosses the socket; anywhere else — or if the zone is full — the
+    payload rides the RPC frame as bytes."""
 
-    def __init__(self, address: str, model: str, timeout: float = 600.0):
+    def __init__(self, address: str, model: str, timeout: float = 600.0, use_ipc: bool = True):
         self.address = address
         self.model = model
         self.rpc = RPCClient(max_idle_per_host=64, codec=b"M")  # msgpack: raw KV bytes, no base64
         self.timeout = timeout
+        self.use_ipc = use_ipc
+        self._ipc = None
+        self.ipc_packets = 0
+        self.wire_packets = 0
+
+    async def _channel(self, device):
+        if self._ipc is None and self.use_ipc and device.type == "cuda":
+            try:
+                rep = await self.rpc.call(self.address, {"op": "kv_channel", "model": self.model}, self.timeout)
+                if rep.get("success") and rep.get("pid") == os.getpid():
+                    self.use_ipc = False  # same process: a handle cannot be opened by its own exporter
+                elif rep.get("success"):
+                    from src.parallel.kv_transfer import IPCSender
+
+                    self._ipc = IPCSender(rep["handle"], rep["capacity"], device)
+                    logger.info("KV IPC channel to %s mapped (%d MiB landing zone)", self.address,
+                                rep["capacity"] >> 20)
+                else:
+                    self.use_ipc = False
+            except Exception as e:  # different node / no IPC: bytes over the socket from now on
+                logger.info("KV IPC channel to %s unavailable (%s); using the RPC payload path", self.address, e)
+                self.use_ipc = False
+        return self._ipc
 
     async def send(self, packet: KVPacket) -> Dict[str, Any]:
+        ch = await self._channel(packet.kv.device)
+        if ch is not None:
+            rep = await self.rpc.call(self.address, {"op": "kv_reserve", "model": self.model,
+                                                     "nbytes": packet.nbytes}, self.timeout)
+            if rep.get("success"):
+                ch.write(rep["offset"], packet.kv, packet.ready)
+                wire = dict(packet_meta(packet), ipc={"offset": rep["offset"]})
+                self.ipc_packets += 1
+                return await self.rpc.call(self.address, {"op": "kv_import", "model": self.model, "packet": wire},
+                                           self.timeout)
+        self.wire_packets += 1
         msg = {"op": "kv_import", "model": self.model, "packet": packet_to_wire(packet)}
         return await self.rpc.call(self.address, msg, self.timeout)
 

@@ -20,6 +20,7 @@ no prompt recompute. For Llama-3-8B a 512-token prompt is 64 MiB of KV.
 from __future__ import annotations
 
 from dataclasses import dataclass, field
+import threading
 from typing import Any, Dict, List, Optional
 
 import numpy as np
@@ -90,6 +91,116 @@ def ship(buf: torch.Tensor, device, ready=None):
         done.record(s)
     buf.record_stream(s)   # the source block may not be reused before the copy has read it
     return out, done
+
+
+class IPCLandingZone:
+    """Decode-worker side of cross-process KV shipping on one node: ONE IPC-shareable device buffer
+    (plain hipMalloc, so this GPU reads it through its caches) that prefill workers map
+    (hipIpcOpenMemHandle) and fill by DMA over xGMI — the packed prompt KV never touches host memory
+    or the RPC socket, which then carries only the metadata. Space is handed out per packet
+    (``reserve``, first fit) and returned once the decode engine has its own copy (``take``).
+
+    The zone stays below 2 GiB: on this ROCm (7.2, dmabuf IPC) hipIpcOpenMemHandle of a 2 GiB
+    allocation never returns in the importing process, while 256 MiB..1 GiB open in < 10 ms
+    (measured, scripts/repro_ipc_kv.py). 1 GiB holds 16 in-flight 512-token Llama-3-8B prompts."""
+
+    ALIGN = 1 << 16
+    MAX_BYTES = (1 << 31) - (1 << 20)
+
+    def __init__(self, device, capacity: int = 1 << 30, uncached: bool = False):
+        from src import _C
+
+        self.device = torch.device(device)
+        self.capacity = int(capacity)
+        if not 0 < self.capacity <= self.MAX_BYTES:
+            raise ValueError(f"landing zone of {self.capacity} bytes: must be in (0, {self.MAX_BYTES}]")
+        with torch.cuda.device(self.device):
+            self.ptr = _C.car_alloc(self.capacity, uncached)
+            self.view = _C.car_tensor(self.ptr, self.capacity, self.device.index or 0)
+        self.handle = _C.car_handle(self.ptr).hex()
+        self._free: List[List[int]] = [[0, self.capacity]]  # sorted [start, end) ranges
+        self._used: Dict[int, int] = {}
+        self._lock = threading.Lock()
+
+    def reserve(self, nbytes: int) -> Optional[int]:
+        n = -(-int(nbytes) // self.ALIGN) * self.ALIGN
+        with self._lock:
+            for r in self._free:
+                if r[1] - r[0] >= n:
+                    off = r[0]
+                    r[0] += n
+                    self._free = [x for x in self._free if x[1] > x[0]]
+                    self._used[off] = n
+                    return off
+        return None
+
+    def release(self, offset: int) -> None:
+        with self._lock:
+            n = self._used.pop(int(offset))
+            self._free.append([offset, offset + n])
+            self._free.sort()
+            merged: List[List[int]] = []
+            for r in self._free:
+                if merged and merged[-1][1] == r[0]:
+                    merged[-1][1] = r[1]
+                else:
+                    merged.append(r)
+            self._free = merged
+
+    def take(self, offset: int, shape: List[int]) -> torch.Tensor:
+        """Copy a delivered packet out of the zone (same-GPU D2D) and free its space."""
+        n = int(np.prod(shape)) * 2
+        with torch.cuda.device(self.device):
+            src = self.view[offset: offset + n].view(torch.bfloat16).view(*shape)
+            kv = src.clone()
+            torch.cuda.current_stream(self.device).synchronize()
+        self.release(offset)
+        return kv
+
+    def close(self) -> None:
+        from src import _C
+
+        self.view = None
+        _C.car_release(self.ptr)
+
+
+class IPCSender:
+    """Prefill-worker side: maps a decode worker's :class:`IPCLandingZone` into this GPU's address
+    space once, then each packet is one device-to-device copy into it (SDMA / blit over xGMI)."""
+
+    def __init__(self, handle_hex: str, capacity: int, device):
+        from src import _C
+
+        self.device = torch.device(device)
+        with torch.cuda.device(self.device):
+            self.ptr = _C.car_open(bytes.fromhex(handle_hex))
+            self.view = _C.car_tensor(self.ptr, int(capacity), self.device.index or 0)
+        self.bytes_sent = 0
+
+    def write(self, offset: int, kv: torch.Tensor, ready=None) -> None:
+        from src import _C
+
+        flat = kv.contiguous().view(torch.uint8).view(-1)
+        with torch.cuda.device(self.device):
+            cur = torch.cuda.current_stream(self.device)
+            if ready is not None:
+                cur.wait_event(ready)
+            # shader stores into the mapped peer buffer (the DMA engines are not used on IPC mappings)
+            _C.car_copy_to(self.ptr + int(offset), flat)
+            cur.synchronize()  # delivered before the decode worker is told to import it
+        self.bytes_sent += flat.numel()
+
+    def close(self) -> None:
+        from src import _C
+
+        self.view = None
+        _C.car_close(self.ptr)
+
+
+def packet_meta(p: KVPacket) -> Dict[str, Any]:
+    """The packet without its KV payload (the IPC path ships the payload by DMA)."""
+    return {"request_id": p.request_id, "prompt_ids": p.prompt_ids, "first_token": p.first_token,
+            "shape": list(p.kv.shape), "block_size": p.block_size, "sampling": p.sampling, "ttft_ms": p.ttft_ms}
 
 
 def packet_to_wire(p: KVPacket) -> Dict[str, Any]:

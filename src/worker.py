@@ -247,7 +247,7 @@ class Worker:
             if not resp.get("success"):
                 self._error_count += 1
             return resp
-        if op in ("kv_export", "kv_import", "engine_stats"):
+        if op in ("kv_export", "kv_import", "kv_channel", "kv_reserve", "engine_stats"):
             m = self.models.get(msg.get("model"))
             if m is None or not hasattr(m, "handle_op"):
                 return {"error": f"op {op} unsupported for model {msg.get('model')!r}", "success": False}
@@ -330,8 +330,8 @@ class Worker:
             self.models[config.model_name] = make_backend(config)
             logger.info("Loaded model '%s' (%s) on worker %s", config.model_name, config.arch, self.worker_id)
             return True
-        except Exception as e:
-            logger.error("Error loading model '%s': %s", config.model_name, e)
+        except Exception:
+            logger.exception("Error loading model '%s'", config.model_name)
             return False
 
     def unload_model(self, model_name: str) -> bool:

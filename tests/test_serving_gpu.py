@@ -101,3 +101,68 @@ def test_gpu_disaggregated_workers_over_rpc():
         for w in (pre, dec, solo):
             await w.shutdown()
     asyncio.run(main())
+
+
+def test_gpu_disaggregated_ipc_landing_zone():
+    """Prefill worker (this process) -> decode worker (a separate process on the same GPU): the
+    packed prompt KV goes by device-to-device copy into the decode worker's IPC landing zone (the
+    xGMI path between two GPUs of a node) and only metadata crosses the socket; tokens match a
+    colocated worker."""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    import time
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    fd, pf = tempfile.mkstemp()
+    os.close(fd)
+    os.unlink(pf)
+    cmd = [sys.executable, "-m", "src.worker", "--worker-id", "dec-ipc", "--host", "127.0.0.1", "--port", "0",
+           "--port-file", pf, "--model", "mini", "--arch", "llama", "--preset", "llama-mini", "--role", "decode",
+           "--max-batch-size", "8", "--max-model-len", "1024", "--num-kv-blocks", "256", "--max-latency-ms", "1"]
+    log = tempfile.TemporaryFile()
+    proc = subprocess.Popen(cmd, cwd=root, stdout=subprocess.DEVNULL, stderr=log)
+    try:
+        t0 = time.time()
+        while not os.path.exists(pf):
+            if proc.poll() is not None:
+                log.seek(0)
+                raise AssertionError(log.read().decode(errors="replace")[-3000:])
+            assert time.time() - t0 < 240, "decode worker did not start"
+            time.sleep(0.2)
+        dport = int(open(pf).read())
+
+        async def main():
+            pre = Worker("pre-ipc", host="127.0.0.1", install_signal_handlers=False)
+            assert pre.load_model(gpu_cfg(role="prefill", overrides={"decode_worker": f"127.0.0.1:{dport}"}))
+            pport = await pre.start()
+            solo = Worker("solo-ipc", host="127.0.0.1", install_signal_handlers=False)
+            assert solo.load_model(gpu_cfg())
+            sport = await solo.start()
+            cp, cs = InferenceClient(f"127.0.0.1:{pport}"), InferenceClient(f"127.0.0.1:{sport}")
+            for plen in (37, 300, 511):
+                req = {"prompt_token_ids": list(range(7, 7 + plen)), "max_tokens": 16, "ignore_eos": True}
+                a = await asyncio.wait_for(cp.call({"model": "mini", "inputs": req}), 60)
+                b = await asyncio.wait_for(cs.call({"model": "mini", "inputs": req}), 60)
+                assert a["success"] and b["success"], (a, b)
+                assert a["outputs"]["disaggregated"]
+                assert a["outputs"]["token_ids"] == b["outputs"]["token_ids"]
+            link = pre.models["mini"]._decode_link
+            assert link.ipc_packets == 3 and link.wire_packets == 0, (link.ipc_packets, link.wire_packets)
+            for x in (cp, cs):
+                x.close()
+            for w in (pre, solo):
+                await w.shutdown()
+        asyncio.run(main())
+    except BaseException:
+        log.seek(0)
+        print("decode worker log:\n" + log.read().decode(errors="replace")[-4000:], flush=True)
+        raise
+    finally:
+        proc.terminate()
+        try:
+            proc.wait(30)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+
