@@ -59,6 +59,8 @@ def main():
         return main_warm(m)
     if len(sys.argv) > 2 and sys.argv[2] == "deep":
         return main_deep(m)
+    if len(sys.argv) > 2 and sys.argv[2] == "moe":
+        return main_moe(m)
     dev = torch.device("cuda:0")
     for name, (n, k, silu) in SHAPES.items():
         wrows = 2 * n if silu else n
@@ -181,6 +183,43 @@ def main_deep(m):
         del ws
         torch.cuda.empty_cache()
 
+
+
+def main_moe(m):
+    """Activation-image height A/B (run under DIE_GD_XR16=0 and =1): the tuned dense configs at M = m,
+    and Mixtral-8x7B's grouped expert projections at m tokens, top-2 random routing."""
+    dev = torch.device("cuda:0")
+    xr16 = __import__("os").environ.get("DIE_GD_XR16", "1")
+    for name in ("qkv_8b", "o_8b", "gate_up_8b", "down_8b"):
+        n, k, silu = SHAPES[name]
+        mode = 1 if silu else (0 if (n, k, 0) in ops.DECODE_GEMM_CFG else 2)
+        wr, sk = ops._cfg_for(n, k, mode)
+        wrows = 2 * n if silu else n
+        x = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
+        wbytes = wrows * k * 2
+        copies = max(2, int(1.5 * 2**30 // wbytes) + 1)
+        ws = [torch.randn(wrows, k, device=dev, dtype=torch.bfloat16) / 64 for _ in range(copies)]
+        us = timeit(lambda w: ops.gemm_decode(x, w, mode, wr, sk), ws)
+        print(json.dumps({"shape": name, "M": m, "xr16": xr16, "us": round(us, 2),
+                          "GBps": round(wbytes / us / 1e3, 1)}), flush=True)
+        del ws
+    e, h, inter = 8, 4096, 14336
+    ids = torch.stack([torch.randperm(e, device=dev)[:2] for _ in range(m)]).to(torch.int32)
+    offsets, sorted_idx, pos = ops.moe_align(ids, e)
+    xs = torch.randn(2 * m, h, device=dev, dtype=torch.bfloat16)
+    a = torch.empty(2 * m, inter, device=dev, dtype=torch.bfloat16)
+    ys = torch.empty(2 * m, h, device=dev, dtype=torch.bfloat16)
+    w13s = [torch.randn(e, 2 * inter, h, device=dev, dtype=torch.bfloat16) / 64 for _ in range(2)]
+    w2s = [torch.randn(e, h, inter, device=dev, dtype=torch.bfloat16) / 64 for _ in range(2)]
+    kern = ops._kern()
+    wr1 = ops._cfg_for(inter, h, 1)[0]
+    for nm, ws, fn in (("moe_w13", w13s, lambda w: kern.gemm_decode_grouped(a, xs, w, offsets, 1, wr1)),
+                       ("moe_w2", w2s, lambda w: kern.gemm_decode_grouped(ys, a, w, offsets, 0,
+                                                                          ops._moe_down_wr(h, inter)))):
+        us = timeit(fn, ws)
+        wbytes = ws[0].numel() * 2
+        print(json.dumps({"shape": nm, "M": m, "rows_per_expert": (offsets[1:] - offsets[:-1]).tolist(),
+                          "xr16": xr16, "us": round(us, 2), "GBps": round(wbytes / us / 1e3, 1)}), flush=True)
 
 if __name__ == "__main__":
     main()

@@ -495,8 +495,11 @@ void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t m
   fz.grp_off = offsets.data_ptr<int>();
   fz.grp_wstride = w.size(1) * K;
   fz.grp_n = (int)E;
-  DIE_HIP(die::launch_gemm_decode(y.data_ptr(), y.stride(0), bf(x), x.stride(0), bf(w), 32, (int)N, (int)K, (int)mode,
-                                  (int)wr, 1, true, fz, cur_stream()));
+  // M = all rows: bounds every expert's rows (the kernel picks the 16-row activation image when <= 16)
+  TORCH_CHECK(x.size(0) >= 1, "grouped: at least one row");
+  DIE_HIP(die::launch_gemm_decode(y.data_ptr(), y.stride(0), bf(x), x.stride(0), bf(w),
+                                  (int)std::min<int64_t>(x.size(0), 32), (int)N, (int)K, (int)mode, (int)wr, 1, true,
+                                  fz, cur_stream()));
 }
 
 // Decode-step input advance (decode_step.hip), for multi-step decode windows.

@@ -25,6 +25,9 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace die {
 namespace gd {
 
@@ -64,7 +67,9 @@ using namespace gd;
 // write-through (sc1) so that workgroups on other XCDs can read it in the same launch.
 // XWAIT = 1: X read with sc1 loads; XWAIT = 2: one agent-scope acquire after the wait, then plain
 // (L2-cacheable) X loads (cdna_hip_programming.md Guideline 16 recipe R1).
-template <int WR, int EPI, int S, bool NT, int KC, int XWAIT = 0, bool WT = false>
+// XR: activation rows staged per chunk (32, or 16 when M <= 16: the X share of every DMA chunk — and of
+// the per-CU miss budget that bounds this kernel — halves; grouped MoE decode has ~8 rows per expert).
+template <int WR, int EPI, int S, bool NT, int KC, int XWAIT = 0, bool WT = false, int XR = MR>
 __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const bf16_t* __restrict__ X, int64_t ldx,
                                         const bf16_t* __restrict__ W, int M, int N_out, int K,
                                         const GemmDecodeFuse& fz, const int bx, const int by, const int ny,
@@ -74,22 +79,24 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
   constexpr int RPP = 64 / CPR;                // rows per 1-KiB DMA piece (2 or 4)
   constexpr bool SILU = EPI == 1 || EPI == 4;
   constexpr int NO = SILU ? WR / 2 : WR;       // output columns per workgroup
-  constexpr int SLOT = (WR + MR) * ROWB;       // bytes per ring slot
-  constexpr int INSTR = (WR + MR) / RPP;       // 1-KiB DMA pieces per chunk
+  constexpr int SLOT = (WR + XR) * ROWB;       // bytes per ring slot
+  constexpr int INSTR = (WR + XR) / RPP;       // 1-KiB DMA pieces per chunk
+  constexpr int MT = XR / 16;                  // 16-row MFMA tiles of activations
   constexpr int PER_WAVE = INSTR / 4;          // pieces issued per wave per chunk
   constexpr int NTILE = WR / 16;               // 16-column MFMA tiles
   constexpr int KSW = KC / 128;                // 32-deep k-steps per wave per chunk
   static_assert(INSTR % 4 == 0 && WR % RPP == 0, "pieces must split over 4 waves, W/X pieces unmixed");
   static_assert((S - 1) * PER_WAVE <= 63, "vmcnt field is 6 bits");
-  constexpr int PX = MR / RPP / 4;             // activation pieces per wave per chunk
-  static_assert((MR / RPP) % 4 == 0, "activation pieces must split over 4 waves");
+  constexpr int PX = XR / RPP / 4;             // activation pieces per wave per chunk
+  static_assert((XR / RPP) % 4 == 0 && (XR == 16 || XR == 32), "activation pieces must split over 4 waves");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (fz.grp_off != nullptr) {
     // grouped (MoE) form: blockIdx.z = expert; its rows of X/Y are [off[e], off[e+1]) of the
     // token-sorted activations, its weights W + e * grp_wstride. Unused experts cost nothing.
+    // (The launcher picks XR = 16 only when ALL experts together have <= 16 rows.)
     const int e = blockIdx.z;
     const int r0 = fz.grp_off[e];
-    M = min(fz.grp_off[e + 1] - r0, MR);
+    M = min(fz.grp_off[e + 1] - r0, XR);
     if (M <= 0) return;
     X += (int64_t)r0 * ldx;
     W += (int64_t)e * fz.grp_wstride;
@@ -151,9 +158,9 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
       ssv[i] = fz.ssp_in[min((tid >> 5) + 8 * i, fz.ssp_tiles - 1) * 32 + (tid & 31)];
   }
 
-  f4 acc[2][NTILE];
+  f4 acc[MT][NTILE];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < MT; ++a)
 #pragma unroll
     for (int b = 0; b < NTILE; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
 
@@ -215,9 +222,9 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
     for (int kk = 0; kk < KSW; ++kk) {
       const int ks = wave * KSW + kk;
       const int lch = 4 * ks + kg;
-      bf16x8 a[2], b[NTILE];
+      bf16x8 a[MT], b[NTILE];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
+      for (int mt = 0; mt < MT; ++mt) {
         const int r = 16 * mt + fr;
         a[mt] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ximg + r * ROWB + 16 * (lch ^ (r & 15))));
       }
@@ -227,7 +234,7 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
         b[nt] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(slot + r * ROWB + 16 * (lch ^ (r & 15))));
       }
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NTILE; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
@@ -239,7 +246,7 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
   // Cross-wave reduction through LDS (the ring is idle now): red[wave][m][WR] fp32.
   float* red = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int nt = 0; nt < NTILE; ++nt)
 #pragma unroll
@@ -351,13 +358,14 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
   }
 }
 
-template <int WR, int EPI, int S, bool NT, int KC>
+template <int WR, int EPI, int S, bool NT, int KC, int XR>
 __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv, int64_t ldy,
                                                           const bf16_t* __restrict__ X, int64_t ldx,
                                                           const bf16_t* __restrict__ W, int M, int N_out, int K,
                                                           GemmDecodeFuse fz) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  gd_body<WR, EPI, S, NT, KC>(smem, Yv, ldy, X, ldx, W, M, N_out, K, fz, blockIdx.x, blockIdx.y, gridDim.y);
+  gd_body<WR, EPI, S, NT, KC, 0, false, XR>(smem, Yv, ldy, X, ldx, W, M, N_out, K, fz, blockIdx.x, blockIdx.y,
+                                           gridDim.y);
 }
 
 // Persistent decode MLP (one launch instead of two): every workgroup first computes gate/up column
@@ -407,13 +415,30 @@ static hipError_t launch_gd(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, 
                             int K, int sk, bool nt, const GemmDecodeFuse& fz, hipStream_t s) {
   constexpr int NO = (EPI == 1 || EPI == 4) ? WR / 2 : WR;
   if (N_out % NO || K % sk || (K / sk) % KC) return hipErrorInvalidValue;
-  const size_t lds = (size_t)S * (WR + MR) * KC * 2;
-  if (nt)
-    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, true, KC>), dim3(N_out / NO, sk, fz.grp_n), dim3(NTH), lds,
-                       s, Y, ldy, X, ldx, W, M, N_out, K, fz);
-  else
-    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, false, KC>), dim3(N_out / NO, sk, fz.grp_n), dim3(NTH), lds,
-                       s, Y, ldy, X, ldx, W, M, N_out, K, fz);
+  // the ring, and after the loop the cross-wave reduction red[4][MR][WR] fp32 + epilogue scratch
+  auto lds_for = [](int xr) {
+    return std::max((size_t)S * (WR + xr) * KC * 2, (size_t)4 * MR * WR * 4 + 2048);
+  };
+  // 16-row activation image when every workgroup sees <= 16 rows (M = all rows, also in the grouped
+  // form). Measured (profiles/micro_gemm_decode_xr16_r1.jsonl): dense 8B projections at M = 8 / 16
+  // ~1.5 % faster on all four shapes; Mixtral grouped experts a tie (the time does not depend on the
+  // activation rows). Splitting a larger expert into two 16-row blocks re-reads its weights and LOSES
+  // (313 -> 345 us at 32 tokens), so M > 16 keeps the 32-row image.
+  static const bool xr16 = [] {
+    const char* e = std::getenv("DIE_GD_XR16");  // A/B knob: 0 = always the 32-row image
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  const bool small = xr16 && nt && M <= 16;
+  if (small) {
+    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, true, KC, 16>), dim3(N_out / NO, sk, fz.grp_n), dim3(NTH),
+                       lds_for(16), s, Y, ldy, X, ldx, W, M, N_out, K, fz);
+  } else if (nt) {
+    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, true, KC, MR>), dim3(N_out / NO, sk, fz.grp_n), dim3(NTH),
+                       lds_for(MR), s, Y, ldy, X, ldx, W, M, N_out, K, fz);
+  } else {
+    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, false, KC, MR>), dim3(N_out / NO, sk, fz.grp_n), dim3(NTH),
+                       lds_for(MR), s, Y, ldy, X, ldx, W, M, N_out, K, fz);
+  }
   return hipGetLastError();
 }
 

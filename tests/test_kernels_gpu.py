@@ -253,7 +253,26 @@ def test_moe(dev, t):
     close(ops.moe_forward(x, w13, w2, gating, k), ref.moe_forward(x, w13, w2, gating, k), atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("t", [8, 32])
+@pytest.mark.parametrize("skew", [True, False])
+def test_moe_decode_grouped(dev, t, skew):
+    """Grouped decode GEMM: 16-row activation image when all experts together have <= 16 rows (t = 8,
+    top-2), 32-row image otherwise; skew routes every token to experts 0 and 1 (t rows each, six idle
+    experts that must read nothing and write nothing)."""
+    h, inter, e, k = 1024, 512, 8, 2
+    x = torch.randn(t, h, device=dev, dtype=torch.bfloat16)
+    w13 = torch.randn(e, 2 * inter, h, device=dev, dtype=torch.bfloat16) / math.sqrt(h)
+    w2 = torch.randn(e, h, inter, device=dev, dtype=torch.bfloat16) / math.sqrt(inter)
+    if skew:
+        ids = torch.tensor([[0, 1]] * t, device=dev, dtype=torch.int32)
+    else:
+        ids = torch.stack([torch.randperm(e, device=dev)[:k] for _ in range(t)]).to(torch.int32)
+    w = torch.softmax(torch.randn(t, k, device=dev), -1)
+    close(ops.moe_apply(x, w13, w2, w, ids, e), ref.moe_experts(x, w13, w2, w, ids), atol=3e-2, rtol=3e-2)
+
+
 @pytest.mark.parametrize("m,n,k", [(1, 4096, 4096), (7, 6144, 4096), (32, 4096, 14336), (32, 1024, 256),
+                                   (16, 4096, 4096), (17, 6144, 4096),
                                    (20, 128256, 4096)])
 def test_gemm_decode(dev, m, n, k):
     x = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
