@@ -87,7 +87,10 @@ def _worker(rank, world, port, q):
         ctl = car.read_ctl()
         dist.barrier()
         car.close()
-        q.put((rank, {k: v[0] for k, v in out.items()}, {k: v[1] for k, v in out.items()}, replay_ok, err, ctl))
+        # results as numpy (bf16 bits): pickled by value, unlike tensors (shared-memory fds that
+        # vanish if this process exits before the parent reads them)
+        q.put((rank, {k: v[0] for k, v in out.items()}, {k: v[1].view(torch.int16).numpy() for k, v in out.items()},
+               replay_ok, err, ctl))
         dist.destroy_process_group()
     except Exception as e:  # surface the failure in the parent
         q.put((rank, repr(e), None, None, None, None))
@@ -117,5 +120,5 @@ def test_custom_allreduce_two_ranks_one_gpu():
         assert not err
         assert ctl[0] == len(SIZES) + 1 + 5 + 1 and ctl[1] == 0, ctl  # one epoch per executed call (not the capture)
     for n in SIZES:
-        assert torch.equal(res[0][2][n], res[1][2][n])  # bit-identical on every rank
+        assert (res[0][2][n] == res[1][2][n]).all()  # bit-identical on every rank
     assert all(p.exitcode == 0 for p in procs)

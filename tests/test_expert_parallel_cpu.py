@@ -50,7 +50,9 @@ def _worker(rank, world, port, q):
         tmax = 5 + 3 * (world - 1)
         padded = ep_moe_forward(x, router, w13_l, w2_l, K, capacity=tmax * K)
         tight = ep_moe_forward(x, router, w13_l, w2_l, K, capacity=2)
-        q.put((rank, exact, padded, tight))
+        # numpy arrays pickle by value: a tensor would travel as a shared-memory fd that vanishes
+        # when this process exits before the parent has read it
+        q.put((rank, exact.numpy(), padded.numpy(), tight.numpy()))
     except Exception as e:  # surface the failure in the parent instead of a queue timeout
         q.put((rank, repr(e), None, None))
         raise
@@ -78,7 +80,7 @@ def test_ep_all_to_all_matches_single_process(world):
     for r in range(world):
         x = _tokens(r)
         want = ref.moe_forward(x, w13, w2, x @ router.t(), K)
-        exact, padded, tight = got[r]
+        exact, padded, tight = (torch.from_numpy(a) for a in got[r])
         torch.testing.assert_close(exact, want, rtol=1e-5, atol=1e-5)
         torch.testing.assert_close(padded, want, rtol=1e-5, atol=1e-5)
         # capacity 2 per destination: assignments past the first two (in token order) are dropped

@@ -54,7 +54,7 @@ def _worker(rank, world, port, q):
         exact = ep_moe_forward(x, r, w13_l, w2_l, K, capacity=None)
         padded = ep_moe_forward(x, r, w13_l, w2_l, K, capacity=(24 + 5 * (world - 1)) * K)
         torch.cuda.synchronize()
-        q.put((rank, exact.float().cpu(), padded.float().cpu()))
+        q.put((rank, exact.float().cpu().numpy(), padded.float().cpu().numpy()))  # by value (see the CPU test)
     finally:
         dist.destroy_process_group()
 
@@ -84,4 +84,4 @@ def test_ep_all_to_all_on_gpu_kernels():
         gating = torch.nn.functional.linear(_tokens(r).to("cuda", bf), router.to("cuda", bf)).float().cpu()
         want = ref.moe_forward(x, w13b, w2b, gating, K)
         for out in got[r]:
-            torch.testing.assert_close(out, want, rtol=5e-2, atol=5e-2)
+            torch.testing.assert_close(torch.from_numpy(out), want, rtol=5e-2, atol=5e-2)
