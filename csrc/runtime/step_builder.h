@@ -22,10 +22,12 @@ inline void build_decode_inputs(const std::vector<std::vector<int>>& block_table
   auto* ctx = reinterpret_cast<int32_t*>(ctx_ptr);
   auto* bt = reinterpret_cast<int32_t*>(bt_ptr);
   const int n = (int)ctx_lens.size();
-  if ((int)block_tables.size() != n || padded < n) throw std::invalid_argument("decode inputs: bad sizes");
+  if ((int)block_tables.size() != n || padded < n || bt_stride < 1)
+    throw std::invalid_argument("decode inputs: bad sizes");
   for (int i = 0; i < n; ++i) {
     const int len = ctx_lens[i];
     const auto& tbl = block_tables[i];
+    if (len < 1) throw std::invalid_argument("decode inputs: context length must be >= 1");
     if ((int)tbl.size() > bt_stride) throw std::invalid_argument("block table wider than buffer");
     const int pos = len - 1;
     if (pos / block_size >= (int)tbl.size()) throw std::invalid_argument("block table too short for position");
@@ -68,6 +70,7 @@ inline int build_prefill_inputs(const std::vector<std::vector<int64_t>>& tokens,
     if ((int)tbl.size() > bt_stride) throw std::invalid_argument("block table wider than buffer");
     const int s0 = starts[i];
     const int len = (int)tk.size();
+    if (len < 1 || s0 < 0) throw std::invalid_argument("prefill inputs: empty chunk or negative start");
     if ((s0 + len + block_size - 1) / block_size > (int)tbl.size())
       throw std::invalid_argument("block table too short for prefill chunk");
     for (int j = 0; j < len; ++j) {
