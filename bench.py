@@ -66,8 +66,13 @@ def parse():
     return p.parse_args()
 
 
-async def serve_wave(batcher, n, prompt_len, gen_len, temperature, rng, tag, vocab=128000):
-    prompts = [[rng.randrange(3, vocab) for _ in range(prompt_len)] for _ in range(n)]
+def make_prompts(rng, n, prompt_len, vocab):
+    """One wave's synthetic prompts (client-side data, generated before the clock starts)."""
+    return [[rng.randrange(3, vocab) for _ in range(prompt_len)] for _ in range(n)]
+
+
+async def serve_wave(batcher, prompts, gen_len, temperature):
+    n = len(prompts)
     t0 = [0.0] * n
     lat = [0.0] * n
 
@@ -156,8 +161,11 @@ def main():
     async def run():
         batcher = Batcher(max_batch_size=args.batch, max_latency_ms=args.max_latency_ms, batch_callback=callback)
         await batcher.start()
+        vocab = engine.arch.vocab_size
         for w in range(args.warmup):
-            await serve_wave(batcher, args.batch, args.prompt_len, args.gen_len, args.temperature, rng, f"w{w}", engine.arch.vocab_size)
+            await serve_wave(batcher, make_prompts(rng, args.batch, args.prompt_len, vocab), args.gen_len,
+                             args.temperature)
+        waves = [make_prompts(rng, args.batch, args.prompt_len, vocab) for _ in range(args.steps)]
         sync()
         if tp is not None:
             engine.runner.stop_followers()
@@ -168,8 +176,7 @@ def main():
         t0 = time.perf_counter()
         lats = []
         for s in range(args.steps):
-            lats += await serve_wave(batcher, args.batch, args.prompt_len, args.gen_len, args.temperature, rng, vocab=engine.arch.vocab_size, tag=
-                                     f"s{s}")
+            lats += await serve_wave(batcher, waves[s], args.gen_len, args.temperature)
             if args.verbose and rank == 0:
                 print(f"step {s}: {time.perf_counter() - t0:.2f}s", file=sys.stderr, flush=True)
         sync()
