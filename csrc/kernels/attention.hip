@@ -168,8 +168,11 @@ __device__ __forceinline__ const bf16_t* kv_row(const bf16_t* cache, const int* 
 
 using namespace attn;
 
-// grid = (q tiles, num_seqs, hkv); block = 256 (4 waves); dynamic LDS = 2 * KV_TILE.
-template <int G>
+// grid = (q tiles, num_seqs, hkv); block = 256 (4 waves); dynamic LDS = 2 * NS * KV_TILE.
+// NS: 32-key sub-tiles per pipeline stage (one barrier and one round of global loads per stage):
+// NS = 2 halves the barriers and doubles the bytes in flight per round; 2 x 37 KiB stages still let
+// two workgroups share a CU's 160 KiB.
+template <int G, int NS>
 __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ q,
                                                            int64_t q_stride, const bf16_t* __restrict__ k_cache,
                                                            const bf16_t* __restrict__ v_cache,
@@ -193,7 +196,8 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(bf16_t* __restrict
   const bool row_valid = tok < qlen;
   const int kv_len_row = min(ctx, pos0 + min(tok, qlen - 1) + 1);
   const int kv_end = min(ctx, pos0 + min(t0 + TPB, qlen));
-  const int ntiles = (kv_end + KT - 1) / KT;
+  constexpr int ST = NS * KT;  // keys per stage
+  const int ntiles = (kv_end + ST - 1) / ST;
   const int wave_last_tok = min(t0 + wave * TPW + TPW, qlen) - 1;
   const int wave_kv_end = pos0 + wave_last_tok + 1;
   const int* bt = block_tables + (int64_t)seq * bt_stride;
@@ -203,16 +207,16 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(bf16_t* __restrict
   State st;
   init_state(st);
 
-  // staging role: key kr and kr+16 of the tile, 16-byte chunk c
+  // staging role: keys kr + 16 i of the stage, 16-byte chunk c
   const int kr = tid >> 4, c = tid & 15;
-  uint4 kreg[2], vreg[2];
+  uint4 kreg[2 * NS], vreg[2 * NS];
   auto load_tile = [&](int kt) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int key = kt * KT + kr + 16 * i;
-      // keys 16i .. 16i+15 of the tile share one block (block_size is a multiple of 16): the
+    for (int i = 0; i < 2 * NS; ++i) {
+      const int key = kt * ST + kr + 16 * i;
+      // keys 16i .. 16i+15 of the stage share one block (block_size is a multiple of 16): the
       // block id is wave-uniform, read by a scalar load instead of a per-lane dependent load
-      const int kb = __builtin_amdgcn_readfirstlane(min(kt * KT + 16 * i, kv_end - 1) / block_size);
+      const int kb = __builtin_amdgcn_readfirstlane(min(kt * ST + 16 * i, kv_end - 1) / block_size);
       const int64_t blk = bt[kb];
       const int64_t roff = ((blk * hkv + kvh) * block_size + key % block_size) * D + c * 8;
       if (key < kv_end) {
@@ -225,12 +229,12 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(bf16_t* __restrict
     }
   };
   auto store_tile = [&](int buf) {
-    char* kl = smem + buf * KV_TILE;
-    char* vl = kl + K_TILE;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      *reinterpret_cast<uint4*>(kl + (kr + 16 * i) * K_PITCH + c * 16) = kreg[i];
-      *reinterpret_cast<uint4*>(vl + (kr + 16 * i) * V_PITCH + c * 16) = vreg[i];
+    for (int i = 0; i < 2 * NS; ++i) {
+      char* kl = smem + (buf * NS + i / 2) * KV_TILE;  // sub-tile i / 2 of the stage
+      char* vl = kl + K_TILE;
+      *reinterpret_cast<uint4*>(kl + (kr + 16 * (i & 1)) * K_PITCH + c * 16) = kreg[i];
+      *reinterpret_cast<uint4*>(vl + (kr + 16 * (i & 1)) * V_PITCH + c * 16) = vreg[i];
     }
   };
 
@@ -240,11 +244,15 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(bf16_t* __restrict
   for (int kt = 0; kt < ntiles; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < ntiles) load_tile(kt + 1);
-    if (kt * KT < wave_kv_end) {  // wave-uniform: tile not entirely in this wave's causal future
-      const char* kl = smem + cur * KV_TILE;
-      f32x16_t s = qk_lds(kl, qf, lane);
-      softmax_tile(s, st, kt * KT, kv_len_row, scale_log2, h);
-      pv_lds(kl + K_TILE, s, st, lane);
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int kb0 = kt * ST + j * KT;
+      if (kb0 < wave_kv_end) {  // wave-uniform: sub-tile not entirely in this wave's causal future
+        const char* kl = smem + (cur * NS + j) * KV_TILE;
+        f32x16_t s = qk_lds(kl, qf, lane);
+        softmax_tile(s, st, kb0, kv_len_row, scale_log2, h);
+        pv_lds(kl + K_TILE, s, st, lane);
+      }
     }
     if (kt + 1 < ntiles) store_tile(cur ^ 1);
     __syncthreads();
@@ -1210,11 +1218,19 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
   const float sl2 = scale * 1.4426950408889634f;
   const int tpb = 4 * (32 / (G > 32 ? 32 : G));
   dim3 grid((max_q_len + tpb - 1) / tpb, num_seqs, hkv), block(256);
-  const size_t lds = 2 * KV_TILE;
-#define DIE_PF(GG)                                                                                          \
-  case GG:                                                                                                  \
-    hipLaunchKernelGGL(attn_prefill_kernel<GG>, grid, block, lds, s, out, q, q_stride, k_cache, v_cache, \
-                       block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2);                  \
+  static const int ns = [] {
+    const char* e = std::getenv("DIE_PF_NS");  // A/B knob: 32-key sub-tiles per stage (1 or 2)
+    return e != nullptr && std::atoi(e) == 1 ? 1 : 2;
+  }();
+  const size_t lds = 2 * ns * KV_TILE;
+#define DIE_PF(GG)                                                                                             \
+  case GG:                                                                                                     \
+    if (ns == 2)                                                                                               \
+      hipLaunchKernelGGL((attn_prefill_kernel<GG, 2>), grid, block, lds, s, out, q, q_stride, k_cache, v_cache, \
+                         block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2);                   \
+    else                                                                                                       \
+      hipLaunchKernelGGL((attn_prefill_kernel<GG, 1>), grid, block, lds, s, out, q, q_stride, k_cache, v_cache, \
+                         block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2);                   \
     break;
   switch (G) {
     DIE_PF(1)
