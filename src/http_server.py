@@ -9,6 +9,10 @@ coordinator's framed-RPC API. It holds no model state — every request becomes 
                             "top_p", "top_k", "seed", "stop_token_ids", "ignore_eos", "stream"}
                            stream=true answers with server-sent events ("data: {...}" chunks,
                            then "data: [DONE]"), text and token ids per chunk
+    POST /v1/chat/completions  {"model", "messages": [{"role", "content"}], same sampling keys}:
+                           the messages rendered in the Llama-3 chat layout (header / end-of-turn
+                           markers as text) plus an open assistant turn; answers "chat.completion"
+                           objects, or "chat.completion.chunk" deltas when streaming
     GET  /v1/models        the coordinator's registered models
     GET  /health           200 when the coordinator answers its health RPC
     GET  /metrics          Prometheus text format (requests, errors, latency, tokens)
@@ -31,6 +35,21 @@ from src.client import InferenceClient
 from src.utils import setup_logging
 
 _SAMPLING = ("max_tokens", "temperature", "top_p", "top_k", "seed", "stop_token_ids", "ignore_eos")
+_ROLES = ("system", "user", "assistant", "tool")
+
+
+def render_chat(messages: Any) -> str:
+    """Llama-3 chat layout: one header + body + end-of-turn per message, then an open assistant
+    header for the model to continue. (The tokenizer adds the beginning-of-text token.)"""
+    if not isinstance(messages, list) or not messages:
+        raise ValueError("messages must be a non-empty list")
+    out = []
+    for m in messages:
+        if not isinstance(m, dict) or m.get("role") not in _ROLES or not isinstance(m.get("content"), str):
+            raise ValueError("each message needs a role in %s and a string content" % (_ROLES,))
+        out.append(f"<|start_header_id|>{m['role']}<|end_header_id|>\n\n{m['content']}<|eot_id|>")
+    out.append("<|start_header_id|>assistant<|end_header_id|>\n\n")
+    return "".join(out)
 
 
 class Gateway:
@@ -48,6 +67,7 @@ class Gateway:
     def app(self) -> web.Application:
         a = web.Application()
         a.router.add_post("/v1/completions", self.completions)
+        a.router.add_post("/v1/chat/completions", self.chat_completions)
         a.router.add_get("/v1/models", self.models)
         a.router.add_get("/health", self.health)
         a.router.add_get("/metrics", self.metrics)
@@ -73,35 +93,59 @@ class Gateway:
         return inp
 
     @staticmethod
-    def _choice(out: Dict[str, Any]) -> Dict[str, Any]:
-        return {"index": 0, "text": out.get("text", ""), "token_ids": out.get("token_ids", []),
-                "finish_reason": out.get("finish_reason"), "logprobs": None}
+    def _choice(out: Dict[str, Any], chat: bool = False) -> Dict[str, Any]:
+        c = {"index": 0, "token_ids": out.get("token_ids", []), "finish_reason": out.get("finish_reason"),
+             "logprobs": None}
+        if chat:
+            c["message"] = {"role": "assistant", "content": out.get("text", "")}
+        else:
+            c["text"] = out.get("text", "")
+        return c
 
     async def completions(self, req: web.Request) -> web.StreamResponse:
+        return await self._serve(req, chat=False)
+
+    async def chat_completions(self, req: web.Request) -> web.StreamResponse:
+        return await self._serve(req, chat=True)
+
+    async def _serve(self, req: web.Request, chat: bool) -> web.StreamResponse:
         t0 = time.perf_counter()
         try:
             body = await req.json()
             model = body["model"]
+            if chat:
+                body = dict(body, prompt=render_chat(body.get("messages")))
             inputs = self._inputs(body)
         except (ValueError, KeyError, json.JSONDecodeError) as e:
             return web.json_response({"error": {"message": f"bad request: {e}", "type": "invalid_request"}},
                                      status=400)
         stream = bool(body.get("stream"))
         self.m_req.labels(model, str(stream).lower()).inc()
-        cid = "cmpl-" + uuid.uuid4().hex[:24]
+        cid = ("chatcmpl-" if chat else "cmpl-") + uuid.uuid4().hex[:24]
         created = int(time.time())
         if not stream:
             rep = await self.client.infer(model, inputs, cache=body.get("cache", True))
-            return self._finish(model, cid, created, rep, t0)
+            return self._finish(model, cid, created, rep, t0, chat)
         resp = web.StreamResponse(headers={"Content-Type": "text/event-stream", "Cache-Control": "no-cache"})
         await resp.prepare(req)
         final: Optional[Dict[str, Any]] = None
+        first = True
         try:
             async for frame in self.client.infer_stream(model, inputs):
                 if frame.get("done") is False:
-                    chunk = {"id": cid, "object": "text_completion", "created": created, "model": model,
-                             "choices": [{"index": 0, "text": frame.get("delta_text", ""),
-                                          "token_ids": frame.get("delta_token_ids", []), "finish_reason": None}]}
+                    if chat:
+                        delta: Dict[str, Any] = {"content": frame.get("delta_text", "")}
+                        if first:
+                            delta["role"] = "assistant"
+                        chunk = {"id": cid, "object": "chat.completion.chunk", "created": created, "model": model,
+                                 "choices": [{"index": 0, "delta": delta,
+                                              "token_ids": frame.get("delta_token_ids", []), "finish_reason": None}]}
+                    else:
+                        chunk = {"id": cid, "object": "text_completion", "created": created, "model": model,
+                                 "choices": [{"index": 0, "text": frame.get("delta_text", ""),
+                                              "token_ids": frame.get("delta_token_ids", []),
+                                              "finish_reason": None}]}
+                    first = False
                     await resp.write(b"data: " + json.dumps(chunk).encode() + b"\n\n")
                 else:
                     final = frame
@@ -114,9 +158,10 @@ class Gateway:
         else:
             out = final["outputs"]
             self._observe(model, out, t0)
-            last = {"id": cid, "object": "text_completion", "created": created, "model": model,
-                    "choices": [{"index": 0, "text": "", "token_ids": [], "finish_reason": out.get("finish_reason")}],
-                    "usage": self._usage(out)}
+            end = {"index": 0, "token_ids": [], "finish_reason": out.get("finish_reason")}
+            end.update({"delta": {}} if chat else {"text": ""})
+            last = {"id": cid, "object": "chat.completion.chunk" if chat else "text_completion", "created": created,
+                    "model": model, "choices": [end], "usage": self._usage(out)}
             await resp.write(b"data: " + json.dumps(last).encode() + b"\n\n")
         await resp.write(b"data: [DONE]\n\n")
         await resp.write_eof()
@@ -133,7 +178,8 @@ class Gateway:
         p, c = int(out.get("num_prompt_tokens", 0)), int(out.get("num_output_tokens", 0))
         return {"prompt_tokens": p, "completion_tokens": c, "total_tokens": p + c}
 
-    def _finish(self, model: str, cid: str, created: int, rep: Dict[str, Any], t0: float) -> web.Response:
+    def _finish(self, model: str, cid: str, created: int, rep: Dict[str, Any], t0: float,
+                chat: bool = False) -> web.Response:
         if not rep.get("success"):
             self.m_err.labels(model).inc()
             status = 404 if "not registered" in str(rep.get("error", "")) else 502
@@ -143,9 +189,9 @@ class Gateway:
             return web.json_response({"id": cid, "object": "text_completion", "created": created, "model": model,
                                       "outputs": out})
         self._observe(model, out, t0)
-        return web.json_response({"id": cid, "object": "text_completion", "created": created, "model": model,
-                                  "choices": [self._choice(out)], "usage": self._usage(out),
-                                  "cached": bool(rep.get("cached"))})
+        return web.json_response({"id": cid, "object": "chat.completion" if chat else "text_completion",
+                                  "created": created, "model": model, "choices": [self._choice(out, chat)],
+                                  "usage": self._usage(out), "cached": bool(rep.get("cached"))})
 
     async def models(self, _req: web.Request) -> web.Response:
         rep = await self.client.call({"op": "models"})

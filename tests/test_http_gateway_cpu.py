@@ -11,7 +11,7 @@ from aiohttp import web
 from src.client import InferenceClient
 from src.config import ModelConfig
 from src.coordinator import Coordinator
-from src.http_server import Gateway
+from src.http_server import Gateway, render_chat
 from src.worker import Worker
 
 
@@ -70,6 +70,32 @@ def test_openai_completions_plain_and_stream():
                 m = await r.text()
                 assert 'die_http_requests_total{model="tiny",stream="true"} 1.0' in m
                 assert "die_http_output_tokens_total" in m
+            # chat: the rendered conversation is an ordinary prompt; plain and streamed agree with RPC
+            msgs = [{"role": "system", "content": "be brief"}, {"role": "user", "content": "hello"}]
+            chat = {"model": "tiny", "messages": msgs, "max_tokens": 7, "ignore_eos": True}
+            want = await InferenceClient(f"127.0.0.1:{cport}").infer(
+                "tiny", {"prompt": render_chat(msgs), "max_tokens": 7, "ignore_eos": True}, cache=False)
+            async with s.post(base + "/v1/chat/completions", json=chat) as r:
+                assert r.status == 200
+                cj = await r.json()
+            assert cj["object"] == "chat.completion" and cj["id"].startswith("chatcmpl-")
+            msg = cj["choices"][0]["message"]
+            assert msg["role"] == "assistant" and msg["content"] == want["outputs"]["text"]
+            assert cj["choices"][0]["token_ids"] == want["outputs"]["token_ids"]
+            deltas, roles = [], []
+            async with s.post(base + "/v1/chat/completions", json=dict(chat, stream=True)) as r:
+                async for line in r.content:
+                    line = line.decode().strip()
+                    if not line.startswith("data: ") or line[6:] == "[DONE]":
+                        continue
+                    ch = json.loads(line[6:])
+                    assert ch["object"] == "chat.completion.chunk"
+                    d = ch["choices"][0]["delta"]
+                    roles.append(d.get("role"))
+                    deltas += ch["choices"][0]["token_ids"]
+            assert roles[0] == "assistant" and deltas == want["outputs"]["token_ids"]
+            async with s.post(base + "/v1/chat/completions", json={"model": "tiny", "messages": []}) as r:
+                assert r.status == 400
             async with s.post(base + "/v1/completions", json={"model": "nope", "prompt": "x"}) as r:
                 assert r.status == 404
             async with s.post(base + "/v1/completions", json={"model": "tiny", "prompt": {"bad": 1}}) as r:
