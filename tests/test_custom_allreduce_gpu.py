@@ -1,8 +1,8 @@
-"""One-shot IPC all-reduce (csrc/kernels/allreduce.hip) on real hardware: two ranks as two
+"""One-shot IPC all-reduce (csrc/kernels/allreduce.hip) on real hardware: 2, 4 and 8 ranks as
 processes sharing the box's one MI355X (the IPC-mapped peer memory is then local, the protocol —
 uncached staging, system-scope flags, epochs, double buffering — is the same one that runs over
 xGMI on an 8-GPU node). Results are checked against the fp32 sum of both inputs rounded once to
-bf16 (the kernel's rank-order fp32 accumulation) and must be bit-identical on both ranks, eagerly
+bf16 (the kernel's rank-order fp32 accumulation) and must be bit-identical on every rank, eagerly
 and under hipGraph replay, across sizes that exercise partial workgroup slices."""
 
 import os
@@ -97,22 +97,24 @@ def _worker(rank, world, port, q):
         raise
 
 
-def test_custom_allreduce_two_ranks_one_gpu():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_custom_allreduce_ranks_one_gpu(world):
+    """world ranks as world processes on the one GPU: 8 exercises the full TP=8 peer loops."""
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
-    for _ in range(2):
+    for _ in range(world):
         r = q.get(timeout=240)
         res[r[0]] = r
     for p in procs:
         p.join(60)
-    for r in (0, 1):
+    for r in range(world):
         assert not isinstance(res[r][1], str), res[r][1]
         _, ok, _, replay_ok, err, ctl = res[r]
         assert all(ok.values()), ok
@@ -120,5 +122,6 @@ def test_custom_allreduce_two_ranks_one_gpu():
         assert not err
         assert ctl[0] == len(SIZES) + 1 + 5 + 1 and ctl[1] == 0, ctl  # one epoch per executed call (not the capture)
     for n in SIZES:
-        assert (res[0][2][n] == res[1][2][n]).all()  # bit-identical on every rank
+        for r in range(1, world):
+            assert (res[0][2][n] == res[r][2][n]).all()  # bit-identical on every rank
     assert all(p.exitcode == 0 for p in procs)
