@@ -482,8 +482,13 @@ constexpr int V3_CHUNK = 2 * DEC_KEYS * DEC_ROW;               // K + V images o
 constexpr int V3_QIMG = 2048;                                  // G <= 8 query rows x 256 B
 constexpr int V3_BUF = V3_CHUNK + V3_QIMG;
 constexpr int V3_ML = 4 * 32 * 2 * 4;                          // per-wave (m, l): 1 KiB
-constexpr int V3_MERGE = V3_ML + 4 * 8 * D * 4;                // + per-wave O for G <= 8: 16 KiB
-constexpr int V3_LDS = 2 * V3_BUF + V3_MERGE + 16;             // 152,592 B
+// merge area: per-wave (m, l) + per-wave O for G <= 8 (17 KiB) — and, idle at a task start, the FUSED
+// prologue's slab staging: sk x (G + 2) rows of 512 B + 1.5 KiB. Sized to the LDS left over (27 KiB),
+// so the qkv projection may use split-K 4 at G = 8 (Llama-3-70B TP=8) and 8 at G = 4.
+constexpr int V3_MERGE = 27 * 1024;
+static_assert(V3_MERGE >= V3_ML + 4 * 8 * D * 4, "merge area holds the per-wave O of G <= 8");
+constexpr int V3_LDS = 2 * V3_BUF + V3_MERGE + 16;             // 162,832 B
+static_assert(V3_LDS <= 160 * 1024, "one v3 workgroup per CU");
 
 
 template <int N>

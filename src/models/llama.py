@@ -58,6 +58,9 @@ class LayerWeights:
             setattr(self, s, None)
 
 
+# LDS staging area of the fused decode attention's prologue (csrc/kernels/attention.hip V3_MERGE)
+V3_MERGE_BYTES = 27 * 1024
+
 class CausalLM:
     """A TP-sharded decoder-only LM (no nn.Module overhead on the hot path)."""
 
@@ -406,9 +409,10 @@ class CausalLM:
         residual-updating o / down projections (wr in {32, 64, 128}: one norm-statistics tile
         per wr output columns)."""
         h, d = self.arch.hidden_size, self.head_dim
-        # the fused attention stages sk x (G + 2) slab rows of 512 B in its 17 KiB merge area
+        # the fused attention stages sk x (G + 2) slab rows of 512 B (+ 1.5 KiB) in its 27 KiB merge
+        # area (V3_MERGE_BYTES): at most 50 rows
         g = max(1, self.hq // self.hkv)
-        wq, sq = ops._cfg_for(self.layers[0].qkv.shape[0], h, 2, max_sk=max(1, 30 // (g + 2)))
+        wq, sq = ops._cfg_for(self.layers[0].qkv.shape[0], h, 2, max_sk=max(1, 50 // (g + 2)))
 
         def resid_cfg(k):
             c = ops.DECODE_GEMM_RESID_CFG.get((h, k))
@@ -451,7 +455,7 @@ class CausalLM:
         g = self.hq // self.hkv
         sq = self.decode_plan()["qkv"][1]
         return (self.norms_folded and self.head_dim == 128 and kv_pool.shape[4] == 16 and g in (1, 2, 4, 8)
-                and ((sq * (g + 2) + 1) // 2) * 1024 + 1536 <= 17408)
+                and ((sq * (g + 2) + 1) // 2) * 1024 + 1536 <= V3_MERGE_BYTES)
 
     def _forward_decode_fused(self, h: torch.Tensor, positions: torch.Tensor, meta: AttnMetadata,
                               kv_pool: torch.Tensor) -> torch.Tensor:

@@ -150,6 +150,43 @@ class TPContext:
         return t
 
 
+class ShardProbeTP(TPContext):
+    """Rank 0's shard of a TP=``world_size`` model in ONE process, collectives replaced by local
+    stand-ins (all-reduce = identity, all-gather = ``world_size`` copies of the local shard,
+    broadcast = nothing). Every GEMM, attention and norm runs at the real per-rank shapes, so the
+    step time is the per-rank COMPUTE of the TP configuration (e.g. Llama-3-70B TP=8 on one GPU,
+    bench/tp_probe.py); the collectives' cost is not in it, and the tokens are meaningless."""
+
+    probe = True
+
+    def __init__(self, world_size: int):
+        super().__init__(rank=0, world_size=world_size, group=None)
+
+    def enable_custom_allreduce(self, max_bytes: int = 8 << 20) -> bool:
+        return False
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        return t
+
+    def all_reduce_residual(self, x: torch.Tensor, resid: torch.Tensor, ssp: torch.Tensor) -> None:
+        from src import ops
+
+        ops.residual_add_sumsq(resid, x, ssp)  # the non-fused path's local launch
+
+    def reduce_scatter_rows(self, t: torch.Tensor) -> torch.Tensor:
+        n = t.shape[0] // self.world_size
+        return t[:n].contiguous()
+
+    def all_gather_rows(self, t: torch.Tensor) -> torch.Tensor:
+        return torch.cat([t] * self.world_size, 0)
+
+    def all_gather_last(self, t: torch.Tensor) -> torch.Tensor:
+        return torch.cat([t] * self.world_size, dim=-1)
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        return t
+
+
 _TP: Optional[TPContext] = None
 
 

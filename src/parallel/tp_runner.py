@@ -100,7 +100,7 @@ class TPModelRunner(ModelRunner):
 
 def agree_num_blocks(n: int, tp) -> int:
     """Every rank must use the same block ids: take the minimum."""
-    if not tp.enabled:
+    if not tp.enabled or getattr(tp, "probe", False):
         return n
     dev = "cuda" if torch.cuda.is_available() and dist.get_backend(tp.group) == "nccl" else "cpu"
     t = torch.tensor([n], dtype=torch.int64, device=dev)

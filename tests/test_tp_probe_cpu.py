@@ -1,0 +1,23 @@
+"""bench/tp_probe.py on CPU: rank 0's shard of a TP=2 / TP=4 model runs the serving workload in one
+process with the collectives stubbed (src/parallel/tp.py ShardProbeTP) — shard shapes, the
+vocab-parallel LM head and the step loop all work without a process group."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("tp", [2, 4])
+def test_tp_probe_runs_shard_on_cpu(tp):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench", "tp_probe.py"), "--preset", "llama-mini",
+                        "--tp", str(tp), "--batch", "3", "--prompt-len", "20", "--gen-len", "5", "--steps", "1",
+                        "--warmup", "0", "--device", "cpu"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["bench"] == "tp_shard_probe" and d["tp"] == tp and d["decode_ms_per_step"] > 0
+    assert "all-reduce" in d["not_included"]
