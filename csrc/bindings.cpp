@@ -325,6 +325,25 @@ void moe_combine(Tensor out, Tensor ys, Tensor pos, Tensor w) {
                                   (int)out.size(1), cur_stream()));
 }
 
+// Fused decode routing: w [T, K] fp32, ids [T, K] int32 from x [T, H] (row stride ldx) and the router
+// weights wg [E, H] bf16 (moe.hip moe_route_kernel).
+void moe_route(Tensor w, Tensor ids, Tensor x, Tensor wg, bool renorm) {
+  DIE_CHECK_CUDA(x);
+  DIE_CHECK_BF16(x);
+  DIE_CHECK_BF16(wg);
+  DIE_CHECK_CONTIG(wg);
+  DIE_CHECK_CONTIG(w);
+  DIE_CHECK_CONTIG(ids);
+  DIE_CHECK_DTYPE(w, at::kFloat);
+  DIE_CHECK_DTYPE(ids, at::kInt);
+  check_rows(x, "x");
+  TORCH_CHECK(wg.dim() == 2 && wg.size(1) == x.size(1), "moe_route: wg [E, H]");
+  TORCH_CHECK(w.dim() == 2 && w.size(0) == x.size(0) && ids.sizes() == w.sizes(), "moe_route: w, ids [T, K]");
+  DIE_HIP(die::launch_moe_route(w.data_ptr<float>(), ids.data_ptr<int>(), bf(x), x.stride(0), bf(wg),
+                                (int)x.size(0), (int)x.size(1), (int)wg.size(0), (int)w.size(1), renorm,
+                                cur_stream()));
+}
+
 void moe_grouped_gemm(Tensor y, Tensor x, Tensor w, Tensor offsets) {
   DIE_CHECK_BF16(y);
   DIE_CHECK_BF16(x);
@@ -723,6 +742,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("row_sumsq", &row_sumsq);
   m.def("residual_add_sumsq", &residual_add_sumsq);
   m.def("decode_advance", &decode_advance);
+  m.def("moe_route", &moe_route);
   m.def("gemm_decode_grouped", &gemm_decode_grouped);
   m.def("fused_add_rms_norm_slab", &fused_add_rms_norm_slab);
   m.def("rope_and_cache_slab", &rope_and_cache_slab);

@@ -45,6 +45,95 @@ __global__ void topk_softmax_kernel(float* __restrict__ w_out, int* __restrict__
     for (int k = 0; k < K; ++k) w_out[(int64_t)t * K + k] /= wsum;
 }
 
+// Decode-sized routing in one launch: router logits x[t] . Wg[e] (fp32 accumulate, rounded to bf16
+// like the GEMM output they replace), softmax, top-K, renormalisation. One workgroup per token; each
+// thread owns 8-element slices of H for all E experts (Wg, E x H bf16, stays in L2 across tokens).
+// Replaces a hipBLASLt [T, H] x [E, H]^T launch (~10 us at T = 32, E = 8) plus topk_softmax_kernel.
+constexpr int ROUTE_MAX_E = 16;
+__global__ void __launch_bounds__(256) moe_route_kernel(float* __restrict__ w_out, int* __restrict__ id_out,
+                                                        const bf16_t* __restrict__ x, int64_t ldx,
+                                                        const bf16_t* __restrict__ wg, int H, int E, int K,
+                                                        int renorm) {
+  __shared__ float red[4][ROUTE_MAX_E];
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float acc[ROUTE_MAX_E];
+#pragma unroll
+  for (int e = 0; e < ROUTE_MAX_E; ++e) acc[e] = 0.f;
+  const bf16_t* xr = x + (int64_t)t * ldx;
+  for (int j = tid * 8; j < H; j += 256 * 8) {
+    const uint4 xv = *reinterpret_cast<const uint4*>(xr + j);
+    float xf[8];
+    const unsigned xw[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      xf[2 * i] = bf2f((bf16_t)(xw[i] & 0xffff));
+      xf[2 * i + 1] = bf2f((bf16_t)(xw[i] >> 16));
+    }
+#pragma unroll
+    for (int e = 0; e < ROUTE_MAX_E; ++e) {
+      if (e >= E) break;
+      const uint4 wv = *reinterpret_cast<const uint4*>(wg + (int64_t)e * H + j);
+      const unsigned ww[4] = {wv.x, wv.y, wv.z, wv.w};
+      float a = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a += xf[2 * i] * bf2f((bf16_t)(ww[i] & 0xffff)) + xf[2 * i + 1] * bf2f((bf16_t)(ww[i] >> 16));
+      acc[e] += a;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < ROUTE_MAX_E; ++e) {
+    if (e >= E) break;
+    float v = acc[e];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[wave][e] = v;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  float g[ROUTE_MAX_E];
+  float mx = -INFINITY;
+  for (int e = 0; e < E; ++e) {
+    g[e] = bf2f(f2bf(red[0][e] + red[1][e] + red[2][e] + red[3][e]));  // bf16 logits, as the GEMM path
+    mx = fmaxf(mx, g[e]);
+  }
+  float z = 0.f;
+  for (int e = 0; e < E; ++e) z += __expf(g[e] - mx);
+  unsigned taken = 0;
+  float wsum = 0.f;
+  float wk[ROUTE_MAX_E];
+  int ik[ROUTE_MAX_E];
+  for (int k = 0; k < K; ++k) {
+    int bi = -1;
+    float bv = -INFINITY;
+    for (int e = 0; e < E; ++e) {
+      if ((taken >> e) & 1u) continue;
+      if (g[e] > bv || bi < 0) {
+        bv = g[e];
+        bi = e;
+      }
+    }
+    taken |= 1u << bi;
+    wk[k] = __expf(bv - mx) / z;
+    ik[k] = bi;
+    wsum += wk[k];
+  }
+  for (int k = 0; k < K; ++k) {
+    w_out[(int64_t)t * K + k] = renorm ? wk[k] / wsum : wk[k];
+    id_out[(int64_t)t * K + k] = ik[k];
+  }
+}
+
+hipError_t launch_moe_route(float* w, int* ids, const bf16_t* x, int64_t ldx, const bf16_t* wg, int T, int H, int E,
+                            int K, bool renorm, hipStream_t s) {
+  if (T == 0) return hipSuccess;
+  if (E < 1 || E > ROUTE_MAX_E || K < 1 || K > E || H % 8 || ldx % 8 ||
+      (reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(wg) & 15))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(moe_route_kernel, dim3(T), dim3(256), 0, s, w, ids, x, ldx, wg, H, E, K, renorm ? 1 : 0);
+  return hipGetLastError();
+}
+
 // One workgroup of 1024 threads. offsets[E+1]; sorted[j] = flat (t*K+k) index; pos[flat] = j.
 __global__ void __launch_bounds__(1024) moe_align_kernel(int* __restrict__ offsets, int* __restrict__ sorted,
                                                          int* __restrict__ pos, const int* __restrict__ ids, int n,

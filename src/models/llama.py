@@ -341,8 +341,8 @@ class CausalLM:
         """This rank's partial FFN / MoE output (summed over the TP group by the caller)."""
         a = self.arch
         if a.is_moe:
-            gating = F.linear(x, lw.router)
-            return ops.moe_forward(x, lw.w13, lw.w2, gating, a.top_k, expert0=self.expert0 if self.ep else None)
+            w, ids = ops.moe_route(x, lw.router, a.top_k)  # one fused launch at decode sizes
+            return ops.moe_forward_routed(x, lw.w13, lw.w2, w, ids, expert0=self.expert0 if self.ep else None)
         return ops.linear(ops.linear_silu_mul(x, lw.gate_up), lw.down)
 
     def _forward_sp(self, residual_full: torch.Tensor, positions: torch.Tensor, meta: AttnMetadata,

@@ -434,6 +434,34 @@ def expert_parallel_local(w: torch.Tensor, ids: torch.Tensor, expert0: int, n_lo
     return torch.where(local, w, torch.zeros_like(w)), ids_l.to(ids.dtype)
 
 
+MOE_ROUTE_MAX_T = 256  # fused routing for decode-sized batches; larger ones: hipBLASLt gating GEMM
+
+
+def moe_route(x: torch.Tensor, router: torch.Tensor, k: int, renorm: bool = True):
+    """Routing weights and expert ids [T, k] from the activations and the router weights [E, H]: one
+    fused launch (logits rounded to bf16, softmax, top-k) for decode-sized GPU batches; otherwise
+    the router GEMM + :func:`topk_softmax`."""
+    t, e = x.shape[0], router.shape[0]
+    if x.is_cuda and t <= MOE_ROUTE_MAX_T and e <= 16 and x.shape[1] % 8 == 0 and x.stride(1) == 1 \
+            and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and router.is_contiguous() \
+            and router.data_ptr() % 16 == 0:
+        w = torch.empty(t, k, dtype=torch.float32, device=x.device)
+        ids = torch.empty(t, k, dtype=torch.int32, device=x.device)
+        _kern().moe_route(w, ids, x, router, renorm)
+        return w, ids
+    return topk_softmax(torch.nn.functional.linear(x, router), k, renorm)
+
+
+def moe_forward_routed(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, w: torch.Tensor, ids: torch.Tensor,
+                       expert0: Optional[int] = None) -> torch.Tensor:
+    """:func:`moe_forward` after routing (``w``, ``ids`` [T, k] over ALL routed experts)."""
+    e = w13.shape[0]
+    if expert0 is not None:
+        w, ids = expert_parallel_local(w, ids, expert0, e)
+        return moe_apply(x, w13, w2, w, ids, e + 1)
+    return moe_apply(x, w13, w2, w, ids, e)
+
+
 def moe_forward(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, gating: torch.Tensor, k: int,
                 renorm: bool = True, expert0: Optional[int] = None) -> torch.Tensor:
     """Fused-routing MoE FFN on the HIP kernels: route → align → gather →
@@ -441,12 +469,8 @@ def moe_forward(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, gating: to
     No host synchronisation (hipGraph-capturable). ``expert0``: expert parallelism — ``w13``/``w2``
     hold experts [expert0, expert0 + E_local) of the ``gating.shape[1]`` routed experts, and the
     output is this rank's partial sum (see :func:`expert_parallel_local`)."""
-    e = w13.shape[0]
     w, ids = topk_softmax(gating, k, renorm)
-    if expert0 is not None:
-        w, ids = expert_parallel_local(w, ids, expert0, e)
-        return moe_apply(x, w13, w2, w, ids, e + 1)  # + the null group of remote assignments
-    return moe_apply(x, w13, w2, w, ids, e)
+    return moe_forward_routed(x, w13, w2, w, ids, expert0)  # EP: + the null group of remote assignments
 
 
 def moe_apply(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, w: torch.Tensor, ids: torch.Tensor,

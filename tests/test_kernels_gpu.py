@@ -253,6 +253,25 @@ def test_moe(dev, t):
     close(ops.moe_forward(x, w13, w2, gating, k), ref.moe_forward(x, w13, w2, gating, k), atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("t,h,e,k", [(32, 4096, 8, 2), (48, 1024, 16, 4), (300, 512, 8, 2)])
+def test_moe_route_fused(dev, t, h, e, k):
+    """Fused decode routing (router GEMV + softmax + top-k in one launch; t = 300 takes the GEMM path)
+    against fp32 logits rounded to bf16 -> reference top-k softmax. Rows whose k-th and (k+1)-th
+    logits tie within bf16 rounding may legitimately pick either expert: there only the weights of
+    the shared picks are compared."""
+    x = torch.randn(t, h, device=dev, dtype=torch.bfloat16)
+    wg = torch.randn(e, h, device=dev, dtype=torch.bfloat16) / math.sqrt(h)
+    w, ids = ops.moe_route(x, wg, k)
+    logits = (x.float() @ wg.float().t()).to(torch.bfloat16).cpu()
+    wr, idr = ref.topk_softmax(logits, k)
+    srt = logits.float().sort(-1, descending=True).values
+    clear = (srt[:, k - 1] - srt[:, k]) > 2e-2 * srt[:, k - 1].abs().clamp(min=1.0)
+    got = ids.cpu().long()
+    assert torch.equal(got[clear].sort(-1).values, idr.long()[clear].sort(-1).values)
+    assert clear.float().mean() > 0.6  # near-ties are rare: most rows must be checked
+    close(w.cpu()[clear], wr[clear], atol=2e-3, rtol=2e-3)
+
+
 @pytest.mark.parametrize("t", [8, 32])
 @pytest.mark.parametrize("skew", [True, False])
 def test_moe_decode_grouped(dev, t, skew):
