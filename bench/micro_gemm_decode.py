@@ -212,10 +212,11 @@ def main_moe(m):
     w13s = [torch.randn(e, 2 * inter, h, device=dev, dtype=torch.bfloat16) / 64 for _ in range(2)]
     w2s = [torch.randn(e, h, inter, device=dev, dtype=torch.bfloat16) / 64 for _ in range(2)]
     kern = ops._kern()
+    none = torch.empty(0, dtype=torch.int32, device=dev)
     wr1 = ops._cfg_for(inter, h, 1)[0]
-    for nm, ws, fn in (("moe_w13", w13s, lambda w: kern.gemm_decode_grouped(a, xs, w, offsets, 1, wr1)),
+    for nm, ws, fn in (("moe_w13", w13s, lambda w: kern.gemm_decode_grouped(a, xs, w, offsets, 1, wr1, none, 1)),
                        ("moe_w2", w2s, lambda w: kern.gemm_decode_grouped(ys, a, w, offsets, 0,
-                                                                          ops._moe_down_wr(h, inter)))):
+                                                                          ops._moe_down_wr(h, inter), none, 1))):
         us = timeit(fn, ws)
         wbytes = ws[0].numel() * 2
         print(json.dumps({"shape": nm, "M": m, "rows_per_expert": (offsets[1:] - offsets[:-1]).tolist(),

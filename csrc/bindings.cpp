@@ -492,7 +492,8 @@ void mlp_decode(Tensor act, Tensor slab, Tensor x, Tensor w_gate_up, Tensor w_do
 // [offsets[e], offsets[e+1]), at most 32 of them — one decode step), w [E, rows, K] stacked
 // expert weights, y [R, N] bf16. mode 1: w[e] = [gate; up] -> silu(gate)*up (N = rows/2);
 // mode 0: plain. Experts with no rows stream no weights.
-void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t mode, int64_t wr) {
+void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t mode, int64_t wr, Tensor rows,
+                         int64_t k) {
   DIE_CHECK_CUDA(x);
   DIE_CHECK_BF16(x);
   DIE_CHECK_BF16(w);
@@ -506,7 +507,13 @@ void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t m
   const int64_t E = w.size(0), K = x.size(1);
   TORCH_CHECK(offsets.numel() >= E + 1, "offsets [E+1]");
   const int64_t N = mode == 1 ? w.size(1) / 2 : w.size(1);
-  TORCH_CHECK(y.size(0) == x.size(0) && y.size(1) == N, "y [R, N]");
+  const bool gather = rows.numel() > 0;  // x in token order, row j of the sorted order = rows[j] / k
+  if (gather) {
+    DIE_CHECK_DTYPE(rows, at::kInt);
+    DIE_CHECK_CONTIG(rows);
+    TORCH_CHECK(k >= 1 && rows.numel() == y.size(0) && x.size(0) * k == y.size(0), "grouped gather: rows [T*k]");
+  }
+  TORCH_CHECK((gather || y.size(0) == x.size(0)) && y.size(1) == N, "y [R, N]");
   TORCH_CHECK(wr == 32 || wr == 48 || wr == 64 || wr == 96 || wr == 112 || wr == 128, "wr");
   const int64_t kc = wr >= 96 ? 128 : 256;
   TORCH_CHECK(K % kc == 0 && N % (mode == 1 ? wr / 2 : wr) == 0, "tile shape");
@@ -514,10 +521,14 @@ void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t m
   fz.grp_off = offsets.data_ptr<int>();
   fz.grp_wstride = w.size(1) * K;
   fz.grp_n = (int)E;
+  if (gather) {
+    fz.grp_rows = rows.data_ptr<int>();
+    fz.grp_k = (int)k;
+  }
   // M = all rows: bounds every expert's rows (the kernel picks the 16-row activation image when <= 16)
-  TORCH_CHECK(x.size(0) >= 1, "grouped: at least one row");
+  TORCH_CHECK(y.size(0) >= 1, "grouped: at least one row");
   DIE_HIP(die::launch_gemm_decode(y.data_ptr(), y.stride(0), bf(x), x.stride(0), bf(w),
-                                  (int)std::min<int64_t>(x.size(0), 32), (int)N, (int)K, (int)mode, (int)wr, 1, true,
+                                  (int)std::min<int64_t>(y.size(0), 32), (int)N, (int)K, (int)mode, (int)wr, 1, true,
                                   fz, cur_stream()));
 }
 

@@ -90,15 +90,17 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
   constexpr int PX = XR / RPP / 4;             // activation pieces per wave per chunk
   static_assert((XR / RPP) % 4 == 0 && (XR == 16 || XR == 32), "activation pieces must split over 4 waves");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int r0 = 0;
   if (fz.grp_off != nullptr) {
     // grouped (MoE) form: blockIdx.z = expert; its rows of X/Y are [off[e], off[e+1]) of the
     // token-sorted activations, its weights W + e * grp_wstride. Unused experts cost nothing.
-    // (The launcher picks XR = 16 only when ALL experts together have <= 16 rows.)
+    // (The launcher picks XR = 16 only when ALL experts together have <= 16 rows.) With grp_rows the
+    // activation rows are gathered from the token order on the fly (no separate gather launch).
     const int e = blockIdx.z;
-    const int r0 = fz.grp_off[e];
+    r0 = fz.grp_off[e];
     M = min(fz.grp_off[e + 1] - r0, XR);
     if (M <= 0) return;
-    X += (int64_t)r0 * ldx;
+    if (fz.grp_rows == nullptr) X += (int64_t)r0 * ldx;
     W += (int64_t)e * fz.grp_wstride;
     Yv = reinterpret_cast<char*>(Yv) + (int64_t)r0 * ldy * (EPI == 2 || EPI == 3 ? 4 : 2);
   }
@@ -121,7 +123,8 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
       if (SILU && row >= NO) grow = N_out + n0 + (row - NO);
       base = W + (int64_t)grow * K;
     } else {
-      base = X + (int64_t)min(row - WR, M - 1) * ldx;
+      const int xr = min(row - WR, M - 1);
+      base = fz.grp_rows != nullptr ? X + (int64_t)(fz.grp_rows[r0 + xr] / fz.grp_k) * ldx : X + (int64_t)xr * ldx;
     }
     src[p] = base + k0 + lch * 8;
     isw[p] = row < WR;

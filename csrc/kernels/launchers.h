@@ -80,6 +80,8 @@ struct GemmDecodeFuse {
   const int* grp_off = nullptr;  // grouped (MoE) form: expert row offsets [grp_n + 1] (device)
   int64_t grp_wstride = 0;       //   elements between experts' weight matrices
   int grp_n = 1;                 //   number of experts (grid z)
+  const int* grp_rows = nullptr; //   optional gather: X row j of the sorted order is token grp_rows[j] / grp_k
+  int grp_k = 1;                 //   (X is then the un-permuted [T, K] activations; Y stays in sorted order)
 };
 hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,
                               int K, int mode, int wr, int sk, bool nt, const GemmDecodeFuse& fz, hipStream_t s);

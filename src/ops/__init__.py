@@ -488,17 +488,21 @@ def moe_apply(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, w: torch.Ten
     ids = ids.to(torch.int32).contiguous()
     w = w.float().contiguous()
     offsets, sorted_idx, pos = moe_align(ids, groups)
-    xs = torch.empty(t * k, hdim, dtype=x.dtype, device=x.device)
-    kern.moe_gather(xs, x, sorted_idx, k)
     # rows of the extra groups are never computed: zero them so that weight 0 x row stays 0
     ys = (torch.zeros if groups > e else torch.empty)(t * k, hdim, dtype=x.dtype, device=x.device)
-    if t <= DECODE_GEMM_MAX_M and _moe_decode_ok(hdim, inter):
+    if t <= DECODE_GEMM_MAX_M and _moe_decode_ok(hdim, inter) and x.is_contiguous():
         # decode: every expert's weights streamed once by the weight-streaming kernel, its
-        # (<= 32) routed tokens riding along; SiLU*mul fused; idle experts read nothing
+        # (<= 32) routed tokens riding along, gathered from x by the kernel itself through the
+        # sorted order; SiLU*mul fused; idle experts read nothing
         a = torch.empty(t * k, inter, dtype=x.dtype, device=x.device)
-        kern.gemm_decode_grouped(a, xs, w13, offsets, 1, _cfg_for(inter, hdim, 1)[0])
-        kern.gemm_decode_grouped(ys, a, w2, offsets, 0, _moe_down_wr(hdim, inter))
-    elif t >= MOE_LIBRARY_MIN_TOKENS and not torch.cuda.is_current_stream_capturing():
+        kern.gemm_decode_grouped(a, x, w13, offsets, 1, _cfg_for(inter, hdim, 1)[0], sorted_idx, k)
+        kern.gemm_decode_grouped(ys, a, w2, offsets, 0, _moe_down_wr(hdim, inter), _NO_ROWS(x.device), 1)
+        out = torch.empty_like(x)
+        kern.moe_combine(out, ys, pos, w)
+        return out
+    xs = torch.empty(t * k, hdim, dtype=x.dtype, device=x.device)
+    kern.moe_gather(xs, x, sorted_idx, k)
+    if t >= MOE_LIBRARY_MIN_TOKENS and not torch.cuda.is_current_stream_capturing():
         # prefill: the per-expert groups are thousands of rows — hipBLASLt GEMMs per expert at
         # ~1.5 PF/s beat the device-offset grouped kernel; costs one host read of the offsets
         off = offsets.tolist()
@@ -518,6 +522,15 @@ def moe_apply(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, w: torch.Ten
 
 
 MOE_LIBRARY_MIN_TOKENS = 256
+_NO_ROWS_CACHE: dict = {}
+
+
+def _NO_ROWS(device) -> torch.Tensor:
+    """Empty int32 tensor: 'no gather' for gemm_decode_grouped (cached per device, graph-safe)."""
+    t = _NO_ROWS_CACHE.get(device)
+    if t is None:
+        t = _NO_ROWS_CACHE[device] = torch.empty(0, dtype=torch.int32, device=device)
+    return t
 
 
 def _moe_decode_ok(hdim: int, inter: int) -> bool:
