@@ -198,15 +198,16 @@ class CausalLM:
         ln2, and the norm weights become ones. Mathematically a no-op (rmsnorm(x) * g @ W^T ==
         rmsnorm(x) @ (W * g)^T); it lets the decode fast path apply the norm as a per-row
         scale inside the GEMM / attention kernels (no norm kernels in the decode layer).
-        Mixtral keeps its norms (the router also consumes the normalised activations)."""
-        if self.arch.is_moe:
-            return
+        Mixtral folds only ln1 (its ln2 output also feeds the router, so the MoE block keeps an
+        explicit RMSNorm)."""
         for i, lw in enumerate(self.layers):
             if layers is not None and i not in layers:
                 continue
             if not bool((lw.ln1 == 1).all()):
                 lw.qkv.mul_(lw.ln1.to(lw.qkv.dtype)[None, :])
                 lw.ln1.fill_(1)
+            if self.arch.is_moe:
+                continue
             if not bool((lw.ln2 == 1).all()):
                 lw.gate_up.mul_(lw.ln2.to(lw.gate_up.dtype)[None, :])
                 lw.ln2.fill_(1)
@@ -308,7 +309,7 @@ class CausalLM:
         if self._slab_path(input_ids):
             if meta.scratch is not None and not meta.is_prefill and self._fused_decode_ok(kv_pool):
                 return self._forward_decode_fused(residual, positions, meta, kv_pool)
-            if not self.tp.enabled:
+            if not self.tp.enabled and not self.arch.is_moe:  # the slab fallback is dense-only
                 return self._forward_decode_slab(residual, positions, meta, kv_pool)
         if self.sequence_parallel and meta.is_prefill:
             return self._forward_sp(residual, positions, meta, kv_pool)
@@ -375,7 +376,7 @@ class CausalLM:
         """Decode-sized steps on the GPU run every projection on the weight-streaming kernel
         (split-K fp32 slabs reduced inside the consumer kernels; no separate reduction or SiLU
         launches). The slab fallback is TP=1 only; the fused path also serves TP."""
-        if not (input_ids.is_cuda and ops.native_available()) or self.arch.is_moe:
+        if not (input_ids.is_cuda and ops.native_available()):
             return False
         m, h = input_ids.shape[0], self.arch.hidden_size
         return (1 <= m <= ops.DECODE_GEMM_MAX_M and h % 256 == 0 and self.inter % 256 == 0
@@ -432,13 +433,13 @@ class CausalLM:
         return plan
 
     def alloc_decode_scratch(self) -> Optional[dict]:
-        if not (self.device.type == "cuda" and ops.native_available()) or self.arch.is_moe:
+        if not (self.device.type == "cuda" and ops.native_available()):
             return None
         p, h = self.decode_plan(), self.arch.hidden_size
         f32, i32 = torch.float32, torch.int32
         # TP: the row-parallel projections are all-reduced first, then one kernel adds into the
-        # residual and writes a single statistics tile
-        to, td = (1, 1) if self.tp.enabled else (h // p["o"][0], h // p["down"][0])
+        # residual and writes a single statistics tile (so does the MoE block's residual add)
+        to, td = (1, 1) if self.tp.enabled else (h // p["o"][0], 1 if self.arch.is_moe else h // p["down"][0])
         if max(to, td) > 128:
             return None
         dev = self.device
@@ -473,8 +474,18 @@ class CausalLM:
             attn = ops.attn_decode_fused(slab, ssp_prev, positions, self.cos_sin, meta.slot_mapping,
                                          k_cache, v_cache, meta.block_tables, meta.ctx_lens, meta.max_ctx, hq, hkv,
                                          self.scale, eps, hid, meta.part_o, meta.part_ml, meta.attn_cnt)
-            if self.tp.enabled:  # row-parallel partial sums -> all-reduce -> residual + statistics (one launch
-                # on the one-shot IPC path, see TPContext.all_reduce_residual)
+            if a.is_moe:  # ln2 stays explicit (it also feeds the router); MoE output added back + statistics
+                if self.tp.enabled:
+                    self.tp.all_reduce_residual(ops.linear(attn, lw.o), h, sc["ssp_a"])
+                else:
+                    ops.linear_slab_residual(attn, lw.o, h, sc["ssp_a"], sc["cnt_a"], *plan["o"])
+                y = self._mlp(lw, ops.rms_norm(h, lw.ln2, eps))
+                if self.tp.enabled:
+                    self.tp.all_reduce_residual(y, h, sc["ssp_b"])
+                else:
+                    ops.residual_add_sumsq(h, y, sc["ssp_b"])
+            elif self.tp.enabled:  # row-parallel partial sums -> all-reduce -> residual + statistics (one
+                # launch on the one-shot IPC path, see TPContext.all_reduce_residual)
                 self.tp.all_reduce_residual(ops.linear(attn, lw.o), h, sc["ssp_a"])
                 act = ops.linear_silu_mul_rownorm(h, lw.gate_up, sc["ssp_a"], eps)
                 self.tp.all_reduce_residual(ops.linear(act, lw.down), h, sc["ssp_b"])
