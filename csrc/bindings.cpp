@@ -344,6 +344,27 @@ void moe_route(Tensor w, Tensor ids, Tensor x, Tensor wg, bool renorm) {
                                 cur_stream()));
 }
 
+// resid [T, H] += combine(ys, pos, w); ssp [>= T] fp32 = row sums of squares of the new residual.
+void moe_combine_residual(Tensor ssp, Tensor resid, Tensor ys, Tensor pos, Tensor w) {
+  DIE_CHECK_CUDA(resid);
+  DIE_CHECK_BF16(resid);
+  DIE_CHECK_BF16(ys);
+  DIE_CHECK_CONTIG(ys);
+  DIE_CHECK_CONTIG(pos);
+  DIE_CHECK_CONTIG(w);
+  DIE_CHECK_CONTIG(ssp);
+  DIE_CHECK_DTYPE(ssp, at::kFloat);
+  DIE_CHECK_DTYPE(pos, at::kInt);
+  DIE_CHECK_DTYPE(w, at::kFloat);
+  check_rows(resid, "resid");
+  const int64_t T = resid.size(0), H = resid.size(1), K = w.size(1);
+  TORCH_CHECK(w.size(0) == T && pos.numel() == T * K && ys.size(0) == T * K && ys.size(1) == H && ssp.numel() >= T,
+              "moe_combine_residual shapes");
+  DIE_HIP(die::launch_moe_combine_residual(ssp.data_ptr<float>(), bf(resid), resid.stride(0), bf(ys),
+                                           pos.data_ptr<int>(), w.data_ptr<float>(), (int)T, (int)K, (int)H,
+                                           cur_stream()));
+}
+
 void moe_grouped_gemm(Tensor y, Tensor x, Tensor w, Tensor offsets) {
   DIE_CHECK_BF16(y);
   DIE_CHECK_BF16(x);
@@ -754,6 +775,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("residual_add_sumsq", &residual_add_sumsq);
   m.def("decode_advance", &decode_advance);
   m.def("moe_route", &moe_route);
+  m.def("moe_combine_residual", &moe_combine_residual);
   m.def("gemm_decode_grouped", &gemm_decode_grouped);
   m.def("fused_add_rms_norm_slab", &fused_add_rms_norm_slab);
   m.def("rope_and_cache_slab", &rope_and_cache_slab);

@@ -54,6 +54,8 @@ hipError_t launch_topk_softmax(float* w, int* ids, const bf16_t* gating, int T, 
                                hipStream_t s);
 hipError_t launch_moe_route(float* w, int* ids, const bf16_t* x, int64_t ldx, const bf16_t* wg, int T, int H, int E,
                             int K, bool renorm, hipStream_t s);
+hipError_t launch_moe_combine_residual(float* ssp, bf16_t* resid, int64_t rstride, const bf16_t* ys, const int* pos,
+                                       const float* w, int T, int K, int H, hipStream_t s);
 hipError_t launch_moe_align(int* offsets, int* sorted, int* pos, const int* ids, int n, int E, hipStream_t s);
 hipError_t launch_moe_gather(bf16_t* xs, const bf16_t* x, const int* sorted, int n, int K, int H, hipStream_t s);
 hipError_t launch_moe_combine(bf16_t* out, const bf16_t* ys, const int* pos, const float* w, int T, int K, int H,

@@ -187,6 +187,48 @@ __global__ void __launch_bounds__(256) moe_combine_kernel(bf16_t* __restrict__ o
   }
 }
 
+// Decode epilogue of a MoE layer in one launch: resid[t] += sum_k w[t,k] * ys[pos[t*K+k]] (fp32 sum, one
+// bf16 rounding) and ssp[t] = sum of squares of the new (rounded) residual row — the next layer's norm
+// statistics. Replaces moe_combine + residual_add_sumsq (one launch and one bf16 round trip fewer).
+__global__ void __launch_bounds__(256) moe_combine_residual_kernel(float* __restrict__ ssp, bf16_t* __restrict__ resid,
+                                                                   int64_t rstride, const bf16_t* __restrict__ ys,
+                                                                   const int* __restrict__ pos,
+                                                                   const float* __restrict__ w, int K, int H) {
+  __shared__ float red[4];
+  const int t = blockIdx.x;
+  uint4* r = reinterpret_cast<uint4*>(resid + (int64_t)t * rstride);
+  float ss = 0.f;
+  for (int c = threadIdx.x; c < H / 8; c += blockDim.x) {
+    float acc[8];
+    unpack8(r[c], acc);
+    for (int k = 0; k < K; ++k) {
+      const float wk = w[(int64_t)t * K + k];
+      float y[8];
+      unpack8(reinterpret_cast<const uint4*>(ys + (int64_t)pos[t * K + k] * H)[c], y);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += wk * y[q];
+    }
+    const uint4 p = pack8(acc);
+    r[c] = p;
+    unpack8(p, acc);  // statistics of the rounded residual, as the next norm sees it
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ss += acc[q] * acc[q];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  if (threadIdx.x == 0) ssp[t] = red[0] + red[1] + red[2] + red[3];
+}
+
+hipError_t launch_moe_combine_residual(float* ssp, bf16_t* resid, int64_t rstride, const bf16_t* ys, const int* pos,
+                                       const float* w, int T, int K, int H, hipStream_t s) {
+  if (T == 0) return hipSuccess;
+  if (H % 8 || T > 32 || rstride % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(moe_combine_residual_kernel, dim3(T), dim3(256), 0, s, ssp, resid, rstride, ys, pos, w, K, H);
+  return hipGetLastError();
+}
+
 // Grouped GEMM: for expert e, rows [off[e], off[e+1]) of X (M x K) times W[e] (N x K, row-major, i.e. y = x W^T).
 // Tile 64 x 64 per workgroup (4 waves, each a 32x32 quadrant), K step 32, LDS staged with a padded pitch.
 // grid = (N/64, ceil(total_rows/64) + E): blockIdx.y enumerates the 64-row tiles of all experts

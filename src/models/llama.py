@@ -479,11 +479,12 @@ class CausalLM:
                     self.tp.all_reduce_residual(ops.linear(attn, lw.o), h, sc["ssp_a"])
                 else:
                     ops.linear_slab_residual(attn, lw.o, h, sc["ssp_a"], sc["cnt_a"], *plan["o"])
-                y = self._mlp(lw, ops.rms_norm(h, lw.ln2, eps))
+                x = ops.rms_norm(h, lw.ln2, eps)
                 if self.tp.enabled:
-                    self.tp.all_reduce_residual(y, h, sc["ssp_b"])
-                else:
-                    ops.residual_add_sumsq(h, y, sc["ssp_b"])
+                    self.tp.all_reduce_residual(self._mlp(lw, x), h, sc["ssp_b"])
+                else:  # combine + residual add + statistics in one launch
+                    wr_, ids_ = ops.moe_route(x, lw.router, a.top_k)
+                    ops.moe_forward_routed(x, lw.w13, lw.w2, wr_, ids_, residual=h, ssp=sc["ssp_b"])
             elif self.tp.enabled:  # row-parallel partial sums -> all-reduce -> residual + statistics (one
                 # launch on the one-shot IPC path, see TPContext.all_reduce_residual)
                 self.tp.all_reduce_residual(ops.linear(attn, lw.o), h, sc["ssp_a"])

@@ -453,13 +453,15 @@ def moe_route(x: torch.Tensor, router: torch.Tensor, k: int, renorm: bool = True
 
 
 def moe_forward_routed(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, w: torch.Tensor, ids: torch.Tensor,
-                       expert0: Optional[int] = None) -> torch.Tensor:
-    """:func:`moe_forward` after routing (``w``, ``ids`` [T, k] over ALL routed experts)."""
+                       expert0: Optional[int] = None, residual: Optional[torch.Tensor] = None,
+                       ssp: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """:func:`moe_forward` after routing (``w``, ``ids`` [T, k] over ALL routed experts). With
+    ``residual``/``ssp``: residual += output and ssp[0, :T] = its row sums of squares (returns residual)."""
     e = w13.shape[0]
     if expert0 is not None:
         w, ids = expert_parallel_local(w, ids, expert0, e)
-        return moe_apply(x, w13, w2, w, ids, e + 1)
-    return moe_apply(x, w13, w2, w, ids, e)
+        return moe_apply(x, w13, w2, w, ids, e + 1, residual, ssp)
+    return moe_apply(x, w13, w2, w, ids, e, residual, ssp)
 
 
 def moe_forward(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, gating: torch.Tensor, k: int,
@@ -474,11 +476,13 @@ def moe_forward(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, gating: to
 
 
 def moe_apply(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, w: torch.Tensor, ids: torch.Tensor,
-              groups: int) -> torch.Tensor:
+              groups: int, residual: Optional[torch.Tensor] = None, ssp: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out[t] = sum_j w[t, j] * expert_{ids[t, j]}(x[t]) for given routing (w [T, k] fp32, ids [T, k]
     int32). ``groups`` may exceed the number of local experts ``w13.shape[0]``: assignments to those
     extra groups are not computed (their weight must be 0)."""
     e = w13.shape[0]
+    if residual is not None and not (x.is_cuda and x.shape[0] <= DECODE_GEMM_MAX_M):
+        return residual_add_sumsq(residual, moe_apply(x, w13, w2, w, ids, groups), ssp)
     if not x.is_cuda:
         return ref.moe_experts(x, w13, w2, w, ids)
     kern = _kern()
@@ -497,6 +501,9 @@ def moe_apply(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, w: torch.Ten
         a = torch.empty(t * k, inter, dtype=x.dtype, device=x.device)
         kern.gemm_decode_grouped(a, x, w13, offsets, 1, _cfg_for(inter, hdim, 1)[0], sorted_idx, k)
         kern.gemm_decode_grouped(ys, a, w2, offsets, 0, _moe_down_wr(hdim, inter), _NO_ROWS(x.device), 1)
+        if residual is not None:  # combine + residual add + next-norm statistics in one launch
+            kern.moe_combine_residual(ssp, residual, ys, pos, w)
+            return residual
         out = torch.empty_like(x)
         kern.moe_combine(out, ys, pos, w)
         return out
@@ -518,6 +525,8 @@ def moe_apply(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, w: torch.Ten
         kern.moe_grouped_gemm(ys, a, w2, offsets)
     out = torch.empty_like(x)
     kern.moe_combine(out, ys, pos, w)
+    if residual is not None:
+        return residual_add_sumsq(residual, out, ssp)
     return out
 
 

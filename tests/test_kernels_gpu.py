@@ -287,7 +287,14 @@ def test_moe_decode_grouped(dev, t, skew):
     else:
         ids = torch.stack([torch.randperm(e, device=dev)[:k] for _ in range(t)]).to(torch.int32)
     w = torch.softmax(torch.randn(t, k, device=dev), -1)
-    close(ops.moe_apply(x, w13, w2, w, ids, e), ref.moe_experts(x, w13, w2, w, ids), atol=3e-2, rtol=3e-2)
+    want = ref.moe_experts(x, w13, w2, w, ids)
+    close(ops.moe_apply(x, w13, w2, w, ids, e), want, atol=3e-2, rtol=3e-2)
+    # decode epilogue form: residual += output, row statistics of the new residual (one launch)
+    h0 = torch.randn(t, h, device=dev, dtype=torch.bfloat16)
+    hres, ssp = h0.clone(), torch.zeros(1, 32, device=dev)
+    ops.moe_apply(x, w13, w2, w, ids, e, residual=hres, ssp=ssp)
+    close(hres, h0.float() + want.float(), atol=5e-2, rtol=3e-2)
+    close(ssp[0, :t], hres.float().pow(2).sum(-1), atol=1e-2, rtol=1e-3)
 
 
 @pytest.mark.parametrize("m,n,k", [(1, 4096, 4096), (7, 6144, 4096), (32, 4096, 14336), (32, 1024, 256),
