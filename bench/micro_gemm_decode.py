@@ -61,6 +61,8 @@ def main():
         return main_deep(m)
     if len(sys.argv) > 2 and sys.argv[2] == "moe":
         return main_moe(m)
+    if len(sys.argv) > 2 and sys.argv[2] == "chain":
+        return main_chain(m)
     dev = torch.device("cuda:0")
     for name, (n, k, silu) in SHAPES.items():
         wrows = 2 * n if silu else n
@@ -221,6 +223,30 @@ def main_moe(m):
         wbytes = ws[0].numel() * 2
         print(json.dumps({"shape": nm, "M": m, "rows_per_expert": (offsets[1:] - offsets[:-1]).tolist(),
                           "xr16": xr16, "us": round(us, 2), "GBps": round(wbytes / us / 1e3, 1)}), flush=True)
+
+
+def main_chain(m):
+    """What one launch streaming n gate/up-sized weight sets back to back (grouped kernel, every expert
+    gets all m rows) buys over n dense launches: the per-launch fill/drain/straggler cost that a
+    persistent decode layer would remove. Cold weights (8 copies cycled)."""
+    dev = torch.device("cuda:0")
+    kern = ops._kern()
+    h, inter = 4096, 14336
+    wr = ops._cfg_for(inter, h, 1)[0]
+    x = torch.randn(m, h, device=dev, dtype=torch.bfloat16)
+    none = torch.empty(0, dtype=torch.int32, device=dev)
+    for n in (1, 2, 4):
+        ws = [torch.randn(n, 2 * inter, h, device=dev, dtype=torch.bfloat16) / 64 for _ in range(max(2, 8 // n))]
+        xs = x.repeat(n, 1).contiguous()
+        a = torch.empty(n * m, inter, device=dev, dtype=torch.bfloat16)
+        offsets = torch.arange(0, (n + 1) * m, m, dtype=torch.int32, device=dev)
+        one = timeit(lambda w: kern.gemm_decode_grouped(a, xs, w, offsets, 1, wr, none, 1), ws)
+        sep = timeit(lambda w: [ops.gemm_decode(x, w[i], 1, wr, 1) for i in range(n)], ws)
+        wbytes = n * 2 * inter * h * 2
+        print(json.dumps({"bench": "chain", "M": m, "n_weight_sets": n, "one_launch_us": round(one, 2),
+                          "separate_launches_us": round(sep, 2), "one_launch_TBps": round(wbytes / one / 1e6, 2),
+                          "separate_TBps": round(wbytes / sep / 1e6, 2)}), flush=True)
+        del ws
 
 if __name__ == "__main__":
     main()
