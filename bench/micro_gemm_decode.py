@@ -235,7 +235,7 @@ def main_chain(m):
     wr = ops._cfg_for(inter, h, 1)[0]
     x = torch.randn(m, h, device=dev, dtype=torch.bfloat16)
     none = torch.empty(0, dtype=torch.int32, device=dev)
-    for n in (1, 2, 4):
+    for n in (1, 2, 4, 8):
         ws = [torch.randn(n, 2 * inter, h, device=dev, dtype=torch.bfloat16) / 64 for _ in range(max(2, 8 // n))]
         xs = x.repeat(n, 1).contiguous()
         a = torch.empty(n * m, inter, device=dev, dtype=torch.bfloat16)
