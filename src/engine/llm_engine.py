@@ -231,6 +231,11 @@ class LLMEngine:
         from src.parallel.kv_transfer import export_blocks, import_blocks
 
         planes = self.pool.planes()
+        # swap-ins first: a sequence resumed and (as a last resort) preempted again in the same step
+        # must have its host KV scattered back before the swap-out gathers those blocks
+        for seq, ids in out.swap_in:
+            import_blocks(planes, ids, seq.swap_buf)
+            seq.swap_buf = None
         for seq, ids in out.swap_out:
             buf = export_blocks(planes, ids)
             if buf.is_cuda:
@@ -239,9 +244,6 @@ class LLMEngine:
                 buf = host
             seq.swap_buf = buf
             self.stats["swap_out_bytes"] = self.stats.get("swap_out_bytes", 0) + buf.numel() * buf.element_size()
-        for seq, ids in out.swap_in:
-            import_blocks(planes, ids, seq.swap_buf)
-            seq.swap_buf = None
 
     def _decode_window(self, seqs: List[Sequence]) -> int:
         """How many decode steps to run before the host looks again: 1 while requests wait for

@@ -127,6 +127,7 @@ class Scheduler:
         now = time.perf_counter() if now is None else now
         out = SchedulerOutput()
         budget = self.cfg.max_num_batched_tokens
+        self._resumed_now = set()
         # 0) resume swapped-out sequences first (FIFO); while one is still parked, admit nothing new
         while self.swapped and len(self.running) < self.cfg.max_num_seqs:
             seq = self.swapped[0]
@@ -140,6 +141,7 @@ class Scheduler:
             self.num_swaps_in += 1
             seq.status = SeqStatus.RUNNING
             self.running.append(seq)
+            self._resumed_now.add(id(seq))
         blocked = bool(self.swapped)
         # 1) continue chunked prefills already running
         for seq in self.running:
@@ -202,8 +204,14 @@ class Scheduler:
         return out
 
     def _pick_victim(self, exclude: Sequence) -> Optional[Sequence]:
+        """Newest arrival first, but a sequence swapped back in during THIS step goes last: its KV
+        is only scattered into its fresh blocks by this step's swap-in, so swapping it straight
+        out again would gather uninitialised blocks (scheduler/_run_swaps)."""
         cands = [s for s in self.running if s is not exclude and s.status == SeqStatus.RUNNING]
-        return max(cands, key=lambda s: s.arrival) if cands else None
+        if not cands:
+            return None
+        resumed = getattr(self, "_resumed_now", set())
+        return max(cands, key=lambda s: (id(s) not in resumed, s.arrival))
 
     def _swap_ok(self, seq: Sequence) -> bool:
         mode = self.cfg.preemption_mode
@@ -236,6 +244,7 @@ class Scheduler:
             return
         self.blocks.free(seq)
         seq.num_computed = 0
+        seq.imported_kv = False  # the recompute re-prefills locally (prefix matching applies again)
         seq.status = SeqStatus.WAITING
         # the generated tokens become part of the prompt for the recompute
         seq.prompt_ids = seq.prompt_ids + seq.output_ids

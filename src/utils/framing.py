@@ -123,7 +123,11 @@ async def read_message(reader: asyncio.StreamReader, allow_pickle: bool = False)
     first = await reader.read(1)
     if not first:
         return None, "eof", b""
-    if first == b"{" or first in b" \t\r\n":
+    # Only '{' marks a legacy request: the reference client always sends json.dumps(dict). Whitespace
+    # bytes are NOT accepted as a legacy start because 0x09/0x0A/0x0D/0x20 are valid high bytes of a
+    # frame length (144-176 MiB, 208-224 MiB, 512-528 MiB: e.g. a 4K-token Llama-3-8B kv_import).
+    # 0x7B << 24 exceeds MAX_FRAME, so '{' can never start a valid frame header.
+    if first == b"{":
         return await read_legacy_json(reader, first), "legacy", CODEC_JSON
     rest = await reader.readexactly(3)
     (n,) = _HDR.unpack(first + rest)

@@ -50,6 +50,34 @@ def test_framing_roundtrip():
     assert pack_frame(obj)[:4] == len(serialize(obj)).to_bytes(4, "big")
 
 
+def test_read_message_large_frame_lengths_are_not_legacy():
+    """Frame lengths whose high byte is 0x09/0x0A/0x0D/0x20 (144-528 MiB, e.g. a 4K-token
+    kv_import) must be parsed as frames, never as legacy JSON (framing.py:126)."""
+    from src.utils.framing import read_message
+
+    async def main():
+        for n in (0x20000000, 0x09000000, 0x0A000010, 0x0D000000):
+            r = asyncio.StreamReader()
+            # header only + EOF: a framed parse must try to read n bytes and fail with
+            # IncompleteReadError; the old legacy path returned/raised JSON errors instead
+            r.feed_data(n.to_bytes(4, "big") + b"J{}")
+            r.feed_eof()
+            with pytest.raises(asyncio.IncompleteReadError):
+                await read_message(r)
+        r = asyncio.StreamReader()
+        r.feed_data(b'{"model": "echo"}')
+        r.feed_eof()
+        obj, mode, _ = await read_message(r)
+        assert mode == "legacy" and obj == {"model": "echo"}
+        r = asyncio.StreamReader()
+        r.feed_data(pack_frame({"op": "health"}))
+        r.feed_eof()
+        obj, mode, _ = await read_message(r)
+        assert mode == "framed" and obj == {"op": "health"}
+
+    asyncio.run(main())
+
+
 def test_in_process_worker_api():
     async def main():
         w = Worker("w", host="127.0.0.1", install_signal_handlers=False)

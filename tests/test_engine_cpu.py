@@ -79,6 +79,42 @@ def test_swap_preemption_under_kv_pressure(mode):
         assert o == greedy_reference(eng.model, p, 30)
 
 
+@pytest.mark.parametrize("blocks,n,plen", [(6, 4, 16), (7, 5, 16), (14, 8, 32), (19, 8, 48)])
+def test_swap_in_and_lockstep_block_crossing(blocks, n, plen):
+    """Lockstep sequences (equal prompt lengths) all need a new KV block in the same step as a
+    swapped sequence resumes: the resumed sequence must not be re-swapped with its
+    fresh, unfilled blocks, and no KV may be lost — tokens equal the no-cache reference."""
+    # (configurations found to crash the round-1 scheduler with AttributeError on swap_buf = None)
+    eng = make_engine(blocks=blocks, max_num_seqs=n, budget=512, prefix=False, preemption="swap", swap_min=0)
+    r = random.Random(1)
+    ps = [[r.randrange(3, 1000) for _ in range(plen)] for _ in range(n)]  # lockstep
+    outs = eng.generate(ps, SamplingParams(max_tokens=40))
+    st = eng.get_stats()
+    assert st["swaps_out"] > 0 and st["swaps_in"] == st["swaps_out"]
+    assert st["kv"]["used"] == 0 and eng.scheduler.swap_used == 0
+    for p, o in zip(ps, outs):
+        assert o == greedy_reference(eng.model, p, 40)
+
+
+def test_resumed_sequence_is_last_resort_victim():
+    from src.engine.sequence import Sequence, SeqStatus
+    from src.preproc import SamplingParams as SP
+
+    eng = make_engine(blocks=16, max_num_seqs=4)
+    sch = eng.scheduler
+    a = Sequence("a", [1, 2, 3], SP(max_tokens=4))
+    b = Sequence("b", [1, 2, 3], SP(max_tokens=4))
+    a.arrival, b.arrival = 1.0, 2.0
+    for q in (a, b):
+        q.status = SeqStatus.RUNNING
+        sch.running.append(q)
+    sch._resumed_now = {id(b)}           # b (newest) was swapped back in this step
+    c = Sequence("c", [1], SP(max_tokens=1))
+    assert sch._pick_victim(exclude=c) is a
+    sch._resumed_now = set()
+    assert sch._pick_victim(exclude=c) is b
+
+
 def test_swap_abort_releases_swap_space():
     eng = make_engine(blocks=12, max_num_seqs=4, budget=256, prefix=False, preemption="swap")
     for i, p in enumerate(prompts(4, seed=3)):
