@@ -391,6 +391,13 @@ void moe_grouped_gemm(Tensor y, Tensor x, Tensor w, Tensor offsets) {
 // (tickets `counters` [N/wr], zeroed once), 4 = mode 1 with rows scaled by the RMSNorm
 // statistics `ssp_in` [T, 32] (eps; the norm weight is folded into w). Unused fusion tensors
 // may be empty.
+// Diagnostics: when set (non-empty int64 tensor [>= 3 * workgroups]), every decode-GEMM launch writes
+// per-workgroup [start, end, xcc] s_memrealtime stamps (100 MHz) there (bench/micro_gd_timeline.py).
+static long long* g_gd_ts = nullptr;
+void gd_set_timestamps(Tensor t) {
+  g_gd_ts = t.numel() ? reinterpret_cast<long long*>(t.data_ptr<int64_t>()) : nullptr;
+}
+
 void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t sk, bool nt, Tensor resid,
                  Tensor ssp_out, Tensor counters, Tensor ssp_in, double eps) {
   DIE_CHECK_CUDA(x);
@@ -398,6 +405,8 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
   DIE_CHECK_BF16(w);
   DIE_CHECK_CONTIG(w);
   check_rows(x, "x");
+  const bool tiled = (mode & 32) != 0;  // w pre-packed by ops.gd_pack_weights for this (mode, wr)
+  mode &= 31;
   const int64_t M = x.size(0), K = x.size(1);
   TORCH_CHECK(M >= 1 && M <= 32, "gemm_decode: 1 <= M <= 32");
   TORCH_CHECK(wr == 32 || wr == 48 || wr == 64 || wr == 96 || wr == 112 || wr == 128 || wr == 33 || wr == 49 ||
@@ -426,6 +435,8 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
   TORCH_CHECK(N % (silu ? wrr / 2 : wrr) == 0, "N not a multiple of the column tile");
   TORCH_CHECK((int64_t)sk * M * N * 4 < ((int64_t)1 << 31) || mode != 3, "slab too large");
   die::GemmDecodeFuse fz;
+  fz.ts = g_gd_ts;
+  fz.tiled = tiled ? 1 : 0;
   if (mode == 3) {
     TORCH_CHECK(wrr == 32 || wrr == 64 || wrr == 128, "mode 3: wr in {32, 64, 128}");
     DIE_CHECK_BF16(resid);
@@ -457,57 +468,6 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
                                   (int)wr, (int)sk, nt, fz, cur_stream()));
 }
 
-// Persistent decode MLP: resid += down(silu(r * x Wg^T) * (r * x Wu^T)) with the norm row scale r from
-// ssp_in, in one launch (see gemm_decode.hip mlp_decode_kernel). act [M, I] bf16 and slab [4, M, H] fp32
-// are scratch; counters [H / 64] and flags [8] int32 zeroed once (re-armed by the kernel); err [1] int32
-// is set to 1 if a hand-off wait gave up (never expected).
-void mlp_decode(Tensor act, Tensor slab, Tensor x, Tensor w_gate_up, Tensor w_down, Tensor ssp_in, Tensor resid,
-                Tensor ssp_out, Tensor counters, Tensor flags, Tensor err, double eps, bool nt, int64_t xmode) {
-  DIE_CHECK_CUDA(x);
-  DIE_CHECK_BF16(x);
-  DIE_CHECK_BF16(w_gate_up);
-  DIE_CHECK_BF16(w_down);
-  DIE_CHECK_CONTIG(w_gate_up);
-  DIE_CHECK_CONTIG(w_down);
-  DIE_CHECK_BF16(act);
-  DIE_CHECK_CONTIG(act);
-  DIE_CHECK_DTYPE(slab, at::kFloat);
-  DIE_CHECK_CONTIG(slab);
-  check_rows(x, "x");
-  const int64_t M = x.size(0), H = x.size(1), I = w_down.size(1);
-  TORCH_CHECK(M >= 1 && M <= 32, "mlp_decode: 1 <= M <= 32");
-  TORCH_CHECK(w_gate_up.dim() == 2 && w_gate_up.size(0) == 2 * I && w_gate_up.size(1) == H, "w_gate_up [2I, H]");
-  TORCH_CHECK(w_down.dim() == 2 && w_down.size(0) == H, "w_down [H, I]");
-  TORCH_CHECK(act.dim() == 2 && act.size(0) >= M && act.size(1) == I, "act [M, I]");
-  TORCH_CHECK(slab.numel() >= 4 * M * H && 4 * M * H * 4 < ((int64_t)1 << 31), "slab [4, M, H]");
-  DIE_CHECK_BF16(resid);
-  check_rows(resid, "resid");
-  TORCH_CHECK(resid.size(0) >= M && resid.size(1) == H, "resid [M, H]");
-  DIE_CHECK_DTYPE(ssp_in, at::kFloat);
-  DIE_CHECK_CONTIG(ssp_in);
-  TORCH_CHECK(ssp_in.dim() == 2 && ssp_in.size(1) == 32 && ssp_in.size(0) >= 1 && ssp_in.size(0) <= 128,
-              "ssp_in [T <= 128, 32]");
-  DIE_CHECK_DTYPE(ssp_out, at::kFloat);
-  DIE_CHECK_CONTIG(ssp_out);
-  TORCH_CHECK(ssp_out.numel() >= (H / 64) * 32, "ssp_out [H/64, 32]");
-  for (const Tensor* t : {&counters, &flags, &err}) {
-    DIE_CHECK_DTYPE((*t), at::kInt);
-    TORCH_CHECK(t->is_cuda() && t->is_contiguous(), "int32 device tensors");
-  }
-  TORCH_CHECK(counters.numel() >= H / 64 && flags.numel() >= 8 && err.numel() >= 1, "counters / flags / err sizes");
-  die::GemmDecodeFuse fz1, fz2;
-  fz1.ssp_in = ssp_in.data_ptr<float>();
-  fz1.ssp_tiles = (int)ssp_in.size(0);
-  fz1.inv_n = 1.f / (float)H;
-  fz1.eps = (float)eps;
-  fz2.resid = bf(resid);
-  fz2.ld_resid = resid.stride(0);
-  fz2.ssp_out = ssp_out.data_ptr<float>();
-  fz2.counters = counters.data_ptr<int>();
-  DIE_HIP(die::launch_mlp_decode(bf(act), bf(x), x.stride(0), bf(w_gate_up), bf(w_down), slab.data_ptr<float>(),
-                                 (int)M, (int)H, (int)I, fz1, fz2, flags.data_ptr<int>(), err.data_ptr<int>(), nt,
-                                 (int)xmode, cur_stream()));
-}
 
 // Grouped (MoE) decode GEMM: x [R, K] token-sorted activations (expert e owns rows
 // [offsets[e], offsets[e+1]), at most 32 of them — one decode step), w [E, rows, K] stacked
@@ -770,7 +730,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_combine", &moe_combine);
   m.def("moe_grouped_gemm", &moe_grouped_gemm);
   m.def("gemm_decode", &gemm_decode);
-  m.def("mlp_decode", &mlp_decode);
+  m.def("gd_set_timestamps", &gd_set_timestamps);
   m.def("row_sumsq", &row_sumsq);
   m.def("residual_add_sumsq", &residual_add_sumsq);
   m.def("decode_advance", &decode_advance);

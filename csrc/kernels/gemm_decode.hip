@@ -60,7 +60,7 @@ using namespace gd;
 // NT: weight pieces are loaded non-temporal (aux = 2): each weight byte is read once per step by one CU,
 // so it should not displace the activations / KV in L2 and MALL (MI355X_MICROARCH.md "nt-weights").
 //
-// The body is a device function so that a persistent launch can chain two of them (mlp_decode_kernel):
+// The body is a device function so that a persistent launch can chain several of them:
 // (bx, by, ny) stand for (blockIdx.x, blockIdx.y, gridDim.y). XWAIT: the activations X are produced
 // inside the same launch — the first S-1 weight chunks are issued, then the workgroup waits until
 // *xflag reaches xtarget, then X is read with device-coherent (sc1) loads. WT: the output is stored
@@ -69,7 +69,7 @@ using namespace gd;
 // (L2-cacheable) X loads (cdna_hip_programming.md Guideline 16 recipe R1).
 // XR: activation rows staged per chunk (32, or 16 when M <= 16: the X share of every DMA chunk — and of
 // the per-CU miss budget that bounds this kernel — halves; grouped MoE decode has ~8 rows per expert).
-template <int WR, int EPI, int S, bool NT, int KC, int XWAIT = 0, bool WT = false, int XR = MR>
+template <int WR, int EPI, int S, bool NT, int KC, int XWAIT = 0, bool WT = false, int XR = MR, int SKC = 0>
 __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const bf16_t* __restrict__ X, int64_t ldx,
                                         const bf16_t* __restrict__ W, int M, int N_out, int K,
                                         const GemmDecodeFuse& fz, const int bx, const int by, const int ny,
@@ -127,8 +127,14 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
       base = fz.grp_rows != nullptr ? X + (int64_t)(fz.grp_rows[r0 + xr] / fz.grp_k) * ldx : X + (int64_t)xr * ldx;
     }
     src[p] = base + k0 + lch * 8;
+    if (row < WR && fz.tiled) {
+      // pre-packed weights (gd_pack_weights): tile bx's K-chunk c is WR/RPP contiguous 1-KiB pieces
+      // already in LDS-image order (rows, swizzle and all), so each piece is one linear 1-KiB read
+      src[p] = W + ((int64_t)bx * (K / KC) + k0 / KC) * (WR / RPP) * 512 + piece * 512 + lane * 8;
+    }
     isw[p] = row < WR;
   }
+  const int64_t wstep = fz.tiled ? (int64_t)(WR / RPP) * 512 : KC;  // W elements per K-chunk
   // part: 3 = whole chunk, 1 = weight pieces only, 2 = activation pieces only
   auto issue = [&](int c, int part = 3) {
     char* slot = smem + (c % S) * SLOT;
@@ -138,9 +144,9 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
       if (isw[p]) {
         if (!(part & 1)) continue;
         if (NT)
-          glds16<2>(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);
+          glds16<2>(src[p] + (int64_t)c * wstep, slot + (wave + 4 * p) * 1024);
         else
-          glds16<0>(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);
+          glds16<0>(src[p] + (int64_t)c * wstep, slot + (wave + 4 * p) * 1024);
       } else {
         if (!(part & 2)) continue;
         if (XWAIT == 1)
@@ -259,22 +265,33 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
       }
   __syncthreads();
   if constexpr (EPI == 3) {
-    // split-K partial -> last arriver: h += sum of partials (bf16), per-tile row sums of squares
+    // split-K partial -> last arriver: h += sum of partials (bf16), per-tile row sums of squares.
+    // Every thread owns EPT float4 groups (row m, columns j..j+3); its own workgroup's partial stays in
+    // registers, so the last arriver reads only the OTHER ny-1 slabs, all of them issued back to back
+    // (SKC = compile-time ny: no per-slab round trip) together with the residual rows.
     constexpr int Q = WR / 4;  // float4 column groups per row (8, 16 or 32 lanes: one row per lane group)
     static_assert(Q == 8 || Q == 16 || Q == 32, "EPI 3 needs wr in {32, 64, 128}");
+    constexpr int EPT = MR * Q / NTH;
+    static_assert(EPT * NTH == MR * Q, "whole float4 groups per thread");
     int* ctl = reinterpret_cast<int*>(smem + 4 * MR * WR * 4);
     const bool single = ny == 1;
-    if (!single) {
-      __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(Yv, 0, 0x7fffffff, 0x00020000);
-      for (int e = tid; e < MR * Q; e += NTH) {
-        const int m = e / Q, j = 4 * (e % Q);
-        if (m >= M) continue;
-        f4 v = f4{0.f, 0.f, 0.f, 0.f};
+    f4 own[EPT];
 #pragma unroll
-        for (int w = 0; w < 4; ++w) v += *reinterpret_cast<const f4*>(red + (w * MR + m) * WR + j);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
-                                               ry, (int)((((int64_t)by * M + m) * ldy + n0 + j) * 4), 0,
-                                               16);  // write-through (sc1): no release fence needed
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tid + i * NTH, m = e / Q, j = 4 * (e % Q);
+      own[i] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int w = 0; w < 4; ++w) own[i] += *reinterpret_cast<const f4*>(red + (w * MR + m) * WR + j);
+    }
+    __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(Yv, 0, 0x7fffffff, 0x00020000);
+    if (!single) {
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) {
+        const int e = tid + i * NTH, m = e / Q, j = 4 * (e % Q);
+        if (m < M)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, own[i]), ry,
+              (int)((((int64_t)by * M + m) * ldy + n0 + j) * 4), 0, 16);  // write-through (sc1): no release fence
       }
       wait_vm<0>();
       __syncthreads();
@@ -283,28 +300,52 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
       __syncthreads();
       if (!ctl[0]) return;
     }
-    __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(Yv, 0, 0x7fffffff, 0x00020000);
-    for (int e = tid; e < MR * Q; e += NTH) {  // Q | 64 and NTH % Q == 0: a row's lanes share a wave
-      const int m = e / Q, j = 4 * (e % Q);
+    uint2 hr[EPT];
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {  // rows clamped (no branch around a load), masked on the write
+      const int e = tid + i * NTH, m = min(e / Q, M - 1), j = 4 * (e % Q);
+      hr[i] = *reinterpret_cast<const uint2*>(fz.resid + (int64_t)m * fz.ld_resid + n0 + j);
+    }
+    if (!single) {
+      if constexpr (SKC > 1) {
+        f4 pv[EPT][SKC - 1];
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+          const int e = tid + i * NTH, m = min(e / Q, M - 1), j = 4 * (e % Q);
+#pragma unroll
+          for (int kk = 0; kk < SKC - 1; ++kk) {
+            const int k = kk + (kk >= by);
+            pv[i][kk] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   ry, (int)((((int64_t)k * M + m) * ldy + n0 + j) * 4), 0, 16));
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < EPT; ++i)
+#pragma unroll
+          for (int kk = 0; kk < SKC - 1; ++kk) own[i] += pv[i][kk];
+      } else {
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+          const int e = tid + i * NTH, m = min(e / Q, M - 1), j = 4 * (e % Q);
+          for (int k = 0; k < ny; ++k)
+            if (k != by)
+              own[i] += __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   ry, (int)((((int64_t)k * M + m) * ldy + n0 + j) * 4), 0, 16));
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {  // Q | 64 and NTH % Q == 0: a row's lanes share a wave
+      const int e = tid + i * NTH, m = e / Q, j = 4 * (e % Q);
+      const f4 v = own[i];
+      float hv[4] = {bf2f((bf16_t)(hr[i].x & 0xffff)) + v[0], bf2f((bf16_t)(hr[i].x >> 16)) + v[1],
+                     bf2f((bf16_t)(hr[i].y & 0xffff)) + v[2], bf2f((bf16_t)(hr[i].y >> 16)) + v[3]};
+      uint2 hw;
+      hw.x = pack2(hv[0], hv[1]);
+      hw.y = pack2(hv[2], hv[3]);
       float ss = 0.f;
       if (m < M) {
-        f4 v = f4{0.f, 0.f, 0.f, 0.f};
-        if (single) {
-#pragma unroll
-          for (int w = 0; w < 4; ++w) v += *reinterpret_cast<const f4*>(red + (w * MR + m) * WR + j);
-        } else {
-          for (int k = 0; k < ny; ++k)
-            v += __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            ry, (int)((((int64_t)k * M + m) * ldy + n0 + j) * 4), 0, 16));
-        }
-        bf16_t* hp = fz.resid + (int64_t)m * fz.ld_resid + n0 + j;
-        const uint2 hr = *reinterpret_cast<const uint2*>(hp);
-        float hv[4] = {bf2f((bf16_t)(hr.x & 0xffff)) + v[0], bf2f((bf16_t)(hr.x >> 16)) + v[1],
-                       bf2f((bf16_t)(hr.y & 0xffff)) + v[2], bf2f((bf16_t)(hr.y >> 16)) + v[3]};
-        uint2 hw;
-        hw.x = pack2(hv[0], hv[1]);
-        hw.y = pack2(hv[2], hv[3]);
-        *reinterpret_cast<uint2*>(hp) = hw;
+        *reinterpret_cast<uint2*>(fz.resid + (int64_t)m * fz.ld_resid + n0 + j) = hw;
         const float r0 = bf2f((bf16_t)(hw.x & 0xffff)), r1 = bf2f((bf16_t)(hw.x >> 16));
         const float r2 = bf2f((bf16_t)(hw.y & 0xffff)), r3 = bf2f((bf16_t)(hw.y >> 16));
         ss = r0 * r0 + r1 * r1 + r2 * r2 + r3 * r3;
@@ -361,59 +402,28 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
   }
 }
 
-template <int WR, int EPI, int S, bool NT, int KC, int XR>
+template <int WR, int EPI, int S, bool NT, int KC, int XR, int SKC = 0>
 __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv, int64_t ldy,
                                                           const bf16_t* __restrict__ X, int64_t ldx,
                                                           const bf16_t* __restrict__ W, int M, int N_out, int K,
                                                           GemmDecodeFuse fz) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  gd_body<WR, EPI, S, NT, KC, 0, false, XR>(smem, Yv, ldy, X, ldx, W, M, N_out, K, fz, blockIdx.x, blockIdx.y,
-                                           gridDim.y);
-}
-
-// Persistent decode MLP (one launch instead of two): every workgroup first computes gate/up column
-// tiles (mode 4: norm row scale + SiLU*mul, 56 outputs per tile, written through to memory), then
-// down-projection tiles (mode 3: 64 columns x 1/4 of K, split-K slabs + last-arriver residual update
-// and next-norm statistics). Down tile (n, s) needs only the activation columns of k-slice s, i.e. the
-// gate/up tiles [s * P, (s + 1) * P): each producer bumps flags[s], and the consumer streams its first
-// weight chunks into the LDS ring BEFORE waiting for flags[s] == P, so the down weight stream starts
-// while the last gate/up tiles drain (no launch boundary, no pipeline refill; cf.
-// cdna_hip_programming.md §5.6: the MLP half of a decode layer at batch 16-32 is faster in one launch).
-// flags[s + 4] counts consumers past the wait; the last one re-arms both words for the next layer.
-// The grid never exceeds the CU count and one workgroup fills a CU's LDS, so every workgroup is
-// resident and the waits cannot deadlock; every spin is bounded (err = 1 on give-up).
-constexpr int MLP_NO1 = 56, MLP_WR2 = 64, MLP_SK2 = 4;
-
-template <bool NT, int XMODE>
-__global__ void __launch_bounds__(NTH) mlp_decode_kernel(bf16_t* __restrict__ act, const bf16_t* __restrict__ X,
-                                                         int64_t ldx, const bf16_t* __restrict__ Wgu,
-                                                         const bf16_t* __restrict__ Wd, float* __restrict__ slab,
-                                                         int M, int H, int I, GemmDecodeFuse fz1, GemmDecodeFuse fz2,
-                                                         int* __restrict__ flags, int* __restrict__ err) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tiles1 = I / MLP_NO1, per_slice = tiles1 / MLP_SK2;
-  const int ntile2 = H / MLP_WR2, tiles2 = ntile2 * MLP_SK2;
-  const int tid = threadIdx.x;
-  for (int t = blockIdx.x; t < tiles1; t += gridDim.x) {
-    gd_body<112, 4, 4, NT, 128, false, true>(smem, act, I, X, ldx, Wgu, M, I, H, fz1, t, 0, 1);
-    wait_vm<0>();     // this thread's write-through stores are acknowledged
-    __syncthreads();  // ... and everyone's; the LDS is free again
-    if (tid == 0) __hip_atomic_fetch_add(flags + t / per_slice, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  for (int t = blockIdx.x; t < tiles2; t += gridDim.x) {
-    const int s = t % MLP_SK2, n = t / MLP_SK2;
-    gd_body<MLP_WR2, 3, 3, NT, 256, XMODE, false>(smem, slab, H, act, I, Wd, M, H, I, fz2, n, s, MLP_SK2, flags + s,
-                                                  per_slice, err);
-    __syncthreads();
-    if (tid == 0 &&
-        __hip_atomic_fetch_add(flags + MLP_SK2 + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ntile2 - 1) {
-      __hip_atomic_store(flags + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(flags + MLP_SK2 + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+  long long t0 = 0;
+  if (fz.ts != nullptr) t0 = __builtin_amdgcn_s_memrealtime();
+  gd_body<WR, EPI, S, NT, KC, 0, false, XR, SKC>(smem, Yv, ldy, X, ldx, W, M, N_out, K, fz, blockIdx.x,
+                                                blockIdx.y, gridDim.y);
+  if (fz.ts != nullptr && threadIdx.x == 0) {  // diagnostics only (bench/micro_gd_timeline.py)
+    const long long t1 = __builtin_amdgcn_s_memrealtime();
+    const int wg = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    int xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    fz.ts[3 * wg] = t0;
+    fz.ts[3 * wg + 1] = t1;
+    fz.ts[3 * wg + 2] = xcc;
   }
 }
 
-template <int WR, int EPI, int S, int KC>
+template <int WR, int EPI, int S, int KC, int SKC = 0>
 static hipError_t launch_gd(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N_out,
                             int K, int sk, bool nt, const GemmDecodeFuse& fz, hipStream_t s) {
   constexpr int NO = (EPI == 1 || EPI == 4) ? WR / 2 : WR;
@@ -433,13 +443,13 @@ static hipError_t launch_gd(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, 
   }();
   const bool small = xr16 && nt && M <= 16;
   if (small) {
-    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, true, KC, 16>), dim3(N_out / NO, sk, fz.grp_n), dim3(NTH),
+    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, true, KC, 16, SKC>), dim3(N_out / NO, sk, fz.grp_n), dim3(NTH),
                        lds_for(16), s, Y, ldy, X, ldx, W, M, N_out, K, fz);
   } else if (nt) {
-    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, true, KC, MR>), dim3(N_out / NO, sk, fz.grp_n), dim3(NTH),
+    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, true, KC, MR, SKC>), dim3(N_out / NO, sk, fz.grp_n), dim3(NTH),
                        lds_for(MR), s, Y, ldy, X, ldx, W, M, N_out, K, fz);
   } else {
-    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, false, KC, MR>), dim3(N_out / NO, sk, fz.grp_n), dim3(NTH),
+    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, false, KC, MR, SKC>), dim3(N_out / NO, sk, fz.grp_n), dim3(NTH),
                        lds_for(MR), s, Y, ldy, X, ldx, W, M, N_out, K, fz);
   }
   return hipGetLastError();
@@ -454,8 +464,14 @@ static hipError_t launch_modes(void* Y, int64_t ldy, const bf16_t* X, int64_t ld
     case 2: return launch_gd<WR, 2, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
     case 4: return launch_gd<WR, 4, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
     case 3:
-      if constexpr (WR == 32 || WR == 64 || WR == 128)
-        return launch_gd<WR, 3, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
+      if constexpr (WR == 32 || WR == 64 || WR == 128) {
+        switch (sk) {  // compile-time split count: the last arriver issues every slab load at once
+          case 2: return launch_gd<WR, 3, S, KC, 2>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
+          case 4: return launch_gd<WR, 3, S, KC, 4>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
+          case 8: return launch_gd<WR, 3, S, KC, 8>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
+          default: return launch_gd<WR, 3, S, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
+        }
+      }
       return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
@@ -489,36 +505,6 @@ hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx
     case 65: return launch_modes<64, 6, 128>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, fz, s);
     default: return hipErrorInvalidValue;
   }
-}
-
-// act [M, I] bf16 scratch (row stride I); slab [4, M, H] fp32 scratch; flags int[8] zeroed once;
-// fz1: ssp_in / ssp_tiles / inv_n / eps of the gate/up norm; fz2: resid / ld_resid / ssp_out /
-// counters [H / 64] of the down projection (as mode 3).
-hipError_t launch_mlp_decode(bf16_t* act, const bf16_t* X, int64_t ldx, const bf16_t* Wgu, const bf16_t* Wd,
-                             float* slab, int M, int H, int I, const GemmDecodeFuse& fz1, const GemmDecodeFuse& fz2,
-                             int* flags, int* err, bool nt, int xmode, hipStream_t s) {
-  if (M <= 0) return hipSuccess;
-  if (xmode != 1 && xmode != 2) return hipErrorInvalidValue;
-  if (M > MR || H % 128 || H % MLP_WR2 || I % (MLP_NO1 * MLP_SK2) || (I / MLP_SK2) % 256 || (I / MLP_SK2) / 256 < 3)
-    return hipErrorInvalidValue;
-  if (fz1.ssp_in == nullptr || fz1.ssp_tiles < 1 || fz1.ssp_tiles > 128 || fz2.resid == nullptr ||
-      fz2.ssp_out == nullptr || fz2.counters == nullptr || flags == nullptr || err == nullptr)
-    return hipErrorInvalidValue;
-  const int tiles = min(I / MLP_NO1, (H / MLP_WR2) * MLP_SK2);
-  const int grid = min(tiles, num_cus());
-  constexpr size_t lds1 = (size_t)4 * (112 + MR) * 128 * 2, lds2 = (size_t)3 * (MLP_WR2 + MR) * 256 * 2;
-  constexpr size_t lds = lds1 > lds2 ? lds1 : lds2;
-  static_assert(lds > 80 * 1024, "one workgroup per CU (residency of the persistent grid)");
-#define DIE_MLP_LAUNCH(NTV, XM)                                                                               \
-  hipLaunchKernelGGL((mlp_decode_kernel<NTV, XM>), dim3(grid), dim3(NTH), lds, s, act, X, ldx, Wgu, Wd, slab, M, H, \
-                     I, fz1, fz2, flags, err)
-  if (nt) {
-    if (xmode == 2) DIE_MLP_LAUNCH(true, 2); else DIE_MLP_LAUNCH(true, 1);
-  } else {
-    if (xmode == 2) DIE_MLP_LAUNCH(false, 2); else DIE_MLP_LAUNCH(false, 1);
-  }
-#undef DIE_MLP_LAUNCH
-  return hipGetLastError();
 }
 
 }  // namespace die

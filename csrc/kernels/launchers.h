@@ -84,13 +84,11 @@ struct GemmDecodeFuse {
   int grp_n = 1;                 //   number of experts (grid z)
   const int* grp_rows = nullptr; //   optional gather: X row j of the sorted order is token grp_rows[j] / grp_k
   int grp_k = 1;                 //   (X is then the un-permuted [T, K] activations; Y stays in sorted order)
+  int tiled = 0;                 // W pre-packed into the kernel's tile order (gd_pack_weights)
+  long long* ts = nullptr;       // diagnostics: per-workgroup [start, end, xcc] s_memrealtime stamps (or null)
 };
 hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,
                               int K, int mode, int wr, int sk, bool nt, const GemmDecodeFuse& fz, hipStream_t s);
-// persistent decode MLP: gate/up (mode 4) then down (mode 3) in one launch (gemm_decode.hip)
-hipError_t launch_mlp_decode(bf16_t* act, const bf16_t* X, int64_t ldx, const bf16_t* Wgu, const bf16_t* Wd,
-                             float* slab, int M, int H, int I, const GemmDecodeFuse& fz1, const GemmDecodeFuse& fz2,
-                             int* flags, int* err, bool nt, int xmode, hipStream_t s);
 // consumers of fp32 split-K slabs [sk][rows][width]
 hipError_t launch_fused_add_rms_norm_slab(bf16_t* out, const float* slab, int sk, bf16_t* residual, const bf16_t* w,
                                           float eps, int rows, int hidden, int64_t out_stride, hipStream_t s);

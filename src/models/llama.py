@@ -21,6 +21,7 @@ The same module runs CPU tensors through :mod:`src.ops.reference` for tests.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -51,11 +52,16 @@ class AttnMetadata:
 
 
 class LayerWeights:
-    __slots__ = ("ln1", "ln2", "qkv", "o", "gate_up", "down", "router", "w13", "w2")
+    __slots__ = ("ln1", "ln2", "qkv", "o", "gate_up", "down", "router", "w13", "w2",
+                 "qkv_t", "o_t", "gate_up_t", "down_t")  # *_t: decode-GEMM tile-order copies (or None)
 
     def __init__(self):
         for s in self.__slots__:
             setattr(self, s, None)
+
+
+def _w(w: torch.Tensor, w_tiled: Optional[torch.Tensor]) -> torch.Tensor:
+    return w if w_tiled is None else w_tiled
 
 
 # LDS staging area of the fused decode attention's prologue (csrc/kernels/attention.hip V3_MERGE)
@@ -219,6 +225,8 @@ class CausalLM:
         q / k / v (gate / up, w1 / w3) may arrive in different calls. Returns the number of
         tensors consumed. ``fold``: fold the norm weights into Wqkv / Wgate_up afterwards (pass
         False while streaming several files, then call :meth:`fold_norm_weights` once)."""
+        for lw in self.layers:  # decode tile-order copies go stale: re-packed by alloc_decode_scratch
+            lw.qkv_t = lw.o_t = lw.gate_up_t = lw.down_t = None
         a, d, r, ws = self.arch, self.head_dim, self.tp.rank, self.tp.world_size
         hq, hkv, inter = self.hq, self.hkv, self.inter
         kv_idx = (r * hkv) if a.num_kv_heads >= ws else r // (ws // a.num_kv_heads)
@@ -426,11 +434,30 @@ class CausalLM:
                 sk //= 2
             return wr, sk
 
-        plan = {"qkv": (wq, sq), "o": resid_cfg(self.hq * d), "down": resid_cfg(self.inter), "mlp_fused": False}
-        if ops.MLP_DECODE_FUSED and not self.tp.enabled and ops.mlp_decode_ok(h, self.inter):
-            # gate/up + down in one persistent launch; its down tiles are 64 columns x 4 k-slices
-            plan["mlp_fused"], plan["down"] = True, (64, 4)
-        return plan
+        gu = ops._cfg_for(self.inter, h, 1)[0] if not self.arch.is_moe else None
+        return {"qkv": (wq, sq), "o": resid_cfg(self.hq * d), "down": resid_cfg(self.inter), "gate_up": gu}
+
+    def pack_decode_weights(self) -> bool:
+        """Keep a second copy of the dense projections in the decode GEMM's tile order
+        (ops.gd_pack_weights: every LDS-DMA piece one linear 1-KiB read) for the fused decode path;
+        prefill keeps the row-major copies for hipBLASLt. Costs one more copy of those weights
+        (8B: +13 GiB of the 288 GB HBM), so it is only done when the weights take <= 1/4 of the
+        device memory. DIE_GD_TILED=0 disables it."""
+        if os.environ.get("DIE_GD_TILED", "1") == "0" or self.arch.is_moe or not self.norms_folded:
+            return False
+        if not (self.device.type == "cuda" and ops.native_available()):
+            return False
+        total = torch.cuda.get_device_properties(self.device).total_memory
+        if 2 * self.weight_bytes() > total // 2:
+            return False
+        p = self.decode_plan()
+        for lw in self.layers:
+            lw.qkv_t = ops.gd_pack_weights(lw.qkv, p["qkv"][0])
+            if not self.tp.enabled:
+                lw.o_t = ops.gd_pack_weights(lw.o, p["o"][0])
+                lw.down_t = ops.gd_pack_weights(lw.down, p["down"][0])
+            lw.gate_up_t = ops.gd_pack_weights(lw.gate_up, p["gate_up"], silu=True)
+        return True
 
     def alloc_decode_scratch(self) -> Optional[dict]:
         if not (self.device.type == "cuda" and ops.native_available()):
@@ -443,13 +470,10 @@ class CausalLM:
         if max(to, td) > 128:
             return None
         dev = self.device
+        self.pack_decode_weights()
         sc = {"plan": p, "ssp0": torch.zeros(1, 32, dtype=f32, device=dev),
               "ssp_a": torch.zeros(to, 32, dtype=f32, device=dev), "cnt_a": torch.zeros(to, dtype=i32, device=dev),
               "ssp_b": torch.zeros(td, 32, dtype=f32, device=dev), "cnt_b": torch.zeros(td, dtype=i32, device=dev)}
-        if p["mlp_fused"]:
-            sc.update(mlp_flags=torch.zeros(8, dtype=i32, device=dev), mlp_err=torch.zeros(1, dtype=i32, device=dev),
-                      mlp_act=torch.empty(32, self.inter, dtype=self.dtype, device=dev),
-                      mlp_slab=torch.empty(4 * 32 * h, dtype=f32, device=dev))
         return sc
 
     def _fused_decode_ok(self, kv_pool: torch.Tensor) -> bool:
@@ -460,7 +484,7 @@ class CausalLM:
 
     def _forward_decode_fused(self, h: torch.Tensor, positions: torch.Tensor, meta: AttnMetadata,
                               kv_pool: torch.Tensor) -> torch.Tensor:
-        """Decode layer = 5 launches (4 with the persistent MLP): qkv (split-K slabs) -> attention (norm scale + slab sum + RoPE
+        """Decode layer = 5 launches: qkv (split-K slabs) -> attention (norm scale + slab sum + RoPE
         + KV write in its prologue) -> o (slabs, last arriver adds into the residual and writes the
         next norm's row statistics) -> gate/up (norm as a row scale, SiLU*mul) -> down (as o).
         The residual stream `h` is updated in place; norm weights are folded into Wqkv / Wgate_up."""
@@ -470,7 +494,8 @@ class CausalLM:
         ssp_prev = ops.row_sumsq(h, out=sc["ssp0"])
         for li, lw in enumerate(self.layers):
             k_cache, v_cache = kv_pool[li, 0], kv_pool[li, 1]
-            slab = ops.linear_slab(h, lw.qkv, sk=plan["qkv"][1], wr=plan["qkv"][0])
+            slab = ops.linear_slab(h, lw.qkv if lw.qkv_t is None else lw.qkv_t, sk=plan["qkv"][1], wr=plan["qkv"][0],
+                                   tiled=lw.qkv_t is not None)
             attn = ops.attn_decode_fused(slab, ssp_prev, positions, self.cos_sin, meta.slot_mapping,
                                          k_cache, v_cache, meta.block_tables, meta.ctx_lens, meta.max_ctx, hq, hkv,
                                          self.scale, eps, hid, meta.part_o, meta.part_ml, meta.attn_cnt)
@@ -488,16 +513,16 @@ class CausalLM:
             elif self.tp.enabled:  # row-parallel partial sums -> all-reduce -> residual + statistics (one
                 # launch on the one-shot IPC path, see TPContext.all_reduce_residual)
                 self.tp.all_reduce_residual(ops.linear(attn, lw.o), h, sc["ssp_a"])
-                act = ops.linear_silu_mul_rownorm(h, lw.gate_up, sc["ssp_a"], eps)
+                act = ops.linear_silu_mul_rownorm(h, _w(lw.gate_up, lw.gate_up_t), sc["ssp_a"], eps, plan["gate_up"],
+                                                  tiled=lw.gate_up_t is not None)
                 self.tp.all_reduce_residual(ops.linear(act, lw.down), h, sc["ssp_b"])
             else:
-                ops.linear_slab_residual(attn, lw.o, h, sc["ssp_a"], sc["cnt_a"], *plan["o"])
-                if plan["mlp_fused"]:  # gate/up -> down hand-off inside one persistent launch
-                    ops.mlp_decode(h, lw.gate_up, lw.down, sc["ssp_a"], eps, h, sc["ssp_b"], sc["cnt_b"],
-                                   sc["mlp_flags"], sc["mlp_err"], sc["mlp_act"][: h.shape[0]], sc["mlp_slab"])
-                else:
-                    act = ops.linear_silu_mul_rownorm(h, lw.gate_up, sc["ssp_a"], eps)
-                    ops.linear_slab_residual(act, lw.down, h, sc["ssp_b"], sc["cnt_b"], *plan["down"])
+                ops.linear_slab_residual(attn, _w(lw.o, lw.o_t), h, sc["ssp_a"], sc["cnt_a"], *plan["o"],
+                                         tiled=lw.o_t is not None)
+                act = ops.linear_silu_mul_rownorm(h, _w(lw.gate_up, lw.gate_up_t), sc["ssp_a"], eps, plan["gate_up"],
+                                                  tiled=lw.gate_up_t is not None)
+                ops.linear_slab_residual(act, _w(lw.down, lw.down_t), h, sc["ssp_b"], sc["cnt_b"], *plan["down"],
+                                         tiled=lw.down_t is not None)
             ssp_prev = sc["ssp_b"]
         return ops.rms_norm(h, self.norm, eps)
 

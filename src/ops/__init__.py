@@ -192,15 +192,6 @@ def _decode_gemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 DECODE_GEMM_NT = True
-# decode MLP (gate/up + down) as one persistent launch where the shapes allow (opt-in, DIE_MLP_FUSED=1):
-# bit-identical to the two launches and measured equal in speed on MI355X (bench/micro_mlp_decode.py:
-# 78.3 vs 78.1 us per Llama-3-8B layer at batch 32, profiles/micro_mlp_decode_r1.jsonl), so the simpler
-# two-launch form stays the default
-MLP_DECODE_FUSED = os.environ.get("DIE_MLP_FUSED", "0") == "1"
-# hand-off of the gate/up activations to the down tiles: 1 = sc1 loads of X on every chunk,
-# 2 = one agent-scope acquire after the flag, then plain L2-cacheable loads
-MLP_XMODE = int(os.environ.get("DIE_MLP_XMODE", "2"))  # non-temporal weight loads (read-once stream)
-
 
 def gemm_decode(x: torch.Tensor, w: torch.Tensor, mode: int = 0, wr: int = 64, sk: int = 1,
                 out: Optional[torch.Tensor] = None, nt: Optional[bool] = None) -> torch.Tensor:
@@ -208,15 +199,46 @@ def gemm_decode(x: torch.Tensor, w: torch.Tensor, mode: int = 0, wr: int = 64, s
     mode 0: bf16 x@w^T; mode 1: bf16 silu(gate)*up (w = [gate; up]);
     mode 2: fp32 split-K slabs [sk, M, N]."""
     m = x.shape[0]
-    n = w.shape[0] // 2 if mode == 1 else w.shape[0]
+    base = mode & 31  # | 32: w pre-packed by gd_pack_weights
+    n = w.shape[0] // 2 if base == 1 else w.shape[0]
     if out is None:
-        if mode == 2:
+        if base == 2:
             out = torch.empty(sk, m, n, dtype=torch.float32, device=x.device)
         else:
             out = torch.empty(m, n, dtype=x.dtype, device=x.device)
     e = _empty(x.device)
     _kern().gemm_decode(out, x, w, mode, wr, sk, DECODE_GEMM_NT if nt is None else nt, e, e, e, e, 0.0)
     return out
+
+
+def gd_kc(wr: int) -> int:
+    """K elements per ring slot of the decode GEMM for a weight-row tile of `wr` (gemm_decode.hip)."""
+    return 128 if (wr >= 96 or wr & 1) else 256
+
+
+def gd_pack_weights(w: torch.Tensor, wr: int, silu: bool = False) -> torch.Tensor:
+    """Re-lay a [rows, K] projection weight in the decode GEMM's tile order: for column tile t and
+    K-chunk c, the tile's (wr x KC) block is contiguous and already in the kernel's LDS-image order
+    (rows of the tile, 16-byte chunks XOR-swizzled by row), so every 1-KiB LDS-DMA piece is one
+    linear read. silu: w = [gate; up] and a tile holds wr/2 gate rows then the matching wr/2 up
+    rows. The result has w's shape (pass mode | 32 to gemm_decode)."""
+    rows, k = w.shape
+    wrr = wr & ~1
+    kc = gd_kc(wr)
+    cpr = kc // 8
+    no = wrr // 2 if silu else wrr
+    n_out = rows // 2 if silu else rows
+    assert n_out % no == 0 and k % kc == 0
+    nt, nch = n_out // no, k // kc
+    t = torch.arange(nt, device=w.device).view(nt, 1) * no
+    j = torch.arange(no, device=w.device).view(1, no)
+    idx = torch.cat([t + j, n_out + t + j], 1) if silu else (t + torch.arange(wrr, device=w.device).view(1, wrr))
+    wt = w[idx.reshape(-1)].view(nt, wrr, nch, cpr, 8)
+    r = torch.arange(wrr, device=w.device).view(1, wrr, 1, 1, 1)
+    q = torch.arange(cpr, device=w.device).view(1, 1, 1, cpr, 1)
+    sw = (q ^ (r & 15)).expand(nt, wrr, nch, cpr, 8)
+    wt = torch.gather(wt, 3, sw)
+    return wt.permute(0, 2, 1, 3, 4).contiguous().view(rows, k)
 
 
 _EMPTY: dict = {}
@@ -230,7 +252,7 @@ def _empty(dev) -> torch.Tensor:
 
 
 def linear_slab_residual(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, ssp_out: torch.Tensor,
-                         counters: torch.Tensor, wr: int = 64, sk: int = 4) -> torch.Tensor:
+                         counters: torch.Tensor, wr: int = 64, sk: int = 4, tiled: bool = False) -> torch.Tensor:
     """resid += x @ w^T (bf16, in place) with split-K reduced by the last-arriving workgroup of
     each column tile, which also writes the tile's row sums of squares of the new residual to
     ssp_out [N/wr, 32] — the statistics of the next RMSNorm (whose weight is folded into the
@@ -238,12 +260,13 @@ def linear_slab_residual(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, 
     m, n = x.shape[0], w.shape[0]
     slab = torch.empty(sk, m, n, dtype=torch.float32, device=x.device)
     e = _empty(x.device)
-    _kern().gemm_decode(slab, x, w, 3, wr, sk, DECODE_GEMM_NT, resid, ssp_out, counters, e, 0.0)
+    _kern().gemm_decode(slab, x, w, 3 | (32 if tiled else 0), wr, sk, DECODE_GEMM_NT, resid, ssp_out, counters, e,
+                        0.0)
     return slab
 
 
 def linear_silu_mul_rownorm(x: torch.Tensor, w_gate_up: torch.Tensor, ssp_in: torch.Tensor, eps: float,
-                            wr: Optional[int] = None) -> torch.Tensor:
+                            wr: Optional[int] = None, tiled: bool = False) -> torch.Tensor:
     """silu(r * x @ gate^T) * (r * x @ up^T) with r = rsqrt(sum_t ssp_in[t] / K + eps) per row:
     RMSNorm (weight folded into w_gate_up) + gate/up + SiLU*mul in one weight stream."""
     n = w_gate_up.shape[0] // 2
@@ -251,33 +274,9 @@ def linear_silu_mul_rownorm(x: torch.Tensor, w_gate_up: torch.Tensor, ssp_in: to
         wr, _ = _cfg_for(n, x.shape[1], 1)
     out = torch.empty(x.shape[0], n, dtype=x.dtype, device=x.device)
     e = _empty(x.device)
-    _kern().gemm_decode(out, x, w_gate_up, 4, wr, 1, DECODE_GEMM_NT, e, e, e, ssp_in, float(eps))
+    _kern().gemm_decode(out, x, w_gate_up, 4 | (32 if tiled else 0), wr, 1, DECODE_GEMM_NT, e, e, e, ssp_in,
+                        float(eps))
     return out
-
-
-def mlp_decode_ok(hidden: int, inter: int) -> bool:
-    """Shapes the persistent decode-MLP kernel takes (gate/up tiles of 56 columns, down tiles of
-    64 columns x 4 k-slices of whole 256-wide chunks), e.g. Llama-3-8B 4096 / 14336."""
-    return hidden % 128 == 0 and inter % 224 == 0 and (inter // 4) % 256 == 0 and inter // 4 >= 768
-
-
-def mlp_decode(x: torch.Tensor, w_gate_up: torch.Tensor, w_down: torch.Tensor, ssp_in: torch.Tensor, eps: float,
-               resid: torch.Tensor, ssp_out: torch.Tensor, counters: torch.Tensor, flags: torch.Tensor,
-               err: torch.Tensor, act: Optional[torch.Tensor] = None, slab: Optional[torch.Tensor] = None) -> None:
-    """resid += down(silu(r x Wg^T) * (r x Wu^T)) in ONE persistent launch (gate/up tiles hand their
-    activation columns to the down tiles through per-k-slice flags; see gemm_decode.hip
-    mlp_decode_kernel). r = rsqrt(sum_t ssp_in[t] / H + eps) per row; ssp_out [H/64, 32] receives the
-    next norm's statistics. counters [H/64] and flags [8] int32, zeroed once; err [1] int32 stays 0
-    unless a hand-off wait gave up. x may alias resid (the down tiles write it only after every
-    gate/up tile has finished reading)."""
-    m, h = x.shape
-    inter = w_down.shape[1]
-    if act is None:
-        act = torch.empty(m, inter, dtype=x.dtype, device=x.device)
-    if slab is None:
-        slab = torch.empty(4, m, h, dtype=torch.float32, device=x.device)
-    _kern().mlp_decode(act, slab, x, w_gate_up, w_down, ssp_in, resid, ssp_out, counters, flags, err, float(eps),
-                       DECODE_GEMM_NT, MLP_XMODE)
 
 
 def residual_add_sumsq(resid: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
@@ -362,13 +361,16 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
     return torch.nn.functional.linear(x, w, out=out) if out is not None else torch.nn.functional.linear(x, w)
 
 
-def linear_slab(x: torch.Tensor, w: torch.Tensor, sk: Optional[int] = None, wr: Optional[int] = None) -> torch.Tensor:
+def linear_slab(x: torch.Tensor, w: torch.Tensor, sk: Optional[int] = None, wr: Optional[int] = None,
+                tiled: bool = False) -> torch.Tensor:
     """fp32 split-K slabs [sk, M, N] of x @ w^T (decode sizes only); the
-    consumer (fused_add_rms_norm_slab / rope_and_cache_slab) reduces them."""
+    consumer (fused_add_rms_norm_slab / rope_and_cache_slab) reduces them.
+    tiled: w was packed by gd_pack_weights for this wr."""
     if sk is None or wr is None:
+        assert not tiled, "a tiled weight needs its packing wr"
         wr0, sk0 = _cfg_for(w.shape[0], x.shape[1], 2)
         wr, sk = wr or wr0, sk or sk0
-    return gemm_decode(x, w, 2, wr, sk)
+    return gemm_decode(x, w, 2 | (32 if tiled else 0), wr, sk)
 
 
 def linear_silu_mul(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:

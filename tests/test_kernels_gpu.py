@@ -360,7 +360,8 @@ def test_rope_and_cache_slab(dev):
 
 
 # ---------------------------------------------------------------- fused decode path pieces
-@pytest.mark.parametrize("wr,sk,k", [(64, 4, 4096), (64, 4, 14336), (32, 1, 2048), (128, 2, 4096)])
+@pytest.mark.parametrize("wr,sk,k", [(64, 4, 4096), (64, 4, 14336), (32, 1, 2048), (128, 2, 4096), (64, 8, 4096),
+                                     (32, 3, 3072)])
 def test_gemm_decode_residual_mode(dev, wr, sk, k):
     """mode 3: resid += x @ w^T with the split-K reduced by the last-arriving workgroup, which
     also writes the per-tile row sums of squares of the new residual."""
@@ -398,40 +399,28 @@ def test_gemm_decode_rownorm_silu(dev, m, inter, k, wr):
     close(y, r, atol=3e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("m,h,inter", [(32, 4096, 14336), (1, 4096, 14336), (19, 2048, 7168)])
-def test_mlp_decode_persistent(dev, m, h, inter):
-    """gate/up -> down in one persistent launch (flag hand-off per k-slice) must equal the two-launch
-    path bit for bit (same tiles, same reduction order) and the fp32 reference; x aliases the
-    residual as in the model; flags re-arm across launches; no hand-off wait gives up."""
-    assert ops.mlp_decode_ok(h, inter)
-    x0 = torch.randn(m, h, device=dev, dtype=torch.bfloat16) * 2
-    wgu = torch.randn(2 * inter, h, device=dev, dtype=torch.bfloat16) / math.sqrt(h)
-    wd = torch.randn(h, inter, device=dev, dtype=torch.bfloat16) / math.sqrt(inter)
-    tin = h // 64
-    ssp_in = torch.zeros(tin, 32, device=dev)
-    ssp_in[:, :m] = x0.float().pow(2).view(m, tin, 64).sum(-1).t()
-    td = h // 64
-    flags = torch.zeros(8, dtype=torch.int32, device=dev)
-    err = torch.zeros(1, dtype=torch.int32, device=dev)
-    cnt = torch.zeros(td, dtype=torch.int32, device=dev)
-    cnt2 = torch.zeros(td, dtype=torch.int32, device=dev)
-    for it in range(3):
-        h1 = x0.clone()
-        ssp1 = torch.full((td, 32), -1.0, device=dev)
-        ops.mlp_decode(h1, wgu, wd, ssp_in, 1e-5, h1, ssp1, cnt, flags, err)
-        h2 = x0.clone()
-        ssp2 = torch.full((td, 32), -1.0, device=dev)
-        act = ops.linear_silu_mul_rownorm(h2, wgu, ssp_in, 1e-5, 112)
-        ops.linear_slab_residual(act, wd, h2, ssp2, cnt2, 64, 4)
-        torch.cuda.synchronize()
-        assert int(err.item()) == 0
-        assert int(flags.abs().sum()) == 0 and int(cnt.abs().sum()) == 0
-        assert torch.equal(h1, h2), (h1.float() - h2.float()).abs().max()
-        assert torch.equal(ssp1, ssp2)
-    xn = x0.float() * torch.rsqrt(x0.float().pow(2).mean(-1, keepdim=True) + 1e-5)
-    gu = xn @ wgu.float().t()
-    ref_h = x0.float() + (torch.nn.functional.silu(gu[:, :inter]) * gu[:, inter:]) @ wd.float().t()
-    close(h1, ref_h.to(torch.bfloat16), atol=6e-2, rtol=2e-2)
+@pytest.mark.parametrize("mode,n,k,wr,sk", [(0, 1024, 4096, 64, 1), (1, 1792, 4096, 112, 1), (2, 4096, 4096, 64, 4),
+                                            (2, 6144, 4096, 48, 2), (4, 2304, 1024, 96, 1)])
+def test_gemm_decode_tiled_weights(dev, mode, n, k, wr, sk):
+    """Weights pre-packed in the kernel's tile order (ops.gd_pack_weights; one linear 1-KiB read per
+    LDS-DMA piece) give bit-identical results to the row-major layout in every epilogue."""
+    m = 19
+    x = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
+    rows = 2 * n if mode in (1, 4) else n
+    w = torch.randn(rows, k, device=dev, dtype=torch.bfloat16) / math.sqrt(k)
+    wt = ops.gd_pack_weights(w, wr, silu=mode in (1, 4))
+    if mode == 4:
+        ssp = x.float().pow(2).sum(-1).view(1, m)
+        ssp_in = torch.zeros(1, 32, device=dev)
+        ssp_in[0, :m] = ssp
+        a = ops.linear_silu_mul_rownorm(x, w, ssp_in, 1e-5, wr)
+        b = ops.linear_silu_mul_rownorm(x, wt, ssp_in, 1e-5, wr, tiled=True)
+    else:
+        a = ops.gemm_decode(x, w, mode=mode, wr=wr, sk=sk)
+        b = ops.gemm_decode(x, wt, mode=mode | 32, wr=wr, sk=sk)
+    assert torch.equal(a, b)
+    if mode == 0:
+        close(a, x.float() @ w.float().t(), atol=2e-2, rtol=1e-2)
 
 
 @pytest.mark.parametrize("g,hkv,big", [(4, 8, False), (8, 1, False), (1, 4, False), (4, 8, True), (4, 8, "v4")])
