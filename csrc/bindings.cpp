@@ -398,6 +398,10 @@ void gd_set_timestamps(Tensor t) {
   g_gd_ts = t.numel() ? reinterpret_cast<long long*>(t.data_ptr<int64_t>()) : nullptr;
 }
 
+void attn_set_timestamps(Tensor t) {
+  die::attn_set_timestamps(t.numel() ? reinterpret_cast<long long*>(t.data_ptr<int64_t>()) : nullptr);
+}
+
 void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t sk, bool nt, Tensor resid,
                  Tensor ssp_out, Tensor counters, Tensor ssp_in, double eps) {
   DIE_CHECK_CUDA(x);
@@ -731,6 +735,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_grouped_gemm", &moe_grouped_gemm);
   m.def("gemm_decode", &gemm_decode);
   m.def("gd_set_timestamps", &gd_set_timestamps);
+  m.def("attn_set_timestamps", &attn_set_timestamps);
   m.def("row_sumsq", &row_sumsq);
   m.def("residual_add_sumsq", &residual_add_sumsq);
   m.def("decode_advance", &decode_advance);

@@ -639,6 +639,10 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
   const int np = (maxp + C - 1) / C;
   const int n_tasks = pairs * np;
   const int pch = lane & 15;
+  // diagnostics (bench/micro_attn_timeline.py): [entry, first chunk landed, prologue done, stream done,
+  // end, xcc] of the workgroup's LAST task, s_memrealtime (100 MHz)
+  long long tsv[5] = {0, 0, 0, 0, 0};
+  if (fz.ts != nullptr) tsv[0] = __builtin_amdgcn_s_memrealtime();
 
 #pragma unroll 1
   for (int t = blockIdx.x; t < n_tasks; t += gridDim.x) {
@@ -674,11 +678,13 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
       }
     };
 
-    issue(c0, 0);
     const bool has_new = FUSED && c1 == nch;  // this part holds the step's new token (key ctx-1)
     char* fa = smem + 2 * V3_BUF;            // FUSED staging (merge area, idle at a task start)
     const int frows = fz.sk * (G + 2);       // slab rows: [s][q heads..., k, v] x 128 fp32
     const int fs_off = ((frows + 1) / 2) * 1024;
+    // Issue order: the prologue's small operands first, then chunk c0 and (if any) chunk c0+1, so the
+    // prologue (FUSED: slab sum, norm scale, RoPE, KV write) runs while both chunks stream in; only a
+    // counted vmcnt separates them (the chunks stay in flight).
     if constexpr (FUSED) {
       if (!(dbg & 2)) {
         const float* srow = fz.slab + (int64_t)seq * fz.width;
@@ -704,66 +710,78 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
         glds16(qb + qr * D + (lane & 15) * 8, smem + V3_CHUNK + i * 1024);
       }
     }
+    issue(c0, 0);
+    const bool two = c0 + 1 < c1;
+    if (two) issue(c0 + 1, 1);
     State st;
     init_state(st);
     bf16x8_t qf[8];
     bf16_t nk0 = 0, nk1 = 0, nv = 0;  // FUSED: the new token's rotated key pair / value element
+    if constexpr (FUSED) {
+      if (two)
+        wait_vm<32>();  // the prologue operands landed; chunks c0 and c0+1 stay in flight
+      else
+        wait_vm<16>();
+      __builtin_amdgcn_s_barrier();
+      // r = rsqrt(mean(h^2) + eps) of this sequence's row
+      float ssum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        ssum += lane + 64 * i < fz.ssp_tiles ? lds_ld32(lds_addr(fa + fs_off + 4 * (lane + 64 * i))) : 0.f;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) ssum += __shfl_xor(ssum, o, 64);
+      const float rn = rsqrtf(ssum * fz.inv_n + fz.eps);
+      const uint32_t cs = lds_addr(fa + fs_off + 512);
+      auto slab_sum = [&](int j, int d) {
+        float v = 0.f;
+        for (int sl = 0; sl < fz.sk; ++sl) v += lds_ld32(lds_addr(fa + ((sl * (G + 2) + j) * D + d) * 4));
+        return v * rn;
+      };
+      for (int it = tid; it < G * 64; it += 256) {  // rotated query rows -> q image (bf16)
+        const int j = it >> 6, p = it & 63;
+        const float a = slab_sum(j, p), bq = slab_sum(j, p + 64);
+        const float co = lds_ld32(cs + 4 * p), si = lds_ld32(cs + 4 * (p + 64));
+        const uint32_t qa = lds_addr(smem + V3_CHUNK + j * 256);
+        lds_st16(qa + 2 * p, f2bf(a * co - bq * si));
+        lds_st16(qa + 2 * (p + 64), f2bf(bq * co + a * si));
+      }
+      if (tid < 64) {  // new key, rotated
+        const float a = slab_sum(G, tid), bq = slab_sum(G, tid + 64);
+        const float co = lds_ld32(cs + 4 * tid), si = lds_ld32(cs + 4 * (tid + 64));
+        nk0 = f2bf(a * co - bq * si);
+        nk1 = f2bf(bq * co + a * si);
+      } else if (tid < 192) {
+        nv = f2bf(slab_sum(G + 1, tid - 64));
+      }
+      // the q image is read after the chunk wait's barrier below: retire this wave's LDS writes first
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
 #pragma unroll 1
     for (int c = c0; c < c1; ++c) {
       const int b = (c - c0) & 1;
       if (c + 1 < c1) {
-        issue(c + 1, b ^ 1);
+        if (c > c0) issue(c + 1, b ^ 1);
         wait_vm<16>();  // chunk c (and the query rows) landed; chunk c+1 stays in flight
       } else {
         wait_vm<0>();
       }
       __builtin_amdgcn_s_barrier();
+      if (fz.ts != nullptr && c == c0) tsv[1] = __builtin_amdgcn_s_memrealtime();
       const char* base = smem + b * V3_BUF;
       if constexpr (FUSED) {
-        if (c == c0) {
-          // r = rsqrt(mean(h^2) + eps) of this sequence's row
-          float ssum = 0.f;
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-            ssum += lane + 64 * i < fz.ssp_tiles ? lds_ld32(lds_addr(fa + fs_off + 4 * (lane + 64 * i))) : 0.f;
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) ssum += __shfl_xor(ssum, o, 64);
-          const float rn = rsqrtf(ssum * fz.inv_n + fz.eps);
-          const uint32_t cs = lds_addr(fa + fs_off + 512);
-          auto slab_sum = [&](int j, int d) {
-            float v = 0.f;
-            for (int sl = 0; sl < fz.sk; ++sl) v += lds_ld32(lds_addr(fa + ((sl * (G + 2) + j) * D + d) * 4));
-            return v * rn;
-          };
-          for (int it = tid; it < G * 64; it += 256) {  // rotated query rows -> q image (bf16)
-            const int j = it >> 6, p = it & 63;
-            const float a = slab_sum(j, p), bq = slab_sum(j, p + 64);
-            const float co = lds_ld32(cs + 4 * p), si = lds_ld32(cs + 4 * (p + 64));
-            const uint32_t qa = lds_addr(smem + V3_CHUNK + j * 256);
-            lds_st16(qa + 2 * p, f2bf(a * co - bq * si));
-            lds_st16(qa + 2 * (p + 64), f2bf(bq * co + a * si));
-          }
-          if (tid < 64) {  // new key, rotated
-            const float a = slab_sum(G, tid), bq = slab_sum(G, tid + 64);
-            const float co = lds_ld32(cs + 4 * tid), si = lds_ld32(cs + 4 * (tid + 64));
-            nk0 = f2bf(a * co - bq * si);
-            nk1 = f2bf(bq * co + a * si);
-          } else if (tid < 192) {
-            nv = f2bf(slab_sum(G + 1, tid - 64));
-          }
-          if (has_new) {
-            const int64_t slot = slot_mapping[seq];  // -1: padded graph row, no write
-            if (slot >= 0) {  // the paged cache, for later steps (this step reads the LDS patch)
-              const int64_t base_kv = ((slot >> 4) * hkv + kvh) * 16 * D + (slot & 15) * D;
-              if (tid < 64) {
-                k_cache[base_kv + tid] = nk0;
-                k_cache[base_kv + tid + 64] = nk1;
-              } else if (tid < 192) {
-                v_cache[base_kv + tid - 64] = nv;
-              }
+        if (has_new && c == c0) {
+          // the paged cache, for later steps (this step reads the LDS patch); stored only now so the
+          // stores do not sit in the vmcnt queue ahead of the counted chunk waits above
+          const int64_t slot = slot_mapping[seq];  // -1: padded graph row, no write
+          if (slot >= 0) {
+            const int64_t base_kv = ((slot >> 4) * hkv + kvh) * 16 * D + (slot & 15) * D;
+            if (tid < 64) {
+              k_cache[base_kv + tid] = nk0;
+              k_cache[base_kv + tid + 64] = nk1;
+            } else if (tid < 192) {
+              v_cache[base_kv + tid - 64] = nv;
             }
           }
-          lds_barrier();
         }
         if (has_new && c + 1 == c1) {  // patch key ctx-1 into this chunk's K / V images
           const int rr = (ctx - 1) - c * DEC_KEYS;
@@ -783,6 +801,7 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
         for (int kk = 0; kk < 8; ++kk)
           qf[kk] = row < G ? as_frag(*reinterpret_cast<const uint4*>(smem + V3_CHUNK + row * 256 + (2 * kk + h) * 16))
                            : zero_frag();
+        if (fz.ts != nullptr) tsv[2] = __builtin_amdgcn_s_memrealtime();
       }
       if (!(dbg & 1)) {
         const int kb = c * DEC_KEYS + 32 * wave;  // keys >= ctx: clamped rows, masked to -inf
@@ -792,6 +811,7 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
       }
       lds_barrier();  // buffer b is refilled by the next iteration
     }
+    if (fz.ts != nullptr) tsv[3] = __builtin_amdgcn_s_memrealtime();
     if (dbg & 32) continue;
 
     // merge the 4 waves' (m, l, O) through LDS
@@ -895,300 +915,13 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
     }
     lds_barrier();  // merge area and buffers are reused by the next task
   }
-}
-
-
-// v4: the v3 kernel at half the workgroup (2 waves, 64-key chunks, 77 KiB of LDS) so TWO workgroups
-// share a CU, and every (sequence, kv head) pair's actual context split into two halves (merged by the
-// same ticket / last-arriver as v3). Profiling v3 at batch 32 (rocprofv3 PMC: 80 of ~150 possible
-// outstanding L1 misses per CU on average, 50 % of cycles stalled on pending misses) showed each CU's
-// miss capacity idle during a task's serial phases — first-chunk latency, the prologue's dependent
-// loads, the final merge and store. With two co-resident workgroups one's serial phase overlaps the
-// other's streaming. Used when the pairs fill the chip (pairs >= CUs); v3's static split otherwise.
-// MEASURED: a tie (19.8 vs v3's 19.4 us at 32 x ~576 keys; bench 46.9 req/s either way), so it is
-// opt-in (DIE_ATTN_V4=1): the idle miss capacity is not the wall — the per-request latency of the
-// paged, permuted KV is (TLB: ~2.9 K UTCL1 translation misses per dispatch at 1.3 M requests).
-constexpr int V4_KEYS = 64;                                     // keys per chunk (2 waves x 32)
-constexpr int V4_CHUNK = 2 * V4_KEYS * DEC_ROW;                 // K + V images: 32 KiB
-constexpr int V4_QIMG = 2048;
-constexpr int V4_BUF = V4_CHUNK + V4_QIMG;
-constexpr int V4_ML = 2 * 32 * 2 * 4;
-constexpr int V4_MERGE = V4_ML + 2 * 8 * D * 4;                 // 8.5 KiB (also the FUSED staging area)
-constexpr int V4_LDS = 2 * V4_BUF + V4_MERGE + 16;              // 78,352 B: two workgroups per CU
-static_assert(2 * V4_LDS <= 160 * 1024, "two v4 workgroups must fit one CU's LDS");
-
-template <int G, bool FUSED>
-__global__ void __launch_bounds__(128, 2) attn_decode_v4_kernel(
-    bf16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters,
-    const bf16_t* __restrict__ q, int64_t q_stride, bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
-    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, int num_seqs, int hq,
-    int hkv, float scale_log2, int maxp, int dbg, AttnDecodeFuse fz, const int64_t* __restrict__ slot_mapping) {
-  constexpr int QI = (G * 256 + 1023) / 1024;  // LDS-DMA instructions for the query rows
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* ml = reinterpret_cast<float*>(smem + 2 * V4_BUF);
-  float* ob = reinterpret_cast<float*>(smem + 2 * V4_BUF + V4_ML);
-  int* ctl = reinterpret_cast<int*>(smem + 2 * V4_BUF + V4_MERGE);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, row = lane & 31;
-  const int pairs = num_seqs * hkv;
-  const int n_tasks = pairs * 2;  // every (sequence, kv head): its actual context split in two halves
-  const int pch = lane & 15;
-
-#pragma unroll 1
-  for (int t = blockIdx.x; t < n_tasks; t += gridDim.x) {
-    const int pair = t % pairs, part = t / pairs;
-    const int seq = pair / hkv, kvh = pair - seq * hkv;
-    const int ctx = __builtin_amdgcn_readfirstlane(ctx_lens[seq]);
-    const int nch = (ctx + V4_KEYS - 1) / V4_KEYS;
-    const int c0 = part * nch / 2, c1 = (part + 1) * nch / 2;
-    if (c0 >= c1) continue;  // uniform (a one-chunk context has one non-empty half)
-    const int* bt = block_tables + (int64_t)seq * bt_stride;
-    const int last_blk = (ctx - 1) >> 4;
-
-    // LDS-DMA chunk c (K and V rows of 128 keys) into buffer b: 16 instructions per lane.
-    auto issue = [&](int c, int b) {
-      if (dbg & 2) return;
-      char* base = smem + b * V4_BUF;
-      // this wave's two 16-key blocks of the chunk; the table row is read speculatively
-      // (clamped to the row, not to the context) so the loads do not wait for ctx
-      const int j0 = c * (V4_KEYS / 16) + 2 * wave;
-      const int e0 = bt[__builtin_amdgcn_readfirstlane(min(j0, bt_stride - 1))];
-      const int e1 = bt[__builtin_amdgcn_readfirstlane(min(j0 + 1, bt_stride - 1))];
-      const int el = j0 + 1 > last_blk ? bt[last_blk] : 0;  // only the context's last chunk needs it
+  if (fz.ts != nullptr && tid == 0) {
+    tsv[4] = __builtin_amdgcn_s_memrealtime();
+    int xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int r = (wave * 8 + i) * 4 + (lane >> 4);            // image row = key in chunk
-        const int j = j0 + (i >> 2);
-        const int64_t blk = j <= last_blk ? (i < 4 ? e0 : e1) : el; // past the context: last block
-        const int key = min(c * V4_KEYS + r, ctx - 1);            // clamp: never read past the context
-        const int64_t roff = ((blk * hkv + kvh) * 16 + (key & 15)) * D;
-        glds16(k_cache + roff + (pch ^ (r & 15)) * 8, base + (wave * 8 + i) * 1024);
-        glds16(v_cache + roff + (pch ^ ((r & 3) << 2)) * 8, base + V4_KEYS * DEC_ROW + (wave * 8 + i) * 1024);
-      }
-    };
-
-    issue(c0, 0);
-    const bool has_new = FUSED && c1 == nch;  // this part holds the step's new token (key ctx-1)
-    char* fa = smem + 2 * V4_BUF;            // FUSED staging (merge area, idle at a task start)
-    const int frows = fz.sk * (G + 2);       // slab rows: [s][q heads..., k, v] x 128 fp32
-    const int fs_off = ((frows + 1) / 2) * 1024;
-    if constexpr (FUSED) {
-      if (!(dbg & 2)) {
-        const float* srow = fz.slab + (int64_t)seq * fz.width;
-        for (int i = wave; i < (frows + 1) / 2; i += 2) {
-          const int ri = min(2 * i + (lane >> 5), frows - 1);
-          const int sl = ri / (G + 2), j = ri - sl * (G + 2);
-          const int col = j < G ? (kvh * G + j) * D : (j == G ? (hq + kvh) * D : (hq + hkv + kvh) * D);
-          glds16(srow + sl * fz.slab_stride + col + (lane & 31) * 4, fa + i * 1024);
-        }
-        if (wave == 0) {
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-            glds4(fz.ssp + min(lane + 64 * i, fz.ssp_tiles - 1) * 32 + seq, fa + fs_off + i * 256);
-        }
-        if (wave == 1)  // decode: the new token sits at position ctx - 1
-          glds16(fz.cos_sin + (int64_t)(ctx - 1) * D + (lane & 31) * 4, fa + fs_off + 512);
-      }
-    } else if (wave == 0 && !(dbg & 2)) {  // the G query rows of this (seq, kv head), 256 B each
-      const bf16_t* qb = q + (int64_t)seq * q_stride + (int64_t)kvh * G * D;
-#pragma unroll
-      for (int i = 0; i < QI; ++i) {
-        const int qr = min(4 * i + (lane >> 4), G - 1);
-        glds16(qb + qr * D + (lane & 15) * 8, smem + V4_CHUNK + i * 1024);
-      }
-    }
-    State st;
-    init_state(st);
-    bf16x8_t qf[8];
-    bf16_t nk0 = 0, nk1 = 0, nv = 0, nv1 = 0;  // FUSED: the new token's rotated key pair / value elements
-#pragma unroll 1
-    for (int c = c0; c < c1; ++c) {
-      const int b = (c - c0) & 1;
-      if (c + 1 < c1) {
-        issue(c + 1, b ^ 1);
-        wait_vm<16>();  // chunk c (and the query rows) landed; chunk c+1 stays in flight
-      } else {
-        wait_vm<0>();
-      }
-      __builtin_amdgcn_s_barrier();
-      const char* base = smem + b * V4_BUF;
-      if constexpr (FUSED) {
-        if (c == c0) {
-          // r = rsqrt(mean(h^2) + eps) of this sequence's row
-          float ssum = 0.f;
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-            ssum += lane + 64 * i < fz.ssp_tiles ? lds_ld32(lds_addr(fa + fs_off + 4 * (lane + 64 * i))) : 0.f;
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) ssum += __shfl_xor(ssum, o, 64);
-          const float rn = rsqrtf(ssum * fz.inv_n + fz.eps);
-          const uint32_t cs = lds_addr(fa + fs_off + 512);
-          auto slab_sum = [&](int j, int d) {
-            float v = 0.f;
-            for (int sl = 0; sl < fz.sk; ++sl) v += lds_ld32(lds_addr(fa + ((sl * (G + 2) + j) * D + d) * 4));
-            return v * rn;
-          };
-          for (int it = tid; it < G * 64; it += 128) {  // rotated query rows -> q image (bf16)
-            const int j = it >> 6, p = it & 63;
-            const float a = slab_sum(j, p), bq = slab_sum(j, p + 64);
-            const float co = lds_ld32(cs + 4 * p), si = lds_ld32(cs + 4 * (p + 64));
-            const uint32_t qa = lds_addr(smem + V4_CHUNK + j * 256);
-            lds_st16(qa + 2 * p, f2bf(a * co - bq * si));
-            lds_st16(qa + 2 * (p + 64), f2bf(bq * co + a * si));
-          }
-          if (tid < 64) {  // new key, rotated
-            const float a = slab_sum(G, tid), bq = slab_sum(G, tid + 64);
-            const float co = lds_ld32(cs + 4 * tid), si = lds_ld32(cs + 4 * (tid + 64));
-            nk0 = f2bf(a * co - bq * si);
-            nk1 = f2bf(bq * co + a * si);
-          } else {  // threads 64..127: value elements d and d + 64
-            nv = f2bf(slab_sum(G + 1, tid - 64));
-            nv1 = f2bf(slab_sum(G + 1, tid));
-          }
-          if (has_new) {
-            const int64_t slot = slot_mapping[seq];  // -1: padded graph row, no write
-            if (slot >= 0) {  // the paged cache, for later steps (this step reads the LDS patch)
-              const int64_t base_kv = ((slot >> 4) * hkv + kvh) * 16 * D + (slot & 15) * D;
-              if (tid < 64) {
-                k_cache[base_kv + tid] = nk0;
-                k_cache[base_kv + tid + 64] = nk1;
-              } else {
-                v_cache[base_kv + tid - 64] = nv;
-                v_cache[base_kv + tid] = nv1;
-              }
-            }
-          }
-          lds_barrier();
-        }
-        if (has_new && c + 1 == c1) {  // patch key ctx-1 into this chunk's K / V images
-          const int rr = (ctx - 1) - c * V4_KEYS;
-          const uint32_t kimg = lds_addr(base) + rr * DEC_ROW, vimg = kimg + V4_KEYS * DEC_ROW;
-          if (tid < 64) {
-            lds_st16(kimg + 16 * ((tid >> 3) ^ (rr & 15)) + 2 * (tid & 7), nk0);
-            lds_st16(kimg + 16 * (((tid + 64) >> 3) ^ (rr & 15)) + 2 * (tid & 7), nk1);
-          } else {
-            const int d = tid - 64, d1 = tid;
-            lds_st16(vimg + 16 * ((d >> 3) ^ ((rr & 3) << 2)) + 2 * (d & 7), nv);
-            lds_st16(vimg + 16 * ((d1 >> 3) ^ ((rr & 3) << 2)) + 2 * (d1 & 7), nv1);
-          }
-          lds_barrier();
-        }
-      }
-      if (c == c0) {
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk)
-          qf[kk] = row < G ? as_frag(*reinterpret_cast<const uint4*>(smem + V4_CHUNK + row * 256 + (2 * kk + h) * 16))
-                           : zero_frag();
-      }
-      if (!(dbg & 1)) {
-        const int kb = c * V4_KEYS + 32 * wave;  // keys >= ctx: clamped rows, masked to -inf
-        f32x16_t s = qk_lds_swz(base + 32 * wave * DEC_ROW, qf, lane);
-        softmax_tile_lazy(s, st, kb, ctx, scale_log2, h);
-        pv_lds_swz_v3(base + V4_KEYS * DEC_ROW + 32 * wave * DEC_ROW, s, st, lane);
-      }
-      lds_barrier();  // buffer b is refilled by the next iteration
-    }
-    if (dbg & 32) continue;
-
-    // merge the 4 waves' (m, l, O) through LDS
-    if (row < G) {
-      if (h == 0) {
-        lds_st32(lds_addr(ml + (wave * 32 + row) * 2 + 0), st.m);
-        lds_st32(lds_addr(ml + (wave * 32 + row) * 2 + 1), st.l);
-      }
-      const uint32_t o = lds_addr(ob + (wave * G + row) * D);
-#pragma unroll
-      for (int db = 0; db < 4; ++db)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4)
-          lds_st128(o + 4 * (32 * db + 8 * g4 + 4 * h),
-                    f32x4_t{st.o[db][4 * g4], st.o[db][4 * g4 + 1], st.o[db][4 * g4 + 2], st.o[db][4 * g4 + 3]});
-    }
-    lds_barrier();
-    const int nparts = nch >= 2 ? 2 : 1;  // non-empty halves of THIS pair
-    for (int e = tid; e < G * (D / 4); e += 128) {
-      const int r = e / (D / 4), d = 4 * (e % (D / 4));
-      float mw[2], lw[2];
-#pragma unroll
-      for (int w = 0; w < 2; ++w) {
-        mw[w] = lds_ld32(lds_addr(ml + (w * 32 + r) * 2));
-        lw[w] = lds_ld32(lds_addr(ml + (w * 32 + r) * 2 + 1));
-      }
-      float M = NEG_BIG;
-#pragma unroll
-      for (int w = 0; w < 2; ++w) M = fmaxf(M, mw[w]);
-      float L = 0.f;
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int w = 0; w < 2; ++w) {
-        const float f = exp2f(mw[w] - M);
-        L += f * lw[w];
-        const f32x4_t v = lds_ld128(lds_addr(ob + (w * G + r) * D + d));
-        acc.x += f * v.x;
-        acc.y += f * v.y;
-        acc.z += f * v.z;
-        acc.w += f * v.w;
-      }
-      const int head = kvh * G + r;
-      if (nparts == 1) {
-        const float inv = L > 0.f ? 1.f / L : 0.f;
-        uint2 pk;
-        pk.x = pack2(acc.x * inv, acc.y * inv);
-        pk.y = pack2(acc.z * inv, acc.w * inv);
-        *reinterpret_cast<uint2*>(out + ((int64_t)seq * hq + head) * D + d) = pk;
-      } else {
-        const int64_t slot = ((int64_t)seq * hq + head) * maxp + part;
-        __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(part_o, 0, 0x7fffffff, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, acc),
-                                               ro, (int)(slot * D + d) * 4, 0, 16);
-        if (d == 0) {
-          __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(part_ml, 0, 0x7fffffff, 0x00020000);
-          const float2 mlv = make_float2(M, L);
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, mlv),
-                                                rm, (int)(slot * 2) * 4, 0, 16);
-        }
-      }
-    }
-    if (nparts > 1) {
-      wait_vm<0>();  // this wave's write-through partial stores are done
-      lds_barrier();
-      if (tid == 0) {
-        const int old = __hip_atomic_fetch_add(counters + pair, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ctl[1] = old == nparts - 1;
-      }
-      lds_barrier();
-      if (ctl[1]) {  // last arriver: merge every part of this pair
-        __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(part_o, 0, 0x7fffffff, 0x00020000);
-        __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(part_ml, 0, 0x7fffffff, 0x00020000);
-        for (int e = tid; e < G * (D / 4); e += 128) {
-          const int r = e / (D / 4), d = 4 * (e % (D / 4));
-          const int head = kvh * G + r;
-          const int64_t s0 = ((int64_t)seq * hq + head) * maxp;
-          float M = NEG_BIG, L = 0.f;
-          float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-          for (int p = 0; p < nparts; ++p) {
-            const auto mv =
-                __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rm, (int)((s0 + p) * 2) * 4, 0, 16));
-            const auto ov = __builtin_bit_cast(
-                float4, __builtin_amdgcn_raw_buffer_load_b128(ro, (int)((s0 + p) * D + d) * 4, 0, 16));
-            const float Mn = fmaxf(M, mv.x);
-            const float a = exp2f(M - Mn), bb = exp2f(mv.x - Mn);
-            L = L * a + mv.y * bb;
-            acc.x = acc.x * a + ov.x * bb;
-            acc.y = acc.y * a + ov.y * bb;
-            acc.z = acc.z * a + ov.z * bb;
-            acc.w = acc.w * a + ov.w * bb;
-            M = Mn;
-          }
-          const float inv = L > 0.f ? 1.f / L : 0.f;
-          uint2 pk;
-          pk.x = pack2(acc.x * inv, acc.y * inv);
-          pk.y = pack2(acc.z * inv, acc.w * inv);
-          *reinterpret_cast<uint2*>(out + ((int64_t)seq * hq + head) * D + d) = pk;
-        }
-        if (tid == 0) __hip_atomic_store(counters + pair, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    lds_barrier();  // merge area and buffers are reused by the next task
+    for (int i = 0; i < 5; ++i) fz.ts[6 * blockIdx.x + i] = tsv[i];
+    fz.ts[6 * blockIdx.x + 5] = xcc;
   }
 }
 
@@ -1251,6 +984,9 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
   return hipGetLastError();
 }
 
+static long long* g_attn_ts = nullptr;
+void attn_set_timestamps(long long* ts) { g_attn_ts = ts; }
+
 hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* counters, const bf16_t* q,
                               int64_t q_stride, bf16_t* k_cache, bf16_t* v_cache, const int* block_tables,
                               int bt_stride, const int* ctx_lens, int num_seqs, int max_ctx, int hq, int hkv,
@@ -1272,37 +1008,15 @@ hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* c
     const int tasks = num_seqs * hkv * maxp3;
     const int ncu = num_cus();
     static const int dbg = getenv("DIE_ATTN_DBG") ? atoi(getenv("DIE_ATTN_DBG")) : 0;  // perf experiments only
-    // opt-in: measured a tie with v3 at batch 32 (19.8 vs 19.4 us, bench 46.9 both; docs/performance.md)
-    const char* v4_env = getenv("DIE_ATTN_V4");  // read per launch (tests toggle it)
-    const int v4_on = v4_env ? atoi(v4_env) : 0;
-    const int pairs = num_seqs * hkv;
-    const bool v4 = v4_on && pairs >= ncu && maxp3 >= 2 &&
-                    (fz == nullptr || ((fz->sk * (G + 2) + 1) / 2) * 1024 + 1536 <= V4_MERGE);
-    if (v4) {
-      dim3 grid4(2 * pairs < 2 * ncu ? 2 * pairs : 2 * ncu), block4(128);
-      const AttnDecodeFuse none4{};
-#define DIE_D4(GG)                                                                                              \
-  case GG:                                                                                                      \
-    if (fz)                                                                                                     \
-      hipLaunchKernelGGL((attn_decode_v4_kernel<GG, true>), grid4, block4, V4_LDS, s, out, part_o, part_ml,     \
-                         counters, q, q_stride, k_cache, v_cache, block_tables, bt_stride, ctx_lens, num_seqs, hq, \
-                         hkv, sl2, maxp3, dbg, *fz, fz->slot_mapping);                                          \
-    else                                                                                                        \
-      hipLaunchKernelGGL((attn_decode_v4_kernel<GG, false>), grid4, block4, V4_LDS, s, out, part_o, part_ml,    \
-                         counters, q, q_stride, k_cache, v_cache, block_tables, bt_stride, ctx_lens, num_seqs, hq, \
-                         hkv, sl2, maxp3, dbg, none4, nullptr);                                                 \
-    break;
-      switch (G) {
-        DIE_D4(1)
-        DIE_D4(2)
-        DIE_D4(4)
-        DIE_D4(8)
-      }
-#undef DIE_D4
-      return hipGetLastError();
-    }
     dim3 grid(tasks < ncu ? tasks : ncu), block(256);
-    const AttnDecodeFuse none{};
+    AttnDecodeFuse none{};
+    none.ts = g_attn_ts;
+    AttnDecodeFuse fzc{};
+    if (fz) {
+      fzc = *fz;
+      fzc.ts = g_attn_ts;
+      fz = &fzc;
+    }
 #define DIE_D3(GG)                                                                                              \
   case GG:                                                                                                      \
     if (fz)                                                                                                     \

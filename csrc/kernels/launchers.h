@@ -39,7 +39,9 @@ struct AttnDecodeFuse {
   float inv_n = 0.f, eps = 0.f;     // 1 / hidden, RMSNorm eps
   const float* cos_sin = nullptr;   // [max_pos][128]: cos | sin, read at position ctx - 1
   const int64_t* slot_mapping = nullptr;
+  long long* ts = nullptr;          // diagnostics: per-workgroup phase stamps [6] (s_memrealtime) or null
 };
+void attn_set_timestamps(long long* ts);  // diagnostics: stamps for every following decode launch
 hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* counters, const bf16_t* q,
                               int64_t q_stride, bf16_t* k_cache, bf16_t* v_cache, const int* block_tables,
                               int bt_stride, const int* ctx_lens, int num_seqs, int max_ctx, int hq, int hkv,

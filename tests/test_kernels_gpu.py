@@ -140,16 +140,13 @@ def test_attn_decode(dev, g, bs, merge):
     assert int(cnt.abs().sum()) == 0
 
 
-@pytest.mark.parametrize("v4", ["0", "1"])
-def test_attn_decode_batch32(dev, v4, monkeypatch):
+def test_attn_decode_batch32(dev):
     """The serving shape: 32 sequences x 8 kv heads (one task per CU, no partials), plus a
     single long sequence (every CU on one pair, all-partials merge)."""
-    monkeypatch.setenv("DIE_ATTN_V4", v4)  # v4: opt-in variant of the self-merging kernel
     hkv, g = 8, 4
     scale = 1 / math.sqrt(128)
-    # 32 x 8 pairs fill the chip: the v4 kernel (two workgroups per CU, each context split in two
-    # halves); the mixed list has one-chunk contexts (one non-empty half: direct output) and 64-key
-    # chunk boundaries; a single long sequence takes v3's static split
+    # the mixed list has one-chunk contexts and chunk boundaries; a single long sequence takes the
+    # static split with every part merged by the last arriver
     mixed = [1, 17, 64, 65, 127, 128, 129] + [300 + 37 * i for i in range(25)]
     for ctxs in ([512 + 7 * i for i in range(32)], mixed, [8000]):
         q, kc, vc, bt, _, ctx, hq = _make_seqs([1] * len(ctxs), ctxs, hkv, 16, dev, g)
@@ -423,12 +420,10 @@ def test_gemm_decode_tiled_weights(dev, mode, n, k, wr, sk):
         close(a, x.float() @ w.float().t(), atol=2e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("g,hkv,big", [(4, 8, False), (8, 1, False), (1, 4, False), (4, 8, True), (4, 8, "v4")])
-def test_attn_decode_fused(dev, g, hkv, big, monkeypatch):
+@pytest.mark.parametrize("g,hkv,big", [(4, 8, False), (8, 1, False), (1, 4, False), (4, 8, True)])
+def test_attn_decode_fused(dev, g, hkv, big):
     """Fused prologue: norm scale + qkv slab sum + RoPE at ctx-1 + KV write, then attention.
-    big: 32 sequences x 8 kv heads; "v4": the same through the opt-in v4 kernel (two workgroups
-    per CU, context halves)."""
-    monkeypatch.setenv("DIE_ATTN_V4", "1" if big == "v4" else "0")
+    big: 32 sequences x 8 kv heads."""
     hq, sk, bs, d = hkv * g, 2, 16, 128
     hid = 1024
     ctxs = [1, 17, 200, 777, 2049]
