@@ -41,7 +41,19 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-METRIC = "req/sec + p50 end-to-end latency, Llama-3-8B batched serving at 1/2/4/8 MI355X"
+METRIC_FMT = "req/sec + p50 end-to-end latency, {model} batched serving at 1/2/4/8 MI355X"
+
+
+def model_label(preset: str) -> str:
+    """Display name of a preset: llama3-8b -> Llama-3-8B, mixtral-8x7b -> Mixtral-8x7B."""
+    from src.models.presets import get_preset
+
+    name = getattr(get_preset(preset), "name", None) or preset
+    if name.startswith("llama3"):
+        name = "Llama-3" + name[len("llama3"):]
+    elif name.startswith("mixtral"):
+        name = "Mixtral" + name[len("mixtral"):]
+    return name.replace("-8b", "-8B").replace("-70b", "-70B").replace("x7b", "x7B")
 
 
 def parse():
@@ -205,8 +217,9 @@ def main():
     total_req = args.steps * args.batch * replicas
     rps = total_req / elapsed
     if rank == 0:
+        label = model_label(args.preset)
         res = {
-            "metric": METRIC,
+            "metric": METRIC_FMT.format(model=label),
             "value": round(rps, 3),
             "unit": "req/s",
             "n_gpus": n_gpus,
@@ -222,7 +235,7 @@ def main():
             "p99_latency_ms": round(1e3 * sorted(lats)[max(0, int(0.99 * len(lats)) - 1)], 2),
             "output_tok_per_s": round(gen_tok * replicas / elapsed, 1),
             "config": {
-                "model": args.preset.replace("llama3", "Llama-3").replace("-8b", "-8B").replace("-70b", "-70B"),
+                "model": label,
                 "global_batch": args.batch * replicas,
                 "seq_len": args.prompt_len + args.gen_len,
                 "prompt_len": args.prompt_len,

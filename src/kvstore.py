@@ -14,18 +14,20 @@ Two caches live here, one per level of the serving stack:
   on-disk persistence (`README.md:14,89`).
 
 * :class:`PagedKVCache` — the GPU KV-block cache: the "kvstore" of the MI355X
-  engine. Blocks live in HBM (one big pool per layer, see
-  :mod:`src.engine.kv_pool`); bookkeeping (free list, ref-counts, prefix-hash
-  index and LRU/TTL eviction of unreferenced cached blocks) is the native C++
-  :class:`BlockManager` (``csrc/runtime/block_manager.cpp``). It exposes the
+  engine. Blocks live in HBM (one pool tensor for all layers, see
+  :class:`src.engine.model_runner.KVPool`); bookkeeping (free list, ref-counts,
+  prefix-hash index and LRU/TTL eviction of unreferenced cached blocks) is the
+  native C++ block manager (``csrc/runtime/block_manager.h``, bound in
+  ``src/_runtime``). It exposes the
   same ``get/set/delete/get_stats`` verbs over block hashes so the coordinator
   and the engine speak one cache vocabulary.
 """
 
 from __future__ import annotations
 
+import json
+import logging
 import os
-import pickle
 import threading
 import time
 from collections import OrderedDict
@@ -33,6 +35,12 @@ from dataclasses import dataclass, field
 from typing import Any, Dict, Generic, Iterable, List, Optional, TypeVar
 
 T = TypeVar("T")
+logger = logging.getLogger(__name__)
+
+
+def _freeze(x):
+    """JSON arrays back to hashable keys (tuples, recursively)."""
+    return tuple(_freeze(v) for v in x) if isinstance(x, list) else x
 
 _POLICIES = ("lru", "lfu", "fifo")
 
@@ -183,24 +191,35 @@ class KVCache:
 
     # ------------------------------------------------------------ persistence
     def save(self, path: Optional[str] = None) -> str:
-        """Snapshot live entries to ``path`` (this process's own file format)."""
+        """Snapshot live entries to ``path`` as JSON (keys and values must be JSON values; tuple
+        keys come back as tuples). Entries that are not JSON-serialisable are skipped. JSON, not
+        pickle: loading a snapshot never executes anything from the file."""
         path = path or self.persist_path
         if not path:
             raise ValueError("no persist path configured")
         with self._lock:
             now = time.time()
             snap = [(k, e.value, e.created_at, e.ttl) for k, e in self.cache.items() if not e.expired(now)]
+        entries, skipped = [], 0
+        for k, v, created, ttl in snap:
+            try:
+                entries.append(json.dumps([k, v, created, ttl]))
+            except (TypeError, ValueError):
+                skipped += 1
+        if skipped:
+            logger.warning("KVCache.save: %d entries are not JSON-serialisable and were not saved", skipped)
         tmp = f"{path}.tmp"
-        with open(tmp, "wb") as f:
-            pickle.dump({"version": 1, "policy": self.eviction_policy, "entries": snap}, f)
+        with open(tmp, "w") as f:
+            f.write('{"version": 2, "policy": %s, "entries": [%s]}' % (json.dumps(self.eviction_policy),
+                                                                        ", ".join(entries)))
         os.replace(tmp, path)
         return path
 
     def load(self, path: Optional[str] = None) -> int:
-        """Restore a snapshot written by :meth:`save` (never a foreign file)."""
+        """Restore a JSON snapshot written by :meth:`save`."""
         path = path or self.persist_path
-        with open(path, "rb") as f:
-            data = pickle.load(f)
+        with open(path) as f:
+            data = json.load(f)
         n = 0
         with self._lock:
             now = time.time()
@@ -209,7 +228,7 @@ class KVCache:
                 if e.expired(now):
                     continue
                 self._evict_if_needed()
-                self.cache[key] = e
+                self.cache[_freeze(key)] = e
                 n += 1
         return n
 

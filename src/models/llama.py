@@ -298,6 +298,29 @@ class CausalLM:
             self.fold_norm_weights()  # checkpoint norm weights -> folded into Wqkv / Wgate_up
         return n
 
+    def reference_copy(self, device="cpu", dtype=torch.float32) -> "CausalLM":
+        """This model's weights (same shard, same folded norms) converted to ``dtype`` on ``device``.
+        On the CPU it runs on the plain-PyTorch reference ops (:mod:`src.ops.reference`): the fp32
+        oracle the GPU engine is checked against at the served shapes (tests/test_oracle_gpu.py).
+        The decode-GEMM tile-order copies are not carried over (they are a GPU layout)."""
+        m = object.__new__(CausalLM)
+        m.__dict__.update({k: v for k, v in self.__dict__.items()
+                           if k not in ("layers", "embed", "norm", "lm_head", "cos_sin")})
+        m.device, m.dtype = torch.device(device), dtype
+
+        def conv(t):
+            return None if t is None else t.detach().to(device=device, dtype=dtype)
+
+        m.embed, m.norm, m.lm_head = conv(self.embed), conv(self.norm), conv(self.lm_head)
+        m.layers = []
+        for lw in self.layers:
+            nl = LayerWeights()
+            for s in ("ln1", "ln2", "qkv", "o", "gate_up", "down", "router", "w13", "w2"):
+                setattr(nl, s, conv(getattr(lw, s)))
+            m.layers.append(nl)
+        m.cos_sin = self.cos_sin.to(device)
+        return m
+
     def weight_bytes(self) -> int:
         tot = self.embed.numel() + self.lm_head.numel() + self.norm.numel()
         for lw in self.layers:

@@ -173,3 +173,23 @@ def test_sampled_generation_is_seeded():
     a = eng.generate([[4, 5, 6]], sp)[0]
     b = eng.generate([[4, 5, 6]], sp)[0]
     assert a == b and len(a) == 6
+
+
+def test_reference_copy_is_an_fp32_twin():
+    """CausalLM.reference_copy (the fp32 oracle of tests/test_oracle_gpu.py): same weights in fp32,
+    independent tensors, same greedy tokens as the source model on the reference ops."""
+    import sys
+
+    sys.path.insert(0, __file__.rsplit("/", 1)[0])
+    from test_oracle_gpu import paged_greedy
+
+    from src.models.llama import CausalLM
+    from src.models.presets import get_preset
+
+    m = CausalLM(get_preset("llama-tiny"), "cpu", dtype=torch.bfloat16, seed=1, max_position=512)
+    r = m.reference_copy("cpu", torch.float32)
+    assert r.layers[0].qkv.dtype == torch.float32 and r.layers[0].qkv.data_ptr() != m.layers[0].qkv.data_ptr()
+    assert torch.equal(r.layers[1].down.to(torch.bfloat16), m.layers[1].down)
+    ps = [[5, 9, 33, 12, 7] * 4, [100, 200, 300]]
+    a, b = paged_greedy(m, ps, 4), paged_greedy(r, ps, 4)
+    assert float((a[2][0] - b[2][0]).norm() / b[2][0].norm()) < 0.02

@@ -200,7 +200,8 @@ TP_PROMPTS = [[5, 9, 33, 12, 7] * 9, [100, 200, 300], list(range(3, 140))]
 def test_tensor_parallel_tp2_on_one_gpu(preset, moe_parallel, sp):
     """The TP=2 code path on real kernels: two ranks share the GPU (gloo, collectives staged
     through the host), Megatron-split weights drawn from the same stream as the TP=1 model;
-    greedy tokens must agree with the TP=1 fp32 reference up to near-ties."""
+    greedy tokens must agree, up to near-ties, with a TP=1 bf16 model built from the same
+    full-size weights (greedy no-cache recompute through the same GPU kernels)."""
     import socket
 
     import torch.multiprocessing as mp

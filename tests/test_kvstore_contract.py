@@ -128,6 +128,22 @@ def test_persistence_roundtrip(tmp_path):
     assert s2.get("a") == {"v": 1} and s2.get("b") == [1, 2]
 
 
+def test_persistence_is_json_not_pickle(tmp_path):
+    """The snapshot is plain JSON (loading never executes file content); tuple keys survive,
+    entries that are not JSON values are skipped rather than pickled."""
+    import json
+
+    p = str(tmp_path / "kv.snap")
+    s = KVCache(max_size=10, persist_path=p)
+    s.set(("llama", "1", 7), "x")
+    s.set("obj", object())
+    s.close()
+    data = json.load(open(p))
+    assert data["version"] == 2 and len(data["entries"]) == 1
+    s2 = KVCache(max_size=10, persist_path=p)
+    assert s2.get(("llama", "1", 7)) == "x" and s2.get("obj") is None
+
+
 def test_thread_safety():
     s = KVCache(max_size=64)
     errs = []
