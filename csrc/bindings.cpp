@@ -195,7 +195,8 @@ void attn_decode_fused(Tensor out, Tensor part_o, Tensor part_ml, Tensor counter
   TORCH_CHECK(block_tables.size(1) * 16 >= max_ctx, "block table narrower than max_ctx");
   DIE_CHECK_DTYPE(ssp, at::kFloat);
   DIE_CHECK_CONTIG(ssp);
-  TORCH_CHECK(ssp.dim() == 2 && ssp.size(1) == 32 && ssp.size(0) >= 1 && ssp.size(0) <= 128, "ssp [T <= 128, 32]");
+  TORCH_CHECK(ssp.dim() == 2 && ssp.size(1) == die::DECODE_SSP_LD && ssp.size(0) >= 1 && ssp.size(0) <= 128,
+              "ssp [T <= 128, 128]");
   DIE_CHECK_DTYPE(positions, at::kLong);
   DIE_CHECK_DTYPE(slot_mapping, at::kLong);
   DIE_CHECK_DTYPE(cos_sin, at::kFloat);
@@ -382,18 +383,23 @@ void moe_grouped_gemm(Tensor y, Tensor x, Tensor w, Tensor offsets) {
                                        (int)N, (int)K, cur_stream()));
 }
 
-// Decode GEMM (M <= 32): x[M, K] @ w^T.
-//   mode 0: y bf16 [M, N], w [N, K]
-//   mode 1: y bf16 [M, N] = silu(x gate^T) * (x up^T), w = [gate; up] [2N, K]
-//   mode 2: y fp32 split-K slabs [sk, M, N], w [N, K]
-// Decode GEMM (gemm_decode.hip). mode 0 bf16, 1 silu*up, 2 fp32 split-K slabs [sk, M, N],
-// 3 slabs + residual update of `resid` [M, N] and row sums of squares `ssp_out` [N/wr, 32]
-// (tickets `counters` [N/wr], zeroed once), 4 = mode 1 with rows scaled by the RMSNorm
-// statistics `ssp_in` [T, 32] (eps; the norm weight is folded into w). Unused fusion tensors
-// may be empty.
+// Decode GEMM (gemm_decode.hip), x [M <= 128, K] @ w^T. mode 0 bf16 y [M, N]; 1 silu(x gate^T) * (x up^T)
+// with w = [gate; up]; 2 fp32 split-K slabs [sk, M, N]; 3 slabs + residual update of `resid` [M, N] and row
+// sums of squares `ssp_out` [N/wr, 128] (tickets `counters` [N/wr], zeroed once); 4 = mode 1 with rows
+// scaled by the RMSNorm statistics `ssp_in` [T, 128] (eps; the norm weight is folded into w). (wr, kc):
+// weight rows and K elements per ring slot of a workgroup. Unused fusion tensors may be empty.
 // Diagnostics: when set (non-empty int64 tensor [>= 3 * workgroups]), every decode-GEMM launch writes
 // per-workgroup [start, end, xcc] s_memrealtime stamps (100 MHz) there (bench/micro_gd_timeline.py).
 static long long* g_gd_ts = nullptr;
+// decode-GEMM tiles that are instantiated (gemm_decode.hip launch_gemm_decode)
+static bool gd_tile_ok(int64_t wr, int64_t kc) {
+  switch (kc) {
+    case 256: return wr == 32 || wr == 48 || wr == 64;
+    case 128: return wr == 32 || wr == 48 || wr == 64 || wr == 96 || wr == 112 || wr == 128;
+    case 64: case 32: return wr == 64 || wr == 128;
+    default: return false;
+  }
+}
 void gd_set_timestamps(Tensor t) {
   g_gd_ts = t.numel() ? reinterpret_cast<long long*>(t.data_ptr<int64_t>()) : nullptr;
 }
@@ -402,8 +408,8 @@ void attn_set_timestamps(Tensor t) {
   die::attn_set_timestamps(t.numel() ? reinterpret_cast<long long*>(t.data_ptr<int64_t>()) : nullptr);
 }
 
-void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t sk, bool nt, Tensor resid,
-                 Tensor ssp_out, Tensor counters, Tensor ssp_in, double eps) {
+void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t kc, int64_t sk, bool nt,
+                 Tensor resid, Tensor ssp_out, Tensor counters, Tensor ssp_in, double eps) {
   DIE_CHECK_CUDA(x);
   DIE_CHECK_BF16(x);
   DIE_CHECK_BF16(w);
@@ -412,14 +418,11 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
   const bool tiled = (mode & 32) != 0;  // w pre-packed by ops.gd_pack_weights for this (mode, wr)
   mode &= 31;
   const int64_t M = x.size(0), K = x.size(1);
-  TORCH_CHECK(M >= 1 && M <= 32, "gemm_decode: 1 <= M <= 32");
-  TORCH_CHECK(wr == 32 || wr == 48 || wr == 64 || wr == 96 || wr == 112 || wr == 128 || wr == 33 || wr == 49 ||
-                  wr == 65,
-              "wr must be one of 32, 48, 64, 96, 112, 128 (or 33 / 49 / 65: the deep-ring variants)");
+  TORCH_CHECK(M >= 1 && M <= 128, "gemm_decode: 1 <= M <= 128");
+  TORCH_CHECK(gd_tile_ok(wr, kc), "gemm_decode: unsupported (wr, kc) tile");
   TORCH_CHECK(mode >= 0 && mode <= 4, "mode");
-  const int64_t kc = (wr >= 96 || (wr & 1)) ? 128 : 256;
-  const int64_t wrr = wr & ~1;  // rows per workgroup
-  TORCH_CHECK(K % (kc * sk) == 0, "gemm_decode: K must be a multiple of the K slot (256, or 128 for wr >= 96) * sk");
+  const int64_t wrr = wr;  // rows per workgroup
+  TORCH_CHECK(K % (kc * sk) == 0, "gemm_decode: K must be a multiple of kc * sk");
   const bool silu = mode == 1 || mode == 4;
   int64_t N, ldy;
   if (mode == 2 || mode == 3) {
@@ -448,7 +451,7 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
     TORCH_CHECK(resid.size(0) >= M && resid.size(1) == N, "resid [M, N]");
     DIE_CHECK_DTYPE(ssp_out, at::kFloat);
     DIE_CHECK_CONTIG(ssp_out);
-    TORCH_CHECK(ssp_out.numel() >= (N / wrr) * 32, "ssp_out [N/wr, 32]");
+    TORCH_CHECK(ssp_out.numel() >= (N / wrr) * die::DECODE_SSP_LD, "ssp_out [N/wr, 128]");
     fz.resid = bf(resid);
     fz.ld_resid = resid.stride(0);
     fz.ssp_out = ssp_out.data_ptr<float>();
@@ -461,15 +464,16 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
   if (mode == 4) {
     DIE_CHECK_DTYPE(ssp_in, at::kFloat);
     DIE_CHECK_CONTIG(ssp_in);
-    TORCH_CHECK(ssp_in.dim() == 2 && ssp_in.size(1) == 32 && ssp_in.size(0) >= 1 && ssp_in.size(0) <= 128,
-                "ssp_in [T <= 128, 32]");
+    TORCH_CHECK(ssp_in.dim() == 2 && ssp_in.size(1) == die::DECODE_SSP_LD && ssp_in.size(0) >= 1 &&
+                    ssp_in.size(0) <= 128,
+                "ssp_in [T <= 128, 128]");
     fz.ssp_in = ssp_in.data_ptr<float>();
     fz.ssp_tiles = (int)ssp_in.size(0);
     fz.inv_n = 1.f / (float)K;
     fz.eps = (float)eps;
   }
   DIE_HIP(die::launch_gemm_decode(y.data_ptr(), ldy, bf(x), x.stride(0), bf(w), (int)M, (int)N, (int)K, (int)mode,
-                                  (int)wr, (int)sk, nt, fz, cur_stream()));
+                                  (int)wr, (int)kc, (int)sk, nt, fz, cur_stream()));
 }
 
 
@@ -513,8 +517,8 @@ void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t m
   // M = all rows: bounds every expert's rows (the kernel picks the 16-row activation image when <= 16)
   TORCH_CHECK(y.size(0) >= 1, "grouped: at least one row");
   DIE_HIP(die::launch_gemm_decode(y.data_ptr(), y.stride(0), bf(x), x.stride(0), bf(w),
-                                  (int)std::min<int64_t>(y.size(0), 32), (int)N, (int)K, (int)mode, (int)wr, 1, true,
-                                  fz, cur_stream()));
+                                  (int)std::min<int64_t>(y.size(0), 32), (int)N, (int)K, (int)mode, (int)wr, (int)kc,
+                                  1, true, fz, cur_stream()));
 }
 
 // Decode-step input advance (decode_step.hip), for multi-step decode windows.
@@ -544,7 +548,8 @@ void residual_add_sumsq(Tensor ssp, Tensor resid, Tensor x) {
   check_rows(resid, "resid");
   DIE_CHECK_DTYPE(ssp, at::kFloat);
   DIE_CHECK_CONTIG(ssp);
-  TORCH_CHECK(x.sizes() == resid.sizes() && x.size(0) <= 32 && ssp.numel() >= 32, "residual_add_sumsq shapes");
+  TORCH_CHECK(x.sizes() == resid.sizes() && x.size(0) <= die::DECODE_SSP_LD && ssp.numel() >= x.size(0),
+              "residual_add_sumsq shapes");
   DIE_HIP(die::launch_residual_add_sumsq(ssp.data_ptr<float>(), bf(resid), bf(x), (int)x.size(0), (int)x.size(1),
                                          resid.stride(0), x.stride(0), cur_stream()));
 }
@@ -555,7 +560,7 @@ void row_sumsq(Tensor ssp, Tensor x) {
   check_rows(x, "x");
   DIE_CHECK_DTYPE(ssp, at::kFloat);
   DIE_CHECK_CONTIG(ssp);
-  TORCH_CHECK(x.size(0) <= 32 && ssp.numel() >= 32, "row_sumsq: x [<= 32, H], ssp [1, 32]");
+  TORCH_CHECK(x.size(0) <= die::DECODE_SSP_LD && ssp.numel() >= x.size(0), "row_sumsq: x [<= 128, H], ssp [1, 128]");
   DIE_HIP(die::launch_row_sumsq(ssp.data_ptr<float>(), bf(x), (int)x.size(0), (int)x.size(1), x.stride(0),
                                 cur_stream()));
 }

@@ -697,7 +697,7 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
         if (wave == 0) {
 #pragma unroll
           for (int i = 0; i < 2; ++i)
-            glds4(fz.ssp + min(lane + 64 * i, fz.ssp_tiles - 1) * 32 + seq, fa + fs_off + i * 256);
+            glds4(fz.ssp + min(lane + 64 * i, fz.ssp_tiles - 1) * DECODE_SSP_LD + seq, fa + fs_off + i * 256);
         }
         if (wave == 1)  // decode: the new token sits at position ctx - 1
           glds16(fz.cos_sin + (int64_t)(ctx - 1) * D + (lane & 31) * 4, fa + fs_off + 512);

@@ -34,7 +34,7 @@ struct AttnDecodeFuse {
   int sk = 0;
   int64_t slab_stride = 0;          // M * width
   int width = 0;                    // (hq + 2 hkv) * 128
-  const float* ssp = nullptr;       // input-norm statistics [ssp_tiles][32]
+  const float* ssp = nullptr;       // input-norm statistics [ssp_tiles][128] (row stride 128)
   int ssp_tiles = 0;
   float inv_n = 0.f, eps = 0.f;     // 1 / hidden, RMSNorm eps
   const float* cos_sin = nullptr;   // [max_pos][128]: cos | sin, read at position ctx - 1
@@ -65,19 +65,21 @@ hipError_t launch_moe_combine(bf16_t* out, const bf16_t* ys, const int* pos, con
 hipError_t launch_moe_grouped_gemm(bf16_t* Y, const bf16_t* X, const bf16_t* W, const int* offsets, int max_rows,
                                    int E, int N, int K, hipStream_t s);
 
-// Fusion operands of the decode GEMM (modes 3 and 4, see gemm_decode.hip).
 hipError_t launch_decode_advance(const int64_t* out, int64_t* ids, int64_t* pos, int* ctx, int64_t* slots,
                                  const int* bt, int bt_width, int64_t* step, int64_t* tokens, int tok_stride,
                                  int* cnt, const int* n_real, int rows, int bs, int k_max, hipStream_t s);
 hipError_t launch_residual_add_sumsq(float* ssp, bf16_t* resid, const bf16_t* x, int rows, int hidden,
                                      int64_t rstride, int64_t xstride, hipStream_t s);
 hipError_t launch_row_sumsq(float* ssp, const bf16_t* x, int rows, int hidden, int64_t stride, hipStream_t s);
+// Fusion operands of the decode GEMM (modes 3 and 4, see gemm_decode.hip). Norm statistics arrays have a
+// row stride of DECODE_SSP_LD = 128 (the largest decode batch).
+constexpr int DECODE_SSP_LD = 128;
 struct GemmDecodeFuse {
   bf16_t* resid = nullptr;       // mode 3: residual stream [M][ld_resid], updated in place
   int64_t ld_resid = 0;
-  float* ssp_out = nullptr;      // mode 3: [N / wr][32] row sums of squares per column tile
+  float* ssp_out = nullptr;      // mode 3: [N / wr][128] row sums of squares per column tile
   int* counters = nullptr;       // mode 3: [N / wr] split-K tickets (zero, re-armed by the kernel)
-  const float* ssp_in = nullptr; // mode 4: producer's [ssp_tiles][32] sums of squares
+  const float* ssp_in = nullptr; // mode 4: producer's [ssp_tiles][128] sums of squares
   int ssp_tiles = 0;
   float inv_n = 0.f;             // 1 / hidden size
   float eps = 0.f;
@@ -90,7 +92,8 @@ struct GemmDecodeFuse {
   long long* ts = nullptr;       // diagnostics: per-workgroup [start, end, xcc] s_memrealtime stamps (or null)
 };
 hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,
-                              int K, int mode, int wr, int sk, bool nt, const GemmDecodeFuse& fz, hipStream_t s);
+                              int K, int mode, int wr, int kc, int sk, bool nt, const GemmDecodeFuse& fz,
+                              hipStream_t s);
 // consumers of fp32 split-K slabs [sk][rows][width]
 hipError_t launch_fused_add_rms_norm_slab(bf16_t* out, const float* slab, int sk, bf16_t* residual, const bf16_t* w,
                                           float eps, int rows, int hidden, int64_t out_stride, hipStream_t s);

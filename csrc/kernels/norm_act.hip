@@ -176,7 +176,7 @@ hipError_t launch_fused_add_rms_norm_slab(bf16_t* out, const float* slab, int sk
 }
 
 // ----------------------------------------------------------------------------
-// Row sums of squares of x [rows <= 32][hidden] into ssp[row] (the [1][32] statistics
+// Row sums of squares of x [rows <= 128][hidden] into ssp[row] (the [1][128] statistics
 // block that the norm-folded decode consumers read). grid = rows, block = 256.
 __global__ void __launch_bounds__(256) row_sumsq_kernel(float* __restrict__ ssp, const bf16_t* __restrict__ x,
                                                         int hidden, int64_t stride) {
@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(256) row_sumsq_kernel(float* __restrict__ ssp,
 
 // resid[row] += x[row] (bf16, in place) and ssp[row] = sum of squares of the new residual:
 // the tensor-parallel form of the decode GEMM's residual epilogue (mode 3), run after the
-// row-parallel projection's all-reduce. grid = rows (<= 32), block = 256.
+// row-parallel projection's all-reduce. grid = rows (<= 128), block = 256.
 __global__ void __launch_bounds__(256) residual_add_sumsq_kernel(float* __restrict__ ssp, bf16_t* __restrict__ resid,
                                                                  const bf16_t* __restrict__ x, int hidden,
                                                                  int64_t rstride, int64_t xstride) {
@@ -228,14 +228,14 @@ __global__ void __launch_bounds__(256) residual_add_sumsq_kernel(float* __restri
 hipError_t launch_residual_add_sumsq(float* ssp, bf16_t* resid, const bf16_t* x, int rows, int hidden,
                                      int64_t rstride, int64_t xstride, hipStream_t s) {
   if (rows == 0) return hipSuccess;
-  if (hidden % 8 || rows > 32) return hipErrorInvalidValue;
+  if (hidden % 8 || rows > DECODE_SSP_LD) return hipErrorInvalidValue;
   hipLaunchKernelGGL(residual_add_sumsq_kernel, dim3(rows), dim3(256), 0, s, ssp, resid, x, hidden, rstride, xstride);
   return hipGetLastError();
 }
 
 hipError_t launch_row_sumsq(float* ssp, const bf16_t* x, int rows, int hidden, int64_t stride, hipStream_t s) {
   if (rows == 0) return hipSuccess;
-  if (hidden % 8 || rows > 32) return hipErrorInvalidValue;
+  if (hidden % 8 || rows > DECODE_SSP_LD) return hipErrorInvalidValue;
   hipLaunchKernelGGL(row_sumsq_kernel, dim3(rows), dim3(256), 0, s, ssp, x, hidden, stride);
   return hipGetLastError();
 }

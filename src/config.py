@@ -80,7 +80,8 @@ class EngineConfig:
     enable_prefix_caching: bool = True
     kv_block_ttl_s: Optional[float] = None  # TTL for cached (unreferenced) KV blocks
     use_cuda_graph: bool = True
-    graph_batch_sizes: List[int] = field(default_factory=lambda: [1, 2, 4, 8, 16, 24, 32])
+    # padded decode batch sizes with a captured hipGraph (those above max_num_seqs are dropped)
+    graph_batch_sizes: List[int] = field(default_factory=lambda: [1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128])
     decode_partition_size: int = 256
     # decode steps replayed back to back on the GPU per host round trip when nothing is waiting
     # for admission (inputs advanced on the device; see src/engine/model_runner.py decode_multi)

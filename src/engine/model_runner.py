@@ -122,7 +122,8 @@ class ModelRunner:
             self.part_o = torch.empty(self.max_seqs * hq * maxp * 128, dtype=torch.float32, device=dev)
             self.part_ml = torch.empty(self.max_seqs * hq * maxp * 2, dtype=torch.float32, device=dev)
             self.attn_cnt = torch.zeros(self.max_seqs * model.hkv, dtype=i32, device=dev)
-            self.dec_scratch = model.alloc_decode_scratch() if hasattr(model, "alloc_decode_scratch") else None
+            self.dec_scratch = (model.alloc_decode_scratch(self.max_seqs) if hasattr(model, "alloc_decode_scratch")
+                                else None)
         else:
             self.part_o = self.part_ml = self.attn_cnt = self.dec_scratch = None
         self.supports_swap = type(self)._sync_step is ModelRunner._sync_step

@@ -52,16 +52,13 @@ class AttnMetadata:
 
 
 class LayerWeights:
-    __slots__ = ("ln1", "ln2", "qkv", "o", "gate_up", "down", "router", "w13", "w2",
-                 "qkv_t", "o_t", "gate_up_t", "down_t")  # *_t: decode-GEMM tile-order copies (or None)
+    # tiled: decode-GEMM tile-order copies {(projection, wr, kc): tensor} (CausalLM.pack_decode_weights)
+    __slots__ = ("ln1", "ln2", "qkv", "o", "gate_up", "down", "router", "w13", "w2", "tiled")
 
     def __init__(self):
         for s in self.__slots__:
             setattr(self, s, None)
-
-
-def _w(w: torch.Tensor, w_tiled: Optional[torch.Tensor]) -> torch.Tensor:
-    return w if w_tiled is None else w_tiled
+        self.tiled = {}
 
 
 # LDS staging area of the fused decode attention's prologue (csrc/kernels/attention.hip V3_MERGE)
@@ -226,7 +223,7 @@ class CausalLM:
         tensors consumed. ``fold``: fold the norm weights into Wqkv / Wgate_up afterwards (pass
         False while streaming several files, then call :meth:`fold_norm_weights` once)."""
         for lw in self.layers:  # decode tile-order copies go stale: re-packed by alloc_decode_scratch
-            lw.qkv_t = lw.o_t = lw.gate_up_t = lw.down_t = None
+            lw.tiled = {}
         a, d, r, ws = self.arch, self.head_dim, self.tp.rank, self.tp.world_size
         hq, hkv, inter = self.hq, self.hkv, self.inter
         kv_idx = (r * hkv) if a.num_kv_heads >= ws else r // (ws // a.num_kv_heads)
@@ -326,7 +323,7 @@ class CausalLM:
         for lw in self.layers:
             for s in LayerWeights.__slots__:
                 t = getattr(lw, s)
-                if t is not None:
+                if isinstance(t, torch.Tensor):
                     tot += t.numel()
         return tot * self.embed.element_size()
 
@@ -338,7 +335,7 @@ class CausalLM:
         eps = self.arch.rms_eps
         residual = F.embedding(input_ids, self.embed)
         if self._slab_path(input_ids):
-            if meta.scratch is not None and not meta.is_prefill and self._fused_decode_ok(kv_pool):
+            if meta.scratch is not None and not meta.is_prefill and self._fused_decode_ok(kv_pool, input_ids.shape[0]):
                 return self._forward_decode_fused(residual, positions, meta, kv_pool)
             if not self.tp.enabled and not self.arch.is_moe:  # the slab fallback is dense-only
                 return self._forward_decode_slab(residual, positions, meta, kv_pool)
@@ -402,7 +399,7 @@ class CausalLM:
             h_s = tp.reduce_scatter_rows(padded(self._mlp(lw, tp.all_gather_rows(x_s)[:T])))
         return tp.all_gather_rows(ops.fused_add_rms_norm(h_s, residual, self.norm, eps))[:T]
 
-    # ------------------------------------------------- decode fast path (M <= 32)
+    # ------------------------------------------------- decode fast path (M <= 128)
     def _slab_path(self, input_ids: torch.Tensor) -> bool:
         """Decode-sized steps on the GPU run every projection on the weight-streaming kernel
         (split-K fp32 slabs reduced inside the consumer kernels; no separate reduction or SiLU
@@ -435,73 +432,95 @@ class CausalLM:
             slab = ops.linear_slab(ops.linear_silu_mul(x, lw.gate_up), lw.down)
         return ops.fused_add_rms_norm_slab(slab, residual, self.norm, eps)
 
-    # ----------------------------------------- fused decode path (norms folded, M <= 32)
-    def decode_plan(self) -> dict:
-        """Decode-GEMM tiles of the fused path: (wr, sk) of the qkv slab projection and of the
-        residual-updating o / down projections (wr in {32, 64, 128}: one norm-statistics tile
-        per wr output columns)."""
+    # ----------------------------------------- fused decode path (norms folded, M <= 128)
+    @staticmethod
+    def decode_bucket(m: int) -> int:
+        """Row bucket of a decode step: the activation image of its GEMMs (32, 64 or 128 rows)."""
+        return 32 if m <= 32 else (64 if m <= 64 else 128)
+
+    def decode_plan(self, m: int = 32) -> dict:
+        """Decode-GEMM tiles of the fused path for steps of ``m`` rows: (wr, kc, sk) of the qkv slab
+        projection and of the residual-updating o / down projections (wr in {32, 64, 128}: one
+        norm-statistics tile per wr output columns), (wr, kc) of the gate/up projection."""
         h, d = self.arch.hidden_size, self.head_dim
+        b = self.decode_bucket(m)
         # the fused attention stages sk x (G + 2) slab rows of 512 B (+ 1.5 KiB) in its 27 KiB merge
         # area (V3_MERGE_BYTES): at most 50 rows
         g = max(1, self.hq // self.hkv)
-        wq, sq = ops._cfg_for(self.layers[0].qkv.shape[0], h, 2, max_sk=max(1, 50 // (g + 2)))
+        qkv = ops.decode_tile(self.layers[0].qkv.shape[0], h, 2, b, max_sk=max(1, 50 // (g + 2)))
+        o = ops.decode_tile(h, self.hq * d, 3, b)
+        down = ops.decode_tile(h, self.inter, 3, b) if not self.arch.is_moe else None
+        gu = ops.decode_tile(self.inter, h, 4, b)[:2] if not self.arch.is_moe else None
+        return {"qkv": qkv, "o": o, "down": down, "gate_up": gu}
 
-        def resid_cfg(k):
-            c = ops.DECODE_GEMM_RESID_CFG.get((h, k))
-            if c is not None:
-                return c
-            wr, sk = ops._cfg_for(h, k, 2)
-            if wr not in (32, 64, 128) or h % wr:
-                wr = 64 if h % 64 == 0 else 32
-            while sk > 1 and k % (256 * sk):
-                sk //= 2
-            return wr, sk
+    def _packed_layouts(self, buckets) -> set:
+        """(projection, wr, kc) tile-order copies the fused path uses for these row buckets."""
+        need = set()
+        for b in buckets:
+            p = self.decode_plan(b)
+            need.add(("qkv", *p["qkv"][:2]))
+            need.add(("gate_up", *p["gate_up"][:2]))
+            if not self.tp.enabled:
+                need.add(("o", *p["o"][:2]))
+                need.add(("down", *p["down"][:2]))
+        return need
 
-        gu = ops._cfg_for(self.inter, h, 1)[0] if not self.arch.is_moe else None
-        return {"qkv": (wq, sq), "o": resid_cfg(self.hq * d), "down": resid_cfg(self.inter), "gate_up": gu}
-
-    def pack_decode_weights(self) -> bool:
-        """Keep a second copy of the dense projections in the decode GEMM's tile order
-        (ops.gd_pack_weights: every LDS-DMA piece one linear 1-KiB read) for the fused decode path;
-        prefill keeps the row-major copies for hipBLASLt. Costs one more copy of those weights
-        (8B: +13 GiB of the 288 GB HBM), so it is only done when the weights take <= 1/4 of the
-        device memory. DIE_GD_TILED=0 disables it."""
+    def pack_decode_weights(self, buckets=(32,)) -> bool:
+        """Keep copies of the dense projections in the decode GEMM's tile order (ops.gd_pack_weights:
+        every LDS-DMA piece one linear 1-KiB read) for the fused decode path — one per (wr, kc) tile the
+        row buckets' plans use; prefill keeps the row-major copies for hipBLASLt. Only done while the
+        weights and their copies take <= 1/2 of the device memory (8B at batch <= 32: +13 GiB of 288 GB;
+        at batch 128: +34 GiB). DIE_GD_TILED=0 disables it."""
         if os.environ.get("DIE_GD_TILED", "1") == "0" or self.arch.is_moe or not self.norms_folded:
             return False
         if not (self.device.type == "cuda" and ops.native_available()):
             return False
+        need = self._packed_layouts(buckets)
+        lw0 = self.layers[0]
+        extra = sum(getattr(lw0, name).numel() * 2 for name, _, _ in need) * len(self.layers)
         total = torch.cuda.get_device_properties(self.device).total_memory
-        if 2 * self.weight_bytes() > total // 2:
+        if self.weight_bytes() + extra > total // 2:
             return False
-        p = self.decode_plan()
         for lw in self.layers:
-            lw.qkv_t = ops.gd_pack_weights(lw.qkv, p["qkv"][0])
-            if not self.tp.enabled:
-                lw.o_t = ops.gd_pack_weights(lw.o, p["o"][0])
-                lw.down_t = ops.gd_pack_weights(lw.down, p["down"][0])
-            lw.gate_up_t = ops.gd_pack_weights(lw.gate_up, p["gate_up"], silu=True)
+            for name, wr, kc in need:
+                if (name, wr, kc) not in lw.tiled:
+                    lw.tiled[(name, wr, kc)] = ops.gd_pack_weights(getattr(lw, name), wr, silu=name == "gate_up",
+                                                                   kc=kc)
         return True
 
-    def alloc_decode_scratch(self) -> Optional[dict]:
+    @staticmethod
+    def decode_buckets(max_rows: int) -> List[int]:
+        """Row buckets a decode batch of up to ``max_rows`` sequences can fall in."""
+        top = CausalLM.decode_bucket(min(max(1, max_rows), ops.DECODE_GEMM_MAX_M))
+        return [b for b in (32, 64, 128) if b <= top]
+
+    def alloc_decode_scratch(self, max_rows: int = 32) -> Optional[dict]:
         if not (self.device.type == "cuda" and ops.native_available()):
             return None
-        p, h = self.decode_plan(), self.arch.hidden_size
+        h = self.arch.hidden_size
+        buckets = self.decode_buckets(max_rows)
+        plans = {b: self.decode_plan(b) for b in buckets}
         f32, i32 = torch.float32, torch.int32
         # TP: the row-parallel projections are all-reduced first, then one kernel adds into the
         # residual and writes a single statistics tile (so does the MoE block's residual add)
-        to, td = (1, 1) if self.tp.enabled else (h // p["o"][0], 1 if self.arch.is_moe else h // p["down"][0])
+        if self.tp.enabled:
+            to = td = 1
+        else:
+            to = max(h // p["o"][0] for p in plans.values())
+            td = 1 if self.arch.is_moe else max(h // p["down"][0] for p in plans.values())
         if max(to, td) > 128:
             return None
         dev = self.device
-        self.pack_decode_weights()
-        sc = {"plan": p, "ssp0": torch.zeros(1, 32, dtype=f32, device=dev),
-              "ssp_a": torch.zeros(to, 32, dtype=f32, device=dev), "cnt_a": torch.zeros(to, dtype=i32, device=dev),
-              "ssp_b": torch.zeros(td, 32, dtype=f32, device=dev), "cnt_b": torch.zeros(td, dtype=i32, device=dev)}
+        self.pack_decode_weights(buckets)
+        ld = ops.SSP_LD
+        sc = {"plans": plans, "ssp0": torch.zeros(1, ld, dtype=f32, device=dev),
+              "ssp_a": torch.zeros(to, ld, dtype=f32, device=dev), "cnt_a": torch.zeros(to, dtype=i32, device=dev),
+              "ssp_b": torch.zeros(td, ld, dtype=f32, device=dev), "cnt_b": torch.zeros(td, dtype=i32, device=dev)}
         return sc
 
-    def _fused_decode_ok(self, kv_pool: torch.Tensor) -> bool:
+    def _fused_decode_ok(self, kv_pool: torch.Tensor, m: int = 32) -> bool:
         g = self.hq // self.hkv
-        sq = self.decode_plan()["qkv"][1]
+        sq = self.decode_plan(m)["qkv"][2]
         return (self.norms_folded and self.head_dim == 128 and kv_pool.shape[4] == 16 and g in (1, 2, 4, 8)
                 and ((sq * (g + 2) + 1) // 2) * 1024 + 1536 <= V3_MERGE_BYTES)
 
@@ -510,43 +529,58 @@ class CausalLM:
         """Decode layer = 5 launches: qkv (split-K slabs) -> attention (norm scale + slab sum + RoPE
         + KV write in its prologue) -> o (slabs, last arriver adds into the residual and writes the
         next norm's row statistics) -> gate/up (norm as a row scale, SiLU*mul) -> down (as o).
-        The residual stream `h` is updated in place; norm weights are folded into Wqkv / Wgate_up."""
+        The residual stream `h` is updated in place; norm weights are folded into Wqkv / Wgate_up.
+        Tiles come from the plan of the step's row bucket (32 / 64 / 128)."""
         a, eps = self.arch, self.arch.rms_eps
-        sc, plan = meta.scratch, meta.scratch["plan"]
+        sc = meta.scratch
+        plan = sc["plans"][self.decode_bucket(h.shape[0])]
         hq, hkv, hid = self.hq, self.hkv, a.hidden_size
+        (wq, kq, sq), (wo, ko, so) = plan["qkv"], plan["o"]
+        # statistics tiles of the residual-updating projections (one per wr output columns; 1 under TP)
+        ssp_a = sc["ssp_a"][: 1 if self.tp.enabled else hid // wo]
+        ssp_b = sc["ssp_b"]
+        if not (self.tp.enabled or a.is_moe):
+            ssp_b = ssp_b[: hid // plan["down"][0]]
+
+        def tw(lw, name, wr, kc):  # (weight, tiled?) for this tile
+            t = lw.tiled.get((name, wr, kc))
+            return (getattr(lw, name), False) if t is None else (t, True)
+
         ssp_prev = ops.row_sumsq(h, out=sc["ssp0"])
         for li, lw in enumerate(self.layers):
             k_cache, v_cache = kv_pool[li, 0], kv_pool[li, 1]
-            slab = ops.linear_slab(h, lw.qkv if lw.qkv_t is None else lw.qkv_t, sk=plan["qkv"][1], wr=plan["qkv"][0],
-                                   tiled=lw.qkv_t is not None)
+            wqkv, tq = tw(lw, "qkv", wq, kq)
+            slab = ops.linear_slab(h, wqkv, sk=sq, wr=wq, tiled=tq, kc=kq)
             attn = ops.attn_decode_fused(slab, ssp_prev, positions, self.cos_sin, meta.slot_mapping,
                                          k_cache, v_cache, meta.block_tables, meta.ctx_lens, meta.max_ctx, hq, hkv,
                                          self.scale, eps, hid, meta.part_o, meta.part_ml, meta.attn_cnt)
             if a.is_moe:  # ln2 stays explicit (it also feeds the router); MoE output added back + statistics
                 if self.tp.enabled:
-                    self.tp.all_reduce_residual(ops.linear(attn, lw.o), h, sc["ssp_a"])
+                    self.tp.all_reduce_residual(ops.linear(attn, lw.o), h, ssp_a)
                 else:
-                    ops.linear_slab_residual(attn, lw.o, h, sc["ssp_a"], sc["cnt_a"], *plan["o"])
+                    ops.linear_slab_residual(attn, lw.o, h, ssp_a, sc["cnt_a"], wo, so, kc=ko)
                 x = ops.rms_norm(h, lw.ln2, eps)
                 if self.tp.enabled:
-                    self.tp.all_reduce_residual(self._mlp(lw, x), h, sc["ssp_b"])
+                    self.tp.all_reduce_residual(self._mlp(lw, x), h, ssp_b)
                 else:  # combine + residual add + statistics in one launch
                     wr_, ids_ = ops.moe_route(x, lw.router, a.top_k)
-                    ops.moe_forward_routed(x, lw.w13, lw.w2, wr_, ids_, residual=h, ssp=sc["ssp_b"])
-            elif self.tp.enabled:  # row-parallel partial sums -> all-reduce -> residual + statistics (one
-                # launch on the one-shot IPC path, see TPContext.all_reduce_residual)
-                self.tp.all_reduce_residual(ops.linear(attn, lw.o), h, sc["ssp_a"])
-                act = ops.linear_silu_mul_rownorm(h, _w(lw.gate_up, lw.gate_up_t), sc["ssp_a"], eps, plan["gate_up"],
-                                                  tiled=lw.gate_up_t is not None)
-                self.tp.all_reduce_residual(ops.linear(act, lw.down), h, sc["ssp_b"])
+                    ops.moe_forward_routed(x, lw.w13, lw.w2, wr_, ids_, residual=h, ssp=ssp_b)
             else:
-                ops.linear_slab_residual(attn, _w(lw.o, lw.o_t), h, sc["ssp_a"], sc["cnt_a"], *plan["o"],
-                                         tiled=lw.o_t is not None)
-                act = ops.linear_silu_mul_rownorm(h, _w(lw.gate_up, lw.gate_up_t), sc["ssp_a"], eps, plan["gate_up"],
-                                                  tiled=lw.gate_up_t is not None)
-                ops.linear_slab_residual(act, _w(lw.down, lw.down_t), h, sc["ssp_b"], sc["cnt_b"], *plan["down"],
-                                         tiled=lw.down_t is not None)
-            ssp_prev = sc["ssp_b"]
+                wg, kg = plan["gate_up"]
+                wgu, tg = tw(lw, "gate_up", wg, kg)
+                if self.tp.enabled:  # row-parallel partial sums -> all-reduce -> residual + statistics (one
+                    # launch on the one-shot IPC path, see TPContext.all_reduce_residual)
+                    self.tp.all_reduce_residual(ops.linear(attn, lw.o), h, ssp_a)
+                    act = ops.linear_silu_mul_rownorm(h, wgu, ssp_a, eps, wg, tiled=tg, kc=kg)
+                    self.tp.all_reduce_residual(ops.linear(act, lw.down), h, ssp_b)
+                else:
+                    wdn_, kd, sd = plan["down"]
+                    wo_t, to_ = tw(lw, "o", wo, ko)
+                    wd_t, td_ = tw(lw, "down", wdn_, kd)
+                    ops.linear_slab_residual(attn, wo_t, h, ssp_a, sc["cnt_a"], wo, so, tiled=to_, kc=ko)
+                    act = ops.linear_silu_mul_rownorm(h, wgu, ssp_a, eps, wg, tiled=tg, kc=kg)
+                    ops.linear_slab_residual(act, wd_t, h, ssp_b, sc["cnt_b"], wdn_, sd, tiled=td_, kc=kd)
+            ssp_prev = ssp_b
         return ops.rms_norm(h, self.norm, eps)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:

@@ -183,7 +183,9 @@ def scatter_blocks(pool: torch.Tensor, ids: torch.Tensor, buf: torch.Tensor) -> 
     _kern().move_blocks(pool, buf, ids, False)
 
 
-DECODE_GEMM_MAX_M = 32
+DECODE_GEMM_MAX_M = 128   # weight-streaming decode GEMM / fused decode path (gemm_decode.hip)
+MOE_DECODE_MAX_T = 32     # expert-streaming grouped decode GEMM (<= 32 rows per expert)
+SSP_LD = 128              # row stride of the norm-statistics arrays [tiles, SSP_LD]
 
 
 def _decode_gemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -193,12 +195,21 @@ def _decode_gemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 
 DECODE_GEMM_NT = True
 
+def gd_tile(wr: int, kc: Optional[int] = None):
+    """(weight rows, K slot) of a decode-GEMM tile. ``kc`` defaults from the legacy wr codes: 256 for
+    32 / 48 / 64 rows, 128 for >= 96 rows, and odd codes 33 / 49 / 65 = the 128-wide deep-ring variants."""
+    if kc is None:
+        kc = 128 if (wr >= 96 or wr & 1) else 256
+    return wr & ~1, kc
+
+
 def gemm_decode(x: torch.Tensor, w: torch.Tensor, mode: int = 0, wr: int = 64, sk: int = 1,
-                out: Optional[torch.Tensor] = None, nt: Optional[bool] = None) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, nt: Optional[bool] = None, kc: Optional[int] = None) -> torch.Tensor:
     """Raw access to the decode GEMM kernel (see csrc/kernels/gemm_decode.hip).
     mode 0: bf16 x@w^T; mode 1: bf16 silu(gate)*up (w = [gate; up]);
-    mode 2: fp32 split-K slabs [sk, M, N]."""
+    mode 2: fp32 split-K slabs [sk, M, N]. ``(wr, kc)``: the workgroup tile (:func:`gd_tile`)."""
     m = x.shape[0]
+    wr, kc = gd_tile(wr, kc)
     base = mode & 31  # | 32: w pre-packed by gd_pack_weights
     n = w.shape[0] // 2 if base == 1 else w.shape[0]
     if out is None:
@@ -207,24 +218,33 @@ def gemm_decode(x: torch.Tensor, w: torch.Tensor, mode: int = 0, wr: int = 64, s
         else:
             out = torch.empty(m, n, dtype=x.dtype, device=x.device)
     e = _empty(x.device)
-    _kern().gemm_decode(out, x, w, mode, wr, sk, DECODE_GEMM_NT if nt is None else nt, e, e, e, e, 0.0)
+    _kern().gemm_decode(out, x, w, mode, wr, kc, sk, DECODE_GEMM_NT if nt is None else nt, e, e, e, e, 0.0)
     return out
 
 
 def gd_kc(wr: int) -> int:
-    """K elements per ring slot of the decode GEMM for a weight-row tile of `wr` (gemm_decode.hip)."""
-    return 128 if (wr >= 96 or wr & 1) else 256
+    """K elements per ring slot of the decode GEMM for a legacy weight-row code `wr` (gemm_decode.hip)."""
+    return gd_tile(wr)[1]
 
 
-def gd_pack_weights(w: torch.Tensor, wr: int, silu: bool = False) -> torch.Tensor:
+def gd_swizzle(r: torch.Tensor, kc: int) -> torch.Tensor:
+    """16-byte chunk swizzle of LDS-image row r for a K slot of kc elements (gemm_decode.hip swz())."""
+    rowb = 2 * kc
+    if rowb >= 256:
+        return r & 15
+    if rowb == 128:
+        return (r >> 1) & 7
+    return (r ^ (r >> 1)) & 3
+
+
+def gd_pack_weights(w: torch.Tensor, wr: int, silu: bool = False, kc: Optional[int] = None) -> torch.Tensor:
     """Re-lay a [rows, K] projection weight in the decode GEMM's tile order: for column tile t and
     K-chunk c, the tile's (wr x KC) block is contiguous and already in the kernel's LDS-image order
     (rows of the tile, 16-byte chunks XOR-swizzled by row), so every 1-KiB LDS-DMA piece is one
     linear read. silu: w = [gate; up] and a tile holds wr/2 gate rows then the matching wr/2 up
     rows. The result has w's shape (pass mode | 32 to gemm_decode)."""
     rows, k = w.shape
-    wrr = wr & ~1
-    kc = gd_kc(wr)
+    wrr, kc = gd_tile(wr, kc)
     cpr = kc // 8
     no = wrr // 2 if silu else wrr
     n_out = rows // 2 if silu else rows
@@ -236,7 +256,7 @@ def gd_pack_weights(w: torch.Tensor, wr: int, silu: bool = False) -> torch.Tenso
     wt = w[idx.reshape(-1)].view(nt, wrr, nch, cpr, 8)
     r = torch.arange(wrr, device=w.device).view(1, wrr, 1, 1, 1)
     q = torch.arange(cpr, device=w.device).view(1, 1, 1, cpr, 1)
-    sw = (q ^ (r & 15)).expand(nt, wrr, nch, cpr, 8)
+    sw = (q ^ gd_swizzle(r, kc)).expand(nt, wrr, nch, cpr, 8)
     wt = torch.gather(wt, 3, sw)
     return wt.permute(0, 2, 1, 3, 4).contiguous().view(rows, k)
 
@@ -252,35 +272,38 @@ def _empty(dev) -> torch.Tensor:
 
 
 def linear_slab_residual(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, ssp_out: torch.Tensor,
-                         counters: torch.Tensor, wr: int = 64, sk: int = 4, tiled: bool = False) -> torch.Tensor:
+                         counters: torch.Tensor, wr: int = 64, sk: int = 4, tiled: bool = False,
+                         kc: Optional[int] = None) -> torch.Tensor:
     """resid += x @ w^T (bf16, in place) with split-K reduced by the last-arriving workgroup of
     each column tile, which also writes the tile's row sums of squares of the new residual to
-    ssp_out [N/wr, 32] — the statistics of the next RMSNorm (whose weight is folded into the
+    ssp_out [N/wr, SSP_LD] — the statistics of the next RMSNorm (whose weight is folded into the
     consuming projection). counters [N/wr] int32, zeroed once. Returns the slab scratch."""
     m, n = x.shape[0], w.shape[0]
+    wr, kc = gd_tile(wr, kc)
     slab = torch.empty(sk, m, n, dtype=torch.float32, device=x.device)
     e = _empty(x.device)
-    _kern().gemm_decode(slab, x, w, 3 | (32 if tiled else 0), wr, sk, DECODE_GEMM_NT, resid, ssp_out, counters, e,
-                        0.0)
+    _kern().gemm_decode(slab, x, w, 3 | (32 if tiled else 0), wr, kc, sk, DECODE_GEMM_NT, resid, ssp_out, counters,
+                        e, 0.0)
     return slab
 
 
 def linear_silu_mul_rownorm(x: torch.Tensor, w_gate_up: torch.Tensor, ssp_in: torch.Tensor, eps: float,
-                            wr: Optional[int] = None, tiled: bool = False) -> torch.Tensor:
+                            wr: Optional[int] = None, tiled: bool = False, kc: Optional[int] = None) -> torch.Tensor:
     """silu(r * x @ gate^T) * (r * x @ up^T) with r = rsqrt(sum_t ssp_in[t] / K + eps) per row:
     RMSNorm (weight folded into w_gate_up) + gate/up + SiLU*mul in one weight stream."""
     n = w_gate_up.shape[0] // 2
     if wr is None:
-        wr, _ = _cfg_for(n, x.shape[1], 1)
+        wr, kc, _ = decode_tile(n, x.shape[1], 4, _bucket(x.shape[0]))
+    wr, kc = gd_tile(wr, kc)
     out = torch.empty(x.shape[0], n, dtype=x.dtype, device=x.device)
     e = _empty(x.device)
-    _kern().gemm_decode(out, x, w_gate_up, 4 | (32 if tiled else 0), wr, 1, DECODE_GEMM_NT, e, e, e, ssp_in,
+    _kern().gemm_decode(out, x, w_gate_up, 4 | (32 if tiled else 0), wr, kc, 1, DECODE_GEMM_NT, e, e, e, ssp_in,
                         float(eps))
     return out
 
 
 def residual_add_sumsq(resid: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
-    """resid += x (bf16, in place); out [1, 32] = per-row sums of squares of the new residual."""
+    """resid += x (bf16, in place); out [1, SSP_LD] = per-row sums of squares of the new residual."""
     if not x.is_cuda:
         resid.copy_((resid.float() + x.float()).to(resid.dtype))
         out.zero_()
@@ -291,9 +314,9 @@ def residual_add_sumsq(resid: torch.Tensor, x: torch.Tensor, out: torch.Tensor) 
 
 
 def row_sumsq(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """[1, 32] fp32 per-row sums of squares of x [M <= 32, H] (RMSNorm statistics)."""
+    """[1, SSP_LD] fp32 per-row sums of squares of x [M <= SSP_LD, H] (RMSNorm statistics)."""
     if out is None:
-        out = torch.zeros(1, 32, dtype=torch.float32, device=x.device)
+        out = torch.zeros(1, SSP_LD, dtype=torch.float32, device=x.device)
     if not x.is_cuda:
         out.zero_()
         out[0, : x.shape[0]] = x.float().pow(2).sum(-1)
@@ -348,37 +371,109 @@ def _cfg_for(n: int, k: int, mode: int, max_sk: int = 8):
     return best
 
 
+def gd_tile_valid(wr: int, kc: int, xr: int) -> bool:
+    """A (wr, kc) tile has an xr-row activation image (mirror of gemm_decode.hip gd_valid)."""
+    rpp = 64 // (kc // 8)
+    slot = (wr + xr) * kc * 2
+    s = min(8, 147456 // slot)
+    per_wave = (wr + xr) // rpp // 4
+    while s > 2 and (s - 1) * per_wave > 63:
+        s -= 1
+    red = (4 if xr < 64 and kc >= 128 else 1) * max(xr, 32) * wr * 4 + 2048
+    return (s >= 2 and (wr + xr) % (4 * rpp) == 0 and xr % rpp == 0 and wr % rpp == 0
+            and not (xr < 64 and kc < 128 and wr % 64) and max(s * slot, red) <= 160 * 1024)
+
+
+# (N, K, mode, row bucket) -> (wr, kc, sk) for the fused decode layer's projections (mode 2 qkv slabs,
+# 3 o / down residual update, 4 gate/up row-norm + SiLU), Llama-3-8B shapes, measured on MI355X with
+# bench/micro_gemm_decode_large.py (cold weights, tile-order packed; profiles/micro_gemm_decode_large_r2.jsonl).
+# The 32-row bucket keeps round 1's in-graph choices (DECODE_GEMM_CFG / DECODE_GEMM_RESID_CFG).
+DECODE_TILE_CFG = {
+    (6144, 4096, 2, 64): (96, 128, 4),     # qkv   15.0 us vs hipBLASLt 17.9
+    (6144, 4096, 2, 128): (48, 128, 2),    #       20.2 vs 25.3
+    (4096, 4096, 3, 64): (64, 128, 4),     # o     13.4 vs 15.3
+    (4096, 4096, 3, 128): (32, 128, 2),    #       16.5 vs 24.6
+    (14336, 4096, 4, 64): (112, 128, 1),   # gate/up + SiLU  45.6 vs 50.5
+    (14336, 4096, 4, 128): (128, 64, 1),   #                 57.2 vs 54.7
+    (4096, 14336, 3, 64): (64, 128, 4),    # down  28.3 vs 40.0
+    (4096, 14336, 3, 128): (128, 64, 8),   #       38.3 vs 75.3
+}
+_GENERIC_TILES = ((64, 128), (128, 64), (32, 128), (64, 64), (128, 32), (64, 32), (112, 128), (96, 128), (48, 128),
+                  (128, 128))
+
+
+def decode_tile(n: int, k: int, mode: int, bucket: int = 32, max_sk: int = 8):
+    """(wr, kc, sk) of the decode GEMM for an [N, K] projection in ``mode`` (0 bf16, 1 / 4 SiLU, 2 slabs,
+    3 residual update) at steps of up to ``bucket`` rows (32, 64, 128)."""
+    import math
+
+    c = DECODE_TILE_CFG.get((n, k, mode, bucket))
+    if c is not None and c[2] <= max_sk:
+        return c
+    if bucket <= 32:
+        if mode == 3:
+            c = DECODE_GEMM_RESID_CFG.get((n, k))
+            if c is None:
+                wr, sk = _cfg_for(n, k, 2, max_sk)
+                if wr not in (32, 64, 128) or n % wr:
+                    wr = 64 if n % 64 == 0 else 32
+                while sk > 1 and k % (256 * sk):
+                    sk //= 2
+                c = (wr, sk)
+            return (*gd_tile(c[0]), c[1])
+        wr, sk = _cfg_for(n, k, {4: 1}.get(mode, mode), max_sk)
+        return (*gd_tile(wr), sk)
+    best, score = None, 1e9
+    for wr, kc in _GENERIC_TILES:
+        cols = wr // 2 if mode in (1, 4) else wr
+        if n % cols or (mode == 3 and wr not in (32, 64, 128)) or not gd_tile_valid(wr, kc, bucket):
+            continue
+        for sk in ((1, 2, 4, 8) if mode in (2, 3) else (1,)):
+            if sk > max_sk or k % (kc * sk):
+                continue
+            sc = abs(math.log2((n // cols) * sk / 256.0))
+            if sc < score - 1e-9:
+                best, score = (wr, kc, sk), sc
+    if best is None:
+        raise ValueError(f"no decode-GEMM tile for N={n} K={k} mode={mode} at {bucket} rows")
+    return best
+
+
+def _bucket(m: int) -> int:
+    return 32 if m <= 32 else (64 if m <= 64 else 128)
+
+
 def decode_slab_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
     return _decode_gemm_ok(x, w) and w.shape[0] % 32 == 0 and w.shape[0] <= DECODE_GEMM_MAX_N
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y = x @ w^T. Decode-sized M (<= 32 rows) runs on the weight-streaming
+    """y = x @ w^T. Decode-sized M (<= 128 rows) runs on the weight-streaming
     gfx950 kernel (gemm_decode.hip); larger M goes to hipBLASLt."""
     if _decode_gemm_ok(x, w) and w.shape[0] % 32 == 0 and w.shape[0] <= DECODE_GEMM_MAX_N:
-        wr, _ = _cfg_for(w.shape[0], x.shape[1], 0)
-        return gemm_decode(x, w, 0, wr, 1, out)
+        wr, kc, _ = decode_tile(w.shape[0], x.shape[1], 0, _bucket(x.shape[0]))
+        return gemm_decode(x, w, 0, wr, 1, out, kc=kc)
     return torch.nn.functional.linear(x, w, out=out) if out is not None else torch.nn.functional.linear(x, w)
 
 
 def linear_slab(x: torch.Tensor, w: torch.Tensor, sk: Optional[int] = None, wr: Optional[int] = None,
-                tiled: bool = False) -> torch.Tensor:
+                tiled: bool = False, kc: Optional[int] = None) -> torch.Tensor:
     """fp32 split-K slabs [sk, M, N] of x @ w^T (decode sizes only); the
     consumer (fused_add_rms_norm_slab / rope_and_cache_slab) reduces them.
-    tiled: w was packed by gd_pack_weights for this wr."""
+    tiled: w was packed by gd_pack_weights for this (wr, kc)."""
     if sk is None or wr is None:
         assert not tiled, "a tiled weight needs its packing wr"
-        wr0, sk0 = _cfg_for(w.shape[0], x.shape[1], 2)
-        wr, sk = wr or wr0, sk or sk0
-    return gemm_decode(x, w, 2 | (32 if tiled else 0), wr, sk)
+        wr0, kc0, sk0 = decode_tile(w.shape[0], x.shape[1], 2, _bucket(x.shape[0]))
+        wr, sk, kc = wr or wr0, sk or sk0, kc or kc0
+    return gemm_decode(x, w, 2 | (32 if tiled else 0), wr, sk, kc=kc)
 
 
 def linear_silu_mul(x: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
     """silu(x @ gate^T) * (x @ up^T) with w_gate_up = [gate; up] (fused epilogue
     in the decode kernel; GEMM + silu_and_mul kernel otherwise)."""
     if _decode_gemm_ok(x, w_gate_up) and (w_gate_up.shape[0] // 2) % 32 == 0:
-        wr, _ = _cfg_for(w_gate_up.shape[0] // 2, x.shape[1], 1)
-        return gemm_decode(x, w_gate_up, 1, wr, 1)
+        wr, kc, _ = decode_tile(w_gate_up.shape[0] // 2, x.shape[1], 1, _bucket(x.shape[0]))
+        return gemm_decode(x, w_gate_up, 1, wr, 1, kc=kc)
     return silu_and_mul(torch.nn.functional.linear(x, w_gate_up))
 
 
@@ -483,7 +578,7 @@ def moe_apply(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, w: torch.Ten
     int32). ``groups`` may exceed the number of local experts ``w13.shape[0]``: assignments to those
     extra groups are not computed (their weight must be 0)."""
     e = w13.shape[0]
-    if residual is not None and not (x.is_cuda and x.shape[0] <= DECODE_GEMM_MAX_M):
+    if residual is not None and not (x.is_cuda and x.shape[0] <= MOE_DECODE_MAX_T):
         return residual_add_sumsq(residual, moe_apply(x, w13, w2, w, ids, groups), ssp)
     if not x.is_cuda:
         return ref.moe_experts(x, w13, w2, w, ids)
@@ -496,7 +591,7 @@ def moe_apply(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, w: torch.Ten
     offsets, sorted_idx, pos = moe_align(ids, groups)
     # rows of the extra groups are never computed: zero them so that weight 0 x row stays 0
     ys = (torch.zeros if groups > e else torch.empty)(t * k, hdim, dtype=x.dtype, device=x.device)
-    if t <= DECODE_GEMM_MAX_M and _moe_decode_ok(hdim, inter) and x.is_contiguous():
+    if t <= MOE_DECODE_MAX_T and _moe_decode_ok(hdim, inter) and x.is_contiguous():
         # decode: every expert's weights streamed once by the weight-streaming kernel, its
         # (<= 32) routed tokens riding along, gathered from x by the kernel itself through the
         # sorted order; SiLU*mul fused; idle experts read nothing

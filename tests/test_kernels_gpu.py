@@ -357,37 +357,41 @@ def test_rope_and_cache_slab(dev):
 
 
 # ---------------------------------------------------------------- fused decode path pieces
-@pytest.mark.parametrize("wr,sk,k", [(64, 4, 4096), (64, 4, 14336), (32, 1, 2048), (128, 2, 4096), (64, 8, 4096),
-                                     (32, 3, 3072)])
-def test_gemm_decode_residual_mode(dev, wr, sk, k):
+@pytest.mark.parametrize("wr,sk,k,m,kc", [(64, 4, 4096, 27, None), (64, 4, 14336, 27, None), (32, 1, 2048, 27, None),
+                                          (128, 2, 4096, 27, None), (64, 8, 4096, 27, None), (32, 3, 3072, 27, None),
+                                          (64, 4, 4096, 100, 128), (128, 8, 4096, 128, 32), (64, 2, 14336, 64, 256),
+                                          (128, 4, 4096, 77, 64)])
+def test_gemm_decode_residual_mode(dev, wr, sk, k, m, kc):
     """mode 3: resid += x @ w^T with the split-K reduced by the last-arriving workgroup, which
     also writes the per-tile row sums of squares of the new residual."""
-    m, h = 27, 4096
+    h = 4096
     x = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
     w = torch.randn(h, k, device=dev, dtype=torch.bfloat16) / math.sqrt(k)
     res = torch.randn(m, h, device=dev, dtype=torch.bfloat16)
     t = h // wr
-    ssp = torch.full((t, 32), -1.0, device=dev)
+    ssp = torch.full((t, ops.SSP_LD), -1.0, device=dev)
     cnt = torch.zeros(t, dtype=torch.int32, device=dev)
     for it in range(2):  # tickets are re-armed: a second launch works too
         r0 = res.clone()
-        ops.linear_slab_residual(x, w, res, ssp, cnt, wr, sk)
+        ops.linear_slab_residual(x, w, res, ssp, cnt, wr, sk, kc=kc)
         expect = (r0.float() + x.float() @ w.float().t()).to(torch.bfloat16)
         close(res, expect, atol=3e-2, rtol=1e-2)
         ss_ref = res.float().pow(2).view(m, t, wr).sum(-1).t()       # [t, m]
         close(ssp[:, :m], ss_ref, atol=1e-2, rtol=1e-3)
-        assert torch.all(ssp[:, m:] == 0)
+        rr = 32 if m <= 32 else (64 if m <= 64 else 128)  # rows of the activation image: padded rows -> 0
+        assert torch.all(ssp[:, m:rr] == 0)
         assert int(cnt.abs().sum()) == 0
 
 
-@pytest.mark.parametrize("m,inter,k,wr", [(32, 14336, 4096, 112), (7, 2048, 1024, 64)])
+@pytest.mark.parametrize("m,inter,k,wr", [(32, 14336, 4096, 112), (7, 2048, 1024, 64), (100, 14336, 4096, 112),
+                                         (64, 2048, 1024, 64)])
 def test_gemm_decode_rownorm_silu(dev, m, inter, k, wr):
     """mode 4: RMSNorm (weight folded into W) as a per-row scale + gate/up + SiLU*mul."""
     x = torch.randn(m, k, device=dev, dtype=torch.bfloat16) * 3
     w = torch.randn(2 * inter, k, device=dev, dtype=torch.bfloat16) / math.sqrt(k)
     ss = x.float().pow(2)
     t = 64 if k % 64 == 0 else 1
-    ssp = torch.zeros(t, 32, device=dev)
+    ssp = torch.zeros(t, ops.SSP_LD, device=dev)
     ssp[:, :m] = ss.view(m, t, -1).sum(-1).t()
     y = ops.linear_silu_mul_rownorm(x, w, ssp, 1e-5, wr)
     xn = x.float() * torch.rsqrt(ss.mean(-1, keepdim=True) + 1e-5)
@@ -408,7 +412,7 @@ def test_gemm_decode_tiled_weights(dev, mode, n, k, wr, sk):
     wt = ops.gd_pack_weights(w, wr, silu=mode in (1, 4))
     if mode == 4:
         ssp = x.float().pow(2).sum(-1).view(1, m)
-        ssp_in = torch.zeros(1, 32, device=dev)
+        ssp_in = torch.zeros(1, ops.SSP_LD, device=dev)
         ssp_in[0, :m] = ssp
         a = ops.linear_silu_mul_rownorm(x, w, ssp_in, 1e-5, wr)
         b = ops.linear_silu_mul_rownorm(x, wt, ssp_in, 1e-5, wr, tiled=True)
@@ -437,7 +441,7 @@ def test_attn_decode_fused(dev, g, hkv, big):
     bt_wide[:, : bt.shape[1]] = bt
     slab = torch.randn(sk, n, width, device=dev) * 0.7   # normalised q/k/v ~ N(0, 1): realistic scores
     ssv = (torch.rand(n, device=dev) + 0.5) * hid
-    ssp = torch.zeros(4, 32, device=dev)
+    ssp = torch.zeros(4, ops.SSP_LD, device=dev)
     ssp[:, :n] = (ssv / 4)[None, :]                     # 4 tiles summing to ssv
     slots = torch.tensor([int(bt[i, (c - 1) // bs]) * bs + (c - 1) % bs for i, c in enumerate(ctxs)],
                          dtype=torch.long, device=dev)
@@ -481,3 +485,37 @@ def test_residual_add_sumsq(dev):
     ops.residual_add_sumsq(res, x, ssp)
     assert torch.equal(res, expect)
     close(ssp[0, :m], expect.float().pow(2).sum(-1), atol=1e-2, rtol=1e-4)
+
+
+# ------------------------------------------------------- decode GEMM at M <= 128
+@pytest.mark.parametrize("m", [33, 64, 100, 128])
+@pytest.mark.parametrize("wr,kc", [(64, 256), (112, 128), (64, 128), (128, 64), (128, 32), (64, 32)])
+def test_gemm_decode_large_m(dev, m, wr, kc):
+    """Every tile at batch sizes past 32 rows (64- and 128-row activation images, waves split the rows),
+    plain and silu epilogues, against fp32; tiles without a 64/128-row image must refuse loudly."""
+    k, n = 4096, 1792
+    x = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(2 * n, k, device=dev, dtype=torch.bfloat16) / math.sqrt(k)
+    try:
+        y = ops.gemm_decode(x, w[:n], 0, wr, 1, kc=kc)
+    except RuntimeError as e:  # (wr, kc) has no image for this many rows: a clean launch error
+        assert "invalid" in str(e).lower() or "unsupported" in str(e).lower(), e
+        return
+    close(y, x.float() @ w[:n].float().t(), atol=2e-2, rtol=2e-2)
+    if wr in (64, 128) or (wr == 112 and n % 56 == 0):
+        ys = ops.gemm_decode(x, w, 1, wr, 1, kc=kc)
+        h = x.float() @ w.float().t()
+        close(ys, torch.nn.functional.silu(h[:, :n]) * h[:, n:], atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("m,wr,kc,sk", [(64, 128, 32, 4), (128, 128, 64, 2), (100, 64, 128, 2), (48, 128, 32, 8)])
+def test_gemm_decode_large_m_slabs_and_tiled(dev, m, wr, kc, sk):
+    """Split-K slabs and tile-order packed weights with the small K slots (swizzle of 128- and 64-byte rows)."""
+    k, n = 4096, 2048
+    x = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(n, k, device=dev, dtype=torch.bfloat16) / math.sqrt(k)
+    a = ops.gemm_decode(x, w, 2, wr, sk, kc=kc)
+    close(a.sum(0), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
+    wt = ops.gd_pack_weights(w, wr, kc=kc)
+    b = ops.gemm_decode(x, wt, 2 | 32, wr, sk, kc=kc)
+    assert torch.equal(a, b)
