@@ -93,6 +93,16 @@ class EngineConfig:
     preemption_mode: str = "auto"
     swap_space_gib: float = 16.0
     swap_min_tokens: int = 256
+    # prompts arriving while sequences decode (src/engine/scheduler.py): "auto" — prompt work that fits
+    # in the decode step's spare rows (mixed_step_tokens - decode rows) rides along in ONE ragged batch
+    # (a mixed step); more than that runs as a prefill step of at most prefill_tokens_while_decoding
+    # tokens, and the next step decodes again (bounded stall). "always": every such step is mixed
+    # (long prompts in mixed_step_tokens-row chunks); "off" (or False): prefill steps as before.
+    # Measured on MI355X (profiles/poisson_r2.jsonl): 512-token prompts ride cheaper as whole prefill
+    # steps than as 96-token chunks on the 128-row decode GEMM, short prompts ride along.
+    mixed_batching: object = "auto"
+    mixed_step_tokens: int = 64
+    prefill_tokens_while_decoding: int = 4096
 
 
 @dataclass

@@ -196,11 +196,20 @@ class LLMEngine:
         t0 = time.perf_counter()
         now = t0
         if out.prefill:
-            toks = self.runner.prefill(out.prefill)
+            # a prefill step, or a mixed step: the decode rows as 1-token chunks in the same ragged batch
+            chunks = out.chunks() if out.decode else out.prefill
+            toks = self.runner.prefill(chunks)
             now = time.perf_counter()
-            self.stats["prefill_time"] += now - t0
-            for c, tok in zip(out.prefill, toks):
+            self.stats["mixed_time" if out.decode else "prefill_time"] = \
+                self.stats.get("mixed_time" if out.decode else "prefill_time", 0.0) + now - t0
+            for c, tok in zip(chunks, toks):
                 seq = c.seq
+                if c.decode:
+                    if seq.status == SeqStatus.FINISHED:
+                        continue
+                    seq.num_computed += 1
+                    self._append(seq, tok, finished)
+                    continue
                 seq.num_computed = c.start + c.length
                 if tok is None:
                     continue

@@ -200,9 +200,10 @@ class ModelRunner:
 
     @torch.inference_mode()
     def prefill(self, chunks: List[PrefillChunk]) -> List[Optional[int]]:
-        """Run one ragged prefill batch; returns the sampled token for every
-        chunk that completes its prompt (None for partial chunks)."""
-        toks = [c.seq.prompt_ids[c.start: c.start + c.length] for c in chunks]
+        """Run one ragged prefill batch — or a mixed step, whose decode rows are 1-token chunks —
+        and return the sampled token for every chunk that completes its prompt or decodes
+        (None for partial prompt chunks)."""
+        toks = [c.tokens() for c in chunks]
         starts = [c.start for c in chunks]
         tables = [c.seq.block_table for c in chunks]
         n = len(chunks)

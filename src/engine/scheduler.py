@@ -3,13 +3,20 @@ Continuous-batching scheduler (iteration-level): the reference Batcher's
 max-batch / max-latency flush (`/root/reference/src/batcher.py:144-166`)
 re-cast for token generation.
 
-Every engine step is either
+Every engine step is one of
 
 * a **prefill step** — new prompts (and chunks of long prompts: chunked
   prefill) packed into one ragged batch of at most ``max_num_batched_tokens``
-  tokens, or
+  tokens — when nothing is decoding;
 * a **decode step** — one token for every running sequence (≤ ``max_num_seqs``),
-  replayed from a captured hipGraph.
+  replayed from a captured hipGraph;
+* a **mixed step** (``EngineConfig.mixed_batching``) — the decode rows of every
+  running sequence plus prompt chunks filling the step up to
+  ``mixed_step_tokens`` rows, run as ONE ragged batch (a decode row is a 1-token
+  chunk). At <= 128 rows every projection is a weight stream on the decode GEMM,
+  so the prompt tokens ride along almost for free and running sequences never
+  stall behind a whole prefill: per-iteration admission, the continuous form of
+  the reference Batcher's size-or-latency flush.
 
 Sequences join the running batch as soon as their prompt is done and leave it
 the step they finish, so the batch never waits for its slowest member.
@@ -44,10 +51,18 @@ class PrefillChunk:
     seq: Sequence
     start: int        # first position computed in this step
     length: int       # tokens computed in this step
+    decode: bool = False  # a decode row of a mixed step (1 token: the last sampled one)
 
     @property
     def completes_prompt(self) -> bool:
         return self.start + self.length >= self.seq.prompt_len
+
+    def tokens(self) -> List[int]:
+        s = self.seq
+        if self.decode:
+            return [s.last_token]
+        return s.prompt_ids[self.start: self.start + self.length] if self.start + self.length <= s.prompt_len \
+            else [s.token_at(i) for i in range(self.start, self.start + self.length)]
 
 
 @dataclass
@@ -62,6 +77,14 @@ class SchedulerOutput:
     @property
     def empty(self) -> bool:
         return not self.prefill and not self.decode
+
+    @property
+    def mixed(self) -> bool:
+        return bool(self.prefill and self.decode)
+
+    def chunks(self) -> List[PrefillChunk]:
+        """A mixed step as one ragged batch: decode rows first (1-token chunks), then prompt chunks."""
+        return [PrefillChunk(s, len(s) - 1, 1, decode=True) for s in self.decode] + self.prefill
 
     @property
     def num_tokens(self) -> int:
@@ -84,6 +107,8 @@ class Scheduler:
         self.num_preemptions = 0
         self.steps_prefill = 0
         self.steps_decode = 0
+        self.steps_mixed = 0
+        self._stalled = False  # the last step was a prefill step that decode-ready sequences waited for
 
     def add(self, seq: Sequence) -> None:
         seq.status = SeqStatus.WAITING
@@ -143,6 +168,30 @@ class Scheduler:
             self.running.append(seq)
             self._resumed_now.add(id(seq))
         blocked = bool(self.swapped)
+        ready = [s for s in self.running if not s.in_prefill and s.num_computed == len(s) - 1]
+        mode = self._mixed_mode()
+        mixed = False
+        if ready and mode != "off":
+            room = min(budget, self.cfg.mixed_step_tokens) - len(ready)
+            pending = self._pending_prompt_tokens(blocked)
+            # "auto": ride along when the prompt work fits the spare rows; otherwise alternate one bounded
+            # prefill step (the decode rows wait for it) with one decode-only step, so decode progresses at
+            # least every other step and no prompt is split into ride-along fragments
+            mixed = mode == "always" or pending <= room
+            if not mixed and self._stalled:
+                self._stalled = False
+                out.decode = self._schedule_decode(ready, out)
+                if out.decode:
+                    self.steps_decode += 1
+                return out
+            if not mixed and pending:
+                budget = min(budget, self.cfg.prefill_tokens_while_decoding)
+        self._stalled = False
+        if mixed:
+            # decode rows first (they are latency-critical); prompt chunks fill the step up to
+            # mixed_step_tokens rows
+            out.decode = self._schedule_decode(ready, out)
+            budget = max(0, min(budget, self.cfg.mixed_step_tokens) - len(out.decode))
         # 1) continue chunked prefills already running
         for seq in self.running:
             if budget <= 0:
@@ -174,12 +223,43 @@ class Scheduler:
                 n = min(seq.prompt_len - seq.num_computed, budget) if seq.in_prefill else remaining
                 out.prefill.append(PrefillChunk(seq, seq.num_computed, n))
                 budget -= n
+        if mixed:
+            if out.prefill and out.decode:
+                self.steps_mixed += 1
+            elif out.prefill:
+                self.steps_prefill += 1
+            elif out.decode:
+                self.steps_decode += 1
+            return out
         if out.prefill:
             self.steps_prefill += 1
+            self._stalled = bool(ready)  # decode rows waited for this step: the next one decodes
             return out
         # 3) decode everything that is past its prompt
-        ready = [s for s in self.running if not s.in_prefill and s.num_computed == len(s) - 1]
-        ready.sort(key=lambda s: s.arrival)
+        out.decode = self._schedule_decode(ready, out)
+        if out.decode:
+            self.steps_decode += 1
+        return out
+
+    def _mixed_mode(self) -> str:
+        m = self.cfg.mixed_batching
+        if m is True:
+            return "always"
+        if m is False or m is None:
+            return "off"
+        return str(m)
+
+    def _pending_prompt_tokens(self, blocked: bool) -> int:
+        """Prompt tokens that could be scheduled now: unfinished chunked prefills, plus (unless
+        admission is blocked) waiting prompts."""
+        n = sum(s.prompt_len - s.num_computed for s in self.running if s.in_prefill)
+        if not blocked:
+            n += sum(max(1, len(s) - s.num_computed) for s in self.waiting)
+        return n
+
+    def _schedule_decode(self, ready: List[Sequence], out: SchedulerOutput) -> List[Sequence]:
+        """One KV slot for every ready sequence (oldest first), preempting the newest when the pool is dry."""
+        ready = sorted(ready, key=lambda s: s.arrival)
         decode: List[Sequence] = []
         for seq in ready:
             if seq.status != SeqStatus.RUNNING:
@@ -198,10 +278,7 @@ class Scheduler:
             # could not find room even after preempting everyone else
             self._preempt(seq, out)
             out.preempted.append(seq)
-        out.decode = decode
-        if decode:
-            self.steps_decode += 1
-        return out
+        return decode
 
     def _pick_victim(self, exclude: Sequence) -> Optional[Sequence]:
         """Newest arrival first, but a sequence swapped back in during THIS step goes last: its KV
@@ -273,4 +350,5 @@ class Scheduler:
             "swaps_in": self.num_swaps_in,
             "steps_prefill": self.steps_prefill,
             "steps_decode": self.steps_decode,
+            "steps_mixed": self.steps_mixed,
         }

@@ -39,7 +39,7 @@ def test_batched_engine_matches_no_cache_reference():
     for p, o in zip(ps, outs):
         assert o == greedy_reference(eng.model, p, 5)
     st = eng.get_stats()
-    assert st["steps_prefill"] >= 2          # budget 64 forces chunked prefill
+    assert st["steps_prefill"] + st["steps_mixed"] >= 2   # budget 64 forces chunked prefill
     assert st["kv"]["used"] == 0             # every block released
 
 
@@ -193,3 +193,74 @@ def test_reference_copy_is_an_fp32_twin():
     ps = [[5, 9, 33, 12, 7] * 4, [100, 200, 300]]
     a, b = paged_greedy(m, ps, 4), paged_greedy(r, ps, 4)
     assert float((a[2][0] - b[2][0]).norm() / b[2][0].norm()) < 0.02
+
+
+def test_mixed_steps_admit_prompts_while_decoding():
+    """Requests arriving while others decode ride along in mixed steps (decode rows + prompt chunks of
+    at most mixed_step_tokens rows in ONE ragged batch): no prefill-only step stalls the running
+    sequences, long prompts are chunked across several mixed steps, and no greedy token changes."""
+    eng = make_engine(max_num_seqs=6, budget=256, blocks=128)
+    eng.cfg.mixed_step_tokens = 24
+    eng.cfg.mixed_batching = "always"
+    ps = prompts(6, seed=11)
+    sp = SamplingParams(max_tokens=12)
+    got = {}
+    for i in range(2):
+        eng.add_request(f"a{i}", ps[i], sp, on_finish=lambda s, i=i: got.__setitem__(i, list(s.output_ids)))
+    eng.step()  # the first two prompts: a plain prefill step (nothing is decoding yet)
+    assert eng.scheduler.steps_prefill == 1
+    step = 0
+    while eng.has_work():
+        if step < 4:  # one arrival per step while the first two decode
+            j = 2 + step
+            eng.add_request(f"a{j}", ps[j], sp, on_finish=lambda s, j=j: got.__setitem__(j, list(s.output_ids)))
+        n_dec = len([s for s in eng.scheduler.running if not s.in_prefill])
+        eng.step()
+        step += 1
+        assert n_dec == 0 or eng.scheduler.steps_prefill == 1  # never a prefill-only step while decoding
+    st = eng.get_stats()
+    assert st["steps_mixed"] >= 4 and st["kv"]["used"] == 0
+    for i, p in enumerate(ps):
+        assert got[i] == greedy_reference(eng.model, p, 12), i
+
+
+def test_mixed_batching_off_keeps_prefill_only_steps():
+    eng = make_engine(max_num_seqs=4, budget=256)
+    eng.cfg.mixed_batching = "off"
+    ps = prompts(3, seed=12)
+    sp = SamplingParams(max_tokens=6)
+    eng.add_request("x0", ps[0], sp)
+    eng.step()
+    eng.step()  # decoding
+    eng.add_request("x1", ps[1], sp)
+    eng.step()
+    assert eng.scheduler.steps_mixed == 0 and eng.scheduler.steps_prefill == 2
+
+
+def test_mixed_auto_policy():
+    """auto: a short prompt arriving while others decode rides along in a mixed step; a long one gets a
+    bounded prefill step (prefill_tokens_while_decoding) and the very next step decodes again."""
+    eng = make_engine(max_num_seqs=6, budget=256, blocks=128)
+    eng.cfg.mixed_step_tokens = 16
+    eng.cfg.prefill_tokens_while_decoding = 48
+    sp = SamplingParams(max_tokens=10)
+    long_p, short_p = prompts(1, seed=20)[0][:5] * 20, [5, 6, 7, 8]
+    got = {}
+    eng.add_request("d0", [9, 10, 11, 12, 13], sp, on_finish=lambda s: got.__setitem__(0, list(s.output_ids)))
+    eng.step()
+    eng.step()
+    s0 = dict(eng.scheduler.stats())
+    eng.add_request("short", short_p, sp, on_finish=lambda s: got.__setitem__(1, list(s.output_ids)))
+    eng.step()
+    assert eng.scheduler.steps_mixed == s0["steps_mixed"] + 1       # 1 decode row + 4 prompt rows <= 16
+    eng.add_request("long", long_p, sp, on_finish=lambda s: got.__setitem__(2, list(s.output_ids)))
+    kinds = []
+    while eng.has_work():
+        st = dict(eng.scheduler.stats())
+        eng.step()
+        d = {k: eng.scheduler.stats()[k] - st[k] for k in ("steps_prefill", "steps_decode", "steps_mixed")}
+        kinds.append(max(d, key=d.get))
+    assert kinds[0] == "steps_prefill"                               # 100 tokens > 16 spare rows: bounded step
+    assert all(not (a == b == "steps_prefill") for a, b in zip(kinds, kinds[1:]))  # never two stalls in a row
+    for i, p in enumerate(([9, 10, 11, 12, 13], short_p, long_p)):
+        assert got[i] == greedy_reference(eng.model, p, 10), i

@@ -271,3 +271,26 @@ def test_swap_preemption_on_gpu():
     for p, o in zip(prompts, outs):
         r, m = reference_with_margins(eng.model, p, 40)
         assert agree(o, r, m), (o, r, m)
+
+
+def test_mixed_steps_on_gpu(engine):
+    """Arrivals while others decode: decode rows + prompt chunks in one ragged batch on the GPU kernels
+    (decode GEMM at <= 128 rows, prefill attention with 1-token decode chunks); tokens unchanged."""
+    rng = random.Random(9)
+    ps = [[rng.randrange(3, 32000) for _ in range(rng.randrange(20, 300))] for _ in range(6)]
+    sp = SamplingParams(max_tokens=16)
+    got = {}
+    m0 = engine.scheduler.steps_mixed
+    for i in range(2):
+        engine.add_request(f"mx{i}", ps[i], sp, on_finish=lambda s, i=i: got.__setitem__(i, list(s.output_ids)))
+    engine.step()
+    k = 2
+    while engine.has_work():
+        if k < len(ps):
+            engine.add_request(f"mx{k}", ps[k], sp, on_finish=lambda s, k=k: got.__setitem__(k, list(s.output_ids)))
+            k += 1
+        engine.step()
+    assert engine.scheduler.steps_mixed > m0
+    for i, p in enumerate(ps):
+        r, m = reference_with_margins(engine.model, p, 16)
+        assert agree(got[i], r, m), (i, got[i], r, m)
