@@ -692,6 +692,38 @@ std::vector<int64_t> car_read_words(int64_t ptr, int64_t n) {  // synchronising 
   return std::vector<int64_t>(h.begin(), h.end());
 }
 
+static die::CarPeers car_peers(const std::vector<int64_t>& bufs, const std::vector<int64_t>& sigs) {
+  const int world = (int)bufs.size();
+  TORCH_CHECK(world >= 2 && world <= die::CAR_MAX_RANKS && (int)sigs.size() == world, "2..8 ranks");
+  die::CarPeers peers;
+  for (int p = 0; p < world; ++p) {
+    TORCH_CHECK(bufs[p] != 0 && sigs[p] != 0, "null peer pointer");
+    peers.buf[p] = reinterpret_cast<die::bf16_t*>(bufs[p]);
+    peers.sig[p] = reinterpret_cast<uint32_t*>(sigs[p]);
+  }
+  return peers;
+}
+
+// out [rows, world * cols] = concatenation of every rank's in [rows, cols] along the last dim
+void car_all_gather(Tensor in, Tensor out, int64_t rank, std::vector<int64_t> bufs, std::vector<int64_t> sigs,
+                    int64_t ctl, int64_t cap_elems, int64_t blocks) {
+  DIE_CHECK_CUDA(in);
+  DIE_CHECK_BF16(in);
+  DIE_CHECK_BF16(out);
+  DIE_CHECK_CONTIG(in);
+  DIE_CHECK_CONTIG(out);
+  const int world = (int)bufs.size();
+  TORCH_CHECK(in.dim() == 2 && out.dim() == 2 && out.size(0) == in.size(0) && out.size(1) == world * in.size(1),
+              "all_gather: in [rows, cols], out [rows, world * cols]");
+  TORCH_CHECK(in.size(1) % 8 == 0 && in.numel() <= cap_elems, "all_gather: cols % 8, numel <= cap");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(in.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "all_gather: 16-byte alignment");
+  TORCH_CHECK(rank >= 0 && rank < world && ctl != 0, "all_gather: bad rank / control word");
+  DIE_HIP(die::launch_custom_all_gather(bf(in), bf(out), in.size(0), in.size(1), (int)rank, world,
+                                        car_peers(bufs, sigs), reinterpret_cast<uint32_t*>(ctl), cap_elems,
+                                        (int)blocks, cur_stream()));
+}
+
 void car_all_reduce(Tensor in, Tensor out, int64_t rank, std::vector<int64_t> bufs, std::vector<int64_t> sigs,
                     int64_t ctl, int64_t cap_elems, int64_t blocks) {
   DIE_CHECK_CUDA(in);
@@ -757,6 +789,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("car_open", &car_open);
   m.def("car_close", &car_close);
   m.def("car_all_reduce", &car_all_reduce);
+  m.def("car_all_gather", &car_all_gather);
   m.def("car_read_words", &car_read_words);
   m.def("car_all_reduce_residual", &car_all_reduce_residual);
 }

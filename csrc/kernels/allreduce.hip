@@ -241,6 +241,78 @@ hipError_t launch_custom_all_reduce(const bf16_t* in, bf16_t* out, int64_t n, in
   return hipGetLastError();
 }
 
+// One-shot all-gather along the last dimension (the vocab-parallel LM head's logits: [rows, cols] per rank
+// -> out [rows, world * cols]), same protocol as the all-reduce: publish, signal, then every rank copies
+// all W shards into place itself. Capturable (device epoch) and it needs no host staging, so the TP decode
+// hipGraph also replays on a gloo group of ranks sharing one GPU.
+__global__ void __launch_bounds__(car::NTH) custom_all_gather_kernel(const bf16_t* __restrict__ in,
+                                                                     bf16_t* __restrict__ out, int64_t nvec,
+                                                                     int64_t cvec, int rank, int world,
+                                                                     CarPeers peers, uint32_t* __restrict__ ctl,
+                                                                     int64_t cap_vec) {
+  using namespace car;
+  const int tid = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
+  const uint32_t epoch = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const int par = (int)(epoch & 1u);
+  const int64_t per = (nvec + nb - 1) / nb;
+  const int64_t v0 = min(nvec, (int64_t)b * per), v1 = min(nvec, v0 + per);
+  const uint4* src = reinterpret_cast<const uint4*>(in);
+  uint4* mine = reinterpret_cast<uint4*>(peers.buf[rank]) + par * cap_vec;
+  for (int64_t i = v0 + tid; i < v1; i += NTH) mine[i] = src[i];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  uint32_t* slots = peers.sig[rank] + ((int64_t)par * CAR_MAX_BLOCKS + b) * CAR_MAX_RANKS;
+  if (tid < 64) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+  if (tid < world && tid != rank) {
+    st_sys(peers.sig[tid] + ((int64_t)par * CAR_MAX_BLOCKS + b) * CAR_MAX_RANKS + rank, epoch);
+    uint32_t it = 0;
+    while (ld_sys(slots + tid) != epoch) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++it > (1u << 25)) {
+        __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  uint4* dst = reinterpret_cast<uint4*>(out);
+  for (int p = 0; p < world; ++p) {
+    const uint4* pb = reinterpret_cast<const uint4*>(peers.buf[p]) + par * cap_vec;
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(pb), 0, 0x7fffffff, 0x00020000);
+    for (int64_t i = v0 + tid; i < v1; i += NTH) {
+      const int64_t row = i / cvec, c = i - row * cvec;
+      // peers' shards: system-coherent loads of their uncached staging (no stale line, no acquire)
+      const uint4 v = p == rank ? src[i]
+                                : __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * 16), 0, 17));
+      dst[(row * world + p) * cvec + c] = v;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (__hip_atomic_fetch_add(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)nb - 1) {
+      __hip_atomic_store(ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+hipError_t launch_custom_all_gather(const bf16_t* in, bf16_t* out, int64_t rows, int64_t cols, int rank, int world,
+                                    const CarPeers& peers, uint32_t* ctl, int64_t cap_elems, int blocks,
+                                    hipStream_t s) {
+  const int64_t n = rows * cols;
+  if (n <= 0) return hipSuccess;
+  if (cols % 8 || world < 2 || world > CAR_MAX_RANKS || rank < 0 || rank >= world || n > cap_elems || blocks < 1 ||
+      blocks > CAR_MAX_BLOCKS || n * 2 >= ((int64_t)1 << 31))
+    return hipErrorInvalidValue;
+  for (int p = 0; p < world; ++p)
+    if (peers.buf[p] == nullptr || peers.sig[p] == nullptr) return hipErrorInvalidValue;
+  const int64_t nvec = n / 8;
+  blocks = (int)std::min<int64_t>(blocks, (nvec + 63) / 64);
+  hipLaunchKernelGGL(custom_all_gather_kernel, dim3(blocks), dim3(car::NTH), 0, s, in, out, nvec, cols / 8, rank,
+                     world, peers, ctl, cap_elems / 8);
+  return hipGetLastError();
+}
+
 // Plain 16-byte vector copy by shader stores: the KV IPC path writes into a peer's landing zone this
 // way (stores from the CUs travel over xGMI like the all-reduce's; no DMA engine involved).
 __global__ void __launch_bounds__(256) ipc_copy_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src,

@@ -116,6 +116,10 @@ hipError_t launch_custom_all_reduce(const bf16_t* in, bf16_t* out, int64_t n, in
 hipError_t launch_custom_all_reduce_residual(const bf16_t* in, bf16_t* resid, float* ssp, int rows, int hidden,
                                              int rank, int world, const CarPeers& peers, uint32_t* ctl,
                                              int64_t cap_elems, hipStream_t s);
+// one-shot all-gather along the last dim: in [rows, cols] per rank -> out [rows, world * cols]
+hipError_t launch_custom_all_gather(const bf16_t* in, bf16_t* out, int64_t rows, int64_t cols, int rank, int world,
+                                    const CarPeers& peers, uint32_t* ctl, int64_t cap_elems, int blocks,
+                                    hipStream_t s);
 hipError_t car_malloc(void** p, size_t bytes, bool uncached = true);
 hipError_t launch_ipc_copy(void* dst, const void* src, int64_t nbytes, hipStream_t s);
 hipError_t car_free(void* p);

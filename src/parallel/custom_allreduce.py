@@ -81,6 +81,16 @@ class CustomAllReduce:
         _kern().car_all_reduce(t, out, self.rank, self.bufs, self.sigs, self.ctl, self.cap, self.blocks)
         return out
 
+    def can_run_gather(self, t: torch.Tensor) -> bool:
+        return (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.is_contiguous()
+                and t.shape[1] % 8 == 0 and 0 < t.numel() * 2 <= self.max_bytes and t.data_ptr() % 16 == 0)
+
+    def all_gather_last(self, t: torch.Tensor) -> torch.Tensor:
+        """[rows, cols] per rank -> [rows, world * cols] (rank-major along the last dim), one launch."""
+        out = torch.empty(t.shape[0], self.world * t.shape[1], dtype=t.dtype, device=t.device)
+        _kern().car_all_gather(t, out, self.rank, self.bufs, self.sigs, self.ctl, self.cap, self.blocks)
+        return out
+
     def can_run_residual(self, x: torch.Tensor, resid: torch.Tensor) -> bool:
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and x.shape[0] <= MAX_BLOCKS
                 and x.shape[1] % 8 == 0 and 2 * x.numel() <= self.max_bytes and x.is_contiguous()

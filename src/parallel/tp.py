@@ -33,6 +33,15 @@ class TPContext:
     world_size: int = 1
     group: Optional[object] = None
     car: Optional[object] = None  # CustomAllReduce (one-shot IPC all-reduce) once enabled
+    # host-side group for the step protocol's headers (gloo): followers learn each step's kind and
+    # sizes without a GPU round trip (None = the default group, when that is gloo already)
+    cpu_group: Optional[object] = None
+
+    def src_rank(self) -> int:
+        """Global rank of this group's rank 0 (the ``src`` of broadcasts)."""
+        if self.group is None:
+            return 0
+        return dist.get_global_rank(self.group, 0)
 
     def enable_custom_allreduce(self, max_bytes: int = 8 << 20) -> bool:
         """Collective over the group: set up the one-shot IPC all-reduce (src/parallel/custom_allreduce.py)
@@ -127,26 +136,38 @@ class TPContext:
         return out
 
     def all_gather_last(self, t: torch.Tensor) -> torch.Tensor:
-        """Concatenate the per-rank shards along the last dim."""
+        """Concatenate the per-rank shards [rows, cols] along the last dim (the vocab-parallel logits):
+        one launch of the one-shot IPC all-gather for decode-sized tensors (hipGraph-capturable on any
+        backend), else ONE all_gather_into_tensor into [W, rows, cols] and a permute."""
         if not self.enabled:
             return t
-        if self._staged(t):
-            c = t.float().cpu().contiguous()
+        car = self.car
+        if car is not None and t.dim() == 2 and car.can_run_gather(t):
+            return car.all_gather_last(t)
+        if self._staged(t) or dist.get_backend(self.group) == "gloo":  # gloo: list form (host-staged for GPU tensors)
+            c = t.float().cpu().contiguous() if t.is_cuda else t.contiguous()
             parts = [torch.empty_like(c) for _ in range(self.world_size)]
             dist.all_gather(parts, c, group=self.group)
             return torch.cat(parts, dim=-1).to(t.device, t.dtype)
-        parts = [torch.empty_like(t) for _ in range(self.world_size)]
-        dist.all_gather(parts, t.contiguous(), group=self.group)
-        return torch.cat(parts, dim=-1)
+        out = torch.empty((self.world_size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out.movedim(0, -2).reshape(*t.shape[:-1], self.world_size * t.shape[-1])
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.enabled:
+            src = self.src_rank() if src == 0 else src
             if self._staged(t):
                 c = t.cpu()
                 dist.broadcast(c, src=src, group=self.group)
                 t.copy_(c)
             else:
                 dist.broadcast(t, src=src, group=self.group)
+        return t
+
+    def broadcast_host(self, t: torch.Tensor) -> torch.Tensor:
+        """Broadcast a small CPU tensor from rank 0 over the host group (no GPU involvement)."""
+        if self.enabled:
+            dist.broadcast(t, src=self.src_rank(), group=self.cpu_group)
         return t
 
 
@@ -186,6 +207,9 @@ class ShardProbeTP(TPContext):
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         return t
 
+    def broadcast_host(self, t: torch.Tensor) -> torch.Tensor:
+        return t
+
 
 _TP: Optional[TPContext] = None
 
@@ -211,13 +235,19 @@ def init_tp(tp_size: Optional[int] = None, backend: Optional[str] = None,
         kw = {"timeout": datetime.timedelta(seconds=timeout_s)} if timeout_s else {}
         dist.init_process_group(backend=backend, **kw)
     rank = dist.get_rank()
-    if dist.get_world_size() == tp:
+    world_all = dist.get_world_size()
+    starts = range(0, world_all, tp)
+    if world_all == tp:
         group = None
     else:
         # consecutive ranks form a TP group (GPUs of one xGMI-connected node)
-        groups = [dist.new_group(list(range(s, s + tp))) for s in range(0, dist.get_world_size(), tp)]
+        groups = [dist.new_group(list(range(s, s + tp))) for s in starts]
         group = groups[rank // tp]
-    _TP = TPContext(rank=rank % tp, world_size=tp, group=group)
+    cpu_group = group
+    if dist.get_backend() != "gloo":  # step headers travel on a host (gloo) group: no GPU sync to read them
+        cpu_groups = [dist.new_group(list(range(s, s + tp)), backend="gloo") for s in starts]
+        cpu_group = cpu_groups[rank // tp]
+    _TP = TPContext(rank=rank % tp, world_size=tp, group=group, cpu_group=cpu_group)
     return _TP
 
 

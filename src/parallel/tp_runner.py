@@ -3,12 +3,24 @@ Tensor-parallel execution of the engine: one process per GPU, rank 0 drives.
 
 Rank 0 owns the scheduler, the KV block manager and the RPC front; every rank
 owns its weight shard and its KV-head shard of the paged pool (the block ids
-are the same on every rank, so one block table serves the whole group). Each
-step rank 0 builds the inputs, copies them to its device and broadcasts a
-6-int header plus the input tensors over RCCL (xGMI); then all ranks run the
-identical forward — including replaying the same captured decode hipGraph —
-and meet in the two per-layer all-reduces and the logits all-gather. Only
-rank 0 copies sampled token ids back to the host.
+are the same on every rank, so one block table serves the whole group).
+
+Step protocol (two messages per step):
+
+1. an 8-word header ``[kind, a, b, c, d, payload words, 0, 0]`` broadcast on the
+   host (gloo) group — followers read it without any GPU round trip;
+2. ONE int64 payload with every input of the step packed back to back (token
+   ids, positions, slots, context lengths, block-table rows, cu_q, last-token
+   indices), built in pinned memory on rank 0, copied up once and broadcast over
+   RCCL (xGMI); every rank unpacks it on the device into the runner's static
+   input buffers.
+
+Then all ranks run the identical forward — including replaying the same
+captured decode hipGraph — and meet in the two per-layer all-reduces (one-shot
+IPC kernel at decode sizes, fused with the residual add) and the logits
+all-gather (one-shot IPC all-gather). Followers never synchronise with their
+GPU: they can queue the next step as soon as its header arrives. Only rank 0
+copies sampled token ids back to the host.
 
 Failure as a unit: the process group carries a finite collective timeout
 (``init_tp(timeout_s=...)``) so a dead rank turns every peer's next collective
@@ -36,39 +48,69 @@ logger = logging.getLogger(__name__)
 
 class TPModelRunner(ModelRunner):
     HEARTBEAT_S = 20.0
+    HDR = 8
 
     def __init__(self, model: CausalLM, pool: KVPool, cfg: EngineConfig, max_model_len: int):
         super().__init__(model, pool, cfg, max_model_len)
         self.tp = model.tp
         self._last_sync = time.monotonic()
-        self.hdr = torch.zeros(6, dtype=torch.int64, device=self.device)
-        self.h_hdr = torch.zeros(6, dtype=torch.int64, pin_memory=self.is_cuda)
+        self.h_hdr = torch.zeros(self.HDR, dtype=torch.int64)  # host (gloo) header
+        cap = 3 * self.max_tokens + self.max_seqs * (self.bt_width + 3) + 1
+        self.h_pkt = torch.zeros(cap, dtype=torch.int64, pin_memory=self.is_cuda)
+        self.d_pkt = torch.zeros(cap, dtype=torch.int64, device=self.device)
+        self.steps_synced = 0
+
+    # ------------------------------------------------------------ protocol
+    def _fields(self, kind: int, a: int, b: int, d: int):
+        """(device buffer view, rows) of the step's inputs, in payload order."""
+        if kind == self.KIND_PREFILL:
+            t, n, nd = a, b, d
+            out = [(self.d_ids, t), (self.d_pos, t), (self.d_slots, t), (self.d_ctx, n), (self.d_bt, n),
+                   (self.d_cu, n + 1)]
+            return out + [(self.d_last, nd)] if nd else out
+        if kind == self.KIND_DECODE:
+            pad = b
+            return [(self.d_ids, pad), (self.d_pos, pad), (self.d_slots, pad), (self.d_ctx, pad), (self.d_bt, pad)]
+        return []
+
+    def _host_of(self, dbuf: torch.Tensor) -> torch.Tensor:
+        return {id(self.d_ids): self.h_ids, id(self.d_pos): self.h_pos, id(self.d_slots): self.h_slots,
+                id(self.d_ctx): self.h_ctx, id(self.d_bt): self.h_bt, id(self.d_cu): self.h_cu,
+                id(self.d_last): self.h_last}[id(dbuf)]
+
+    def _pack(self, kind: int, a: int, b: int, d: int) -> int:
+        pkt = self.h_pkt.numpy()
+        o = 0
+        for dbuf, rows in self._fields(kind, a, b, d):
+            src = self._host_of(dbuf)[:rows].numpy().reshape(-1)
+            pkt[o:o + src.size] = src
+            o += src.size
+        return o
+
+    def _unpack(self, kind: int, a: int, b: int, d: int) -> None:
+        o = 0
+        for dbuf, rows in self._fields(kind, a, b, d):
+            view = dbuf[:rows]
+            n = view.numel()
+            view.copy_(self.d_pkt[o:o + n].view(view.shape))  # int64 -> int32 where the buffer is int32
+            o += n
 
     def _bcast(self, t: torch.Tensor) -> None:
         self.tp.broadcast(t, src=0)
 
     def _sync_step(self, kind: int, a: int = 0, b: int = 0, c: int = 0, d: int = 0) -> None:
+        """Leader: header on the host group, then the packed payload (the leader's own device buffers
+        were already filled by the runner's H2D copies, so it does not unpack)."""
         if not self.tp.enabled:
             return
         self._last_sync = time.monotonic()
-        self.h_hdr.copy_(torch.tensor([kind, a, b, c, d, 0], dtype=torch.int64))
-        self.hdr.copy_(self.h_hdr, non_blocking=self.is_cuda)
-        self._bcast(self.hdr)
-        self._bcast_inputs(kind, a, b, c, d)
-
-    def _bcast_inputs(self, kind: int, a: int, b: int, c: int, d: int) -> None:
-        if kind == self.KIND_PREFILL:
-            t, n, nd = a, b, d
-            for buf in (self.d_ids[:t], self.d_pos[:t], self.d_slots[:t], self.d_ctx[:n], self.d_bt[:n],
-                        self.d_cu[: n + 1]):
-                self._bcast(buf)
-            if nd:
-                self._bcast(self.d_last[:nd])
-        elif kind == self.KIND_DECODE:
-            pad = b
-            for buf in (self.d_ids[:pad], self.d_pos[:pad], self.d_slots[:pad], self.d_ctx[:pad],
-                        self.d_bt[:pad]):
-                self._bcast(buf)
+        nw = self._pack(kind, a, b, d)
+        self.h_hdr.copy_(torch.tensor([kind, a, b, c, d, nw, 0, 0], dtype=torch.int64))
+        self.tp.broadcast_host(self.h_hdr)
+        if nw:
+            self.d_pkt[:nw].copy_(self.h_pkt[:nw], non_blocking=self.is_cuda)
+            self._bcast(self.d_pkt[:nw])
+        self.steps_synced += 1
 
     def idle_tick(self) -> None:
         if self.tp.enabled and self.tp.rank == 0 and time.monotonic() - self._last_sync > self.HEARTBEAT_S:
@@ -80,22 +122,24 @@ class TPModelRunner(ModelRunner):
 
     @torch.inference_mode()
     def follower_loop(self) -> None:
-        """Ranks > 0: mirror rank 0's steps until it sends STOP."""
+        """Ranks > 0: mirror rank 0's steps until it sends STOP. No host-device synchronisation: the
+        header arrives on the host group, the payload and the step's kernels are queued on the stream."""
         assert self.tp.rank != 0
         while True:
-            self._bcast(self.hdr)
-            kind, a, b, c, d, _ = (int(x) for x in self.hdr.tolist())
+            self.tp.broadcast_host(self.h_hdr)
+            kind, a, b, c, d, nw = (int(x) for x in self.h_hdr.tolist()[:6])
             if kind == self.KIND_STOP:
                 return
             if kind == self.KIND_HEARTBEAT:
                 continue
-            self._bcast_inputs(kind, a, b, c, d)
+            if nw:
+                self._bcast(self.d_pkt[:nw])
+                self._unpack(kind, a, b, d)
             if kind == self.KIND_PREFILL:
                 self._exec_prefill(a, b, c, d, True)
             else:
                 self._exec_decode(a, b)
-            if self.is_cuda:
-                torch.cuda.current_stream(self.device).synchronize()
+            self.steps_synced += 1
 
 
 def agree_num_blocks(n: int, tp) -> int:

@@ -83,6 +83,23 @@ def _worker(rank, world, port, q):
         fused_ok = torch.equal(resid.cpu(), want) and torch.allclose(
             ssp[:m].cpu(), want.float().pow(2).sum(-1), rtol=1e-4, atol=1e-2)
         replay_ok.append(fused_ok)
+        # one-shot all-gather along the last dim (vocab-parallel logits), eager and under hipGraph replay
+        rows, cols = 24, 4000
+        g = torch.Generator(device="cuda").manual_seed(31 + rank)
+        part = torch.randn(rows, cols, device="cuda", generator=g).to(torch.bfloat16)
+        got = car.all_gather_last(part)
+        torch.cuda.synchronize()
+        parts = [torch.empty(rows, cols) for _ in range(world)]
+        dist.all_gather(parts, part.float().cpu())
+        replay_ok.append(torch.equal(got.cpu(), torch.cat(parts, -1).to(torch.bfloat16)))
+        gin = torch.zeros(rows, cols, device="cuda", dtype=torch.bfloat16)
+        gg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gg):
+            gout = car.all_gather_last(gin)
+        gin.fill_(float(rank + 1))
+        gg.replay()
+        torch.cuda.synchronize()
+        replay_ok.append(all(bool((gout[:, p * cols:(p + 1) * cols].float() == p + 1).all()) for p in range(world)))
         err = car.error()
         ctl = car.read_ctl()
         dist.barrier()
@@ -120,7 +137,8 @@ def test_custom_allreduce_ranks_one_gpu(world):
         assert all(ok.values()), ok
         assert all(replay_ok), replay_ok
         assert not err
-        assert ctl[0] == len(SIZES) + 1 + 5 + 1 and ctl[1] == 0, ctl  # one epoch per executed call (not the capture)
+        # one epoch per executed call (not the captures): sizes, graph warm-up, 5 replays, fused, 2 gathers
+        assert ctl[0] == len(SIZES) + 1 + 5 + 1 + 2 and ctl[1] == 0, ctl
     for n in SIZES:
         for r in range(1, world):
             assert (res[0][2][n] == res[r][2][n]).all()  # bit-identical on every rank

@@ -166,7 +166,7 @@ def test_kv_export_import_exact(engine):
     dec.abort("kvx")
 
 
-def _tp_gpu_worker(rank, world, port, q, preset, moe_parallel="tp", sp=False):
+def _tp_gpu_worker(rank, world, port, q, preset, moe_parallel="tp", sp=False, graphs=False):
     import os
 
     import torch.distributed as dist
@@ -179,13 +179,15 @@ def _tp_gpu_worker(rank, world, port, q, preset, moe_parallel="tp", sp=False):
     try:
         tp = TPContext(rank=rank, world_size=world)
         cfg = EngineConfig(max_num_seqs=4, max_num_batched_tokens=256, num_kv_blocks=128, max_latency_ms=0.0,
-                           use_cuda_graph=False)
-        obj = build_tp_engine(preset, tp, "cuda:0", cfg=cfg, max_model_len=512, capture=False,
+                           use_cuda_graph=graphs, graph_batch_sizes=[1, 2, 4])
+        obj = build_tp_engine(preset, tp, "cuda:0", cfg=cfg, max_model_len=512, capture=graphs,
                               full_init=True, seed=3, moe_parallel=moe_parallel, sequence_parallel=sp)
         if rank == 0:
             obj.eos_token_id = None
-            q.put((obj.generate(TP_PROMPTS, SamplingParams(max_tokens=8)), tp.car is not None))
+            outs = obj.generate(TP_PROMPTS, SamplingParams(max_tokens=8))
+            replayed = bool(obj.runner.graphs)
             obj.runner.stop_followers()
+            q.put((outs, tp.car is not None, replayed, bool(tp.car.error()) if tp.car is not None else None))
         else:
             obj.follower_loop()
     finally:
@@ -195,11 +197,14 @@ def _tp_gpu_worker(rank, world, port, q, preset, moe_parallel="tp", sp=False):
 TP_PROMPTS = [[5, 9, 33, 12, 7] * 9, [100, 200, 300], list(range(3, 140))]
 
 
-@pytest.mark.parametrize("preset,moe_parallel,sp", [("llama-mini", "tp", False), ("mixtral-tiny", "tp", False),
-                                                    ("mixtral-tiny", "ep", False), ("llama-mini", "tp", True)])
-def test_tensor_parallel_tp2_on_one_gpu(preset, moe_parallel, sp):
-    """The TP=2 code path on real kernels: two ranks share the GPU (gloo, collectives staged
-    through the host), Megatron-split weights drawn from the same stream as the TP=1 model;
+@pytest.mark.parametrize("preset,moe_parallel,sp,world,graphs",
+                         [("llama-mini", "tp", False, 2, False), ("mixtral-tiny", "tp", False, 2, False),
+                          ("mixtral-tiny", "ep", False, 2, False), ("llama-mini", "tp", True, 2, False),
+                          ("llama-mini", "tp", False, 4, True), ("llama-mini", "tp", False, 8, True)])
+def test_tensor_parallel_on_one_gpu(preset, moe_parallel, sp, world, graphs):
+    """The TP code path on real kernels: 2, 4 or 8 ranks share the GPU (gloo for the step protocol;
+    all-reduces and the logits all-gather on the one-shot IPC kernels, which the decode hipGraphs
+    replay), Megatron-split weights drawn from the same stream as the TP=1 model;
     greedy tokens must agree, up to near-ties, with a TP=1 bf16 model built from the same
     full-size weights (greedy no-cache recompute through the same GPU kernels)."""
     import socket
@@ -215,14 +220,16 @@ def test_tensor_parallel_tp2_on_one_gpu(preset, moe_parallel, sp):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_tp_gpu_worker, args=(r, 2, port, q, preset, moe_parallel, sp)) for r in range(2)]
+    procs = [ctx.Process(target=_tp_gpu_worker, args=(r, world, port, q, preset, moe_parallel, sp, graphs))
+             for r in range(world)]
     for p in procs:
         p.start()
-    got, used_car = q.get(timeout=600)
+    got, used_car, replayed, car_err = q.get(timeout=600)
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
-    assert used_car  # decode/prefill all-reduces went through the one-shot IPC kernel (allreduce.hip)
+    assert used_car and car_err is False  # all-reduces / logits all-gather on the one-shot IPC kernels
+    assert replayed == graphs             # graphs: decode steps replayed hipGraphs on every rank
     m = CausalLM(get_preset(preset), "cuda:0", seed=3, max_position=512, full_init=True)
     for p, o in zip(TP_PROMPTS, got):
         r, mg = reference_with_margins(m, p, 8)
