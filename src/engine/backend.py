@@ -239,17 +239,33 @@ class LLMBackend:
         from src.preproc import SamplingParams
 
         d = msg["packet"]
-        if d.get("ipc") is not None:  # payload already delivered by DMA into the landing zone
-            kv = self._landing_zone().take(int(d["ipc"]["offset"]), d["shape"])
+        handed: List[bool] = []
+        off = -1
+        if d.get("ipc") is not None:  # payload already delivered into the landing zone by the sender's copy
+            zone, off = self._landing_zone(), int(d["ipc"]["offset"])
+            kv = zone.claim(off, d["shape"])  # a view: the engine scatters straight from the zone
+
+            def on_imported(ev, zone=zone, off=off, handed=handed):
+                handed.append(True)
+                zone.release_after(off, ev)
+
             packet = KVPacket(d["request_id"], list(d["prompt_ids"]), int(d["first_token"]), kv,
-                              int(d["block_size"]), dict(d.get("sampling") or {}), d.get("ttft_ms"))
+                              int(d["block_size"]), dict(d.get("sampling") or {}), d.get("ttft_ms"),
+                              on_imported=on_imported)
             self.ipc_imports += 1
         else:
             packet = packet_for_import(d, self.engine.device)
         sp = SamplingParams(**packet.sampling) if packet.sampling else SamplingParams()
         if not self.async_engine.running:
             self.async_engine.start()
-        seq = await self.async_engine.submit(packet.request_id, [], sp, user_data={"import_packet": packet})
+        try:
+            seq = await self.async_engine.submit(packet.request_id, [], sp, user_data={"import_packet": packet})
+        except Exception:
+            # the engine failed before importing it: free the slot now (a cancelled caller does not free it:
+            # the queued import still runs and releases it behind its scatter)
+            if packet.on_imported is not None and not handed:
+                self._landing_zone().release(off)
+            raise
         return {"success": True, "outputs": build_llm_output(
             seq.output_ids, self.tokenizer, prompt_len=seq.prompt_len, finish_reason=seq.finish_reason or "length",
             ttft_ms=packet.ttft_ms, latency_ms=seq.latency_ms())}
@@ -259,7 +275,14 @@ class LLMBackend:
 
     async def handle_op(self, op: str, msg: Dict[str, Any]) -> Dict[str, Any]:
         if op == "engine_stats":
-            return {"success": True, "stats": self.async_engine.stats()}
+            st = self.async_engine.stats()
+            if self._zone is not None:
+                z = self._zone
+                z._reap()
+                st["kv_zone"] = {"slots_used": len(z._used), "reserved": len(z._reserved_at),
+                                 "pending_release": len(z._pending), "expired": z.expired,
+                                 "capacity": z.capacity}
+            return {"success": True, "stats": st}
         if op == "kv_import":
             return await self._kv_import(msg)
         if op == "kv_channel":  # same-node prefill workers map this GPU's landing zone (IPC)
@@ -268,9 +291,18 @@ class LLMBackend:
             z = self._landing_zone()
             return {"success": True, "handle": z.handle, "capacity": z.capacity, "device": str(z.device),
                     "pid": os.getpid()}
-        if op == "kv_reserve":
-            off = self._landing_zone().reserve(int(msg["nbytes"]))
+        if op == "kv_reserve":  # optionally wait up to wait_s for slots to come back (no host sync: polling)
+            zone, n = self._landing_zone(), int(msg["nbytes"])
+            if n > zone.capacity:
+                return {"success": False, "offset": None, "error": "packet larger than the landing zone"}
+            deadline = time.monotonic() + float(msg.get("wait_s") or 0.0)
+            off = zone.reserve(n)
+            while off is None and time.monotonic() < deadline:
+                await asyncio.sleep(0.0005)
+                off = zone.reserve(n)
             return {"success": off is not None, "offset": off}
+        if op == "kv_release":  # a sender gave up on a reserved slot (copy or kv_import failed)
+            return {"success": self._landing_zone().release(int(msg["offset"]))}
         raise ValueError(f"unsupported op {op}")
 
     def get_metrics(self) -> Dict[str, Any]:

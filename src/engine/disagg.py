@@ -16,6 +16,7 @@ control-plane RPC (``op: kv_import``).
 
 from __future__ import annotations
 
+import asyncio
 import logging
 import os
 import time
@@ -57,7 +58,11 @@ class DisaggregatedServer:
             pseq.sampling = sampling
             return pseq
         t0 = time.perf_counter()
-        kv, ready = ship(pseq.kv_export, self.decode.engine.device, getattr(pseq, "kv_export_ready", None))
+        dst = self.decode.engine.device
+        if dst.type == "cuda" and pseq.kv_export.is_cuda:  # peer copy on a transfer stream: no host sync
+            kv, ready = ship(pseq.kv_export, dst, getattr(pseq, "kv_export_ready", None))
+        else:  # a host hop waits for the gather: off the event-loop thread
+            kv, ready = await asyncio.to_thread(ship, pseq.kv_export, dst, getattr(pseq, "kv_export_ready", None))
         self.transfer_s += time.perf_counter() - t0   # issue time: the copy itself is asynchronous
         self.transfers += 1
         self.bytes_moved += kv.numel() * kv.element_size()
@@ -79,17 +84,26 @@ class RemoteDecodeLink:
     two GPUs) and only the metadata crosses the socket; anywhere else — or if the zone is full — the
     payload rides the RPC frame as bytes."""
 
-    def __init__(self, address: str, model: str, timeout: float = 600.0, use_ipc: bool = True):
+    def __init__(self, address: str, model: str, timeout: float = 600.0, use_ipc: bool = True,
+                 reserve_wait_s: float = 30.0):
         self.address = address
+        self.reserve_wait_s = reserve_wait_s
         self.model = model
         self.rpc = RPCClient(max_idle_per_host=64, codec=b"M")  # msgpack: raw KV bytes, no base64
         self.timeout = timeout
         self.use_ipc = use_ipc
         self._ipc = None
+        self._ipc_lock = asyncio.Lock()
         self.ipc_packets = 0
         self.wire_packets = 0
 
     async def _channel(self, device):
+        if self._ipc is not None or not self.use_ipc or device.type != "cuda":
+            return self._ipc
+        async with self._ipc_lock:  # concurrent first sends: map the zone once
+            return await self._open_channel(device)
+
+    async def _open_channel(self, device):
         if self._ipc is None and self.use_ipc and device.type == "cuda":
             try:
                 rep = await self.rpc.call(self.address, {"op": "kv_channel", "model": self.model}, self.timeout)
@@ -111,16 +125,34 @@ class RemoteDecodeLink:
     async def send(self, packet: KVPacket) -> Dict[str, Any]:
         ch = await self._channel(packet.kv.device)
         if ch is not None:
+            # the decode worker waits (briefly) for a slot to come back rather than refuse: slots return as
+            # soon as its engine has scattered them, and the byte path is far slower than waiting
             rep = await self.rpc.call(self.address, {"op": "kv_reserve", "model": self.model,
-                                                     "nbytes": packet.nbytes}, self.timeout)
+                                                     "nbytes": packet.nbytes, "wait_s": self.reserve_wait_s},
+                                      self.timeout)
             if rep.get("success"):
-                ch.write(rep["offset"], packet.kv, packet.ready)
-                wire = dict(packet_meta(packet), ipc={"offset": rep["offset"]})
-                self.ipc_packets += 1
-                return await self.rpc.call(self.address, {"op": "kv_import", "model": self.model, "packet": wire},
-                                           self.timeout)
+                off = rep["offset"]
+                imported = False
+                try:
+                    # the copy runs on a transfer stream after the prefill engine's gather; the event loop
+                    # only polls its completion event (no synchronize on this thread)
+                    await ch.write_async(off, packet.kv, packet.ready)
+                    wire = dict(packet_meta(packet), ipc={"offset": off})
+                    self.ipc_packets += 1
+                    imported = True  # from here the decode worker owns the slot (released after its scatter)
+                    return await self.rpc.call(self.address, {"op": "kv_import", "model": self.model,
+                                                              "packet": wire}, self.timeout)
+                except BaseException:
+                    if not imported:  # the slot would leak: hand it back (best effort; it also expires)
+                        try:
+                            await self.rpc.call(self.address, {"op": "kv_release", "model": self.model,
+                                                               "offset": off}, 30.0)
+                        except Exception:
+                            logger.warning("kv_release of slot %d on %s failed", off, self.address)
+                    raise
         self.wire_packets += 1
-        msg = {"op": "kv_import", "model": self.model, "packet": packet_to_wire(packet)}
+        # device -> host copy of the payload: off the event-loop thread
+        msg = {"op": "kv_import", "model": self.model, "packet": await asyncio.to_thread(packet_to_wire, packet)}
         return await self.rpc.call(self.address, msg, self.timeout)
 
 

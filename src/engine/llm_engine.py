@@ -136,6 +136,19 @@ class LLMEngine:
                      on_finish: Optional[Callable[[Sequence], None]] = None) -> Sequence:
         """Resume a sequence whose prompt KV was computed by a prefill worker:
         allocate blocks, scatter the shipped KV into them, join the decode batch."""
+        try:
+            return self._add_imported(packet, sampling, on_finish)
+        finally:
+            # the packet's buffer (e.g. an IPC landing-zone slot) is free once the scatter queued above
+            # has run: hand the importer an event recorded behind it (never a host sync)
+            if getattr(packet, "on_imported", None) is not None:
+                ev = None
+                if packet.kv.is_cuda:
+                    ev = torch.cuda.Event()
+                    ev.record(torch.cuda.current_stream(self.device))
+                packet.on_imported(ev)
+
+    def _add_imported(self, packet, sampling: SamplingParams, on_finish) -> Sequence:
         from src.parallel.kv_transfer import import_blocks
 
         if packet.block_size != self.cfg.block_size:

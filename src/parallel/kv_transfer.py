@@ -7,8 +7,9 @@ with the ``move_blocks`` HIP kernel, and ships it to the decode worker's GPU:
 
 * same process, other GPU  → ``tensor.to(dst)`` = ``hipMemcpyPeerAsync`` over
   xGMI (SDMA engines; compute keeps running);
-* other process, same node → RCCL point-to-point (``dist.send/recv``), which
-  also rides xGMI (:class:`RCCLChannel`);
+* other process, same node → a device-to-device copy into the decode worker's
+  IPC-mapped landing zone (:class:`IPCSender` / :class:`IPCLandingZone`), or
+  RCCL point-to-point between ranks of one group (:class:`RCCLChannel`);
 * anywhere else            → framed bytes over the control-plane TCP socket
   (:func:`packet_to_wire` / :func:`packet_from_wire`), the CPU fallback.
 
@@ -21,7 +22,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 import threading
-from typing import Any, Dict, List, Optional
+import time
+from typing import Any, Callable, Dict, List, Optional
 
 import numpy as np
 import torch
@@ -40,6 +42,9 @@ class KVPacket:
     sampling: Dict[str, Any] = field(default_factory=dict)
     ttft_ms: Optional[float] = None
     ready: Any = None                # HIP event: kv is complete on its device (None = already complete)
+    # called by the importing engine thread with an event recorded behind its scatter (the kv buffer
+    # may be reused once that event completes): frees an IPC landing-zone slot without a host sync
+    on_imported: Optional[Callable[[Any], None]] = None
 
     @property
     def nbytes(self) -> int:
@@ -96,9 +101,16 @@ def ship(buf: torch.Tensor, device, ready=None):
 class IPCLandingZone:
     """Decode-worker side of cross-process KV shipping on one node: ONE IPC-shareable device buffer
     (plain hipMalloc, so this GPU reads it through its caches) that prefill workers map
-    (hipIpcOpenMemHandle) and fill by DMA over xGMI — the packed prompt KV never touches host memory
-    or the RPC socket, which then carries only the metadata. Space is handed out per packet
-    (``reserve``, first fit) and returned once the decode engine has its own copy (``take``).
+    (hipIpcOpenMemHandle) and fill with device-to-device copies over xGMI — the packed prompt KV never
+    touches host memory or the RPC socket, which then carries only the metadata.
+
+    Lifecycle of a slot (no host synchronisation anywhere):
+    ``reserve`` (kv_reserve RPC, first fit) → the sender copies and tells us (kv_import) → ``claim``
+    hands the engine a VIEW of the slot (no clone) → the engine thread scatters it straight into its
+    paged pool with ``move_blocks`` and calls ``release_after`` with an event recorded behind the
+    scatter → the slot returns to the free list once that event has completed (checked without
+    blocking whenever space is reserved). A reservation that is never imported (sender failed, client
+    gone) is returned by ``release`` (kv_release RPC) or expires after ``reserve_ttl_s``.
 
     The zone stays below 2 GiB: on this ROCm (7.2, dmabuf IPC) hipIpcOpenMemHandle of a 2 GiB
     allocation never returns in the importing process, while 256 MiB..1 GiB open in < 10 ms
@@ -107,7 +119,7 @@ class IPCLandingZone:
     ALIGN = 1 << 16
     MAX_BYTES = (1 << 31) - (1 << 20)
 
-    def __init__(self, device, capacity: int = 1 << 30, uncached: bool = False):
+    def __init__(self, device, capacity: int = 1 << 30, uncached: bool = False, reserve_ttl_s: float = 120.0):
         from src import _C
 
         self.device = torch.device(device)
@@ -118,11 +130,30 @@ class IPCLandingZone:
             self.ptr = _C.car_alloc(self.capacity, uncached)
             self.view = _C.car_tensor(self.ptr, self.capacity, self.device.index or 0)
         self.handle = _C.car_handle(self.ptr).hex()
+        self.reserve_ttl_s = reserve_ttl_s
         self._free: List[List[int]] = [[0, self.capacity]]  # sorted [start, end) ranges
         self._used: Dict[int, int] = {}
+        self._reserved_at: Dict[int, float] = {}   # reserved, not yet imported (expire after the TTL)
+        self._pending: List[Any] = []              # (offset, event): released once the scatter has run
         self._lock = threading.Lock()
+        self.expired = 0
+
+    def _reap(self) -> None:
+        now = time.monotonic()
+        with self._lock:
+            done, keep = [], []
+            for o, e in self._pending:  # query each event once: it may complete between two looks
+                (done if e is None or e.query() else keep).append((o, e))
+            self._pending = keep
+            stale = [o for o, t in self._reserved_at.items() if now - t > self.reserve_ttl_s]
+        for o, _ in done:
+            self.release(o)
+        for o in stale:
+            self.expired += 1
+            self.release(o)
 
     def reserve(self, nbytes: int) -> Optional[int]:
+        self._reap()
         n = -(-int(nbytes) // self.ALIGN) * self.ALIGN
         with self._lock:
             for r in self._free:
@@ -131,12 +162,16 @@ class IPCLandingZone:
                     r[0] += n
                     self._free = [x for x in self._free if x[1] > x[0]]
                     self._used[off] = n
+                    self._reserved_at[off] = time.monotonic()
                     return off
         return None
 
-    def release(self, offset: int) -> None:
+    def release(self, offset: int) -> bool:
         with self._lock:
-            n = self._used.pop(int(offset))
+            n = self._used.pop(int(offset), None)
+            self._reserved_at.pop(int(offset), None)
+            if n is None:
+                return False
             self._free.append([offset, offset + n])
             self._free.sort()
             merged: List[List[int]] = []
@@ -146,15 +181,29 @@ class IPCLandingZone:
                 else:
                     merged.append(r)
             self._free = merged
+            return True
+
+    def claim(self, offset: int, shape: List[int]) -> torch.Tensor:
+        """A delivered packet as a bf16 view of its slot (the slot stays allocated until ``release_after``)."""
+        offset = int(offset)
+        n = int(np.prod(shape)) * 2
+        with self._lock:
+            if offset not in self._used or self._used[offset] < n:
+                raise ValueError(f"kv_import of an unknown or too small landing-zone slot at {offset}")
+            self._reserved_at.pop(offset, None)  # imported: no longer expires
+        return self.view[offset: offset + n].view(torch.bfloat16).view(*shape)
+
+    def release_after(self, offset: int, event=None) -> None:
+        """Free the slot once ``event`` (recorded behind the consumer's scatter) has completed."""
+        with self._lock:
+            self._pending.append((int(offset), event))
 
     def take(self, offset: int, shape: List[int]) -> torch.Tensor:
-        """Copy a delivered packet out of the zone (same-GPU D2D) and free its space."""
-        n = int(np.prod(shape)) * 2
-        with torch.cuda.device(self.device):
-            src = self.view[offset: offset + n].view(torch.bfloat16).view(*shape)
-            kv = src.clone()
-            torch.cuda.current_stream(self.device).synchronize()
-        self.release(offset)
+        """Copy a delivered packet out of the zone and free its slot (tests / callers without a stream)."""
+        kv = self.claim(offset, shape).clone()
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self.release_after(offset, ev)
         return kv
 
     def close(self) -> None:
@@ -166,29 +215,53 @@ class IPCLandingZone:
 
 class IPCSender:
     """Prefill-worker side: maps a decode worker's :class:`IPCLandingZone` into this GPU's address
-    space once, then each packet is one device-to-device copy into it (SDMA / blit over xGMI)."""
+    space once, then each packet is one device-to-device copy into it on a dedicated transfer stream,
+    ordered after the prefill engine's gather by its event. ``write`` returns that copy's completion
+    event; ``write_async`` awaits it by polling (the asyncio thread never blocks on the GPU).
+
+    ``DIE_KV_COPY=dma`` copies with hipMemcpyAsync (copy engines; compute keeps all CUs) instead of the
+    default shader-store copy kernel (bench/micro_ipc_copy.py measures both)."""
 
     def __init__(self, handle_hex: str, capacity: int, device):
+        import os
+
         from src import _C
 
         self.device = torch.device(device)
         with torch.cuda.device(self.device):
             self.ptr = _C.car_open(bytes.fromhex(handle_hex))
             self.view = _C.car_tensor(self.ptr, int(capacity), self.device.index or 0)
+            self.stream = torch.cuda.Stream(device=self.device)
+        self.dma = os.environ.get("DIE_KV_COPY", "shader") == "dma"
         self.bytes_sent = 0
 
-    def write(self, offset: int, kv: torch.Tensor, ready=None) -> None:
+    def write(self, offset: int, kv: torch.Tensor, ready=None):
         from src import _C
 
         flat = kv.contiguous().view(torch.uint8).view(-1)
-        with torch.cuda.device(self.device):
-            cur = torch.cuda.current_stream(self.device)
+        s = self.stream
+        with torch.cuda.device(self.device), torch.cuda.stream(s):
             if ready is not None:
-                cur.wait_event(ready)
-            # shader stores into the mapped peer buffer (the DMA engines are not used on IPC mappings)
-            _C.car_copy_to(self.ptr + int(offset), flat)
-            cur.synchronize()  # delivered before the decode worker is told to import it
+                s.wait_event(ready)
+            else:
+                s.wait_stream(torch.cuda.current_stream(self.device))
+            if self.dma:
+                self.view[int(offset): int(offset) + flat.numel()].copy_(flat, non_blocking=True)
+            else:  # shader stores into the mapped peer buffer
+                _C.car_copy_to(self.ptr + int(offset), flat)
+            done = torch.cuda.Event()
+            done.record(s)
+        flat.record_stream(s)  # the staging tensor lives until the copy has read it
         self.bytes_sent += flat.numel()
+        return done
+
+    async def write_async(self, offset: int, kv: torch.Tensor, ready=None, poll_s: float = 2e-4) -> None:
+        """Copy and wait for delivery without blocking the event loop."""
+        import asyncio
+
+        done = self.write(offset, kv, ready)
+        while not done.query():
+            await asyncio.sleep(poll_s)
 
     def close(self) -> None:
         from src import _C

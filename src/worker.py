@@ -247,7 +247,7 @@ class Worker:
             if not resp.get("success"):
                 self._error_count += 1
             return resp
-        if op in ("kv_export", "kv_import", "kv_channel", "kv_reserve", "engine_stats"):
+        if op in ("kv_export", "kv_import", "kv_channel", "kv_reserve", "kv_release", "engine_stats"):
             m = self.models.get(msg.get("model"))
             if m is None or not hasattr(m, "handle_op"):
                 return {"error": f"op {op} unsupported for model {msg.get('model')!r}", "success": False}

@@ -150,6 +150,29 @@ def test_gpu_disaggregated_ipc_landing_zone():
                 assert a["outputs"]["token_ids"] == b["outputs"]["token_ids"]
             link = pre.models["mini"]._decode_link
             assert link.ipc_packets == 3 and link.wire_packets == 0, (link.ipc_packets, link.wire_packets)
+            cd = InferenceClient(f"127.0.0.1:{dport}")
+
+            async def zone():
+                st = await cd.call({"op": "engine_stats", "model": "mini"})
+                return st["stats"]["kv_zone"]
+
+            z = await zone()  # every imported slot went back behind the decode engine's scatter
+            assert z["slots_used"] == 0 and z["pending_release"] == 0, z
+            # a sender whose copy fails after kv_reserve hands the slot back (kv_release), no leak
+            real = link._ipc.write_async
+
+            async def broken(*a, **k):
+                raise RuntimeError("injected copy failure")
+            link._ipc.write_async = broken
+            req = {"prompt_token_ids": list(range(9, 200)), "max_tokens": 8, "ignore_eos": True}
+            r = await asyncio.wait_for(cp.call({"model": "mini", "inputs": req}), 60)
+            assert not r["success"]
+            z = await zone()
+            assert z["slots_used"] == 0 and z["reserved"] == 0, z
+            link._ipc.write_async = real
+            r = await asyncio.wait_for(cp.call({"model": "mini", "inputs": req}), 60)
+            assert r["success"] and r["outputs"]["disaggregated"]
+            cd.close()
             for x in (cp, cs):
                 x.close()
             for w in (pre, solo):
