@@ -111,6 +111,34 @@ async def load(client, model, make_inputs, n, conc):
     return time.perf_counter() - t0, lat, ok
 
 
+def _client_proc(caddr, n, conc, q):
+    async def run():
+        c = InferenceClient(caddr)
+        await load(c, "echo", lambda i: {"i": i, "payload": "x" * 64}, conc, conc)  # warm connections
+        t0 = time.perf_counter()
+        el, lat, ok = await load(c, "echo", lambda i: {"i": i, "payload": "x" * 64}, n, conc)
+        c.close()
+        q.put((t0, t0 + el, lat, ok))
+    asyncio.run(run())
+
+
+def multi_client_load(caddr, n, conc, procs):
+    """Load from several processes (one event loop cannot saturate a multi-process coordinator): each
+    sends n/procs requests at conc/procs; the rate is over the union of their timed windows."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_client_proc, args=(caddr, n // procs, max(1, conc // procs), q)) for _ in range(procs)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=600) for _ in ps]
+    for p in ps:
+        p.join(60)
+    t0, t1 = min(r[0] for r in res), max(r[1] for r in res)
+    return t1 - t0, [x for r in res for x in r[2]], sum(r[3] for r in res)
+
+
 async def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", choices=["mock", "llm"], default="mock")
@@ -126,19 +154,48 @@ async def main():
     ap.add_argument("--strategy", default="least_connections")
     ap.add_argument("--direct", action="store_true",
                     help="client-side load balancer straight to the workers (the reference harness's topology)")
+    ap.add_argument("--coord-procs", type=int, default=0,
+                    help="0: coordinator in this process (shares the client's event loop); N >= 1: a separate "
+                         "`python -m src.coordinator --procs N` (N processes on one SO_REUSEPORT port)")
+    ap.add_argument("--client-procs", type=int, default=1, help="load-generator processes (mock mode)")
     args = ap.parse_args()
 
-    coord = Coordinator(port=0, max_batch_size=32, max_latency_ms=args.max_latency_ms, strategy=args.strategy,
-                        health_check_interval=2.0)
-    port = await coord.start()
+    coord, cproc = None, None
+    if args.coord_procs:
+        fd, pf = tempfile.mkstemp()
+        os.close(fd)
+        os.unlink(pf)
+        cproc = subprocess.Popen([sys.executable, "-m", "src.coordinator", "--listen-port", "0", "--procs",
+                                  str(args.coord_procs), "--port-file", pf, "--max-latency-ms",
+                                  str(args.max_latency_ms), "--strategy", args.strategy],
+                                 cwd=ROOT, stdout=subprocess.DEVNULL, stderr=open("/tmp/bench_coord.log", "w"))
+        for _ in range(600):
+            if os.path.exists(pf):
+                break
+            await asyncio.sleep(0.1)
+        port = int(open(pf).read())
+    else:
+        coord = Coordinator(port=0, max_batch_size=32, max_latency_ms=args.max_latency_ms, strategy=args.strategy,
+                            health_check_interval=2.0)
+        port = await coord.start()
     caddr = f"127.0.0.1:{port}"
     n_workers = args.workers if args.mode == "mock" else args.gpus
     procs = [spawn_worker(f"bw{i}", caddr, args, gpu=i if args.mode == "llm" else None) for i in range(n_workers)]
     try:
+        probe = InferenceClient(caddr)
         for _ in range(600):
-            if coord.healthy_worker_count() == n_workers:
+            if coord is not None and coord.healthy_worker_count() == n_workers:
                 break
+            if coord is None:  # every process of a multi-process coordinator must know every worker
+                counts = []
+                for _ in range(4 * max(1, args.coord_procs)):
+                    c = InferenceClient(caddr)
+                    counts.append((await c.call({"op": "health"})).get("workers", 0))
+                    c.close()
+                if min(counts) == n_workers:
+                    break
             await asyncio.sleep(0.1)
+        probe.close()
         if args.direct:
             client = DirectClient([w["address"] for w in (coord.router.get_worker_info(x)
                                                           for x in coord.router.workers)], args.strategy)
@@ -159,12 +216,16 @@ async def main():
             await load(client, model, make_inputs, 32 * n_workers, 32 * n_workers)  # warm-up
         for conc in [int(c) for c in args.concurrency.split(",")]:
             n = args.requests if args.mode == "mock" else max(conc, 3 * 32 * n_workers)
-            el, lat, ok = await load(client, model, make_inputs, n, conc)
+            if args.mode == "mock" and args.client_procs > 1:
+                el, lat, ok = multi_client_load(caddr, n, conc, args.client_procs)
+            else:
+                el, lat, ok = await load(client, model, make_inputs, n, conc)
             rps = n / el
             ref = REF.get((args.mock_latency_ms, conc, n_workers)) if args.mode == "mock" else None
             print(json.dumps({
                 "bench": "serve_rpc", "mode": args.mode, "workers": n_workers, "concurrency": conc,
                 "topology": "client-LB->worker" if args.direct else "client->coordinator->worker",
+                "coordinator_procs": args.coord_procs or "in-process", "client_procs": args.client_procs,
                 "requests": n, "ok": ok, "req_per_s": round(rps, 1),
                 "p50_ms": round(1e3 * percentile(lat, 50), 2), "p99_ms": round(1e3 * percentile(lat, 99), 2),
                 "mock_latency_ms": args.mock_latency_ms if args.mode == "mock" else None,
@@ -181,7 +242,11 @@ async def main():
                 p.wait(10)
             except subprocess.TimeoutExpired:
                 p.kill()
-        await coord.stop()
+        if coord is not None:
+            await coord.stop()
+        if cproc is not None:
+            cproc.terminate()
+            cproc.wait(30)
 
 
 if __name__ == "__main__":

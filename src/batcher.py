@@ -168,6 +168,23 @@ class Batcher:
             self._spawn(key, batch, to_flush)
         return req.future
 
+    def try_direct(self, model_name: str, version: str) -> bool:
+        """Claim an idle key (nothing queued, nothing in flight) for ONE request dispatched by the caller
+        itself, without a batch task or future: the latency path of a lone request. While it is in
+        flight the key counts as busy, so concurrent requests still form batches behind it.
+        Pair with :meth:`release_direct`. No await inside: atomic on the event loop."""
+        key = f"{model_name}:{version}"
+        if not (self._running and self.eager_when_idle) or key in self._batches or self._inflight_by_key.get(key):
+            return False
+        self._inflight_by_key[key] = 1
+        self.total_requests += 1
+        self.total_batches += 1
+        return True
+
+    def release_direct(self, model_name: str, version: str) -> None:
+        key = f"{model_name}:{version}"
+        self._inflight_by_key[key] = self._inflight_by_key.get(key, 1) - 1
+
     def _detach(self, key: str, batch: Batch) -> List[BatchedRequest]:
         """Take the batch's requests and forget the batch. Caller holds the lock."""
         reqs = list(batch.requests)

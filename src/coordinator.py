@@ -30,7 +30,6 @@ import hashlib
 import json
 import logging
 import os
-import sys
 import time
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -73,8 +72,14 @@ class Coordinator:
         request_timeout_s: float = 600.0,
         health_check_interval: float = 5.0,
         dispatch: Optional[str] = None,
+        reuse_port: bool = False,
     ):
         self.host, self.port = host, port
+        # several coordinator processes may share one listening port (SO_REUSEPORT: the kernel spreads
+        # connections over them); they forward worker (un)registrations to each other (peer_addrs)
+        self.reuse_port = reuse_port
+        self.peer_addrs: List[str] = []
+        self.peer_server: Optional[asyncio.AbstractServer] = None
         self.strategy = LoadBalancerStrategy(strategy)
         self.max_retries = max_retries
         self.request_timeout_s = request_timeout_s
@@ -113,12 +118,28 @@ class Coordinator:
             await lb.start()
         # backlog: a burst of >100 new client connections must not hit SYN retransmits (1 s stalls)
         self.server = await asyncio.start_server(self._handle_connection, self.host, self.port, limit=1 << 26,
-                                                 backlog=4096)
+                                                 backlog=4096, reuse_port=self.reuse_port or None)
         self.port = self.server.sockets[0].getsockname()[1]
         logger.info("Coordinator listening on %s:%d", self.host, self.port)
         return self.port
 
+    async def start_peer_server(self) -> str:
+        """A private listener on which sibling coordinator processes reach THIS process (forwarded
+        registrations); returns its address."""
+        self.peer_server = await asyncio.start_server(self._handle_connection, self.host, 0, limit=1 << 26)
+        return f"{self.host}:{self.peer_server.sockets[0].getsockname()[1]}"
+
+    async def _forward(self, msg: Dict[str, Any]) -> None:
+        fwd = dict(msg, _fwd=True)
+        for a in self.peer_addrs:
+            try:
+                await self.rpc.call(a, fwd, timeout=10.0)
+            except Exception as e:  # a sibling that is down re-learns membership from health checks
+                logger.warning("forwarding %s to sibling %s failed: %s", msg.get("op"), a, e)
+
     async def stop(self) -> None:
+        if self.peer_server:
+            self.peer_server.close()
         if self.server:
             self.server.close()
             with contextlib.suppress(Exception):
@@ -244,9 +265,13 @@ class Coordinator:
             return {"error": f"unknown request_id {rid!r}", "success": False}
         if op == "register":
             self.register_worker(msg["worker_id"], msg["address"], msg.get("models", {}), msg.get("metadata"))
+            if self.peer_addrs and not msg.get("_fwd"):
+                await self._forward(msg)
             return {"success": True}
         if op == "unregister":
             self.unregister_worker(msg["worker_id"])
+            if self.peer_addrs and not msg.get("_fwd"):
+                await self._forward(msg)
             return {"success": True}
         if op == "health":
             return {"success": True, "role": "coordinator", "workers": len(self.router.workers)}
@@ -309,10 +334,20 @@ class Coordinator:
             self.stats["errors"] += 1
             return {"error": f"no healthy shard for {model}:{version}", "success": False}
         tr.mark(rid, "coord.routed")
+        vkey = f"{version}#{shard.shard_id}"
         try:
-            fut = await self.batcher.add_request(model, f"{version}#{shard.shard_id}",
-                                                 {"inputs": inputs, "request_id": rid, "key": key})
-            resp = await asyncio.wait_for(fut, self.request_timeout_s)
+            if self.batcher.try_direct(model, vkey):
+                # an idle shard: dispatch this request itself, no batch task / future in between (the lone
+                # request's latency path); requests arriving meanwhile still batch behind it
+                try:
+                    tr.mark(rid, "coord.dispatch")
+                    resp = await self._send(model, version, shard.shard_id, key,
+                                            {"op": "infer", "model": model, "inputs": inputs, "request_id": rid})
+                finally:
+                    self.batcher.release_direct(model, vkey)
+            else:
+                fut = await self.batcher.add_request(model, vkey, {"inputs": inputs, "request_id": rid, "key": key})
+                resp = await asyncio.wait_for(fut, self.request_timeout_s)
         except Exception as e:
             self.stats["errors"] += 1
             return {"error": str(e) or type(e).__name__, "success": False, "request_id": rid}
@@ -466,12 +501,13 @@ def build_arg_parser():
     p.add_argument("--max-latency-ms", type=float, default=None)
     p.add_argument("--dispatch", default=None, choices=["batch", "stream"])
     p.add_argument("--port-file", default=None)
+    p.add_argument("--procs", type=int, default=1,
+                   help="coordinator processes sharing the listening port (SO_REUSEPORT); registrations are "
+                        "forwarded between them")
     return p
 
 
-async def main(argv=None) -> None:
-    setup_logging()
-    args = build_arg_parser().parse_args(argv)
+def _configure(args) -> DeploymentConfig:
     cfg = DeploymentConfig.from_yaml(args.config) if args.config else DeploymentConfig()
     cfg.listen_host = args.listen_host or cfg.listen_host
     cfg.listen_port = args.listen_port if args.listen_port is not None else cfg.listen_port
@@ -481,6 +517,84 @@ async def main(argv=None) -> None:
         cfg.batch_max_size = args.max_batch_size
     if args.max_latency_ms:
         cfg.batch_max_latency_ms = args.max_latency_ms
+    return cfg
+
+
+def _child_main(ns: Dict[str, Any], conn) -> None:
+    """One of --procs coordinator processes: serve the shared port, report the private peer address,
+    learn the siblings' addresses, add the static workers, then serve until terminated."""
+    import argparse
+
+    async def run():
+        setup_logging()
+        args = argparse.Namespace(**ns)
+        cfg = _configure(args)
+        coord = Coordinator.from_config(cfg)
+        coord.reuse_port = True
+        coord.dispatch_override = args.dispatch
+        await coord.start()
+        conn.send(await coord.start_peer_server())
+        loop = asyncio.get_running_loop()
+        coord.peer_addrs = await loop.run_in_executor(None, conn.recv)
+        addrs = list(args.worker) + [w.address for w in cfg.workers]
+        await asyncio.gather(*(coord.add_static_worker(a) for a in addrs))
+        conn.send("ready")
+        try:
+            await asyncio.Event().wait()
+        finally:
+            await coord.stop()
+
+    with contextlib.suppress(KeyboardInterrupt):
+        asyncio.run(run())
+
+
+def run_multi(args) -> None:
+    """Parent of --procs N coordinator processes on one port."""
+    import multiprocessing as mp
+    import signal
+    import socket
+
+    port = args.listen_port
+    if not port:  # pick a free port for all of them
+        s = socket.socket()
+        s.bind((args.listen_host, 0))
+        port = s.getsockname()[1]
+        s.close()
+    ns = dict(vars(args), listen_port=port)
+    ctx = mp.get_context("spawn")
+    pipes, procs = [], []
+    for _ in range(args.procs):
+        a, b = ctx.Pipe()
+        p = ctx.Process(target=_child_main, args=(ns, b), daemon=True)
+        p.start()
+        pipes.append(a)
+        procs.append(p)
+    peers = [a.recv() for a in pipes]
+    for i, a in enumerate(pipes):
+        a.send([x for j, x in enumerate(peers) if j != i])
+    for a in pipes:
+        assert a.recv() == "ready"
+    if args.port_file:
+        with open(args.port_file + ".tmp", "w") as f:
+            f.write(str(port))
+        os.replace(args.port_file + ".tmp", args.port_file)
+    print(f"Coordinator x{args.procs} listening on {args.listen_host}:{port}", flush=True)
+
+    def stop(*_):
+        for p in procs:
+            p.terminate()
+    signal.signal(signal.SIGTERM, stop)
+    try:
+        for p in procs:
+            p.join()
+    except KeyboardInterrupt:
+        stop()
+
+
+async def main(argv=None) -> None:
+    setup_logging()
+    args = build_arg_parser().parse_args(argv)
+    cfg = _configure(args)
     coord = Coordinator.from_config(cfg)
     coord.dispatch_override = args.dispatch
     port = await coord.start()
@@ -498,5 +612,9 @@ async def main(argv=None) -> None:
 
 
 if __name__ == "__main__":
-    with contextlib.suppress(KeyboardInterrupt):
-        asyncio.run(main())
+    _args = build_arg_parser().parse_args()
+    if _args.procs > 1:
+        run_multi(_args)
+    else:
+        with contextlib.suppress(KeyboardInterrupt):
+            asyncio.run(main())

@@ -156,3 +156,53 @@ def test_coordinator_two_workers_end_to_end():
                 p.wait()
             await coord.stop()
     asyncio.run(main())
+
+
+def test_multi_process_coordinator_shares_port_and_forwards_registration(tmp_path):
+    """--procs 3: three coordinator processes on one SO_REUSEPORT port; a worker registers with
+    whichever accepts its connection and the registration is forwarded to the siblings, so requests
+    on any connection (spread by the kernel) are served."""
+    import os
+    import subprocess
+    import sys
+    import time
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pf = str(tmp_path / "coord.port")
+    coord = subprocess.Popen([sys.executable, "-m", "src.coordinator", "--listen-port", "0", "--procs", "3",
+                              "--port-file", pf], cwd=root, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    worker = None
+    try:
+        t0 = time.time()
+        while not os.path.exists(pf):
+            assert coord.poll() is None and time.time() - t0 < 60, "coordinators did not start"
+            time.sleep(0.1)
+        cport = int(open(pf).read())
+        wpf = str(tmp_path / "w.port")
+        worker = subprocess.Popen([sys.executable, "-m", "src.worker", "--worker-id", "w-mp", "--host", "127.0.0.1",
+                                   "--port", "0", "--port-file", wpf, "--model", "echo", "--arch", "mock",
+                                   "--mock-latency-ms", "0", "--coordinator", f"127.0.0.1:{cport}"],
+                                  cwd=root, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        while not os.path.exists(wpf):
+            assert worker.poll() is None and time.time() - t0 < 90, "worker did not start"
+            time.sleep(0.1)
+
+        async def main():
+            ok = 0
+            for i in range(24):  # fresh connections: the kernel spreads them over the 3 processes
+                c = InferenceClient(f"127.0.0.1:{cport}")
+                for _ in range(50):
+                    r = await c.call({"model": "echo", "inputs": {"x": i}, "cache": False})
+                    if r.get("success"):
+                        break
+                    await asyncio.sleep(0.05)  # registration still propagating
+                ok += bool(r.get("success"))
+                c.close()
+            return ok
+
+        assert asyncio.run(main()) == 24
+    finally:
+        for p in (worker, coord):
+            if p is not None:
+                p.terminate()
+                p.wait(30)
