@@ -17,7 +17,11 @@
 //  * K rows in LDS use a 272-byte pitch so the 16-lane ds_read_b128 groups hit
 //    16 distinct 16-byte slots (T2's goal via padding; register staging).
 //  * Online softmax in base 2 with a finite running-max sentinel so fully
-//    masked tiles never produce NaN.
+//    masked tiles never produce NaN; the running max only moves (and O is only
+//    rescaled) when a tile's max exceeds it by > 8 in log2 units (lazy rescale:
+//    +17-19 % prefill throughput, profiles/micro_attn_prefill_r2.jsonl), the
+//    scale is folded into the exponent's fma, and tiles inside every row's causal
+//    window skip the key mask.
 //  * Prefill: 4 waves share double-buffered K/V tiles (one barrier per tile,
 //    the next tile's global loads in flight during compute: T14).
 //    Decode: each wave streams its own 64 keys (K straight to VGPRs, V through
@@ -157,6 +161,82 @@ __device__ __forceinline__ void pv_lds(const char* vlds, const f32x16_t& p, Stat
   }
 }
 
+// Online softmax with a lazy rescale (decode and prefill): the running max is only moved (and O, l
+// rescaled) when a tile's max exceeds it by more than 8 in log2 units, so P <= 2^8 stays
+// exact in fp32/bf16 and the 64-accumulator rescale (AGPR read-multiply-write) runs a few
+// times per sequence instead of every 32 keys. v_exp_f32 directly (exp2(-inf) = 0).
+__device__ __forceinline__ void softmax_tile_lazy(f32x16_t& s, State& st, int kbase, int kv_len, float scale_log2,
+                                                  int h) {
+  float mx = -INFINITY;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int key = kbase + (r & 3) + 8 * (r >> 2) + 4 * h;
+    const float v = key < kv_len ? s[r] * scale_log2 : -INFINITY;
+    s[r] = v;
+    mx = fmaxf(mx, v);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  const bool need = mx > st.m + 8.f;
+  if (__any(need)) {
+    const float m_use = need ? mx : st.m;
+    const float alpha = __builtin_amdgcn_exp2f(st.m - m_use);
+    st.l *= alpha;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st.o[db][r] *= alpha;
+    st.m = m_use;
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float p = __builtin_amdgcn_exp2f(s[r] - st.m);
+    s[r] = p;
+    sum += p;
+  }
+  sum += __shfl_xor(sum, 32, 64);
+  st.l += sum;
+}
+
+// Prefill variant of the lazy softmax: the running max is kept on RAW scores (the scale is folded into
+// the exponent's fma: p = exp2(s * scale - m * scale)), and tiles that lie entirely inside every row's
+// causal window (MASK = false, decided per wave) skip the per-element key test.
+template <bool MASK>
+__device__ __forceinline__ void softmax_tile_prefill(f32x16_t& s, State& st, int kbase, int kv_len, float scale_log2,
+                                                     int h) {
+  float mx = -INFINITY;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    if constexpr (MASK) {
+      const int key = kbase + (r & 3) + 8 * (r >> 2) + 4 * h;
+      s[r] = key < kv_len ? s[r] : -INFINITY;
+    }
+    mx = fmaxf(mx, s[r]);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
+  const bool need = mx > st.m + 8.f;
+  if (__any(need)) {
+    const float m_use = need ? mx : st.m;
+    const float alpha = __builtin_amdgcn_exp2f(st.m - m_use);
+    st.l *= alpha;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st.o[db][r] *= alpha;
+    st.m = m_use;
+  }
+  const float nm = -st.m;
+  float sum = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r], scale_log2, nm));
+    s[r] = p;
+    sum += p;
+  }
+  sum += __shfl_xor(sum, 32, 64);
+  st.l += sum;
+}
+
 __device__ __forceinline__ const bf16_t* kv_row(const bf16_t* cache, const int* bt, int key, int block_size,
                                                 int hkv, int kvh) {
   const int64_t blk = bt[key / block_size];
@@ -200,6 +280,9 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(bf16_t* __restrict
   const int ntiles = (kv_end + ST - 1) / ST;
   const int wave_last_tok = min(t0 + wave * TPW + TPW, qlen) - 1;
   const int wave_kv_end = pos0 + wave_last_tok + 1;
+  // the wave's first row sees keys [0, pos0 + first token + 1); tiles below that need no causal mask
+  // (padded rows past qlen clamp to the last token, so they see at least as much)
+  const int wave_kv_min = min(ctx, pos0 + min(t0 + wave * TPW, qlen - 1) + 1);
   const int* bt = block_tables + (int64_t)seq * bt_stride;
 
   bf16x8_t qf[8];
@@ -250,7 +333,10 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(bf16_t* __restrict
       if (kb0 < wave_kv_end) {  // wave-uniform: sub-tile not entirely in this wave's causal future
         const char* kl = smem + (cur * NS + j) * KV_TILE;
         f32x16_t s = qk_lds(kl, qf, lane);
-        softmax_tile(s, st, kb0, kv_len_row, scale_log2, h);
+        if (kb0 + KT <= wave_kv_min)  // every key of the tile is visible to every row of the wave
+          softmax_tile_prefill<false>(s, st, kb0, kv_len_row, scale_log2, h);
+        else
+          softmax_tile_prefill<true>(s, st, kb0, kv_len_row, scale_log2, h);
         pv_lds(kl + K_TILE, s, st, lane);
       }
     }
@@ -546,43 +632,6 @@ __device__ __forceinline__ void pv_lds_swz_v3(const char* vimg, const f32x16_t& 
       st.o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a8), pf[s2], st.o[db], 0,
                                                          0, 0);
     }
-}
-
-// Online softmax for decode with a lazy rescale: the running max is only moved (and O, l
-// rescaled) when a tile's max exceeds it by more than 8 in log2 units, so P <= 2^8 stays
-// exact in fp32/bf16 and the 64-accumulator rescale (AGPR read-multiply-write) runs a few
-// times per sequence instead of every 32 keys. v_exp_f32 directly (exp2(-inf) = 0).
-__device__ __forceinline__ void softmax_tile_lazy(f32x16_t& s, State& st, int kbase, int kv_len, float scale_log2,
-                                                  int h) {
-  float mx = -INFINITY;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int key = kbase + (r & 3) + 8 * (r >> 2) + 4 * h;
-    const float v = key < kv_len ? s[r] * scale_log2 : -INFINITY;
-    s[r] = v;
-    mx = fmaxf(mx, v);
-  }
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  const bool need = mx > st.m + 8.f;
-  if (__any(need)) {
-    const float m_use = need ? mx : st.m;
-    const float alpha = __builtin_amdgcn_exp2f(st.m - m_use);
-    st.l *= alpha;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) st.o[db][r] *= alpha;
-    st.m = m_use;
-  }
-  float sum = 0.f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float p = __builtin_amdgcn_exp2f(s[r] - st.m);
-    s[r] = p;
-    sum += p;
-  }
-  sum += __shfl_xor(sum, 32, 64);
-  st.l += sum;
 }
 
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
@@ -956,19 +1005,11 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
   const float sl2 = scale * 1.4426950408889634f;
   const int tpb = 4 * (32 / (G > 32 ? 32 : G));
   dim3 grid((max_q_len + tpb - 1) / tpb, num_seqs, hkv), block(256);
-  static const int ns = [] {
-    const char* e = std::getenv("DIE_PF_NS");  // A/B knob: 32-key sub-tiles per stage (1 or 2)
-    return e != nullptr && std::atoi(e) == 1 ? 1 : 2;
-  }();
-  const size_t lds = 2 * ns * KV_TILE;
+  const size_t lds = 2 * 2 * KV_TILE;
 #define DIE_PF(GG)                                                                                             \
   case GG:                                                                                                     \
-    if (ns == 2)                                                                                               \
-      hipLaunchKernelGGL((attn_prefill_kernel<GG, 2>), grid, block, lds, s, out, q, q_stride, k_cache, v_cache, \
-                         block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2);                   \
-    else                                                                                                       \
-      hipLaunchKernelGGL((attn_prefill_kernel<GG, 1>), grid, block, lds, s, out, q, q_stride, k_cache, v_cache, \
-                         block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2);                   \
+    hipLaunchKernelGGL((attn_prefill_kernel<GG, 2>), grid, block, lds, s, out, q, q_stride, k_cache, v_cache,   \
+                       block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2);                     \
     break;
   switch (G) {
     DIE_PF(1)
