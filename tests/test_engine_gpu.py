@@ -288,6 +288,8 @@ def test_mixed_steps_on_gpu(engine):
     sp = SamplingParams(max_tokens=16)
     got = {}
     m0 = engine.scheduler.steps_mixed
+    mode0 = engine.cfg.mixed_batching
+    engine.cfg.mixed_batching = "always"  # long prompts too ride along in mixed_step_tokens-row chunks
     for i in range(2):
         engine.add_request(f"mx{i}", ps[i], sp, on_finish=lambda s, i=i: got.__setitem__(i, list(s.output_ids)))
     engine.step()
@@ -297,6 +299,7 @@ def test_mixed_steps_on_gpu(engine):
             engine.add_request(f"mx{k}", ps[k], sp, on_finish=lambda s, k=k: got.__setitem__(k, list(s.output_ids)))
             k += 1
         engine.step()
+    engine.cfg.mixed_batching = mode0
     assert engine.scheduler.steps_mixed > m0
     for i, p in enumerate(ps):
         r, m = reference_with_margins(engine.model, p, 16)
