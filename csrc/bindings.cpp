@@ -169,10 +169,10 @@ void attn_decode(Tensor out, Tensor part_o, Tensor part_ml, Tensor counters, Ten
 // Decode attention with the fused prologue: q / new K,V built from the qkv projection's
 // fp32 split-K slabs [sk, M, (hq+2hkv)*128] (RMSNorm row scale from ssp [T, 32], RoPE from
 // cos_sin [max_pos, 128] at positions [M]); the new K/V go to the paged cache at slot_mapping.
-static die::AttnDecodeFuse attn_fuse_args(Tensor out, Tensor part_o, Tensor part_ml, Tensor counters, Tensor slab,
-                                           Tensor ssp, Tensor positions, Tensor cos_sin, Tensor slot_mapping,
-                                           Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor ctx_lens,
-                                           int64_t max_ctx, int64_t hq, int64_t hkv, double eps, int64_t hidden) {
+void attn_decode_fused(Tensor out, Tensor part_o, Tensor part_ml, Tensor counters, Tensor slab, Tensor ssp,
+                       Tensor positions, Tensor cos_sin, Tensor slot_mapping, Tensor k_cache, Tensor v_cache,
+                       Tensor block_tables, Tensor ctx_lens, int64_t max_ctx, int64_t hq, int64_t hkv, double scale,
+                       double eps, int64_t hidden) {
   DIE_CHECK_CUDA(slab);
   DIE_CHECK_DTYPE(slab, at::kFloat);
   DIE_CHECK_CONTIG(slab);
@@ -222,73 +222,11 @@ static die::AttnDecodeFuse attn_fuse_args(Tensor out, Tensor part_o, Tensor part
   fz.eps = (float)eps;
   fz.cos_sin = cos_sin.data_ptr<float>();
   fz.slot_mapping = slot_mapping.data_ptr<int64_t>();
-  return fz;
-}
-
-void attn_decode_fused(Tensor out, Tensor part_o, Tensor part_ml, Tensor counters, Tensor slab, Tensor ssp,
-                       Tensor positions, Tensor cos_sin, Tensor slot_mapping, Tensor k_cache, Tensor v_cache,
-                       Tensor block_tables, Tensor ctx_lens, int64_t max_ctx, int64_t hq, int64_t hkv, double scale,
-                       double eps, int64_t hidden) {
-  const die::AttnDecodeFuse fz = attn_fuse_args(out, part_o, part_ml, counters, slab, ssp, positions, cos_sin,
-                                                slot_mapping, k_cache, v_cache, block_tables, ctx_lens, max_ctx, hq,
-                                                hkv, eps, hidden);
-  const int64_t D = 128, nseq = ctx_lens.numel();
   DIE_HIP(die::launch_attn_decode(bf(out), part_o.data_ptr<float>(), part_ml.data_ptr<float>(),
                                   counters.data_ptr<int>(), nullptr, 0, bf(k_cache), bf(v_cache),
                                   block_tables.data_ptr<int>(), (int)block_tables.size(1), ctx_lens.data_ptr<int>(),
                                   (int)nseq, (int)max_ctx, (int)hq, (int)hkv, (int)D, 16, (float)scale, &fz,
                                   cur_stream()));
-}
-
-// attn_decode_fused + the o-proj with the residual update (gemm_decode mode 3, tile (64, 256), split-K 4,
-// tile-order packed wo) in ONE launch: resid += out @ wo^T, ssp_out [N/64, 128] = row sums of squares of
-// the new residual per column tile. oslab [4, M, N] fp32 scratch, ocnt [N/64] and sync [hkv + 2] int32
-// zeroed once (re-armed by the kernel; sync[hkv + 1] != 0 flags a timed-out wait).
-void attn_oproj_decode_fused(Tensor out, Tensor part_o, Tensor part_ml, Tensor counters, Tensor slab, Tensor ssp,
-                             Tensor positions, Tensor cos_sin, Tensor slot_mapping, Tensor k_cache, Tensor v_cache,
-                             Tensor block_tables, Tensor ctx_lens, int64_t max_ctx, int64_t hq, int64_t hkv,
-                             double scale, double eps, int64_t hidden, Tensor wo, Tensor oslab, Tensor resid,
-                             Tensor ssp_out, Tensor ocnt, Tensor sync) {
-  const die::AttnDecodeFuse fz = attn_fuse_args(out, part_o, part_ml, counters, slab, ssp, positions, cos_sin,
-                                                slot_mapping, k_cache, v_cache, block_tables, ctx_lens, max_ctx, hq,
-                                                hkv, eps, hidden);
-  const int64_t D = 128, nseq = ctx_lens.numel(), K = hq * D;
-  TORCH_CHECK(nseq >= 1 && nseq <= 32, "attention + o-proj: 1..32 rows");
-  TORCH_CHECK(out.dim() == 2 && out.size(1) == K && out.stride(0) == K, "out [M, hq*128] contiguous");
-  DIE_CHECK_BF16(wo);
-  DIE_CHECK_CONTIG(wo);
-  TORCH_CHECK(wo.dim() == 2 && wo.size(1) == K && wo.size(0) % 64 == 0, "wo [N, hq*128] (tile-order packed, wr 64)");
-  const int64_t N = wo.size(0);
-  DIE_CHECK_DTYPE(oslab, at::kFloat);
-  DIE_CHECK_CONTIG(oslab);
-  TORCH_CHECK(oslab.numel() >= 4 * nseq * N, "oslab [4, M, N]");
-  DIE_CHECK_BF16(resid);
-  check_rows(resid, "resid");
-  TORCH_CHECK(resid.size(0) >= nseq && resid.size(1) == N, "resid [M, N]");
-  DIE_CHECK_DTYPE(ssp_out, at::kFloat);
-  DIE_CHECK_CONTIG(ssp_out);
-  TORCH_CHECK(ssp_out.numel() >= (N / 64) * die::DECODE_SSP_LD, "ssp_out [N/64, 128]");
-  DIE_CHECK_DTYPE(ocnt, at::kInt);
-  TORCH_CHECK(ocnt.is_cuda() && ocnt.numel() >= N / 64, "ocnt [N/64] int32");
-  DIE_CHECK_DTYPE(sync, at::kInt);
-  TORCH_CHECK(sync.is_cuda() && sync.numel() >= hkv + 2, "sync [hkv + 2] int32");
-  die::AttnOprojFuse of;
-  of.w = bf(wo);
-  of.n = (int)N;
-  of.k = (int)K;
-  of.sk = 4;
-  of.slab = oslab.data_ptr<float>();
-  of.sync = sync.data_ptr<int>();
-  of.g.resid = bf(resid);
-  of.g.ld_resid = resid.stride(0);
-  of.g.ssp_out = ssp_out.data_ptr<float>();
-  of.g.counters = ocnt.data_ptr<int>();
-  of.g.tiled = 1;
-  DIE_HIP(die::launch_attn_oproj_decode(bf(out), part_o.data_ptr<float>(), part_ml.data_ptr<float>(),
-                                        counters.data_ptr<int>(), bf(k_cache), bf(v_cache),
-                                        block_tables.data_ptr<int>(), (int)block_tables.size(1),
-                                        ctx_lens.data_ptr<int>(), (int)nseq, (int)max_ctx, (int)hq, (int)hkv,
-                                        (float)scale, fz, of, cur_stream()));
 }
 
 int64_t decode_partials(int64_t max_ctx) { return die::attn_decode_max_partials((int)max_ctx); }
@@ -821,7 +759,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_prefill", &attn_prefill);
   m.def("attn_decode", &attn_decode);
   m.def("attn_decode_fused", &attn_decode_fused);
-  m.def("attn_oproj_decode_fused", &attn_oproj_decode_fused);
   m.def("decode_partials", &decode_partials);
   m.def("sample", &sample, py::arg("out"), py::arg("logits"), py::arg("temperature") = py::none(),
         py::arg("top_k") = py::none(), py::arg("top_p") = py::none(), py::arg("seeds") = py::none(),

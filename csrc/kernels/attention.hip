@@ -31,7 +31,6 @@
 #include <cstdlib>
 
 #include "common.h"
-#include "gemm_decode.h"
 #include "launchers.h"
 
 namespace die {
@@ -113,7 +112,7 @@ __device__ __forceinline__ void softmax_tile(f32x16_t& s, State& st, int kbase, 
     s[r] = v;
     mx = fmaxf(mx, v);
   }
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  mx = xor32_max(mx);
   const float m_new = fmaxf(st.m, mx);
   const float alpha = exp2f(st.m - m_new);
   float sum = 0.f;
@@ -123,7 +122,7 @@ __device__ __forceinline__ void softmax_tile(f32x16_t& s, State& st, int kbase, 
     s[r] = p;
     sum += p;
   }
-  sum += __shfl_xor(sum, 32, 64);
+  sum = xor32_sum(sum);
   st.l = st.l * alpha + sum;
   st.m = m_new;
 #pragma unroll
@@ -176,7 +175,7 @@ __device__ __forceinline__ void softmax_tile_lazy(f32x16_t& s, State& st, int kb
     s[r] = v;
     mx = fmaxf(mx, v);
   }
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  mx = xor32_max(mx);
   const bool need = mx > st.m + 8.f;
   if (__any(need)) {
     const float m_use = need ? mx : st.m;
@@ -195,7 +194,7 @@ __device__ __forceinline__ void softmax_tile_lazy(f32x16_t& s, State& st, int kb
     s[r] = p;
     sum += p;
   }
-  sum += __shfl_xor(sum, 32, 64);
+  sum = xor32_sum(sum);
   st.l += sum;
 }
 
@@ -214,7 +213,7 @@ __device__ __forceinline__ void softmax_tile_prefill(f32x16_t& s, State& st, int
     }
     mx = fmaxf(mx, s[r]);
   }
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
+  mx = xor32_max(mx) * scale_log2;
   const bool need = mx > st.m + 8.f;
   if (__any(need)) {
     const float m_use = need ? mx : st.m;
@@ -234,7 +233,7 @@ __device__ __forceinline__ void softmax_tile_prefill(f32x16_t& s, State& st, int
     s[r] = p;
     sum += p;
   }
-  sum += __shfl_xor(sum, 32, 64);
+  sum = xor32_sum(sum);
   st.l += sum;
 }
 
@@ -661,19 +660,6 @@ __device__ __forceinline__ void lds_st16(uint32_t a, uint32_t v) {
   asm volatile("ds_write_b16 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
 
-// bf16 output quad (4 elements at element offset off): OSIG = write-through (sc1), read by other
-// workgroups of the same launch
-template <bool OSIG>
-__device__ __forceinline__ void store_out(bf16_t* out, int64_t off, uint2 pk) {
-  if constexpr (OSIG) {
-    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0x7fffffff, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, pk), r,
-                                          (int)(off * 2), 0, 16);
-  } else {
-    *reinterpret_cast<uint2*>(out + off) = pk;
-  }
-}
-
 __device__ __forceinline__ void glds4(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((global_cvoid*)src, (lds_void*)lds_wave_base, 4, 0, 0);
 }
@@ -685,19 +671,14 @@ __device__ __forceinline__ void glds4(const void* src, char* lds_wave_base) {
 // row straight into this step's LDS image. The separate RoPE/KV-write and RMSNorm kernels of
 // the decode layer disappear. Everything the prologue needs arrives by LDS-DMA, staged in the
 // merge area (idle at a task start), so no ordinary load stalls the chunk stream.
-//
-// OSIG (attention + o-proj launch, attn_oproj_v3_kernel): the bf16 output rows are written through to
-// memory (sc1 stores) and every (sequence, kv head) whose final output this workgroup wrote is counted in
-// odone[kv head] (one relaxed agent-scope add after the stores completed), which the o-proj tiles of
-// the same launch wait on.
-template <int G, bool FUSED, bool OSIG>
-__device__ __forceinline__ void attn_v3_body(
-    char* smem, bf16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml,
-    int* __restrict__ counters, const bf16_t* __restrict__ q, int64_t q_stride, bf16_t* __restrict__ k_cache,
-    bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
-    const int* __restrict__ ctx_lens, int num_seqs, int hq, int hkv, float scale_log2, int maxp, int dbg,
-    const AttnDecodeFuse& fz, const int64_t* __restrict__ slot_mapping, int* __restrict__ odone) {
+template <int G, bool FUSED>
+__global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
+    bf16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters,
+    const bf16_t* __restrict__ q, int64_t q_stride, bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, int num_seqs, int hq,
+    int hkv, float scale_log2, int maxp, int dbg, AttnDecodeFuse fz, const int64_t* __restrict__ slot_mapping) {
   constexpr int QI = (G * 256 + 1023) / 1024;  // LDS-DMA instructions for the query rows
+  extern __shared__ __attribute__((aligned(16))) char smem[];
   float* ml = reinterpret_cast<float*>(smem + 2 * V3_BUF);
   float* ob = reinterpret_cast<float*>(smem + 2 * V3_BUF + V3_ML);
   int* ctl = reinterpret_cast<int*>(smem + 2 * V3_BUF + V3_MERGE);
@@ -719,12 +700,7 @@ __device__ __forceinline__ void attn_v3_body(
     const int ctx = __builtin_amdgcn_readfirstlane(ctx_lens[seq]);
     const int nch = (ctx + DEC_KEYS - 1) / DEC_KEYS;
     const int c0 = part * C;
-    if (c0 >= nch) {  // uniform
-      // an empty context (never a real decode row): count it as done, its output row is not read
-      if (OSIG && part == 0 && nch == 0 && tid == 0)
-        __hip_atomic_fetch_add(odone + kvh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      continue;
-    }
+    if (c0 >= nch) continue;  // uniform
     const int c1 = min(c0 + C, nch);
     const int* bt = block_tables + (int64_t)seq * bt_stride;
     const int last_blk = (ctx - 1) >> 4;
@@ -932,7 +908,7 @@ __device__ __forceinline__ void attn_v3_body(
         uint2 pk;
         pk.x = pack2(acc.x * inv, acc.y * inv);
         pk.y = pack2(acc.z * inv, acc.w * inv);
-        store_out<OSIG>(out, ((int64_t)seq * hq + head) * D + d, pk);
+        *reinterpret_cast<uint2*>(out + ((int64_t)seq * hq + head) * D + d) = pk;
       } else {
         const int64_t slot = ((int64_t)seq * hq + head) * maxp + part;
         __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(part_o, 0, 0x7fffffff, 0x00020000);
@@ -981,16 +957,9 @@ __device__ __forceinline__ void attn_v3_body(
           uint2 pk;
           pk.x = pack2(acc.x * inv, acc.y * inv);
           pk.y = pack2(acc.z * inv, acc.w * inv);
-          store_out<OSIG>(out, ((int64_t)seq * hq + head) * D + d, pk);
+          *reinterpret_cast<uint2*>(out + ((int64_t)seq * hq + head) * D + d) = pk;
         }
         if (tid == 0) __hip_atomic_store(counters + pair, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    if constexpr (OSIG) {
-      if (nparts == 1 || ctl[1]) {  // this workgroup wrote the pair's output (uniform)
-        wait_vm<0>();               // every wave's write-through stores are done
-        lds_barrier();
-        if (tid == 0) __hip_atomic_fetch_add(odone + kvh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     lds_barrier();  // merge area and buffers are reused by the next task
@@ -1005,126 +974,6 @@ __device__ __forceinline__ void attn_v3_body(
   }
 }
 
-template <int G, bool FUSED>
-__global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
-    bf16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters,
-    const bf16_t* __restrict__ q, int64_t q_stride, bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
-    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, int num_seqs, int hq,
-    int hkv, float scale_log2, int maxp, int dbg, AttnDecodeFuse fz, const int64_t* __restrict__ slot_mapping) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  attn_v3_body<G, FUSED, false>(smem, out, part_o, part_ml, counters, q, q_stride, k_cache, v_cache, block_tables,
-                                bt_stride, ctx_lens, num_seqs, hq, hkv, scale_log2, maxp, dbg, fz, slot_mapping,
-                                nullptr);
-}
-
-// ---------------------------------------------------------------------------
-// Attention + o-proj in one persistent launch (decode, TP = 1, dense). The o-proj is the mode-3
-// decode GEMM (split-K slabs, last arriver adds into the residual and writes the next norm's row
-// statistics); each of its tiles reads K slice `by` of the attention output = the q heads of a few kv
-// heads. Grid = one workgroup per CU: each workgroup first runs its attention tasks (attn_v3_body,
-// output written through and counted per kv head), then its o-proj tiles (gd_body with an X-wait:
-// the tile's first weight chunks stream in while it polls the counts of the kv heads it reads, then
-// its activation pieces follow as sc1 loads). What this removes: the o-proj launch and its ramp, and
-// the idle weight stream while attention's tail runs. Hand-off (MI355X_MICROARCH.md, inter-workgroup
-// visibility table, first row): sc1 stores -> every wave's vmcnt(0) -> barrier -> one lane's
-// agent-scope add; consumer: one lane's sc1 poll, the other waves load after a barrier it joins.
-// The poll is bounded (error flag sync[hkv + 1]); every workgroup is resident (LDS: one per CU), and no
-// workgroup waits on a task of a workgroup that is itself waiting (attention tasks come first).
-struct OprojWait {
-  static constexpr bool active = true;
-  int* sync;
-  int kv0, kv1, target, err;
-  __device__ void operator()() const {
-    if (threadIdx.x == 0) {
-      for (int kv = kv0; kv < kv1; ++kv) {
-        int n = 0;
-        while (__hip_atomic_load(sync + kv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-          __builtin_amdgcn_s_sleep(2);
-          if (++n == (1 << 22)) {
-            __hip_atomic_store(sync + err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-        }
-      }
-    }
-    __builtin_amdgcn_s_barrier();  // raw: the weight pieces stay in flight
-  }
-};
-
-constexpr int OP_WR = 64, OP_KC = 256, OP_SK = 4;  // the o-proj tile (8B: 64 column tiles x 4 = 256)
-
-template <int G, int XR>
-__global__ void __launch_bounds__(256, 1) attn_oproj_v3_kernel(
-    bf16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters,
-    bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
-    const int* __restrict__ ctx_lens, int num_seqs, int hq, int hkv, float scale_log2, int maxp, AttnDecodeFuse fz,
-    AttnOprojFuse of) {
-  constexpr int S = gd::ring_slots(OP_WR, XR, OP_KC);
-  static_assert((size_t)S * (OP_WR + XR) * OP_KC * 2 <= (size_t)V3_LDS, "o-proj ring fits the attention LDS");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  attn_v3_body<G, true, true>(smem, out, part_o, part_ml, counters, nullptr, 0, k_cache, v_cache, block_tables,
-                              bt_stride, ctx_lens, num_seqs, hq, hkv, scale_log2, maxp, 0, fz, fz.slot_mapping,
-                              of.sync);
-  __syncthreads();
-  const int ncol = of.n / OP_WR, ntile = ncol * OP_SK, kper = of.k / OP_SK, hk = G * D;
-#pragma unroll 1
-  for (int t = blockIdx.x; t < ntile; t += gridDim.x) {
-    const int by = t / ncol, bx = t - by * ncol;
-    const OprojWait w{of.sync, by * kper / hk, (by * kper + kper + hk - 1) / hk, num_seqs, hkv + 1};
-    gd::gd_body<OP_WR, 3, S, true, OP_KC, XR, OP_SK, OprojWait>(smem, of.slab, of.n, out, (int64_t)hq * D, of.w,
-                                                                 num_seqs, of.n, of.k, of.g, bx, by, OP_SK, w);
-    __syncthreads();  // the ring is refilled by the next tile
-  }
-  if (threadIdx.x == 0 &&
-      __hip_atomic_fetch_add(of.sync + hkv, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
-    // last workgroup out: every poll is over, re-arm the counts for the next launch
-    for (int kv = 0; kv < hkv; ++kv) __hip_atomic_store(of.sync + kv, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(of.sync + hkv, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-hipError_t launch_attn_oproj_decode(bf16_t* out, float* part_o, float* part_ml, int* counters, bf16_t* k_cache,
-                                    bf16_t* v_cache, const int* block_tables, int bt_stride, const int* ctx_lens,
-                                    int num_seqs, int max_ctx, int hq, int hkv, float scale, const AttnDecodeFuse& fz,
-                                    const AttnOprojFuse& of, hipStream_t s) {
-  if (num_seqs == 0) return hipSuccess;
-  if (hq % hkv || num_seqs > 32 || counters == nullptr || of.sync == nullptr || of.w == nullptr) return hipErrorInvalidValue;
-  const int G = hq / hkv;
-  const int maxp3 = (max_ctx + DEC_KEYS - 1) / DEC_KEYS;
-  if ((int64_t)num_seqs * hq * maxp3 * D * 4 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
-  if (fz.sk < 1 || fz.ssp_tiles < 1 || fz.ssp_tiles > 128 || ((fz.sk * (G + 2) + 1) / 2) * 1024 + 1536 > V3_MERGE)
-    return hipErrorInvalidValue;
-  // o-proj: K = hq * 128 in 4 slices of >= 3 ring chunks, whole 64-column tiles, mode-3 operands
-  if (of.sk != OP_SK || of.k != hq * D || of.n % OP_WR || (of.k / OP_SK) % OP_KC || of.k / OP_SK / OP_KC < 3 ||
-      of.g.resid == nullptr || of.g.ssp_out == nullptr || of.g.counters == nullptr || !of.g.tiled ||
-      of.g.grp_off != nullptr || (int64_t)OP_SK * num_seqs * of.n * 4 >= ((int64_t)1 << 31))
-    return hipErrorInvalidValue;
-  const float sl2 = scale * 1.4426950408889634f;
-  AttnDecodeFuse fzc = fz;
-  fzc.ts = nullptr;
-  const dim3 grid(num_cus()), block(256);
-#define DIE_AO(GG, XR)                                                                                      \
-  hipLaunchKernelGGL((attn_oproj_v3_kernel<GG, XR>), grid, block, V3_LDS, s, out, part_o, part_ml, counters, \
-                     k_cache, v_cache, block_tables, bt_stride, ctx_lens, num_seqs, hq, hkv, sl2, maxp3, fzc, of)
-#define DIE_AOG(GG)          \
-  case GG:                   \
-    if (num_seqs <= 16)      \
-      DIE_AO(GG, 16);        \
-    else                     \
-      DIE_AO(GG, 32);        \
-    break;
-  switch (G) {
-    DIE_AOG(1)
-    DIE_AOG(2)
-    DIE_AOG(4)
-    DIE_AOG(8)
-    default:
-      return hipErrorInvalidValue;
-  }
-#undef DIE_AOG
-#undef DIE_AO
-  return hipGetLastError();
-}
 
 // grid = (num_seqs, hq); block = 128 (one lane per head-dim element).
 __global__ void __launch_bounds__(128) attn_decode_reduce_kernel(bf16_t* __restrict__ out,

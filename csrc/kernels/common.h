@@ -40,8 +40,25 @@ __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
   }
 }
 
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+
+// two floats -> packed bf16 pair (a low): ONE v_cvt_pk_bf16_f32 with both operands (a scalar cast per
+// element costs a cvt each plus a shift and an or)
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  const f32x2_t v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+
+// x op x' where x' is the value of lane (i ^ 32): one v_permlane32_swap_b32 (VALU) instead of a
+// ds_bpermute round trip through the LDS unit
+__device__ __forceinline__ float xor32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
 __device__ __forceinline__ uint4 pack8(const float* f) {

@@ -30,15 +30,367 @@
 //    that the CONSUMER kernel (fused attention prologue, RMSNorm) sums; or the
 //    split-K last arriver adds the tile into the residual stream and writes the
 //    next RMSNorm's row statistics.
+#include "common.h"
+#include "launchers.h"
 
-#include "gemm_decode.h"
 #include <algorithm>
 #include <cstdlib>
 
 namespace die {
+namespace gd {
+
+constexpr int NTH = 256;              // threads per workgroup
+constexpr int SSP_LD = 128;           // row stride of the norm-statistics arrays ([tiles][SSP_LD])
+constexpr int RING_BYTES = 147456;    // LDS for the ring (144 KiB; the epilogue scratch reuses it)
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void global_cvoid;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f4;
+
+template <int AUX = 0>
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((global_cvoid*)src, (lds_void*)lds_wave_base, 16, 0, AUX);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// 16-byte chunk swizzle of image row r for a row of ROWB bytes: conflict-free ds_read_b128 of the
+// 16x16x32 A/B fragments (16 rows x one chunk per lane group) for every supported K slot.
+template <int ROWB>
+__device__ __forceinline__ int swz(int r) {
+  if constexpr (ROWB >= 256) return r & 15;
+  else if constexpr (ROWB == 128) return (r >> 1) & 7;
+  else return (r ^ (r >> 1)) & 3;  // 64-byte rows
+}
+
+// LDS ring depth for a (WR, XR, KC) tile: the deepest that fits RING_BYTES and the 6-bit vmcnt
+constexpr int ring_slots(int wr, int xr, int kc) {
+  const int slot = (wr + xr) * kc * 2;
+  const int per_wave = (wr + xr) / (64 / (kc / 8)) / 4;
+  int s = RING_BYTES / slot;
+  if (s > 8) s = 8;
+  while (s > 2 && (s - 1) * per_wave > 63) --s;
+  return s;
+}
+
+}  // namespace gd
 
 using namespace gd;
 
+// EPI 0: bf16 Y = XW^T. EPI 1: bf16 Y[:, j] = silu(g_j) * u_j, W = [gate(N_out rows); up(N_out rows)].
+// EPI 2: fp32 slab Y[blockIdx.y][m][n] (split-K partial). EPI 3: slab + last-arriver residual update.
+// EPI 4: EPI 1 with the rows scaled by the RMSNorm statistics ssp_in.
+// WR = weight rows in the workgroup's image; output columns per workgroup = WR (EPI 0/2/3) or WR/2 (EPI 1/4).
+// KC = K elements per ring slot. XR = activation rows staged per chunk.
+// NT: weight pieces are loaded non-temporal (aux = 2): each weight byte is read once per step by one CU,
+// so it should not displace the activations / KV in L2 and MALL (MI355X_MICROARCH.md "nt-weights").
+template <int WR, int EPI, int S, bool NT, int KC, int XR, int SKC = 0>
+__device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const bf16_t* __restrict__ X, int64_t ldx,
+                                        const bf16_t* __restrict__ W, int M, int N_out, int K,
+                                        const GemmDecodeFuse& fz, const int bx, const int by, const int ny) {
+  constexpr int ROWB = KC * 2;                 // bytes per image row
+  constexpr int CPR = KC / 8;                  // 16-byte chunks per row
+  constexpr int RPP = 64 / CPR;                // rows per 1-KiB DMA piece
+  constexpr bool SILU = EPI == 1 || EPI == 4;
+  constexpr int NO = SILU ? WR / 2 : WR;       // output columns per workgroup
+  constexpr int SLOT = (WR + XR) * ROWB;       // bytes per ring slot
+  constexpr int INSTR = (WR + XR) / RPP;       // 1-KiB DMA pieces per chunk
+  constexpr int SPLIT = XR >= 64 ? 2 : (KC >= 128 ? 0 : 1);  // waves split 0: K, 1: columns, 2: rows
+  constexpr int NTILE = WR / 16;               // 16-column MFMA tiles
+  constexpr int MT = SPLIT == 2 ? XR / 64 : XR / 16;   // 16-row MFMA tiles per wave
+  constexpr int NTW = SPLIT == 1 ? NTILE / 4 : NTILE;  // 16-column MFMA tiles per wave
+  constexpr int KSW = SPLIT == 0 ? KC / 128 : KC / 32; // 32-deep k-steps per wave per chunk
+  constexpr int NRED = SPLIT == 0 ? 4 : 1;     // partial copies summed by the epilogue
+  constexpr int RR = XR < 32 ? 32 : XR;        // row pitch of the epilogue scratch
+  constexpr int PER_WAVE = INSTR / 4;          // pieces issued per wave per chunk
+  static_assert(KSW >= 1 && (SPLIT != 1 || NTILE % 4 == 0), "tile does not split over 4 waves");
+  static_assert(INSTR % 4 == 0 && WR % RPP == 0 && XR % RPP == 0, "pieces must split over 4 waves, W/X unmixed");
+  static_assert((S - 1) * PER_WAVE <= 63 && S >= 2, "vmcnt field is 6 bits");
+  static_assert(S * SLOT <= 160 * 1024, "ring exceeds LDS");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int r0 = 0;
+  if (fz.grp_off != nullptr) {
+    // grouped (MoE) form: blockIdx.z = expert; its rows of X/Y are [off[e], off[e+1]) of the
+    // token-sorted activations, its weights W + e * grp_wstride. Unused experts cost nothing.
+    // (The launcher picks XR from the largest possible group.) With grp_rows the activation rows are
+    // gathered from the token order on the fly (no separate gather launch).
+    const int e = blockIdx.z;
+    r0 = fz.grp_off[e];
+    M = min(fz.grp_off[e + 1] - r0, XR);
+    if (M <= 0) return;
+    if (fz.grp_rows == nullptr) X += (int64_t)r0 * ldx;
+    W += (int64_t)e * fz.grp_wstride;
+    Yv = reinterpret_cast<char*>(Yv) + (int64_t)r0 * ldy * (EPI == 2 || EPI == 3 ? 4 : 2);
+  }
+  const int n0 = bx * NO;
+  const int kper = K / ny;
+  const int k0 = by * kper;
+  const int nch = kper / KC;
+
+  // Per-lane source rows for this wave's DMA pieces (fixed across chunks).
+  const bf16_t* src[PER_WAVE];
+  bool isw[PER_WAVE];
+#pragma unroll
+  for (int p = 0; p < PER_WAVE; ++p) {
+    const int piece = wave + 4 * p;
+    const int row = RPP * piece + lane / CPR;  // image row: [0, WR) = W, [WR, WR+XR) = X
+    const int lch = (lane % CPR) ^ swz<ROWB>(row);
+    const bf16_t* base;
+    if (row < WR) {
+      int grow = n0 + row;
+      if (SILU && row >= NO) grow = N_out + n0 + (row - NO);
+      base = W + (int64_t)grow * K;
+    } else {
+      const int xr = min(row - WR, M - 1);
+      base = fz.grp_rows != nullptr ? X + (int64_t)(fz.grp_rows[r0 + xr] / fz.grp_k) * ldx : X + (int64_t)xr * ldx;
+    }
+    src[p] = base + k0 + lch * 8;
+    if (row < WR && fz.tiled) {
+      // pre-packed weights (gd_pack_weights): tile bx's K-chunk c is WR/RPP contiguous 1-KiB pieces
+      // already in LDS-image order (rows, swizzle and all), so each piece is one linear 1-KiB read
+      src[p] = W + ((int64_t)bx * (K / KC) + k0 / KC) * (WR / RPP) * 512 + piece * 512 + lane * 8;
+    }
+    isw[p] = row < WR;
+  }
+  const int64_t wstep = fz.tiled ? (int64_t)(WR / RPP) * 512 : KC;  // W elements per K-chunk
+  auto issue = [&](int c) {
+    char* slot = smem + (c % S) * SLOT;
+#pragma unroll
+    for (int p = 0; p < PER_WAVE; ++p) {
+      // a piece is all-weight or all-activation rows: wave-uniform branch
+      if (isw[p]) {
+        if (NT)
+          glds16<2>(src[p] + (int64_t)c * wstep, slot + (wave + 4 * p) * 1024);
+        else
+          glds16<0>(src[p] + (int64_t)c * wstep, slot + (wave + 4 * p) * 1024);
+      } else {
+        glds16<0>(src[p] + (int64_t)c * KC, slot + (wave + 4 * p) * 1024);
+      }
+    }
+  };
+
+  // EPI 4: this thread's share of the producer's per-tile sums of squares (row tid % RR, tiles
+  // tid / RR + NSL * i), loaded before any LDS-DMA and first used in the epilogue, so no wait lands
+  // inside the weight stream. Index clamped, masked later (no branches).
+  constexpr int NSL = NTH / RR;                // tile slices
+  constexpr int NPF = (128 + NSL - 1) / NSL;   // prefetched statistics per thread (<= 128 tiles)
+  float ssv[EPI == 4 ? NPF : 1];
+  if constexpr (EPI == 4) {
+#pragma unroll
+    for (int i = 0; i < NPF; ++i)
+      ssv[i] = fz.ssp_in[min(tid / RR + NSL * i, fz.ssp_tiles - 1) * SSP_LD + (tid % RR)];
+  }
+
+  f4 acc[MT][NTW];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NTW; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int c = 0; c < S - 1; ++c)
+    if (c < nch) issue(c);
+
+  const int fr = lane & 15, kg = lane >> 4;
+#pragma unroll 1
+  for (int c = 0; c < nch; ++c) {
+    if (c + S - 1 < nch) issue(c + S - 1);
+    const int after = min(S - 1, nch - 1 - c);  // chunks issued after c
+    switch (after) {  // counted wait: the younger chunks stay in flight
+      case 7: wait_vm<(S > 7 ? 7 : 0) * PER_WAVE>(); break;
+      case 6: wait_vm<(S > 6 ? 6 : 0) * PER_WAVE>(); break;
+      case 5: wait_vm<(S > 5 ? 5 : 0) * PER_WAVE>(); break;
+      case 4: wait_vm<(S > 4 ? 4 : 0) * PER_WAVE>(); break;
+      case 3: wait_vm<(S > 3 ? 3 : 0) * PER_WAVE>(); break;
+      case 2: wait_vm<(S > 2 ? 2 : 0) * PER_WAVE>(); break;
+      case 1: wait_vm<PER_WAVE>(); break;
+      default: wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    const char* slot = smem + (c % S) * SLOT;
+    const char* ximg = slot + WR * ROWB;
+#pragma unroll
+    for (int kk = 0; kk < KSW; ++kk) {
+      const int ks = SPLIT == 0 ? wave * KSW + kk : kk;
+      const int lch = 4 * ks + kg;
+      bf16x8 a[MT], b[NTW];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int r = 16 * (SPLIT == 2 ? wave * MT + mt : mt) + fr;
+        a[mt] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ximg + r * ROWB + 16 * (lch ^ swz<ROWB>(r))));
+      }
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int r = 16 * (SPLIT == 1 ? wave * NTW + nt : nt) + fr;
+        b[nt] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(slot + r * ROWB + 16 * (lch ^ swz<ROWB>(r))));
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // slot c%S is refilled next iteration
+  }
+
+  // Partials through LDS (the ring is idle now): red[NRED][RR][WR] fp32.
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        // C: col = lane&15, row = (lane>>4)*4 + r
+        const int m = 16 * (SPLIT == 2 ? wave * MT + mt : mt) + 4 * kg + r;
+        const int n = 16 * (SPLIT == 1 ? wave * NTW + nt : nt) + fr;
+        red[((SPLIT == 0 ? wave : 0) * RR + m) * WR + n] = acc[mt][nt][r];
+      }
+  __syncthreads();
+  char* escr = smem + NRED * RR * WR * 4;  // epilogue scratch after the partials
+  if constexpr (EPI == 3) {
+    // split-K partial -> last arriver: h += sum of partials (bf16), per-tile row sums of squares.
+    // Every thread owns EPT float4 groups (row m, columns j..j+3); its own workgroup's partial stays in
+    // registers, so the last arriver reads only the OTHER ny-1 slabs, all of them issued back to back
+    // (SKC = compile-time ny: no per-slab round trip) together with the residual rows.
+    constexpr int Q = WR / 4;  // float4 column groups per row (8, 16 or 32 lanes: one row per lane group)
+    static_assert(Q == 8 || Q == 16 || Q == 32, "EPI 3 needs wr in {32, 64, 128}");
+    constexpr int EPT = RR * Q / NTH;
+    static_assert(EPT * NTH == RR * Q, "whole float4 groups per thread");
+    int* ctl = reinterpret_cast<int*>(escr);
+    const bool single = ny == 1;
+    f4 own[EPT];
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tid + i * NTH, m = e / Q, j = 4 * (e % Q);
+      own[i] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int w = 0; w < NRED; ++w) own[i] += *reinterpret_cast<const f4*>(red + (w * RR + m) * WR + j);
+    }
+    __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(Yv, 0, 0x7fffffff, 0x00020000);
+    if (!single) {
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) {
+        const int e = tid + i * NTH, m = e / Q, j = 4 * (e % Q);
+        if (m < M)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, own[i]), ry,
+              (int)((((int64_t)by * M + m) * ldy + n0 + j) * 4), 0, 16);  // write-through (sc1): no release fence
+      }
+      wait_vm<0>();
+      __syncthreads();
+      if (tid == 0)
+        ctl[0] = __hip_atomic_fetch_add(fz.counters + bx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ny - 1;
+      __syncthreads();
+      if (!ctl[0]) return;
+    }
+    uint2 hr[EPT];
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {  // rows clamped (no branch around a load), masked on the write
+      const int e = tid + i * NTH, m = min(e / Q, M - 1), j = 4 * (e % Q);
+      hr[i] = *reinterpret_cast<const uint2*>(fz.resid + (int64_t)m * fz.ld_resid + n0 + j);
+    }
+    if (!single) {
+      if constexpr (SKC > 1) {
+        // the other slabs in groups of IG float4 groups x (SKC - 1) loads in flight (<= 32 registers of 16 B)
+        constexpr int IG = EPT * (SKC - 1) <= 32 ? EPT : (32 / (SKC - 1) > 0 ? 32 / (SKC - 1) : 1);
+#pragma unroll
+        for (int i0 = 0; i0 < EPT; i0 += IG) {
+          f4 pv[IG][SKC - 1];
+#pragma unroll
+          for (int ii = 0; ii < IG; ++ii) {
+            const int e = tid + (i0 + ii) * NTH, m = min(e / Q, M - 1), j = 4 * (e % Q);
+#pragma unroll
+            for (int kk = 0; kk < SKC - 1; ++kk) {
+              const int k = kk + (kk >= by);
+              pv[ii][kk] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                      ry, (int)((((int64_t)k * M + m) * ldy + n0 + j) * 4), 0, 16));
+            }
+          }
+#pragma unroll
+          for (int ii = 0; ii < IG; ++ii)
+#pragma unroll
+            for (int kk = 0; kk < SKC - 1; ++kk) own[i0 + ii] += pv[ii][kk];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+          const int e = tid + i * NTH, m = min(e / Q, M - 1), j = 4 * (e % Q);
+          for (int k = 0; k < ny; ++k)
+            if (k != by)
+              own[i] += __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   ry, (int)((((int64_t)k * M + m) * ldy + n0 + j) * 4), 0, 16));
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {  // Q | 64 and NTH % Q == 0: a row's lanes share a wave
+      const int e = tid + i * NTH, m = e / Q, j = 4 * (e % Q);
+      const f4 v = own[i];
+      float hv[4] = {bf2f((bf16_t)(hr[i].x & 0xffff)) + v[0], bf2f((bf16_t)(hr[i].x >> 16)) + v[1],
+                     bf2f((bf16_t)(hr[i].y & 0xffff)) + v[2], bf2f((bf16_t)(hr[i].y >> 16)) + v[3]};
+      uint2 hw;
+      hw.x = pack2(hv[0], hv[1]);
+      hw.y = pack2(hv[2], hv[3]);
+      float ss = 0.f;
+      if (m < M) {
+        *reinterpret_cast<uint2*>(fz.resid + (int64_t)m * fz.ld_resid + n0 + j) = hw;
+        const float q0 = bf2f((bf16_t)(hw.x & 0xffff)), q1 = bf2f((bf16_t)(hw.x >> 16));
+        const float q2 = bf2f((bf16_t)(hw.y & 0xffff)), q3 = bf2f((bf16_t)(hw.y >> 16));
+        ss = q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3;
+      }
+#pragma unroll
+      for (int o = Q / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+      if (e % Q == 0 && m < SSP_LD) fz.ssp_out[bx * SSP_LD + m] = m < M ? ss : 0.f;
+    }
+    if (!single && tid == 0) __hip_atomic_store(fz.counters + bx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if constexpr (EPI == 4) {
+    // row scale r[m] = rsqrt(sum_t ssp[t][m] / n + eps) (the RMSNorm whose weight is folded into W)
+    float* part = reinterpret_cast<float*>(escr);  // [NSL][RR]
+    float* rs = part + NTH;
+    float acc_ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) acc_ss += tid / RR + NSL * i < fz.ssp_tiles ? ssv[i] : 0.f;
+    part[tid] = acc_ss;  // tid = slice * RR + row
+    __syncthreads();
+    if (tid < RR) {
+      float t = 0.f;
+#pragma unroll
+      for (int sl = 0; sl < NSL; ++sl) t += part[sl * RR + tid];
+      rs[tid] = rsqrtf(t * fz.inv_n + fz.eps);
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < RR * NO; e += NTH) {
+    const int m = e / NO, j = e % NO;
+    if (m >= M) continue;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NRED; ++w) v += red[(w * RR + m) * WR + j];
+    if (SILU) {
+      float u = 0.f;
+#pragma unroll
+      for (int w = 0; w < NRED; ++w) u += red[(w * RR + m) * WR + NO + j];
+      if constexpr (EPI == 4) {
+        const float r = reinterpret_cast<const float*>(escr)[NTH + m];
+        v *= r;
+        u *= r;
+      }
+      v = v / (1.f + __expf(-v)) * u;
+    }
+    if (EPI == 2)
+      reinterpret_cast<float*>(Yv)[((int64_t)by * M + m) * ldy + n0 + j] = v;
+    else
+      reinterpret_cast<bf16_t*>(Yv)[(int64_t)m * ldy + n0 + j] = f2bf(v);
+  }
+}
 
 template <int WR, int EPI, int S, bool NT, int KC, int XR, int SKC = 0>
 __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv, int64_t ldy,

@@ -94,21 +94,6 @@ struct GemmDecodeFuse {
 hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,
                               int K, int mode, int wr, int kc, int sk, bool nt, const GemmDecodeFuse& fz,
                               hipStream_t s);
-// Decode attention (fused prologue) + o-proj with the residual update in ONE persistent launch
-// (attention.hip, attn_oproj_v3_kernel): after its attention tasks every workgroup runs o-proj tiles of
-// the mode-3 decode GEMM, each waiting only for the kv heads of its K slice.
-struct AttnOprojFuse {
-  const bf16_t* w = nullptr;  // o-proj weights [n, k], tile-order packed for (wr, kc) = (64, 256)
-  int n = 0, k = 0;           // hidden, hq * 128
-  int sk = 0;                 // split-K (4)
-  float* slab = nullptr;      // [sk][M][n] fp32 partials
-  int* sync = nullptr;        // [hkv + 2] int32 zeroed once: per-kv-head done counts, exit ticket, error flag
-  GemmDecodeFuse g;           // mode 3: resid, ssp_out, counters; tiled = 1
-};
-hipError_t launch_attn_oproj_decode(bf16_t* out, float* part_o, float* part_ml, int* counters, bf16_t* k_cache,
-                                    bf16_t* v_cache, const int* block_tables, int bt_stride, const int* ctx_lens,
-                                    int num_seqs, int max_ctx, int hq, int hkv, float scale, const AttnDecodeFuse& fz,
-                                    const AttnOprojFuse& of, hipStream_t s);
 // consumers of fp32 split-K slabs [sk][rows][width]
 hipError_t launch_fused_add_rms_norm_slab(bf16_t* out, const float* slab, int sk, bf16_t* residual, const bf16_t* w,
                                           float eps, int rows, int hidden, int64_t out_stride, hipStream_t s);

@@ -516,11 +516,6 @@ class CausalLM:
         sc = {"plans": plans, "ssp0": torch.zeros(1, ld, dtype=f32, device=dev),
               "ssp_a": torch.zeros(to, ld, dtype=f32, device=dev), "cnt_a": torch.zeros(to, dtype=i32, device=dev),
               "ssp_b": torch.zeros(td, ld, dtype=f32, device=dev), "cnt_b": torch.zeros(td, dtype=i32, device=dev)}
-        if os.environ.get("DIE_FUSE_OPROJ", "0") != "0" and not (self.tp.enabled or self.arch.is_moe):
-            # attention + o-proj in one launch (ops.attn_oproj_decode_fused): per-kv-head done counts,
-            # exit ticket, error flag. Measured a tie with the two launches (docs/performance.md), so off
-            # by default: its polls assume every workgroup of the launch is resident (a whole GPU)
-            sc["osync"] = torch.zeros(self.hkv + 2, dtype=i32, device=dev)
         return sc
 
     def _fused_decode_ok(self, kv_pool: torch.Tensor, m: int = 32) -> bool:
@@ -551,22 +546,14 @@ class CausalLM:
             t = lw.tiled.get((name, wr, kc))
             return (getattr(lw, name), False) if t is None else (t, True)
 
-        # attention and the o-proj residual update in one launch: dense, TP = 1, <= 32 rows, (64, 256) x 4
-        fuse_o = (sc.get("osync") is not None and h.shape[0] <= 32 and (wo, ko, so) == (64, 256, 4))
         ssp_prev = ops.row_sumsq(h, out=sc["ssp0"])
         for li, lw in enumerate(self.layers):
             k_cache, v_cache = kv_pool[li, 0], kv_pool[li, 1]
             wqkv, tq = tw(lw, "qkv", wq, kq)
             slab = ops.linear_slab(h, wqkv, sk=sq, wr=wq, tiled=tq, kc=kq)
-            aargs = (slab, ssp_prev, positions, self.cos_sin, meta.slot_mapping, k_cache, v_cache, meta.block_tables,
-                     meta.ctx_lens, meta.max_ctx, hq, hkv, self.scale, eps, hid, meta.part_o, meta.part_ml,
-                     meta.attn_cnt)
-            wo_t, to_ = tw(lw, "o", wo, ko)
-            o_done = fuse_o and to_
-            if o_done:
-                attn = ops.attn_oproj_decode_fused(*aargs, wo_t, h, ssp_a, sc["cnt_a"], sc["osync"])
-            else:
-                attn = ops.attn_decode_fused(*aargs)
+            attn = ops.attn_decode_fused(slab, ssp_prev, positions, self.cos_sin, meta.slot_mapping,
+                                         k_cache, v_cache, meta.block_tables, meta.ctx_lens, meta.max_ctx, hq, hkv,
+                                         self.scale, eps, hid, meta.part_o, meta.part_ml, meta.attn_cnt)
             if a.is_moe:  # ln2 stays explicit (it also feeds the router); MoE output added back + statistics
                 if self.tp.enabled:
                     self.tp.all_reduce_residual(ops.linear(attn, lw.o), h, ssp_a)
@@ -588,9 +575,9 @@ class CausalLM:
                     self.tp.all_reduce_residual(ops.linear(act, lw.down), h, ssp_b)
                 else:
                     wdn_, kd, sd = plan["down"]
+                    wo_t, to_ = tw(lw, "o", wo, ko)
                     wd_t, td_ = tw(lw, "down", wdn_, kd)
-                    if not o_done:
-                        ops.linear_slab_residual(attn, wo_t, h, ssp_a, sc["cnt_a"], wo, so, tiled=to_, kc=ko)
+                    ops.linear_slab_residual(attn, wo_t, h, ssp_a, sc["cnt_a"], wo, so, tiled=to_, kc=ko)
                     act = ops.linear_silu_mul_rownorm(h, wgu, ssp_a, eps, wg, tiled=tg, kc=kg)
                     ops.linear_slab_residual(act, wd_t, h, ssp_b, sc["cnt_b"], wdn_, sd, tiled=td_, kc=kd)
             ssp_prev = ssp_b

@@ -137,26 +137,6 @@ def attn_decode_fused(qkv_slab: torch.Tensor, ssp: torch.Tensor, positions: torc
     return out
 
 
-def attn_oproj_decode_fused(qkv_slab: torch.Tensor, ssp: torch.Tensor, positions: torch.Tensor,
-                            cos_sin: torch.Tensor, slot_mapping: torch.Tensor, k_cache: torch.Tensor,
-                            v_cache: torch.Tensor, block_tables: torch.Tensor, ctx_lens: torch.Tensor, max_ctx: int,
-                            hq: int, hkv: int, scale: float, eps: float, hidden: int, part_o: torch.Tensor,
-                            part_ml: torch.Tensor, counters: torch.Tensor, wo_tiled: torch.Tensor,
-                            resid: torch.Tensor, ssp_out: torch.Tensor, ocnt: torch.Tensor,
-                            sync: torch.Tensor) -> torch.Tensor:
-    """attn_decode_fused followed by the o-proj residual update (linear_slab_residual, tile (64, 256),
-    split-K 4, `wo_tiled` = gd_pack_weights(wo, 64, kc=256)) in ONE persistent launch (attention.hip,
-    attn_oproj_v3_kernel): resid += attn @ wo^T, ssp_out [N/64, SSP_LD] = the new residual's per-tile row
-    sums of squares. sync: int32 [hkv + 2] zeroed once. At most 32 rows. Returns the attention output."""
-    n = ctx_lens.numel()
-    out = torch.empty(n, hq * 128, dtype=torch.bfloat16, device=qkv_slab.device)
-    oslab = torch.empty(4, n, wo_tiled.shape[0], dtype=torch.float32, device=qkv_slab.device)
-    _kern().attn_oproj_decode_fused(out, part_o, part_ml, counters, qkv_slab, ssp, positions, cos_sin,
-                                    slot_mapping, k_cache, v_cache, block_tables, ctx_lens, max_ctx, hq, hkv, scale,
-                                    eps, hidden, wo_tiled, oslab, resid, ssp_out, ocnt, sync)
-    return out
-
-
 def decode_advance(out, ids, pos, ctx, slots, bt, step, tokens, cnt, n_real, rows: int, block_size: int) -> None:
     """Device-side advance of the decode inputs (decode_step.hip); see ModelRunner.decode_multi."""
     _kern().decode_advance(out, ids, pos, ctx, slots, bt, step, tokens, cnt, n_real, rows, block_size)

@@ -476,59 +476,6 @@ def test_attn_decode_fused(dev, g, hkv, big):
     assert int(cnt.abs().sum()) == 0
 
 
-@pytest.mark.parametrize("g,hkv,n", [(4, 8, 32), (4, 8, 7), (4, 8, 1), (8, 4, 20), (2, 16, 32), (1, 32, 16)])
-def test_attn_oproj_decode_fused(dev, g, hkv, n):
-    """Attention + o-proj residual update in one persistent launch (attn_oproj_v3_kernel) against the two
-    launches it replaces (attn_decode_fused, then linear_slab_residual with the same tile): identical
-    attention output and residual, same statistics; the in-kernel hand-off counters re-arm (two calls)."""
-    hq, sk, bs, d, hid = hkv * g, 2, 16, 128, 4096
-    ctxs = ([1, 17, 200, 777, 2049, 64, 65] + [300 + 37 * i for i in range(32)])[:n]
-    width = (hq + 2 * hkv) * d
-    _, kc, vc, bt, _, ctx, _ = _make_seqs([1] * n, ctxs, hkv, bs, dev, g)
-    max_ctx = 4096
-    bt_wide = torch.zeros(n, max_ctx // bs, dtype=torch.int32, device=dev)
-    bt_wide[:, : bt.shape[1]] = bt
-    slab = torch.randn(sk, n, width, device=dev) * 0.7
-    ssv = (torch.rand(n, device=dev) + 0.5) * hid
-    ssp = torch.zeros(4, ops.SSP_LD, device=dev)
-    ssp[:, :n] = (ssv / 4)[None, :]
-    slots = torch.tensor([int(bt[i, (c - 1) // bs]) * bs + (c - 1) % bs for i, c in enumerate(ctxs)],
-                         dtype=torch.long, device=dev)
-    pos = (ctx - 1).long()
-    cs = ref.rope_cos_sin(8192, d, 500000.0, dev)
-    maxp = ops.decode_partials(max_ctx)
-    po = torch.empty(n * hq * maxp * d, device=dev)
-    pm = torch.empty(n * hq * maxp * 2, device=dev)
-    cnt = torch.zeros(n * hkv, dtype=torch.int32, device=dev)
-    wo = torch.randn(hid, hq * d, device=dev, dtype=torch.bfloat16) / math.sqrt(hq * d)
-    wo_t = ops.gd_pack_weights(wo, 64, kc=256)
-    h0 = torch.randn(n, hid, device=dev, dtype=torch.bfloat16)
-    h_ref, h_fused = h0.clone(), h0.clone()
-    ssp_ref = torch.zeros(hid // 64, ops.SSP_LD, device=dev)
-    ssp_f = torch.zeros_like(ssp_ref)
-    ocnt_ref = torch.zeros(hid // 64, dtype=torch.int32, device=dev)
-    ocnt = torch.zeros_like(ocnt_ref)
-    sync = torch.zeros(hkv + 2, dtype=torch.int32, device=dev)
-    args = (slab, ssp, pos, cs, slots, kc, vc, bt_wide, ctx, max_ctx, hq, hkv, 1 / math.sqrt(d), 1e-5, hid, po, pm,
-            cnt)
-    for _ in range(2):
-        a_ref = ops.attn_decode_fused(*args)
-        ops.linear_slab_residual(a_ref, wo_t, h_ref, ssp_ref, ocnt_ref, 64, 4, tiled=True, kc=256)
-        a_f = ops.attn_oproj_decode_fused(*args, wo_t, h_fused, ssp_f, ocnt, sync)
-        torch.cuda.synchronize()
-        assert int(sync[hkv + 1]) == 0, "a hand-off wait timed out"
-        assert int(sync.abs().sum()) == 0 and int(ocnt.abs().sum()) == 0 and int(cnt.abs().sum()) == 0
-        assert torch.equal(a_f, a_ref)
-        # the split-K last arriver (which of the 4 slices adds the others) differs between the launches:
-        # fp32 sums in another order, so the residual may differ by a bf16 rounding step
-        close(h_fused, h_ref, atol=1e-2, rtol=8e-3)
-        close(ssp_f[:, :n], ssp_ref[:, :n], atol=1e-2, rtol=1e-2)
-        h_fused.copy_(h_ref)
-    # and against fp32 math
-    close(h_fused, (h0.float() + 2 * (a_ref.float() @ wo.float().t())), atol=6e-2, rtol=2e-2)
-    assert (h_fused.float() - h0.float()).abs().max() > 0.1  # the update happened
-
-
 def test_residual_add_sumsq(dev):
     m, h = 13, 8192
     res = torch.randn(m, h, device=dev, dtype=torch.bfloat16)
