@@ -90,6 +90,8 @@ def main():
     ap.add_argument("--max-num-seqs", type=int, default=64)
     ap.add_argument("--mixed-step-tokens", type=int, default=64)
     ap.add_argument("--modes", default="auto,off,always")
+    # prefill batching under load, "tokens:wait_ms" per run (0:0 = off; EngineConfig.prefill_batch_tokens)
+    ap.add_argument("--prefill-batch", default="0:0")
     ap.add_argument("--device", default="cuda")
     a = ap.parse_args()
     dev = torch.device("cuda:0" if a.device == "cuda" else "cpu")
@@ -115,17 +117,26 @@ def main():
         await closed_wave(32)
         dstep = (eng.stats["decode_time"] - s0["decode_time"]) / (a.gen_len - 1) * 1e3
         print(json.dumps({"bench": "poisson", "pure_decode_step_ms_batch32": round(dstep, 3)}), flush=True)
-        for mi, mode in enumerate(a.modes.split(",")):
+        runs = [(mode, pb) for mode in a.modes.split(",") for pb in a.prefill_batch.split(",")]
+        for mi, (mode, pb) in enumerate(runs):
             eng.cfg.mixed_batching = mode
+            pbt, pbw = pb.split(":")
+            eng.cfg.prefill_batch_tokens, eng.cfg.prefill_batch_wait_ms = int(pbt), float(pbw)
             for r in (float(x) for x in a.rates.split(",")):
                 st0 = dict(eng.scheduler.stats())
                 hit0 = eng.stats["prefix_hit_tokens"]
+                t0s = {k: eng.stats.get(k, 0.0) for k in ("prefill_time", "decode_time", "mixed_time")}
                 # distinct prompts per (mode, rate): no run is served from another run's cached prefix blocks
                 res = await run_rate(aeng, r, a.requests, a.prompt_len, a.gen_len, vocab, seed=int(r * 100) + 7919 * mi)
                 res["prefix_hit_tokens"] = eng.stats["prefix_hit_tokens"] - hit0
                 st1 = eng.scheduler.stats()
                 steps = {k: st1[k] - st0[k] for k in ("steps_prefill", "steps_decode", "steps_mixed")}
-                res.update({"bench": "poisson", "mode": mode, "rate_rps": r, "requests": a.requests,
+                # engine time per step kind (decode steps counted per scheduler step: a window of k steps is one)
+                res["ms_per_step"] = {k.split("_")[0]: round((eng.stats.get(k, 0.0) - t0s[k]) * 1e3 / max(1, steps[n]), 2)
+                                      for k, n in (("prefill_time", "steps_prefill"), ("decode_time", "steps_decode"),
+                                                   ("mixed_time", "steps_mixed"))}
+                res.update({"bench": "poisson", "mode": mode, "prefill_batch": {"tokens": int(pbt), "wait_ms": float(pbw)},
+                            "rate_rps": r, "requests": a.requests,
                             "model": a.preset, "prompt_len": a.prompt_len, "gen_len": a.gen_len,
                             "tpot_p99_over_decode_step": round(res["tpot_ms"]["p99"] / dstep, 3), "steps": steps})
                 print(json.dumps(res), flush=True)

@@ -77,6 +77,7 @@ class LLMEngine:
             swap_blocks = int(cfg.swap_space_gib * 2**30 // per_block)
         self.scheduler = Scheduler(cfg, self.blocks, self.max_model_len, swap_capacity_blocks=swap_blocks)
         self.seqs: Dict[str, Sequence] = {}
+        self._step_est = 0.004  # EMA of one decode step (s): sizes windows that must end by a deadline
         self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "finished": 0, "prefill_time": 0.0,
                       "decode_time": 0.0, "steps": 0, "prefix_hit_tokens": 0}
         logger.info("KV pool: %d blocks x %d tokens = %.1f GiB (%d tokens)", nblocks, cfg.block_size,
@@ -236,6 +237,7 @@ class LLMEngine:
             toks_k = self.runner.decode_multi(out.decode, k) if k > 1 else [self.runner.decode(out.decode)]
             now = time.perf_counter()
             self.stats["decode_time"] += now - t0
+            self._step_est = 0.8 * self._step_est + 0.2 * (now - t0) / max(1, len(toks_k))
             for toks in toks_k:
                 for seq, tok in zip(out.decode, toks):
                     if seq.status == SeqStatus.FINISHED:  # stopped earlier in the window: discard
@@ -276,8 +278,15 @@ class LLMEngine:
         further than the longest remaining generation and the context limit, and only if KV
         slots for the whole window can be reserved now."""
         kmax = int(getattr(self.cfg, "decode_window", 1))
-        if kmax <= 1 or not getattr(self.runner, "supports_multistep", False) or self.scheduler.waiting:
+        if kmax <= 1 or not getattr(self.runner, "supports_multistep", False):
             return 1
+        if self.scheduler.waiting:
+            # prompts held for a larger prefill step (Scheduler._defer_prefill): a window that ends by
+            # their deadline; otherwise they must not sit behind a window
+            dl = self.scheduler.defer_deadline
+            if dl is None:
+                return 1
+            kmax = min(kmax, int((dl - time.perf_counter()) / max(self._step_est, 1e-4)))
         k = min(kmax, max(s.sampling.max_tokens - len(s.output_ids) for s in seqs),
                 min(self.max_model_len - len(s) + 1 for s in seqs))
         if k <= 1:

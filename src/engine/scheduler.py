@@ -109,6 +109,9 @@ class Scheduler:
         self.steps_decode = 0
         self.steps_mixed = 0
         self._stalled = False  # the last step was a prefill step that decode-ready sequences waited for
+        # while new prompts are held for a larger prefill step (cfg.prefill_batch_tokens): the time by
+        # which the oldest must be admitted (the engine sizes its decode windows to end by then)
+        self.defer_deadline: Optional[float] = None
 
     def add(self, seq: Sequence) -> None:
         seq.status = SeqStatus.WAITING
@@ -178,6 +181,11 @@ class Scheduler:
             # prefill step (the decode rows wait for it) with one decode-only step, so decode progresses at
             # least every other step and no prompt is split into ride-along fragments
             mixed = mode == "always" or pending <= room
+            if not mixed and self._defer_prefill(now, blocked):
+                out.decode = self._schedule_decode(ready, out)
+                if out.decode:
+                    self.steps_decode += 1
+                return out
             if not mixed and self._stalled:
                 self._stalled = False
                 out.decode = self._schedule_decode(ready, out)
@@ -186,6 +194,11 @@ class Scheduler:
                 return out
             if not mixed and pending:
                 budget = min(budget, self.cfg.prefill_tokens_while_decoding)
+        elif ready and self._defer_prefill(now, blocked):
+            out.decode = self._schedule_decode(ready, out)
+            if out.decode:
+                self.steps_decode += 1
+            return out
         self._stalled = False
         if mixed:
             # decode rows first (they are latency-critical); prompt chunks fill the step up to
@@ -240,6 +253,22 @@ class Scheduler:
         if out.decode:
             self.steps_decode += 1
         return out
+
+    def _defer_prefill(self, now: float, blocked: bool) -> bool:
+        """Hold newly arrived prompts while sequences decode (cfg.prefill_batch_tokens): True while
+        fewer than that many prompt tokens wait and the oldest is younger than prefill_batch_wait_ms.
+        Chunked prefills already running are never held."""
+        self.defer_deadline = None
+        want = int(getattr(self.cfg, "prefill_batch_tokens", 0) or 0)
+        if want <= 0 or blocked or not self.waiting or any(s.in_prefill for s in self.running):
+            return False
+        if sum(max(1, len(s) - s.num_computed) for s in self.waiting) >= want:
+            return False
+        deadline = self.waiting[0].arrival + float(self.cfg.prefill_batch_wait_ms) / 1e3
+        if now >= deadline:
+            return False
+        self.defer_deadline = deadline
+        return True
 
     def _mixed_mode(self) -> str:
         m = self.cfg.mixed_batching

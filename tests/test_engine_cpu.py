@@ -264,3 +264,38 @@ def test_mixed_auto_policy():
     assert all(not (a == b == "steps_prefill") for a, b in zip(kinds, kinds[1:]))  # never two stalls in a row
     for i, p in enumerate(([9, 10, 11, 12, 13], short_p, long_p)):
         assert got[i] == greedy_reference(eng.model, p, 10), i
+
+
+def test_prefill_batching_under_load():
+    """prefill_batch_tokens: while a sequence decodes, a prompt needing a prefill step is held (decode
+    steps continue) until enough prompt tokens wait or the oldest has waited prefill_batch_wait_ms."""
+    eng = make_engine(max_num_seqs=6, budget=256, blocks=128)
+    eng.cfg.mixed_batching = "off"
+    eng.cfg.prefill_batch_tokens = 60
+    eng.cfg.prefill_batch_wait_ms = 1e6
+    sp = SamplingParams(max_tokens=12)
+    got = {}
+    ps = [p[:5] * 5 for p in prompts(3, seed=21)]  # 25-token prompts
+    eng.add_request("d0", [9, 10, 11, 12, 13], sp, on_finish=lambda s: got.__setitem__(0, list(s.output_ids)))
+    eng.step()
+    eng.add_request("a", ps[0], sp, on_finish=lambda s: got.__setitem__(1, list(s.output_ids)))
+    st = dict(eng.scheduler.stats())
+    eng.step()
+    eng.step()
+    assert eng.scheduler.stats()["steps_prefill"] == st["steps_prefill"]     # 25 < 60 tokens: held
+    assert eng.scheduler.defer_deadline is not None
+    eng.add_request("b", ps[1], sp, on_finish=lambda s: got.__setitem__(2, list(s.output_ids)))
+    eng.step()
+    assert eng.scheduler.stats()["steps_prefill"] == st["steps_prefill"]     # 50 < 60: still held
+    eng.add_request("c", ps[2], sp, on_finish=lambda s: got.__setitem__(3, list(s.output_ids)))
+    eng.step()
+    assert eng.scheduler.stats()["steps_prefill"] == st["steps_prefill"] + 1  # 75 >= 60: one prefill step
+    eng.cfg.prefill_batch_wait_ms = 0.0                                       # deadline passed: admit at once
+    eng.add_request("e", ps[0][:7], sp, on_finish=lambda s: got.__setitem__(4, list(s.output_ids)))
+    st = dict(eng.scheduler.stats())
+    eng.step()
+    assert eng.scheduler.stats()["steps_prefill"] == st["steps_prefill"] + 1
+    while eng.has_work():
+        eng.step()
+    for i, p in enumerate(([9, 10, 11, 12, 13], ps[0], ps[1], ps[2], ps[0][:7])):
+        assert got[i] == greedy_reference(eng.model, p, 12), i
