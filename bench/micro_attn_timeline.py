@@ -33,7 +33,7 @@ def main():
     width = (hq + 2 * hkv) * d
     sk = 2
     slab = torch.randn(sk, n, width, device=dev) * 0.7
-    ssp = torch.zeros(hid // 64, 32, device=dev)
+    ssp = torch.zeros(hid // 64, ops.SSP_LD, device=dev)
     ssp[:, :n] = float(hid) / ssp.shape[0]
     pos = (ctx - 1).long()
     cs = ref.rope_cos_sin(8192, d, 500000.0, dev)

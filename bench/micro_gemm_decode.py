@@ -129,7 +129,7 @@ def main_resid(m):
                 kc = 128 if wr >= 96 else 256
                 if k % (kc * sk) or (n // wr) * sk > 1024:
                     continue
-                ssp = torch.zeros(n // wr, 32, device=dev)
+                ssp = torch.zeros(n // wr, ops.SSP_LD, device=dev)
                 cnt = torch.zeros(n // wr, dtype=torch.int32, device=dev)
                 us = timeit(lambda w: ops.linear_slab_residual(x, w, res, ssp, cnt, wr, sk), ws)
                 print(json.dumps({"shape": name, "M": m, "mode": 3, "wr": wr, "sk": sk, "us": round(us, 2),

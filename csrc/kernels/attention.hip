@@ -814,7 +814,13 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
       } else {
         wait_vm<0>();
       }
-      __builtin_amdgcn_s_barrier();
+      // Each wave DMAs exactly the 32 K / V rows it computes on (rows 32 * wave ...), so after its own
+      // counted wait it needs no other wave. The workgroup barrier stays where another wave's data is
+      // involved: the first chunk (the query image, written by every thread or DMA'd by wave 0) and,
+      // FUSED, the chunk that gets the new token's row patched in (every wave's DMA of it must have
+      // landed before the patch is written). Waves otherwise run decoupled through the chunks instead
+      // of at the pace of the slowest wave's loads.
+      if (c == c0 || (FUSED && has_new && c + 1 == c1)) __builtin_amdgcn_s_barrier();
       if (fz.ts != nullptr && c == c0) tsv[1] = __builtin_amdgcn_s_memrealtime();
       const char* base = smem + b * V3_BUF;
       if constexpr (FUSED) {
@@ -858,7 +864,8 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
         softmax_tile_lazy(s, st, kb, ctx, scale_log2, h);
         pv_lds_swz_v3(base + DEC_KEYS * DEC_ROW + 32 * wave * DEC_ROW, s, st, lane);
       }
-      lds_barrier();  // buffer b is refilled by the next iteration
+      // buffer b is refilled (next iteration's DMA, this wave's own rows) only after this wave's reads
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     if (fz.ts != nullptr) tsv[3] = __builtin_amdgcn_s_memrealtime();
     if (dbg & 32) continue;
