@@ -478,11 +478,11 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
 
 
 // Grouped (MoE) decode GEMM: x [R, K] token-sorted activations (expert e owns rows
-// [offsets[e], offsets[e+1]), at most 32 of them — one decode step), w [E, rows, K] stacked
+// [offsets[e], offsets[e+1]), at most max_rows (<= 128) of them — one decode step), w [E, rows, K] stacked
 // expert weights, y [R, N] bf16. mode 1: w[e] = [gate; up] -> silu(gate)*up (N = rows/2);
 // mode 0: plain. Experts with no rows stream no weights.
-void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t mode, int64_t wr, Tensor rows,
-                         int64_t k) {
+void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t mode, int64_t wr, int64_t kc,
+                         Tensor rows, int64_t k, int64_t max_rows) {
   DIE_CHECK_CUDA(x);
   DIE_CHECK_BF16(x);
   DIE_CHECK_BF16(w);
@@ -503,8 +503,10 @@ void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t m
     TORCH_CHECK(k >= 1 && rows.numel() == y.size(0) && x.size(0) * k == y.size(0), "grouped gather: rows [T*k]");
   }
   TORCH_CHECK((gather || y.size(0) == x.size(0)) && y.size(1) == N, "y [R, N]");
-  TORCH_CHECK(wr == 32 || wr == 48 || wr == 64 || wr == 96 || wr == 112 || wr == 128, "wr");
-  const int64_t kc = wr >= 96 ? 128 : 256;
+  TORCH_CHECK(gd_tile_ok(wr, kc), "grouped: unsupported (wr, kc) tile");
+  // max_rows bounds every expert's rows (a token routes to an expert at most once: <= tokens); it picks
+  // the activation image (16 / 32 / 64 / 128 rows) and clamps each group to it
+  TORCH_CHECK(max_rows >= 1 && max_rows <= 128, "grouped: 1 <= max_rows <= 128");
   TORCH_CHECK(K % kc == 0 && N % (mode == 1 ? wr / 2 : wr) == 0, "tile shape");
   die::GemmDecodeFuse fz;
   fz.grp_off = offsets.data_ptr<int>();
@@ -514,11 +516,10 @@ void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t m
     fz.grp_rows = rows.data_ptr<int>();
     fz.grp_k = (int)k;
   }
-  // M = all rows: bounds every expert's rows (the kernel picks the 16-row activation image when <= 16)
   TORCH_CHECK(y.size(0) >= 1, "grouped: at least one row");
   DIE_HIP(die::launch_gemm_decode(y.data_ptr(), y.stride(0), bf(x), x.stride(0), bf(w),
-                                  (int)std::min<int64_t>(y.size(0), 32), (int)N, (int)K, (int)mode, (int)wr, (int)kc,
-                                  1, true, fz, cur_stream()));
+                                  (int)std::min<int64_t>(y.size(0), max_rows), (int)N, (int)K, (int)mode, (int)wr,
+                                  (int)kc, 1, true, fz, cur_stream()));
 }
 
 // Decode-step input advance (decode_step.hip), for multi-step decode windows.

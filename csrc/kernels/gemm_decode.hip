@@ -463,7 +463,6 @@ static hipError_t launch_gd(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, 
     return launch_gd_xr<WR, EPI, KC, 16, SKC>(Y, ldy, X, ldx, W, M, N_out, K, sk, nt, fz, s);
   if (M <= 32 && gd_valid(WR, 32, KC))
     return launch_gd_xr<WR, EPI, KC, 32, SKC>(Y, ldy, X, ldx, W, M, N_out, K, sk, nt, fz, s);
-  if (fz.grp_off != nullptr) return hipErrorInvalidValue;  // grouped (MoE) form: <= 32 rows per expert
   if (M <= 64 && gd_valid(WR, 64, KC))
     return launch_gd_xr<WR, EPI, KC, 64, SKC>(Y, ldy, X, ldx, W, M, N_out, K, sk, nt, fz, s);
   if (M <= 128 && gd_valid(WR, 128, KC))

@@ -224,7 +224,7 @@ __global__ void __launch_bounds__(256) moe_combine_residual_kernel(float* __rest
 hipError_t launch_moe_combine_residual(float* ssp, bf16_t* resid, int64_t rstride, const bf16_t* ys, const int* pos,
                                        const float* w, int T, int K, int H, hipStream_t s) {
   if (T == 0) return hipSuccess;
-  if (H % 8 || T > 32 || rstride % 8) return hipErrorInvalidValue;
+  if (H % 8 || T > DECODE_SSP_LD || rstride % 8) return hipErrorInvalidValue;
   hipLaunchKernelGGL(moe_combine_residual_kernel, dim3(T), dim3(256), 0, s, ssp, resid, rstride, ys, pos, w, K, H);
   return hipGetLastError();
 }

@@ -184,7 +184,9 @@ def scatter_blocks(pool: torch.Tensor, ids: torch.Tensor, buf: torch.Tensor) -> 
 
 
 DECODE_GEMM_MAX_M = 128   # weight-streaming decode GEMM / fused decode path (gemm_decode.hip)
-MOE_DECODE_MAX_T = 32     # expert-streaming grouped decode GEMM (<= 32 rows per expert)
+# expert-streaming grouped decode GEMM up to this many tokens (<= 128 rows per expert: 16/32/64/128-row
+# images); DIE_MOE_DECODE_MAX_T=32 restores round 1's limit (above it: the tiled grouped GEMM) for A/B
+MOE_DECODE_MAX_T = min(128, int(os.environ.get("DIE_MOE_DECODE_MAX_T", "128")))
 SSP_LD = 128              # row stride of the norm-statistics arrays [tiles, SSP_LD]
 
 
@@ -591,13 +593,16 @@ def moe_apply(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, w: torch.Ten
     offsets, sorted_idx, pos = moe_align(ids, groups)
     # rows of the extra groups are never computed: zero them so that weight 0 x row stays 0
     ys = (torch.zeros if groups > e else torch.empty)(t * k, hdim, dtype=x.dtype, device=x.device)
-    if t <= MOE_DECODE_MAX_T and _moe_decode_ok(hdim, inter) and x.is_contiguous():
-        # decode: every expert's weights streamed once by the weight-streaming kernel, its
-        # (<= 32) routed tokens riding along, gathered from x by the kernel itself through the
-        # sorted order; SiLU*mul fused; idle experts read nothing
+    tiles = _moe_decode_tiles(hdim, inter, t) if t <= MOE_DECODE_MAX_T and x.is_contiguous() else None
+    if tiles is not None:
+        # decode: every expert's weights streamed once by the weight-streaming kernel, its routed
+        # tokens (<= t, so the activation image of the step's row bucket holds any expert's group)
+        # riding along, gathered from x by the kernel itself through the sorted order; SiLU*mul
+        # fused; idle experts read nothing
+        (wr1, kc1), (wr2, kc2) = tiles
         a = torch.empty(t * k, inter, dtype=x.dtype, device=x.device)
-        kern.gemm_decode_grouped(a, x, w13, offsets, 1, _cfg_for(inter, hdim, 1)[0], sorted_idx, k)
-        kern.gemm_decode_grouped(ys, a, w2, offsets, 0, _moe_down_wr(hdim, inter), _NO_ROWS(x.device), 1)
+        kern.gemm_decode_grouped(a, x, w13, offsets, 1, wr1, kc1, sorted_idx, k, t)
+        kern.gemm_decode_grouped(ys, a, w2, offsets, 0, wr2, kc2, _NO_ROWS(x.device), 1, t)
         if residual is not None:  # combine + residual add + next-norm statistics in one launch
             kern.moe_combine_residual(ssp, residual, ys, pos, w)
             return residual
@@ -639,9 +644,24 @@ def _NO_ROWS(device) -> torch.Tensor:
     return t
 
 
-def _moe_decode_ok(hdim: int, inter: int) -> bool:
-    wr1 = _cfg_for(inter, hdim, 1)[0]
-    return hdim % 256 == 0 and inter % 256 == 0 and inter % (wr1 // 2) == 0 and hdim % 64 == 0
+def _moe_decode_tiles(hdim: int, inter: int, t: int):
+    """((wr, kc) of the gate/up grouped GEMM, (wr, kc) of the down one) for a decode step of t tokens, or
+    None when the shapes do not tile. Up to 32 rows: round 1's measured choice (gate/up as the dense
+    gate/up shape, down wr 64 / 32 at a 256-wide K slot); above, the row bucket's generic tile."""
+    if hdim % 64 or inter % 64:
+        return None
+    if t <= 32:
+        wr1 = _cfg_for(inter, hdim, 1)[0]
+        if hdim % 256 or inter % 256 or inter % (wr1 // 2):
+            return None
+        return gd_tile(wr1), gd_tile(64)
+    try:
+        b = _bucket(t)
+        wr1, kc1, _ = decode_tile(inter, hdim, 1, b, max_sk=1)
+        wr2, kc2, _ = decode_tile(hdim, inter, 0, b, max_sk=1)
+    except ValueError:
+        return None
+    return (wr1, kc1), (wr2, kc2)
 
 
 def _moe_down_wr(hdim: int, inter: int) -> int:

@@ -235,7 +235,7 @@ def test_block_movers(dev):
     assert torch.equal(other[:, ids], pool[:, ids])
 
 
-@pytest.mark.parametrize("t", [5, 32, 77, 600])  # decode streaming / grouped kernel / per-expert hipBLASLt
+@pytest.mark.parametrize("t", [5, 32, 77, 200, 600])  # decode streaming (<= 128) / grouped kernel / hipBLASLt
 def test_moe(dev, t):
     h, inter, e, k = 512, 256, 8, 2
     x = torch.randn(t, h, device=dev, dtype=torch.bfloat16)
@@ -269,12 +269,13 @@ def test_moe_route_fused(dev, t, h, e, k):
     close(w.cpu()[clear], wr[clear], atol=2e-3, rtol=2e-3)
 
 
-@pytest.mark.parametrize("t", [8, 32])
+@pytest.mark.parametrize("t", [8, 32, 48, 100, 128])
 @pytest.mark.parametrize("skew", [True, False])
 def test_moe_decode_grouped(dev, t, skew):
     """Grouped decode GEMM: 16-row activation image when all experts together have <= 16 rows (t = 8,
-    top-2), 32-row image otherwise; skew routes every token to experts 0 and 1 (t rows each, six idle
-    experts that must read nothing and write nothing)."""
+    top-2), 32 / 64 / 128-row images above (the step's row bucket bounds any expert's group); skew routes
+    every token to experts 0 and 1 (t rows each, six idle experts that must read nothing and write
+    nothing)."""
     h, inter, e, k = 1024, 512, 8, 2
     x = torch.randn(t, h, device=dev, dtype=torch.bfloat16)
     w13 = torch.randn(e, 2 * inter, h, device=dev, dtype=torch.bfloat16) / math.sqrt(h)
@@ -288,7 +289,7 @@ def test_moe_decode_grouped(dev, t, skew):
     close(ops.moe_apply(x, w13, w2, w, ids, e), want, atol=3e-2, rtol=3e-2)
     # decode epilogue form: residual += output, row statistics of the new residual (one launch)
     h0 = torch.randn(t, h, device=dev, dtype=torch.bfloat16)
-    hres, ssp = h0.clone(), torch.zeros(1, 32, device=dev)
+    hres, ssp = h0.clone(), torch.zeros(1, ops.SSP_LD, device=dev)
     ops.moe_apply(x, w13, w2, w, ids, e, residual=hres, ssp=ssp)
     close(hres, h0.float() + want.float(), atol=5e-2, rtol=3e-2)
     close(ssp[0, :t], hres.float().pow(2).sum(-1), atol=1e-2, rtol=1e-3)
