@@ -218,9 +218,9 @@ def main_moe(m):
     wr1 = ops._cfg_for(inter, h, 1)[0]
     wr2 = ops._moe_down_wr(h, inter)
     for nm, ws, fn in (("moe_w13", w13s, lambda w: kern.gemm_decode_grouped(a, xs, w, offsets, 1, *ops.gd_tile(wr1),
-                                                                            none, 1, m)),
+                                                                            none, 1, m, 1)),
                        ("moe_w2", w2s, lambda w: kern.gemm_decode_grouped(ys, a, w, offsets, 0, *ops.gd_tile(wr2),
-                                                                          none, 1, m))):
+                                                                          none, 1, m, 1))):
         us = timeit(fn, ws)
         wbytes = ws[0].numel() * 2
         print(json.dumps({"shape": nm, "M": m, "rows_per_expert": (offsets[1:] - offsets[:-1]).tolist(),
@@ -242,7 +242,7 @@ def main_chain(m):
         xs = x.repeat(n, 1).contiguous()
         a = torch.empty(n * m, inter, device=dev, dtype=torch.bfloat16)
         offsets = torch.arange(0, (n + 1) * m, m, dtype=torch.int32, device=dev)
-        one = timeit(lambda w: kern.gemm_decode_grouped(a, xs, w, offsets, 1, *ops.gd_tile(wr), none, 1, m), ws)
+        one = timeit(lambda w: kern.gemm_decode_grouped(a, xs, w, offsets, 1, *ops.gd_tile(wr), none, 1, m, 1), ws)
         sep = timeit(lambda w: [ops.gemm_decode(x, w[i], 1, wr, 1) for i in range(n)], ws)
         wbytes = n * 2 * inter * h * 2
         print(json.dumps({"bench": "chain", "M": m, "n_weight_sets": n, "one_launch_us": round(one, 2),

@@ -366,23 +366,6 @@ void moe_combine_residual(Tensor ssp, Tensor resid, Tensor ys, Tensor pos, Tenso
                                            cur_stream()));
 }
 
-void moe_grouped_gemm(Tensor y, Tensor x, Tensor w, Tensor offsets) {
-  DIE_CHECK_BF16(y);
-  DIE_CHECK_BF16(x);
-  DIE_CHECK_BF16(w);
-  DIE_CHECK_CONTIG(y);
-  DIE_CHECK_CONTIG(x);
-  DIE_CHECK_CONTIG(w);
-  DIE_CHECK_DTYPE(offsets, at::kInt);
-  TORCH_CHECK(w.dim() == 3 && x.dim() == 2 && y.dim() == 2, "w [E,N,K], x [M,K], y [M,N]");
-  const int64_t E = w.size(0), N = w.size(1), K = w.size(2);
-  TORCH_CHECK(x.size(1) == K && y.size(1) == N && y.size(0) == x.size(0) && offsets.numel() >= E + 1,
-              "moe_grouped_gemm shapes");
-  TORCH_CHECK(N % 64 == 0 && K % 32 == 0, "N % 64 and K % 32 required");
-  DIE_HIP(die::launch_moe_grouped_gemm(bf(y), bf(x), bf(w), offsets.data_ptr<int>(), (int)x.size(0), (int)E,
-                                       (int)N, (int)K, cur_stream()));
-}
-
 // Decode GEMM (gemm_decode.hip), x [M <= 128, K] @ w^T. mode 0 bf16 y [M, N]; 1 silu(x gate^T) * (x up^T)
 // with w = [gate; up]; 2 fp32 split-K slabs [sk, M, N]; 3 slabs + residual update of `resid` [M, N] and row
 // sums of squares `ssp_out` [N/wr, 128] (tickets `counters` [N/wr], zeroed once); 4 = mode 1 with rows
@@ -482,7 +465,7 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
 // expert weights, y [R, N] bf16. mode 1: w[e] = [gate; up] -> silu(gate)*up (N = rows/2);
 // mode 0: plain. Experts with no rows stream no weights.
 void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t mode, int64_t wr, int64_t kc,
-                         Tensor rows, int64_t k, int64_t max_rows) {
+                         Tensor rows, int64_t k, int64_t max_rows, int64_t segs) {
   DIE_CHECK_CUDA(x);
   DIE_CHECK_BF16(x);
   DIE_CHECK_BF16(w);
@@ -494,7 +477,9 @@ void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t m
   TORCH_CHECK(mode == 0 || mode == 1, "grouped: mode 0 or 1");
   TORCH_CHECK(w.dim() == 3 && w.size(2) == x.size(1), "w [E, rows, K]");
   const int64_t E = w.size(0), K = x.size(1);
-  TORCH_CHECK(offsets.numel() >= E + 1, "offsets [E+1]");
+  // segs > 1: expert e's rows come as segs groups (offsets [E * segs + 1], group g -> expert g / segs), each
+  // of at most max_rows rows, for steps whose experts may get more rows than the activation image holds
+  TORCH_CHECK(segs >= 1 && offsets.numel() >= E * segs + 1, "offsets [E * segs + 1]");
   const int64_t N = mode == 1 ? w.size(1) / 2 : w.size(1);
   const bool gather = rows.numel() > 0;  // x in token order, row j of the sorted order = rows[j] / k
   if (gather) {
@@ -511,7 +496,8 @@ void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t m
   die::GemmDecodeFuse fz;
   fz.grp_off = offsets.data_ptr<int>();
   fz.grp_wstride = w.size(1) * K;
-  fz.grp_n = (int)E;
+  fz.grp_n = (int)(E * segs);
+  fz.grp_div = (int)segs;
   if (gather) {
     fz.grp_rows = rows.data_ptr<int>();
     fz.grp_k = (int)k;
@@ -770,7 +756,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_align", &moe_align);
   m.def("moe_gather", &moe_gather);
   m.def("moe_combine", &moe_combine);
-  m.def("moe_grouped_gemm", &moe_grouped_gemm);
   m.def("gemm_decode", &gemm_decode);
   m.def("gd_set_timestamps", &gd_set_timestamps);
   m.def("attn_set_timestamps", &attn_set_timestamps);

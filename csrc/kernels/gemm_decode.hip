@@ -114,8 +114,9 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int r0 = 0;
   if (fz.grp_off != nullptr) {
-    // grouped (MoE) form: blockIdx.z = expert; its rows of X/Y are [off[e], off[e+1]) of the
-    // token-sorted activations, its weights W + e * grp_wstride. Unused experts cost nothing.
+    // grouped (MoE) form: blockIdx.z = group; its rows of X/Y are [off[e], off[e+1]) of the
+    // token-sorted activations, its weights those of expert e / grp_div (an expert with more rows than
+    // the image is split into grp_div segments). Empty groups cost nothing.
     // (The launcher picks XR from the largest possible group.) With grp_rows the activation rows are
     // gathered from the token order on the fly (no separate gather launch).
     const int e = blockIdx.z;
@@ -123,7 +124,7 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
     M = min(fz.grp_off[e + 1] - r0, XR);
     if (M <= 0) return;
     if (fz.grp_rows == nullptr) X += (int64_t)r0 * ldx;
-    W += (int64_t)e * fz.grp_wstride;
+    W += (int64_t)(e / fz.grp_div) * fz.grp_wstride;
     Yv = reinterpret_cast<char*>(Yv) + (int64_t)r0 * ldy * (EPI == 2 || EPI == 3 ? 4 : 2);
   }
   const int n0 = bx * NO;

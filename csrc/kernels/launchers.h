@@ -62,8 +62,6 @@ hipError_t launch_moe_align(int* offsets, int* sorted, int* pos, const int* ids,
 hipError_t launch_moe_gather(bf16_t* xs, const bf16_t* x, const int* sorted, int n, int K, int H, hipStream_t s);
 hipError_t launch_moe_combine(bf16_t* out, const bf16_t* ys, const int* pos, const float* w, int T, int K, int H,
                               hipStream_t s);
-hipError_t launch_moe_grouped_gemm(bf16_t* Y, const bf16_t* X, const bf16_t* W, const int* offsets, int max_rows,
-                                   int E, int N, int K, hipStream_t s);
 
 hipError_t launch_decode_advance(const int64_t* out, int64_t* ids, int64_t* pos, int* ctx, int64_t* slots,
                                  const int* bt, int bt_width, int64_t* step, int64_t* tokens, int tok_stride,
@@ -85,7 +83,8 @@ struct GemmDecodeFuse {
   float eps = 0.f;
   const int* grp_off = nullptr;  // grouped (MoE) form: expert row offsets [grp_n + 1] (device)
   int64_t grp_wstride = 0;       //   elements between experts' weight matrices
-  int grp_n = 1;                 //   number of experts (grid z)
+  int grp_n = 1;                 //   number of groups (grid z)
+  int grp_div = 1;               //   groups per expert (segments of <= XR rows): W index = group / grp_div
   const int* grp_rows = nullptr; //   optional gather: X row j of the sorted order is token grp_rows[j] / grp_k
   int grp_k = 1;                 //   (X is then the un-permuted [T, K] activations; Y stays in sorted order)
   int tiled = 0;                 // W pre-packed into the kernel's tile order (gd_pack_weights)

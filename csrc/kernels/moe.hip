@@ -4,9 +4,8 @@
 //                   the T*K (token, slot) assignments (one workgroup, LDS
 //                   atomics; E <= 256);
 //   moe_gather    — x_sorted[j] = x[sorted[j] / K]   (16-byte row copies);
-//   moe_grouped_gemm — y_sorted = x_sorted @ W[e]^T for each expert segment,
-//                   device-side offsets (no host sync, hipGraph friendly),
-//                   MFMA 32x32x16 bf16, 64x64 output tiles;
+//   (the expert GEMMs themselves run on the expert-streaming grouped decode GEMM,
+//    gemm_decode.hip, or per expert on hipBLASLt for large prefills: src/ops moe_apply);
 //   moe_combine   — out[t] = sum_k w[t,k] * y_sorted[pos[t*K+k]].
 #include "common.h"
 #include "launchers.h"
@@ -229,66 +228,6 @@ hipError_t launch_moe_combine_residual(float* ssp, bf16_t* resid, int64_t rstrid
   return hipGetLastError();
 }
 
-// Grouped GEMM: for expert e, rows [off[e], off[e+1]) of X (M x K) times W[e] (N x K, row-major, i.e. y = x W^T).
-// Tile 64 x 64 per workgroup (4 waves, each a 32x32 quadrant), K step 32, LDS staged with a padded pitch.
-// grid = (N/64, ceil(total_rows/64) + E): blockIdx.y enumerates the 64-row tiles of all experts
-// back to back (expert e owns ceil(rows_e/64) tiles); surplus workgroups exit.
-constexpr int GG_BM = 64, GG_BN = 64, GG_BK = 32;
-constexpr int GG_PITCH = GG_BK * 2 + 16;  // bytes per LDS row (80): 16-lane b128 groups spread over slots
-
-__global__ void __launch_bounds__(256) moe_grouped_gemm_kernel(bf16_t* __restrict__ Y, const bf16_t* __restrict__ X,
-                                                               const bf16_t* __restrict__ W,
-                                                               const int* __restrict__ offsets, int E, int N, int K) {
-  __shared__ __attribute__((aligned(16))) char lds[(GG_BM + GG_BN) * GG_PITCH];
-  int e = 0, tile = blockIdx.y, r0 = 0, r1 = 0;
-  for (; e < E; ++e) {
-    r0 = offsets[e];
-    r1 = offsets[e + 1];
-    const int nt = (r1 - r0 + GG_BM - 1) / GG_BM;
-    if (tile < nt) break;
-    tile -= nt;
-  }
-  if (e >= E) return;
-  const int m0 = r0 + tile * GG_BM;
-  const int n0 = blockIdx.x * GG_BN;
-  const bf16_t* We = W + (int64_t)e * N * K;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;  // 2x2 waves of 32x32
-  f32x16_t acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  // staging: 64 rows x 32 cols bf16 = 64 x 4 chunks of 16 B per operand → one chunk each for A and B per thread
-  const int sr = tid >> 2, sc = tid & 3;
-  char* la = lds;
-  char* lb = lds + GG_BM * GG_PITCH;
-  for (int k0 = 0; k0 < K; k0 += GG_BK) {
-    const int arow = m0 + sr;
-    uint4 av = arow < r1 ? *reinterpret_cast<const uint4*>(X + (int64_t)arow * K + k0 + sc * 8) : make_uint4(0, 0, 0, 0);
-    uint4 bv = *reinterpret_cast<const uint4*>(We + (int64_t)(n0 + sr) * K + k0 + sc * 8);
-    __syncthreads();
-    *reinterpret_cast<uint4*>(la + sr * GG_PITCH + sc * 16) = av;
-    *reinterpret_cast<uint4*>(lb + sr * GG_PITCH + sc * 16) = bv;
-    __syncthreads();
-    const int h = lane >> 5, rr = lane & 31;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      // A: rows of X (M), B: rows of W (N) — both are "row-major along K" so each lane reads 16 contiguous bytes.
-      const bf16x8_t a =
-          __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(la + (32 * wm + rr) * GG_PITCH + (2 * kk + h) * 16));
-      const bf16x8_t b =
-          __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(lb + (32 * wn + rr) * GG_PITCH + (2 * kk + h) * 16));
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
-    }
-  }
-  // C layout: col (n) = lane&31, row (m) = (r&3) + 8(r>>2) + 4h
-  const int h = lane >> 5, col = n0 + 32 * wn + (lane & 31);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = m0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * h;
-    if (row < r1) Y[(int64_t)row * N + col] = f2bf(acc[r]);
-  }
-}
-
 hipError_t launch_topk_softmax(float* w, int* ids, const bf16_t* gating, int T, int E, int K, bool renorm,
                                hipStream_t s) {
   if (T == 0) return hipSuccess;
@@ -319,13 +258,5 @@ hipError_t launch_moe_combine(bf16_t* out, const bf16_t* ys, const int* pos, con
   return hipGetLastError();
 }
 
-hipError_t launch_moe_grouped_gemm(bf16_t* Y, const bf16_t* X, const bf16_t* W, const int* offsets, int max_rows,
-                                   int E, int N, int K, hipStream_t s) {
-  if (max_rows == 0) return hipSuccess;
-  if (N % GG_BN || K % GG_BK) return hipErrorInvalidValue;
-  dim3 grid(N / GG_BN, (max_rows + GG_BM - 1) / GG_BM + E);
-  hipLaunchKernelGGL(moe_grouped_gemm_kernel, grid, dim3(256), 0, s, Y, X, W, offsets, E, N, K);
-  return hipGetLastError();
-}
 
 }  // namespace die

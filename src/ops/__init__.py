@@ -425,6 +425,14 @@ def decode_tile(n: int, k: int, mode: int, bucket: int = 32, max_sk: int = 8):
             return (*gd_tile(c[0]), c[1])
         wr, sk = _cfg_for(n, k, {4: 1}.get(mode, mode), max_sk)
         return (*gd_tile(wr), sk)
+    return _generic_tile(n, k, mode, bucket, max_sk)
+
+
+def _generic_tile(n: int, k: int, mode: int, bucket: int, max_sk: int = 8):
+    """The (wr, kc, sk) tile that exists for `bucket` activation rows and brings the grid closest to 256
+    workgroups (one per CU)."""
+    import math
+
     best, score = None, 1e9
     for wr, kc in _GENERIC_TILES:
         cols = wr // 2 if mode in (1, 4) else wr
@@ -593,27 +601,30 @@ def moe_apply(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, w: torch.Ten
     offsets, sorted_idx, pos = moe_align(ids, groups)
     # rows of the extra groups are never computed: zero them so that weight 0 x row stays 0
     ys = (torch.zeros if groups > e else torch.empty)(t * k, hdim, dtype=x.dtype, device=x.device)
-    tiles = _moe_decode_tiles(hdim, inter, t) if t <= MOE_DECODE_MAX_T and x.is_contiguous() else None
-    if tiles is not None:
+    x = x.contiguous()
+    tiles = _moe_decode_tiles(hdim, inter, t)
+    if tiles is not None and t <= MOE_DECODE_MAX_T:
         # decode: every expert's weights streamed once by the weight-streaming kernel, its routed
         # tokens (<= t, so the activation image of the step's row bucket holds any expert's group)
         # riding along, gathered from x by the kernel itself through the sorted order; SiLU*mul
         # fused; idle experts read nothing
         (wr1, kc1), (wr2, kc2) = tiles
         a = torch.empty(t * k, inter, dtype=x.dtype, device=x.device)
-        kern.gemm_decode_grouped(a, x, w13, offsets, 1, wr1, kc1, sorted_idx, k, t)
-        kern.gemm_decode_grouped(ys, a, w2, offsets, 0, wr2, kc2, _NO_ROWS(x.device), 1, t)
+        kern.gemm_decode_grouped(a, x, w13, offsets, 1, wr1, kc1, sorted_idx, k, t, 1)
+        kern.gemm_decode_grouped(ys, a, w2, offsets, 0, wr2, kc2, _NO_ROWS(x.device), 1, t, 1)
         if residual is not None:  # combine + residual add + next-norm statistics in one launch
             kern.moe_combine_residual(ssp, residual, ys, pos, w)
             return residual
         out = torch.empty_like(x)
         kern.moe_combine(out, ys, pos, w)
         return out
-    xs = torch.empty(t * k, hdim, dtype=x.dtype, device=x.device)
-    kern.moe_gather(xs, x, sorted_idx, k)
-    if t >= MOE_LIBRARY_MIN_TOKENS and not torch.cuda.is_current_stream_capturing():
+    seg_tiles = _moe_decode_tiles(hdim, inter, MOE_DECODE_MAX_T)
+    capturing = torch.cuda.is_current_stream_capturing()
+    if (t >= MOE_LIBRARY_MIN_TOKENS or seg_tiles is None) and not capturing:
         # prefill: the per-expert groups are thousands of rows — hipBLASLt GEMMs per expert at
-        # ~1.5 PF/s beat the device-offset grouped kernel; costs one host read of the offsets
+        # ~1.5 PF/s; costs one host read of the offsets per layer
+        xs = torch.empty(t * k, hdim, dtype=x.dtype, device=x.device)
+        kern.moe_gather(xs, x, sorted_idx, k)
         off = offsets.tolist()
         for ei in range(e):
             a0, a1 = off[ei], off[ei + 1]
@@ -621,10 +632,20 @@ def moe_apply(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, w: torch.Ten
                 act = silu_and_mul(torch.nn.functional.linear(xs[a0:a1], w13[ei]))
                 torch.nn.functional.linear(act, w2[ei], out=ys[a0:a1])
     else:
-        h = torch.empty(t * k, w13.shape[1], dtype=x.dtype, device=x.device)
-        kern.moe_grouped_gemm(h, xs, w13, offsets)
-        a = silu_and_mul(h)
-        kern.moe_grouped_gemm(ys, a, w2, offsets)
+        # between the decode path and the library path (and under graph capture): the expert-streaming
+        # grouped GEMM with each expert's rows cut into segments of <= 128 (offsets built on the device,
+        # no host read); an expert with r rows streams its weights ceil(r / 128) times
+        if seg_tiles is None:
+            raise ValueError(f"MoE shapes hidden={hdim} inter={inter} do not tile the grouped decode GEMM "
+                             "(needed under graph capture)")
+        (wr1, kc1), (wr2, kc2) = seg_tiles
+        segs = (t + MOE_DECODE_MAX_T - 1) // MOE_DECODE_MAX_T
+        j = torch.arange(segs, device=x.device, dtype=torch.int32) * MOE_DECODE_MAX_T
+        off_v = torch.minimum(offsets[:-1, None] + j[None, :], offsets[1:, None]).reshape(-1)
+        off_v = torch.cat([off_v, offsets[-1:]]).to(torch.int32).contiguous()
+        a = torch.empty(t * k, inter, dtype=x.dtype, device=x.device)
+        kern.gemm_decode_grouped(a, x, w13, off_v, 1, wr1, kc1, sorted_idx, k, MOE_DECODE_MAX_T, segs)
+        kern.gemm_decode_grouped(ys, a, w2, off_v, 0, wr2, kc2, _NO_ROWS(x.device), 1, MOE_DECODE_MAX_T, segs)
     out = torch.empty_like(x)
     kern.moe_combine(out, ys, pos, w)
     if residual is not None:
@@ -648,17 +669,16 @@ def _moe_decode_tiles(hdim: int, inter: int, t: int):
     """((wr, kc) of the gate/up grouped GEMM, (wr, kc) of the down one) for a decode step of t tokens, or
     None when the shapes do not tile. Up to 32 rows: round 1's measured choice (gate/up as the dense
     gate/up shape, down wr 64 / 32 at a 256-wide K slot); above, the row bucket's generic tile."""
-    if hdim % 64 or inter % 64:
+    if hdim % 32 or inter % 32:
         return None
     if t <= 32:
         wr1 = _cfg_for(inter, hdim, 1)[0]
-        if hdim % 256 or inter % 256 or inter % (wr1 // 2):
-            return None
-        return gd_tile(wr1), gd_tile(64)
-    try:
+        if not (hdim % 256 or inter % 256 or inter % (wr1 // 2) or hdim % 64):
+            return gd_tile(wr1), gd_tile(64)
+    try:  # the row bucket's generic tiles (also for small shards, e.g. experts split under TP)
         b = _bucket(t)
-        wr1, kc1, _ = decode_tile(inter, hdim, 1, b, max_sk=1)
-        wr2, kc2, _ = decode_tile(hdim, inter, 0, b, max_sk=1)
+        wr1, kc1, _ = _generic_tile(inter, hdim, 1, b, max_sk=1)
+        wr2, kc2, _ = _generic_tile(hdim, inter, 0, b, max_sk=1)
     except ValueError:
         return None
     return (wr1, kc1), (wr2, kc2)
