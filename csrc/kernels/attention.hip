@@ -731,9 +731,9 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
     char* fa = smem + 2 * V3_BUF;            // FUSED staging (merge area, idle at a task start)
     const int frows = fz.sk * (G + 2);       // slab rows: [s][q heads..., k, v] x 128 fp32
     const int fs_off = ((frows + 1) / 2) * 1024;
-    // Issue order: the prologue's small operands first, then chunk c0 and (if any) chunk c0+1, so the
-    // prologue (FUSED: slab sum, norm scale, RoPE, KV write) runs while both chunks stream in; only a
-    // counted vmcnt separates them (the chunks stay in flight).
+    // Issue order: the prologue's small operands first, then chunk c0, so the prologue (FUSED: slab
+    // sum, norm scale, RoPE, KV write) runs while the chunk streams in; only a counted vmcnt separates
+    // them (the chunk stays in flight).
     if constexpr (FUSED) {
       if (!(dbg & 2)) {
         const float* srow = fz.slab + (int64_t)seq * fz.width;
@@ -759,18 +759,16 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
         glds16(qb + qr * D + (lane & 15) * 8, smem + V3_CHUNK + i * 1024);
       }
     }
+    // chunk c0+1 is issued only after the prologue (in the loop below): with every workgroup asking for
+    // two 64 KiB chunks at once the memory system interleaves them and the first lands late
+    // (micro_attn_timeline: span 23.3 -> 22.0-22.6 us; bench decode 2.33 -> 2.305-2.32 s per wave)
     issue(c0, 0);
-    const bool two = c0 + 1 < c1;
-    if (two) issue(c0 + 1, 1);
     State st;
     init_state(st);
     bf16x8_t qf[8];
     bf16_t nk0 = 0, nk1 = 0, nv = 0;  // FUSED: the new token's rotated key pair / value element
     if constexpr (FUSED) {
-      if (two)
-        wait_vm<32>();  // the prologue operands landed; chunks c0 and c0+1 stay in flight
-      else
-        wait_vm<16>();
+      wait_vm<16>();  // the prologue operands landed; chunk c0 stays in flight
       __builtin_amdgcn_s_barrier();
       // r = rsqrt(mean(h^2) + eps) of this sequence's row
       float ssum = 0.f;
@@ -809,7 +807,7 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
     for (int c = c0; c < c1; ++c) {
       const int b = (c - c0) & 1;
       if (c + 1 < c1) {
-        if (c > c0) issue(c + 1, b ^ 1);
+        issue(c + 1, b ^ 1);
         wait_vm<16>();  // chunk c (and the query rows) landed; chunk c+1 stays in flight
       } else {
         wait_vm<0>();
