@@ -302,7 +302,7 @@ class PagedKVCache:
     C++ :class:`BlockManager`; ``get/set/delete`` operate on *prefix hashes*
     (hash of a full block of token ids chained with its parent's hash) so a
     cached prompt prefix can be looked up like any other cache key.
-    The device tensors are owned by :class:`src.engine.kv_pool.KVPool`.
+    The device tensors are owned by :class:`src.engine.model_runner.KVPool`.
     """
 
     def __init__(self, num_blocks: int, block_size: int, enable_prefix_caching: bool = True,

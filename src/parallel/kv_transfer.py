@@ -271,7 +271,7 @@ class IPCSender:
 
 
 def packet_meta(p: KVPacket) -> Dict[str, Any]:
-    """The packet without its KV payload (the IPC path ships the payload by DMA)."""
+    """The packet without its KV payload (the IPC path writes the payload into the landing zone)."""
     return {"request_id": p.request_id, "prompt_ids": p.prompt_ids, "first_token": p.first_token,
             "shape": list(p.kv.shape), "block_size": p.block_size, "sampling": p.sampling, "ttft_ms": p.ttft_ms}
 
