@@ -448,8 +448,12 @@ class CausalLM:
         # area (V3_MERGE_BYTES): at most 50 rows
         g = max(1, self.hq // self.hkv)
         qkv = ops.decode_tile(self.layers[0].qkv.shape[0], h, 2, b, max_sk=max(1, 50 // (g + 2)))
-        o = ops.decode_tile(h, self.hq * d, 3, b)
-        down = ops.decode_tile(h, self.inter, 3, b) if not self.arch.is_moe else None
+        if self.tp.enabled:  # row-parallel o / down: bf16 partial sums (mode 0) for the all-reduce
+            o = ops.decode_tile(h, self.hq * d, 0, b)
+            down = ops.decode_tile(h, self.inter, 0, b) if not self.arch.is_moe else None
+        else:                # residual-updating split-K (mode 3)
+            o = ops.decode_tile(h, self.hq * d, 3, b)
+            down = ops.decode_tile(h, self.inter, 3, b) if not self.arch.is_moe else None
         gu = ops.decode_tile(self.inter, h, 4, b)[:2] if not self.arch.is_moe else None
         return {"qkv": qkv, "o": o, "down": down, "gate_up": gu}
 
@@ -460,8 +464,8 @@ class CausalLM:
             p = self.decode_plan(b)
             need.add(("qkv", *p["qkv"][:2]))
             need.add(("gate_up", *p["gate_up"][:2]))
-            if not self.tp.enabled:
-                need.add(("o", *p["o"][:2]))
+            need.add(("o", *p["o"][:2]))      # under TP: the row-parallel shards, plain bf16 tiles
+            if p["down"] is not None:
                 need.add(("down", *p["down"][:2]))
         return need
 
@@ -475,8 +479,14 @@ class CausalLM:
             return False
         if not (self.device.type == "cuda" and ops.native_available()):
             return False
-        need = self._packed_layouts(buckets)
         lw0 = self.layers[0]
+
+        def tiles(name, wr, kc):  # the tile covers the (shard's) weight exactly
+            rows, k = getattr(lw0, name).shape
+            silu = name == "gate_up"
+            return k % kc == 0 and (rows // 2 if silu else rows) % (wr // 2 if silu else wr) == 0
+
+        need = {t for t in self._packed_layouts(buckets) if tiles(*t)}
         extra = sum(getattr(lw0, name).numel() * 2 for name, _, _ in need) * len(self.layers)
         total = torch.cuda.get_device_properties(self.device).total_memory
         if self.weight_bytes() + extra > total // 2:
@@ -570,9 +580,9 @@ class CausalLM:
                 wgu, tg = tw(lw, "gate_up", wg, kg)
                 if self.tp.enabled:  # row-parallel partial sums -> all-reduce -> residual + statistics (one
                     # launch on the one-shot IPC path, see TPContext.all_reduce_residual)
-                    self.tp.all_reduce_residual(ops.linear(attn, lw.o), h, ssp_a)
+                    self.tp.all_reduce_residual(self._row_parallel(attn, lw, "o", plan), h, ssp_a)
                     act = ops.linear_silu_mul_rownorm(h, wgu, ssp_a, eps, wg, tiled=tg, kc=kg)
-                    self.tp.all_reduce_residual(ops.linear(act, lw.down), h, ssp_b)
+                    self.tp.all_reduce_residual(self._row_parallel(act, lw, "down", plan), h, ssp_b)
                 else:
                     wdn_, kd, sd = plan["down"]
                     wo_t, to_ = tw(lw, "o", wo, ko)
@@ -582,6 +592,14 @@ class CausalLM:
                     ops.linear_slab_residual(act, wd_t, h, ssp_b, sc["cnt_b"], wdn_, sd, tiled=td_, kc=kd)
             ssp_prev = ssp_b
         return ops.rms_norm(h, self.norm, eps)
+
+    @staticmethod
+    def _row_parallel(x: torch.Tensor, lw, name: str, plan: dict) -> torch.Tensor:
+        """TP decode: this rank's partial sum of a row-parallel projection, on its tile-order copy when
+        one was packed for the step's row bucket (else the row-major weight)."""
+        wr, kc = plan[name][:2]
+        t = lw.tiled.get((name, wr, kc))
+        return ops.linear(x, getattr(lw, name)) if t is None else ops.linear_tiled(x, t, wr, kc)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         logits = ops.linear(hidden, self.lm_head)

@@ -466,6 +466,11 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
     return torch.nn.functional.linear(x, w, out=out) if out is not None else torch.nn.functional.linear(x, w)
 
 
+def linear_tiled(x: torch.Tensor, w: torch.Tensor, wr: int, kc: int) -> torch.Tensor:
+    """y = x @ w^T (bf16, decode sizes) with w packed by gd_pack_weights for the (wr, kc) tile."""
+    return gemm_decode(x, w, 0 | 32, wr, 1, kc=kc)
+
+
 def linear_slab(x: torch.Tensor, w: torch.Tensor, sk: Optional[int] = None, wr: Optional[int] = None,
                 tiled: bool = False, kc: Optional[int] = None) -> torch.Tensor:
     """fp32 split-K slabs [sk, M, N] of x @ w^T (decode sizes only); the
