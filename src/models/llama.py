@@ -10,7 +10,7 @@ Per decoder layer (T = tokens of the step):
     o   = a @ Wo^T   (+ all_reduce over RCCL if TP)     hipBLASLt
     x   = fused_add_rms_norm(o, residual, ln2)          HIP
     Llama:   d = silu_and_mul(x @ Wgu^T) @ Wd^T          hipBLASLt + HIP
-    Mixtral: d = moe_forward(x, router)                  HIP routing + MFMA grouped GEMM
+    Mixtral: d = moe_forward(x, router)                  HIP routing + expert-streaming grouped GEMM
     (+ all_reduce if TP)
 
 Weights are stored pre-fused ([q|k|v] and [gate|up]) so each projection is one

@@ -185,7 +185,7 @@ def scatter_blocks(pool: torch.Tensor, ids: torch.Tensor, buf: torch.Tensor) -> 
 
 DECODE_GEMM_MAX_M = 128   # weight-streaming decode GEMM / fused decode path (gemm_decode.hip)
 # expert-streaming grouped decode GEMM up to this many tokens (<= 128 rows per expert: 16/32/64/128-row
-# images); DIE_MOE_DECODE_MAX_T=32 restores round 1's limit (above it: the tiled grouped GEMM) for A/B
+# images); DIE_MOE_DECODE_MAX_T=32 restores round 1's limit for A/B (above it: <= 128-row segments)
 MOE_DECODE_MAX_T = min(128, int(os.environ.get("DIE_MOE_DECODE_MAX_T", "128")))
 SSP_LD = 128              # row stride of the norm-statistics arrays [tiles, SSP_LD]
 
