@@ -154,6 +154,7 @@ class Scheduler:
     def schedule(self, now: Optional[float] = None) -> SchedulerOutput:
         now = time.perf_counter() if now is None else now
         out = SchedulerOutput()
+        self.defer_deadline = None  # set again below only if this step holds new prompts back
         budget = self.cfg.max_num_batched_tokens
         self._resumed_now = set()
         # 0) resume swapped-out sequences first (FIFO); while one is still parked, admit nothing new
