@@ -248,12 +248,15 @@ __device__ __forceinline__ const bf16_t* kv_row(const bf16_t* cache, const int* 
 
 using namespace attn;
 
-// grid = (q tiles, num_seqs, hkv); block = 256 (4 waves); dynamic LDS = 2 * NS * KV_TILE.
-// NS: 32-key sub-tiles per pipeline stage (one barrier and one round of global loads per stage):
-// NS = 2 halves the barriers and doubles the bytes in flight per round; 2 x 37 KiB stages still let
-// two workgroups share a CU's 160 KiB.
-template <int G, int NS>
-__global__ void __launch_bounds__(256, 2) attn_prefill_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ q,
+// grid = (q tiles, num_seqs, hkv); block = 64 NW (NW waves, 32 query rows each); dynamic LDS =
+// 2 * NS * KV_TILE. NS: 32-key sub-tiles per pipeline stage (one barrier and one round of global loads
+// per stage): NS = 2 halves the barriers and doubles the bytes in flight per round.
+// NW: every key / value byte staged into LDS is used by NW x 32 query rows, so L2 -> LDS traffic per
+// FLOP falls as 1 / NW. At NW = 4 (two workgroups per CU) the staging skeleton alone — loads, LDS
+// writes, barriers, no math — took 423 of 931 us at 4 x 4,096 (about 10 TB/s of L2 reads); NW = 8 (one
+// 512-thread workgroup per CU, the same 8 waves) halves that traffic.
+template <int G, int NS, int NW>
+__global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ q,
                                                            int64_t q_stride, const bf16_t* __restrict__ k_cache,
                                                            const bf16_t* __restrict__ v_cache,
                                                            const int* __restrict__ block_tables, int bt_stride,
@@ -261,7 +264,7 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(bf16_t* __restrict
                                                            const int* __restrict__ ctx_lens, int hq, int hkv,
                                                            int block_size, float scale_log2) {
   constexpr int TPW = 32 / G;   // tokens per wave
-  constexpr int TPB = 4 * TPW;  // tokens per workgroup
+  constexpr int TPB = NW * TPW;  // tokens per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int seq = blockIdx.y, kvh = blockIdx.z;
   const int qbeg = cu_q[seq], qlen = cu_q[seq + 1] - qbeg;
@@ -290,43 +293,38 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(bf16_t* __restrict
   State st;
   init_state(st);
 
-  // staging role: keys kr + 16 i of the stage, 16-byte chunk c
+  // staging role: keys kr + RPP i of the stage (RPP = rows per pass of the whole workgroup), 16-byte
+  // chunk c. Two register sets (A, B) hold the stages two and one ahead of the one being computed, so a
+  // stage's L2 round trip is hidden behind two stages of compute. The sets are native vectors (uint4
+  // struct copies became memcpys through scratch) indexed through static_for (compile-time indices).
+  constexpr int RPP = 4 * NW, NP = ST / RPP;
+  static_assert(ST % RPP == 0 && KT % RPP == 0, "a pass must not straddle two 32-key sub-tiles");
   const int kr = tid >> 4, c = tid & 15;
-  uint4 kreg[2 * NS], vreg[2 * NS];
-  auto load_tile = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < 2 * NS; ++i) {
-      const int key = kt * ST + kr + 16 * i;
-      // keys 16i .. 16i+15 of the stage share one block (block_size is a multiple of 16): the
-      // block id is wave-uniform, read by a scalar load instead of a per-lane dependent load
-      const int kb = __builtin_amdgcn_readfirstlane(min(kt * ST + 16 * i, kv_end - 1) / block_size);
-      const int64_t blk = bt[kb];
-      const int64_t roff = ((blk * hkv + kvh) * block_size + key % block_size) * D + c * 8;
-      if (key < kv_end) {
-        kreg[i] = *reinterpret_cast<const uint4*>(k_cache + roff);
-        vreg[i] = *reinterpret_cast<const uint4*>(v_cache + roff);
-      } else {
-        kreg[i] = make_uint4(0, 0, 0, 0);
-        vreg[i] = make_uint4(0, 0, 0, 0);
-      }
-    }
+  u32x4_t kA[NP], vA[NP], kB[NP], vB[NP];
+  auto load_one = [&](int kt, auto I, u32x4_t* kreg, u32x4_t* vreg) __attribute__((always_inline)) {
+    constexpr int i = decltype(I)::value;
+    const int key = kt * ST + kr + RPP * i;
+    // a wave stages 4 consecutive keys (4-aligned, block_size is a multiple of 16), all in one block: the
+    // block id is wave-uniform, read by a scalar load instead of a per-lane dependent load. Keys past
+    // kv_end re-read row kv_end - 1 of the same block: finite values the causal mask zeroes, and no
+    // branch, so the wait counter stays exact with two sets in flight.
+    const int kb = __builtin_amdgcn_readfirstlane(min(kt * ST + RPP * i + (kr & ~3), kv_end - 1) / block_size);
+    const int64_t blk = bt[kb];
+    const int64_t roff = ((blk * hkv + kvh) * block_size + min(key, kv_end - 1) % block_size) * D + c * 8;
+    kreg[i] = *reinterpret_cast<const u32x4_t*>(k_cache + roff);
+    vreg[i] = *reinterpret_cast<const u32x4_t*>(v_cache + roff);
   };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 2 * NS; ++i) {
-      char* kl = smem + (buf * NS + i / 2) * KV_TILE;  // sub-tile i / 2 of the stage
-      char* vl = kl + K_TILE;
-      *reinterpret_cast<uint4*>(kl + (kr + 16 * (i & 1)) * K_PITCH + c * 16) = kreg[i];
-      *reinterpret_cast<uint4*>(vl + (kr + 16 * (i & 1)) * V_PITCH + c * 16) = vreg[i];
-    }
+  auto store_one = [&](int buf, auto I, const u32x4_t* kreg, const u32x4_t* vreg) __attribute__((always_inline)) {
+    constexpr int i = decltype(I)::value;
+    constexpr int ks = RPP * i;                                // first key of the pass in the stage
+    char* kl = smem + (buf * NS + ks / KT) * KV_TILE;  // its 32-key sub-tile
+    char* vl = kl + K_TILE;
+    *reinterpret_cast<u32x4_t*>(kl + (ks % KT + kr) * K_PITCH + c * 16) = kreg[i];
+    *reinterpret_cast<u32x4_t*>(vl + (ks % KT + kr) * V_PITCH + c * 16) = vreg[i];
   };
-
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < ntiles) load_tile(kt + 1);
+#define DIE_LOAD_STAGE(kt, K, V) static_for<NP>([&](auto I) { load_one(kt, I, K, V); })
+#define DIE_STORE_STAGE(buf, K, V) static_for<NP>([&](auto I) { store_one(buf, I, K, V); })
+  auto compute = [&](int kt, int cur) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
       const int kb0 = kt * ST + j * KT;
@@ -340,9 +338,33 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(bf16_t* __restrict
         pv_lds(kl + K_TILE, s, st, lane);
       }
     }
-    if (kt + 1 < ntiles) store_tile(cur ^ 1);
-    __syncthreads();
+  };
+
+  // stage s lives in register set A (s even) or B (s odd), then in LDS buffer s & 1
+  DIE_LOAD_STAGE(0, kA, vA);
+  DIE_LOAD_STAGE(min(1, ntiles - 1), kB, vB);  // past the last stage: a harmless re-read, never stored
+  DIE_STORE_STAGE(0, kA, vA);
+  __syncthreads();
+  // the per-stage barrier orders the LDS writes and reads only: no vmcnt(0) (a __syncthreads here would
+  // drain the prefetch that is meant to stay in flight across it)
+  auto stage_barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+#pragma unroll 1
+  for (int kt = 0; kt < ntiles; kt += 2) {
+    DIE_LOAD_STAGE(min(kt + 2, ntiles - 1), kA, vA);  // set A is free: stage kt is in LDS buffer 0
+    compute(kt, 0);
+    if (kt + 1 < ntiles) DIE_STORE_STAGE(1, kB, vB);       // buffer 1 was last read two stages ago
+    stage_barrier();
+    if (kt + 1 >= ntiles) break;
+    DIE_LOAD_STAGE(min(kt + 3, ntiles - 1), kB, vB);
+    compute(kt + 1, 1);
+    if (kt + 2 < ntiles) DIE_STORE_STAGE(0, kA, vA);
+    stage_barrier();
   }
+#undef DIE_LOAD_STAGE
+#undef DIE_STORE_STAGE
 
   if (row_valid) {
     const float inv = 1.f / st.l;
@@ -1008,13 +1030,21 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
   if (head_dim != D || hq % hkv || block_size % 16) return hipErrorInvalidValue;
   const int G = hq / hkv;
   const float sl2 = scale * 1.4426950408889634f;
-  const int tpb = 4 * (32 / (G > 32 ? 32 : G));
-  dim3 grid((max_q_len + tpb - 1) / tpb, num_seqs, hkv), block(256);
+  static const int nw = [] {
+    const char* e = getenv("DIE_PF_NW");
+    return e && atoi(e) == 4 ? 4 : 8;
+  }();
+  const int tpb = nw * (32 / (G > 32 ? 32 : G));
+  dim3 grid((max_q_len + tpb - 1) / tpb, num_seqs, hkv), block(64 * nw);
   const size_t lds = 2 * 2 * KV_TILE;
 #define DIE_PF(GG)                                                                                             \
   case GG:                                                                                                     \
-    hipLaunchKernelGGL((attn_prefill_kernel<GG, 2>), grid, block, lds, s, out, q, q_stride, k_cache, v_cache,   \
-                       block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2);                     \
+    if (nw == 8)                                                                                               \
+      hipLaunchKernelGGL((attn_prefill_kernel<GG, 2, 8>), grid, block, lds, s, out, q, q_stride, k_cache,      \
+                         v_cache, block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2);          \
+    else                                                                                                       \
+      hipLaunchKernelGGL((attn_prefill_kernel<GG, 2, 4>), grid, block, lds, s, out, q, q_stride, k_cache,      \
+                         v_cache, block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2);          \
     break;
   switch (G) {
     DIE_PF(1)

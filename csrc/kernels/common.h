@@ -18,6 +18,7 @@ typedef uint16_t bf16_t;  // storage type for bfloat16
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;   // MFMA A/B fragment
 typedef __attribute__((ext_vector_type(4))) short short4_t;
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;      // 16-byte register staging
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;   // 32x32 MFMA accumulator
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;     // 16x16 MFMA accumulator
 
@@ -59,6 +60,18 @@ __device__ __forceinline__ float xor32_max(float x) {
 __device__ __forceinline__ float xor32_sum(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// f(IntC<0>{}) ... f(IntC<N - 1>{}): a loop unrolled by the front end, so
+// register arrays indexed by the constant are split into VGPRs before any optimisation pass runs
+template <int I> struct IntC {
+  static constexpr int value = I;
+};
+template <int N, int I = 0, typename F> __device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(IntC<I>{});
+    static_for<N, I + 1>(f);
+  }
 }
 
 __device__ __forceinline__ uint4 pack8(const float* f) {
