@@ -86,6 +86,9 @@ class EngineConfig:
     # decode steps replayed back to back on the GPU per host round trip when nothing is waiting
     # for admission (inputs advanced on the device; see src/engine/model_runner.py decode_multi)
     decode_window: int = 8
+    # queue the next decode window behind the running one while the batch is unchanged, so the GPU
+    # does not idle while the host applies a window's tokens (ModelRunner.decode_continue)
+    async_decode: bool = True
     # KV-pool exhaustion during decode: "recompute" drops the victim's KV and re-prefills it later;
     # "swap" copies its blocks to pinned host memory and scatters them back on resume (no
     # recompute); "auto" swaps sequences with at least `swap_min_tokens` of context and recomputes

@@ -191,13 +191,27 @@ class LLMEngine:
             self._complete(seq)
 
     def has_work(self) -> bool:
-        return self.scheduler.has_work()
+        return self.scheduler.has_work() or self.runner.inflight is not None
 
     # ----------------------------------------------------------------- step
     def step(self) -> List[Sequence]:
         """One engine iteration. Returns the sequences that finished in it."""
-        out: SchedulerOutput = self.scheduler.schedule()
         finished: List[Sequence] = []
+        if self.runner.inflight is not None:
+            # a decode window is queued on the GPU: queue the next one behind it when the batch is
+            # unchanged (nothing waiting, nobody finishing by length), then apply its tokens while the
+            # GPU runs on; otherwise apply them and schedule as usual
+            seqs, pending = self.runner.inflight_batch()
+            t0 = time.perf_counter()
+            toks_k = self.runner.decode_continue(self._continuation_window(seqs, pending))
+            now = time.perf_counter()
+            self.stats["decode_time"] += now - t0
+            self._apply_window(seqs, toks_k, finished)
+            if self.runner.inflight is not None:
+                self.stats["queued_windows"] = self.stats.get("queued_windows", 0) + 1
+                self.stats["steps"] += 1
+                return finished
+        out: SchedulerOutput = self.scheduler.schedule()
         for s in out.preempted:
             if s.status == SeqStatus.FINISHED:  # rejected at admission
                 s.finish_time = time.perf_counter()
@@ -234,17 +248,16 @@ class LLMEngine:
                 self._append(seq, tok, finished)
         else:
             k = self._decode_window(out.decode)
-            toks_k = self.runner.decode_multi(out.decode, k) if k > 1 else [self.runner.decode(out.decode)]
+            if k > 1:
+                toks_k = self.runner.decode_multi(out.decode, k, self._continuation_window(out.decode, k))
+                if self.runner.inflight is not None:
+                    self.stats["queued_windows"] = self.stats.get("queued_windows", 0) + 1
+            else:
+                toks_k = [self.runner.decode(out.decode)]
             now = time.perf_counter()
             self.stats["decode_time"] += now - t0
             self._step_est = 0.8 * self._step_est + 0.2 * (now - t0) / max(1, len(toks_k))
-            for toks in toks_k:
-                for seq, tok in zip(out.decode, toks):
-                    if seq.status == SeqStatus.FINISHED:  # stopped earlier in the window: discard
-                        continue
-                    seq.num_computed += 1
-                    self._append(seq, tok, finished)
-            self.stats["decode_windows"] = self.stats.get("decode_windows", 0) + 1
+            self._apply_window(out.decode, toks_k, finished)
         self.stats["steps"] += 1
         if self.cfg.kv_block_ttl_s:
             self.blocks.evict_expired()
@@ -271,6 +284,39 @@ class LLMEngine:
                 buf = host
             seq.swap_buf = buf
             self.stats["swap_out_bytes"] = self.stats.get("swap_out_bytes", 0) + buf.numel() * buf.element_size()
+
+    def _apply_window(self, seqs: List[Sequence], toks_k: List[List[int]], finished: List[Sequence]) -> None:
+        for toks in toks_k:
+            for seq, tok in zip(seqs, toks):
+                if seq.status == SeqStatus.FINISHED:  # stopped earlier in the window (or aborted): discard
+                    continue
+                seq.num_computed += 1
+                self._append(seq, tok, finished)
+        self.stats["decode_windows"] = self.stats.get("decode_windows", 0) + 1
+
+    def _continuation_window(self, seqs: List[Sequence], pending: int) -> int:
+        """Steps of a window to queue behind one of `pending` steps not yet applied (0: none). Only
+        while the batch cannot change at the boundary: nothing waiting or swapped, every running
+        sequence in the batch, none reaching max_tokens / the context limit within the queued
+        window, and KV slots for both windows reserved now. An EOS inside the queued window only
+        wastes the continuation's rows for that sequence (its tokens are discarded)."""
+        if not self.cfg.async_decode or not getattr(self.runner, "supports_multistep", False):
+            return 0
+        sch = self.scheduler
+        if sch.waiting or sch.swapped or len(sch.running) != len(seqs):
+            return 0
+        ids = {id(s) for s in seqs}
+        if any(id(s) not in ids or s.status != SeqStatus.RUNNING or s.in_prefill for s in sch.running):
+            return 0
+        k = min(int(self.cfg.decode_window),
+                min(s.sampling.max_tokens - len(s.output_ids) - pending for s in seqs),
+                min(self.max_model_len - (len(s) + pending) + 1 for s in seqs))
+        if k <= 1:
+            return 0
+        for s in seqs:
+            if not self.blocks.ensure_slots(s, len(s) + pending + k - 1):
+                return 0
+        return k
 
     def _decode_window(self, seqs: List[Sequence]) -> int:
         """How many decode steps to run before the host looks again: 1 while requests wait for

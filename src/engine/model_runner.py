@@ -93,7 +93,16 @@ class ModelRunner:
         self.h_step = torch.zeros(self.max_seqs, dtype=i64, pin_memory=pin)
         self.h_out = torch.zeros(self.max_seqs, dtype=i64, pin_memory=pin)
         self.k_max = max(1, int(getattr(cfg, "decode_window", 1)))
-        self.h_tokens = torch.zeros(self.k_max, self.max_seqs, dtype=i64, pin_memory=pin)
+        # two halves of k_max rows: a window's tokens land in one half while the next (continuation)
+        # window, already queued behind it, writes the other
+        self.h_tokens = torch.zeros(2 * self.k_max, self.max_seqs, dtype=i64, pin_memory=pin)
+        # continuation-window staging (block tables + first-step slots), double-buffered by parity: a
+        # set is rewritten only after the window that read it has been waited for
+        self.h_cbt = [torch.zeros(self.max_seqs, self.bt_width, dtype=i32, pin_memory=pin) for _ in range(2)]
+        self.h_cslots = [torch.zeros(self.max_seqs, dtype=i64, pin_memory=pin) for _ in range(2)]
+        self.h_cscratch = (torch.zeros(self.max_seqs, dtype=i64), torch.zeros(self.max_seqs, dtype=i32))
+        self._cpar = 0
+        self.inflight: Optional[Dict[str, object]] = None  # a queued window whose tokens are not yet read
         self.h_ctl = torch.zeros(2, dtype=i32, pin_memory=pin)   # [window step counter, real rows]
         # numpy views over the pinned buffers (zero-copy) for cheap bulk writes
         self.n_ids, self.n_temp, self.n_topk = self.h_ids.numpy(), self.h_temp.numpy(), self.h_topk.numpy()
@@ -114,7 +123,7 @@ class ModelRunner:
         self.d_seed = torch.zeros(self.max_seqs, dtype=i64, device=dev)
         self.d_step = torch.zeros(self.max_seqs, dtype=i64, device=dev)
         self.d_out = torch.zeros(self.max_seqs, dtype=i64, device=dev)
-        self.d_tokens = torch.zeros(self.k_max, self.max_seqs, dtype=i64, device=dev)
+        self.d_tokens = torch.zeros(2 * self.k_max, self.max_seqs, dtype=i64, device=dev)
         self.d_ctl = torch.zeros(2, dtype=i32, device=dev)
         if self.is_cuda:
             maxp = ops.decode_partials(max_model_len)
@@ -305,17 +314,22 @@ class ModelRunner:
         return self._to_host(ids, n)
 
     @torch.inference_mode()
-    def decode_multi(self, seqs: List[Sequence], k: int) -> List[List[int]]:
+    def decode_multi(self, seqs: List[Sequence], k: int, k_next: int = 0) -> List[List[int]]:
         """k decode steps for the same batch in one host round trip: the step's hipGraph ends
         with a device-side input advance (sampled ids -> next ids, positions/context/step + 1,
         next slot from the block table), so the graph is replayed k times back to back and the
         k x n sampled tokens come back in one copy. The caller has reserved KV slots for the
-        k positions. Falls back to single steps where no graph covers the batch."""
+        k positions. Falls back to single steps where no graph covers the batch.
+
+        k_next > 1 (slots reserved for k + k_next positions): a continuation window of k_next
+        steps is queued behind this one before the host waits, so the GPU runs it while the
+        caller applies this window's tokens; :meth:`decode_continue` collects it."""
         n = len(seqs)
         pad = self._pad_for(n)
         g = self.graphs.get(pad)
         if k <= 1 or g is None or not self.supports_multistep:
             return [self.decode(seqs)]
+        assert self.inflight is None, "a queued decode window must be collected first"
         k = min(k, self.k_max)
         self.n_ids[:n] = [s.last_token for s in seqs]
         self.n_ids[n:pad] = 0
@@ -330,8 +344,58 @@ class ModelRunner:
         for _ in range(k):
             g.replay()
         self.h_tokens[:k].copy_(self.d_tokens[:k], non_blocking=True)
-        torch.cuda.current_stream(self.device).synchronize()
+        if k_next > 1:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self._queue_continuation(seqs, k, k_next, base=self.k_max)
+            ev.synchronize()
+        else:
+            torch.cuda.current_stream(self.device).synchronize()
         return self.h_tokens[:k, :n].tolist()
+
+    def _queue_continuation(self, seqs: List[Sequence], pending: int, k: int, base: int) -> None:
+        """Queue k more decode steps for `seqs` behind a window of `pending` steps whose tokens the
+        host has not applied yet (len(s) excludes them). Positions, context lengths and ids are
+        already advanced on the device; the block tables (grown for the new positions) and the
+        first step's slots (the queued window's last advance read the old tables) are re-sent."""
+        n = len(seqs)
+        pad = self._pad_for(n)
+        k = min(k, self.k_max)
+        par = self._cpar
+        self._cpar ^= 1
+        hbt, hsl = self.h_cbt[par], self.h_cslots[par]
+        spos, sctx = self.h_cscratch
+        self.rt.build_decode_inputs([s.block_table for s in seqs], [len(s) + pending for s in seqs], self.bs,
+                                    spos.data_ptr(), hsl.data_ptr(), sctx.data_ptr(), hbt.data_ptr(),
+                                    self.bt_width, pad)
+        self.d_bt[:pad].copy_(hbt[:pad], non_blocking=True)
+        self.d_slots[:pad].copy_(hsl[:pad], non_blocking=True)
+        self.d_ctl[0:1].fill_(base)  # token rows [base, base + k)
+        g = self.graphs[pad]
+        for _ in range(k):
+            g.replay()
+        self.h_tokens[base:base + k].copy_(self.d_tokens[base:base + k], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self.inflight = {"seqs": list(seqs), "k": k, "base": base, "event": ev}
+
+    def inflight_batch(self):
+        """(sequences, steps) of the queued window, or None."""
+        w = self.inflight
+        return None if w is None else (w["seqs"], w["k"])
+
+    @torch.inference_mode()
+    def decode_continue(self, k_next: int = 0) -> List[List[int]]:
+        """Collect the queued window's tokens ([k][n]); first, if k_next > 1 (the caller reserved
+        the slots and the batch is unchanged), queue the next window behind it."""
+        w = self.inflight
+        assert w is not None
+        self.inflight = None
+        if k_next > 1:
+            self._queue_continuation(w["seqs"], w["k"], k_next, base=self.k_max - w["base"])
+        w["event"].synchronize()
+        b, k, n = w["base"], w["k"], len(w["seqs"])
+        return self.h_tokens[b:b + k, :n].tolist()
 
     def _exec_decode(self, n: int, pad: int) -> torch.Tensor:
         g = self.graphs.get(pad)

@@ -304,3 +304,57 @@ def test_mixed_steps_on_gpu(engine):
     for i, p in enumerate(ps):
         r, m = reference_with_margins(engine.model, p, 16)
         assert agree(got[i], r, m), (i, got[i], r, m)
+
+
+def _run_requests(eng, reqs, late=None, late_at=6):
+    res = {}
+
+    def add(i, p, sp):
+        eng.add_request(f"aw-{i}-{random.random()}", p, sp, on_finish=lambda s, i=i: res.__setitem__(i, list(s.output_ids)))
+
+    for i, (p, sp) in enumerate(reqs):
+        add(i, p, sp)
+    steps = 0
+    while eng.has_work():
+        eng.step()
+        steps += 1
+        if late is not None and steps == late_at:
+            add(len(reqs), *late)
+    return [res[i] for i in range(len(res))]
+
+
+def test_queued_decode_windows_match_synchronous():
+    """Decode windows queued behind the running one (async_decode) give exactly the tokens of
+    synchronous windows: mixed max_tokens (batch shrinks at window boundaries), a stop token hit
+    inside a queued window, windows that need new KV blocks, and a late arrival that ends the chain."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rng = random.Random(7)
+    prompts = [[rng.randrange(1, 4000) for _ in range(n)] for n in (40, 17, 90, 5, 64, 33)]
+    engs = {}
+    for mode in (False, True):
+        cfg = EngineConfig(max_num_seqs=8, max_num_batched_tokens=512, num_kv_blocks=512, max_latency_ms=0.0,
+                           graph_batch_sizes=[1, 2, 4, 8], decode_window=8, async_decode=mode)
+        engs[mode] = LLMEngine.from_preset("llama-mini", device="cuda:0", cfg=cfg, max_model_len=1024, seed=3)
+        engs[mode].eos_token_id = None
+    lens = [70, 23, 41, 64, 9, 50]
+    base = _run_requests(engs[False], [(p, SamplingParams(max_tokens=n)) for p, n in zip(prompts, lens)])
+    out = _run_requests(engs[True], [(p, SamplingParams(max_tokens=n)) for p, n in zip(prompts, lens)])
+    assert out == base
+    assert engs[True].stats.get("queued_windows", 0) > 0
+    assert engs[False].stats.get("queued_windows", 0) == 0
+    # a stop token that first appears deep in one sequence's output (inside a queued window)
+    stop = base[0][37]
+    first = base[0].index(stop)
+    reqs = [(p, SamplingParams(max_tokens=n, stop_token_ids=[stop] if i == 0 else [])) for i, (p, n) in
+            enumerate(zip(prompts, lens))]
+    b2 = _run_requests(engs[False], reqs)
+    o2 = _run_requests(engs[True], reqs)
+    assert o2 == b2 and len(o2[0]) == first + 1
+    # a prompt arriving while windows are queued: the chain ends, the prompt is admitted
+    late = (prompts[2][:30], SamplingParams(max_tokens=20))
+    b3 = _run_requests(engs[False], [(p, SamplingParams(max_tokens=n)) for p, n in zip(prompts, lens)], late)
+    o3 = _run_requests(engs[True], [(p, SamplingParams(max_tokens=n)) for p, n in zip(prompts, lens)], late)
+    assert o3 == b3 and len(o3) == len(prompts) + 1
+    # the queued windows leak no KV blocks
+    assert engs[True].blocks.bm.num_available() == engs[False].blocks.bm.num_available()
