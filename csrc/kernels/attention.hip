@@ -262,13 +262,21 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
                                                            const int* __restrict__ block_tables, int bt_stride,
                                                            const int* __restrict__ cu_q,
                                                            const int* __restrict__ ctx_lens, int hq, int hkv,
-                                                           int block_size, float scale_log2) {
+                                                           int block_size, float scale_log2, int xcd_swz) {
   constexpr int TPW = 32 / G;   // tokens per wave
   constexpr int TPB = NW * TPW;  // tokens per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int seq = blockIdx.y, kvh = blockIdx.z;
+  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (hardware id mod 8), so the
+  // q tiles of one (sequence, kv head), which all stream the same K/V, would each land on a different
+  // L2. Remap (bijectively) so that every XCD gets a contiguous run of logical ids: a group's tiles
+  // share one L2 and its K/V is fetched from HBM / MALL once per group instead of once per tile.
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int hw = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int nwg = gx * gy * gridDim.z, xq = nwg >> 3, xr = nwg & 7, xcd = hw & 7;
+  const int lid = xcd_swz ? (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (hw >> 3) : hw;
+  const int bx = lid % gx, seq = (lid / gx) % gy, kvh = lid / (gx * gy);
   const int qbeg = cu_q[seq], qlen = cu_q[seq + 1] - qbeg;
-  const int t0 = (gridDim.x - 1 - blockIdx.x) * TPB;  // heaviest (latest) tiles launch first
+  const int t0 = (gx - 1 - bx) * TPB;  // heaviest (latest) tiles of a group launch first
   if (t0 >= qlen) return;
   const int ctx = ctx_lens[seq];
   const int pos0 = ctx - qlen;
@@ -1034,6 +1042,10 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
     const char* e = getenv("DIE_PF_NW");
     return e && atoi(e) == 4 ? 4 : 8;
   }();
+  static const int xcd_swz = [] {
+    const char* e = getenv("DIE_PF_XCD");
+    return e && atoi(e) == 0 ? 0 : 1;
+  }();
   const int tpb = nw * (32 / (G > 32 ? 32 : G));
   dim3 grid((max_q_len + tpb - 1) / tpb, num_seqs, hkv), block(64 * nw);
   const size_t lds = 2 * 2 * KV_TILE;
@@ -1041,10 +1053,10 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
   case GG:                                                                                                     \
     if (nw == 8)                                                                                               \
       hipLaunchKernelGGL((attn_prefill_kernel<GG, 2, 8>), grid, block, lds, s, out, q, q_stride, k_cache,      \
-                         v_cache, block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2);          \
+                         v_cache, block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2, xcd_swz);          \
     else                                                                                                       \
       hipLaunchKernelGGL((attn_prefill_kernel<GG, 2, 4>), grid, block, lds, s, out, q, q_stride, k_cache,      \
-                         v_cache, block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2);          \
+                         v_cache, block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2, xcd_swz);          \
     break;
   switch (G) {
     DIE_PF(1)
