@@ -18,7 +18,9 @@ def main():
     nblocks = n * nb_seq + 8
     kc = torch.randn(nblocks, hkv, bs, d, device=dev, dtype=torch.bfloat16)
     vc = torch.randn(nblocks, hkv, bs, d, device=dev, dtype=torch.bfloat16)
-    bt = torch.randperm(nblocks, device=dev)[: n * nb_seq].view(n, nb_seq).to(torch.int32)
+    # DIE_MICRO_BT=seq: blocks in allocation order (what a fresh engine hands out); default: a random permutation
+    order = torch.arange(nblocks, device=dev) if os.environ.get("DIE_MICRO_BT") == "seq" else torch.randperm(nblocks, device=dev)
+    bt = order[: n * nb_seq].view(n, nb_seq).to(torch.int32)
     cu = torch.arange(0, (n + 1) * L, L, dtype=torch.int32, device=dev)
     ctx = torch.full((n,), L, dtype=torch.int32, device=dev)
     q = torch.randn(n * L, (hq + 2 * hkv) * d, device=dev, dtype=torch.bfloat16)[:, : hq * d]
