@@ -273,7 +273,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
   const int gx = gridDim.x, gy = gridDim.y;
   const int hw = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
   const int nwg = gx * gy * gridDim.z, xq = nwg >> 3, xr = nwg & 7, xcd = hw & 7;
-  const int lid = xcd_swz ? (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (hw >> 3) : hw;
+  const int lid = (xcd_swz & 1) ? (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (hw >> 3) : hw;
   const int bx = lid % gx, seq = (lid / gx) % gy, kvh = lid / (gx * gy);
   const int qbeg = cu_q[seq], qlen = cu_q[seq + 1] - qbeg;
   const int t0 = (gx - 1 - bx) * TPB;  // heaviest (latest) tiles of a group launch first
@@ -297,7 +297,9 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
   const int* bt = block_tables + (int64_t)seq * bt_stride;
 
   bf16x8_t qf[8];
-  load_q(qf, row_valid ? q + (int64_t)(qbeg + tok) * q_stride + (int64_t)head * D : nullptr, h);
+  // xcd_swz bit 1 (diagnostic): every row reads the Q row of token 0 (an L2 hit) instead of its own
+  load_q(qf, row_valid ? q + ((xcd_swz & 2) ? (int64_t)head * D : (int64_t)(qbeg + tok) * q_stride + (int64_t)head * D)
+                       : nullptr, h);
   State st;
   init_state(st);
 
@@ -374,9 +376,15 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
 #undef DIE_LOAD_STAGE
 #undef DIE_STORE_STAGE
 
-  if (row_valid) {
+  // Epilogue: O staged through LDS and stored as whole rows. Stored straight from the MFMA layout, every
+  // 8-byte lane store touched 32 rows (32 partial lines per instruction) and the store tail cost ~45 us
+  // of a 32 x 512 prefill (micro_attn_prefill_xcd_r2.txt); a row of 256 B is 16 lanes x 16 B, so each
+  // wave stores its 32 x 128 tile in 8 instructions of 4 full rows. The loop ended on a barrier that
+  // follows every wave's last LDS read, so the ring is free; each wave uses its own 32-row region.
+  if (!(xcd_swz & 4)) {  // bit 2 (diagnostic): no O store
+    constexpr int OP = 272;  // staging row pitch (bytes): 2-way conflicts at most on the b64 writes
+    char* ob = smem + wave * 32 * OP;
     const float inv = 1.f / st.l;
-    bf16_t* orow = out + (int64_t)(qbeg + tok) * hq * D + (int64_t)head * D;
 #pragma unroll
     for (int db = 0; db < 4; ++db)
 #pragma unroll
@@ -385,8 +393,19 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
         uint2 v;
         v.x = pack2(st.o[db][4 * g4 + 0] * inv, st.o[db][4 * g4 + 1] * inv);
         v.y = pack2(st.o[db][4 * g4 + 2] * inv, st.o[db][4 * g4 + 3] * inv);
-        *reinterpret_cast<uint2*>(orow + d) = v;
+        *reinterpret_cast<uint2*>(ob + row * OP + d * 2) = v;
       }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const int c16 = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = 4 * i + (lane >> 4);  // this lane's row of the wave tile
+      const int rtok = t0 + wave * TPW + r / G;
+      const uint4 v = *reinterpret_cast<const uint4*>(ob + r * OP + c16 * 16);
+      if (rtok < qlen)
+        *reinterpret_cast<uint4*>(out + (int64_t)(qbeg + rtok) * hq * D + (int64_t)(kvh * G + r % G) * D + c16 * 8) = v;
+    }
   }
 }
 
@@ -1043,8 +1062,8 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
     return e && atoi(e) == 4 ? 4 : 8;
   }();
   static const int xcd_swz = [] {
-    const char* e = getenv("DIE_PF_XCD");
-    return e && atoi(e) == 0 ? 0 : 1;
+    const char* e = getenv("DIE_PF_XCD");  // bit 0: XCD-aware order (default on); bits 1-2: diagnostics
+    return e ? atoi(e) : 1;
   }();
   const int tpb = nw * (32 / (G > 32 ? 32 : G));
   dim3 grid((max_q_len + tpb - 1) / tpb, num_seqs, hkv), block(64 * nw);
