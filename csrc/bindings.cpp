@@ -83,7 +83,7 @@ void check_cache(const Tensor& c, int64_t hkv, int64_t head_dim, const char* nam
 }
 
 void rope_and_cache(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor slot_mapping, Tensor k_cache,
-                    Tensor v_cache, int64_t hq, int64_t hkv, int64_t head_dim) {
+                    Tensor v_cache, int64_t hq, int64_t hkv, int64_t head_dim, bool rot_q) {
   DIE_CHECK_CUDA(qkv);
   DIE_CHECK_BF16(qkv);
   check_rows(qkv, "qkv");
@@ -99,11 +99,11 @@ void rope_and_cache(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor slot_ma
   TORCH_CHECK(k_cache.sizes() == v_cache.sizes(), "k/v cache shapes differ");
   DIE_HIP(die::launch_rope_and_cache(bf(qkv), qkv.stride(0), positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
                                      slot_mapping.data_ptr<int64_t>(), bf(k_cache), bf(v_cache), (int)qkv.size(0),
-                                     (int)hq, (int)hkv, (int)head_dim, (int)k_cache.size(2), cur_stream()));
+                                     (int)hq, (int)hkv, (int)head_dim, (int)k_cache.size(2), cur_stream(), rot_q));
 }
 
 void attn_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor cu_q,
-                  Tensor ctx_lens, int64_t max_q_len, int64_t hq, int64_t hkv, double scale) {
+                  Tensor ctx_lens, int64_t max_q_len, int64_t hq, int64_t hkv, double scale, Tensor cos_sin) {
   DIE_CHECK_CUDA(q);
   DIE_CHECK_BF16(q);
   DIE_CHECK_BF16(out);
@@ -122,10 +122,19 @@ void attn_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor b
   const int64_t nseq = ctx_lens.numel();
   TORCH_CHECK(cu_q.numel() >= nseq + 1 && block_tables.dim() == 2 && block_tables.size(0) >= nseq,
               "cu_q / block_tables sizes");
+  // cos_sin (optional, numel 0 = absent): [max_pos, 128] fp32; Q rows are rotated on load (unrotated q)
+  const bool rot = cos_sin.numel() > 0;
+  if (rot) {
+    DIE_CHECK_DTYPE(cos_sin, at::kFloat);
+    DIE_CHECK_CONTIG(cos_sin);
+    TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D && cos_sin.device() == q.device(),
+                "cos_sin must be [max_pos, 128] on q's device");
+  }
   DIE_HIP(die::launch_attn_prefill(bf(out), bf(q), q.stride(0), bf(k_cache), bf(v_cache),
                                    block_tables.data_ptr<int>(), (int)block_tables.size(1), cu_q.data_ptr<int>(),
                                    ctx_lens.data_ptr<int>(), (int)nseq, (int)max_q_len, (int)hq, (int)hkv, (int)D,
-                                   (int)k_cache.size(2), (float)scale, cur_stream()));
+                                   (int)k_cache.size(2), (float)scale, cur_stream(),
+                                   rot ? cos_sin.data_ptr<float>() : nullptr, rot ? (int)cos_sin.size(0) : 0));
 }
 
 // counters: int32 [>= num_seqs * hkv], zero before first use (the kernel re-arms them); an empty tensor

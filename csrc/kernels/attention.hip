@@ -262,7 +262,8 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
                                                            const int* __restrict__ block_tables, int bt_stride,
                                                            const int* __restrict__ cu_q,
                                                            const int* __restrict__ ctx_lens, int hq, int hkv,
-                                                           int block_size, float scale_log2, int xcd_swz) {
+                                                           int block_size, float scale_log2, int xcd_swz,
+                                                           const float* __restrict__ cos_sin, int n_pos) {
   constexpr int TPW = 32 / G;   // tokens per wave
   constexpr int TPB = NW * TPW;  // tokens per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -300,6 +301,26 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
   // xcd_swz bit 1 (diagnostic): every row reads the Q row of token 0 (an L2 hit) instead of its own
   load_q(qf, row_valid ? q + ((xcd_swz & 2) ? (int64_t)head * D : (int64_t)(qbeg + tok) * q_stride + (int64_t)head * D)
                        : nullptr, h);
+  if (cos_sin != nullptr && row_valid) {
+    // RoPE (neox pairs (i, i + 64)) on the Q row as it is loaded: qf[kk] holds dims 16 kk + 8 h + [0, 8)
+    // and qf[kk + 4] their partners, so the rotation is lane-local (the rope kernel skips q)
+    const float* cs = cos_sin + (int64_t)min(pos0 + tok, n_pos - 1) * D;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      float a[8], b[8], ya[8], yb[8];
+      unpack8(__builtin_bit_cast(uint4, qf[kk]), a);
+      unpack8(__builtin_bit_cast(uint4, qf[kk + 4]), b);
+      const int i0 = 16 * kk + 8 * h;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float co = cs[i0 + j], si = cs[D / 2 + i0 + j];
+        ya[j] = a[j] * co - b[j] * si;
+        yb[j] = b[j] * co + a[j] * si;
+      }
+      qf[kk] = as_frag(pack8(ya));
+      qf[kk + 4] = as_frag(pack8(yb));
+    }
+  }
   State st;
   init_state(st);
 
@@ -1052,8 +1073,9 @@ __global__ void __launch_bounds__(128) attn_decode_reduce_kernel(bf16_t* __restr
 hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, const bf16_t* k_cache,
                                const bf16_t* v_cache, const int* block_tables, int bt_stride, const int* cu_q,
                                const int* ctx_lens, int num_seqs, int max_q_len, int hq, int hkv, int head_dim,
-                               int block_size, float scale, hipStream_t s) {
+                               int block_size, float scale, hipStream_t s, const float* cos_sin, int n_pos) {
   if (num_seqs == 0 || max_q_len == 0) return hipSuccess;
+  if (cos_sin != nullptr && n_pos < 1) return hipErrorInvalidValue;
   if (head_dim != D || hq % hkv || block_size % 16) return hipErrorInvalidValue;
   const int G = hq / hkv;
   const float sl2 = scale * 1.4426950408889634f;
@@ -1072,10 +1094,10 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
   case GG:                                                                                                     \
     if (nw == 8)                                                                                               \
       hipLaunchKernelGGL((attn_prefill_kernel<GG, 2, 8>), grid, block, lds, s, out, q, q_stride, k_cache,      \
-                         v_cache, block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2, xcd_swz);          \
+                         v_cache, block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2, xcd_swz, cos_sin, n_pos);          \
     else                                                                                                       \
       hipLaunchKernelGGL((attn_prefill_kernel<GG, 2, 4>), grid, block, lds, s, out, q, q_stride, k_cache,      \
-                         v_cache, block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2, xcd_swz);          \
+                         v_cache, block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2, xcd_swz, cos_sin, n_pos);          \
     break;
   switch (G) {
     DIE_PF(1)

@@ -18,7 +18,7 @@ hipError_t launch_silu_and_mul(bf16_t* out, const bf16_t* in, int rows, int inte
 
 hipError_t launch_rope_and_cache(bf16_t* qkv, int64_t qkv_stride, const int64_t* positions, const float* cos_sin,
                                  const int64_t* slot_mapping, bf16_t* k_cache, bf16_t* v_cache, int num_tokens,
-                                 int hq, int hkv, int head_dim, int block_size, hipStream_t s);
+                                 int hq, int hkv, int head_dim, int block_size, hipStream_t s, bool rot_q = true);
 hipError_t launch_copy_blocks(bf16_t* pool, const int64_t* pairs, int num_pairs, int planes, int64_t num_blocks,
                               int64_t slab, hipStream_t s);
 hipError_t launch_move_blocks(bf16_t* pool, bf16_t* buf, const int64_t* ids, int n, int planes, int64_t num_blocks,
@@ -27,7 +27,8 @@ hipError_t launch_move_blocks(bf16_t* pool, bf16_t* buf, const int64_t* ids, int
 hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, const bf16_t* k_cache,
                                const bf16_t* v_cache, const int* block_tables, int bt_stride, const int* cu_q,
                                const int* ctx_lens, int num_seqs, int max_q_len, int hq, int hkv, int head_dim,
-                               int block_size, float scale, hipStream_t s);
+                               int block_size, float scale, hipStream_t s, const float* cos_sin = nullptr,
+                               int n_pos = 0);
 // Fused decode-attention prologue (attention.hip, attn_decode_v3_kernel<G, true>).
 struct AttnDecodeFuse {
   const float* slab = nullptr;      // qkv projection split-K slabs [sk][M][width] fp32

@@ -19,7 +19,7 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16_t* __restrict__ qk
                                                          const float* __restrict__ cos_sin,
                                                          const int64_t* __restrict__ slot_mapping,
                                                          bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
-                                                         int hq, int hkv, int block_size) {
+                                                         int hq, int hkv, int block_size, int rot_q) {
   constexpr int HALF = D / 2;
   constexpr int RC = HALF / 8;  // 8-wide rotation chunks per head
   constexpr int VC = D / 8;     // 16-byte chunks per head
@@ -28,11 +28,13 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16_t* __restrict__ qk
   const int64_t pos = positions[tok];
   const int64_t slot = slot_mapping ? slot_mapping[tok] : -1;
   const float* cs = cos_sin + pos * D;
-  const int n_rot = (hq + hkv) * RC;
+  // rot_q = 0: q is left as it is (prefill attention rotates its Q rows itself when it loads them)
+  const int h0 = rot_q ? 0 : hq;
+  const int n_rot = (hq + hkv - h0) * RC;
   const int n_items = n_rot + hkv * VC;
   for (int it = threadIdx.x; it < n_items; it += blockDim.x) {
     if (it < n_rot) {
-      const int head = it / RC, c = it % RC;
+      const int head = h0 + it / RC, c = it % RC;
       bf16_t* x = row + head * D + c * 8;
       float a[8], b[8], co[8], si[8], ya[8], yb[8];
       unpack8(*reinterpret_cast<const uint4*>(x), a);
@@ -69,17 +71,17 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16_t* __restrict__ qk
 
 hipError_t launch_rope_and_cache(bf16_t* qkv, int64_t qkv_stride, const int64_t* positions, const float* cos_sin,
                                  const int64_t* slot_mapping, bf16_t* k_cache, bf16_t* v_cache, int num_tokens,
-                                 int hq, int hkv, int head_dim, int block_size, hipStream_t s) {
+                                 int hq, int hkv, int head_dim, int block_size, hipStream_t s, bool rot_q) {
   if (num_tokens == 0) return hipSuccess;
   dim3 grid(num_tokens), block(256);
   switch (head_dim) {
     case 64:
       hipLaunchKernelGGL(rope_cache_kernel<64>, grid, block, 0, s, qkv, qkv_stride, positions, cos_sin,
-                         slot_mapping, k_cache, v_cache, hq, hkv, block_size);
+                         slot_mapping, k_cache, v_cache, hq, hkv, block_size, (int)rot_q);
       break;
     case 128:
       hipLaunchKernelGGL(rope_cache_kernel<128>, grid, block, 0, s, qkv, qkv_stride, positions, cos_sin,
-                         slot_mapping, k_cache, v_cache, hq, hkv, block_size);
+                         slot_mapping, k_cache, v_cache, hq, hkv, block_size, (int)rot_q);
       break;
     default:
       return hipErrorInvalidValue;

@@ -5,7 +5,7 @@ Per decoder layer (T = tokens of the step):
 
     x   = fused_add_rms_norm(h, residual, ln1)          HIP  (residual += h in place)
     qkv = x @ Wqkv^T                                    hipBLASLt   [T, (hq+2hkv)*128]
-    rope_and_cache(qkv → q rotated in place, k/v → paged HBM blocks)   HIP
+    rope_and_cache(k rotated, k/v → paged HBM blocks; prefill q is rotated by the attention Q load)   HIP
     a   = attn_prefill | attn_decode (paged, GQA)       HIP  (MFMA)
     o   = a @ Wo^T   (+ all_reduce over RCCL if TP)     hipBLASLt
     x   = fused_add_rms_norm(o, residual, ln2)          HIP
@@ -358,11 +358,14 @@ class CausalLM:
         d, hq, hkv = self.head_dim, self.hq, self.hkv
         qkv = ops.linear(x, lw.qkv)
         k_cache, v_cache = kv_pool[li, 0], kv_pool[li, 1]
-        ops.rope_and_cache(qkv, positions, self.cos_sin, meta.slot_mapping, k_cache, v_cache, hq, hkv, d)
+        # prefill on the GPU: q's RoPE happens in the attention kernel's Q load (no q round trip through HBM)
+        fuse_q = meta.is_prefill and qkv.is_cuda
+        ops.rope_and_cache(qkv, positions, self.cos_sin, meta.slot_mapping, k_cache, v_cache, hq, hkv, d,
+                           rot_q=not fuse_q)
         q = qkv[:, : hq * d]
         if meta.is_prefill:
             return ops.attn_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_q, meta.ctx_lens,
-                                    meta.max_q_len, hq, hkv, self.scale)
+                                    meta.max_q_len, hq, hkv, self.scale, cos_sin=self.cos_sin if fuse_q else None)
         return ops.attn_decode(q, k_cache, v_cache, meta.block_tables, meta.ctx_lens, meta.max_ctx, hq, hkv,
                                self.scale, part_o=meta.part_o, part_ml=meta.part_ml, counters=meta.attn_cnt)
 

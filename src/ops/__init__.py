@@ -73,20 +73,28 @@ def silu_and_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.T
     return out
 
 
-def rope_and_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq: int, hkv: int, head_dim: int) -> None:
+def rope_and_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq: int, hkv: int, head_dim: int,
+                   rot_q: bool = True) -> None:
+    """Rotate k (and q unless rot_q=False: prefill attention then rotates its Q rows on load, see
+    attn_prefill's cos_sin) and write k / v into the paged cache."""
     if not qkv.is_cuda:
+        assert rot_q, "the CPU reference path rotates q here"
         ref.rope_and_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq, hkv, head_dim)
         return
-    _kern().rope_and_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq, hkv, head_dim)
+    _kern().rope_and_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq, hkv, head_dim, rot_q)
 
 
 def attn_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_q_len: int, hq: int, hkv: int,
-                 scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 scale: float, out: Optional[torch.Tensor] = None, cos_sin: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Causal paged prefill attention. cos_sin ([max_pos, 128] fp32): q is NOT yet rotated, the kernel
+    applies RoPE to each Q row as it loads it (token positions ctx - q_len + i)."""
     if not q.is_cuda:
+        assert cos_sin is None, "the CPU reference path takes a rotated q"
         return ref.attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, hq, hkv, scale).reshape(q.shape[0], -1)
     if out is None:
         out = torch.empty(q.shape[0], hq * 128, dtype=q.dtype, device=q.device)
-    _kern().attn_prefill(out, q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_q_len, hq, hkv, scale)
+    _kern().attn_prefill(out, q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_q_len, hq, hkv, scale,
+                         cos_sin if cos_sin is not None else _empty(q.device))
     return out
 
 

@@ -119,6 +119,45 @@ def test_attn_prefill(dev, g):
     close(out, r, atol=2.5e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("g", [4, 8])
+def test_attn_prefill_fused_rope(dev, g):
+    """Prefill attention that rotates its Q rows on load (cos_sin) == RoPE applied to q first, and the
+    fp32 reference on the rotated q; positions ctx - q_len + i (chunked prefill over a cached prefix)."""
+    hkv = 8 if g == 4 else 1
+    qlens = [1, 37, 128, 200, 64]
+    ctxs = [1, 37, 300, 200, 1000]
+    q, kc, vc, bt, cu, ctx, hq = _make_seqs(qlens, ctxs, hkv, 16, dev, g)
+    cs = ref.rope_cos_sin(4096, 128, 500000.0, dev)
+    pos = torch.cat([torch.arange(c - n, c) for n, c in zip(qlens, ctxs)]).to(dev)
+    # q rotated up front in fp32 (the rope kernel's math), rounded to bf16 as the unfused path stores it
+    qr32 = q.float().view(q.shape[0], hq, 128)
+    co, si = cs[pos, :64][:, None, :], cs[pos, 64:][:, None, :]
+    a, b = qr32[..., :64], qr32[..., 64:]
+    qr = torch.cat([a * co - b * si, b * co + a * si], -1).to(torch.bfloat16).view_as(q)
+    scale = 1 / math.sqrt(128)
+    fused = ops.attn_prefill(q, kc, vc, bt, cu, ctx, max(qlens), hq, hkv, scale, cos_sin=cs)
+    plain = ops.attn_prefill(qr, kc, vc, bt, cu, ctx, max(qlens), hq, hkv, scale)
+    close(fused, plain, atol=1e-2, rtol=1e-2)
+    r = ref.attention(qr, kc, vc, bt, cu, ctx, hq, hkv, scale).reshape(q.shape[0], -1)
+    close(fused, r, atol=2.5e-2, rtol=2e-2)
+
+
+def test_rope_and_cache_keeps_q(dev):
+    """rot_q=False: k rotated and cached exactly as with rot_q=True, q left untouched."""
+    hq, hkv, t, bs, nb = 32, 8, 45, 16, 16
+    qkv = torch.randn(t, (hq + 2 * hkv) * 128, device=dev, dtype=torch.bfloat16)
+    pos = torch.randint(0, 4000, (t,), device=dev)
+    slots = torch.randperm(nb * bs, device=dev)[:t]
+    cs = ref.rope_cos_sin(4096, 128, 500000.0, dev)
+    kc1, vc1 = _paged(nb, hkv, bs, dev)
+    kc2, vc2 = _paged(nb, hkv, bs, dev)
+    q1, q2 = qkv.clone(), qkv.clone()
+    ops.rope_and_cache(q1, pos, cs, slots, kc1, vc1, hq, hkv, 128)
+    ops.rope_and_cache(q2, pos, cs, slots, kc2, vc2, hq, hkv, 128, rot_q=False)
+    assert torch.equal(q2[:, : hq * 128], qkv[:, : hq * 128])
+    assert torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
+
+
 @pytest.mark.parametrize("g,bs,merge", [(4, 16, False), (8, 16, False), (4, 32, False), (1, 16, False),
                                          (2, 16, False), (4, 16, True)])
 def test_attn_decode(dev, g, bs, merge):
