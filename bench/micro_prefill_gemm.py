@@ -1,5 +1,5 @@
 """Prefill GEMM microbenchmark: y = x @ W^T at M = 16384 tokens (32 x 512 prompts) for the
-Llama-3-8B projections, library default vs the TunableOp table in configs/ (DIE_TUNED_GEMMS=1).
+Llama-3-8B projections on hipBLASLt (the library default the engine's prefill uses).
 python bench/micro_prefill_gemm.py [M]
 """
 import json
@@ -11,12 +11,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def bench(m, tuned):
-    if tuned:
-        os.environ["DIE_TUNED_GEMMS"] = "1"
-        from src.ops.gemm_tuning import enable_tuned_gemms
-
-        assert enable_tuned_gemms()
+def bench(m, tuned=False):
     dev = torch.device("cuda:0")
     for name, (n, k) in {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096),
                          "down": (4096, 14336)}.items():
@@ -39,4 +34,4 @@ def bench(m, tuned):
 
 if __name__ == "__main__":
     m = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
-    bench(m, len(sys.argv) > 2 and sys.argv[2] == "tuned")
+    bench(m)

@@ -41,12 +41,44 @@ __device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
 }
 }  // namespace car
 
+// Steps 2 + 3 of the protocol for one workgroup: lanes 0..world-1 (except this rank's) signal peer `tid`
+// and wait for its signal. The wait is bounded (`spin_limit` polls): a peer that never signals (dead, or
+// out of step after skipping a call) sets the sticky error word ctl[2] and s_fail, and the caller then
+// POISONS its output (NaN) instead of reducing stale peer buffers. Once ctl[2] is set, later calls do
+// not wait at all (fail fast): the group is broken as a unit, and the host raises an engine fault on
+// its next token readback (TPModelRunner._to_host).
+__device__ __forceinline__ void car_wait_peers(const CarPeers& peers, uint32_t* slots, uint32_t* ctl, uint32_t epoch,
+                                               int par, int b, int rank, int world, int tid, uint32_t spin_limit,
+                                               int& s_fail) {
+  using namespace car;
+  if (tid < world && tid != rank) {
+    st_sys(peers.sig[tid] + ((int64_t)par * CAR_MAX_BLOCKS + b) * CAR_MAX_RANKS + rank, epoch);
+    bool ok = __hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+    uint32_t it = 0;
+    while (ok && ld_sys(slots + tid) != epoch) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++it > spin_limit) ok = false;
+    }
+    if (!ok) {
+      __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_fail = 1;
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint4 car_nan8() {
+  const uint32_t n = 0x7fc07fc0u;  // two bf16 quiet NaNs
+  return make_uint4(n, n, n, n);
+}
+
 __global__ void __launch_bounds__(car::NTH) custom_all_reduce_kernel(const bf16_t* __restrict__ in,
                                                                      bf16_t* __restrict__ out, int64_t nvec,
                                                                      int rank, int world, CarPeers peers,
                                                                      uint32_t* __restrict__ ctl, int64_t cap_vec,
-                                                                     int mode) {
+                                                                     int mode, uint32_t spin_limit) {
   using namespace car;
+  __shared__ int s_fail;
   const int tid = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
   const uint32_t epoch = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   const int par = (int)(epoch & 1u);
@@ -56,6 +88,7 @@ __global__ void __launch_bounds__(car::NTH) custom_all_reduce_kernel(const bf16_
   // 1. publish this rank's slice
   const uint4* src = reinterpret_cast<const uint4*>(in);
   uint4* mine = reinterpret_cast<uint4*>(peers.buf[rank]) + par * cap_vec;
+  if (tid == 0) s_fail = 0;
   for (int64_t i = v0 + tid; i < v1; i += NTH) mine[i] = src[i];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's staging stores are acknowledged
   __syncthreads();
@@ -63,22 +96,12 @@ __global__ void __launch_bounds__(car::NTH) custom_all_reduce_kernel(const bf16_
   // issued by the wave that then stores the flags, so program order covers them)
   uint32_t* slots = peers.sig[rank] + ((int64_t)par * CAR_MAX_BLOCKS + b) * CAR_MAX_RANKS;
   if (tid < 64 && !(mode & 2)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
-  if (tid < world && tid != rank) {
-    st_sys(peers.sig[tid] + ((int64_t)par * CAR_MAX_BLOCKS + b) * CAR_MAX_RANKS + rank, epoch);
-    uint32_t it = 0;
-    while (ld_sys(slots + tid) != epoch) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++it > (1u << 25)) {  // ~2 s: a missing peer reports instead of hanging the GPU
-        __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
+  car_wait_peers(peers, slots, ctl, epoch, par, b, rank, world, tid, spin_limit, s_fail);
   // mode bit 0: the peers' slices are read with system-coherent (sc0 sc1) loads of uncached memory,
   // so no cache can hold a stale copy and no L2-invalidating acquire is needed (the loads issue
   // only after the polls returned: control dependency + the barrier above)
   if (!(mode & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const bool failed = s_fail != 0;
 
   // 4. reduce in rank order (bit-identical on every rank)
   const uint4* bufs[CAR_MAX_RANKS];
@@ -87,6 +110,10 @@ __global__ void __launch_bounds__(car::NTH) custom_all_reduce_kernel(const bf16_
     bufs[p] = p < world ? reinterpret_cast<const uint4*>(peers.buf[p]) + par * cap_vec : nullptr;
   uint4* dst = reinterpret_cast<uint4*>(out);
   for (int64_t i = v0 + tid; i < v1; i += NTH) {
+    if (failed) {  // never reduce what a missing peer left in its buffer
+      dst[i] = car_nan8();
+      continue;
+    }
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int p = 0; p < world; ++p) {
       uint4 v;
@@ -129,9 +156,10 @@ __global__ void __launch_bounds__(car::NTH) custom_all_reduce_kernel(const bf16_
 // each row's statistics come from one deterministic block reduction. Same protocol as above.
 __global__ void __launch_bounds__(car::NTH) custom_all_reduce_residual_kernel(
     const bf16_t* __restrict__ in, bf16_t* __restrict__ resid, float* __restrict__ ssp, int hidden, int rank,
-    int world, CarPeers peers, uint32_t* __restrict__ ctl, int64_t cap_vec, int mode) {
+    int world, CarPeers peers, uint32_t* __restrict__ ctl, int64_t cap_vec, int mode, uint32_t spin_limit) {
   using namespace car;
   __shared__ float red[NTH / 64];
+  __shared__ int s_fail;
   const int tid = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
   const uint32_t epoch = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   const int par = (int)(epoch & 1u);
@@ -139,27 +167,22 @@ __global__ void __launch_bounds__(car::NTH) custom_all_reduce_residual_kernel(
   const int64_t v0 = (int64_t)b * hv, v1 = v0 + hv;
   const uint4* src = reinterpret_cast<const uint4*>(in);
   uint4* mine = reinterpret_cast<uint4*>(peers.buf[rank]) + par * cap_vec;
+  if (tid == 0) s_fail = 0;
   for (int64_t i = v0 + tid; i < v1; i += NTH) mine[i] = src[i];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   uint32_t* slots = peers.sig[rank] + ((int64_t)par * CAR_MAX_BLOCKS + b) * CAR_MAX_RANKS;
   if (tid < 64 && !(mode & 2)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  if (tid < world && tid != rank) {
-    st_sys(peers.sig[tid] + ((int64_t)par * CAR_MAX_BLOCKS + b) * CAR_MAX_RANKS + rank, epoch);
-    uint32_t it = 0;
-    while (ld_sys(slots + tid) != epoch) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++it > (1u << 25)) {
-        __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
+  car_wait_peers(peers, slots, ctl, epoch, par, b, rank, world, tid, spin_limit, s_fail);
   if (!(mode & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const bool failed = s_fail != 0;
   uint4* r = reinterpret_cast<uint4*>(resid);
   float ss = 0.f;
   for (int64_t i = v0 + tid; i < v1; i += NTH) {
+    if (failed) {  // poison the residual row: nothing downstream may look valid
+      r[i] = car_nan8();
+      continue;
+    }
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int p = 0; p < world; ++p) {
       uint4 v;
@@ -209,6 +232,17 @@ __global__ void __launch_bounds__(car::NTH) custom_all_reduce_residual_kernel(
   }
 }
 
+// Polls of a peer's flag before a call gives up (each poll ~s_sleep 2 + an uncached load: 2^25 ~ 2 s);
+// DIE_CAR_SPIN overrides it (tests of the failure path use a few thousand).
+static uint32_t car_spin_limit() {
+  static const uint32_t v = [] {
+    const char* e = getenv("DIE_CAR_SPIN");
+    const long long x = e ? atoll(e) : 0;
+    return x > 0 ? (uint32_t)std::min<long long>(x, 0xffffffffll) : (1u << 25);
+  }();
+  return v;
+}
+
 hipError_t launch_custom_all_reduce_residual(const bf16_t* in, bf16_t* resid, float* ssp, int rows, int hidden,
                                              int rank, int world, const CarPeers& peers, uint32_t* ctl,
                                              int64_t cap_elems, hipStream_t s) {
@@ -220,7 +254,7 @@ hipError_t launch_custom_all_reduce_residual(const bf16_t* in, bf16_t* resid, fl
     if (peers.buf[p] == nullptr || peers.sig[p] == nullptr) return hipErrorInvalidValue;
   static const int mode = getenv("DIE_CAR_MODE") ? atoi(getenv("DIE_CAR_MODE")) : 1;
   hipLaunchKernelGGL(custom_all_reduce_residual_kernel, dim3(rows), dim3(car::NTH), 0, s, in, resid, ssp, hidden,
-                     rank, world, peers, ctl, cap_elems / 8, mode);
+                     rank, world, peers, ctl, cap_elems / 8, mode, car_spin_limit());
   return hipGetLastError();
 }
 
@@ -237,7 +271,7 @@ hipError_t launch_custom_all_reduce(const bf16_t* in, bf16_t* out, int64_t n, in
   blocks = (int)std::min<int64_t>(blocks, (nvec + 63) / 64);  // at least 64 vectors (1 KiB) per workgroup
   static const int mode = getenv("DIE_CAR_MODE") ? atoi(getenv("DIE_CAR_MODE")) : 1;
   hipLaunchKernelGGL(custom_all_reduce_kernel, dim3(blocks), dim3(car::NTH), 0, s, in, out, nvec, rank, world,
-                     peers, ctl, cap_elems / 8, mode);
+                     peers, ctl, cap_elems / 8, mode, car_spin_limit());
   return hipGetLastError();
 }
 
@@ -249,8 +283,9 @@ __global__ void __launch_bounds__(car::NTH) custom_all_gather_kernel(const bf16_
                                                                      bf16_t* __restrict__ out, int64_t nvec,
                                                                      int64_t cvec, int rank, int world,
                                                                      CarPeers peers, uint32_t* __restrict__ ctl,
-                                                                     int64_t cap_vec) {
+                                                                     int64_t cap_vec, uint32_t spin_limit) {
   using namespace car;
+  __shared__ int s_fail;
   const int tid = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
   const uint32_t epoch = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   const int par = (int)(epoch & 1u);
@@ -258,23 +293,14 @@ __global__ void __launch_bounds__(car::NTH) custom_all_gather_kernel(const bf16_
   const int64_t v0 = min(nvec, (int64_t)b * per), v1 = min(nvec, v0 + per);
   const uint4* src = reinterpret_cast<const uint4*>(in);
   uint4* mine = reinterpret_cast<uint4*>(peers.buf[rank]) + par * cap_vec;
+  if (tid == 0) s_fail = 0;
   for (int64_t i = v0 + tid; i < v1; i += NTH) mine[i] = src[i];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   uint32_t* slots = peers.sig[rank] + ((int64_t)par * CAR_MAX_BLOCKS + b) * CAR_MAX_RANKS;
   if (tid < 64) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
-  if (tid < world && tid != rank) {
-    st_sys(peers.sig[tid] + ((int64_t)par * CAR_MAX_BLOCKS + b) * CAR_MAX_RANKS + rank, epoch);
-    uint32_t it = 0;
-    while (ld_sys(slots + tid) != epoch) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++it > (1u << 25)) {
-        __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
+  car_wait_peers(peers, slots, ctl, epoch, par, b, rank, world, tid, spin_limit, s_fail);
+  const bool failed = s_fail != 0;
   uint4* dst = reinterpret_cast<uint4*>(out);
   for (int p = 0; p < world; ++p) {
     const uint4* pb = reinterpret_cast<const uint4*>(peers.buf[p]) + par * cap_vec;
@@ -283,7 +309,8 @@ __global__ void __launch_bounds__(car::NTH) custom_all_gather_kernel(const bf16_
       const int64_t row = i / cvec, c = i - row * cvec;
       // peers' shards: system-coherent loads of their uncached staging (no stale line, no acquire)
       const uint4 v = p == rank ? src[i]
-                                : __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * 16), 0, 17));
+                      : failed ? car_nan8()
+                               : __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * 16), 0, 17));
       dst[(row * world + p) * cvec + c] = v;
     }
   }
@@ -309,7 +336,7 @@ hipError_t launch_custom_all_gather(const bf16_t* in, bf16_t* out, int64_t rows,
   const int64_t nvec = n / 8;
   blocks = (int)std::min<int64_t>(blocks, (nvec + 63) / 64);
   hipLaunchKernelGGL(custom_all_gather_kernel, dim3(blocks), dim3(car::NTH), 0, s, in, out, nvec, cols / 8, rank,
-                     world, peers, ctl, cap_elems / 8);
+                     world, peers, ctl, cap_elems / 8, car_spin_limit());
   return hipGetLastError();
 }
 

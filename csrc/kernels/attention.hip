@@ -33,6 +33,15 @@
 #include "common.h"
 #include "launchers.h"
 
+// Diagnostic bisection bits (DIE_ATTN_DBG for decode, DIE_PF_XCD bits 1-2 for prefill) exist only in a
+// diagnostics build (-DDIE_KERNEL_DIAG, `DIE_KERNEL_DIAG=1 python -m src._build --force`); in the production
+// build DIAG(x) is the constant 0 and those branches are compiled out.
+#ifdef DIE_KERNEL_DIAG
+#define DIAG(x) (x)
+#else
+#define DIAG(x) 0
+#endif
+
 namespace die {
 namespace attn {
 
@@ -299,7 +308,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
 
   bf16x8_t qf[8];
   // xcd_swz bit 1 (diagnostic): every row reads the Q row of token 0 (an L2 hit) instead of its own
-  load_q(qf, row_valid ? q + ((xcd_swz & 2) ? (int64_t)head * D : (int64_t)(qbeg + tok) * q_stride + (int64_t)head * D)
+  load_q(qf, row_valid ? q + (DIAG(xcd_swz & 2) ? (int64_t)head * D : (int64_t)(qbeg + tok) * q_stride + (int64_t)head * D)
                        : nullptr, h);
   if (cos_sin != nullptr && row_valid) {
     // RoPE (neox pairs (i, i + 64)) on the Q row as it is loaded: qf[kk] holds dims 16 kk + 8 h + [0, 8)
@@ -402,7 +411,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
   // of a 32 x 512 prefill (micro_attn_prefill_xcd_r2.txt); a row of 256 B is 16 lanes x 16 B, so each
   // wave stores its 32 x 128 tile in 8 instructions of 4 full rows. The loop ended on a barrier that
   // follows every wave's last LDS read, so the ring is free; each wave uses its own 32-row region.
-  if (!(xcd_swz & 4)) {  // bit 2 (diagnostic): no O store
+  if (!DIAG(xcd_swz & 4)) {  // bit 2 (diagnostic): no O store
     constexpr int OP = 272;  // staging row pitch (bytes): 2-way conflicts at most on the b64 writes
     char* ob = smem + wave * 32 * OP;
     const float inv = 1.f / st.l;
@@ -777,7 +786,7 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
 
     // LDS-DMA chunk c (K and V rows of 128 keys) into buffer b: 16 instructions per lane.
     auto issue = [&](int c, int b) {
-      if (dbg & 2) return;
+      if (DIAG(dbg & 2)) return;
       char* base = smem + b * V3_BUF;
       // this wave's two 16-key blocks of the chunk; the table row is read speculatively
       // (clamped to the row, not to the context) so the loads do not wait for ctx
@@ -805,7 +814,7 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
     // sum, norm scale, RoPE, KV write) runs while the chunk streams in; only a counted vmcnt separates
     // them (the chunk stays in flight).
     if constexpr (FUSED) {
-      if (!(dbg & 2)) {
+      if (!DIAG(dbg & 2)) {
         const float* srow = fz.slab + (int64_t)seq * fz.width;
         for (int i = wave; i < (frows + 1) / 2; i += 4) {
           const int ri = min(2 * i + (lane >> 5), frows - 1);
@@ -821,7 +830,7 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
         if (wave == 1)  // decode: the new token sits at position ctx - 1
           glds16(fz.cos_sin + (int64_t)(ctx - 1) * D + (lane & 31) * 4, fa + fs_off + 512);
       }
-    } else if (wave == 0 && !(dbg & 2)) {  // the G query rows of this (seq, kv head), 256 B each
+    } else if (wave == 0 && !DIAG(dbg & 2)) {  // the G query rows of this (seq, kv head), 256 B each
       const bf16_t* qb = q + (int64_t)seq * q_stride + (int64_t)kvh * G * D;
 #pragma unroll
       for (int i = 0; i < QI; ++i) {
@@ -926,7 +935,7 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
                            : zero_frag();
         if (fz.ts != nullptr) tsv[2] = __builtin_amdgcn_s_memrealtime();
       }
-      if (!(dbg & 1)) {
+      if (!DIAG(dbg & 1)) {
         const int kb = c * DEC_KEYS + 32 * wave;  // keys >= ctx: clamped rows, masked to -inf
         f32x16_t s = qk_lds_swz(base + 32 * wave * DEC_ROW, qf, lane);
         softmax_tile_lazy(s, st, kb, ctx, scale_log2, h);
@@ -936,7 +945,7 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     if (fz.ts != nullptr) tsv[3] = __builtin_amdgcn_s_memrealtime();
-    if (dbg & 32) continue;
+    if (DIAG(dbg & 32)) continue;
 
     // merge the 4 waves' (m, l, O) through LDS
     if (row < G) {
@@ -1136,7 +1145,11 @@ hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* c
     const float sl2 = scale * 1.4426950408889634f;
     const int tasks = num_seqs * hkv * maxp3;
     const int ncu = num_cus();
+#ifdef DIE_KERNEL_DIAG
     static const int dbg = getenv("DIE_ATTN_DBG") ? atoi(getenv("DIE_ATTN_DBG")) : 0;  // perf experiments only
+#else
+    constexpr int dbg = 0;
+#endif
     dim3 grid(tasks < ncu ? tasks : ncu), block(256);
     AttnDecodeFuse none{};
     none.ts = g_attn_ts;

@@ -5,6 +5,7 @@ kernels and the torch bindings into ``src/_C*.so`` and the host runtime
 
     python -m src._build            # incremental
     python -m src._build --force
+    DIE_KERNEL_DIAG=1 python -m src._build --force   # diagnostics build (kernel bisection bits)
 
 The kernels are compiled once here with ``hipcc --offload-arch=gfx950`` and the
 ``.so`` files travel with the repo snapshot to the GPU box.
@@ -67,7 +68,8 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
         obj = os.path.join(OBJ, k + ".o")
         objs.append(obj)
         if force or _newer(obj, [src] + hdrs):
-            jobs_list.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", CSRC,
+            diag = ["-DDIE_KERNEL_DIAG"] if os.environ.get("DIE_KERNEL_DIAG") == "1" else []
+            jobs_list.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *diag, "-I", CSRC,
                               "-c", src, "-o", obj])
     bsrc = os.path.join(CSRC, "bindings.cpp")
     bobj = os.path.join(OBJ, "bindings.o")

@@ -176,6 +176,10 @@ class Batcher:
         key = f"{model_name}:{version}"
         if not (self._running and self.eager_when_idle) or key in self._batches or self._inflight_by_key.get(key):
             return False
+        # the direct request counts against max_inflight_batches like a batch does: refuse when every
+        # slot is taken (the caller then queues normally), else take one without suspending
+        if self._sem is not None and not self._try_acquire_slot():
+            return False
         self._inflight_by_key[key] = 1
         self.total_requests += 1
         self.total_batches += 1
@@ -184,6 +188,21 @@ class Batcher:
     def release_direct(self, model_name: str, version: str) -> None:
         key = f"{model_name}:{version}"
         self._inflight_by_key[key] = self._inflight_by_key.get(key, 1) - 1
+        if self._sem is not None:
+            self._sem.release()
+
+    def _try_acquire_slot(self) -> bool:
+        """Non-blocking acquire of the in-flight semaphore (asyncio.Semaphore has none): when it is not
+        locked, acquire() completes without suspending, so drive that coroutine to its end here."""
+        if self._sem.locked():
+            return False
+        coro = self._sem.acquire()
+        try:
+            coro.send(None)
+        except StopIteration:
+            return True
+        coro.close()  # it suspended (cannot happen while unlocked): leave the semaphore as it was
+        return False
 
     def _detach(self, key: str, batch: Batch) -> List[BatchedRequest]:
         """Take the batch's requests and forget the batch. Caller holds the lock."""

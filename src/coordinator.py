@@ -341,8 +341,10 @@ class Coordinator:
                 # request's latency path); requests arriving meanwhile still batch behind it
                 try:
                     tr.mark(rid, "coord.dispatch")
+                    # one deadline over every retry (the batch path bounds its future the same way)
                     resp = await self._send(model, version, shard.shard_id, key,
-                                            {"op": "infer", "model": model, "inputs": inputs, "request_id": rid})
+                                            {"op": "infer", "model": model, "inputs": inputs, "request_id": rid},
+                                            deadline=time.monotonic() + self.request_timeout_s)
                 finally:
                     self.batcher.release_direct(model, vkey)
             else:
@@ -427,19 +429,28 @@ class Coordinator:
                 out.append(p)
         return out
 
-    async def _send(self, model: str, version: str, shard_id: int, key: str, msg: Dict[str, Any]) -> Dict[str, Any]:
+    async def _send(self, model: str, version: str, shard_id: int, key: str, msg: Dict[str, Any],
+                    deadline: Optional[float] = None) -> Dict[str, Any]:
+        """Send to the routed worker, retrying on the next candidates. ``deadline`` (time.monotonic())
+        bounds all attempts together: each one gets only the time that is left."""
         lb = self._lb(model, version)
         last_err = "no worker available"
         tried = 0
+        if deadline is None:
+            deadline = time.monotonic() + self.request_timeout_s
         for wid, addr in self._candidates(model, version, shard_id, key):
             if tried > self.max_retries:
+                break
+            left = deadline - time.monotonic()
+            if left <= 0:
+                last_err = f"request timed out after {self.request_timeout_s:g} s"
                 break
             if tried:
                 self.stats["retries"] += 1
             tried += 1
             try:
                 async with lb.track(wid):
-                    rep = await self.rpc.call(addr, msg, timeout=self.request_timeout_s)
+                    rep = await self.rpc.call(addr, msg, timeout=min(self.request_timeout_s, left))
                     if not isinstance(rep, dict):
                         raise RPCError("malformed reply")
                     if not rep.get("success") and rep.get("retryable"):
@@ -467,8 +478,10 @@ class Coordinator:
             outs = rep["outputs_list"]
             return [{"model": model, "outputs": o, "worker_id": rep.get("worker_id"), "success": True}
                     for o in outs]
+        deadline = time.monotonic() + self.request_timeout_s
         return [self._send(model, version, shard_id, it["key"],
-                           {"op": "infer", "model": model, "inputs": it["inputs"], "request_id": it["request_id"]})
+                           {"op": "infer", "model": model, "inputs": it["inputs"], "request_id": it["request_id"]},
+                           deadline=deadline)
                 for it in items]
 
     # ---------------------------------------------------------------- stats

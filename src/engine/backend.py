@@ -243,7 +243,7 @@ class LLMBackend:
         off = -1
         if d.get("ipc") is not None:  # payload already delivered into the landing zone by the sender's copy
             zone, off = self._landing_zone(), int(d["ipc"]["offset"])
-            kv = zone.claim(off, d["shape"])  # a view: the engine scatters straight from the zone
+            kv = zone.claim(off, d["shape"], d["ipc"].get("gen"))  # a view: the engine scatters from the zone
 
             def on_imported(ev, zone=zone, off=off, handed=handed):
                 handed.append(True)
@@ -300,9 +300,10 @@ class LLMBackend:
             while off is None and time.monotonic() < deadline:
                 await asyncio.sleep(0.0005)
                 off = zone.reserve(n)
-            return {"success": off is not None, "offset": off}
+            return {"success": off is not None, "offset": off,
+                    "gen": zone.generation(off) if off is not None else None}
         if op == "kv_release":  # a sender gave up on a reserved slot (copy or kv_import failed)
-            return {"success": self._landing_zone().release(int(msg["offset"]))}
+            return {"success": self._landing_zone().release(int(msg["offset"]), msg.get("gen"))}
         raise ValueError(f"unsupported op {op}")
 
     def get_metrics(self) -> Dict[str, Any]:

@@ -131,29 +131,49 @@ class RemoteDecodeLink:
                                                      "nbytes": packet.nbytes, "wait_s": self.reserve_wait_s},
                                       self.timeout)
             if rep.get("success"):
-                off = rep["offset"]
+                off, gen = rep["offset"], rep.get("gen")
                 imported = False
+                issued: Dict[str, Any] = {}
                 try:
                     # the copy runs on a transfer stream after the prefill engine's gather; the event loop
                     # only polls its completion event (no synchronize on this thread)
-                    await ch.write_async(off, packet.kv, packet.ready)
-                    wire = dict(packet_meta(packet), ipc={"offset": off})
+                    await ch.write_async(off, packet.kv, packet.ready, issued=issued)
+                    wire = dict(packet_meta(packet), ipc={"offset": off, "gen": gen})
                     self.ipc_packets += 1
                     imported = True  # from here the decode worker owns the slot (released after its scatter)
                     return await self.rpc.call(self.address, {"op": "kv_import", "model": self.model,
                                                               "packet": wire}, self.timeout)
                 except BaseException:
                     if not imported:  # the slot would leak: hand it back (best effort; it also expires)
-                        try:
-                            await self.rpc.call(self.address, {"op": "kv_release", "model": self.model,
-                                                               "offset": off}, 30.0)
-                        except Exception:
-                            logger.warning("kv_release of slot %d on %s failed", off, self.address)
+                        ev = issued.get("event")
+                        if ev is not None and not ev.query():
+                            # cancelled while the copy still writes into the slot: release it only once the
+                            # copy has finished, or another sender could get the slot and be overwritten
+                            asyncio.ensure_future(self._release_after_copy(off, gen, ev))
+                        else:
+                            await self._release(off, gen)
                     raise
         self.wire_packets += 1
         # device -> host copy of the payload: off the event-loop thread
         msg = {"op": "kv_import", "model": self.model, "packet": await asyncio.to_thread(packet_to_wire, packet)}
         return await self.rpc.call(self.address, msg, self.timeout)
+
+
+    async def _release(self, off: int, gen) -> None:
+        try:
+            await self.rpc.call(self.address, {"op": "kv_release", "model": self.model, "offset": off, "gen": gen},
+                                30.0)
+        except Exception:
+            logger.warning("kv_release of slot %d on %s failed", off, self.address)
+
+    async def _release_after_copy(self, off: int, gen, ev, poll_s: float = 2e-4, limit_s: float = 60.0) -> None:
+        t0 = time.monotonic()
+        while not ev.query():
+            if time.monotonic() - t0 > limit_s:  # never completes: leave the slot to the reservation TTL
+                logger.warning("KV copy into slot %d never completed; slot left to expire", off)
+                return
+            await asyncio.sleep(poll_s)
+        await self._release(off, gen)
 
 
 def sampling_to_dict(sp: SamplingParams) -> Dict[str, Any]:

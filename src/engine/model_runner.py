@@ -70,10 +70,6 @@ class ModelRunner:
         self.max_model_len = max_model_len
         self.bt_width = (max_model_len + self.bs - 1) // self.bs
         self.rt = native_runtime()
-        if self.is_cuda:
-            from src.ops.gemm_tuning import enable_tuned_gemms
-
-            enable_tuned_gemms()  # prefill GEMM solutions measured on MI355X (configs/)
         self.max_seqs = cfg.max_num_seqs
         self.max_tokens = max(cfg.max_num_batched_tokens, self.max_seqs)
         pin = self.is_cuda
@@ -193,9 +189,17 @@ class ModelRunner:
     def _to_host(self, ids: torch.Tensor, n: int) -> List[int]:
         if self.is_cuda:
             self.h_out[:n].copy_(ids[:n], non_blocking=True)
+            self._queue_fault_readback()
             torch.cuda.current_stream(self.device).synchronize()
+            self._raise_on_fault()
             return self.h_out[:n].tolist()
         return ids[:n].tolist()
+
+    def _queue_fault_readback(self) -> None:
+        """Hook: queue device-side error words behind the step (read with the tokens, same sync)."""
+
+    def _raise_on_fault(self) -> None:
+        """Hook: raise if a device-side error word read by :meth:`_queue_fault_readback` is set."""
 
     # ------------------------------------------------------------ prefill
     KIND_STOP, KIND_PREFILL, KIND_DECODE, KIND_HEARTBEAT = 0, 1, 2, 3
@@ -236,7 +240,9 @@ class ModelRunner:
             for j, i in enumerate(done):
                 res[i] = vals[j]
         elif self.is_cuda:
+            self._queue_fault_readback()
             torch.cuda.current_stream(self.device).synchronize()
+            self._raise_on_fault()
         return res
 
     def _exec_prefill(self, t: int, n: int, max_q: int, nd: int, greedy: bool) -> Optional[torch.Tensor]:

@@ -181,7 +181,10 @@ class Scheduler:
             # "auto": ride along when the prompt work fits the spare rows; otherwise alternate one bounded
             # prefill step (the decode rows wait for it) with one decode-only step, so decode progresses at
             # least every other step and no prompt is split into ride-along fragments
-            mixed = mode == "always" or pending <= room
+            # "always" mixes while prompt chunks still get a real share of the step; once the decode rows
+            # leave fewer than a quarter of mixed_step_tokens spare it falls back to the alternation below,
+            # so running prompts and new arrivals cannot be starved by a large decode batch
+            mixed = (mode == "always" and room >= max(1, self.cfg.mixed_step_tokens // 4)) or pending <= room
             if not mixed and self._defer_prefill(now, blocked):
                 out.decode = self._schedule_decode(ready, out)
                 if out.decode:

@@ -93,7 +93,13 @@ class KVCache:
         self.misses = 0
         self.evictions = 0
         if persist_path and os.path.exists(persist_path):
-            self.load(persist_path)
+            try:
+                self.load(persist_path)
+            except (OSError, UnicodeDecodeError, ValueError, TypeError, KeyError) as e:
+                # a version-1 (pickle) snapshot of an older build, or a truncated / foreign file: start
+                # empty rather than fail the coordinator at startup (never fall back to unpickling it)
+                logger.warning("KVCache: ignoring unreadable snapshot %s (%s); starting empty", persist_path, e)
+                self.cache.clear()
 
     # ------------------------------------------------------------------ core
     def _victim(self):
@@ -218,8 +224,10 @@ class KVCache:
     def load(self, path: Optional[str] = None) -> int:
         """Restore a JSON snapshot written by :meth:`save`."""
         path = path or self.persist_path
-        with open(path) as f:
+        with open(path, encoding="utf-8") as f:
             data = json.load(f)
+        if not isinstance(data, dict) or data.get("version") != 2:
+            raise ValueError(f"{path}: not a version-2 JSON KVCache snapshot")
         n = 0
         with self._lock:
             now = time.time()

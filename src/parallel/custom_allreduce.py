@@ -107,8 +107,13 @@ class CustomAllReduce:
         return list(_kern().car_read_words(self.ctl, 3))
 
     def error(self) -> bool:
-        """True once a call gave up waiting for a peer (a dead rank): its output is garbage."""
+        """True once a call gave up waiting for a peer (a dead rank, or a rank out of step). The sticky
+        word stays set: that call's output was poisoned (NaN) and every later call fails fast."""
         return bool(self.read_ctl()[2])
+
+    def error_word(self) -> torch.Tensor:
+        """The sticky error word as a 1-element device tensor (for a non-blocking readback)."""
+        return self._ctl[2:3]
 
     def close(self) -> None:
         k = _kern()

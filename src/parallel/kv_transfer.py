@@ -130,9 +130,17 @@ class IPCLandingZone:
             self.ptr = _C.car_alloc(self.capacity, uncached)
             self.view = _C.car_tensor(self.ptr, self.capacity, self.device.index or 0)
         self.handle = _C.car_handle(self.ptr).hex()
+        self._init_book(reserve_ttl_s)
+
+    def _init_book(self, reserve_ttl_s: float) -> None:
+        """Slot bookkeeping (host only; CPU-testable without a device buffer)."""
         self.reserve_ttl_s = reserve_ttl_s
         self._free: List[List[int]] = [[0, self.capacity]]  # sorted [start, end) ranges
         self._used: Dict[int, int] = {}
+        # generation of each reservation: a late kv_import / kv_release of an expired reservation whose
+        # offset was handed out again must not touch the new owner's slot
+        self._gen_of: Dict[int, int] = {}
+        self._next_gen = 1
         self._reserved_at: Dict[int, float] = {}   # reserved, not yet imported (expire after the TTL)
         self._pending: List[Any] = []              # (offset, event): released once the scatter has run
         self._lock = threading.Lock()
@@ -153,6 +161,7 @@ class IPCLandingZone:
             self.release(o)
 
     def reserve(self, nbytes: int) -> Optional[int]:
+        """First-fit reservation; returns the slot offset (its generation: :meth:`generation`)."""
         self._reap()
         n = -(-int(nbytes) // self.ALIGN) * self.ALIGN
         with self._lock:
@@ -163,13 +172,24 @@ class IPCLandingZone:
                     self._free = [x for x in self._free if x[1] > x[0]]
                     self._used[off] = n
                     self._reserved_at[off] = time.monotonic()
+                    self._gen_of[off] = self._next_gen
+                    self._next_gen += 1
                     return off
         return None
 
-    def release(self, offset: int) -> bool:
+    def generation(self, offset: int) -> Optional[int]:
         with self._lock:
-            n = self._used.pop(int(offset), None)
-            self._reserved_at.pop(int(offset), None)
+            return self._gen_of.get(int(offset))
+
+    def release(self, offset: int, gen: Optional[int] = None) -> bool:
+        """Free a slot. With ``gen``: only if it is still that reservation (a stale release is refused)."""
+        with self._lock:
+            offset = int(offset)
+            if gen is not None and self._gen_of.get(offset) != int(gen):
+                return False
+            n = self._used.pop(offset, None)
+            self._reserved_at.pop(offset, None)
+            self._gen_of.pop(offset, None)
             if n is None:
                 return False
             self._free.append([offset, offset + n])
@@ -183,13 +203,18 @@ class IPCLandingZone:
             self._free = merged
             return True
 
-    def claim(self, offset: int, shape: List[int]) -> torch.Tensor:
-        """A delivered packet as a bf16 view of its slot (the slot stays allocated until ``release_after``)."""
+    def claim(self, offset: int, shape: List[int], gen: Optional[int] = None) -> torch.Tensor:
+        """A delivered packet as a bf16 view of its slot (the slot stays allocated until ``release_after``).
+        ``gen``: the reservation's generation; an import for an expired reservation whose offset was
+        reserved again is rejected (it would scatter the new owner's half-written bytes)."""
         offset = int(offset)
         n = int(np.prod(shape)) * 2
         with self._lock:
             if offset not in self._used or self._used[offset] < n:
                 raise ValueError(f"kv_import of an unknown or too small landing-zone slot at {offset}")
+            if gen is not None and self._gen_of.get(offset) != int(gen):
+                raise ValueError(f"kv_import of a stale reservation at {offset} (generation {gen}, "
+                                 f"slot now {self._gen_of.get(offset)})")
             self._reserved_at.pop(offset, None)  # imported: no longer expires
         return self.view[offset: offset + n].view(torch.bfloat16).view(*shape)
 
@@ -255,11 +280,16 @@ class IPCSender:
         self.bytes_sent += flat.numel()
         return done
 
-    async def write_async(self, offset: int, kv: torch.Tensor, ready=None, poll_s: float = 2e-4) -> None:
-        """Copy and wait for delivery without blocking the event loop."""
+    async def write_async(self, offset: int, kv: torch.Tensor, ready=None, poll_s: float = 2e-4,
+                          issued: Optional[Dict[str, Any]] = None) -> None:
+        """Copy and wait for delivery without blocking the event loop. ``issued["event"]`` is set to the
+        copy's completion event as soon as the copy is queued, so a caller that is cancelled while
+        waiting knows the copy may still be writing into the slot."""
         import asyncio
 
         done = self.write(offset, kv, ready)
+        if issued is not None:
+            issued["event"] = done
         while not done.query():
             await asyncio.sleep(poll_s)
 

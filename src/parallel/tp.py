@@ -36,6 +36,9 @@ class TPContext:
     # host-side group for the step protocol's headers (gloo): followers learn each step's kind and
     # sizes without a GPU round trip (None = the default group, when that is gloo already)
     cpu_group: Optional[object] = None
+    # test hook: run the collectives even at world_size 1 (a one-rank RCCL group pins the RCCL branches'
+    # shapes and dtypes on a one-GPU box; tests/test_rccl_gpu.py)
+    force_collectives: bool = False
 
     def src_rank(self) -> int:
         """Global rank of this group's rank 0 (the ``src`` of broadcasts)."""
@@ -58,7 +61,7 @@ class TPContext:
 
     @property
     def enabled(self) -> bool:
-        return self.world_size > 1
+        return self.world_size > 1 or self.force_collectives
 
     def shard(self, n: int) -> int:
         if n % self.world_size:

@@ -46,6 +46,11 @@ from src.models.llama import CausalLM
 logger = logging.getLogger(__name__)
 
 
+class TPGroupFault(RuntimeError):
+    """A collective of the TP group gave up waiting for a peer (dead or out of step): the step's
+    outputs are poisoned and the group must be taken out of service as a unit."""
+
+
 class TPModelRunner(ModelRunner):
     HEARTBEAT_S = 20.0
     HDR = 8
@@ -59,6 +64,19 @@ class TPModelRunner(ModelRunner):
         self.h_pkt = torch.zeros(cap, dtype=torch.int64, pin_memory=self.is_cuda)
         self.d_pkt = torch.zeros(cap, dtype=torch.int64, device=self.device)
         self.steps_synced = 0
+        # the one-shot collectives' sticky error word (custom_allreduce ctl[2]), read back with the tokens
+        self.h_fault = torch.zeros(1, dtype=torch.int32, pin_memory=self.is_cuda)
+
+    # ------------------------------------------------------------ failure as a unit
+    def _queue_fault_readback(self) -> None:
+        car = self.tp.car
+        if car is not None:
+            self.h_fault.copy_(car.error_word(), non_blocking=True)
+
+    def _raise_on_fault(self) -> None:
+        if self.tp.car is not None and int(self.h_fault[0]):
+            raise TPGroupFault(f"TP rank {self.tp.rank}: a one-shot collective timed out waiting for a peer; "
+                               "its outputs were poisoned and no token of this step is returned")
 
     # ------------------------------------------------------------ protocol
     def _fields(self, kind: int, a: int, b: int, d: int):

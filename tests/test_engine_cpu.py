@@ -299,3 +299,29 @@ def test_prefill_batching_under_load():
         eng.step()
     for i, p in enumerate(([9, 10, 11, 12, 13], ps[0], ps[1], ps[2], ps[0][:7])):
         assert got[i] == greedy_reference(eng.model, p, 12), i
+
+
+def test_always_mixed_does_not_starve_prompts_behind_a_large_decode_batch():
+    """mixed_batching="always" with at least mixed_step_tokens decoding sequences used to leave a
+    budget of 0 rows for prompt chunks: a new arrival (or a running chunked prefill) made no progress
+    until enough decoders finished. It now falls back to the prefill/decode alternation."""
+    eng = make_engine(max_num_seqs=12, budget=256, blocks=256)
+    eng.cfg.mixed_step_tokens = 8
+    eng.cfg.mixed_batching = "always"
+    ps = prompts(11, seed=21)
+    long_sp, short_sp = SamplingParams(max_tokens=40), SamplingParams(max_tokens=4)
+    got = {}
+    for i in range(10):  # 10 decoders > mixed_step_tokens
+        eng.add_request(f"d{i}", ps[i][:20], long_sp)
+    eng.step()
+    eng.step()
+    eng.add_request("late", ps[10], short_sp, on_finish=lambda s: got.__setitem__("late", list(s.output_ids)))
+    for _ in range(12):  # well before any of the 40-token decoders can finish
+        eng.step()
+        if "late" in got:
+            break
+    assert "late" in got, "the late prompt was starved by the decode batch"
+    assert got["late"] == greedy_reference(eng.model, ps[10], 4)
+    while eng.has_work():
+        eng.step()
+    assert eng.get_stats()["kv"]["used"] == 0

@@ -358,3 +358,80 @@ def test_queued_decode_windows_match_synchronous():
     assert o3 == b3 and len(o3) == len(prompts) + 1
     # the queued windows leak no KV blocks
     assert engs[True].blocks.bm.num_available() == engs[False].blocks.bm.num_available()
+
+
+def _tp_fault_worker(rank, world, port, q):
+    """One rank skips a one-shot collective (out of step, as a rank that died mid-step would be)."""
+    import os
+
+    os.environ["DIE_CAR_SPIN"] = "200000"  # bounded waits of well under a second (read at the first launch)
+    import torch.distributed as dist
+
+    from src.parallel.tp import TPContext
+    from src.parallel.tp_runner import TPGroupFault, build_tp_engine
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tp = TPContext(rank=rank, world_size=world)
+        cfg = EngineConfig(max_num_seqs=4, max_num_batched_tokens=256, num_kv_blocks=128, max_latency_ms=0.0,
+                           use_cuda_graph=False)
+        obj = build_tp_engine("llama-mini", tp, "cuda:0", cfg=cfg, max_model_len=512, capture=False,
+                              full_init=True, seed=3)
+        if rank == 0:
+            obj.eos_token_id = None
+            finished = []
+            for i, p in enumerate(TP_PROMPTS):
+                obj.add_request(f"f{i}", p, SamplingParams(max_tokens=8), on_finish=finished.append)
+            tokens_before = None
+            try:
+                while obj.has_work():
+                    obj.step()
+                    tokens_before = [len(s.output_ids) for s in obj.scheduler.running]
+                q.put(("no fault raised", None, None))
+            except TPGroupFault:
+                after = [len(s.output_ids) for s in obj.scheduler.running]
+                q.put(("raised", len(finished), (tokens_before, after)))
+            obj.runner.stop_followers()
+        else:
+            car = tp.car
+            real = car.all_reduce_residual
+            calls = [0]
+
+            def skip_one(*a, **k):  # the 5th residual all-reduce (first decode step) never happens here
+                calls[0] += 1
+                if calls[0] != 5:
+                    real(*a, **k)
+            car.all_reduce_residual = skip_one
+            obj.follower_loop()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tp_group_fails_as_a_unit():
+    """A rank that skips a collective must not make the leader reduce stale peer buffers: the one-shot
+    kernel gives up after its bounded wait, poisons its output and sets the sticky error word, which the
+    leader reads back with the step's tokens and raises as TPGroupFault — no token of that step (or any
+    later one) reaches a request (the reference marks failed workers at
+    /root/reference/src/router.py:233-245)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_tp_fault_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    status, n_finished, toks = q.get(timeout=300)
+    for p in procs:
+        p.join(120)
+    assert status == "raised", status
+    assert n_finished == 0                  # no request completed with poisoned tokens
+    before, after = toks
+    assert before is not None and before == after, toks  # the faulting step appended no token
+    assert all(p.exitcode == 0 for p in procs)

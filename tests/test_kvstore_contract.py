@@ -162,3 +162,26 @@ def test_thread_safety():
     [t.start() for t in ts]
     [t.join() for t in ts]
     assert not errs and len(s) <= 64
+
+
+def test_legacy_or_corrupt_snapshot_starts_empty(tmp_path):
+    """A version-1 pickle snapshot (older build), a truncated file or foreign JSON must not stop the
+    store (and so the coordinator) from starting; it is never unpickled."""
+    import pickle
+
+    cases = {
+        "legacy.pkl": pickle.dumps({"version": 1, "entries": {"a": 1}}),
+        "truncated.json": b'{"version": 2, "policy": "lru", "entries": [["a", 1',
+        "foreign.json": b'["not", "a", "snapshot"]',
+        "v3.json": b'{"version": 3, "entries": []}',
+    }
+    for name, blob in cases.items():
+        p = tmp_path / name
+        p.write_bytes(blob)
+        store = KVCache(max_size=4, persist_path=str(p))
+        assert len(store) == 0, name
+        store.set("k", "v")
+        store.close()  # the next save overwrites the bad file with a valid snapshot
+        again = KVCache(max_size=4, persist_path=str(p))
+        assert again.get("k") == "v", name
+        again.close()

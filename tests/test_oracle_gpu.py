@@ -25,8 +25,9 @@ from src.models.llama import AttnMetadata  # noqa: E402
 from src.preproc import SamplingParams  # noqa: E402
 
 STEPS = 8
-# decode batches: the bench's 32 rows, and 100 rows (128-row activation images, waves split the rows)
-N_SEQS = [32, 100]
+# (decode batch, prompt lengths): the bench's 32 rows, 100 rows (128-row activation images, waves split the
+# rows) and the served length itself — 32 prompts of ~512 tokens, the headline's prefill shape
+N_SEQS = [(32, 8, 48), (100, 8, 48), (32, 500, 513)]
 
 
 @torch.inference_mode()
@@ -98,13 +99,13 @@ def setup(request):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     assert ops.native_available()
-    n_seq = request.param
-    cfg = EngineConfig(max_num_seqs=n_seq, max_num_batched_tokens=16384, max_latency_ms=0.0, num_kv_blocks=1024)
+    n_seq, lo, hi = request.param
+    cfg = EngineConfig(max_num_seqs=n_seq, max_num_batched_tokens=16384, max_latency_ms=0.0, num_kv_blocks=1280)
     eng = LLMEngine.from_preset("llama3-8b", device="cuda:0", cfg=cfg, max_model_len=1024, seed=11, num_layers=2)
     eng.eos_token_id = None
     ref = eng.model.reference_copy("cpu", torch.float32)
     rng = random.Random(7)
-    prompts = [[rng.randrange(3, 128256) for _ in range(rng.randrange(8, 48))] for _ in range(n_seq)]
+    prompts = [[rng.randrange(3, 128256) for _ in range(rng.randrange(lo, hi))] for _ in range(n_seq)]
     cpu = paged_greedy(ref, prompts, STEPS)
     yield eng, prompts, cpu
     del eng
