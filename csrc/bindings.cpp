@@ -746,6 +746,77 @@ void car_all_reduce(Tensor in, Tensor out, int64_t rank, std::vector<int64_t> bu
 
 }  // namespace
 
+// Persistent decode step (decode_persistent.hip): the instantiation's tiles and workspace layout for a shape.
+std::vector<int64_t> decode_persistent_config(int64_t H, int64_t I, int64_t hq, int64_t hkv, int64_t layers) {
+  int cfg[7];
+  int64_t lay[4];
+  if (!die::decode_persistent_config((int)H, (int)I, (int)hq, (int)hkv, (int)layers, cfg, lay)) return {};
+  return {cfg[0], cfg[1], cfg[2], cfg[3], cfg[4], cfg[5], cfg[6], lay[0], lay[1], lay[2], lay[3]};
+}
+
+// layers [l0, l1) of a dense decode step in one launch. `table` [L, 6] int64 = per layer the device pointers of
+// the tile-packed qkv / o / gate_up / down weights and of the layer's K / V cache (built by the model from
+// tensors it keeps alive); `pool` [L, 2, blocks, hkv, 16, 128] is only checked against the table's geometry.
+void decode_persistent(Tensor ws, Tensor table, Tensor h, Tensor ssp0, Tensor block_tables, Tensor ctx_lens,
+                       Tensor slot_mapping, Tensor cos_sin, Tensor pool, int64_t l0, int64_t l1, int64_t I,
+                       int64_t hq, int64_t hkv, double scale, double eps) {
+  DIE_CHECK_CUDA(h);
+  DIE_CHECK_BF16(h);
+  DIE_CHECK_CONTIG(h);
+  TORCH_CHECK(h.dim() == 2 && h.size(0) >= 1 && h.size(0) <= 32, "h [M <= 32, H]");
+  const int64_t M = h.size(0), H = h.size(1), L = table.size(0);
+  int cfg[7];
+  int64_t lay[4];
+  TORCH_CHECK(die::decode_persistent_config((int)H, (int)I, (int)hq, (int)hkv, (int)L, cfg, lay),
+              "decode_persistent: no instantiation for this model shape");
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.is_contiguous() && table.dim() == 2 &&
+                  table.size(1) == 6, "table [L, 6] int64 on the GPU");
+  TORCH_CHECK(0 <= l0 && l0 < l1 && l1 <= L, "layer range");
+  TORCH_CHECK(ws.is_cuda() && ws.is_contiguous() && ws.numel() * ws.element_size() >= lay[0] &&
+                  reinterpret_cast<uintptr_t>(ws.data_ptr()) % 256 == 0, "workspace too small or misaligned");
+  DIE_CHECK_CUDA(pool);
+  DIE_CHECK_BF16(pool);
+  DIE_CHECK_CONTIG(pool);
+  TORCH_CHECK(pool.dim() == 6 && pool.size(0) == L && pool.size(1) == 2 && pool.size(3) == hkv && pool.size(4) == 16 &&
+                  pool.size(5) == 128, "pool [L, 2, blocks, hkv, 16, 128]");
+  DIE_CHECK_DTYPE(ssp0, at::kFloat);
+  DIE_CHECK_CONTIG(ssp0);
+  TORCH_CHECK(ssp0.dim() == 2 && ssp0.size(1) == die::DECODE_SSP_LD && ssp0.size(0) >= 1 && ssp0.size(0) <= 128,
+              "ssp0 [tiles <= 128, 128]");
+  DIE_CHECK_DTYPE(block_tables, at::kInt);
+  DIE_CHECK_CONTIG(block_tables);
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= M, "block_tables [>= M, width]");
+  DIE_CHECK_DTYPE(ctx_lens, at::kInt);
+  TORCH_CHECK(ctx_lens.is_contiguous() && ctx_lens.numel() >= M, "ctx_lens [>= M]");
+  DIE_CHECK_DTYPE(slot_mapping, at::kLong);
+  TORCH_CHECK(slot_mapping.is_contiguous() && slot_mapping.numel() >= M, "slot_mapping [>= M]");
+  DIE_CHECK_DTYPE(cos_sin, at::kFloat);
+  DIE_CHECK_CONTIG(cos_sin);
+  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == 128, "cos_sin [max_pos, 128]");
+  die::DpArgs a{};
+  a.layers = reinterpret_cast<const die::DpLayerW*>(table.data_ptr());
+  a.ws = reinterpret_cast<char*>(ws.data_ptr());
+  a.h = bf(h);
+  a.ssp0 = ssp0.data_ptr<float>();
+  a.bt = block_tables.data_ptr<int>();
+  a.ctx = ctx_lens.data_ptr<int>();
+  a.slots = slot_mapping.data_ptr<int64_t>();
+  a.cos_sin = cos_sin.data_ptr<float>();
+  a.l0 = (int)l0;
+  a.l1 = (int)l1;
+  a.M = (int)M;
+  a.bt_stride = (int)block_tables.stride(0);
+  a.ssp0_tiles = (int)ssp0.size(0);
+  a.scale_log2 = (float)(scale * 1.4426950408889634);
+  a.eps = (float)eps;
+  a.inv_h = 1.f / (float)H;
+  a.H = (int)H;
+  a.I = (int)I;
+  a.hq = (int)hq;
+  a.hkv = (int)hkv;
+  DIE_HIP(die::launch_decode_persistent(a, cur_stream()));
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "Hand-written gfx950 (MI355X) HIP kernels";
   m.def("rms_norm", &rms_norm);
@@ -755,6 +826,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_prefill", &attn_prefill);
   m.def("attn_decode", &attn_decode);
   m.def("attn_decode_fused", &attn_decode_fused);
+  m.def("decode_persistent_config", &decode_persistent_config);
+  m.def("decode_persistent", &decode_persistent);
   m.def("decode_partials", &decode_partials);
   m.def("sample", &sample, py::arg("out"), py::arg("logits"), py::arg("temperature") = py::none(),
         py::arg("top_k") = py::none(), py::arg("top_p") = py::none(), py::arg("seeds") = py::none(),

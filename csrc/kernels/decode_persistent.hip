@@ -1,0 +1,958 @@
+// Persistent decode step: every layer of a dense Llama decode step (qkv -> attention -> o -> gate/up ->
+// down, M <= 32 rows) in ONE launch, one 256-thread workgroup per CU, with a weight / KV stream that never
+// stops at an op boundary.
+//
+// Why (MI355X_MICROARCH.md "prefetch-credit", "engine-vs-launches"): as five launches
+// per layer every op pays its own fill (first-chunk latency), drain (stragglers) and launch gap — about
+// 24 us of a 106 us layer at batch 32. The weights (and the attention's cached K/V) never depend on the
+// activations, so here a loader keeps issuing the NEXT op's weight chunks into the LDS ring while the
+// current op drains and while its dependency resolves; only the small activation stream waits.
+//
+// Structure:
+//  * Work = (layer, phase, task) in a fixed order; phase = qkv | attention | o | gate/up | down. Every phase
+//    has ~one task per CU (column tile x K slice for the GEMMs, (sequence, kv head) pair for attention);
+//    workgroup b runs tasks b, b + P, ... of each phase. A task is a sequence of chunks: one K slice
+//    of KC = 128 (GEMMs: WR weight rows + 32 activation rows, 256-byte swizzled image rows) or 128 keys
+//    (attention: K and V images, 64 KiB).
+//  * The chunks of all tasks form one stream through a 128 KiB byte ring in LDS (a chunk is contiguous;
+//    positions are monotonic, a chunk that would straddle the end starts at the next lap). Three walkers
+//    run over the same deterministic sequence: the W walker issues the weight / K/V pieces as soon as the
+//    ring has room, the X walker issues the activation pieces once the chunk's phase is READY, and the
+//    consumer computes.
+//  * Wave roles (vmcnt is per wave and loads/stores retire in issue order, so an early stream and a late
+//    stream must never share a wave): waves 0 and 1 issue ONLY the early stream (weights, K/V), wave 2
+//    ONLY the late stream (activations, attention prologue operands, norm statistics), wave 3 never loads
+//    into the ring — it polls the dependency counters, does every global store of the epilogues (sc1,
+//    write-through), takes the split-K tickets and publishes. All four waves compute (MFMA).
+//  * Hand-offs (MI355X_MICROARCH.md visibility table, row 1): the producer's payload is stored sc1 by
+//    wave 3, drained (vmcnt(0)), then ONE lane adds to the phase counter (agent scope, sharded over 8
+//    words). The consumer's wave 3 polls the counter with relaxed agent loads, publishes READY in LDS,
+//    and the X loads that follow are sc1 LDS-DMA.
+//  * Determinism: the GEMM partial sums of the four waves are combined through LDS in wave order, the
+//    attention merge in wave order, split-K slabs in slice order — the same arithmetic as the multi-launch
+//    path (gemm_decode.hip SPLIT 0 tiles at KC = 128, attention.hip v3 FUSED with one part per pair), so
+//    the two paths are bit-identical for the same tiles (tests/test_decode_persistent_gpu.py).
+//  * Deadlock freedom: dependencies only point to earlier phases and a workgroup runs its tasks in
+//    order; the grid is one workgroup per CU (all resident). Every wait is bounded: a timeout sets the
+//    error word and lets the launch drain (its outputs are then garbage, and the host raises).
+#include "attn_common.h"
+#include "common.h"
+#include "launchers.h"
+
+namespace die {
+namespace dp {
+
+using namespace attn;
+
+constexpr int NTH = 256;
+constexpr int RING = 128 * 1024;             // weight / KV stream
+constexpr int SCR = 27 * 1024;               // per-task scratch (GEMM partial sums | attention staging, merge)
+constexpr int CTLB = 256;                    // control words
+constexpr int LDS_TOTAL = RING + SCR + CTLB; // 159,744 B: one workgroup per CU
+constexpr int XR = 32;                       // activation rows per chunk (decode rows M <= 32)
+constexpr int KC = 128;                      // K per GEMM chunk
+constexpr int ROWB = 256;                    // bytes per GEMM image row
+constexpr int ACH = 65536;                   // attention chunk: 128 keys of K + V
+constexpr int NSH = 8;                       // counter shards
+constexpr int NPH = 5;
+enum { P_QKV = 0, P_ATT = 1, P_O = 2, P_GU = 3, P_DN = 4 };
+// SCR layout. GEMM tasks:
+constexpr int S_RED = 0;                     // partial sums [32][RS] fp32 (<= 18 KiB)
+constexpr int S_STAT = 18 * 1024;            // gate/up: the o-projection's norm statistics [tiles <= 64][32]
+// attention tasks: prologue staging, then (after the prologue) the merge area at 0
+constexpr int S_ASSP = 20 * 1024;            // input-norm statistics, 2 x 256 B
+constexpr int S_ACOS = 20 * 1024 + 512;      // cos | sin row at the new token's position (1 KiB DMA)
+constexpr int S_AQ = 21 * 1024 + 512;        // rotated query rows, G <= 8 x 256 B
+constexpr int S_ANKV = 23 * 1024 + 512;      // the new token's rotated key and value (bf16), 512 B
+constexpr int S_ML = 0;                      // merge: per-wave (m, l) [4][32][2]
+constexpr int S_OB = 1024;                   //        per-wave O [4][G][128] fp32 (<= 16 KiB)
+// CTL
+constexpr int C_READY = 0;                   // highest phase id known READY (int)
+constexpr int C_RS = 64;                     // gate/up epilogue: row scales [32] fp32
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f4;
+typedef __attribute__((ext_vector_type(4))) unsigned u4;
+
+template <int AUX>
+__device__ __forceinline__ void dma16(const void* src, char* lds) {
+  __builtin_amdgcn_global_load_lds((global_cvoid*)src, (lds_void*)lds, 16, 0, AUX);
+}
+__device__ __forceinline__ void dma4(const void* src, char* lds) {
+  __builtin_amdgcn_global_load_lds((global_cvoid*)src, (lds_void*)lds, 4, 0, 16);
+}
+
+#define DP_W1(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+#define DP_W8(A) DP_W1(A) DP_W1(A + 1) DP_W1(A + 2) DP_W1(A + 3) DP_W1(A + 4) DP_W1(A + 5) DP_W1(A + 6) DP_W1(A + 7)
+// s_waitcnt vmcnt(n) for a run-time n: until at most n of this wave's vector-memory ops are outstanding
+__device__ __forceinline__ void wait_vm_dyn(int n) {
+  n = n < 0 ? 0 : (n > 63 ? 63 : n);
+  switch (n) {
+    DP_W8(0) DP_W8(8) DP_W8(16) DP_W8(24) DP_W8(32) DP_W8(40) DP_W8(48) DP_W8(56)
+  }
+}
+#undef DP_W8
+#undef DP_W1
+
+__device__ __forceinline__ void barrier() { __builtin_amdgcn_s_barrier(); }
+__device__ __forceinline__ void lds_fence_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// ------------------------------------------------------------------------------------------------------
+// Model geometry and tiles are compile-time (one instantiation per served shape: no run-time divisions and
+// few live scalar registers); only the decode rows M, the grid and the pointers are run-time.
+template <int H_, int I_, int HQ_, int HKV_, int WRQ_, int SKQ_, int WRO_, int SKO_, int WRG_, int WRD_, int SKD_>
+struct Cfg {
+  static constexpr int H = H_, I = I_, HQ = HQ_, HKV = HKV_, G = HQ_ / HKV_, NQ = (HQ_ + 2 * HKV_) * 128;
+  static constexpr int WRQ = WRQ_, SKQ = SKQ_, WRO = WRO_, SKO = SKO_, WRG = WRG_, WRD = WRD_, SKD = SKD_;
+  static constexpr int TQ = NQ / WRQ, NTQ = TQ * SKQ, CQ = H / SKQ / KC;        // qkv tiles, tasks, chunks
+  static constexpr int TO = H / WRO, NTO = TO * SKO, CO = HQ * 128 / SKO / KC;  // o
+  static constexpr int NTG = I / (WRG / 2), CG = H / KC;                       // gate/up
+  static constexpr int TD = H / WRD, NTD = TD * SKD, CD = I / SKD / KC;        // down
+  static_assert(NQ % WRQ == 0 && H % WRO == 0 && I % (WRG / 2) == 0 && H % WRD == 0, "tiles cover N");
+  static_assert(H % (SKQ * KC) == 0 && (HQ * 128) % (SKO * KC) == 0 && I % (SKD * KC) == 0, "K slices");
+  static_assert(TO <= 64, "gate/up stages the o statistics of <= 64 tiles");
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8, "GQA group");
+};
+
+// workspace layout (bytes), rows padded to XR = 32
+template <class C>
+struct WS {
+  static constexpr int64_t a16(int64_t x) { return (x + 15) / 16 * 16; }
+  static constexpr int SKOD = C::SKO > C::SKD ? C::SKO : C::SKD;
+  static constexpr int64_t SLABQ = 0;                                          // f32 [SKQ][32][NQ]
+  static constexpr int64_t ATTN = a16(SLABQ + (int64_t)C::SKQ * XR * C::NQ * 4);  // bf16 [32][HQ 128]
+  static constexpr int64_t SLABOD = a16(ATTN + (int64_t)XR * C::HQ * 128 * 2);  // f32 [SKOD][32][H]
+  static constexpr int64_t ACT = a16(SLABOD + (int64_t)SKOD * XR * C::H * 4);   // bf16 [32][I]
+  static constexpr int64_t SSPO = a16(ACT + (int64_t)XR * C::I * 2);           // f32 [TO][128]
+  static constexpr int64_t SSPD = a16(SSPO + (int64_t)C::TO * 128 * 4);        // f32 [TD][128]
+  static constexpr int64_t TICKO = a16(SSPD + (int64_t)C::TD * 128 * 4);       // i32 [TO]
+  static constexpr int64_t TICKD = a16(TICKO + (int64_t)C::TO * 4);            // i32 [TD]
+  static constexpr int64_t ERR = a16(TICKD + (int64_t)C::TD * 4);              // i32 [4]
+  static constexpr int64_t SYNC = ERR + 16;                                    // i32 [layers][DP_SYNC_LD]
+  static __device__ __forceinline__ float* slab_q(const DpArgs& a) { return reinterpret_cast<float*>(a.ws + SLABQ); }
+  static __device__ __forceinline__ bf16_t* attn(const DpArgs& a) { return reinterpret_cast<bf16_t*>(a.ws + ATTN); }
+  static __device__ __forceinline__ float* slab_od(const DpArgs& a) { return reinterpret_cast<float*>(a.ws + SLABOD); }
+  static __device__ __forceinline__ bf16_t* act(const DpArgs& a) { return reinterpret_cast<bf16_t*>(a.ws + ACT); }
+  static __device__ __forceinline__ float* ssp_o(const DpArgs& a) { return reinterpret_cast<float*>(a.ws + SSPO); }
+  static __device__ __forceinline__ float* ssp_d(const DpArgs& a) { return reinterpret_cast<float*>(a.ws + SSPD); }
+  static __device__ __forceinline__ int* tick_o(const DpArgs& a) { return reinterpret_cast<int*>(a.ws + TICKO); }
+  static __device__ __forceinline__ int* tick_d(const DpArgs& a) { return reinterpret_cast<int*>(a.ws + TICKD); }
+  static __device__ __forceinline__ int* err(const DpArgs& a) { return reinterpret_cast<int*>(a.ws + ERR); }
+  static __device__ __forceinline__ int* sync(const DpArgs& a) { return reinterpret_cast<int*>(a.ws + SYNC); }
+};
+
+struct Rt {  // run-time uniforms
+  int P, b, M, l0, l1;
+};
+
+template <class C>
+__device__ __forceinline__ int ntasks(const Rt& r, int p) {
+  switch (p) {
+    case P_QKV: return C::NTQ;
+    case P_ATT: return r.M * C::HKV;
+    case P_O: return C::NTO;
+    case P_GU: return C::NTG;
+    default: return C::NTD;
+  }
+}
+
+template <class C>
+__device__ __forceinline__ int wr_of(int p) {
+  return p == P_QKV ? C::WRQ : p == P_O ? C::WRO : p == P_GU ? C::WRG : C::WRD;
+}
+
+template <class C>
+__device__ __forceinline__ uint32_t chunk_bytes(int p) {
+  return p == P_ATT ? (uint32_t)ACH : (uint32_t)((wr_of<C>(p) + XR) * ROWB);
+}
+
+// (column tile, K slice) of split-K task t: the slices of one tile go to workgroups b, b + 8, ... (one XCD
+// under round-robin placement, so the last arriver reads the other slices from its own L2 — speed only)
+template <int TILES, int SK>
+__device__ __forceinline__ void tile_slice(int t, int& tile, int& slice) {
+  if constexpr (SK > 1 && TILES % 8 == 0) {
+    const int grp = t / (8 * SK), r = t - grp * 8 * SK;
+    tile = grp * 8 + (r & 7);
+    slice = r >> 3;
+  } else {
+    tile = t / SK;
+    slice = t - tile * SK;
+  }
+}
+
+// A walker over this workgroup's chunk sequence: phase index q = (layer - l0) * NPH + phase, task t, chunk k
+// of nch, sequence number idx, ring position pos (monotonic; a chunk never straddles the ring's end).
+struct Walk {
+  int q, t, k, nch, idx;
+  uint32_t pos;
+};
+
+__device__ __forceinline__ int wl(const Rt& r, const Walk& w) { return r.l0 + w.q / NPH; }
+__device__ __forceinline__ int wp(const Walk& w) { return w.q % NPH; }
+
+template <class C>
+__device__ __forceinline__ int task_chunks(const DpArgs& a, int p, int t) {
+  switch (p) {
+    case P_QKV: return C::CQ;
+    case P_ATT: return (__builtin_amdgcn_readfirstlane(a.ctx[t / C::HKV]) + DEC_KEYS - 1) / DEC_KEYS;
+    case P_O: return C::CO;
+    case P_GU: return C::CG;
+    default: return C::CD;
+  }
+}
+
+// first task of phase index >= w.q for this workgroup (phases without a task for it are skipped)
+template <class C>
+__device__ __forceinline__ void walk_settle(Walk& w, const Rt& r, const DpArgs& a, int qend) {
+  while (w.q < qend && w.t >= ntasks<C>(r, wp(w))) {
+    ++w.q;
+    w.t = r.b;
+  }
+  if (w.q < qend) {
+    w.nch = task_chunks<C>(a, wp(w), w.t);
+    const uint32_t sz = chunk_bytes<C>(wp(w)), off = w.pos % RING;
+    if (off + sz > RING) w.pos += RING - off;
+  }
+}
+
+template <class C>
+__device__ __forceinline__ void walk_begin(Walk& w, const Rt& r, const DpArgs& a, int qend) {
+  w.q = 0;
+  w.t = r.b;
+  w.k = 0;
+  w.idx = 0;
+  w.pos = 0;
+  walk_settle<C>(w, r, a, qend);
+}
+
+template <class C>
+__device__ __forceinline__ void walk_next(Walk& w, const Rt& r, const DpArgs& a, int qend) {
+  w.pos += chunk_bytes<C>(wp(w));
+  ++w.idx;
+  if (++w.k < w.nch) {
+    const uint32_t sz = chunk_bytes<C>(wp(w)), off = w.pos % RING;
+    if (off + sz > RING) w.pos += RING - off;
+    return;
+  }
+  w.k = 0;
+  w.t += r.P;
+  walk_settle<C>(w, r, a, qend);
+}
+
+// pieces (1 KiB LDS-DMA instructions) this wave issues for a chunk: waves 0 / 1 the early stream, wave 2 the
+// late stream; the same counts drive the issue and the counted waits
+template <class C>
+__device__ __forceinline__ int w_pieces(int p, int wave) {
+  if (wave > 1) return 0;
+  return p == P_ATT ? 32 : wr_of<C>(p) / 8;  // WR rows x 256 B = WR / 4 pieces, split over two waves
+}
+template <class C>
+__device__ __forceinline__ int x_pieces(const Rt& r, int p, int t, int k, int wave) {
+  if (wave != 2) return 0;
+  if (p == P_ATT) return k == 0 ? (C::SKQ * (C::G + 2) + 1) / 2 + 3 : 0;
+  int n = XR * ROWB / 1024;  // 8
+  if (p == P_GU && k == 0 && t == r.b) n += (C::TO + 7) / 8;  // the o statistics, once per layer
+  return n;
+}
+
+// ------------------------------------------------------------------------------------------------------
+// issue: early stream (waves 0, 1): weight pieces (nt) or the attention task's K (wave 0) / V (wave 1) image
+template <class C>
+__device__ __forceinline__ void issue_w(const Walk& w, const Rt& r, const DpArgs& a, char* ring, int wave, int lane) {
+  char* slot = ring + (w.pos % RING);
+  const int p = wp(w);
+  const DpLayerW& L = a.layers[wl(r, w)];
+  if (p == P_ATT) {
+    const int seq = w.t / C::HKV, kvh = w.t - seq * C::HKV;
+    const int ctx = __builtin_amdgcn_readfirstlane(a.ctx[seq]);
+    const int* bt = a.bt + (int64_t)seq * a.bt_stride;
+    const bf16_t* cache = wave == 0 ? L.kc : L.vc;
+    char* img = slot + wave * (DEC_KEYS * DEC_ROW);
+    const int pch = lane & 15;
+#pragma unroll 4
+    for (int i = 0; i < 32; ++i) {
+      const int kr0 = w.k * DEC_KEYS + 4 * i;
+      const int64_t blk = bt[__builtin_amdgcn_readfirstlane(min(kr0, ctx - 1) >> 4)];
+      const int rr = 4 * i + (lane >> 4);
+      const int key = min(kr0 + (lane >> 4), ctx - 1);  // past the context: the last key (masked later)
+      const int64_t roff = ((blk * C::HKV + kvh) * 16 + (key & 15)) * D;
+      const int c = wave == 0 ? (pch ^ (rr & 15)) : (pch ^ ((rr & 3) << 2));
+      dma16<0>(cache + roff + c * 8, img + i * 1024);
+    }
+    return;
+  }
+  const bf16_t* base;
+  int npw;
+  auto gemm_base = [&](const bf16_t* W, int tile, int kch, int wr, int kfull) {
+    return W + ((int64_t)tile * (kfull / KC) + kch) * (int64_t)wr * KC + lane * 8;
+  };
+  int tile, slice;
+  switch (p) {
+    case P_QKV:
+      tile_slice<C::TQ, C::SKQ>(w.t, tile, slice);
+      base = gemm_base(L.qkv, tile, slice * C::CQ + w.k, C::WRQ, C::H);
+      npw = C::WRQ / 8;
+      break;
+    case P_O:
+      tile_slice<C::TO, C::SKO>(w.t, tile, slice);
+      base = gemm_base(L.o, tile, slice * C::CO + w.k, C::WRO, C::HQ * D);
+      npw = C::WRO / 8;
+      break;
+    case P_GU:
+      base = gemm_base(L.gu, w.t, w.k, C::WRG, C::H);
+      npw = C::WRG / 8;
+      break;
+    default:
+      tile_slice<C::TD, C::SKD>(w.t, tile, slice);
+      base = gemm_base(L.dn, tile, slice * C::CD + w.k, C::WRD, C::I);
+      npw = C::WRD / 8;
+      break;
+  }
+  for (int j = 0; j < npw; ++j) {
+    const int piece = 2 * j + wave;
+    dma16<2>(base + piece * 512, slot + piece * 1024);  // nt: each weight byte is read once per step
+  }
+}
+
+// late stream (wave 2): this chunk's activation rows (sc1: produced in this launch) and the task's prologue
+// operands
+template <class C>
+__device__ __forceinline__ void issue_x(const Walk& w, const Rt& r, const DpArgs& a, char* ring, char* scr, int lane) {
+  char* slot = ring + (w.pos % RING);
+  const int p = wp(w), l = wl(r, w);
+  if (p == P_ATT) {
+    if (w.k != 0) return;
+    constexpr int G = C::G, FR = C::SKQ * (G + 2);
+    const int seq = w.t / C::HKV, kvh = w.t - seq * C::HKV;
+    const float* srow = WS<C>::slab_q(a) + (int64_t)seq * C::NQ;
+    const int64_t sstride = (int64_t)XR * C::NQ;
+#pragma unroll
+    for (int i = 0; i < (FR + 1) / 2; ++i) {
+      const int ri = min(2 * i + (lane >> 5), FR - 1);
+      const int sl = ri / (G + 2), j = ri - sl * (G + 2);
+      const int col = j < G ? (kvh * G + j) * D : (j == G ? (C::HQ + kvh) * D : (C::HQ + C::HKV + kvh) * D);
+      dma16<16>(srow + sl * sstride + col + (lane & 31) * 4, scr + i * 1024);
+    }
+    const bool first = l == r.l0;
+    const float* ssp = first ? a.ssp0 : WS<C>::ssp_d(a);
+    const int tiles = first ? a.ssp0_tiles : C::TD;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) dma4(ssp + min(lane + 64 * i, tiles - 1) * DECODE_SSP_LD + seq, scr + S_ASSP + i * 256);
+    const int ctx = __builtin_amdgcn_readfirstlane(a.ctx[seq]);
+    dma16<0>(a.cos_sin + (int64_t)(ctx - 1) * D + (lane & 31) * 4, scr + S_ACOS);
+    return;
+  }
+  const bf16_t* X;
+  int64_t ldx;
+  int k0, wr, tile, slice;
+  switch (p) {
+    case P_QKV:
+      tile_slice<C::TQ, C::SKQ>(w.t, tile, slice);
+      X = a.h; ldx = C::H; k0 = slice * (C::H / C::SKQ); wr = C::WRQ;
+      break;
+    case P_O:
+      tile_slice<C::TO, C::SKO>(w.t, tile, slice);
+      X = WS<C>::attn(a); ldx = C::HQ * D; k0 = slice * (C::HQ * D / C::SKO); wr = C::WRO;
+      break;
+    case P_GU:
+      X = a.h; ldx = C::H; k0 = 0; wr = C::WRG;
+      break;
+    default:
+      tile_slice<C::TD, C::SKD>(w.t, tile, slice);
+      X = WS<C>::act(a); ldx = C::I; k0 = slice * (C::I / C::SKD); wr = C::WRD;
+      break;
+  }
+  char* ximg = slot + wr * ROWB;
+  k0 += w.k * KC;
+#pragma unroll
+  for (int i = 0; i < XR * ROWB / 1024; ++i) {
+    const int rr = 4 * i + (lane >> 4);
+    const int lch = (lane & 15) ^ (rr & 15);
+    dma16<16>(X + (int64_t)min(rr, r.M - 1) * ldx + k0 + lch * 8, ximg + i * 1024);
+  }
+  if (p == P_GU && w.k == 0 && w.t == r.b) {  // the o-projection's per-tile row statistics [tile][0..31]
+#pragma unroll
+    for (int j = 0; j < (C::TO + 7) / 8; ++j) {
+      const int t = min(8 * j + (lane >> 3), C::TO - 1);
+      dma16<16>(WS<C>::ssp_o(a) + t * DECODE_SSP_LD + (lane & 7) * 4, scr + S_STAT + j * 1024);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------
+// dependency counters: sync[(l - l0) * DP_SYNC_LD + phase * NSH + shard]
+template <class C>
+__device__ __forceinline__ int* counter(const DpArgs& a, const Rt& r, int l, int p) {
+  return WS<C>::sync(a) + (l - r.l0) * DP_SYNC_LD + p * NSH;
+}
+
+// phase (l, p) may load its activations: its producer phase has published every task / tile
+template <class C>
+__device__ __forceinline__ bool dep_met(const DpArgs& a, const Rt& r, int l, int p, int lane) {
+  int pl = l, pp, target;
+  switch (p) {
+    case P_QKV:
+      if (l == r.l0) return true;
+      pl = l - 1; pp = P_DN; target = C::TD; break;
+    case P_ATT: pp = P_QKV; target = C::NTQ; break;
+    case P_O: pp = P_ATT; target = r.M * C::HKV; break;
+    case P_GU: pp = P_O; target = C::TO; break;
+    default: pp = P_GU; target = C::NTG; break;
+  }
+  const int* c = counter<C>(a, r, pl, pp);
+  int v = lane < NSH ? __hip_atomic_load(c + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+#pragma unroll
+  for (int o = 4; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return __builtin_amdgcn_readfirstlane(v) >= target;
+}
+
+// bounded wait (wave 3) until phase (l, p)'s producers have all published
+template <class C>
+__device__ __forceinline__ void wait_dep(const DpArgs& a, const Rt& r, int l, int p, int lane) {
+  const long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+  while (!dep_met<C>(a, r, l, p, lane)) {
+    if (__hip_atomic_load(WS<C>::err(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;  // failed
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ll) {  // 2 s: a producer never came
+      if (lane == 0) __hip_atomic_store(WS<C>::err(a), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+template <class C>
+__device__ __forceinline__ void publish(const DpArgs& a, const Rt& r, int l, int p, int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every sc1 store of this wave has been acknowledged
+  if (lane == 0)
+    __hip_atomic_fetch_add(counter<C>(a, r, l, p) + (r.b & (NSH - 1)), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void st_sc1_f4(float* p, f4 v) {
+  __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p, 0, 16, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rs, 0, 0, 16);
+}
+__device__ __forceinline__ void st_sc1_u2(void* p, uint2 v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_u1(void* p, uint32_t v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ f4 ld_sc1_f4(const float* p) {
+  __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, 16, 0x00020000);
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, 0, 16));
+}
+__device__ __forceinline__ uint2 ld_sc1_u2(const void* p) {
+  const unsigned long long v = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+  return __builtin_bit_cast(uint2, v);
+}
+
+// ------------------------------------------------------------------------------------------------------
+// GEMM chunk: wave w takes the 32-deep k-step w of the chunk for both 16-row halves of the activation image
+template <int WR>
+__device__ __forceinline__ void gemm_chunk(const char* slot, f4 (&acc)[2][8], int wave, int lane) {
+  constexpr int NT = WR / 16;
+  const char* ximg = slot + WR * ROWB;
+  const int fr = lane & 15, lch = 4 * wave + (lane >> 4);
+  bf16x8 av[2], bv[NT];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int rr = 16 * mt + fr;
+    av[mt] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ximg + rr * ROWB + 16 * (lch ^ (rr & 15))));
+  }
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int rr = 16 * nt + fr;
+    bv[nt] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(slot + rr * ROWB + 16 * (lch ^ (rr & 15))));
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+      acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt], bv[nt], acc[mt][nt], 0, 0, 0);
+}
+
+template <int WR>
+constexpr int red_ld() { return WR % 32 == 0 ? WR + 16 : WR; }  // LDS row pitch of the partial sums (floats)
+
+// sum the four waves' partials into S_RED in wave order (the multi-launch kernel's order): 0 + w0 + w1 + w2 + w3
+template <int WR>
+__device__ __forceinline__ void reduce_waves(float* red, f4 (&acc)[2][8], int wave, int lane) {
+  constexpr int NT = WR / 16, RS = red_ld<WR>();
+  const int fr = lane & 15, kg = lane >> 4;
+#pragma unroll 1
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float* p = red + (16 * mt + 4 * kg + q) * RS + 16 * nt + fr;
+            *p = (w == 0 ? 0.f : *p) + acc[mt][nt][q];
+          }
+    }
+    lds_fence_barrier();
+  }
+}
+
+__device__ __forceinline__ void zero_acc(f4 (&acc)[2][8]) {
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+}
+
+// qkv epilogue (wave 3): this slice's fp32 partial -> slab_q[slice] (the attention prologue sums the slices)
+template <class C>
+__device__ __forceinline__ void epi_qkv(const float* red, const Rt& r, const DpArgs& a, int t, int lane) {
+  constexpr int WR = C::WRQ, RS = red_ld<WR>(), Q = WR / 4;
+  int tile, slice;
+  tile_slice<C::TQ, C::SKQ>(t, tile, slice);
+  float* dst = WS<C>::slab_q(a) + (int64_t)slice * XR * C::NQ + tile * WR;
+  for (int e = lane; e < XR * Q; e += 64) {
+    const int m = e / Q, j = 4 * (e - m * Q);
+    if (m < r.M) st_sc1_f4(dst + (int64_t)m * C::NQ + j, *reinterpret_cast<const f4*>(red + m * RS + j));
+  }
+}
+
+// o / down epilogue (wave 3): split-K partial -> slab; the last arriver adds every slice into the residual
+// stream (bf16, in place) and writes the tile's row sums of squares (the next RMSNorm's statistics)
+template <int WR, int TILES, int SK, int H>
+__device__ __forceinline__ bool epi_resid(const float* red, const Rt& r, float* slab, bf16_t* hres, int t, int* tick,
+                                          float* ssp, int lane) {
+  constexpr int RS = red_ld<WR>(), Q = WR / 4, EPL = XR * Q / 64;
+  static_assert(Q == 8 || Q == 16 || Q == 32, "a row's float4 groups must sit in one wave");
+  int tile, slice;
+  tile_slice<TILES, SK>(t, tile, slice);
+  const int n0 = tile * WR;
+  f4 own[EPL];
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const int e = lane + 64 * i, m = e / Q, j = 4 * (e - m * Q);
+    own[i] = *reinterpret_cast<const f4*>(red + m * RS + j);
+  }
+  if constexpr (SK > 1) {
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+      const int e = lane + 64 * i, m = e / Q, j = 4 * (e - m * Q);
+      if (m < r.M) st_sc1_f4(slab + ((int64_t)slice * XR + m) * H + n0 + j, own[i]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(tick + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != SK - 1) return false;
+    // last arriver: own + the other slices in slice order (the multi-launch epilogue's order)
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+      const int e = lane + 64 * i, m = min(e / Q, r.M - 1), j = 4 * (e - (e / Q) * Q);
+#pragma unroll
+      for (int s = 0; s < SK; ++s)
+        if (s != slice) own[i] += ld_sc1_f4(slab + ((int64_t)s * XR + m) * H + n0 + j);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const int e = lane + 64 * i, m = e / Q, j = 4 * (e - m * Q);
+    bf16_t* hp = hres + (int64_t)min(m, r.M - 1) * H + n0 + j;
+    const uint2 hr = ld_sc1_u2(hp);
+    const f4 v = own[i];
+    const float hv[4] = {bf2f((bf16_t)(hr.x & 0xffff)) + v[0], bf2f((bf16_t)(hr.x >> 16)) + v[1],
+                         bf2f((bf16_t)(hr.y & 0xffff)) + v[2], bf2f((bf16_t)(hr.y >> 16)) + v[3]};
+    uint2 hw;
+    hw.x = pack2(hv[0], hv[1]);
+    hw.y = pack2(hv[2], hv[3]);
+    float ss = 0.f;
+    if (m < r.M) {
+      st_sc1_u2(hp, hw);
+      const float q0 = bf2f((bf16_t)(hw.x & 0xffff)), q1 = bf2f((bf16_t)(hw.x >> 16));
+      const float q2 = bf2f((bf16_t)(hw.y & 0xffff)), q3 = bf2f((bf16_t)(hw.y >> 16));
+      ss = q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3;
+    }
+#pragma unroll
+    for (int o = Q / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    if (e % Q == 0) st_sc1_u1(ssp + tile * DECODE_SSP_LD + m, __float_as_uint(m < r.M ? ss : 0.f));
+  }
+  if (SK > 1 && lane == 0) __hip_atomic_store(tick + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+// gate/up epilogue (wave 3): RMSNorm row scale (weight folded into W) from the o-projection's statistics (the
+// multi-launch kernel's summation order: 8 tile slices, each summed in tile order), SiLU(gate) * up -> act
+template <class C>
+__device__ __forceinline__ void epi_gu(const float* red, const char* scr, char* ctl, const Rt& r, const DpArgs& a,
+                                       int t, int lane) {
+  constexpr int WR = C::WRG, RS = red_ld<WR>(), NO = WR / 2, NP = NO / 2;
+  float* rs = reinterpret_cast<float*>(ctl + C_RS);
+  if (lane < XR) {
+    const float* st = reinterpret_cast<const float*>(scr + S_STAT);
+    float tot = 0.f;
+#pragma unroll
+    for (int sl = 0; sl < 8; ++sl) {
+      float part = 0.f;
+      for (int tt = sl; tt < C::TO; tt += 8) part += st[tt * 32 + lane];
+      tot += part;
+    }
+    rs[lane] = rsqrtf(tot * a.inv_h + a.eps);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  for (int e = lane; e < XR * NP; e += 64) {
+    const int m = e / NP, j = 2 * (e - m * NP);
+    if (m >= r.M) continue;
+    const float sc = rs[m];
+    const float g0 = red[m * RS + j] * sc, g1 = red[m * RS + j + 1] * sc;
+    const float u0 = red[m * RS + NO + j] * sc, u1 = red[m * RS + NO + j + 1] * sc;
+    const float v0 = g0 / (1.f + __expf(-g0)) * u0, v1 = g1 / (1.f + __expf(-g1)) * u1;
+    st_sc1_u1(WS<C>::act(a) + (int64_t)m * C::I + t * NO + j, pack2(v0, v1));
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------
+// attention prologue (all threads; attention.hip v3 FUSED, same arithmetic): RMSNorm scale of the sequence's
+// row from the statistics tiles, split-K sum of the qkv slab rows, RoPE at position ctx - 1 -> the rotated
+// query image (LDS) and the new token's rotated key / value (registers of threads 0..191, and LDS for wave 3)
+template <int G, int SKQ>
+__device__ __forceinline__ void att_prologue(char* scr, const DpArgs& a, int stat_tiles, int tid, int lane,
+                                             bf16_t& nk0, bf16_t& nk1, bf16_t& nv) {
+  const float* sp = reinterpret_cast<const float*>(scr + S_ASSP);
+  float ssum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) ssum += lane + 64 * i < stat_tiles ? sp[lane + 64 * i] : 0.f;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ssum += __shfl_xor(ssum, o, 64);
+  const float rn = rsqrtf(ssum * a.inv_h + a.eps);
+  const float* cs = reinterpret_cast<const float*>(scr + S_ACOS);
+  const float* sl = reinterpret_cast<const float*>(scr);
+  auto slab_sum = [&](int j, int d) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < SKQ; ++k) v += sl[(k * (G + 2) + j) * D + d];
+    return v * rn;
+  };
+  bf16_t* qimg = reinterpret_cast<bf16_t*>(scr + S_AQ);
+  for (int it = tid; it < G * 64; it += NTH) {
+    const int j = it >> 6, p = it & 63;
+    const float x0 = slab_sum(j, p), x1 = slab_sum(j, p + 64);
+    const float co = cs[p], si = cs[p + 64];
+    qimg[j * D + p] = f2bf(x0 * co - x1 * si);
+    qimg[j * D + p + 64] = f2bf(x1 * co + x0 * si);
+  }
+  bf16_t* nkv = reinterpret_cast<bf16_t*>(scr + S_ANKV);
+  if (tid < 64) {
+    const float x0 = slab_sum(G, tid), x1 = slab_sum(G, tid + 64);
+    const float co = cs[tid], si = cs[tid + 64];
+    nk0 = f2bf(x0 * co - x1 * si);
+    nk1 = f2bf(x1 * co + x0 * si);
+    nkv[tid] = nk0;
+    nkv[tid + 64] = nk1;
+  } else if (tid < 192) {
+    nv = f2bf(slab_sum(G + 1, tid - 64));
+    nkv[D + tid - 64] = nv;
+  }
+}
+
+// the four waves' (m, l, O) merged in wave order (v3's one-part path) -> bf16 output rows of the G heads
+template <class C>
+__device__ __forceinline__ void att_merge_store(const char* scr, const DpArgs& a, int seq, int kvh, int lane) {
+  constexpr int G = C::G;
+  const float* ml = reinterpret_cast<const float*>(scr + S_ML);
+  const float* ob = reinterpret_cast<const float*>(scr + S_OB);
+  for (int e = lane; e < G * (D / 4); e += 64) {
+    const int rr = e / (D / 4), d = 4 * (e % (D / 4));
+    float mw[4], lw[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      mw[w] = ml[(w * 32 + rr) * 2];
+      lw[w] = ml[(w * 32 + rr) * 2 + 1];
+    }
+    float Mx = NEG_BIG;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) Mx = fmaxf(Mx, mw[w]);
+    float L = 0.f;
+    float ac[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float f = exp2f(mw[w] - Mx);
+      L += f * lw[w];
+      const f4 v = *reinterpret_cast<const f4*>(ob + (w * G + rr) * D + d);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ac[q] += f * v[q];
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+    uint2 pk;
+    pk.x = pack2(ac[0] * inv, ac[1] * inv);
+    pk.y = pack2(ac[2] * inv, ac[3] * inv);
+    st_sc1_u2(WS<C>::attn(a) + ((int64_t)seq * C::HQ + kvh * G + rr) * D + d, pk);
+  }
+}
+
+// The stream machinery shared by every task type: per consumed chunk, (A) issue the early stream into the ring,
+// (B) issue the late stream of READY chunks — or wait for the consumed chunk's phase —, (C) counted waits and
+// the chunk barrier; after the compute, (E) a non-blocking look-ahead poll and (F) the slot-free barrier.
+template <class C>
+struct Stream {
+  const DpArgs& a;
+  const Rt& r;
+  char* ring;
+  char* scr;
+  int* ready;
+  int wave, qend;
+  Walk cw, ww, xw;
+  int issued, cum, rq;
+
+  __device__ __forceinline__ Stream(const DpArgs& a_, const Rt& r_, char* ring_, char* scr_, int* ready_, int wave_,
+                                    int qend_)
+      : a(a_), r(r_), ring(ring_), scr(scr_), ready(ready_), wave(wave_), qend(qend_), issued(0), cum(0), rq(0) {
+    walk_begin<C>(cw, r, a, qend);
+    ww = cw;
+    xw = cw;
+  }
+
+  // steps A-C for the chunk cw; returns its slot
+  __device__ __forceinline__ char* begin(int lane) {
+    while (ww.q < qend && ww.pos + chunk_bytes<C>(wp(ww)) <= cw.pos + RING && ww.idx - cw.idx < 16) {
+      if (wave < 2) {
+        issue_w<C>(ww, r, a, ring, wave, lane);
+        issued += w_pieces<C>(wp(ww), wave);
+      }
+      walk_next<C>(ww, r, a, qend);
+    }
+#pragma unroll 1
+    for (;;) {
+      while (xw.idx < ww.idx && xw.q <= rq && !(wp(xw) == P_ATT && xw.k == 0 && xw.idx > cw.idx)) {
+        if (wave == 2) {
+          issue_x<C>(xw, r, a, ring, scr, lane);
+          issued += x_pieces<C>(r, wp(xw), xw.t, xw.k, 2);
+        }
+        walk_next<C>(xw, r, a, qend);
+      }
+      if (xw.idx > cw.idx) break;
+      if (wave == 3) {  // the consumed chunk's activations cannot be loaded yet: wait for its phase
+        wait_dep<C>(a, r, wl(r, cw), wp(cw), lane);
+        if (lane == 0) *ready = cw.q;
+      }
+      lds_fence_barrier();
+      rq = __builtin_amdgcn_readfirstlane(*ready);
+    }
+    if (wave < 3) {
+      const int mine = wave < 2 ? w_pieces<C>(wp(cw), wave) : x_pieces<C>(r, wp(cw), cw.t, cw.k, 2);
+      wait_vm_dyn(issued - (cum + mine));
+      cum += mine;
+    }
+    barrier();
+    return ring + (cw.pos % RING);
+  }
+
+  // steps E-F, then advance to the next chunk
+  __device__ __forceinline__ void end(int lane) {
+    if (wave == 3 && xw.idx < ww.idx && xw.q > rq && dep_met<C>(a, r, wl(r, xw), wp(xw), lane) && lane == 0)
+      *ready = xw.q;
+    lds_fence_barrier();
+    rq = __builtin_amdgcn_readfirstlane(*ready);
+    walk_next<C>(cw, r, a, qend);
+  }
+};
+
+// lane-derived values made opaque per chunk: otherwise the compiler hoists every loop-invariant per-lane
+// address (dozens of 64-bit pointers) out of the loops and spills them
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+template <class C, int WR, int PH>
+__device__ __forceinline__ void gemm_task(Stream<C>& S, char* ctl, int lane0) {
+  constexpr int NT = WR / 16;
+  f4 acc[2][8];
+  zero_acc(acc);
+  const int t = S.cw.t, l = wl(S.r, S.cw), nch = S.cw.nch;
+  const int wave = S.wave;
+#pragma unroll 1
+  for (int k = 0; k < nch; ++k) {
+    const int lane = opaque(lane0);
+    char* slot = S.begin(lane);
+    gemm_chunk<WR>(slot, acc, wave, lane);
+    if (k == nch - 1) {
+      float* red = reinterpret_cast<float*>(S.scr + S_RED);
+      reduce_waves<WR>(red, acc, wave, lane);
+      if (wave == 3) {
+        bool pub = true;
+        if constexpr (PH == P_QKV) epi_qkv<C>(red, S.r, S.a, t, lane);
+        else if constexpr (PH == P_O)
+          pub = epi_resid<WR, C::TO, C::SKO, C::H>(red, S.r, WS<C>::slab_od(S.a), S.a.h, t, WS<C>::tick_o(S.a),
+                                                   WS<C>::ssp_o(S.a), lane);
+        else if constexpr (PH == P_GU) epi_gu<C>(red, S.scr, ctl, S.r, S.a, t, lane);
+        else pub = epi_resid<WR, C::TD, C::SKD, C::H>(red, S.r, WS<C>::slab_od(S.a), S.a.h, t, WS<C>::tick_d(S.a),
+                                                      WS<C>::ssp_d(S.a), lane);
+        if (pub) publish<C>(S.a, S.r, l, PH, lane);
+      }
+    }
+    (void)NT;
+    S.end(lane);
+  }
+}
+
+template <class C>
+__device__ __forceinline__ void att_task(Stream<C>& S, int lane0) {
+  constexpr int G = C::G;
+  const DpArgs& a = S.a;
+  const int t = S.cw.t, l = wl(S.r, S.cw), nch = S.cw.nch;
+  const int wave = S.wave;
+  const int seq = t / C::HKV, kvh = t - seq * C::HKV;
+  const int ctx = __builtin_amdgcn_readfirstlane(a.ctx[seq]);
+  State st;
+  init_state(st);
+  bf16x8_t qf[8];
+  bf16_t nk0 = 0, nk1 = 0, nv = 0;
+#pragma unroll 1
+  for (int k = 0; k < nch; ++k) {
+    const int lane = opaque(lane0);
+    const int tid = wave * 64 + lane, h = lane >> 5, row = lane & 31;
+    char* slot = S.begin(lane);
+    if (k == 0) {
+      att_prologue<G, C::SKQ>(S.scr, a, l == S.r.l0 ? a.ssp0_tiles : C::TD, tid, lane, nk0, nk1, nv);
+      lds_fence_barrier();
+      if (wave == 3) {  // the new token's K / V to the paged cache (for later steps; this one patches LDS)
+        const int64_t sl = a.slots[seq];
+        if (sl >= 0) {
+          const DpLayerW& L = a.layers[l];
+          const int64_t base = ((sl >> 4) * C::HKV + kvh) * 16 * D + (sl & 15) * D;
+          const uint32_t* nkv = reinterpret_cast<const uint32_t*>(S.scr + S_ANKV);
+          reinterpret_cast<uint32_t*>(L.kc + base)[lane] = nkv[lane];
+          reinterpret_cast<uint32_t*>(L.vc + base)[lane] = nkv[64 + lane];
+        }
+      }
+      const bf16_t* qimg = reinterpret_cast<const bf16_t*>(S.scr + S_AQ);
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk)
+        qf[kk] = row < G ? as_frag(*reinterpret_cast<const uint4*>(qimg + row * D + (2 * kk + h) * 8)) : zero_frag();
+    }
+    if (k == nch - 1) {  // patch key ctx - 1 (this step's token) into the chunk's K / V images
+      const int rr = (ctx - 1) - k * DEC_KEYS;
+      const uint32_t kimg = lds_addr(slot) + rr * DEC_ROW, vimg = kimg + DEC_KEYS * DEC_ROW;
+      if (tid < 64) {
+        lds_st16(kimg + 16 * ((tid >> 3) ^ (rr & 15)) + 2 * (tid & 7), nk0);
+        lds_st16(kimg + 16 * (((tid + 64) >> 3) ^ (rr & 15)) + 2 * (tid & 7), nk1);
+      } else if (tid < 192) {
+        const int d = tid - 64;
+        lds_st16(vimg + 16 * ((d >> 3) ^ ((rr & 3) << 2)) + 2 * (d & 7), nv);
+      }
+      lds_fence_barrier();
+    }
+    {
+      const int kb = k * DEC_KEYS + 32 * wave;  // keys >= ctx: clamped rows, masked to -inf
+      f32x16_t sc = qk_lds_swz(slot + 32 * wave * DEC_ROW, qf, lane);
+      softmax_tile_lazy(sc, st, kb, ctx, a.scale_log2, h);
+      pv_lds_swz_v3(slot + DEC_KEYS * DEC_ROW + 32 * wave * DEC_ROW, sc, st, lane);
+    }
+    if (k == nch - 1) {
+      lds_fence_barrier();  // every wave is done with the staging area: the merge reuses it
+      const uint32_t ml = lds_addr(S.scr + S_ML), ob = lds_addr(S.scr + S_OB);
+      if (row < G) {
+        if (h == 0) {  // (uniform base + offset: no divergent generic->LDS pointer casts)
+          lds_st32(ml + 8 * (wave * 32 + row), st.m);
+          lds_st32(ml + 8 * (wave * 32 + row) + 4, st.l);
+        }
+        const uint32_t o = ob + 4 * (wave * G + row) * D;
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4)
+            lds_st128(o + 4 * (32 * db + 8 * g4 + 4 * h),
+                      f32x4_t{st.o[db][4 * g4], st.o[db][4 * g4 + 1], st.o[db][4 * g4 + 2], st.o[db][4 * g4 + 3]});
+      }
+      lds_fence_barrier();
+      if (wave == 3) {
+        att_merge_store<C>(S.scr, a, seq, kvh, lane);
+        publish<C>(a, S.r, l, P_ATT, lane);
+      }
+    }
+    S.end(lane);
+  }
+}
+
+template <class C>
+__global__ void __launch_bounds__(NTH, 1) decode_persistent_kernel(DpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ctl = smem + RING + SCR;
+  const int lane0 = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  Rt r;
+  r.P = gridDim.x;
+  r.b = blockIdx.x;
+  r.M = a.M;
+  r.l0 = a.l0;
+  r.l1 = a.l1;
+  int* ready = reinterpret_cast<int*>(ctl + C_READY);
+  if (threadIdx.x == 0) *ready = 0;  // phase 0 (the first layer's qkv) reads h as it was before the launch
+  lds_fence_barrier();
+  Stream<C> S(a, r, smem, smem + RING, ready, wave, (a.l1 - a.l0) * NPH);
+#pragma unroll 1
+  while (S.cw.q < S.qend) {
+    switch (wp(S.cw)) {
+      case P_QKV: gemm_task<C, C::WRQ, P_QKV>(S, ctl, lane0); break;
+      case P_ATT: att_task<C>(S, lane0); break;
+      case P_O: gemm_task<C, C::WRO, P_O>(S, ctl, lane0); break;
+      case P_GU: gemm_task<C, C::WRG, P_GU>(S, ctl, lane0); break;
+      default: gemm_task<C, C::WRD, P_DN>(S, ctl, lane0); break;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// shape / tile instantiations: Llama-3-8B (32 q / 8 kv heads, hidden 4096, FFN 14336) with the tiles that put
+// one task per CU in every phase, and llama-mini (the GPU tests' model)
+using Cfg8B = Cfg<4096, 14336, 32, 8, 96, 4, 64, 4, 112, 64, 4>;
+using CfgMini = Cfg<1024, 2048, 8, 2, 64, 2, 64, 2, 64, 64, 2>;
+
+template <class C>
+static bool cfg_matches(const DpArgs& a) {
+  return a.H == C::H && a.I == C::I && a.hq == C::HQ && a.hkv == C::HKV;
+}
+
+template <class C>
+static hipError_t launch_cfg(const DpArgs& a, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(a.ws + WS<C>::SYNC, 0, sizeof(int) * DP_SYNC_LD * (a.l1 - a.l0), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(decode_persistent_kernel<C>, dim3(num_cus()), dim3(NTH), LDS_TOTAL, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace dp
+
+// the instantiation for a model shape: its tiles and workspace layout, or false
+bool decode_persistent_config(int H, int I, int hq, int hkv, int layers, int* cfg7, int64_t* lay4) {
+  using namespace dp;
+  auto put = [&](auto c) {
+    using C = decltype(c);
+    const int v[7] = {C::WRQ, C::SKQ, C::WRO, C::SKO, C::WRG, C::WRD, C::SKD};
+    for (int i = 0; i < 7; ++i) cfg7[i] = v[i];
+    lay4[0] = WS<C>::SYNC + (int64_t)4 * DP_SYNC_LD * layers;
+    lay4[1] = WS<C>::ERR;
+    lay4[2] = WS<C>::SYNC;
+    lay4[3] = WS<C>::SLABQ;
+    return true;
+  };
+  if (H == Cfg8B::H && I == Cfg8B::I && hq == Cfg8B::HQ && hkv == Cfg8B::HKV) return put(Cfg8B{});
+  if (H == CfgMini::H && I == CfgMini::I && hq == CfgMini::HQ && hkv == CfgMini::HKV) return put(CfgMini{});
+  return false;
+}
+
+// One persistent launch for layers [l0, l1) of a dense decode step (see the header comment). The caller
+// (bindings.cpp) has validated every shape; here: the counters are zeroed (a memset node under capture)
+// and the instantiation for the shape is launched.
+hipError_t launch_decode_persistent(const DpArgs& a, hipStream_t s) {
+  using namespace dp;
+  if (a.M < 1 || a.M > XR || a.l1 <= a.l0) return hipErrorInvalidValue;
+  if (cfg_matches<Cfg8B>(a)) return launch_cfg<Cfg8B>(a, s);
+  if (cfg_matches<CfgMini>(a)) return launch_cfg<CfgMini>(a, s);
+  return hipErrorInvalidValue;
+}
+
+}  // namespace die

@@ -27,7 +27,8 @@ EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 ARCH = os.environ.get("DIE_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-KERNELS = ["norm_act", "rope_cache", "attention", "sampling", "moe", "gemm_decode", "decode_step", "allreduce"]
+KERNELS = ["norm_act", "rope_cache", "attention", "sampling", "moe", "gemm_decode", "decode_step", "allreduce",
+           "decode_persistent"]
 
 
 def _torch_paths():

@@ -100,6 +100,7 @@ class ModelRunner:
         self._cpar = 0
         self.inflight: Optional[Dict[str, object]] = None  # a queued window whose tokens are not yet read
         self.h_ctl = torch.zeros(2, dtype=i32, pin_memory=pin)   # [window step counter, real rows]
+        self.h_perr = torch.zeros(1, dtype=i32, pin_memory=pin)  # persistent decode kernel's error word
         # numpy views over the pinned buffers (zero-copy) for cheap bulk writes
         self.n_ids, self.n_temp, self.n_topk = self.h_ids.numpy(), self.h_temp.numpy(), self.h_topk.numpy()
         self.n_topp, self.n_seed, self.n_step = self.h_topp.numpy(), self.h_seed.numpy(), self.h_step.numpy()
@@ -129,6 +130,9 @@ class ModelRunner:
             self.attn_cnt = torch.zeros(self.max_seqs * model.hkv, dtype=i32, device=dev)
             self.dec_scratch = (model.alloc_decode_scratch(self.max_seqs) if hasattr(model, "alloc_decode_scratch")
                                 else None)
+            # every decode layer in one persistent launch where the model shape has an instantiation
+            if self.dec_scratch is not None and hasattr(model, "prepare_persistent"):
+                model.prepare_persistent(pool.tensor, self.dec_scratch)
         else:
             self.part_o = self.part_ml = self.attn_cnt = self.dec_scratch = None
         self.supports_swap = type(self)._sync_step is ModelRunner._sync_step
@@ -196,10 +200,16 @@ class ModelRunner:
         return ids[:n].tolist()
 
     def _queue_fault_readback(self) -> None:
-        """Hook: queue device-side error words behind the step (read with the tokens, same sync)."""
+        """Queue device-side error words behind the step (read with the tokens, same sync): the persistent
+        decode kernel's timeout word."""
+        ps = self.dec_scratch.get("persistent") if self.dec_scratch else None
+        if ps is not None:
+            self.h_perr.copy_(ps["err"], non_blocking=True)
 
     def _raise_on_fault(self) -> None:
-        """Hook: raise if a device-side error word read by :meth:`_queue_fault_readback` is set."""
+        """Raise if an error word read by :meth:`_queue_fault_readback` is set."""
+        if self.dec_scratch and self.dec_scratch.get("persistent") is not None and int(self.h_perr[0]):
+            raise RuntimeError("persistent decode step: a dependency wait timed out (outputs invalid)")
 
     # ------------------------------------------------------------ prefill
     KIND_STOP, KIND_PREFILL, KIND_DECODE, KIND_HEARTBEAT = 0, 1, 2, 3
@@ -350,6 +360,7 @@ class ModelRunner:
         for _ in range(k):
             g.replay()
         self.h_tokens[:k].copy_(self.d_tokens[:k], non_blocking=True)
+        self._queue_fault_readback()
         if k_next > 1:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.device))
@@ -357,6 +368,7 @@ class ModelRunner:
             ev.synchronize()
         else:
             torch.cuda.current_stream(self.device).synchronize()
+        self._raise_on_fault()
         return self.h_tokens[:k, :n].tolist()
 
     def _queue_continuation(self, seqs: List[Sequence], pending: int, k: int, base: int) -> None:
@@ -381,6 +393,7 @@ class ModelRunner:
         for _ in range(k):
             g.replay()
         self.h_tokens[base:base + k].copy_(self.d_tokens[base:base + k], non_blocking=True)
+        self._queue_fault_readback()
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
         self.inflight = {"seqs": list(seqs), "k": k, "base": base, "event": ev}
@@ -400,6 +413,7 @@ class ModelRunner:
         if k_next > 1:
             self._queue_continuation(w["seqs"], w["k"], k_next, base=self.k_max - w["base"])
         w["event"].synchronize()
+        self._raise_on_fault()
         b, k, n = w["base"], w["k"], len(w["seqs"])
         return self.h_tokens[b:b + k, :n].tolist()
 

@@ -531,6 +531,39 @@ class CausalLM:
               "ssp_b": torch.zeros(td, ld, dtype=f32, device=dev), "cnt_b": torch.zeros(td, dtype=i32, device=dev)}
         return sc
 
+    def persistent_config(self) -> Optional[dict]:
+        """Tiles / workspace of the persistent decode-step kernel for this model, or None (TP, MoE, unfolded
+        norms, a shape without an instantiation, or DIE_PERSISTENT=0)."""
+        if os.environ.get("DIE_PERSISTENT", "0") == "0" or self.tp.enabled or self.arch.is_moe:
+            return None
+        if not (self.device.type == "cuda" and ops.native_available() and self.norms_folded and self.head_dim == 128):
+            return None
+        return ops.decode_persistent_config(self.arch.hidden_size, self.inter, self.hq, self.hkv, len(self.layers))
+
+    def prepare_persistent(self, kv_pool: torch.Tensor, scratch: Optional[dict]) -> bool:
+        """Set up the persistent decode step for ``kv_pool`` (block size 16): tile-order weight copies for its
+        tiles (KC 128), the per-layer pointer table and the zeroed workspace, kept in ``scratch``. Call before
+        any hipGraph capture (it allocates)."""
+        cfg = self.persistent_config()
+        if cfg is None or scratch is None or kv_pool.shape[4] != 16 or self.hq // self.hkv not in (1, 2, 4, 8):
+            return False
+        tiles = {"qkv": cfg["wrq"], "o": cfg["wro"], "gate_up": cfg["wrg"], "down": cfg["wrd"]}
+        rows = []
+        for li, lw in enumerate(self.layers):
+            ptrs = []
+            for name, wr in tiles.items():
+                key = (name, wr, 128)
+                if key not in lw.tiled:
+                    lw.tiled[key] = ops.gd_pack_weights(getattr(lw, name), wr, silu=name == "gate_up", kc=128)
+                ptrs.append(lw.tiled[key].data_ptr())
+            ptrs += [kv_pool[li, 0].data_ptr(), kv_pool[li, 1].data_ptr()]
+            rows.append(ptrs)
+        table = torch.tensor(rows, dtype=torch.int64, device=self.device)
+        ws = torch.zeros(cfg["ws_bytes"], dtype=torch.uint8, device=self.device)
+        scratch["persistent"] = {"cfg": cfg, "table": table, "ws": ws, "pool_ptr": kv_pool.data_ptr(),
+                                 "err": ws[cfg["err_off"]:cfg["err_off"] + 4].view(torch.int32)}
+        return True
+
     def _fused_decode_ok(self, kv_pool: torch.Tensor, m: int = 32) -> bool:
         g = self.hq // self.hkv
         sq = self.decode_plan(m)["qkv"][2]
@@ -560,6 +593,13 @@ class CausalLM:
             return (getattr(lw, name), False) if t is None else (t, True)
 
         ssp_prev = ops.row_sumsq(h, out=sc["ssp0"])
+        ps = sc.get("persistent")
+        if ps is not None and h.shape[0] <= 32 and ps["pool_ptr"] == kv_pool.data_ptr():
+            # every layer in one persistent launch (weight / KV stream kept running across op boundaries)
+            ops.decode_persistent(ps["ws"], ps["table"], h, ssp_prev, meta.block_tables, meta.ctx_lens,
+                                  meta.slot_mapping, self.cos_sin, kv_pool, 0, len(self.layers), self.inter, hq,
+                                  hkv, self.scale, eps)
+            return ops.rms_norm(h, self.norm, eps)
         for li, lw in enumerate(self.layers):
             k_cache, v_cache = kv_pool[li, 0], kv_pool[li, 1]
             wqkv, tq = tw(lw, "qkv", wq, kq)

@@ -145,6 +145,28 @@ def attn_decode_fused(qkv_slab: torch.Tensor, ssp: torch.Tensor, positions: torc
     return out
 
 
+def decode_persistent_config(hidden: int, inter: int, hq: int, hkv: int, layers: int) -> Optional[dict]:
+    """Tiles and workspace layout of the persistent decode-step kernel (csrc/kernels/decode_persistent.hip) for
+    a model shape, or None when it has no instantiation."""
+    if _C is None:
+        return None
+    v = list(_C.decode_persistent_config(hidden, inter, hq, hkv, layers))
+    if not v:
+        return None
+    keys = ("wrq", "skq", "wro", "sko", "wrg", "wrd", "skd", "ws_bytes", "err_off", "sync_off", "slabq_off")
+    return dict(zip(keys, v))
+
+
+def decode_persistent(ws: torch.Tensor, table: torch.Tensor, h: torch.Tensor, ssp0: torch.Tensor,
+                      block_tables: torch.Tensor, ctx_lens: torch.Tensor, slot_mapping: torch.Tensor,
+                      cos_sin: torch.Tensor, pool: torch.Tensor, l0: int, l1: int, inter: int, hq: int, hkv: int,
+                      scale: float, eps: float) -> None:
+    """Layers [l0, l1) of a dense decode step in ONE persistent launch (h updated in place, the new tokens'
+    K / V written to the pool). ``table`` [L, 6] int64: the layers' packed weight and cache pointers."""
+    _kern().decode_persistent(ws, table, h, ssp0, block_tables, ctx_lens, slot_mapping, cos_sin, pool, l0, l1,
+                              inter, hq, hkv, scale, eps)
+
+
 def decode_advance(out, ids, pos, ctx, slots, bt, step, tokens, cnt, n_real, rows: int, block_size: int) -> None:
     """Device-side advance of the decode inputs (decode_step.hip); see ModelRunner.decode_multi."""
     _kern().decode_advance(out, ids, pos, ctx, slots, bt, step, tokens, cnt, n_real, rows, block_size)

@@ -69,11 +69,13 @@ class TPModelRunner(ModelRunner):
 
     # ------------------------------------------------------------ failure as a unit
     def _queue_fault_readback(self) -> None:
+        super()._queue_fault_readback()
         car = self.tp.car
         if car is not None:
             self.h_fault.copy_(car.error_word(), non_blocking=True)
 
     def _raise_on_fault(self) -> None:
+        super()._raise_on_fault()
         if self.tp.car is not None and int(self.h_fault[0]):
             raise TPGroupFault(f"TP rank {self.tp.rank}: a one-shot collective timed out waiting for a peer; "
                                "its outputs were poisoned and no token of this step is returned")
