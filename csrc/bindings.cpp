@@ -749,9 +749,11 @@ void car_all_reduce(Tensor in, Tensor out, int64_t rank, std::vector<int64_t> bu
 // Persistent decode step (decode_persistent.hip): the instantiation's tiles and workspace layout for a shape.
 std::vector<int64_t> decode_persistent_config(int64_t H, int64_t I, int64_t hq, int64_t hkv, int64_t layers) {
   int cfg[7];
-  int64_t lay[4];
+  int64_t lay[9];
   if (!die::decode_persistent_config((int)H, (int)I, (int)hq, (int)hkv, (int)layers, cfg, lay)) return {};
-  return {cfg[0], cfg[1], cfg[2], cfg[3], cfg[4], cfg[5], cfg[6], lay[0], lay[1], lay[2], lay[3]};
+  std::vector<int64_t> v(cfg, cfg + 7);
+  v.insert(v.end(), lay, lay + 9);
+  return v;
 }
 
 // layers [l0, l1) of a dense decode step in one launch. `table` [L, 6] int64 = per layer the device pointers of
@@ -766,7 +768,7 @@ void decode_persistent(Tensor ws, Tensor table, Tensor h, Tensor ssp0, Tensor bl
   TORCH_CHECK(h.dim() == 2 && h.size(0) >= 1 && h.size(0) <= 32, "h [M <= 32, H]");
   const int64_t M = h.size(0), H = h.size(1), L = table.size(0);
   int cfg[7];
-  int64_t lay[4];
+  int64_t lay[9];
   TORCH_CHECK(die::decode_persistent_config((int)H, (int)I, (int)hq, (int)hkv, (int)L, cfg, lay),
               "decode_persistent: no instantiation for this model shape");
   TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.is_contiguous() && table.dim() == 2 &&
@@ -807,7 +809,7 @@ void decode_persistent(Tensor ws, Tensor table, Tensor h, Tensor ssp0, Tensor bl
   a.M = (int)M;
   a.bt_stride = (int)block_tables.stride(0);
   a.ssp0_tiles = (int)ssp0.size(0);
-  a.scale_log2 = (float)(scale * 1.4426950408889634);
+  a.scale_log2 = (float)scale * 1.4426950408889634f;  // as the attention launchers round it
   a.eps = (float)eps;
   a.inv_h = 1.f / (float)H;
   a.H = (int)H;

@@ -933,10 +933,9 @@ bool decode_persistent_config(int H, int I, int hq, int hkv, int layers, int* cf
     using C = decltype(c);
     const int v[7] = {C::WRQ, C::SKQ, C::WRO, C::SKO, C::WRG, C::WRD, C::SKD};
     for (int i = 0; i < 7; ++i) cfg7[i] = v[i];
-    lay4[0] = WS<C>::SYNC + (int64_t)4 * DP_SYNC_LD * layers;
-    lay4[1] = WS<C>::ERR;
-    lay4[2] = WS<C>::SYNC;
-    lay4[3] = WS<C>::SLABQ;
+    const int64_t v2[9] = {WS<C>::SYNC + (int64_t)4 * DP_SYNC_LD * layers, WS<C>::ERR, WS<C>::SYNC, WS<C>::SLABQ,
+                           WS<C>::ATTN, WS<C>::SLABOD, WS<C>::ACT, WS<C>::SSPO, WS<C>::SSPD};
+    for (int i = 0; i < 9; ++i) lay4[i] = v2[i];
     return true;
   };
   if (H == Cfg8B::H && I == Cfg8B::I && hq == Cfg8B::HQ && hkv == Cfg8B::HKV) return put(Cfg8B{});

@@ -149,8 +149,8 @@ struct DpArgs {
   int H, I, hq, hkv;       // the model shape (selects the instantiation; checked by the launcher)
 };
 // the instantiation for a model shape: cfg7 = {wrq, skq, wro, sko, wrg, wrd, skd} and the workspace layout
-// lay4 = {bytes for `layers` layers, offset of the error word, offset of the counters, offset of slab_q};
-// false if the shape has none
+// lay4[9] = {bytes for `layers` layers, offsets of: the error word, the counters, slab_q, attn, slab_od, act,
+// ssp_o, ssp_d}; false if the shape has none
 bool decode_persistent_config(int H, int I, int hq, int hkv, int layers, int* cfg7, int64_t* lay4);
 hipError_t launch_decode_persistent(const DpArgs& a, hipStream_t s);
 hipError_t launch_ipc_copy(void* dst, const void* src, int64_t nbytes, hipStream_t s);

@@ -29,6 +29,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 KERNELS = ["norm_act", "rope_cache", "attention", "sampling", "moe", "gemm_decode", "decode_step", "allreduce",
            "decode_persistent"]
+CONTRACT_ON = {"attention", "gemm_decode", "decode_persistent"}
 
 
 def _torch_paths():
@@ -68,10 +69,13 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
         src = os.path.join(kdir, k + ".hip")
         obj = os.path.join(OBJ, k + ".o")
         objs.append(obj)
-        if force or _newer(obj, [src] + hdrs):
+        if force or _newer(obj, [src] + hdrs + [os.path.abspath(__file__)]):
             diag = ["-DDIE_KERNEL_DIAG"] if os.environ.get("DIE_KERNEL_DIAG") == "1" else []
-            jobs_list.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *diag, "-I", CSRC,
-                              "-c", src, "-o", obj])
+            # the decode kernels fuse multiply-adds per source expression only (not across statements): the
+            # persistent decode step and the multi-launch path then round identically (bit-exact tests)
+            contract = ["-ffp-contract=on"] if k in CONTRACT_ON else []
+            jobs_list.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *diag, *contract, "-I",
+                              CSRC, "-c", src, "-o", obj])
     bsrc = os.path.join(CSRC, "bindings.cpp")
     bobj = os.path.join(OBJ, "bindings.o")
     objs.append(bobj)

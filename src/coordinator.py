@@ -44,6 +44,7 @@ from src.model_registry import ModelRegistry, rendezvous_score  # noqa: E402
 from src.router import Router, WorkerHealth  # noqa: E402
 from src.rpc import RPCClient, RPCError  # noqa: E402
 from src.utils import (  # noqa: E402
+    CODEC_MSGPACK,
     GLOBAL_TRACER,
     ProtocolError,
     new_request_id,
@@ -93,7 +94,8 @@ class Coordinator:
         # applies while a previous batch for that shard is still in flight.
         self.batcher = Batcher(max_batch_size=max_batch_size, max_latency_ms=max_latency_ms,
                                batch_callback=self._batch_callback, eager_when_idle=True)
-        self.rpc = RPCClient(max_idle_per_host=512)
+        # coordinator -> worker frames in msgpack (C codec: ~3x cheaper than json per hop); clients keep JSON
+        self.rpc = RPCClient(max_idle_per_host=512, codec=CODEC_MSGPACK)
         self.tracer = GLOBAL_TRACER
         self.server: Optional[asyncio.AbstractServer] = None
         self._pending: Dict[str, asyncio.Task] = {}
@@ -410,24 +412,27 @@ class Coordinator:
             return self.dispatch_override
         return "batch" if self._model_arch.get(model, "mock") == "mock" else "stream"
 
-    def _candidates(self, model: str, version: str, shard_id: int, key: str) -> List[Tuple[str, str]]:
-        """Ordered worker candidates: LB choice in the routed shard first, then
-        the shard's other healthy workers, then other healthy shards by key affinity."""
+    def _candidates(self, model: str, version: str, shard_id: int, key: str):
+        """Ordered worker candidates, generated lazily (the fallbacks are only computed after a failure):
+        LB choice in the routed shard first, then the shard's other healthy workers, then other healthy
+        shards by key affinity."""
         lb = self._lb(model, version)
-        out: List[Tuple[str, str]] = []
+        seen: List[Tuple[str, str]] = []
         first = lb.pick(group=str(shard_id))
         if first:
-            out.append(first)
-        for w, addr in lb.workers.items():
-            if lb.groups.get(w) == str(shard_id) and lb.is_healthy(w) and (w, addr) not in out:
-                out.append((w, addr))
+            seen.append(first)
+            yield first
+        for w, addr in list(lb.workers.items()):
+            if lb.groups.get(w) == str(shard_id) and lb.is_healthy(w) and (w, addr) not in seen:
+                seen.append((w, addr))
+                yield w, addr
         others = [s for s in self.router.healthy_shards(model, version) if s.shard_id != shard_id]
         others.sort(key=lambda s: -rendezvous_score(key, s.shard_id))
         for s in others:
             p = lb.pick(group=str(s.shard_id))
-            if p and p not in out:
-                out.append(p)
-        return out
+            if p and p not in seen:
+                seen.append(p)
+                yield p
 
     async def _send(self, model: str, version: str, shard_id: int, key: str, msg: Dict[str, Any],
                     deadline: Optional[float] = None) -> Dict[str, Any]:

@@ -18,6 +18,7 @@ from typing import Any, Dict, List, Optional
 from src.config import ModelConfig
 
 _seq = itertools.count()
+_PREFIX = uuid.uuid4().hex[:12]  # per process: ids stay collision-free across workers without a uuid per request
 
 
 class FakeModel:
@@ -48,7 +49,7 @@ class FakeModel:
             "metadata": {
                 "batch_size": batch_size,
                 "timestamp": time.time(),
-                "request_id": f"req_{uuid.uuid4().hex[:12]}_{next(_seq)}",
+                "request_id": f"req_{_PREFIX}_{next(_seq)}",
             },
         }
 

@@ -153,7 +153,8 @@ def decode_persistent_config(hidden: int, inter: int, hq: int, hkv: int, layers:
     v = list(_C.decode_persistent_config(hidden, inter, hq, hkv, layers))
     if not v:
         return None
-    keys = ("wrq", "skq", "wro", "sko", "wrg", "wrd", "skd", "ws_bytes", "err_off", "sync_off", "slabq_off")
+    keys = ("wrq", "skq", "wro", "sko", "wrg", "wrd", "skd", "ws_bytes", "err_off", "sync_off", "slabq_off",
+            "attn_off", "slabod_off", "act_off", "sspo_off", "sspd_off")
     return dict(zip(keys, v))
 
 

@@ -17,14 +17,21 @@ from __future__ import annotations
 import contextlib
 import json
 import threading
+import itertools
 import time
 import uuid
 from collections import OrderedDict
 from typing import Any, Dict, Iterator, List, Optional
 
 
+_RID_PREFIX = uuid.uuid4().hex[:16]  # per process
+_RID_SEQ = itertools.count()
+
+
 def new_request_id() -> str:
-    return uuid.uuid4().hex
+    """Unique request id: a random per-process prefix + a counter (one uuid4 per request was ~10 us of the
+    coordinator's per-request cost)."""
+    return f"{_RID_PREFIX}{next(_RID_SEQ):016x}"
 
 
 def percentile(values: List[float], q: float) -> float:

@@ -161,13 +161,19 @@ class Worker:
         await self._stop_event.wait()
 
     # -------------------------------------------------------------- network
+    IDLE_TIMEOUT_S = 3600.0
+
     async def _handle_connection(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
         self._conns.add(writer)
+        # an idle connection is dropped after IDLE_TIMEOUT_S by ONE timer re-armed per request (asyncio.wait_for
+        # around every read cost a task + a timer per request: the mock worker's largest per-request cost)
+        loop = asyncio.get_running_loop()
+        idle = [loop.call_later(self.IDLE_TIMEOUT_S, writer.transport.abort)]
         try:
             while True:
                 try:
-                    msg, mode, codec = await asyncio.wait_for(read_message(reader), timeout=3600)
-                except (asyncio.IncompleteReadError, ConnectionError, asyncio.TimeoutError):
+                    msg, mode, codec = await read_message(reader)
+                except (asyncio.IncompleteReadError, ConnectionError):
                     break
                 except (ProtocolError, ValueError) as e:
                     self._error_count += 1
@@ -175,6 +181,8 @@ class Worker:
                         writer.write(pack_frame({"error": f"bad request: {e}", "success": False}))
                         await writer.drain()
                     break
+                idle[0].cancel()
+                idle[0] = loop.call_later(self.IDLE_TIMEOUT_S, writer.transport.abort)
                 if mode == "eof":
                     break  # TCP-connect probe: not a request
                 t0 = time.perf_counter()
@@ -197,6 +205,7 @@ class Worker:
                     break
                 logger.debug("request done in %.2f ms", (time.perf_counter() - t0) * 1e3)
         finally:
+            idle[0].cancel()
             self._conns.discard(writer)
             with contextlib.suppress(Exception):
                 writer.close()

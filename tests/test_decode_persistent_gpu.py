@@ -51,8 +51,11 @@ def _run_both(preset, n_layers, M, ctxs, seed=0):
     ref_sc = {k: v for k, v in sc.items() if k != "persistent"}
     ref_sc["plans"] = {b: plan for b in sc["plans"]}
     outs = {}
-    for name, scratch in (("multi", ref_sc), ("persistent", sc)):
-        p = pool.clone()
+    p_ref = pool.clone()
+    # the persistent step's pointer table is bound to `pool` itself (a clone would silently take the
+    # multi-launch path): the reference runs on a copy made before either step
+    assert sc["persistent"]["pool_ptr"] == pool.data_ptr()
+    for name, scratch, p in (("multi", ref_sc, p_ref), ("persistent", sc, pool)):
         meta = AttnMetadata(False, slots, bt, ctx, max_ctx=max_ctx, scratch=scratch, **meta_kw)
         with torch.inference_mode():
             hid = m.forward(ids, pos, meta, p)
@@ -62,12 +65,12 @@ def _run_both(preset, n_layers, M, ctxs, seed=0):
     return outs, err
 
 
-@pytest.mark.parametrize("M", [32, 7, 1])
-def test_persistent_matches_multi_launch_mini(M):
-    """llama-mini (4 layers, 8 q / 2 kv heads): contexts within one 128-key chunk (the multi-launch attention
-    then also runs one part per pair)."""
+@pytest.mark.parametrize("M,layers", [(32, 1), (32, 4), (7, 4), (1, 4)])
+def test_persistent_matches_multi_launch_mini(M, layers):
+    """llama-mini (8 q / 2 kv heads): contexts within one 128-key chunk (the multi-launch attention then also
+    runs one part per pair)."""
     ctxs = [1 + (37 * i) % 128 for i in range(M)]
-    outs, err = _run_both("llama-mini", 4, M, ctxs)
+    outs, err = _run_both("llama-mini", layers, M, ctxs)
     assert err == 0
     (h0, p0), (h1, p1) = outs["multi"], outs["persistent"]
     assert torch.isfinite(h1.float()).all()
@@ -114,3 +117,61 @@ def test_persistent_repeated_launches_are_identical():
     assert int(sc["persistent"]["err"].item()) == 0
     for r in res[1:]:
         assert torch.equal(r, res[0])
+
+
+@pytest.mark.parametrize("preset,ctxs", [("llama-mini", [1 + (37 * i) % 128 for i in range(32)]),
+                                         ("llama3-8b", [500 + 4 * i for i in range(32)])])
+def test_persistent_intermediates_one_layer(preset, ctxs):
+    """Stage by stage (one layer, 32 rows): the workspace's qkv slabs, attention output, o-projection statistics,
+    SiLU output and down statistics against the same stages of the multi-launch path."""
+    M = 32
+    m, pool, bt, ctx, pos, slots, ids, meta_kw, max_ctx = _setup(preset, 1, M, ctxs)
+    sc = m.alloc_decode_scratch(M)
+    assert m.prepare_persistent(pool, sc)
+    cfg, ws = sc["persistent"]["cfg"], sc["persistent"]["ws"]
+    lw, eps, H, nq = m.layers[0], m.arch.rms_eps, m.arch.hidden_size, (m.hq + 2 * m.hkv) * 128
+
+    def view(off, shape, dt):
+        n = 1
+        for d in shape:
+            n *= d
+        return ws[off:off + n * torch.tensor([], dtype=dt).element_size()].view(dt).view(*shape)
+
+    with torch.inference_mode():
+        h0 = torch.nn.functional.embedding(ids, m.embed)
+        # multi-launch stages with the persistent tiles (on a copy of the pool: the persistent kernel's table
+        # points at `pool` itself)
+        h = h0.clone()
+        p = pool.clone()
+        p2 = pool
+        ssp0 = ops.row_sumsq(h)
+        slab = ops.linear_slab(h, lw.tiled[("qkv", cfg["wrq"], 128)], sk=cfg["skq"], wr=cfg["wrq"], tiled=True, kc=128)
+        attn = ops.attn_decode_fused(slab, ssp0, pos, m.cos_sin, slots, p[0, 0], p[0, 1], bt, ctx, max_ctx, m.hq,
+                                     m.hkv, m.scale, eps, H, meta_kw["part_o"], meta_kw["part_ml"], meta_kw["attn_cnt"])
+        to, td = H // cfg["wro"], H // cfg["wrd"]
+        ssp_a = torch.zeros(to, 128, device=h.device)
+        ssp_b = torch.zeros(td, 128, device=h.device)
+        ops.linear_slab_residual(attn, lw.tiled[("o", cfg["wro"], 128)], h, ssp_a,
+                                 torch.zeros(to, dtype=torch.int32, device=h.device), cfg["wro"], cfg["sko"],
+                                 tiled=True, kc=128)
+        act = ops.linear_silu_mul_rownorm(h, lw.tiled[("gate_up", cfg["wrg"], 128)], ssp_a, eps, cfg["wrg"],
+                                          tiled=True, kc=128)
+        ops.linear_slab_residual(act, lw.tiled[("down", cfg["wrd"], 128)], h, ssp_b,
+                                 torch.zeros(td, dtype=torch.int32, device=h.device), cfg["wrd"], cfg["skd"],
+                                 tiled=True, kc=128)
+        # the persistent kernel on the same inputs
+        h2 = h0.clone()
+        ops.decode_persistent(ws, sc["persistent"]["table"], h2, ops.row_sumsq(h2), bt, ctx, slots, m.cos_sin, p2, 0,
+                              1, m.inter, m.hq, m.hkv, m.scale, eps)
+        torch.cuda.synchronize()
+    got = {
+        "slab_q": view(cfg["slabq_off"], (cfg["skq"], 32, nq), torch.float32)[:, :M],
+        "attn": view(cfg["attn_off"], (32, m.hq * 128), torch.bfloat16)[:M],
+        "ssp_o": view(cfg["sspo_off"], (to, 128), torch.float32)[:, :M],
+        "act": view(cfg["act_off"], (32, m.inter), torch.bfloat16)[:M],
+        "ssp_d": view(cfg["sspd_off"], (td, 128), torch.float32)[:, :M],
+        "h": h2, "kv": p2,
+    }
+    want = {"slab_q": slab, "attn": attn, "ssp_o": ssp_a[:, :M], "act": act, "ssp_d": ssp_b[:, :M], "h": h, "kv": p}
+    bad = {k: float((got[k].float() - want[k].float()).abs().max()) for k in want if not torch.equal(got[k], want[k])}
+    assert not bad, bad
