@@ -2,6 +2,8 @@
 // validates device/dtype/shape up front and throws on mismatch — a wrong shape
 // never reaches a kernel (a faulting kernel can take down every GPU on the
 // host) — then launches on the current HIP stream (graph-capture safe).
+#include <cstdlib>
+
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
@@ -761,7 +763,7 @@ std::vector<int64_t> decode_persistent_config(int64_t H, int64_t I, int64_t hq, 
 // tensors it keeps alive); `pool` [L, 2, blocks, hkv, 16, 128] is only checked against the table's geometry.
 void decode_persistent(Tensor ws, Tensor table, Tensor h, Tensor ssp0, Tensor block_tables, Tensor ctx_lens,
                        Tensor slot_mapping, Tensor cos_sin, Tensor pool, int64_t l0, int64_t l1, int64_t I,
-                       int64_t hq, int64_t hkv, double scale, double eps) {
+                       int64_t hq, int64_t hkv, double scale, double eps, c10::optional<Tensor> prof) {
   DIE_CHECK_CUDA(h);
   DIE_CHECK_BF16(h);
   DIE_CHECK_CONTIG(h);
@@ -816,6 +818,16 @@ void decode_persistent(Tensor ws, Tensor table, Tensor h, Tensor ssp0, Tensor bl
   a.I = (int)I;
   a.hq = (int)hq;
   a.hkv = (int)hkv;
+  if (prof.has_value()) {  // timeline stamps (written only by DIE_KERNEL_DIAG builds)
+    int dev = 0, ncu = 0;
+    DIE_HIP(hipGetDevice(&dev));
+    DIE_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    TORCH_CHECK(prof->is_cuda() && prof->scalar_type() == at::kLong && prof->is_contiguous() &&
+                    prof->numel() >= (int64_t)ncu * ((l1 - l0) * 5 * 4 + 32), "prof [grid, phases * 4 + 32] int64");
+    a.prof = reinterpret_cast<uint64_t*>(prof->data_ptr());
+    const char* dbg = std::getenv("DIE_DP_DBG");  // experiment switches, read only by diagnostic builds
+    a.dbg = dbg ? std::atoi(dbg) : 0;
+  }
   DIE_HIP(die::launch_decode_persistent(a, cur_stream()));
 }
 

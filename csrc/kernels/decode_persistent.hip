@@ -53,7 +53,9 @@ constexpr int XR = 32;                       // activation rows per chunk (decod
 constexpr int KC = 128;                      // K per GEMM chunk
 constexpr int ROWB = 256;                    // bytes per GEMM image row
 constexpr int ACH = 65536;                   // attention chunk: 128 keys of K + V
-constexpr int NSH = 8;                       // counter shards
+constexpr int NSH = 64;                      // counter shards (one per lane of the polling wave)
+constexpr int LINEI = 32;                    // ints per 128-byte line: every shard / ticket on its own line
+                                             // (same-line atomics from 256 CUs serialise: ~80 us per phase)
 constexpr int NPH = 5;
 enum { P_QKV = 0, P_ATT = 1, P_O = 2, P_GU = 3, P_DN = 4 };
 // SCR layout. GEMM tasks:
@@ -74,12 +76,34 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f4;
 typedef __attribute__((ext_vector_type(4))) unsigned u4;
 
+extern __shared__ __attribute__((aligned(16))) char dp_smem[];
+__device__ __forceinline__ uint32_t lds_of(const void* p);
+__device__ __forceinline__ lds_void* lds_ptr(const void* p) {  // (integer -> LDS pointer: no null check)
+  return reinterpret_cast<lds_void*>((uintptr_t)lds_of(p));
+}
 template <int AUX>
 __device__ __forceinline__ void dma16(const void* src, char* lds) {
-  __builtin_amdgcn_global_load_lds((global_cvoid*)src, (lds_void*)lds, 16, 0, AUX);
+  __builtin_amdgcn_global_load_lds((global_cvoid*)src, lds_ptr(lds), 16, 0, AUX);
 }
 __device__ __forceinline__ void dma4(const void* src, char* lds) {
-  __builtin_amdgcn_global_load_lds((global_cvoid*)src, (lds_void*)lds, 4, 0, 16);
+  __builtin_amdgcn_global_load_lds((global_cvoid*)src, lds_ptr(lds), 4, 0, 16);
+}
+
+// Read-only launch inputs (layer table, block tables, context lengths, slots) are wave-uniform: scalar loads.
+// As vector loads, each use would wait for vmcnt and so drain the loader waves' prefetch stream.
+__device__ __forceinline__ int sld_i32(const void* p) {
+  int v;
+  asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p));
+  return v;
+}
+__device__ __forceinline__ int64_t sld_i64(const void* p) {
+  int64_t v;
+  asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p));
+  return v;
+}
+template <class T>
+__device__ __forceinline__ T* lw_ptr(T* const* field) {  // a pointer field of the layer table
+  return reinterpret_cast<T*>(sld_i64(field));
 }
 
 #define DP_W1(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
@@ -93,6 +117,12 @@ __device__ __forceinline__ void wait_vm_dyn(int n) {
 }
 #undef DP_W8
 #undef DP_W1
+
+// the kernel's LDS; LDS addresses of pointers into it are taken as (symbol + byte offset): an address-space
+// cast of a pointer the compiler holds in VGPRs ICEs instruction selection on this toolchain
+__device__ __forceinline__ uint32_t lds_of(const void* p) {
+  return lds_addr(dp_smem) + (uint32_t)(reinterpret_cast<const char*>(p) - dp_smem);
+}
 
 __device__ __forceinline__ void barrier() { __builtin_amdgcn_s_barrier(); }
 __device__ __forceinline__ void lds_fence_barrier() {
@@ -128,10 +158,10 @@ struct WS {
   static constexpr int64_t ACT = a16(SLABOD + (int64_t)SKOD * XR * C::H * 4);   // bf16 [32][I]
   static constexpr int64_t SSPO = a16(ACT + (int64_t)XR * C::I * 2);           // f32 [TO][128]
   static constexpr int64_t SSPD = a16(SSPO + (int64_t)C::TO * 128 * 4);        // f32 [TD][128]
-  static constexpr int64_t TICKO = a16(SSPD + (int64_t)C::TD * 128 * 4);       // i32 [TO]
-  static constexpr int64_t TICKD = a16(TICKO + (int64_t)C::TO * 4);            // i32 [TD]
-  static constexpr int64_t ERR = a16(TICKD + (int64_t)C::TD * 4);              // i32 [4]
-  static constexpr int64_t SYNC = ERR + 16;                                    // i32 [layers][DP_SYNC_LD]
+  static constexpr int64_t TICKO = (SSPD + (int64_t)C::TD * 128 * 4 + 127) / 128 * 128;  // i32 [TO][32]
+  static constexpr int64_t TICKD = TICKO + (int64_t)C::TO * 128;              // i32 [TD][32]
+  static constexpr int64_t ERR = TICKD + (int64_t)C::TD * 128;                // i32 [32]
+  static constexpr int64_t SYNC = ERR + 128;                                  // i32 [layers][DP_SYNC_LD]
   static __device__ __forceinline__ float* slab_q(const DpArgs& a) { return reinterpret_cast<float*>(a.ws + SLABQ); }
   static __device__ __forceinline__ bf16_t* attn(const DpArgs& a) { return reinterpret_cast<bf16_t*>(a.ws + ATTN); }
   static __device__ __forceinline__ float* slab_od(const DpArgs& a) { return reinterpret_cast<float*>(a.ws + SLABOD); }
@@ -146,7 +176,13 @@ struct WS {
 
 struct Rt {  // run-time uniforms
   int P, b, M, l0, l1;
+  int dbg;  // diagnostic builds: experiment switches (DpArgs::dbg); 0 otherwise
 };
+#ifdef DIE_KERNEL_DIAG
+#define DP_DBG(r) ((r).dbg)
+#else
+#define DP_DBG(r) 0
+#endif
 
 template <class C>
 __device__ __forceinline__ int ntasks(const Rt& r, int p) {
@@ -197,7 +233,7 @@ template <class C>
 __device__ __forceinline__ int task_chunks(const DpArgs& a, int p, int t) {
   switch (p) {
     case P_QKV: return C::CQ;
-    case P_ATT: return (__builtin_amdgcn_readfirstlane(a.ctx[t / C::HKV]) + DEC_KEYS - 1) / DEC_KEYS;
+    case P_ATT: return (sld_i32(a.ctx + t / C::HKV) + DEC_KEYS - 1) / DEC_KEYS;
     case P_O: return C::CO;
     case P_GU: return C::CG;
     default: return C::CD;
@@ -264,18 +300,18 @@ template <class C>
 __device__ __forceinline__ void issue_w(const Walk& w, const Rt& r, const DpArgs& a, char* ring, int wave, int lane) {
   char* slot = ring + (w.pos % RING);
   const int p = wp(w);
-  const DpLayerW& L = a.layers[wl(r, w)];
+  const DpLayerW* L = a.layers + wl(r, w);
   if (p == P_ATT) {
     const int seq = w.t / C::HKV, kvh = w.t - seq * C::HKV;
-    const int ctx = __builtin_amdgcn_readfirstlane(a.ctx[seq]);
+    const int ctx = sld_i32(a.ctx + seq);
     const int* bt = a.bt + (int64_t)seq * a.bt_stride;
-    const bf16_t* cache = wave == 0 ? L.kc : L.vc;
+    const bf16_t* cache = lw_ptr(wave == 0 ? &L->kc : &L->vc);
     char* img = slot + wave * (DEC_KEYS * DEC_ROW);
     const int pch = lane & 15;
 #pragma unroll 4
     for (int i = 0; i < 32; ++i) {
       const int kr0 = w.k * DEC_KEYS + 4 * i;
-      const int64_t blk = bt[__builtin_amdgcn_readfirstlane(min(kr0, ctx - 1) >> 4)];
+      const int64_t blk = sld_i32(bt + (min(kr0, ctx - 1) >> 4));
       const int rr = 4 * i + (lane >> 4);
       const int key = min(kr0 + (lane >> 4), ctx - 1);  // past the context: the last key (masked later)
       const int64_t roff = ((blk * C::HKV + kvh) * 16 + (key & 15)) * D;
@@ -293,21 +329,21 @@ __device__ __forceinline__ void issue_w(const Walk& w, const Rt& r, const DpArgs
   switch (p) {
     case P_QKV:
       tile_slice<C::TQ, C::SKQ>(w.t, tile, slice);
-      base = gemm_base(L.qkv, tile, slice * C::CQ + w.k, C::WRQ, C::H);
+      base = gemm_base(lw_ptr(&L->qkv), tile, slice * C::CQ + w.k, C::WRQ, C::H);
       npw = C::WRQ / 8;
       break;
     case P_O:
       tile_slice<C::TO, C::SKO>(w.t, tile, slice);
-      base = gemm_base(L.o, tile, slice * C::CO + w.k, C::WRO, C::HQ * D);
+      base = gemm_base(lw_ptr(&L->o), tile, slice * C::CO + w.k, C::WRO, C::HQ * D);
       npw = C::WRO / 8;
       break;
     case P_GU:
-      base = gemm_base(L.gu, w.t, w.k, C::WRG, C::H);
+      base = gemm_base(lw_ptr(&L->gu), w.t, w.k, C::WRG, C::H);
       npw = C::WRG / 8;
       break;
     default:
       tile_slice<C::TD, C::SKD>(w.t, tile, slice);
-      base = gemm_base(L.dn, tile, slice * C::CD + w.k, C::WRD, C::I);
+      base = gemm_base(lw_ptr(&L->dn), tile, slice * C::CD + w.k, C::WRD, C::I);
       npw = C::WRD / 8;
       break;
   }
@@ -341,7 +377,7 @@ __device__ __forceinline__ void issue_x(const Walk& w, const Rt& r, const DpArgs
     const int tiles = first ? a.ssp0_tiles : C::TD;
 #pragma unroll
     for (int i = 0; i < 2; ++i) dma4(ssp + min(lane + 64 * i, tiles - 1) * DECODE_SSP_LD + seq, scr + S_ASSP + i * 256);
-    const int ctx = __builtin_amdgcn_readfirstlane(a.ctx[seq]);
+    const int ctx = sld_i32(a.ctx + seq);
     dma16<0>(a.cos_sin + (int64_t)(ctx - 1) * D + (lane & 31) * 4, scr + S_ACOS);
     return;
   }
@@ -371,7 +407,10 @@ __device__ __forceinline__ void issue_x(const Walk& w, const Rt& r, const DpArgs
   for (int i = 0; i < XR * ROWB / 1024; ++i) {
     const int rr = 4 * i + (lane >> 4);
     const int lch = (lane & 15) ^ (rr & 15);
-    dma16<16>(X + (int64_t)min(rr, r.M - 1) * ldx + k0 + lch * 8, ximg + i * 1024);
+    if (DP_DBG(r) & 1)
+      dma16<0>(X + (int64_t)min(rr, r.M - 1) * ldx + k0 + lch * 8, ximg + i * 1024);
+    else
+      dma16<16>(X + (int64_t)min(rr, r.M - 1) * ldx + k0 + lch * 8, ximg + i * 1024);
   }
   if (p == P_GU && w.k == 0 && w.t == r.b) {  // the o-projection's per-tile row statistics [tile][0..31]
 #pragma unroll
@@ -383,30 +422,42 @@ __device__ __forceinline__ void issue_x(const Walk& w, const Rt& r, const DpArgs
 }
 
 // ------------------------------------------------------------------------------------------------------
-// dependency counters: sync[(l - l0) * DP_SYNC_LD + phase * NSH + shard]
+// dependency counters: sync[(l - l0) * DP_SYNC_LD + (phase * NSH + shard) * LINEI]
 template <class C>
 __device__ __forceinline__ int* counter(const DpArgs& a, const Rt& r, int l, int p) {
-  return WS<C>::sync(a) + (l - r.l0) * DP_SYNC_LD + p * NSH;
+  return WS<C>::sync(a) + (l - r.l0) * DP_SYNC_LD + p * NSH * LINEI;
 }
 
-// phase (l, p) may load its activations: its producer phase has published every task / tile
+// phase (l, p) may load its activations once its producer phase has published every task / tile: the
+// producer's counter (nullptr: produced before the launch) and the count it reaches
 template <class C>
-__device__ __forceinline__ bool dep_met(const DpArgs& a, const Rt& r, int l, int p, int lane) {
-  int pl = l, pp, target;
+__device__ __forceinline__ const int* dep_src(const DpArgs& a, const Rt& r, int l, int p, int& target) {
+  int pl = l, pp;
   switch (p) {
     case P_QKV:
-      if (l == r.l0) return true;
+      if (l == r.l0) return nullptr;
       pl = l - 1; pp = P_DN; target = C::TD; break;
     case P_ATT: pp = P_QKV; target = C::NTQ; break;
     case P_O: pp = P_ATT; target = r.M * C::HKV; break;
     case P_GU: pp = P_O; target = C::TO; break;
     default: pp = P_GU; target = C::NTG; break;
   }
-  const int* c = counter<C>(a, r, pl, pp);
-  int v = lane < NSH ? __hip_atomic_load(c + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  return counter<C>(a, r, pl, pp);
+}
+// one shard per lane (a relaxed agent-scope load; the caller may consume it a chunk later)
+__device__ __forceinline__ int dep_load(const int* c, int lane) {
+  return __hip_atomic_load(c + lane * LINEI, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool dep_sum_met(int v, int target) {
 #pragma unroll
-  for (int o = 4; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return __builtin_amdgcn_readfirstlane(v) >= target;
+}
+template <class C>
+__device__ __forceinline__ bool dep_met(const DpArgs& a, const Rt& r, int l, int p, int lane) {
+  int target = 0;
+  const int* c = dep_src<C>(a, r, l, p, target);
+  return c == nullptr || dep_sum_met(dep_load(c, lane), target);
 }
 
 // bounded wait (wave 3) until phase (l, p)'s producers have all published
@@ -427,12 +478,23 @@ template <class C>
 __device__ __forceinline__ void publish(const DpArgs& a, const Rt& r, int l, int p, int lane) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every sc1 store of this wave has been acknowledged
   if (lane == 0)
-    __hip_atomic_fetch_add(counter<C>(a, r, l, p) + (r.b & (NSH - 1)), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(counter<C>(a, r, l, p) + (r.b & (NSH - 1)) * LINEI, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ void st_sc1_f4(float* p, f4 v) {
-  __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p, 0, 16, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rs, 0, 0, 16);
+// sc1 vector accesses through a buffer resource. The resource lives in SGPRs, so its base MUST be
+// wave-uniform (a per-lane base makes the compiler wrap every access in a 64-iteration waterfall loop); the
+// per-lane part is the 32-bit byte offset.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* uniform_base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uniform_base), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void st_sc1_f4(__amdgpu_buffer_rsrc_t rs, int off, f4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rs, off, 0, 16);
+}
+__device__ __forceinline__ f4 ld_sc1_f4(__amdgpu_buffer_rsrc_t rs, int off) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
+}
+__device__ __forceinline__ uint2 ld_sc1_u2(__amdgpu_buffer_rsrc_t rs, int off) {
+  return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 16));
 }
 __device__ __forceinline__ void st_sc1_u2(void* p, uint2 v) {
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
@@ -441,83 +503,91 @@ __device__ __forceinline__ void st_sc1_u2(void* p, uint2 v) {
 __device__ __forceinline__ void st_sc1_u1(void* p, uint32_t v) {
   __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ f4 ld_sc1_f4(const float* p) {
-  __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, 16, 0x00020000);
-  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, 0, 16));
-}
-__device__ __forceinline__ uint2 ld_sc1_u2(const void* p) {
-  const unsigned long long v = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-  return __builtin_bit_cast(uint2, v);
-}
 
 // ------------------------------------------------------------------------------------------------------
-// GEMM chunk: wave w takes the 32-deep k-step w of the chunk for both 16-row halves of the activation image
+// GEMM chunk, split over the waves by output columns: wave w owns the 16-column tiles w, w + 4 (< WR / 16) and
+// runs all four 32-deep k-steps of the chunk for both 16-row halves of the activation image — no cross-wave
+// reduction at the end of a task, so the loader waves never read the partial sums back through LDS
 template <int WR>
-__device__ __forceinline__ void gemm_chunk(const char* slot, f4 (&acc)[2][8], int wave, int lane) {
-  constexpr int NT = WR / 16;
+__device__ __forceinline__ void gemm_chunk(const char* slot, f4 (&acc)[2][2], int wave, int lane) {
+  constexpr int NT = WR / 16, NTW = (NT + 3) / 4;  // tiles per wave (a wave short of NTW repeats its last:
+                                                   // unconditional MFMAs keep the accumulators in AGPRs)
   const char* ximg = slot + WR * ROWB;
-  const int fr = lane & 15, lch = 4 * wave + (lane >> 4);
-  bf16x8 av[2], bv[NT];
+  const int fr = lane & 15;
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    const int rr = 16 * mt + fr;
-    av[mt] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ximg + rr * ROWB + 16 * (lch ^ (rr & 15))));
-  }
+  for (int ks = 0; ks < 4; ++ks) {
+    const int lch = 4 * ks + (lane >> 4);
+    bf16x8 av[2], bv[NTW];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int rr = 16 * nt + fr;
-    bv[nt] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(slot + rr * ROWB + 16 * (lch ^ (rr & 15))));
-  }
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-      acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt], bv[nt], acc[mt][nt], 0, 0, 0);
-}
-
-template <int WR>
-constexpr int red_ld() { return WR % 32 == 0 ? WR + 16 : WR; }  // LDS row pitch of the partial sums (floats)
-
-// sum the four waves' partials into S_RED in wave order (the multi-launch kernel's order): 0 + w0 + w1 + w2 + w3
-template <int WR>
-__device__ __forceinline__ void reduce_waves(float* red, f4 (&acc)[2][8], int wave, int lane) {
-  constexpr int NT = WR / 16, RS = red_ld<WR>();
-  const int fr = lane & 15, kg = lane >> 4;
-#pragma unroll 1
-  for (int w = 0; w < 4; ++w) {
-    if (wave == w) {
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            float* p = red + (16 * mt + 4 * kg + q) * RS + 16 * nt + fr;
-            *p = (w == 0 ? 0.f : *p) + acc[mt][nt][q];
-          }
+    for (int mt = 0; mt < 2; ++mt) {
+      const int rr = 16 * mt + fr;
+      av[mt] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ximg + rr * ROWB + 16 * (lch ^ (rr & 15))));
     }
-    lds_fence_barrier();
+#pragma unroll
+    for (int i = 0; i < NTW; ++i) {
+      const int rr = 16 * min(wave + 4 * i, NT - 1) + fr;
+      bv[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(slot + rr * ROWB + 16 * (lch ^ (rr & 15))));
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int i = 0; i < NTW; ++i) acc[mt][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt], bv[i], acc[mt][i], 0, 0, 0);
   }
 }
 
-__device__ __forceinline__ void zero_acc(f4 (&acc)[2][8]) {
+template <int WR>
+constexpr int red_ld() { return WR % 32 == 0 ? WR + 16 : WR; }  // LDS row pitch of the tile sums (floats)
+
+// every wave's finished column tiles -> S_RED [32 rows][RS] (asm LDS writes: no compiler-inserted vmcnt wait
+// in the loader waves), then one barrier
+template <int WR>
+__device__ __forceinline__ void stash_tiles(float* red, const f4 (&acc)[2][2], int wave, int lane) {
+  constexpr int NT = WR / 16, NTW = (NT + 3) / 4, RS = red_ld<WR>();
+  const int fr = lane & 15, kg = lane >> 4;
+  const uint32_t base = lds_of(red);
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-    for (int nt = 0; nt < 8; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < NTW; ++i)
+      if (wave + 4 * i < NT)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          lds_st32(base + 4 * ((16 * mt + 4 * kg + q) * RS + 16 * (wave + 4 * i) + fr), acc[mt][i][q]);
+  lds_fence_barrier();
 }
+
+__device__ __forceinline__ void zero_acc(f4 (&acc)[2][2]) {
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) acc[mt][i] = f4{0.f, 0.f, 0.f, 0.f};
+}
+
+// The epilogues below run in wave 3 alone and are written as load batch -> arithmetic -> store batch:
+// vmcnt counts stores too, so a load or LDS read placed after a store would wait for that store's
+// write-through round trip (one serialised round trip per row otherwise). sched_fence() keeps the batches
+// apart.
+__device__ __forceinline__ void sched_fence() { asm volatile("" ::: "memory"); }
 
 // qkv epilogue (wave 3): this slice's fp32 partial -> slab_q[slice] (the attention prologue sums the slices)
 template <class C>
 __device__ __forceinline__ void epi_qkv(const float* red, const Rt& r, const DpArgs& a, int t, int lane) {
-  constexpr int WR = C::WRQ, RS = red_ld<WR>(), Q = WR / 4;
+  constexpr int WR = C::WRQ, RS = red_ld<WR>(), Q = WR / 4, EPL = XR * Q / 64;
+  static_assert(XR * Q % 64 == 0, "whole float4 groups per lane");
   int tile, slice;
   tile_slice<C::TQ, C::SKQ>(t, tile, slice);
-  float* dst = WS<C>::slab_q(a) + (int64_t)slice * XR * C::NQ + tile * WR;
-  for (int e = lane; e < XR * Q; e += 64) {
-    const int m = e / Q, j = 4 * (e - m * Q);
-    if (m < r.M) st_sc1_f4(dst + (int64_t)m * C::NQ + j, *reinterpret_cast<const f4*>(red + m * RS + j));
+  const auto dst = brsrc(WS<C>::slab_q(a) + (int64_t)slice * XR * C::NQ + tile * WR);
+  f4 v[EPL];
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const int e = lane + 64 * i, m = e / Q, j = 4 * (e - m * Q);
+    v[i] = *reinterpret_cast<const f4*>(red + m * RS + j);
+  }
+  sched_fence();
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const int e = lane + 64 * i, m = e / Q, j = 4 * (e - m * Q);
+    if (m < r.M) st_sc1_f4(dst, 4 * (m * C::NQ + j), v[i]);
   }
 }
 
@@ -531,55 +601,76 @@ __device__ __forceinline__ bool epi_resid(const float* red, const Rt& r, float* 
   int tile, slice;
   tile_slice<TILES, SK>(t, tile, slice);
   const int n0 = tile * WR;
+  const auto rslab = brsrc(slab + n0), rh = brsrc(hres + n0);
   f4 own[EPL];
 #pragma unroll
   for (int i = 0; i < EPL; ++i) {
     const int e = lane + 64 * i, m = e / Q, j = 4 * (e - m * Q);
     own[i] = *reinterpret_cast<const f4*>(red + m * RS + j);
   }
+  sched_fence();
   if constexpr (SK > 1) {
 #pragma unroll
     for (int i = 0; i < EPL; ++i) {
       const int e = lane + 64 * i, m = e / Q, j = 4 * (e - m * Q);
-      if (m < r.M) st_sc1_f4(slab + ((int64_t)slice * XR + m) * H + n0 + j, own[i]);
+      if (m < r.M) st_sc1_f4(rslab, 4 * ((slice * XR + m) * H + j), own[i]);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(tick + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) old = __hip_atomic_fetch_add(tick + tile * LINEI, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     old = __builtin_amdgcn_readfirstlane(old);
     if (old != SK - 1) return false;
-    // last arriver: own + the other slices in slice order (the multi-launch epilogue's order)
-#pragma unroll
-    for (int i = 0; i < EPL; ++i) {
-      const int e = lane + 64 * i, m = min(e / Q, r.M - 1), j = 4 * (e - (e / Q) * Q);
-#pragma unroll
-      for (int s = 0; s < SK; ++s)
-        if (s != slice) own[i] += ld_sc1_f4(slab + ((int64_t)s * XR + m) * H + n0 + j);
-    }
   }
+  // (last arriver) one batch of loads: the residual rows and the other slices' partials
+  uint2 hr[EPL];
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const int e = lane + 64 * i, m = min(e / Q, r.M - 1), j = 4 * (e - (e / Q) * Q);
+    hr[i] = ld_sc1_u2(rh, 2 * (m * H + j));
+  }
+  if constexpr (SK > 1) {
+    f4 oth[SK - 1][EPL];
+#pragma unroll
+    for (int s = 0; s < SK - 1; ++s) {
+      const int sidx = s < slice ? s : s + 1;
+#pragma unroll
+      for (int i = 0; i < EPL; ++i) {
+        const int e = lane + 64 * i, m = min(e / Q, r.M - 1), j = 4 * (e - (e / Q) * Q);
+        oth[s][i] = ld_sc1_f4(rslab, 4 * ((sidx * XR + m) * H + j));
+      }
+    }
+    // own + the other slices in slice order (the multi-launch epilogue's order)
+#pragma unroll
+    for (int s = 0; s < SK - 1; ++s)
+#pragma unroll
+      for (int i = 0; i < EPL; ++i) own[i] += oth[s][i];
+  }
+  uint2 hw[EPL];
+  float ss[EPL];
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const int e = lane + 64 * i, m = e / Q;
+    const f4 v = own[i];
+    const float hv[4] = {bf2f((bf16_t)(hr[i].x & 0xffff)) + v[0], bf2f((bf16_t)(hr[i].x >> 16)) + v[1],
+                         bf2f((bf16_t)(hr[i].y & 0xffff)) + v[2], bf2f((bf16_t)(hr[i].y >> 16)) + v[3]};
+    hw[i].x = pack2(hv[0], hv[1]);
+    hw[i].y = pack2(hv[2], hv[3]);
+    const float q0 = bf2f((bf16_t)(hw[i].x & 0xffff)), q1 = bf2f((bf16_t)(hw[i].x >> 16));
+    const float q2 = bf2f((bf16_t)(hw[i].y & 0xffff)), q3 = bf2f((bf16_t)(hw[i].y >> 16));
+    ss[i] = m < r.M ? q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3 : 0.f;
+  }
+#pragma unroll
+  for (int o = Q / 2; o > 0; o >>= 1)
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) ss[i] += __shfl_xor(ss[i], o, 64);
+  sched_fence();
 #pragma unroll
   for (int i = 0; i < EPL; ++i) {
     const int e = lane + 64 * i, m = e / Q, j = 4 * (e - m * Q);
-    bf16_t* hp = hres + (int64_t)min(m, r.M - 1) * H + n0 + j;
-    const uint2 hr = ld_sc1_u2(hp);
-    const f4 v = own[i];
-    const float hv[4] = {bf2f((bf16_t)(hr.x & 0xffff)) + v[0], bf2f((bf16_t)(hr.x >> 16)) + v[1],
-                         bf2f((bf16_t)(hr.y & 0xffff)) + v[2], bf2f((bf16_t)(hr.y >> 16)) + v[3]};
-    uint2 hw;
-    hw.x = pack2(hv[0], hv[1]);
-    hw.y = pack2(hv[2], hv[3]);
-    float ss = 0.f;
-    if (m < r.M) {
-      st_sc1_u2(hp, hw);
-      const float q0 = bf2f((bf16_t)(hw.x & 0xffff)), q1 = bf2f((bf16_t)(hw.x >> 16));
-      const float q2 = bf2f((bf16_t)(hw.y & 0xffff)), q3 = bf2f((bf16_t)(hw.y >> 16));
-      ss = q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3;
-    }
-#pragma unroll
-    for (int o = Q / 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
-    if (e % Q == 0) st_sc1_u1(ssp + tile * DECODE_SSP_LD + m, __float_as_uint(m < r.M ? ss : 0.f));
+    if (m < r.M) st_sc1_u2(hres + (int64_t)m * H + n0 + j, hw[i]);
+    if (e % Q == 0) st_sc1_u1(ssp + tile * DECODE_SSP_LD + m, __float_as_uint(ss[i]));
   }
-  if (SK > 1 && lane == 0) __hip_atomic_store(tick + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (SK > 1 && lane == 0) __hip_atomic_store(tick + tile * LINEI, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
 
@@ -588,7 +679,7 @@ __device__ __forceinline__ bool epi_resid(const float* red, const Rt& r, float* 
 template <class C>
 __device__ __forceinline__ void epi_gu(const float* red, const char* scr, char* ctl, const Rt& r, const DpArgs& a,
                                        int t, int lane) {
-  constexpr int WR = C::WRG, RS = red_ld<WR>(), NO = WR / 2, NP = NO / 2;
+  constexpr int WR = C::WRG, RS = red_ld<WR>(), NO = WR / 2, NP = NO / 2, EPL = (XR * NP + 63) / 64;
   float* rs = reinterpret_cast<float*>(ctl + C_RS);
   if (lane < XR) {
     const float* st = reinterpret_cast<const float*>(scr + S_STAT);
@@ -602,14 +693,21 @@ __device__ __forceinline__ void epi_gu(const float* red, const char* scr, char* 
     rs[lane] = rsqrtf(tot * a.inv_h + a.eps);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  for (int e = lane; e < XR * NP; e += 64) {
-    const int m = e / NP, j = 2 * (e - m * NP);
-    if (m >= r.M) continue;
+  uint32_t pk[EPL];
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const int e = min(lane + 64 * i, XR * NP - 1), m = e / NP, j = 2 * (e - m * NP);
     const float sc = rs[m];
     const float g0 = red[m * RS + j] * sc, g1 = red[m * RS + j + 1] * sc;
     const float u0 = red[m * RS + NO + j] * sc, u1 = red[m * RS + NO + j + 1] * sc;
     const float v0 = g0 / (1.f + __expf(-g0)) * u0, v1 = g1 / (1.f + __expf(-g1)) * u1;
-    st_sc1_u1(WS<C>::act(a) + (int64_t)m * C::I + t * NO + j, pack2(v0, v1));
+    pk[i] = pack2(v0, v1);
+  }
+  sched_fence();
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const int e = lane + 64 * i, m = e / NP, j = 2 * (e - m * NP);
+    if (e < XR * NP && m < r.M) st_sc1_u1(WS<C>::act(a) + (int64_t)m * C::I + t * NO + j, pk[i]);
   }
 }
 
@@ -657,13 +755,19 @@ __device__ __forceinline__ void att_prologue(char* scr, const DpArgs& a, int sta
   }
 }
 
-// the four waves' (m, l, O) merged in wave order (v3's one-part path) -> bf16 output rows of the G heads
+// the four waves' (m, l, O) merged in wave order (v3's one-part path) -> bf16 output rows of the G heads; and
+// the new token's K / V row to the paged cache (for later steps — this step patched it into the LDS images)
 template <class C>
-__device__ __forceinline__ void att_merge_store(const char* scr, const DpArgs& a, int seq, int kvh, int lane) {
-  constexpr int G = C::G;
+__device__ __forceinline__ void att_merge_store(const char* scr, const DpArgs& a, int l, int seq, int kvh, int lane) {
+  constexpr int G = C::G, EPL = (G * (D / 4) + 63) / 64;
   const float* ml = reinterpret_cast<const float*>(scr + S_ML);
   const float* ob = reinterpret_cast<const float*>(scr + S_OB);
-  for (int e = lane; e < G * (D / 4); e += 64) {
+  const uint32_t* nkv = reinterpret_cast<const uint32_t*>(scr + S_ANKV);
+  const uint32_t kw = nkv[lane], vw = nkv[64 + lane];
+  uint2 pk[EPL];
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const int e = min(lane + 64 * i, G * (D / 4) - 1);
     const int rr = e / (D / 4), d = 4 * (e % (D / 4));
     float mw[4], lw[4];
 #pragma unroll
@@ -685,77 +789,154 @@ __device__ __forceinline__ void att_merge_store(const char* scr, const DpArgs& a
       for (int q = 0; q < 4; ++q) ac[q] += f * v[q];
     }
     const float inv = L > 0.f ? 1.f / L : 0.f;
-    uint2 pk;
-    pk.x = pack2(ac[0] * inv, ac[1] * inv);
-    pk.y = pack2(ac[2] * inv, ac[3] * inv);
-    st_sc1_u2(WS<C>::attn(a) + ((int64_t)seq * C::HQ + kvh * G + rr) * D + d, pk);
+    pk[i].x = pack2(ac[0] * inv, ac[1] * inv);
+    pk[i].y = pack2(ac[2] * inv, ac[3] * inv);
+  }
+  const int64_t sl = sld_i64(a.slots + seq);
+  const DpLayerW* Lw = a.layers + l;
+  sched_fence();
+  if (sl >= 0) {
+    const int64_t base = ((sl >> 4) * C::HKV + kvh) * 16 * D + (sl & 15) * D;
+    reinterpret_cast<uint32_t*>(lw_ptr(&Lw->kc) + base)[lane] = kw;
+    reinterpret_cast<uint32_t*>(lw_ptr(&Lw->vc) + base)[lane] = vw;
+  }
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const int e = lane + 64 * i;
+    const int rr = e / (D / 4), d = 4 * (e % (D / 4));
+    if (e < G * (D / 4)) st_sc1_u2(WS<C>::attn(a) + ((int64_t)seq * C::HQ + kvh * G + rr) * D + d, pk[i]);
   }
 }
 
-// The stream machinery shared by every task type: per consumed chunk, (A) issue the early stream into the ring,
-// (B) issue the late stream of READY chunks — or wait for the consumed chunk's phase —, (C) counted waits and
-// the chunk barrier; after the compute, (E) a non-blocking look-ahead poll and (F) the slot-free barrier.
-template <class C>
+// The stream machinery, specialised per wave role at compile time (each role keeps only its own walkers:
+// fewer live scalars, no spills in the chunk loop). Per consumed chunk every role passes the same two
+// barriers: begin() ends with the "chunk landed" barrier, end() is the "slot free" barrier.
+//  R_W (waves 0, 1): issue the early stream (weights, K/V) while the ring has room; counted wait for this
+//       chunk's pieces.
+//  R_X (wave 2): issue the late stream (activations, prologue operands) of chunks whose phase is READY (the
+//       LDS word `ready`, written by R_C; spins on it — no barrier — when the consumed chunk's phase is not);
+//       counted wait.
+//  R_C (wave 3): makes the consumed chunk's phase READY (blocking wait on the producer counters), and keeps
+//       one asynchronous look-ahead poll of the next phase in flight (issued in end(), consumed a chunk later).
+enum { R_W = 0, R_X = 1, R_C = 2 };
+
+template <class C, int ROLE_>
 struct Stream {
+  static constexpr int ROLE = ROLE_;
   const DpArgs& a;
   const Rt& r;
   char* ring;
   char* scr;
-  int* ready;
+  uint32_t ready;  // LDS address of the READY word
   int wave, qend;
-  Walk cw, ww, xw;
+  Walk cw;  // the consumed chunk
+  Walk sw;  // R_W / R_X: this role's stream walker
   int issued, cum, rq;
+  int pollq, pollv, pollt, pub;  // R_C: look-ahead poll in flight (phase, this lane's shard, target); the
+                                 // READY value last written to LDS
+#ifdef DIE_KERNEL_DIAG
+  uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // cycles per stage of the chunk loop (diagnostics)
+  uint64_t tlast = 0;
+  __device__ __forceinline__ void tick(int i) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    tacc[i] += t - tlast;
+    tlast = t;
+  }
+#else
+  __device__ __forceinline__ void tick(int) {}
+#endif
 
-  __device__ __forceinline__ Stream(const DpArgs& a_, const Rt& r_, char* ring_, char* scr_, int* ready_, int wave_,
-                                    int qend_)
-      : a(a_), r(r_), ring(ring_), scr(scr_), ready(ready_), wave(wave_), qend(qend_), issued(0), cum(0), rq(0) {
+  __device__ __forceinline__ Stream(const DpArgs& a_, const Rt& r_, char* ring_, char* scr_, uint32_t ready_,
+                                    int wave_, int qend_)
+      : a(a_), r(r_), ring(ring_), scr(scr_), ready(ready_), wave(wave_), qend(qend_), issued(0), cum(0), rq(0),
+        pollq(-1), pollv(0), pollt(0), pub(0) {
     walk_begin<C>(cw, r, a, qend);
-    ww = cw;
-    xw = cw;
+    sw = cw;
+#ifdef DIE_KERNEL_DIAG
+    tlast = __builtin_amdgcn_s_memtime();
+#endif
   }
 
-  // steps A-C for the chunk cw; returns its slot
+  __device__ __forceinline__ bool room(const Walk& w) const {  // w's chunk fits in the ring behind cw
+    return w.q < qend && w.pos + chunk_bytes<C>(wp(w)) <= cw.pos + RING && w.idx - cw.idx < 16;
+  }
+
   __device__ __forceinline__ char* begin(int lane) {
-    while (ww.q < qend && ww.pos + chunk_bytes<C>(wp(ww)) <= cw.pos + RING && ww.idx - cw.idx < 16) {
-      if (wave < 2) {
-        issue_w<C>(ww, r, a, ring, wave, lane);
-        issued += w_pieces<C>(wp(ww), wave);
-      }
-      walk_next<C>(ww, r, a, qend);
-    }
-#pragma unroll 1
-    for (;;) {
-      while (xw.idx < ww.idx && xw.q <= rq && !(wp(xw) == P_ATT && xw.k == 0 && xw.idx > cw.idx)) {
-        if (wave == 2) {
-          issue_x<C>(xw, r, a, ring, scr, lane);
-          issued += x_pieces<C>(r, wp(xw), xw.t, xw.k, 2);
+    tick(0);  // (compute of the previous chunk / task epilogue)
+    if constexpr (ROLE == R_W) {
+      while (room(sw)) {
+        if (!(DP_DBG(r) & 4)) {
+          issue_w<C>(sw, r, a, ring, wave, lane);
+          issued += w_pieces<C>(wp(sw), wave);
         }
-        walk_next<C>(xw, r, a, qend);
+        walk_next<C>(sw, r, a, qend);
       }
-      if (xw.idx > cw.idx) break;
-      if (wave == 3) {  // the consumed chunk's activations cannot be loaded yet: wait for its phase
-        wait_dep<C>(a, r, wl(r, cw), wp(cw), lane);
-        if (lane == 0) *ready = cw.q;
-      }
-      lds_fence_barrier();
-      rq = __builtin_amdgcn_readfirstlane(*ready);
-    }
-    if (wave < 3) {
-      const int mine = wave < 2 ? w_pieces<C>(wp(cw), wave) : x_pieces<C>(r, wp(cw), cw.t, cw.k, 2);
+      tick(1);
+      int mine = w_pieces<C>(wp(cw), wave);
+      if (DP_DBG(r) & 4) mine = 0;
       wait_vm_dyn(issued - (cum + mine));
       cum += mine;
+    } else if constexpr (ROLE == R_X) {
+#pragma unroll 1
+      for (;;) {
+        int v;
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ready) : "memory");
+        rq = __builtin_amdgcn_readfirstlane(v);
+        while (room(sw) && sw.q <= rq && !(wp(sw) == P_ATT && sw.k == 0 && sw.idx > cw.idx)) {
+          if (!(DP_DBG(r) & 2)) {
+            issue_x<C>(sw, r, a, ring, scr, lane);
+            issued += x_pieces<C>(r, wp(sw), sw.t, sw.k, 2);
+          }
+          walk_next<C>(sw, r, a, qend);
+        }
+        if (sw.idx > cw.idx) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      tick(2);
+      int mine = x_pieces<C>(r, wp(cw), cw.t, cw.k, 2);
+      if (DP_DBG(r) & 2) mine = 0;
+      wait_vm_dyn(issued - (cum + mine));
+      cum += mine;
+    } else {
+      if (pollq >= 0) {  // the look-ahead poll issued a chunk ago
+        if (dep_sum_met(pollv, pollt)) rq = pollq;
+        pollq = -1;
+      }
+      if (cw.q > rq) {  // the consumed chunk's activations cannot be loaded yet: wait for its phase
+        wait_dep<C>(a, r, wl(r, cw), wp(cw), lane);
+        rq = cw.q;
+      }
+      if (rq != pub) {
+        asm volatile("ds_write_b32 %0, %1" ::"v"(ready), "v"(rq) : "memory");
+        pub = rq;
+      }
+      tick(2);
     }
+    tick(3);
     barrier();
+    tick(4);
     return ring + (cw.pos % RING);
   }
 
-  // steps E-F, then advance to the next chunk
   __device__ __forceinline__ void end(int lane) {
-    if (wave == 3 && xw.idx < ww.idx && xw.q > rq && dep_met<C>(a, r, wl(r, xw), wp(xw), lane) && lane == 0)
-      *ready = xw.q;
+    tick(5);  // compute
+    if constexpr (ROLE == R_C) {
+      // the phase after the last READY one: issue one shard load per lane now, sum it at the next begin()
+      if (pollq < 0 && rq + 1 < qend) {
+        const int q = rq + 1;
+        const int* c = dep_src<C>(a, r, r.l0 + q / NPH, q % NPH, pollt);
+        if (c == nullptr) {
+          rq = q;
+        } else {
+          pollv = dep_load(c, lane);
+          pollq = q;
+        }
+      }
+    }
+    tick(6);
     lds_fence_barrier();
-    rq = __builtin_amdgcn_readfirstlane(*ready);
     walk_next<C>(cw, r, a, qend);
+    tick(7);
   }
 };
 
@@ -766,22 +947,39 @@ __device__ __forceinline__ int opaque(int v) {
   return v;
 }
 
-template <class C, int WR, int PH>
-__device__ __forceinline__ void gemm_task(Stream<C>& S, char* ctl, int lane0) {
-  constexpr int NT = WR / 16;
-  f4 acc[2][8];
+// timeline stamps (diagnostic builds only, DIE_KERNEL_DIAG): per workgroup and phase index, the 100 MHz clock
+// at task entry, data ready, compute done and epilogue done
+#ifdef DIE_KERNEL_DIAG
+#define DP_STAMP(S, q, i)                                                                      \
+  do {                                                                                         \
+    if ((S).a.prof && (S).ROLE == R_C && lane == 0)                                              \
+      (S).a.prof[((int64_t)blockIdx.x * (S).qend + (q)) * 4 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define DP_STAMP(S, q, i) \
+  do {                    \
+  } while (0)
+#endif
+
+template <class C, int WR, int PH, class S_>
+__device__ __forceinline__ void gemm_task(S_& S, char* ctl, int lane0) {
+  f4 acc[2][2];
   zero_acc(acc);
-  const int t = S.cw.t, l = wl(S.r, S.cw), nch = S.cw.nch;
+  const int t = S.cw.t, l = wl(S.r, S.cw), nch = S.cw.nch, q0 = S.cw.q;
   const int wave = S.wave;
+  (void)q0;
 #pragma unroll 1
   for (int k = 0; k < nch; ++k) {
     const int lane = opaque(lane0);
+    if (k == 0) DP_STAMP(S, q0, 0);
     char* slot = S.begin(lane);
+    if (k == 0) DP_STAMP(S, q0, 1);
     gemm_chunk<WR>(slot, acc, wave, lane);
     if (k == nch - 1) {
+      DP_STAMP(S, q0, 2);
       float* red = reinterpret_cast<float*>(S.scr + S_RED);
-      reduce_waves<WR>(red, acc, wave, lane);
-      if (wave == 3) {
+      stash_tiles<WR>(red, acc, wave, lane);
+      if constexpr (S_::ROLE == R_C) {
         bool pub = true;
         if constexpr (PH == P_QKV) epi_qkv<C>(red, S.r, S.a, t, lane);
         else if constexpr (PH == P_O)
@@ -793,19 +991,20 @@ __device__ __forceinline__ void gemm_task(Stream<C>& S, char* ctl, int lane0) {
         if (pub) publish<C>(S.a, S.r, l, PH, lane);
       }
     }
-    (void)NT;
     S.end(lane);
+    if (k == nch - 1) DP_STAMP(S, q0, 3);
   }
 }
 
-template <class C>
-__device__ __forceinline__ void att_task(Stream<C>& S, int lane0) {
+template <class C, class S_>
+__device__ __forceinline__ void att_task(S_& S, int lane0) {
   constexpr int G = C::G;
   const DpArgs& a = S.a;
-  const int t = S.cw.t, l = wl(S.r, S.cw), nch = S.cw.nch;
+  const int t = S.cw.t, l = wl(S.r, S.cw), nch = S.cw.nch, q0 = S.cw.q;
   const int wave = S.wave;
+  (void)q0;
   const int seq = t / C::HKV, kvh = t - seq * C::HKV;
-  const int ctx = __builtin_amdgcn_readfirstlane(a.ctx[seq]);
+  const int ctx = sld_i32(a.ctx + seq);
   State st;
   init_state(st);
   bf16x8_t qf[8];
@@ -814,28 +1013,30 @@ __device__ __forceinline__ void att_task(Stream<C>& S, int lane0) {
   for (int k = 0; k < nch; ++k) {
     const int lane = opaque(lane0);
     const int tid = wave * 64 + lane, h = lane >> 5, row = lane & 31;
+    if (k == 0) DP_STAMP(S, q0, 0);
     char* slot = S.begin(lane);
+    if (k == 0) DP_STAMP(S, q0, 1);
     if (k == 0) {
       att_prologue<G, C::SKQ>(S.scr, a, l == S.r.l0 ? a.ssp0_tiles : C::TD, tid, lane, nk0, nk1, nv);
       lds_fence_barrier();
-      if (wave == 3) {  // the new token's K / V to the paged cache (for later steps; this one patches LDS)
-        const int64_t sl = a.slots[seq];
-        if (sl >= 0) {
-          const DpLayerW& L = a.layers[l];
-          const int64_t base = ((sl >> 4) * C::HKV + kvh) * 16 * D + (sl & 15) * D;
-          const uint32_t* nkv = reinterpret_cast<const uint32_t*>(S.scr + S_ANKV);
-          reinterpret_cast<uint32_t*>(L.kc + base)[lane] = nkv[lane];
-          reinterpret_cast<uint32_t*>(L.vc + base)[lane] = nkv[64 + lane];
-        }
-      }
-      const bf16_t* qimg = reinterpret_cast<const bf16_t*>(S.scr + S_AQ);
+      {  // the rotated query rows (asm reads: no compiler-inserted vmcnt wait in the loader waves)
+        const uint32_t qa = lds_of(S.scr + S_AQ) + min(row, G - 1) * (D * 2) + h * 16;
+        u4 f[8];
+        asm volatile(
+            "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:32\n\tds_read_b128 %2, %8 offset:64\n\t"
+            "ds_read_b128 %3, %8 offset:96\n\tds_read_b128 %4, %8 offset:128\n\tds_read_b128 %5, %8 offset:160\n\t"
+            "ds_read_b128 %6, %8 offset:192\n\tds_read_b128 %7, %8 offset:224\n\ts_waitcnt lgkmcnt(0)"
+            : "=v"(f[0]), "=v"(f[1]), "=v"(f[2]), "=v"(f[3]), "=v"(f[4]), "=v"(f[5]), "=v"(f[6]), "=v"(f[7])
+            : "v"(qa)
+            : "memory");
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk)
-        qf[kk] = row < G ? as_frag(*reinterpret_cast<const uint4*>(qimg + row * D + (2 * kk + h) * 8)) : zero_frag();
+        for (int kk = 0; kk < 8; ++kk)
+          qf[kk] = row < G ? __builtin_bit_cast(bf16x8_t, f[kk]) : zero_frag();
+      }
     }
     if (k == nch - 1) {  // patch key ctx - 1 (this step's token) into the chunk's K / V images
       const int rr = (ctx - 1) - k * DEC_KEYS;
-      const uint32_t kimg = lds_addr(slot) + rr * DEC_ROW, vimg = kimg + DEC_KEYS * DEC_ROW;
+      const uint32_t kimg = lds_of(slot) + rr * DEC_ROW, vimg = kimg + DEC_KEYS * DEC_ROW;
       if (tid < 64) {
         lds_st16(kimg + 16 * ((tid >> 3) ^ (rr & 15)) + 2 * (tid & 7), nk0);
         lds_st16(kimg + 16 * (((tid + 64) >> 3) ^ (rr & 15)) + 2 * (tid & 7), nk1);
@@ -852,8 +1053,9 @@ __device__ __forceinline__ void att_task(Stream<C>& S, int lane0) {
       pv_lds_swz_v3(slot + DEC_KEYS * DEC_ROW + 32 * wave * DEC_ROW, sc, st, lane);
     }
     if (k == nch - 1) {
+      DP_STAMP(S, q0, 2);
       lds_fence_barrier();  // every wave is done with the staging area: the merge reuses it
-      const uint32_t ml = lds_addr(S.scr + S_ML), ob = lds_addr(S.scr + S_OB);
+      const uint32_t ml = lds_of(S.scr + S_ML), ob = lds_of(S.scr + S_OB);
       if (row < G) {
         if (h == 0) {  // (uniform base + offset: no divergent generic->LDS pointer casts)
           lds_st32(ml + 8 * (wave * 32 + row), st.m);
@@ -868,19 +1070,43 @@ __device__ __forceinline__ void att_task(Stream<C>& S, int lane0) {
                       f32x4_t{st.o[db][4 * g4], st.o[db][4 * g4 + 1], st.o[db][4 * g4 + 2], st.o[db][4 * g4 + 3]});
       }
       lds_fence_barrier();
-      if (wave == 3) {
-        att_merge_store<C>(S.scr, a, seq, kvh, lane);
+      if constexpr (S_::ROLE == R_C) {
+        att_merge_store<C>(S.scr, a, l, seq, kvh, lane);
         publish<C>(a, S.r, l, P_ATT, lane);
       }
     }
     S.end(lane);
+    if (k == nch - 1) DP_STAMP(S, q0, 3);
   }
+}
+
+template <class C, int ROLE>
+__device__ __forceinline__ void run_role(const DpArgs& a, const Rt& r, char* smem, uint32_t ready, int wave,
+                                         int lane0) {
+  char* ctl = smem + RING + SCR;
+  using St = Stream<C, ROLE>;
+  St S(a, r, smem, smem + RING, ready, wave, (a.l1 - a.l0) * NPH);
+#pragma unroll 1
+  while (S.cw.q < S.qend) {
+    switch (wp(S.cw)) {
+      case P_QKV: gemm_task<C, C::WRQ, P_QKV, St>(S, ctl, lane0); break;
+      case P_ATT: att_task<C, St>(S, lane0); break;
+      case P_O: gemm_task<C, C::WRO, P_O, St>(S, ctl, lane0); break;
+      case P_GU: gemm_task<C, C::WRG, P_GU, St>(S, ctl, lane0); break;
+      default: gemm_task<C, C::WRD, P_DN, St>(S, ctl, lane0); break;
+    }
+  }
+#ifdef DIE_KERNEL_DIAG
+  if (a.prof && lane0 == 0) {  // per-wave stage cycles after the timeline stamps
+    uint64_t* tp = a.prof + (int64_t)gridDim.x * S.qend * 4 + (blockIdx.x * 4 + wave) * 8;
+    for (int i = 0; i < 8; ++i) tp[i] = S.tacc[i];
+  }
+#endif
 }
 
 template <class C>
 __global__ void __launch_bounds__(NTH, 1) decode_persistent_kernel(DpArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* ctl = smem + RING + SCR;
+  char* smem = dp_smem;
   const int lane0 = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   Rt r;
@@ -889,20 +1115,14 @@ __global__ void __launch_bounds__(NTH, 1) decode_persistent_kernel(DpArgs a) {
   r.M = a.M;
   r.l0 = a.l0;
   r.l1 = a.l1;
-  int* ready = reinterpret_cast<int*>(ctl + C_READY);
-  if (threadIdx.x == 0) *ready = 0;  // phase 0 (the first layer's qkv) reads h as it was before the launch
+  r.dbg = a.dbg;
+  const uint32_t ready = lds_of(smem + RING + SCR + C_READY);
+  if (threadIdx.x == 0)  // phase 0 (the first layer's qkv) reads h as it was before the launch
+    asm volatile("ds_write_b32 %0, %1" ::"v"(ready), "v"(0) : "memory");
   lds_fence_barrier();
-  Stream<C> S(a, r, smem, smem + RING, ready, wave, (a.l1 - a.l0) * NPH);
-#pragma unroll 1
-  while (S.cw.q < S.qend) {
-    switch (wp(S.cw)) {
-      case P_QKV: gemm_task<C, C::WRQ, P_QKV>(S, ctl, lane0); break;
-      case P_ATT: att_task<C>(S, lane0); break;
-      case P_O: gemm_task<C, C::WRO, P_O>(S, ctl, lane0); break;
-      case P_GU: gemm_task<C, C::WRG, P_GU>(S, ctl, lane0); break;
-      default: gemm_task<C, C::WRD, P_DN>(S, ctl, lane0); break;
-    }
-  }
+  if (wave < 2) run_role<C, R_W>(a, r, smem, ready, wave, lane0);
+  else if (wave == 2) run_role<C, R_X>(a, r, smem, ready, wave, lane0);
+  else run_role<C, R_C>(a, r, smem, ready, wave, lane0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 

@@ -131,7 +131,7 @@ struct DpLayerW {
   bf16_t* kc;         // the layer's paged K / V cache [blocks][hkv][16][128]
   bf16_t* vc;
 };
-constexpr int DP_SYNC_LD = 64;  // dependency counter words per layer (5 phases x 8 shards, padded)
+constexpr int DP_SYNC_LD = 5 * 64 * 32;  // dependency counter words per layer: 5 phases x 64 shards x 128 B
 // Scratch of the persistent step lives in ONE workspace (compile-time offsets per model shape, rows padded
 // to 32): qkv slabs, attention output, o / down slabs, SiLU output, norm statistics, split-K tickets, the
 // error word and the per-layer dependency counters (decode_persistent_layout gives the offsets).
@@ -147,6 +147,8 @@ struct DpArgs {
   int l0, l1, M, bt_stride, ssp0_tiles;
   float scale_log2, eps, inv_h;
   int H, I, hq, hkv;       // the model shape (selects the instantiation; checked by the launcher)
+  uint64_t* prof;          // diagnostic builds: timeline stamps [grid][phases][4] (nullptr: none)
+  int dbg;                 // diagnostic builds: experiment switches (DIE_DP_DBG)
 };
 // the instantiation for a model shape: cfg7 = {wrq, skq, wro, sko, wrg, wrd, skd} and the workspace layout
 // lay4[9] = {bytes for `layers` layers, offsets of: the error word, the counters, slab_q, attn, slab_od, act,

@@ -598,7 +598,7 @@ class CausalLM:
             # every layer in one persistent launch (weight / KV stream kept running across op boundaries)
             ops.decode_persistent(ps["ws"], ps["table"], h, ssp_prev, meta.block_tables, meta.ctx_lens,
                                   meta.slot_mapping, self.cos_sin, kv_pool, 0, len(self.layers), self.inter, hq,
-                                  hkv, self.scale, eps)
+                                  hkv, self.scale, eps, ps.get("prof"))
             return ops.rms_norm(h, self.norm, eps)
         for li, lw in enumerate(self.layers):
             k_cache, v_cache = kv_pool[li, 0], kv_pool[li, 1]

@@ -161,11 +161,12 @@ def decode_persistent_config(hidden: int, inter: int, hq: int, hkv: int, layers:
 def decode_persistent(ws: torch.Tensor, table: torch.Tensor, h: torch.Tensor, ssp0: torch.Tensor,
                       block_tables: torch.Tensor, ctx_lens: torch.Tensor, slot_mapping: torch.Tensor,
                       cos_sin: torch.Tensor, pool: torch.Tensor, l0: int, l1: int, inter: int, hq: int, hkv: int,
-                      scale: float, eps: float) -> None:
+                      scale: float, eps: float, prof: Optional[torch.Tensor] = None) -> None:
     """Layers [l0, l1) of a dense decode step in ONE persistent launch (h updated in place, the new tokens'
-    K / V written to the pool). ``table`` [L, 6] int64: the layers' packed weight and cache pointers."""
+    K / V written to the pool). ``table`` [L, 6] int64: the layers' packed weight and cache pointers.
+    ``prof`` (int64 [CUs, phases, 4]) receives timeline stamps in DIE_KERNEL_DIAG builds."""
     _kern().decode_persistent(ws, table, h, ssp0, block_tables, ctx_lens, slot_mapping, cos_sin, pool, l0, l1,
-                              inter, hq, hkv, scale, eps)
+                              inter, hq, hkv, scale, eps, prof)
 
 
 def decode_advance(out, ids, pos, ctx, slots, bt, step, tokens, cnt, n_real, rows: int, block_size: int) -> None:

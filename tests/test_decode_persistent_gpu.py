@@ -1,7 +1,9 @@
 """The persistent decode-step kernel (csrc/kernels/decode_persistent.hip): every layer of a dense decode step
-in one launch. Its arithmetic is the multi-launch fused path's (gemm_decode.hip SPLIT-0 tiles at KC 128, the
-v3 attention's one-part FUSED path, split-K slabs in slice order), so with the same tiles the two must agree
-BIT FOR BIT — the residual stream after the last layer and the new tokens' K / V in the paged cache."""
+in one launch, against the multi-launch fused path with the same tiles. The attention (v3 one-part FUSED),
+the split-K slab order and the epilogue arithmetic are the same; the GEMM accumulation order is not (the
+persistent kernel splits a chunk over the waves by output columns, gemm_decode.hip by k-steps), so the two
+agree to fp32 rounding before the bf16 casts: normwise within 5e-3 (a few bf16 ulps after 4 layers). The
+persistent kernel itself is deterministic: repeated launches give the same bits."""
 
 import math
 import os
@@ -40,6 +42,14 @@ def _setup(preset, n_layers, M, ctxs, seed=0, max_ctx=1024):
     return m, pool, bt, ctx, pos, slots, ids, meta_kw, max_ctx
 
 
+def _assert_close(got, want, rel=5e-3, name=""):
+    g, w = got.float(), want.float()
+    assert torch.isfinite(g).all(), name
+    nerr = float((g - w).norm() / w.norm().clamp_min(1e-30))
+    merr = float((g - w).abs().max() / w.abs().max().clamp_min(1e-30))
+    assert nerr <= rel and merr <= 8 * rel, (name, nerr, merr)
+
+
 def _run_both(preset, n_layers, M, ctxs, seed=0):
     m, pool, bt, ctx, pos, slots, ids, meta_kw, max_ctx = _setup(preset, n_layers, M, ctxs, seed)
     sc = m.alloc_decode_scratch(M)
@@ -73,21 +83,19 @@ def test_persistent_matches_multi_launch_mini(M, layers):
     outs, err = _run_both("llama-mini", layers, M, ctxs)
     assert err == 0
     (h0, p0), (h1, p1) = outs["multi"], outs["persistent"]
-    assert torch.isfinite(h1.float()).all()
-    assert torch.equal(h0, h1), float((h0.float() - h1.float()).abs().max())
-    assert torch.equal(p0, p1)
+    _assert_close(h1, h0, name="h")
+    _assert_close(p1, p0, name="kv")
 
 
 def test_persistent_matches_multi_launch_8b_shapes():
     """Llama-3-8B layer shapes (2 layers), the bench's 32 rows at 500-640 keys: every phase has one task per
-    CU, attention spans 4-5 chunks per task; bit-exact against the multi-launch path with the same tiles."""
+    CU, attention spans 4-5 chunks per task."""
     ctxs = [500 + 4 * i for i in range(32)]
     outs, err = _run_both("llama3-8b", 2, 32, ctxs, seed=3)
     assert err == 0
     (h0, p0), (h1, p1) = outs["multi"], outs["persistent"]
-    assert torch.isfinite(h1.float()).all()
-    assert torch.equal(h0, h1), float((h0.float() - h1.float()).abs().max())
-    assert torch.equal(p0, p1)
+    _assert_close(h1, h0, name="h")
+    _assert_close(p1, p0, name="kv")
 
 
 def test_persistent_repeated_launches_are_identical():
@@ -173,5 +181,5 @@ def test_persistent_intermediates_one_layer(preset, ctxs):
         "h": h2, "kv": p2,
     }
     want = {"slab_q": slab, "attn": attn, "ssp_o": ssp_a[:, :M], "act": act, "ssp_d": ssp_b[:, :M], "h": h, "kv": p}
-    bad = {k: float((got[k].float() - want[k].float()).abs().max()) for k in want if not torch.equal(got[k], want[k])}
-    assert not bad, bad
+    for k in want:
+        _assert_close(got[k], want[k], name=k)
