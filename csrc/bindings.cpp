@@ -775,7 +775,9 @@ void decode_persistent(Tensor ws, Tensor table, Tensor h, Tensor ssp0, Tensor bl
               "decode_persistent: no instantiation for this model shape");
   TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.is_contiguous() && table.dim() == 2 &&
                   table.size(1) == 6, "table [L, 6] int64 on the GPU");
-  TORCH_CHECK(0 <= l0 && l0 < l1 && l1 <= L, "layer range");
+  // the workspace's dependency counters are never reset (each launch advances them by a fixed amount): one
+  // workspace serves one layer range, the whole table
+  TORCH_CHECK(l0 == 0 && l1 == L, "decode_persistent runs every layer of its table (l0 = 0, l1 = L)");
   TORCH_CHECK(ws.is_cuda() && ws.is_contiguous() && ws.numel() * ws.element_size() >= lay[0] &&
                   reinterpret_cast<uintptr_t>(ws.data_ptr()) % 256 == 0, "workspace too small or misaligned");
   DIE_CHECK_CUDA(pool);

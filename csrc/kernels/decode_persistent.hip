@@ -25,9 +25,12 @@
 //    into the ring — it polls the dependency counters, does every global store of the epilogues (sc1,
 //    write-through), takes the split-K tickets and publishes. All four waves compute (MFMA).
 //  * Hand-offs (MI355X_MICROARCH.md visibility table, row 1): the producer's payload is stored sc1 by
-//    wave 3, drained (vmcnt(0)), then ONE lane adds to the phase counter (agent scope, sharded over 8
-//    words). The consumer's wave 3 polls the counter with relaxed agent loads, publishes READY in LDS,
-//    and the X loads that follow are sc1 LDS-DMA.
+//    wave 3, drained (vmcnt(0)), then ONE lane adds to the phase counter (agent scope, 64 shards, one
+//    128-byte line each). The consumer's wave 3 polls the counter with relaxed agent loads, publishes READY
+//    in LDS, and the activation loads that follow are sc1 LDS-DMA.
+//  * The counters and split-K tickets are never reset (no memset node in the step's graph): every launch
+//    advances each phase's counter by a fixed amount (the attention phase is padded to 32 * HKV tasks),
+//    the launch's epoch comes from the workgroups' exit count, and "met" is a wrap-around difference.
 //  * Determinism: the GEMM partial sums of the four waves are combined through LDS in wave order, the
 //    attention merge in wave order, split-K slabs in slice order — the same arithmetic as the multi-launch
 //    path (gemm_decode.hip SPLIT 0 tiles at KC = 128, attention.hip v3 FUSED with one part per pair), so
@@ -161,7 +164,8 @@ struct WS {
   static constexpr int64_t TICKO = (SSPD + (int64_t)C::TD * 128 * 4 + 127) / 128 * 128;  // i32 [TO][32]
   static constexpr int64_t TICKD = TICKO + (int64_t)C::TO * 128;              // i32 [TD][32]
   static constexpr int64_t ERR = TICKD + (int64_t)C::TD * 128;                // i32 [32]
-  static constexpr int64_t SYNC = ERR + 128;                                  // i32 [layers][DP_SYNC_LD]
+  static constexpr int64_t DONE = ERR + 128;                                  // u64 [64 shards][16]: exits
+  static constexpr int64_t SYNC = DONE + (int64_t)NSH * 128;                  // u32 [layers][DP_SYNC_LD]
   static __device__ __forceinline__ float* slab_q(const DpArgs& a) { return reinterpret_cast<float*>(a.ws + SLABQ); }
   static __device__ __forceinline__ bf16_t* attn(const DpArgs& a) { return reinterpret_cast<bf16_t*>(a.ws + ATTN); }
   static __device__ __forceinline__ float* slab_od(const DpArgs& a) { return reinterpret_cast<float*>(a.ws + SLABOD); }
@@ -172,6 +176,9 @@ struct WS {
   static __device__ __forceinline__ int* tick_d(const DpArgs& a) { return reinterpret_cast<int*>(a.ws + TICKD); }
   static __device__ __forceinline__ int* err(const DpArgs& a) { return reinterpret_cast<int*>(a.ws + ERR); }
   static __device__ __forceinline__ int* sync(const DpArgs& a) { return reinterpret_cast<int*>(a.ws + SYNC); }
+  static __device__ __forceinline__ unsigned long long* done(const DpArgs& a) {
+    return reinterpret_cast<unsigned long long*>(a.ws + DONE);
+  }
 };
 
 struct Rt {  // run-time uniforms
@@ -438,7 +445,7 @@ __device__ __forceinline__ const int* dep_src(const DpArgs& a, const Rt& r, int 
       if (l == r.l0) return nullptr;
       pl = l - 1; pp = P_DN; target = C::TD; break;
     case P_ATT: pp = P_QKV; target = C::NTQ; break;
-    case P_O: pp = P_ATT; target = r.M * C::HKV; break;
+    case P_O: pp = P_ATT; target = XR * C::HKV; break;  // M * HKV tasks + the launch's padding
     case P_GU: pp = P_O; target = C::TO; break;
     default: pp = P_GU; target = C::NTG; break;
   }
@@ -448,26 +455,38 @@ __device__ __forceinline__ const int* dep_src(const DpArgs& a, const Rt& r, int 
 __device__ __forceinline__ int dep_load(const int* c, int lane) {
   return __hip_atomic_load(c + lane * LINEI, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ bool dep_sum_met(int v, int target) {
+// the counters are never reset: in launch e a phase's counter runs from e * target to (e + 1) * target
+// (mod 2^32), so "met" is (sum - e * target) >= target in wrap-around arithmetic
+__device__ __forceinline__ bool dep_sum_met(int v, int target, uint32_t ep) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return __builtin_amdgcn_readfirstlane(v) >= target;
-}
-template <class C>
-__device__ __forceinline__ bool dep_met(const DpArgs& a, const Rt& r, int l, int p, int lane) {
-  int target = 0;
-  const int* c = dep_src<C>(a, r, l, p, target);
-  return c == nullptr || dep_sum_met(dep_load(c, lane), target);
+  const uint32_t cur = (uint32_t)__builtin_amdgcn_readfirstlane(v) - ep * (uint32_t)target;
+  return cur >= (uint32_t)target;
 }
 
 // bounded wait (wave 3) until phase (l, p)'s producers have all published
 template <class C>
-__device__ __forceinline__ void wait_dep(const DpArgs& a, const Rt& r, int l, int p, int lane) {
+__device__ __forceinline__ void wait_dep(const DpArgs& a, const Rt& r, int l, int p, uint32_t ep, int lane) {
+  int target = 0;
+  const int* c = dep_src<C>(a, r, l, p, target);
+  if (c == nullptr) return;
   const long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-  while (!dep_met<C>(a, r, l, p, lane)) {
-    if (__hip_atomic_load(WS<C>::err(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;  // failed
+  int* err = WS<C>::err(a);
+#pragma unroll 1
+  for (;;) {
+    int v = dep_load(c, lane);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    v = (int)((uint32_t)__builtin_amdgcn_readfirstlane(v) - ep * (uint32_t)target);
+    if ((uint32_t)v >= (uint32_t)target) return;
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;  // failed elsewhere
     if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ll) {  // 2 s: a producer never came
-      if (lane == 0) __hip_atomic_store(WS<C>::err(a), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) {  // err = {1, the waiting workgroup, layer * 8 + phase, producers seen}
+        __hip_atomic_store(err + 1, r.b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(err + 2, l * 8 + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(err + 3, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       return;
     }
     __builtin_amdgcn_s_sleep(2);
@@ -619,7 +638,8 @@ __device__ __forceinline__ bool epi_resid(const float* red, const Rt& r, float* 
     int old = 0;
     if (lane == 0) old = __hip_atomic_fetch_add(tick + tile * LINEI, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     old = __builtin_amdgcn_readfirstlane(old);
-    if (old != SK - 1) return false;
+    static_assert((SK & (SK - 1)) == 0, "tickets count modulo SK (a power of two: wrap-safe)");
+    if ((old & (SK - 1)) != SK - 1) return false;  // never reset: SK arrivals per tile per layer
   }
   // (last arriver) one batch of loads: the residual rows and the other slices' partials
   uint2 hr[EPL];
@@ -670,7 +690,6 @@ __device__ __forceinline__ bool epi_resid(const float* red, const Rt& r, float* 
     if (m < r.M) st_sc1_u2(hres + (int64_t)m * H + n0 + j, hw[i]);
     if (e % Q == 0) st_sc1_u1(ssp + tile * DECODE_SSP_LD + m, __float_as_uint(ss[i]));
   }
-  if (SK > 1 && lane == 0) __hip_atomic_store(tick + tile * LINEI, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
 
@@ -834,6 +853,7 @@ struct Stream {
   int issued, cum, rq;
   int pollq, pollv, pollt, pub;  // R_C: look-ahead poll in flight (phase, this lane's shard, target); the
                                  // READY value last written to LDS
+  uint32_t ep;                   // R_C: this launch's epoch (launches completed before it)
 #ifdef DIE_KERNEL_DIAG
   uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // cycles per stage of the chunk loop (diagnostics)
   uint64_t tlast = 0;
@@ -849,7 +869,22 @@ struct Stream {
   __device__ __forceinline__ Stream(const DpArgs& a_, const Rt& r_, char* ring_, char* scr_, uint32_t ready_,
                                     int wave_, int qend_)
       : a(a_), r(r_), ring(ring_), scr(scr_), ready(ready_), wave(wave_), qend(qend_), issued(0), cum(0), rq(0),
-        pollq(-1), pollv(0), pollt(0), pub(0) {
+        pollq(-1), pollv(0), pollt(0), pub(0), ep(0) {
+    if constexpr (ROLE_ == R_C) {
+      // every workgroup adds 1 to a done shard when it exits: during launch e the total is in
+      // [e * grid, (e + 1) * grid), so floor(total / grid) is this launch's epoch whatever the timing
+      unsigned long long d = __hip_atomic_load(WS<C>::done(a) + (threadIdx.x & 63) * 16, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+      ep = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(d / (unsigned long long)r.P));
+      // a phase's counter must advance by the same amount every launch: the attention phase has M * HKV
+      // tasks, so workgroup 0 adds the (XR - M) * HKV missing ones up front
+      if (r.b == 0 && r.M < XR && (threadIdx.x & 63) == 0)
+        for (int l = r.l0; l < r.l1; ++l)
+          __hip_atomic_fetch_add(counter<C>(a, r, l, P_ATT), (XR - r.M) * C::HKV, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+    }
     walk_begin<C>(cw, r, a, qend);
     sw = cw;
 #ifdef DIE_KERNEL_DIAG
@@ -899,11 +934,11 @@ struct Stream {
       cum += mine;
     } else {
       if (pollq >= 0) {  // the look-ahead poll issued a chunk ago
-        if (dep_sum_met(pollv, pollt)) rq = pollq;
+        if (dep_sum_met(pollv, pollt, ep)) rq = pollq;
         pollq = -1;
       }
       if (cw.q > rq) {  // the consumed chunk's activations cannot be loaded yet: wait for its phase
-        wait_dep<C>(a, r, wl(r, cw), wp(cw), lane);
+        wait_dep<C>(a, r, wl(r, cw), wp(cw), ep, lane);
         rq = cw.q;
       }
       if (rq != pub) {
@@ -1026,7 +1061,8 @@ __device__ __forceinline__ void att_task(S_& S, int lane0) {
             "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:32\n\tds_read_b128 %2, %8 offset:64\n\t"
             "ds_read_b128 %3, %8 offset:96\n\tds_read_b128 %4, %8 offset:128\n\tds_read_b128 %5, %8 offset:160\n\t"
             "ds_read_b128 %6, %8 offset:192\n\tds_read_b128 %7, %8 offset:224\n\ts_waitcnt lgkmcnt(0)"
-            : "=v"(f[0]), "=v"(f[1]), "=v"(f[2]), "=v"(f[3]), "=v"(f[4]), "=v"(f[5]), "=v"(f[6]), "=v"(f[7])
+            : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]), "=&v"(f[5]), "=&v"(f[6]),
+              "=&v"(f[7])
             : "v"(qa)
             : "memory");
 #pragma unroll
@@ -1124,6 +1160,9 @@ __global__ void __launch_bounds__(NTH, 1) decode_persistent_kernel(DpArgs a) {
   else if (wave == 2) run_role<C, R_X>(a, r, smem, ready, wave, lane0);
   else run_role<C, R_C>(a, r, smem, ready, wave, lane0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (threadIdx.x == 0)  // this workgroup's exit (the next launch derives its epoch from the total)
+    __hip_atomic_fetch_add(WS<C>::done(a) + (blockIdx.x & (NSH - 1)) * 16, 1ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // shape / tile instantiations: Llama-3-8B (32 q / 8 kv heads, hidden 4096, FFN 14336) with the tiles that put
@@ -1138,8 +1177,6 @@ static bool cfg_matches(const DpArgs& a) {
 
 template <class C>
 static hipError_t launch_cfg(const DpArgs& a, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(a.ws + WS<C>::SYNC, 0, sizeof(int) * DP_SYNC_LD * (a.l1 - a.l0), s);
-  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(decode_persistent_kernel<C>, dim3(num_cus()), dim3(NTH), LDS_TOTAL, s, a);
   return hipGetLastError();
 }
@@ -1164,8 +1201,8 @@ bool decode_persistent_config(int H, int I, int hq, int hkv, int layers, int* cf
 }
 
 // One persistent launch for layers [l0, l1) of a dense decode step (see the header comment). The caller
-// (bindings.cpp) has validated every shape; here: the counters are zeroed (a memset node under capture)
-// and the instantiation for the shape is launched.
+// (bindings.cpp) has validated every shape; here only the instantiation for the shape is chosen (the
+// dependency counters need no per-launch reset).
 hipError_t launch_decode_persistent(const DpArgs& a, hipStream_t s) {
   using namespace dp;
   if (a.M < 1 || a.M > XR || a.l1 <= a.l0) return hipErrorInvalidValue;

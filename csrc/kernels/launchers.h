@@ -137,7 +137,7 @@ constexpr int DP_SYNC_LD = 5 * 64 * 32;  // dependency counter words per layer: 
 // error word and the per-layer dependency counters (decode_persistent_layout gives the offsets).
 struct DpArgs {
   const DpLayerW* layers;  // device array, indexed by absolute layer
-  char* ws;                // workspace (zero-initialised once; the counters are re-zeroed every launch)
+  char* ws;                // workspace (zero-initialised once; its counters only ever advance)
   bf16_t* h;               // residual stream [M][H] (in / out)
   const float* ssp0;       // statistics of h at entry [ssp0_tiles][128]
   const int* bt;           // block tables [M][bt_stride]

@@ -561,7 +561,9 @@ class CausalLM:
         table = torch.tensor(rows, dtype=torch.int64, device=self.device)
         ws = torch.zeros(cfg["ws_bytes"], dtype=torch.uint8, device=self.device)
         scratch["persistent"] = {"cfg": cfg, "table": table, "ws": ws, "pool_ptr": kv_pool.data_ptr(),
-                                 "err": ws[cfg["err_off"]:cfg["err_off"] + 4].view(torch.int32)}
+                                 "err": ws[cfg["err_off"]:cfg["err_off"] + 4].view(torch.int32),
+                                 # {err, waiting workgroup, layer * 8 + phase, producers seen} after a timeout
+                                 "err_info": ws[cfg["err_off"]:cfg["err_off"] + 16].view(torch.int32)}
         return True
 
     def _fused_decode_ok(self, kv_pool: torch.Tensor, m: int = 32) -> bool:
