@@ -65,12 +65,17 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
     incs, torch_lib, abi = _torch_paths()
     jobs_list = []
     objs = []
+    is_diag = os.environ.get("DIE_KERNEL_DIAG") == "1"
+    # diagnostics builds keep their own objects; the link re-runs whenever the flavour changes
+    flavour = os.path.join(OBJ, ".flavour")
+    prev = open(flavour).read() if os.path.exists(flavour) else ""
+    relink = prev != ("diag" if is_diag else "release")
     for k in KERNELS:
         src = os.path.join(kdir, k + ".hip")
-        obj = os.path.join(OBJ, k + ".o")
+        obj = os.path.join(OBJ, k + (".diag.o" if is_diag else ".o"))
         objs.append(obj)
         if force or _newer(obj, [src] + hdrs + [os.path.abspath(__file__)]):
-            diag = ["-DDIE_KERNEL_DIAG"] if os.environ.get("DIE_KERNEL_DIAG") == "1" else []
+            diag = ["-DDIE_KERNEL_DIAG"] if is_diag else []
             # the decode kernels fuse multiply-adds per source expression only (not across statements): the
             # persistent decode step and the multi-launch path then round identically (bit-exact tests)
             contract = ["-ffp-contract=on"] if k in CONTRACT_ON else []
@@ -91,10 +96,12 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
         for res in ex.map(_run, jobs_list):
             if verbose and res:
                 print(res)
-    if force or _newer(out, objs):
+    if force or relink or _newer(out, objs):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out,
               "-L", torch_lib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
               f"-Wl,-rpath,{torch_lib}"])
+        with open(flavour, "w") as f:
+            f.write("diag" if is_diag else "release")
     return out
 
 

@@ -20,6 +20,7 @@ from __future__ import annotations
 import asyncio
 import json
 import pickle
+import re
 import struct
 from typing import Any, Optional, Tuple
 
@@ -94,23 +95,73 @@ async def write_frame(writer: asyncio.StreamWriter, obj: Any, codec: bytes = COD
     await writer.drain()
 
 
+_STRUCT = re.compile(rb'["\\{}\[\]]')
+
+
+class _JsonObjectEnd:
+    """Incremental scanner for the end of one top-level JSON object: tracks brace depth outside strings
+    (with escapes), so each byte is looked at once however the document is chunked."""
+
+    __slots__ = ("depth", "in_str", "esc")
+
+    def __init__(self) -> None:
+        self.depth = 0
+        self.in_str = False
+        self.esc = False
+
+    def feed(self, data: bytes, base: int) -> int:
+        """Scan ``data`` (at offset ``base`` of the stream); return the stream offset one past the object's
+        closing brace, or -1 if it has not closed yet. Only the structural bytes are visited."""
+        depth, in_str, esc = self.depth, self.in_str, self.esc
+        # position of the previous structural byte (a backslash escapes only the byte right after it; one
+        # that ended the previous chunk escapes byte 0 of this one)
+        last = -1 if esc else -2
+        for m in _STRUCT.finditer(data):
+            i = m.start()
+            c = data[i]
+            if esc and i == last + 1:
+                esc = False
+                last = i
+                continue
+            esc = False
+            last = i
+            if in_str:
+                if c == 0x5C:  # backslash
+                    esc = True
+                elif c == 0x22:  # quote
+                    in_str = False
+            elif c == 0x22:
+                in_str = True
+            elif c == 0x7B or c == 0x5B:  # { [
+                depth += 1
+            elif c == 0x7D or c == 0x5D:  # } ]
+                depth -= 1
+                if depth == 0:
+                    self.depth, self.in_str, self.esc = depth, in_str, esc
+                    return base + i + 1
+        if esc and last != len(data) - 1:
+            esc = False  # the escaped byte was an ordinary character
+        self.depth, self.in_str, self.esc = depth, in_str, esc
+        return -1
+
+
 async def read_legacy_json(reader: asyncio.StreamReader, first: bytes, limit: int = MAX_FRAME) -> Any:
-    """Read an unframed JSON document that started with ``first``: accumulate
-    chunks until the buffer parses (or EOF)."""
+    """Read an unframed JSON document that started with ``first``: accumulate chunks until the top-level
+    object closes (one linear scan), then decode it once; at EOF decode what arrived (raises the real
+    error if it is incomplete)."""
     buf = bytearray(first)
-    dec = json.JSONDecoder()
-    while True:
-        try:
-            obj, _ = dec.raw_decode(buf.decode())
-            return obj
-        except (json.JSONDecodeError, UnicodeDecodeError):
-            pass
+    scan = _JsonObjectEnd()
+    end = scan.feed(first, 0)
+    while end < 0:
         chunk = await reader.read(65536)
         if not chunk:
-            return json.loads(buf.decode())  # raises the real error
+            return json.loads(buf.decode())
+        base = len(buf)
         buf += chunk
         if len(buf) > limit:
             raise ProtocolError("legacy request too large")
+        end = scan.feed(chunk, base)
+    return json.loads(bytes(buf[:end]).decode())
 
 
 async def read_message(reader: asyncio.StreamReader, allow_pickle: bool = False) -> Tuple[Optional[Any], str, bytes]:
