@@ -25,7 +25,7 @@
 //    into the ring — it polls the dependency counters, does every global store of the epilogues (sc1,
 //    write-through), takes the split-K tickets and publishes. All four waves compute (MFMA).
 //  * Hand-offs (MI355X_MICROARCH.md visibility table, row 1): the producer's payload is stored sc1 by
-//    wave 3, drained (vmcnt(0)), then ONE lane adds to the phase counter (agent scope, 64 shards, one
+//    wave 3, drained (vmcnt(0)), then ONE lane adds to the phase counter (agent scope, 16 shards, one
 //    128-byte line each). The consumer's wave 3 polls the counter with relaxed agent loads, publishes READY
 //    in LDS, and the activation loads that follow are sc1 LDS-DMA.
 //  * The counters and split-K tickets are never reset (no memset node in the step's graph): every launch
@@ -56,7 +56,7 @@ constexpr int XR = 32;                       // activation rows per chunk (decod
 constexpr int KC = 128;                      // K per GEMM chunk
 constexpr int ROWB = 256;                    // bytes per GEMM image row
 constexpr int ACH = 65536;                   // attention chunk: 128 keys of K + V
-constexpr int NSH = 64;                      // counter shards (one per lane of the polling wave)
+constexpr int NSH = 16;                      // counter shards (lanes 0..15 of the polling wave)
 constexpr int LINEI = 32;                    // ints per 128-byte line: every shard / ticket on its own line
                                              // (same-line atomics from 256 CUs serialise: ~80 us per phase)
 constexpr int NPH = 5;
@@ -453,13 +453,13 @@ __device__ __forceinline__ const int* dep_src(const DpArgs& a, const Rt& r, int 
 }
 // one shard per lane (a relaxed agent-scope load; the caller may consume it a chunk later)
 __device__ __forceinline__ int dep_load(const int* c, int lane) {
-  return __hip_atomic_load(c + lane * LINEI, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return lane < NSH ? __hip_atomic_load(c + lane * LINEI, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
 }
 // the counters are never reset: in launch e a phase's counter runs from e * target to (e + 1) * target
 // (mod 2^32), so "met" is (sum - e * target) >= target in wrap-around arithmetic
 __device__ __forceinline__ bool dep_sum_met(int v, int target, uint32_t ep) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = NSH / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   const uint32_t cur = (uint32_t)__builtin_amdgcn_readfirstlane(v) - ep * (uint32_t)target;
   return cur >= (uint32_t)target;
 }
@@ -476,7 +476,7 @@ __device__ __forceinline__ void wait_dep(const DpArgs& a, const Rt& r, int l, in
   for (;;) {
     int v = dep_load(c, lane);
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    for (int o = NSH / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     v = (int)((uint32_t)__builtin_amdgcn_readfirstlane(v) - ep * (uint32_t)target);
     if ((uint32_t)v >= (uint32_t)target) return;
     if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;  // failed elsewhere
@@ -489,7 +489,7 @@ __device__ __forceinline__ void wait_dep(const DpArgs& a, const Rt& r, int l, in
       }
       return;
     }
-    __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_s_sleep(8);  // ~0.2 us between polls: each poll is NSH uncached line loads
   }
 }
 
@@ -835,8 +835,9 @@ __device__ __forceinline__ void att_merge_store(const char* scr, const DpArgs& a
 //  R_X (wave 2): issue the late stream (activations, prologue operands) of chunks whose phase is READY (the
 //       LDS word `ready`, written by R_C; spins on it — no barrier — when the consumed chunk's phase is not);
 //       counted wait.
-//  R_C (wave 3): makes the consumed chunk's phase READY (blocking wait on the producer counters), and keeps
-//       one asynchronous look-ahead poll of the next phase in flight (issued in end(), consumed a chunk later).
+//  R_C (wave 3): makes the consumed chunk's phase READY (blocking wait on the producer counters). There is
+//       no look-ahead poll: the next phase cannot complete before this workgroup's own task of the current
+//       phase has published, and every poll reads NSH uncached lines.
 enum { R_W = 0, R_X = 1, R_C = 2 };
 
 template <class C, int ROLE_>
@@ -851,8 +852,7 @@ struct Stream {
   Walk cw;  // the consumed chunk
   Walk sw;  // R_W / R_X: this role's stream walker
   int issued, cum, rq;
-  int pollq, pollv, pollt, pub;  // R_C: look-ahead poll in flight (phase, this lane's shard, target); the
-                                 // READY value last written to LDS
+  int pub;                       // R_C: the READY value last written to LDS
   uint32_t ep;                   // R_C: this launch's epoch (launches completed before it)
 #ifdef DIE_KERNEL_DIAG
   uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // cycles per stage of the chunk loop (diagnostics)
@@ -869,14 +869,15 @@ struct Stream {
   __device__ __forceinline__ Stream(const DpArgs& a_, const Rt& r_, char* ring_, char* scr_, uint32_t ready_,
                                     int wave_, int qend_)
       : a(a_), r(r_), ring(ring_), scr(scr_), ready(ready_), wave(wave_), qend(qend_), issued(0), cum(0), rq(0),
-        pollq(-1), pollv(0), pollt(0), pub(0), ep(0) {
+        pub(0), ep(0) {
     if constexpr (ROLE_ == R_C) {
       // every workgroup adds 1 to a done shard when it exits: during launch e the total is in
       // [e * grid, (e + 1) * grid), so floor(total / grid) is this launch's epoch whatever the timing
-      unsigned long long d = __hip_atomic_load(WS<C>::done(a) + (threadIdx.x & 63) * 16, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
+      const int ln = threadIdx.x & 63;
+      unsigned long long d = ln < NSH ? __hip_atomic_load(WS<C>::done(a) + ln * 16, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT) : 0ull;
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+      for (int o = NSH / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
       ep = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(d / (unsigned long long)r.P));
       // a phase's counter must advance by the same amount every launch: the attention phase has M * HKV
       // tasks, so workgroup 0 adds the (XR - M) * HKV missing ones up front
@@ -933,10 +934,6 @@ struct Stream {
       wait_vm_dyn(issued - (cum + mine));
       cum += mine;
     } else {
-      if (pollq >= 0) {  // the look-ahead poll issued a chunk ago
-        if (dep_sum_met(pollv, pollt, ep)) rq = pollq;
-        pollq = -1;
-      }
       if (cw.q > rq) {  // the consumed chunk's activations cannot be loaded yet: wait for its phase
         wait_dep<C>(a, r, wl(r, cw), wp(cw), ep, lane);
         rq = cw.q;
@@ -955,19 +952,6 @@ struct Stream {
 
   __device__ __forceinline__ void end(int lane) {
     tick(5);  // compute
-    if constexpr (ROLE == R_C) {
-      // the phase after the last READY one: issue one shard load per lane now, sum it at the next begin()
-      if (pollq < 0 && rq + 1 < qend) {
-        const int q = rq + 1;
-        const int* c = dep_src<C>(a, r, r.l0 + q / NPH, q % NPH, pollt);
-        if (c == nullptr) {
-          rq = q;
-        } else {
-          pollv = dep_load(c, lane);
-          pollq = q;
-        }
-      }
-    }
     tick(6);
     lds_fence_barrier();
     walk_next<C>(cw, r, a, qend);

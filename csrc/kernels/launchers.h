@@ -131,7 +131,7 @@ struct DpLayerW {
   bf16_t* kc;         // the layer's paged K / V cache [blocks][hkv][16][128]
   bf16_t* vc;
 };
-constexpr int DP_SYNC_LD = 5 * 64 * 32;  // dependency counter words per layer: 5 phases x 64 shards x 128 B
+constexpr int DP_SYNC_LD = 5 * 16 * 32;  // dependency counter words per layer: 5 phases x 16 shards x 128 B
 // Scratch of the persistent step lives in ONE workspace (compile-time offsets per model shape, rows padded
 // to 32): qkv slabs, attention output, o / down slabs, SiLU output, norm statistics, split-K tickets, the
 // error word and the per-layer dependency counters (decode_persistent_layout gives the offsets).

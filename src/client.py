@@ -11,13 +11,19 @@ from typing import Any, Dict, Optional
 
 from src.rpc import RPCClient
 from src.utils import parse_address
+from src.utils.framing import CODEC_JSON, CODEC_MSGPACK, msgpack
 
 
 class InferenceClient:
-    def __init__(self, address: str, timeout: float = 600.0):
+    """Framed RPC client. Frames are msgpack when it is importable (servers answer in the request's codec;
+    JSON encoding of every reply was the largest single cost of the coordinator's request path), JSON
+    otherwise or with ``codec="json"``."""
+
+    def __init__(self, address: str, timeout: float = 600.0, codec: str = "msgpack"):
         self.address = address
         self.timeout = timeout
-        self._rpc = RPCClient(max_idle_per_host=1024)
+        use_mp = codec == "msgpack" and msgpack is not None
+        self._rpc = RPCClient(max_idle_per_host=1024, codec=CODEC_MSGPACK if use_mp else CODEC_JSON)
 
     async def infer(self, model: str, inputs: Any, version: Optional[str] = None,
                     request_key: Optional[str] = None, cache: bool = True, **extra) -> Dict[str, Any]:
