@@ -25,11 +25,16 @@ def main():
     meta = AttnMetadata(False, slots, bt, ctx, max_ctx=max_ctx, scratch=sc, **meta_kw)
     outs, pools, stages = [], [], []
     cfg, ws = sc["persistent"]["cfg"], sc["persistent"]["ws"]
-    names = [("slab_q", "slabq_off", "attn_off"), ("attn", "attn_off", "slabod_off"), ("slab_od", "slabod_off", "act_off"),
-             ("act", "act_off", "sspo_off"), ("ssp_o", "sspo_off", "sspd_off"), ("ssp_d", "sspd_off", "err_off")]
+    H, nq = m.arch.hidden_size, (m.hq + 2 * m.hkv) * 128
+    sizes = {"slab_q": cfg["skq"] * 32 * nq * 4, "attn": 32 * m.hq * 128 * 2,
+             "slab_od": max(cfg["sko"], cfg["skd"]) * 32 * H * 4, "act": 32 * m.inter * 2,
+             "ssp_o": (H // cfg["wro"]) * 128 * 4, "ssp_d": (H // cfg["wrd"]) * 128 * 4}
+    offs = {"slab_q": "slabq_off", "attn": "attn_off", "slab_od": "slabod_off", "act": "act_off",
+            "ssp_o": "sspo_off", "ssp_d": "sspd_off"}
+    names = [(n, offs[n], sizes[n]) for n in sizes]
 
     def snap():
-        return {n: ws[cfg[a]:cfg[b]].clone() for n, a, b in names}
+        return {n: ws[cfg[o]:cfg[o] + sz].clone() for n, o, sz in names}
     with torch.inference_mode():
         for _ in range(reps):
             outs.append(m.forward(ids, pos, meta, pool).clone())

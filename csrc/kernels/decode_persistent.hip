@@ -156,20 +156,44 @@ struct WS {
   static constexpr int64_t a16(int64_t x) { return (x + 15) / 16 * 16; }
   static constexpr int SKOD = C::SKO > C::SKD ? C::SKO : C::SKD;
   static constexpr int64_t SLABQ = 0;                                          // f32 [SKQ][32][NQ]
-  static constexpr int64_t ATTN = a16(SLABQ + (int64_t)C::SKQ * XR * C::NQ * 4);  // bf16 [32][HQ 128]
-  static constexpr int64_t SLABOD = a16(ATTN + (int64_t)XR * C::HQ * 128 * 2);  // f32 [SKOD][32][H]
-  static constexpr int64_t ACT = a16(SLABOD + (int64_t)SKOD * XR * C::H * 4);   // bf16 [32][I]
-  static constexpr int64_t SSPO = a16(ACT + (int64_t)XR * C::I * 2);           // f32 [TO][128]
+  static constexpr int64_t SLABOD = a16(SLABQ + (int64_t)C::SKQ * XR * C::NQ * 4);  // f32 [SKOD][32][H]
+  static constexpr int64_t SSPO = a16(SLABOD + (int64_t)SKOD * XR * C::H * 4);  // f32 [TO][128]
   static constexpr int64_t SSPD = a16(SSPO + (int64_t)C::TO * 128 * 4);        // f32 [TD][128]
   static constexpr int64_t TICKO = (SSPD + (int64_t)C::TD * 128 * 4 + 127) / 128 * 128;  // i32 [TO][32]
   static constexpr int64_t TICKD = TICKO + (int64_t)C::TO * 128;              // i32 [TD][32]
   static constexpr int64_t ERR = TICKD + (int64_t)C::TD * 128;                // i32 [32]
-  static constexpr int64_t DONE = ERR + 128;                                  // u64 [64 shards][16]: exits
+  static constexpr int64_t DONE = ERR + 128;                                  // u64 [NSH shards][16]: exits
   static constexpr int64_t SYNC = DONE + (int64_t)NSH * 128;                  // u32 [layers][DP_SYNC_LD]
+  // Per-layer activations, each written once per launch (the residual stream is not updated in place):
+  // an XCD's L2 can never hold a stale line of one, so the activation loads are plain cached loads
+  // (each line comes from memory once per XCD instead of once per CU with sc1).
+  static constexpr int64_t L_ATTN = a16((int64_t)XR * C::HQ * 128 * 2);        // bf16 [32][HQ 128]
+  static constexpr int64_t L_ACT = a16((int64_t)XR * C::I * 2);                // bf16 [32][I]
+  static constexpr int64_t L_H = a16((int64_t)XR * C::H * 2);                  // bf16 [32][H]
+  static constexpr int64_t PER_LAYER = L_ATTN + L_ACT + 2 * L_H;               // attn, act, h after o / down
+  static __host__ __device__ __forceinline__ int64_t acts(int layers) {
+    return SYNC + (int64_t)4 * DP_SYNC_LD * layers;
+  }
+  static __device__ __forceinline__ char* lay(const DpArgs& a, int l) {
+    return a.ws + acts(a.l1 - a.l0) + (int64_t)(l - a.l0) * PER_LAYER;
+  }
+  static __device__ __forceinline__ bf16_t* attn(const DpArgs& a, int l) {
+    return reinterpret_cast<bf16_t*>(lay(a, l));
+  }
+  static __device__ __forceinline__ bf16_t* act(const DpArgs& a, int l) {
+    return reinterpret_cast<bf16_t*>(lay(a, l) + L_ATTN);
+  }
+  static __device__ __forceinline__ bf16_t* h_mid(const DpArgs& a, int l) {  // after the o-projection
+    return reinterpret_cast<bf16_t*>(lay(a, l) + L_ATTN + L_ACT);
+  }
+  static __device__ __forceinline__ bf16_t* h_in(const DpArgs& a, int l) {  // the layer's input
+    return l == a.l0 ? a.h : reinterpret_cast<bf16_t*>(lay(a, l - 1) + L_ATTN + L_ACT + L_H);
+  }
+  static __device__ __forceinline__ bf16_t* h_out(const DpArgs& a, int l) {  // after down (last: a.h)
+    return l == a.l1 - 1 ? a.h : reinterpret_cast<bf16_t*>(lay(a, l) + L_ATTN + L_ACT + L_H);
+  }
   static __device__ __forceinline__ float* slab_q(const DpArgs& a) { return reinterpret_cast<float*>(a.ws + SLABQ); }
-  static __device__ __forceinline__ bf16_t* attn(const DpArgs& a) { return reinterpret_cast<bf16_t*>(a.ws + ATTN); }
   static __device__ __forceinline__ float* slab_od(const DpArgs& a) { return reinterpret_cast<float*>(a.ws + SLABOD); }
-  static __device__ __forceinline__ bf16_t* act(const DpArgs& a) { return reinterpret_cast<bf16_t*>(a.ws + ACT); }
   static __device__ __forceinline__ float* ssp_o(const DpArgs& a) { return reinterpret_cast<float*>(a.ws + SSPO); }
   static __device__ __forceinline__ float* ssp_d(const DpArgs& a) { return reinterpret_cast<float*>(a.ws + SSPD); }
   static __device__ __forceinline__ int* tick_o(const DpArgs& a) { return reinterpret_cast<int*>(a.ws + TICKO); }
@@ -394,18 +418,18 @@ __device__ __forceinline__ void issue_x(const Walk& w, const Rt& r, const DpArgs
   switch (p) {
     case P_QKV:
       tile_slice<C::TQ, C::SKQ>(w.t, tile, slice);
-      X = a.h; ldx = C::H; k0 = slice * (C::H / C::SKQ); wr = C::WRQ;
+      X = WS<C>::h_in(a, l); ldx = C::H; k0 = slice * (C::H / C::SKQ); wr = C::WRQ;
       break;
     case P_O:
       tile_slice<C::TO, C::SKO>(w.t, tile, slice);
-      X = WS<C>::attn(a); ldx = C::HQ * D; k0 = slice * (C::HQ * D / C::SKO); wr = C::WRO;
+      X = WS<C>::attn(a, l); ldx = C::HQ * D; k0 = slice * (C::HQ * D / C::SKO); wr = C::WRO;
       break;
     case P_GU:
-      X = a.h; ldx = C::H; k0 = 0; wr = C::WRG;
+      X = WS<C>::h_mid(a, l); ldx = C::H; k0 = 0; wr = C::WRG;
       break;
     default:
       tile_slice<C::TD, C::SKD>(w.t, tile, slice);
-      X = WS<C>::act(a); ldx = C::I; k0 = slice * (C::I / C::SKD); wr = C::WRD;
+      X = WS<C>::act(a, l); ldx = C::I; k0 = slice * (C::I / C::SKD); wr = C::WRD;
       break;
   }
   char* ximg = slot + wr * ROWB;
@@ -414,10 +438,10 @@ __device__ __forceinline__ void issue_x(const Walk& w, const Rt& r, const DpArgs
   for (int i = 0; i < XR * ROWB / 1024; ++i) {
     const int rr = 4 * i + (lane >> 4);
     const int lch = (lane & 15) ^ (rr & 15);
-    if (DP_DBG(r) & 1)
-      dma16<0>(X + (int64_t)min(rr, r.M - 1) * ldx + k0 + lch * 8, ximg + i * 1024);
-    else
+    if (DP_DBG(r) & 1)  // diagnostics A/B: coherent (sc1) activation loads
       dma16<16>(X + (int64_t)min(rr, r.M - 1) * ldx + k0 + lch * 8, ximg + i * 1024);
+    else  // write-once per launch: cached loads (see WS)
+      dma16<0>(X + (int64_t)min(rr, r.M - 1) * ldx + k0 + lch * 8, ximg + i * 1024);
   }
   if (p == P_GU && w.k == 0 && w.t == r.b) {  // the o-projection's per-tile row statistics [tile][0..31]
 #pragma unroll
@@ -613,14 +637,14 @@ __device__ __forceinline__ void epi_qkv(const float* red, const Rt& r, const DpA
 // o / down epilogue (wave 3): split-K partial -> slab; the last arriver adds every slice into the residual
 // stream (bf16, in place) and writes the tile's row sums of squares (the next RMSNorm's statistics)
 template <int WR, int TILES, int SK, int H>
-__device__ __forceinline__ bool epi_resid(const float* red, const Rt& r, float* slab, bf16_t* hres, int t, int* tick,
-                                          float* ssp, int lane) {
+__device__ __forceinline__ bool epi_resid(const float* red, const Rt& r, float* slab, const bf16_t* hin, bf16_t* hout,
+                                          int t, int* tick, float* ssp, int lane) {
   constexpr int RS = red_ld<WR>(), Q = WR / 4, EPL = XR * Q / 64;
   static_assert(Q == 8 || Q == 16 || Q == 32, "a row's float4 groups must sit in one wave");
   int tile, slice;
   tile_slice<TILES, SK>(t, tile, slice);
   const int n0 = tile * WR;
-  const auto rslab = brsrc(slab + n0), rh = brsrc(hres + n0);
+  const auto rslab = brsrc(slab + n0), rh = brsrc(hin + n0);
   f4 own[EPL];
 #pragma unroll
   for (int i = 0; i < EPL; ++i) {
@@ -687,7 +711,7 @@ __device__ __forceinline__ bool epi_resid(const float* red, const Rt& r, float* 
 #pragma unroll
   for (int i = 0; i < EPL; ++i) {
     const int e = lane + 64 * i, m = e / Q, j = 4 * (e - m * Q);
-    if (m < r.M) st_sc1_u2(hres + (int64_t)m * H + n0 + j, hw[i]);
+    if (m < r.M) st_sc1_u2(hout + (int64_t)m * H + n0 + j, hw[i]);
     if (e % Q == 0) st_sc1_u1(ssp + tile * DECODE_SSP_LD + m, __float_as_uint(ss[i]));
   }
   return true;
@@ -697,7 +721,7 @@ __device__ __forceinline__ bool epi_resid(const float* red, const Rt& r, float* 
 // multi-launch kernel's summation order: 8 tile slices, each summed in tile order), SiLU(gate) * up -> act
 template <class C>
 __device__ __forceinline__ void epi_gu(const float* red, const char* scr, char* ctl, const Rt& r, const DpArgs& a,
-                                       int t, int lane) {
+                                       int l, int t, int lane) {
   constexpr int WR = C::WRG, RS = red_ld<WR>(), NO = WR / 2, NP = NO / 2, EPL = (XR * NP + 63) / 64;
   float* rs = reinterpret_cast<float*>(ctl + C_RS);
   if (lane < XR) {
@@ -726,7 +750,7 @@ __device__ __forceinline__ void epi_gu(const float* red, const char* scr, char* 
 #pragma unroll
   for (int i = 0; i < EPL; ++i) {
     const int e = lane + 64 * i, m = e / NP, j = 2 * (e - m * NP);
-    if (e < XR * NP && m < r.M) st_sc1_u1(WS<C>::act(a) + (int64_t)m * C::I + t * NO + j, pk[i]);
+    if (e < XR * NP && m < r.M) st_sc1_u1(WS<C>::act(a, l) + (int64_t)m * C::I + t * NO + j, pk[i]);
   }
 }
 
@@ -823,7 +847,7 @@ __device__ __forceinline__ void att_merge_store(const char* scr, const DpArgs& a
   for (int i = 0; i < EPL; ++i) {
     const int e = lane + 64 * i;
     const int rr = e / (D / 4), d = 4 * (e % (D / 4));
-    if (e < G * (D / 4)) st_sc1_u2(WS<C>::attn(a) + ((int64_t)seq * C::HQ + kvh * G + rr) * D + d, pk[i]);
+    if (e < G * (D / 4)) st_sc1_u2(WS<C>::attn(a, l) + ((int64_t)seq * C::HQ + kvh * G + rr) * D + d, pk[i]);
   }
 }
 
@@ -1002,10 +1026,12 @@ __device__ __forceinline__ void gemm_task(S_& S, char* ctl, int lane0) {
         bool pub = true;
         if constexpr (PH == P_QKV) epi_qkv<C>(red, S.r, S.a, t, lane);
         else if constexpr (PH == P_O)
-          pub = epi_resid<WR, C::TO, C::SKO, C::H>(red, S.r, WS<C>::slab_od(S.a), S.a.h, t, WS<C>::tick_o(S.a),
+          pub = epi_resid<WR, C::TO, C::SKO, C::H>(red, S.r, WS<C>::slab_od(S.a), WS<C>::h_in(S.a, l),
+                                                   WS<C>::h_mid(S.a, l), t, WS<C>::tick_o(S.a),
                                                    WS<C>::ssp_o(S.a), lane);
-        else if constexpr (PH == P_GU) epi_gu<C>(red, S.scr, ctl, S.r, S.a, t, lane);
-        else pub = epi_resid<WR, C::TD, C::SKD, C::H>(red, S.r, WS<C>::slab_od(S.a), S.a.h, t, WS<C>::tick_d(S.a),
+        else if constexpr (PH == P_GU) epi_gu<C>(red, S.scr, ctl, S.r, S.a, l, t, lane);
+        else pub = epi_resid<WR, C::TD, C::SKD, C::H>(red, S.r, WS<C>::slab_od(S.a), WS<C>::h_mid(S.a, l),
+                                                      WS<C>::h_out(S.a, l), t, WS<C>::tick_d(S.a),
                                                       WS<C>::ssp_d(S.a), lane);
         if (pub) publish<C>(S.a, S.r, l, PH, lane);
       }
@@ -1174,8 +1200,9 @@ bool decode_persistent_config(int H, int I, int hq, int hkv, int layers, int* cf
     using C = decltype(c);
     const int v[7] = {C::WRQ, C::SKQ, C::WRO, C::SKO, C::WRG, C::WRD, C::SKD};
     for (int i = 0; i < 7; ++i) cfg7[i] = v[i];
-    const int64_t v2[9] = {WS<C>::SYNC + (int64_t)4 * DP_SYNC_LD * layers, WS<C>::ERR, WS<C>::SYNC, WS<C>::SLABQ,
-                           WS<C>::ATTN, WS<C>::SLABOD, WS<C>::ACT, WS<C>::SSPO, WS<C>::SSPD};
+    const int64_t base = WS<C>::acts(layers);  // layer 0's attention output / SiLU output
+    const int64_t v2[9] = {base + (int64_t)layers * WS<C>::PER_LAYER, WS<C>::ERR, WS<C>::SYNC, WS<C>::SLABQ,
+                           base, WS<C>::SLABOD, base + WS<C>::L_ATTN, WS<C>::SSPO, WS<C>::SSPD};
     for (int i = 0; i < 9; ++i) lay4[i] = v2[i];
     return true;
   };
