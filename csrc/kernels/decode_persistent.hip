@@ -175,7 +175,7 @@ struct WS {
     return SYNC + (int64_t)4 * DP_SYNC_LD * layers;
   }
   static __device__ __forceinline__ char* lay(const DpArgs& a, int l) {
-    return a.ws + acts(a.l1 - a.l0) + (int64_t)(l - a.l0) * PER_LAYER;
+    return a.ws + acts(a.l1) + (int64_t)l * PER_LAYER;  // (the launcher requires l0 = 0)
   }
   static __device__ __forceinline__ bf16_t* attn(const DpArgs& a, int l) {
     return reinterpret_cast<bf16_t*>(lay(a, l));
@@ -187,7 +187,7 @@ struct WS {
     return reinterpret_cast<bf16_t*>(lay(a, l) + L_ATTN + L_ACT);
   }
   static __device__ __forceinline__ bf16_t* h_in(const DpArgs& a, int l) {  // the layer's input
-    return l == a.l0 ? a.h : reinterpret_cast<bf16_t*>(lay(a, l - 1) + L_ATTN + L_ACT + L_H);
+    return l == 0 ? a.h : reinterpret_cast<bf16_t*>(lay(a, l - 1) + L_ATTN + L_ACT + L_H);
   }
   static __device__ __forceinline__ bf16_t* h_out(const DpArgs& a, int l) {  // after down (last: a.h)
     return l == a.l1 - 1 ? a.h : reinterpret_cast<bf16_t*>(lay(a, l) + L_ATTN + L_ACT + L_H);
@@ -205,8 +205,8 @@ struct WS {
   }
 };
 
-struct Rt {  // run-time uniforms
-  int P, b, M, l0, l1;
+struct Rt {  // run-time uniforms (layers [0, l1): the launcher requires l0 = 0)
+  int P, b, M, l1;
   int dbg;  // diagnostic builds: experiment switches (DpArgs::dbg); 0 otherwise
 };
 #ifdef DIE_KERNEL_DIAG
@@ -257,7 +257,7 @@ struct Walk {
   uint32_t pos;
 };
 
-__device__ __forceinline__ int wl(const Rt& r, const Walk& w) { return r.l0 + w.q / NPH; }
+__device__ __forceinline__ int wl(const Rt& r, const Walk& w) { return w.q / NPH; }
 __device__ __forceinline__ int wp(const Walk& w) { return w.q % NPH; }
 
 template <class C>
@@ -325,10 +325,18 @@ __device__ __forceinline__ int x_pieces(const Rt& r, int p, int t, int k, int wa
   return n;
 }
 
+// lane-derived values made opaque per chunk: otherwise the compiler hoists every loop-invariant per-lane
+// address (dozens of 64-bit pointers) out of the loops and spills them
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 // ------------------------------------------------------------------------------------------------------
 // issue: early stream (waves 0, 1): weight pieces (nt) or the attention task's K (wave 0) / V (wave 1) image
 template <class C>
 __device__ __forceinline__ void issue_w(const Walk& w, const Rt& r, const DpArgs& a, char* ring, int wave, int lane) {
+  lane = opaque(lane);  // per-lane addressing stays inside the branch that issues (no hoisting out of the loops)
   char* slot = ring + (w.pos % RING);
   const int p = wp(w);
   const DpLayerW* L = a.layers + wl(r, w);
@@ -388,10 +396,12 @@ __device__ __forceinline__ void issue_w(const Walk& w, const Rt& r, const DpArgs
 // operands
 template <class C>
 __device__ __forceinline__ void issue_x(const Walk& w, const Rt& r, const DpArgs& a, char* ring, char* scr, int lane) {
+  lane = opaque(lane);  // per-lane addressing stays inside the branch that issues (no hoisting out of the loops)
   char* slot = ring + (w.pos % RING);
   const int p = wp(w), l = wl(r, w);
   if (p == P_ATT) {
     if (w.k != 0) return;
+    lane = opaque(lane);
     constexpr int G = C::G, FR = C::SKQ * (G + 2);
     const int seq = w.t / C::HKV, kvh = w.t - seq * C::HKV;
     const float* srow = WS<C>::slab_q(a) + (int64_t)seq * C::NQ;
@@ -403,7 +413,7 @@ __device__ __forceinline__ void issue_x(const Walk& w, const Rt& r, const DpArgs
       const int col = j < G ? (kvh * G + j) * D : (j == G ? (C::HQ + kvh) * D : (C::HQ + C::HKV + kvh) * D);
       dma16<16>(srow + sl * sstride + col + (lane & 31) * 4, scr + i * 1024);
     }
-    const bool first = l == r.l0;
+    const bool first = l == 0;
     const float* ssp = first ? a.ssp0 : WS<C>::ssp_d(a);
     const int tiles = first ? a.ssp0_tiles : C::TD;
 #pragma unroll
@@ -456,7 +466,7 @@ __device__ __forceinline__ void issue_x(const Walk& w, const Rt& r, const DpArgs
 // dependency counters: sync[(l - l0) * DP_SYNC_LD + (phase * NSH + shard) * LINEI]
 template <class C>
 __device__ __forceinline__ int* counter(const DpArgs& a, const Rt& r, int l, int p) {
-  return WS<C>::sync(a) + (l - r.l0) * DP_SYNC_LD + p * NSH * LINEI;
+  return WS<C>::sync(a) + l * DP_SYNC_LD + p * NSH * LINEI;
 }
 
 // phase (l, p) may load its activations once its producer phase has published every task / tile: the
@@ -466,7 +476,7 @@ __device__ __forceinline__ const int* dep_src(const DpArgs& a, const Rt& r, int 
   int pl = l, pp;
   switch (p) {
     case P_QKV:
-      if (l == r.l0) return nullptr;
+      if (l == 0) return nullptr;
       pl = l - 1; pp = P_DN; target = C::TD; break;
     case P_ATT: pp = P_QKV; target = C::NTQ; break;
     case P_O: pp = P_ATT; target = XR * C::HKV; break;  // M * HKV tasks + the launch's padding
@@ -585,6 +595,7 @@ constexpr int red_ld() { return WR % 32 == 0 ? WR + 16 : WR; }  // LDS row pitch
 // in the loader waves), then one barrier
 template <int WR>
 __device__ __forceinline__ void stash_tiles(float* red, const f4 (&acc)[2][2], int wave, int lane) {
+  lane = opaque(lane);  // (per-lane addressing is not hoisted out of the chunk loops)
   constexpr int NT = WR / 16, NTW = (NT + 3) / 4, RS = red_ld<WR>();
   const int fr = lane & 15, kg = lane >> 4;
   const uint32_t base = lds_of(red);
@@ -615,6 +626,7 @@ __device__ __forceinline__ void sched_fence() { asm volatile("" ::: "memory"); }
 // qkv epilogue (wave 3): this slice's fp32 partial -> slab_q[slice] (the attention prologue sums the slices)
 template <class C>
 __device__ __forceinline__ void epi_qkv(const float* red, const Rt& r, const DpArgs& a, int t, int lane) {
+  lane = opaque(lane);  // (per-lane addressing is not hoisted out of the chunk loops)
   constexpr int WR = C::WRQ, RS = red_ld<WR>(), Q = WR / 4, EPL = XR * Q / 64;
   static_assert(XR * Q % 64 == 0, "whole float4 groups per lane");
   int tile, slice;
@@ -639,6 +651,7 @@ __device__ __forceinline__ void epi_qkv(const float* red, const Rt& r, const DpA
 template <int WR, int TILES, int SK, int H>
 __device__ __forceinline__ bool epi_resid(const float* red, const Rt& r, float* slab, const bf16_t* hin, bf16_t* hout,
                                           int t, int* tick, float* ssp, int lane) {
+  lane = opaque(lane);  // (per-lane addressing is not hoisted out of the chunk loops)
   constexpr int RS = red_ld<WR>(), Q = WR / 4, EPL = XR * Q / 64;
   static_assert(Q == 8 || Q == 16 || Q == 32, "a row's float4 groups must sit in one wave");
   int tile, slice;
@@ -722,6 +735,7 @@ __device__ __forceinline__ bool epi_resid(const float* red, const Rt& r, float* 
 template <class C>
 __device__ __forceinline__ void epi_gu(const float* red, const char* scr, char* ctl, const Rt& r, const DpArgs& a,
                                        int l, int t, int lane) {
+  lane = opaque(lane);  // (per-lane addressing is not hoisted out of the chunk loops)
   constexpr int WR = C::WRG, RS = red_ld<WR>(), NO = WR / 2, NP = NO / 2, EPL = (XR * NP + 63) / 64;
   float* rs = reinterpret_cast<float*>(ctl + C_RS);
   if (lane < XR) {
@@ -761,6 +775,7 @@ __device__ __forceinline__ void epi_gu(const float* red, const char* scr, char* 
 template <int G, int SKQ>
 __device__ __forceinline__ void att_prologue(char* scr, const DpArgs& a, int stat_tiles, int tid, int lane,
                                              bf16_t& nk0, bf16_t& nk1, bf16_t& nv) {
+  lane = opaque(lane);  // (per-lane addressing is not hoisted out of the chunk loops)
   const float* sp = reinterpret_cast<const float*>(scr + S_ASSP);
   float ssum = 0.f;
 #pragma unroll
@@ -802,6 +817,7 @@ __device__ __forceinline__ void att_prologue(char* scr, const DpArgs& a, int sta
 // the new token's K / V row to the paged cache (for later steps — this step patched it into the LDS images)
 template <class C>
 __device__ __forceinline__ void att_merge_store(const char* scr, const DpArgs& a, int l, int seq, int kvh, int lane) {
+  lane = opaque(lane);  // (per-lane addressing is not hoisted out of the chunk loops)
   constexpr int G = C::G, EPL = (G * (D / 4) + 63) / 64;
   const float* ml = reinterpret_cast<const float*>(scr + S_ML);
   const float* ob = reinterpret_cast<const float*>(scr + S_OB);
@@ -906,7 +922,7 @@ struct Stream {
       // a phase's counter must advance by the same amount every launch: the attention phase has M * HKV
       // tasks, so workgroup 0 adds the (XR - M) * HKV missing ones up front
       if (r.b == 0 && r.M < XR && (threadIdx.x & 63) == 0)
-        for (int l = r.l0; l < r.l1; ++l)
+        for (int l = 0; l < r.l1; ++l)
           __hip_atomic_fetch_add(counter<C>(a, r, l, P_ATT), (XR - r.M) * C::HKV, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -983,12 +999,6 @@ struct Stream {
   }
 };
 
-// lane-derived values made opaque per chunk: otherwise the compiler hoists every loop-invariant per-lane
-// address (dozens of 64-bit pointers) out of the loops and spills them
-__device__ __forceinline__ int opaque(int v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
 
 // timeline stamps (diagnostic builds only, DIE_KERNEL_DIAG): per workgroup and phase index, the 100 MHz clock
 // at task entry, data ready, compute done and epilogue done
@@ -1062,7 +1072,7 @@ __device__ __forceinline__ void att_task(S_& S, int lane0) {
     char* slot = S.begin(lane);
     if (k == 0) DP_STAMP(S, q0, 1);
     if (k == 0) {
-      att_prologue<G, C::SKQ>(S.scr, a, l == S.r.l0 ? a.ssp0_tiles : C::TD, tid, lane, nk0, nk1, nv);
+      att_prologue<G, C::SKQ>(S.scr, a, l == 0 ? a.ssp0_tiles : C::TD, tid, lane, nk0, nk1, nv);
       lds_fence_barrier();
       {  // the rotated query rows (asm reads: no compiler-inserted vmcnt wait in the loader waves)
         const uint32_t qa = lds_of(S.scr + S_AQ) + min(row, G - 1) * (D * 2) + h * 16;
@@ -1131,7 +1141,7 @@ __device__ __forceinline__ void run_role(const DpArgs& a, const Rt& r, char* sme
                                          int lane0) {
   char* ctl = smem + RING + SCR;
   using St = Stream<C, ROLE>;
-  St S(a, r, smem, smem + RING, ready, wave, (a.l1 - a.l0) * NPH);
+  St S(a, r, smem, smem + RING, ready, wave, r.l1 * NPH);
 #pragma unroll 1
   while (S.cw.q < S.qend) {
     switch (wp(S.cw)) {
@@ -1159,7 +1169,6 @@ __global__ void __launch_bounds__(NTH, 1) decode_persistent_kernel(DpArgs a) {
   r.P = gridDim.x;
   r.b = blockIdx.x;
   r.M = a.M;
-  r.l0 = a.l0;
   r.l1 = a.l1;
   r.dbg = a.dbg;
   const uint32_t ready = lds_of(smem + RING + SCR + C_READY);
@@ -1216,7 +1225,7 @@ bool decode_persistent_config(int H, int I, int hq, int hkv, int layers, int* cf
 // dependency counters need no per-launch reset).
 hipError_t launch_decode_persistent(const DpArgs& a, hipStream_t s) {
   using namespace dp;
-  if (a.M < 1 || a.M > XR || a.l1 <= a.l0) return hipErrorInvalidValue;
+  if (a.M < 1 || a.M > XR || a.l0 != 0 || a.l1 < 1) return hipErrorInvalidValue;
   if (cfg_matches<Cfg8B>(a)) return launch_cfg<Cfg8B>(a, s);
   if (cfg_matches<CfgMini>(a)) return launch_cfg<CfgMini>(a, s);
   return hipErrorInvalidValue;
