@@ -1,43 +1,40 @@
 // Persistent decode step: every layer of a dense Llama decode step (qkv -> attention -> o -> gate/up ->
-// down, M <= 32 rows) in ONE launch, one 256-thread workgroup per CU, with a weight / KV stream that never
-// stops at an op boundary.
+// down, M <= 32 rows) in ONE launch, one 256-thread workgroup per CU, with a weight / KV stream that does not
+// stop at an op boundary.
 //
 // Why (MI355X_MICROARCH.md "prefetch-credit", "engine-vs-launches"): as five launches
-// per layer every op pays its own fill (first-chunk latency), drain (stragglers) and launch gap — about
-// 24 us of a 106 us layer at batch 32. The weights (and the attention's cached K/V) never depend on the
-// activations, so here a loader keeps issuing the NEXT op's weight chunks into the LDS ring while the
-// current op drains and while its dependency resolves; only the small activation stream waits.
+// per layer every op pays its own fill (first-chunk latency), drain and launch gap. The weights (and the
+// attention's cached K/V) never depend on the activations, so here the NEXT task's weight chunks are issued
+// into the LDS ring while the current task finishes, runs its epilogue and waits for its dependency; only
+// the small activation pieces wait.
 //
-// Structure:
+// Structure (round 3 rewrite: the first version's three generic walkers and wave roles cost ~160 us per layer
+// in bookkeeping alone, measured with every load switched off):
 //  * Work = (layer, phase, task) in a fixed order; phase = qkv | attention | o | gate/up | down. Every phase
 //    has ~one task per CU (column tile x K slice for the GEMMs, (sequence, kv head) pair for attention);
-//    workgroup b runs tasks b, b + P, ... of each phase. A task is a sequence of chunks: one K slice
-//    of KC = 128 (GEMMs: WR weight rows + 32 activation rows, 256-byte swizzled image rows) or 128 keys
-//    (attention: K and V images, 64 KiB).
-//  * The chunks of all tasks form one stream through a 128 KiB byte ring in LDS (a chunk is contiguous;
-//    positions are monotonic, a chunk that would straddle the end starts at the next lap). Three walkers
-//    run over the same deterministic sequence: the W walker issues the weight / K/V pieces as soon as the
-//    ring has room, the X walker issues the activation pieces once the chunk's phase is READY, and the
-//    consumer computes.
-//  * Wave roles (vmcnt is per wave and loads/stores retire in issue order, so an early stream and a late
-//    stream must never share a wave): waves 0 and 1 issue ONLY the early stream (weights, K/V), wave 2
-//    ONLY the late stream (activations, attention prologue operands, norm statistics), wave 3 never loads
-//    into the ring — it polls the dependency counters, does every global store of the epilogues (sc1,
-//    write-through), takes the split-K tickets and publishes. All four waves compute (MFMA).
-//  * Hand-offs (MI355X_MICROARCH.md visibility table, row 1): the producer's payload is stored sc1 by
-//    wave 3, drained (vmcnt(0)), then ONE lane adds to the phase counter (agent scope, 16 shards, one
-//    128-byte line each). The consumer's wave 3 polls the counter with relaxed agent loads, publishes READY
-//    in LDS, and the activation loads that follow are sc1 LDS-DMA.
+//    workgroup b runs tasks b, b + P, ... of each phase. A task is nch chunks: one K slice of KC = 128 (GEMMs:
+//    WR weight rows + 32 activation rows, 256-byte swizzled image rows) or 128 keys (attention: K and V images,
+//    64 KiB). Each phase's chunk loop is compiled for that phase (tiles are compile-time).
+//  * The chunks form one stream through a 128 KiB byte ring in LDS (positions monotonic; a chunk never
+//    straddles the end). Before every chunk the workgroup tops the ring up: the current task's chunks
+//    (weights + activations, split over the four waves), then the next task's WEIGHT pieces (waves 0..2). A
+//    chunk whose activations were not ready when its weights went out gets its activation pieces issued once
+//    the dependency is met ("late X").
+//  * vmcnt is per wave and retires in issue order, so each wave records, per chunk, how many vector-memory ops
+//    it had issued after its last piece of that chunk (lane seq % 64 of a VGPR, v_writelane / v_readlane) and
+//    waits with a counted vmcnt for exactly that. Wave 3 issues no next-task prefetch: its queue is empty when
+//    it runs an epilogue (global loads / write-through stores), polls a dependency or publishes. Pieces that
+//    land in the task scratch (norm statistics, attention prologue operands) are wave 3's too, issued after
+//    its previous epilogue read that scratch.
+//  * Hand-offs (MI355X_MICROARCH.md visibility table, row 1): the producer's payload is stored sc1 by wave 3,
+//    drained (vmcnt(0)), then ONE lane adds to the phase counter (agent scope, 16 shards, one 128-byte line
+//    each). A consumer's wave 3 polls the shards with relaxed agent loads, then a barrier releases the others.
 //  * The counters and split-K tickets are never reset (no memset node in the step's graph): every launch
 //    advances each phase's counter by a fixed amount (the attention phase is padded to 32 * HKV tasks),
 //    the launch's epoch comes from the workgroups' exit count, and "met" is a wrap-around difference.
-//  * Determinism: the GEMM partial sums of the four waves are combined through LDS in wave order, the
-//    attention merge in wave order, split-K slabs in slice order — the same arithmetic as the multi-launch
-//    path (gemm_decode.hip SPLIT 0 tiles at KC = 128, attention.hip v3 FUSED with one part per pair), so
-//    the two paths are bit-identical for the same tiles (tests/test_decode_persistent_gpu.py).
-//  * Deadlock freedom: dependencies only point to earlier phases and a workgroup runs its tasks in
-//    order; the grid is one workgroup per CU (all resident). Every wait is bounded: a timeout sets the
-//    error word and lets the launch drain (its outputs are then garbage, and the host raises).
+//  * Deadlock freedom: dependencies only point to earlier phases and a workgroup runs its tasks in order; the
+//    grid is one workgroup per CU (all resident). Every wait is bounded: a timeout sets the error word and lets
+//    the launch drain (its outputs are then garbage, and the host raises).
 #include "attn_common.h"
 #include "common.h"
 #include "launchers.h"
@@ -56,6 +53,7 @@ constexpr int XR = 32;                       // activation rows per chunk (decod
 constexpr int KC = 128;                      // K per GEMM chunk
 constexpr int ROWB = 256;                    // bytes per GEMM image row
 constexpr int ACH = 65536;                   // attention chunk: 128 keys of K + V
+constexpr int AHEAD = 8;                     // chunks in the ring at most (the per-wave vmcnt field is 6 bits)
 constexpr int NSH = 16;                      // counter shards (lanes 0..15 of the polling wave)
 constexpr int LINEI = 32;                    // ints per 128-byte line: every shard / ticket on its own line
                                              // (same-line atomics from 256 CUs serialise: ~80 us per phase)
@@ -72,7 +70,6 @@ constexpr int S_ANKV = 23 * 1024 + 512;      // the new token's rotated key and 
 constexpr int S_ML = 0;                      // merge: per-wave (m, l) [4][32][2]
 constexpr int S_OB = 1024;                   //        per-wave O [4][G][128] fp32 (<= 16 KiB)
 // CTL
-constexpr int C_READY = 0;                   // highest phase id known READY (int)
 constexpr int C_RS = 64;                     // gate/up epilogue: row scales [32] fp32
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -132,7 +129,6 @@ __device__ __forceinline__ void lds_fence_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 }
-
 // ------------------------------------------------------------------------------------------------------
 // Model geometry and tiles are compile-time (one instantiation per served shape: no run-time divisions and
 // few live scalar registers); only the decode rows M, the grid and the pointers are run-time.
@@ -214,7 +210,6 @@ struct Rt {  // run-time uniforms (layers [0, l1): the launcher requires l0 = 0)
 #else
 #define DP_DBG(r) 0
 #endif
-
 template <class C>
 __device__ __forceinline__ int ntasks(const Rt& r, int p) {
   switch (p) {
@@ -250,160 +245,93 @@ __device__ __forceinline__ void tile_slice(int t, int& tile, int& slice) {
   }
 }
 
-// A walker over this workgroup's chunk sequence: phase index q = (layer - l0) * NPH + phase, task t, chunk k
-// of nch, sequence number idx, ring position pos (monotonic; a chunk never straddles the ring's end).
-struct Walk {
-  int q, t, k, nch, idx;
-  uint32_t pos;
-};
-
-__device__ __forceinline__ int wl(const Rt& r, const Walk& w) { return w.q / NPH; }
-__device__ __forceinline__ int wp(const Walk& w) { return w.q % NPH; }
+// read-only launch inputs (layer table, block tables, context lengths) through the constant address space:
+// wave-uniform addresses become scalar loads that the compiler batches and waits for (lgkmcnt) itself; as
+// vector loads every use would wait on vmcnt and so on the ring's in-flight stream
+template <class T>
+__device__ __forceinline__ T cld(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)p;
+}
 
 template <class C>
 __device__ __forceinline__ int task_chunks(const DpArgs& a, int p, int t) {
   switch (p) {
     case P_QKV: return C::CQ;
-    case P_ATT: return (sld_i32(a.ctx + t / C::HKV) + DEC_KEYS - 1) / DEC_KEYS;
+    case P_ATT: return (cld(a.ctx + t / C::HKV) + DEC_KEYS - 1) / DEC_KEYS;
     case P_O: return C::CO;
     case P_GU: return C::CG;
     default: return C::CD;
   }
 }
 
-// first task of phase index >= w.q for this workgroup (phases without a task for it are skipped)
-template <class C>
-__device__ __forceinline__ void walk_settle(Walk& w, const Rt& r, const DpArgs& a, int qend) {
-  while (w.q < qend && w.t >= ntasks<C>(r, wp(w))) {
-    ++w.q;
-    w.t = r.b;
-  }
-  if (w.q < qend) {
-    w.nch = task_chunks<C>(a, wp(w), w.t);
-    const uint32_t sz = chunk_bytes<C>(wp(w)), off = w.pos % RING;
-    if (off + sz > RING) w.pos += RING - off;
-  }
-}
-
-template <class C>
-__device__ __forceinline__ void walk_begin(Walk& w, const Rt& r, const DpArgs& a, int qend) {
-  w.q = 0;
-  w.t = r.b;
-  w.k = 0;
-  w.idx = 0;
-  w.pos = 0;
-  walk_settle<C>(w, r, a, qend);
-}
-
-template <class C>
-__device__ __forceinline__ void walk_next(Walk& w, const Rt& r, const DpArgs& a, int qend) {
-  w.pos += chunk_bytes<C>(wp(w));
-  ++w.idx;
-  if (++w.k < w.nch) {
-    const uint32_t sz = chunk_bytes<C>(wp(w)), off = w.pos % RING;
-    if (off + sz > RING) w.pos += RING - off;
-    return;
-  }
-  w.k = 0;
-  w.t += r.P;
-  walk_settle<C>(w, r, a, qend);
-}
-
-// pieces (1 KiB LDS-DMA instructions) this wave issues for a chunk: waves 0 / 1 the early stream, wave 2 the
-// late stream; the same counts drive the issue and the counted waits
-template <class C>
-__device__ __forceinline__ int w_pieces(int p, int wave) {
-  if (wave > 1) return 0;
-  return p == P_ATT ? 32 : wr_of<C>(p) / 8;  // WR rows x 256 B = WR / 4 pieces, split over two waves
-}
-template <class C>
-__device__ __forceinline__ int x_pieces(const Rt& r, int p, int t, int k, int wave) {
-  if (wave != 2) return 0;
-  if (p == P_ATT) return k == 0 ? (C::SKQ * (C::G + 2) + 1) / 2 + 3 : 0;
-  int n = XR * ROWB / 1024;  // 8
-  if (p == P_GU && k == 0 && t == r.b) n += (C::TO + 7) / 8;  // the o statistics, once per layer
-  return n;
-}
-
-// lane-derived values made opaque per chunk: otherwise the compiler hoists every loop-invariant per-lane
-// address (dozens of 64-bit pointers) out of the loops and spills them
+// lane-derived values made opaque per call: otherwise the compiler hoists every loop-invariant per-lane
+// address (dozens of 64-bit pointers) out of the task loops and spills them
 __device__ __forceinline__ int opaque(int v) {
   asm volatile("" : "+v"(v));
   return v;
 }
 
 // ------------------------------------------------------------------------------------------------------
-// issue: early stream (waves 0, 1): weight pieces (nt) or the attention task's K (wave 0) / V (wave 1) image
-template <class C>
-__device__ __forceinline__ void issue_w(const Walk& w, const Rt& r, const DpArgs& a, char* ring, int wave, int lane) {
-  lane = opaque(lane);  // per-lane addressing stays inside the branch that issues (no hoisting out of the loops)
-  char* slot = ring + (w.pos % RING);
-  const int p = wp(w);
-  const DpLayerW* L = a.layers + wl(r, w);
-  if (p == P_ATT) {
-    const int seq = w.t / C::HKV, kvh = w.t - seq * C::HKV;
-    const int ctx = sld_i32(a.ctx + seq);
+// Weight pieces (1 KiB LDS-DMA each) of chunk k of task t, phase P: piece j is issued by wave j % nw (nw = 4
+// for the current task, 3 for the next task's prefetch). GEMM: WR / 4 pieces of the tile-packed weights (each
+// one linear 1 KiB read, nt: each weight byte is read once per step). Attention: 32 pieces of the K image
+// (row r, 16-byte chunk c at c ^ (r & 15)) and 32 of the V image (c ^ ((r & 3) << 2)); keys past the context
+// load the last key (masked later).
+template <class C, int P>
+__device__ __forceinline__ void issue_w(const DpArgs& a, int l, int t, int k, char* slot, int nw, int wave, int lane,
+                                        int& issued) {
+  lane = opaque(lane);
+  const DpLayerW* L = a.layers + l;
+  if constexpr (P == P_ATT) {
+    const int seq = t / C::HKV, kvh = t - seq * C::HKV;
+    const int ctx = cld(a.ctx + seq);
     const int* bt = a.bt + (int64_t)seq * a.bt_stride;
-    const bf16_t* cache = lw_ptr(wave == 0 ? &L->kc : &L->vc);
-    char* img = slot + wave * (DEC_KEYS * DEC_ROW);
-    const int pch = lane & 15;
-#pragma unroll 4
-    for (int i = 0; i < 32; ++i) {
-      const int kr0 = w.k * DEC_KEYS + 4 * i;
-      const int64_t blk = sld_i32(bt + (min(kr0, ctx - 1) >> 4));
-      const int rr = 4 * i + (lane >> 4);
-      const int key = min(kr0 + (lane >> 4), ctx - 1);  // past the context: the last key (masked later)
+    const bf16_t* kc = cld(&L->kc);
+    const bf16_t* vc = cld(&L->vc);
+    const int lastb = (ctx - 1) >> 4, pch = lane & 15, sub = lane >> 4;
+#pragma unroll 1
+    for (int j = wave; j < 64; j += nw) {
+      const int i = j & 31;
+      const int kr0 = k * DEC_KEYS + 4 * i;
+      const int64_t blk = cld(bt + min(kr0 >> 4, lastb));
+      const int rr = 4 * i + sub;
+      const int key = min(kr0 + sub, ctx - 1);
       const int64_t roff = ((blk * C::HKV + kvh) * 16 + (key & 15)) * D;
-      const int c = wave == 0 ? (pch ^ (rr & 15)) : (pch ^ ((rr & 3) << 2));
-      dma16<0>(cache + roff + c * 8, img + i * 1024);
+      if (j < 32) dma16<0>(kc + roff + (pch ^ (rr & 15)) * 8, slot + i * 1024);
+      else dma16<0>(vc + roff + (pch ^ ((rr & 3) << 2)) * 8, slot + DEC_KEYS * DEC_ROW + i * 1024);
+      ++issued;
     }
-    return;
-  }
-  const bf16_t* base;
-  int npw;
-  auto gemm_base = [&](const bf16_t* W, int tile, int kch, int wr, int kfull) {
-    return W + ((int64_t)tile * (kfull / KC) + kch) * (int64_t)wr * KC + lane * 8;
-  };
-  int tile, slice;
-  switch (p) {
-    case P_QKV:
-      tile_slice<C::TQ, C::SKQ>(w.t, tile, slice);
-      base = gemm_base(lw_ptr(&L->qkv), tile, slice * C::CQ + w.k, C::WRQ, C::H);
-      npw = C::WRQ / 8;
-      break;
-    case P_O:
-      tile_slice<C::TO, C::SKO>(w.t, tile, slice);
-      base = gemm_base(lw_ptr(&L->o), tile, slice * C::CO + w.k, C::WRO, C::HQ * D);
-      npw = C::WRO / 8;
-      break;
-    case P_GU:
-      base = gemm_base(lw_ptr(&L->gu), w.t, w.k, C::WRG, C::H);
-      npw = C::WRG / 8;
-      break;
-    default:
-      tile_slice<C::TD, C::SKD>(w.t, tile, slice);
-      base = gemm_base(lw_ptr(&L->dn), tile, slice * C::CD + w.k, C::WRD, C::I);
-      npw = C::WRD / 8;
-      break;
-  }
-  for (int j = 0; j < npw; ++j) {
-    const int piece = 2 * j + wave;
-    dma16<2>(base + piece * 512, slot + piece * 1024);  // nt: each weight byte is read once per step
+  } else {
+    constexpr int WR = P == P_QKV ? C::WRQ : P == P_O ? C::WRO : P == P_GU ? C::WRG : C::WRD;
+    constexpr int KF = P == P_QKV ? C::H : P == P_O ? C::HQ * D : P == P_GU ? C::H : C::I;  // full K
+    constexpr int CPS = P == P_QKV ? C::CQ : P == P_O ? C::CO : P == P_GU ? C::CG : C::CD;  // chunks per slice
+    int tile, slice;
+    if constexpr (P == P_QKV) tile_slice<C::TQ, C::SKQ>(t, tile, slice);
+    else if constexpr (P == P_O) tile_slice<C::TO, C::SKO>(t, tile, slice);
+    else if constexpr (P == P_GU) { tile = t; slice = 0; }
+    else tile_slice<C::TD, C::SKD>(t, tile, slice);
+    const bf16_t* W = P == P_QKV ? cld(&L->qkv) : P == P_O ? cld(&L->o) : P == P_GU ? cld(&L->gu) : cld(&L->dn);
+    const bf16_t* base = W + ((int64_t)tile * (KF / KC) + slice * CPS + k) * (int64_t)WR * KC + lane * 8;
+#pragma unroll 1
+    for (int j = wave; j < WR / 4; j += nw) {
+      dma16<2>(base + j * 512, slot + j * 1024);
+      ++issued;
+    }
   }
 }
 
-// late stream (wave 2): this chunk's activation rows (sc1: produced in this launch) and the task's prologue
-// operands
-template <class C>
-__device__ __forceinline__ void issue_x(const Walk& w, const Rt& r, const DpArgs& a, char* ring, char* scr, int lane) {
-  lane = opaque(lane);  // per-lane addressing stays inside the branch that issues (no hoisting out of the loops)
-  char* slot = ring + (w.pos % RING);
-  const int p = wp(w), l = wl(r, w);
-  if (p == P_ATT) {
-    if (w.k != 0) return;
-    lane = opaque(lane);
+// Activation pieces of chunk k (only once the task's dependency is met). GEMM: the 32 activation rows of the
+// chunk's K range (rows >= M repeat row M - 1), every wave; gate/up's chunk 0 also stages the o-projection's
+// per-tile row statistics in the scratch (wave 3). Attention chunk 0: the prologue operands in the scratch
+// (wave 3): the qkv slab rows of the pair, the input-norm statistics and the cos / sin row.
+template <class C, int P>
+__device__ __forceinline__ void issue_x(const DpArgs& a, const Rt& r, int l, int t, int k, char* slot, char* scr,
+                                        int wave, int lane, int& issued) {
+  lane = opaque(lane);
+  if constexpr (P == P_ATT) {
+    if (k != 0 || wave != 3) return;
     constexpr int G = C::G, FR = C::SKQ * (G + 2);
-    const int seq = w.t / C::HKV, kvh = w.t - seq * C::HKV;
+    const int seq = t / C::HKV, kvh = t - seq * C::HKV;
     const float* srow = WS<C>::slab_q(a) + (int64_t)seq * C::NQ;
     const int64_t sstride = (int64_t)XR * C::NQ;
 #pragma unroll
@@ -418,46 +346,43 @@ __device__ __forceinline__ void issue_x(const Walk& w, const Rt& r, const DpArgs
     const int tiles = first ? a.ssp0_tiles : C::TD;
 #pragma unroll
     for (int i = 0; i < 2; ++i) dma4(ssp + min(lane + 64 * i, tiles - 1) * DECODE_SSP_LD + seq, scr + S_ASSP + i * 256);
-    const int ctx = sld_i32(a.ctx + seq);
+    const int ctx = cld(a.ctx + seq);
     dma16<0>(a.cos_sin + (int64_t)(ctx - 1) * D + (lane & 31) * 4, scr + S_ACOS);
-    return;
-  }
-  const bf16_t* X;
-  int64_t ldx;
-  int k0, wr, tile, slice;
-  switch (p) {
-    case P_QKV:
-      tile_slice<C::TQ, C::SKQ>(w.t, tile, slice);
-      X = WS<C>::h_in(a, l); ldx = C::H; k0 = slice * (C::H / C::SKQ); wr = C::WRQ;
-      break;
-    case P_O:
-      tile_slice<C::TO, C::SKO>(w.t, tile, slice);
-      X = WS<C>::attn(a, l); ldx = C::HQ * D; k0 = slice * (C::HQ * D / C::SKO); wr = C::WRO;
-      break;
-    case P_GU:
-      X = WS<C>::h_mid(a, l); ldx = C::H; k0 = 0; wr = C::WRG;
-      break;
-    default:
-      tile_slice<C::TD, C::SKD>(w.t, tile, slice);
-      X = WS<C>::act(a, l); ldx = C::I; k0 = slice * (C::I / C::SKD); wr = C::WRD;
-      break;
-  }
-  char* ximg = slot + wr * ROWB;
-  k0 += w.k * KC;
+    issued += (FR + 1) / 2 + 3;
+  } else {
+    constexpr int WR = P == P_QKV ? C::WRQ : P == P_O ? C::WRO : P == P_GU ? C::WRG : C::WRD;
+    const bf16_t* X;
+    int64_t ldx;
+    int k0 = 0, tile, slice;
+    if constexpr (P == P_QKV) {
+      tile_slice<C::TQ, C::SKQ>(t, tile, slice);
+      X = WS<C>::h_in(a, l); ldx = C::H; k0 = slice * (C::H / C::SKQ);
+    } else if constexpr (P == P_O) {
+      tile_slice<C::TO, C::SKO>(t, tile, slice);
+      X = WS<C>::attn(a, l); ldx = C::HQ * D; k0 = slice * (C::HQ * D / C::SKO);
+    } else if constexpr (P == P_GU) {
+      X = WS<C>::h_mid(a, l); ldx = C::H;
+    } else {
+      tile_slice<C::TD, C::SKD>(t, tile, slice);
+      X = WS<C>::act(a, l); ldx = C::I; k0 = slice * (C::I / C::SKD);
+    }
+    char* ximg = slot + WR * ROWB;
+    k0 += k * KC;
 #pragma unroll
-  for (int i = 0; i < XR * ROWB / 1024; ++i) {
-    const int rr = 4 * i + (lane >> 4);
-    const int lch = (lane & 15) ^ (rr & 15);
-    if (DP_DBG(r) & 1)  // diagnostics A/B: coherent (sc1) activation loads
-      dma16<16>(X + (int64_t)min(rr, r.M - 1) * ldx + k0 + lch * 8, ximg + i * 1024);
-    else  // write-once per launch: cached loads (see WS)
-      dma16<0>(X + (int64_t)min(rr, r.M - 1) * ldx + k0 + lch * 8, ximg + i * 1024);
-  }
-  if (p == P_GU && w.k == 0 && w.t == r.b) {  // the o-projection's per-tile row statistics [tile][0..31]
+    for (int i = 0; i < 2; ++i) {  // 8 pieces, two per wave; write-once per launch: cached loads (see WS)
+      const int j = wave + 4 * i;
+      const int rr = 4 * j + (lane >> 4);
+      const int lch = (lane & 15) ^ (rr & 15);
+      dma16<0>(X + (int64_t)min(rr, r.M - 1) * ldx + k0 + lch * 8, ximg + j * 1024);
+    }
+    issued += 2;
+    if (P == P_GU && k == 0 && wave == 3) {  // the o-projection's per-tile row statistics [tile][0..31]
 #pragma unroll
-    for (int j = 0; j < (C::TO + 7) / 8; ++j) {
-      const int t = min(8 * j + (lane >> 3), C::TO - 1);
-      dma16<16>(WS<C>::ssp_o(a) + t * DECODE_SSP_LD + (lane & 7) * 4, scr + S_STAT + j * 1024);
+      for (int j = 0; j < (C::TO + 7) / 8; ++j) {
+        const int tt = min(8 * j + (lane >> 3), C::TO - 1);
+        dma16<16>(WS<C>::ssp_o(a) + tt * DECODE_SSP_LD + (lane & 7) * 4, scr + S_STAT + j * 1024);
+      }
+      issued += (C::TO + 7) / 8;
     }
   }
 }
@@ -488,14 +413,6 @@ __device__ __forceinline__ const int* dep_src(const DpArgs& a, const Rt& r, int 
 // one shard per lane (a relaxed agent-scope load; the caller may consume it a chunk later)
 __device__ __forceinline__ int dep_load(const int* c, int lane) {
   return lane < NSH ? __hip_atomic_load(c + lane * LINEI, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-}
-// the counters are never reset: in launch e a phase's counter runs from e * target to (e + 1) * target
-// (mod 2^32), so "met" is (sum - e * target) >= target in wrap-around arithmetic
-__device__ __forceinline__ bool dep_sum_met(int v, int target, uint32_t ep) {
-#pragma unroll
-  for (int o = NSH / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  const uint32_t cur = (uint32_t)__builtin_amdgcn_readfirstlane(v) - ep * (uint32_t)target;
-  return cur >= (uint32_t)target;
 }
 
 // bounded wait (wave 3) until phase (l, p)'s producers have all published
@@ -867,251 +784,248 @@ __device__ __forceinline__ void att_merge_store(const char* scr, const DpArgs& a
   }
 }
 
-// The stream machinery, specialised per wave role at compile time (each role keeps only its own walkers:
-// fewer live scalars, no spills in the chunk loop). Per consumed chunk every role passes the same two
-// barriers: begin() ends with the "chunk landed" barrier, end() is the "slot free" barrier.
-//  R_W (waves 0, 1): issue the early stream (weights, K/V) while the ring has room; counted wait for this
-//       chunk's pieces.
-//  R_X (wave 2): issue the late stream (activations, prologue operands) of chunks whose phase is READY (the
-//       LDS word `ready`, written by R_C; spins on it — no barrier — when the consumed chunk's phase is not);
-//       counted wait.
-//  R_C (wave 3): makes the consumed chunk's phase READY (blocking wait on the producer counters). There is
-//       no look-ahead poll: the next phase cannot complete before this workgroup's own task of the current
-//       phase has published, and every poll reads NSH uncached lines.
-enum { R_W = 0, R_X = 1, R_C = 2 };
-
-template <class C, int ROLE_>
-struct Stream {
-  static constexpr int ROLE = ROLE_;
-  const DpArgs& a;
-  const Rt& r;
-  char* ring;
-  char* scr;
-  uint32_t ready;  // LDS address of the READY word
-  int wave, qend;
-  Walk cw;  // the consumed chunk
-  Walk sw;  // R_W / R_X: this role's stream walker
-  int issued, cum, rq;
-  int pub;                       // R_C: the READY value last written to LDS
-  uint32_t ep;                   // R_C: this launch's epoch (launches completed before it)
-#ifdef DIE_KERNEL_DIAG
-  uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // cycles per stage of the chunk loop (diagnostics)
-  uint64_t tlast = 0;
-  __device__ __forceinline__ void tick(int i) {
-    const uint64_t t = __builtin_amdgcn_s_memtime();
-    tacc[i] += t - tlast;
-    tlast = t;
-  }
-#else
-  __device__ __forceinline__ void tick(int) {}
-#endif
-
-  __device__ __forceinline__ Stream(const DpArgs& a_, const Rt& r_, char* ring_, char* scr_, uint32_t ready_,
-                                    int wave_, int qend_)
-      : a(a_), r(r_), ring(ring_), scr(scr_), ready(ready_), wave(wave_), qend(qend_), issued(0), cum(0), rq(0),
-        pub(0), ep(0) {
-    if constexpr (ROLE_ == R_C) {
-      // every workgroup adds 1 to a done shard when it exits: during launch e the total is in
-      // [e * grid, (e + 1) * grid), so floor(total / grid) is this launch's epoch whatever the timing
-      const int ln = threadIdx.x & 63;
-      unsigned long long d = ln < NSH ? __hip_atomic_load(WS<C>::done(a) + ln * 16, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-#pragma unroll
-      for (int o = NSH / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
-      ep = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(d / (unsigned long long)r.P));
-      // a phase's counter must advance by the same amount every launch: the attention phase has M * HKV
-      // tasks, so workgroup 0 adds the (XR - M) * HKV missing ones up front
-      if (r.b == 0 && r.M < XR && (threadIdx.x & 63) == 0)
-        for (int l = 0; l < r.l1; ++l)
-          __hip_atomic_fetch_add(counter<C>(a, r, l, P_ATT), (XR - r.M) * C::HKV, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-    }
-    walk_begin<C>(cw, r, a, qend);
-    sw = cw;
-#ifdef DIE_KERNEL_DIAG
-    tlast = __builtin_amdgcn_s_memtime();
-#endif
-  }
-
-  __device__ __forceinline__ bool room(const Walk& w) const {  // w's chunk fits in the ring behind cw
-    return w.q < qend && w.pos + chunk_bytes<C>(wp(w)) <= cw.pos + RING && w.idx - cw.idx < 16;
-  }
-
-  __device__ __forceinline__ char* begin(int lane) {
-    tick(0);  // (compute of the previous chunk / task epilogue)
-    if constexpr (ROLE == R_W) {
-      while (room(sw)) {
-        if (!(DP_DBG(r) & 4)) {
-          issue_w<C>(sw, r, a, ring, wave, lane);
-          issued += w_pieces<C>(wp(sw), wave);
-        }
-        walk_next<C>(sw, r, a, qend);
-      }
-      tick(1);
-      int mine = w_pieces<C>(wp(cw), wave);
-      if (DP_DBG(r) & 4) mine = 0;
-      wait_vm_dyn(issued - (cum + mine));
-      cum += mine;
-    } else if constexpr (ROLE == R_X) {
-#pragma unroll 1
-      for (;;) {
-        int v;
-        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ready) : "memory");
-        rq = __builtin_amdgcn_readfirstlane(v);
-        while (room(sw) && sw.q <= rq && !(wp(sw) == P_ATT && sw.k == 0 && sw.idx > cw.idx)) {
-          if (!(DP_DBG(r) & 2)) {
-            issue_x<C>(sw, r, a, ring, scr, lane);
-            issued += x_pieces<C>(r, wp(sw), sw.t, sw.k, 2);
-          }
-          walk_next<C>(sw, r, a, qend);
-        }
-        if (sw.idx > cw.idx) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      tick(2);
-      int mine = x_pieces<C>(r, wp(cw), cw.t, cw.k, 2);
-      if (DP_DBG(r) & 2) mine = 0;
-      wait_vm_dyn(issued - (cum + mine));
-      cum += mine;
-    } else {
-      if (cw.q > rq) {  // the consumed chunk's activations cannot be loaded yet: wait for its phase
-        wait_dep<C>(a, r, wl(r, cw), wp(cw), ep, lane);
-        rq = cw.q;
-      }
-      if (rq != pub) {
-        asm volatile("ds_write_b32 %0, %1" ::"v"(ready), "v"(rq) : "memory");
-        pub = rq;
-      }
-      tick(2);
-    }
-    tick(3);
-    barrier();
-    tick(4);
-    return ring + (cw.pos % RING);
-  }
-
-  __device__ __forceinline__ void end(int lane) {
-    tick(5);  // compute
-    tick(6);
-    lds_fence_barrier();
-    walk_next<C>(cw, r, a, qend);
-    tick(7);
-  }
-};
-
-
+// ------------------------------------------------------------------------------------------------------
 // timeline stamps (diagnostic builds only, DIE_KERNEL_DIAG): per workgroup and phase index, the 100 MHz clock
 // at task entry, data ready, compute done and epilogue done
 #ifdef DIE_KERNEL_DIAG
-#define DP_STAMP(S, q, i)                                                                      \
-  do {                                                                                         \
-    if ((S).a.prof && (S).ROLE == R_C && lane == 0)                                              \
-      (S).a.prof[((int64_t)blockIdx.x * (S).qend + (q)) * 4 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+#define DP_STAMP(E, q, i)                                                                     \
+  do {                                                                                        \
+    if ((E).a.prof && (E).wave == 3 && (E).lane0 == 0)                                        \
+      (E).a.prof[((int64_t)blockIdx.x * (E).r.l1 * NPH + (q)) * 4 + (i)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
-#define DP_STAMP(S, q, i) \
+#define DP_STAMP(E, q, i) \
   do {                    \
   } while (0)
 #endif
 
-template <class C, int WR, int PH, class S_>
-__device__ __forceinline__ void gemm_task(S_& S, char* ctl, int lane0) {
-  f4 acc[2][2];
-  zero_acc(acc);
-  const int t = S.cw.t, l = wl(S.r, S.cw), nch = S.cw.nch, q0 = S.cw.q;
-  const int wave = S.wave;
-  (void)q0;
-#pragma unroll 1
-  for (int k = 0; k < nch; ++k) {
-    const int lane = opaque(lane0);
-    if (k == 0) DP_STAMP(S, q0, 0);
-    char* slot = S.begin(lane);
-    if (k == 0) DP_STAMP(S, q0, 1);
-    gemm_chunk<WR>(slot, acc, wave, lane);
-    if (k == nch - 1) {
-      DP_STAMP(S, q0, 2);
-      float* red = reinterpret_cast<float*>(S.scr + S_RED);
-      stash_tiles<WR>(red, acc, wave, lane);
-      if constexpr (S_::ROLE == R_C) {
-        bool pub = true;
-        if constexpr (PH == P_QKV) epi_qkv<C>(red, S.r, S.a, t, lane);
-        else if constexpr (PH == P_O)
-          pub = epi_resid<WR, C::TO, C::SKO, C::H>(red, S.r, WS<C>::slab_od(S.a), WS<C>::h_in(S.a, l),
-                                                   WS<C>::h_mid(S.a, l), t, WS<C>::tick_o(S.a),
-                                                   WS<C>::ssp_o(S.a), lane);
-        else if constexpr (PH == P_GU) epi_gu<C>(red, S.scr, ctl, S.r, S.a, l, t, lane);
-        else pub = epi_resid<WR, C::TD, C::SKD, C::H>(red, S.r, WS<C>::slab_od(S.a), WS<C>::h_mid(S.a, l),
-                                                      WS<C>::h_out(S.a, l), t, WS<C>::tick_d(S.a),
-                                                      WS<C>::ssp_d(S.a), lane);
-        if (pub) publish<C>(S.a, S.r, l, PH, lane);
-      }
-    }
-    S.end(lane);
-    if (k == nch - 1) DP_STAMP(S, q0, 3);
-  }
-}
+__device__ __forceinline__ int rdlane(int v, int i) { return __builtin_amdgcn_readlane(v, i & 63); }
+// (a compare-and-select: this toolchain has no writelane builtin, and an asm v_writelane with both operands
+// in SGPRs breaks the constant-bus limit)
+__device__ __forceinline__ int wrlane(int v, int i, int old) { return (int)(threadIdx.x & 63) == (i & 63) ? v : old; }
 
-template <class C, class S_>
-__device__ __forceinline__ void att_task(S_& S, int lane0) {
-  constexpr int G = C::G;
-  const DpArgs& a = S.a;
-  const int t = S.cw.t, l = wl(S.r, S.cw), nch = S.cw.nch, q0 = S.cw.q;
-  const int wave = S.wave;
-  (void)q0;
-  const int seq = t / C::HKV, kvh = t - seq * C::HKV;
-  const int ctx = sld_i32(a.ctx + seq);
-  State st;
-  init_state(st);
-  bf16x8_t qf[8];
-  bf16_t nk0 = 0, nk1 = 0, nv = 0;
+// The workgroup's stream engine. Every field but `marks` / `posv` is wave-uniform (SGPRs); the four waves hold
+// identical copies except for `issued` / `marks` (each wave counts its own vector-memory ops).
+template <class C>
+struct Eng {
+  const DpArgs& a;
+  const Rt& r;
+  char* smem;   // the ring at byte 0
+  char* scr;
+  char* ctl;
+  int wave, lane0;
+  uint32_t ep;  // wave 3: this launch's epoch (launches completed before it)
+  uint32_t iend;      // ring position after the last issued chunk
+  int iseq, cseq;     // sequence numbers: next chunk to issue, chunk being consumed
+  int issued;         // this wave's vector-memory ops into the ring / scratch so far
+  int marks, posv;    // lane (seq % 64): `issued` after this wave's last piece of chunk seq | its ring position
+  int cl, cp, ct, cn, ck, cx;  // current task: layer, phase, task, chunks, chunks issued (weights), with X
+  bool xr;                     // the current task's activation pieces may be issued
+  int nl, np, nt, nn, nk;      // the next task (nl >= l1: none), its chunks, chunks issued (weights only)
+
+  __device__ __forceinline__ Eng(const DpArgs& a_, const Rt& r_, char* smem_, int wave_, int lane0_)
+      : a(a_), r(r_), smem(smem_), scr(smem_ + RING), ctl(smem_ + RING + SCR), wave(wave_), lane0(lane0_), ep(0),
+        iend(0), iseq(0), cseq(0), issued(0), marks(0), posv(0), ck(0), cx(0), xr(false), nk(0) {
+    cl = 0; cp = 0; ct = r.b;
+    settle(cl, cp, ct);
+    cn = cl < r.l1 ? task_chunks<C>(a, cp, ct) : 0;
+    nl = cl; np = cp; nt = ct + r.P;
+    settle(nl, np, nt);
+    nn = nl < r.l1 ? task_chunks<C>(a, np, nt) : 0;
+  }
+
+  // first task of phase index >= (l, p) for this workgroup (phases without a task for it are skipped)
+  __device__ __forceinline__ void settle(int& l, int& p, int& t) const {
+    while (l < r.l1 && t >= ntasks<C>(r, p)) {
+      if (++p == NPH) { p = 0; ++l; }
+      t = r.b;
+    }
+  }
+
+  __device__ __forceinline__ void issue_w_any(int p, int l, int t, int k, char* slot, int nw) {
+    switch (p) {
+      case P_QKV: issue_w<C, P_QKV>(a, l, t, k, slot, nw, wave, lane0, issued); break;
+      case P_ATT: issue_w<C, P_ATT>(a, l, t, k, slot, nw, wave, lane0, issued); break;
+      case P_O: issue_w<C, P_O>(a, l, t, k, slot, nw, wave, lane0, issued); break;
+      case P_GU: issue_w<C, P_GU>(a, l, t, k, slot, nw, wave, lane0, issued); break;
+      default: issue_w<C, P_DN>(a, l, t, k, slot, nw, wave, lane0, issued); break;
+    }
+  }
+
+  // top the ring up: the current task's chunks (weights + activations once xr, else weights only), then the
+  // next task's weights; stops at the first chunk that does not fit behind the chunk being consumed
+  template <int P>
+  __device__ __forceinline__ void fill() {
 #pragma unroll 1
-  for (int k = 0; k < nch; ++k) {
-    const int lane = opaque(lane0);
-    const int tid = wave * 64 + lane, h = lane >> 5, row = lane & 31;
-    if (k == 0) DP_STAMP(S, q0, 0);
-    char* slot = S.begin(lane);
-    if (k == 0) DP_STAMP(S, q0, 1);
-    if (k == 0) {
-      att_prologue<G, C::SKQ>(S.scr, a, l == 0 ? a.ssp0_tiles : C::TD, tid, lane, nk0, nk1, nv);
-      lds_fence_barrier();
-      {  // the rotated query rows (asm reads: no compiler-inserted vmcnt wait in the loader waves)
-        const uint32_t qa = lds_of(S.scr + S_AQ) + min(row, G - 1) * (D * 2) + h * 16;
-        u4 f[8];
-        asm volatile(
-            "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:32\n\tds_read_b128 %2, %8 offset:64\n\t"
-            "ds_read_b128 %3, %8 offset:96\n\tds_read_b128 %4, %8 offset:128\n\tds_read_b128 %5, %8 offset:160\n\t"
-            "ds_read_b128 %6, %8 offset:192\n\tds_read_b128 %7, %8 offset:224\n\ts_waitcnt lgkmcnt(0)"
-            : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]), "=&v"(f[5]), "=&v"(f[6]),
-              "=&v"(f[7])
-            : "v"(qa)
-            : "memory");
+    for (;;) {
+      const bool own = ck < cn;
+      if (!own && !(nl < r.l1 && nk < nn)) return;
+      const uint32_t z = own ? chunk_bytes<C>(P) : chunk_bytes<C>(np);
+      const uint32_t off = iend % RING;
+      const uint32_t st = off + z > RING ? iend + (RING - off) : iend;
+      const uint32_t lim = (cseq < iseq ? (uint32_t)rdlane(posv, cseq) : iend) + RING;
+      if (st + z > lim || iseq - cseq >= AHEAD) return;
+      char* slot = smem + (st % RING);
+      if (own) {
+        if (xr) {
+          issue_w<C, P>(a, cl, ct, ck, slot, 4, wave, lane0, issued);
+          issue_x<C, P>(a, r, cl, ct, ck, slot, scr, wave, lane0, issued);
+          ++cx;
+        } else if (wave < 3) {
+          issue_w<C, P>(a, cl, ct, ck, slot, 3, wave, lane0, issued);
+        }
+        ++ck;
+      } else {
+        if (wave < 3) issue_w_any(np, nl, nt, nk, slot, 3);
+        ++nk;
+      }
+      posv = wrlane((int)st, iseq, posv);
+      marks = wrlane(issued, iseq, marks);
+      ++iseq;
+      iend = st + z;
+    }
+  }
+
+  // wait until this wave's pieces of chunk seq have landed (the younger ones stay in flight)
+  __device__ __forceinline__ void wait_chunk(int seq) const { wait_vm_dyn(issued - rdlane(marks, seq)); }
+  __device__ __forceinline__ char* slot_of(int seq) const { return smem + ((uint32_t)rdlane(posv, seq) % RING); }
+
+  // the next task becomes current
+  __device__ __forceinline__ void advance() {
+    cl = nl; cp = np; ct = nt; cn = nn; ck = nk; cx = 0; xr = false;
+    nl = cl; np = cp; nt = ct + r.P;
+    settle(nl, np, nt);
+    nn = nl < r.l1 ? task_chunks<C>(a, np, nt) : 0;
+    nk = 0;
+  }
+
+  // task start: the weights keep streaming while wave 3 waits for the producers (first task of a phase), then
+  // the activation pieces of the chunks already in the ring
+  template <int P>
+  __device__ __forceinline__ void start(int base) {
+    int target = 0;
+    xr = ct != r.b || dep_src<C>(a, r, cl, P, target) == nullptr;
+    if (!xr) {
+      fill<P>();
+      if (wave == 3) wait_dep<C>(a, r, cl, P, ep, lane0);
+      barrier();
+      xr = true;
+#pragma unroll 1
+      for (int k = cx; k < ck; ++k) {
+        issue_x<C, P>(a, r, cl, ct, k, slot_of(base + k), scr, wave, lane0, issued);
+        marks = wrlane(issued, base + k, marks);
+      }
+      cx = ck;
+    }
+  }
+
+  template <int P>
+  __device__ __forceinline__ void gemm_task() {
+    constexpr int WR = P == P_QKV ? C::WRQ : P == P_O ? C::WRO : P == P_GU ? C::WRG : C::WRD;
+    const int base = cseq, q0 = cl * NPH + P, l = cl, t = ct, nch = cn;
+    (void)q0;
+    DP_STAMP(*this, q0, 0);
+    start<P>(base);
+    f4 acc[2][2];
+    zero_acc(acc);
+#pragma unroll 1
+    for (int k = 0; k < nch; ++k) {
+      fill<P>();
+      wait_chunk(base + k);
+      barrier();
+      if (k == 0) DP_STAMP(*this, q0, 1);
+      gemm_chunk<WR>(slot_of(base + k), acc, wave, opaque(lane0));
+      if (k < nch - 1) {
+        lds_fence_barrier();  // the slot may be refilled
+        ++cseq;
+      }
+    }
+    DP_STAMP(*this, q0, 2);
+    float* red = reinterpret_cast<float*>(scr + S_RED);
+    stash_tiles<WR>(red, acc, wave, opaque(lane0));  // (its barrier also frees the last chunk's slot)
+    ++cseq;
+    if (wave == 3) {
+      const int lane = opaque(lane0);
+      bool pub = true;
+      if constexpr (P == P_QKV) epi_qkv<C>(red, r, a, t, lane);
+      else if constexpr (P == P_O)
+        pub = epi_resid<WR, C::TO, C::SKO, C::H>(red, r, WS<C>::slab_od(a), WS<C>::h_in(a, l), WS<C>::h_mid(a, l), t,
+                                                 WS<C>::tick_o(a), WS<C>::ssp_o(a), lane);
+      else if constexpr (P == P_GU) epi_gu<C>(red, scr, ctl, r, a, l, t, lane);
+      else pub = epi_resid<WR, C::TD, C::SKD, C::H>(red, r, WS<C>::slab_od(a), WS<C>::h_mid(a, l), WS<C>::h_out(a, l),
+                                                    t, WS<C>::tick_d(a), WS<C>::ssp_d(a), lane);
+      if (pub) publish<C>(a, r, l, P, lane);
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    DP_STAMP(*this, q0, 3);
+    advance();
+  }
+
+  __device__ __forceinline__ void att_task() {
+    constexpr int G = C::G;
+    const int base = cseq, q0 = cl * NPH + P_ATT, l = cl, t = ct, nch = cn;
+    (void)q0;
+    DP_STAMP(*this, q0, 0);
+    const int seq = t / C::HKV, kvh = t - seq * C::HKV;
+    const int ctx = cld(a.ctx + seq);
+    start<P_ATT>(base);
+    State st;
+    init_state(st);
+    bf16x8_t qf[8];
+    bf16_t nk0 = 0, nk1 = 0, nv = 0;
+#pragma unroll 1
+    for (int k = 0; k < nch; ++k) {
+      fill<P_ATT>();
+      wait_chunk(base + k);
+      barrier();
+      const int lane = opaque(lane0);
+      const int tid = wave * 64 + lane, h = lane >> 5, row = lane & 31;
+      char* slot = slot_of(base + k);
+      if (k == 0) {
+        DP_STAMP(*this, q0, 1);
+        att_prologue<G, C::SKQ>(scr, a, l == 0 ? a.ssp0_tiles : C::TD, tid, lane, nk0, nk1, nv);
+        lds_fence_barrier();
+        {  // the rotated query rows (asm reads: no compiler-inserted vmcnt wait behind the ring's stream)
+          const uint32_t qa = lds_of(scr + S_AQ) + min(row, G - 1) * (D * 2) + h * 16;
+          u4 f[8];
+          asm volatile(
+              "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:32\n\tds_read_b128 %2, %8 offset:64\n\t"
+              "ds_read_b128 %3, %8 offset:96\n\tds_read_b128 %4, %8 offset:128\n\tds_read_b128 %5, %8 offset:160\n\t"
+              "ds_read_b128 %6, %8 offset:192\n\tds_read_b128 %7, %8 offset:224\n\ts_waitcnt lgkmcnt(0)"
+              : "=&v"(f[0]), "=&v"(f[1]), "=&v"(f[2]), "=&v"(f[3]), "=&v"(f[4]), "=&v"(f[5]), "=&v"(f[6]),
+                "=&v"(f[7])
+              : "v"(qa)
+              : "memory");
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk)
-          qf[kk] = row < G ? __builtin_bit_cast(bf16x8_t, f[kk]) : zero_frag();
+          for (int kk = 0; kk < 8; ++kk) qf[kk] = row < G ? __builtin_bit_cast(bf16x8_t, f[kk]) : zero_frag();
+        }
       }
-    }
-    if (k == nch - 1) {  // patch key ctx - 1 (this step's token) into the chunk's K / V images
-      const int rr = (ctx - 1) - k * DEC_KEYS;
-      const uint32_t kimg = lds_of(slot) + rr * DEC_ROW, vimg = kimg + DEC_KEYS * DEC_ROW;
-      if (tid < 64) {
-        lds_st16(kimg + 16 * ((tid >> 3) ^ (rr & 15)) + 2 * (tid & 7), nk0);
-        lds_st16(kimg + 16 * (((tid + 64) >> 3) ^ (rr & 15)) + 2 * (tid & 7), nk1);
-      } else if (tid < 192) {
-        const int d = tid - 64;
-        lds_st16(vimg + 16 * ((d >> 3) ^ ((rr & 3) << 2)) + 2 * (d & 7), nv);
+      if (k == nch - 1) {  // patch key ctx - 1 (this step's token) into the chunk's K / V images
+        const int rr = (ctx - 1) - k * DEC_KEYS;
+        const uint32_t kimg = lds_of(slot) + rr * DEC_ROW, vimg = kimg + DEC_KEYS * DEC_ROW;
+        if (tid < 64) {
+          lds_st16(kimg + 16 * ((tid >> 3) ^ (rr & 15)) + 2 * (tid & 7), nk0);
+          lds_st16(kimg + 16 * (((tid + 64) >> 3) ^ (rr & 15)) + 2 * (tid & 7), nk1);
+        } else if (tid < 192) {
+          const int d = tid - 64;
+          lds_st16(vimg + 16 * ((d >> 3) ^ ((rr & 3) << 2)) + 2 * (d & 7), nv);
+        }
+        lds_fence_barrier();
       }
-      lds_fence_barrier();
+      {
+        const int kb = k * DEC_KEYS + 32 * wave;  // keys >= ctx: clamped rows, masked to -inf
+        f32x16_t sc = qk_lds_swz(slot + 32 * wave * DEC_ROW, qf, lane);
+        softmax_tile_lazy(sc, st, kb, ctx, a.scale_log2, h);
+        pv_lds_swz_v3(slot + DEC_KEYS * DEC_ROW + 32 * wave * DEC_ROW, sc, st, lane);
+      }
+      lds_fence_barrier();  // the slot may be refilled (last chunk: the staging area becomes the merge area)
+      ++cseq;
     }
+    DP_STAMP(*this, q0, 2);
     {
-      const int kb = k * DEC_KEYS + 32 * wave;  // keys >= ctx: clamped rows, masked to -inf
-      f32x16_t sc = qk_lds_swz(slot + 32 * wave * DEC_ROW, qf, lane);
-      softmax_tile_lazy(sc, st, kb, ctx, a.scale_log2, h);
-      pv_lds_swz_v3(slot + DEC_KEYS * DEC_ROW + 32 * wave * DEC_ROW, sc, st, lane);
-    }
-    if (k == nch - 1) {
-      DP_STAMP(S, q0, 2);
-      lds_fence_barrier();  // every wave is done with the staging area: the merge reuses it
-      const uint32_t ml = lds_of(S.scr + S_ML), ob = lds_of(S.scr + S_OB);
+      const int lane = opaque(lane0);
+      const int h = lane >> 5, row = lane & 31;
+      const uint32_t ml = lds_of(scr + S_ML), ob = lds_of(scr + S_OB);
       if (row < G) {
         if (h == 0) {  // (uniform base + offset: no divergent generic->LDS pointer casts)
           lds_st32(ml + 8 * (wave * 32 + row), st.m);
@@ -1126,59 +1040,55 @@ __device__ __forceinline__ void att_task(S_& S, int lane0) {
                       f32x4_t{st.o[db][4 * g4], st.o[db][4 * g4 + 1], st.o[db][4 * g4 + 2], st.o[db][4 * g4 + 3]});
       }
       lds_fence_barrier();
-      if constexpr (S_::ROLE == R_C) {
-        att_merge_store<C>(S.scr, a, l, seq, kvh, lane);
-        publish<C>(a, S.r, l, P_ATT, lane);
+      if (wave == 3) {
+        att_merge_store<C>(scr, a, l, seq, kvh, lane);
+        publish<C>(a, r, l, P_ATT, lane);
       }
     }
-    S.end(lane);
-    if (k == nch - 1) DP_STAMP(S, q0, 3);
+    DP_STAMP(*this, q0, 3);
+    advance();
   }
-}
-
-template <class C, int ROLE>
-__device__ __forceinline__ void run_role(const DpArgs& a, const Rt& r, char* smem, uint32_t ready, int wave,
-                                         int lane0) {
-  char* ctl = smem + RING + SCR;
-  using St = Stream<C, ROLE>;
-  St S(a, r, smem, smem + RING, ready, wave, r.l1 * NPH);
-#pragma unroll 1
-  while (S.cw.q < S.qend) {
-    switch (wp(S.cw)) {
-      case P_QKV: gemm_task<C, C::WRQ, P_QKV, St>(S, ctl, lane0); break;
-      case P_ATT: att_task<C, St>(S, lane0); break;
-      case P_O: gemm_task<C, C::WRO, P_O, St>(S, ctl, lane0); break;
-      case P_GU: gemm_task<C, C::WRG, P_GU, St>(S, ctl, lane0); break;
-      default: gemm_task<C, C::WRD, P_DN, St>(S, ctl, lane0); break;
-    }
-  }
-#ifdef DIE_KERNEL_DIAG
-  if (a.prof && lane0 == 0) {  // per-wave stage cycles after the timeline stamps
-    uint64_t* tp = a.prof + (int64_t)gridDim.x * S.qend * 4 + (blockIdx.x * 4 + wave) * 8;
-    for (int i = 0; i < 8; ++i) tp[i] = S.tacc[i];
-  }
-#endif
-}
+};
 
 template <class C>
 __global__ void __launch_bounds__(NTH, 1) decode_persistent_kernel(DpArgs a) {
-  char* smem = dp_smem;
-  const int lane0 = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   Rt r;
   r.P = gridDim.x;
   r.b = blockIdx.x;
   r.M = a.M;
   r.l1 = a.l1;
   r.dbg = a.dbg;
-  const uint32_t ready = lds_of(smem + RING + SCR + C_READY);
-  if (threadIdx.x == 0)  // phase 0 (the first layer's qkv) reads h as it was before the launch
-    asm volatile("ds_write_b32 %0, %1" ::"v"(ready), "v"(0) : "memory");
-  lds_fence_barrier();
-  if (wave < 2) run_role<C, R_W>(a, r, smem, ready, wave, lane0);
-  else if (wave == 2) run_role<C, R_X>(a, r, smem, ready, wave, lane0);
-  else run_role<C, R_C>(a, r, smem, ready, wave, lane0);
+  const int lane0 = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  Eng<C> e(a, r, dp_smem, wave, lane0);
+  if (wave == 3) {
+    // every workgroup adds 1 to a done shard when it exits: during launch e the total is in
+    // [e * grid, (e + 1) * grid), so floor(total / grid) is this launch's epoch whatever the timing
+    unsigned long long d = lane0 < NSH ? __hip_atomic_load(WS<C>::done(a) + lane0 * 16, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+#pragma unroll
+    for (int o = NSH / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+    e.ep = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(d / (unsigned long long)r.P));
+    // a phase's counter must advance by the same amount every launch: the attention phase has M * HKV
+    // tasks, so workgroup 0 adds the (XR - M) * HKV missing ones up front
+    if (r.b == 0 && r.M < XR && lane0 == 0)
+      for (int l = 0; l < r.l1; ++l)
+        __hip_atomic_fetch_add(counter<C>(a, r, l, P_ATT), (XR - r.M) * C::HKV, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+#pragma unroll 1
+  while (e.cl < r.l1) {
+    switch (e.cp) {
+      case P_QKV: e.template gemm_task<P_QKV>(); break;
+      case P_ATT: e.att_task(); break;
+      case P_O: e.template gemm_task<P_O>(); break;
+      case P_GU: e.template gemm_task<P_GU>(); break;
+      default: e.template gemm_task<P_DN>(); break;
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   if (threadIdx.x == 0)  // this workgroup's exit (the next launch derives its epoch from the total)
     __hip_atomic_fetch_add(WS<C>::done(a) + (blockIdx.x & (NSH - 1)) * 16, 1ull, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -1232,3 +1142,4 @@ hipError_t launch_decode_persistent(const DpArgs& a, hipStream_t s) {
 }
 
 }  // namespace die
+

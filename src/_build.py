@@ -5,7 +5,7 @@ kernels and the torch bindings into ``src/_C*.so`` and the host runtime
 
     python -m src._build            # incremental
     python -m src._build --force
-    DIE_KERNEL_DIAG=1 python -m src._build --force   # diagnostics build (kernel bisection bits)
+    DIE_KERNEL_DIAG=1 python -m src._build   # diagnostics build -> src/_Cdiag*.so (DIE_C_DIAG=1 loads it)
 
 The kernels are compiled once here with ``hipcc --offload-arch=gfx950`` and the
 ``.so`` files travel with the repo snapshot to the GPU box.
@@ -59,17 +59,14 @@ def _headers(d: str):
 
 def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
     os.makedirs(OBJ, exist_ok=True)
-    out = os.path.join(ROOT, "src", "_C" + EXT_SUFFIX)
+    is_diag = os.environ.get("DIE_KERNEL_DIAG") == "1"
+    # the diagnostics build is a separate file (loaded instead of _C with DIE_C_DIAG=1): both travel
+    out = os.path.join(ROOT, "src", ("_Cdiag" if is_diag else "_C") + EXT_SUFFIX)
     kdir = os.path.join(CSRC, "kernels")
     hdrs = _headers(kdir)
     incs, torch_lib, abi = _torch_paths()
     jobs_list = []
     objs = []
-    is_diag = os.environ.get("DIE_KERNEL_DIAG") == "1"
-    # diagnostics builds keep their own objects; the link re-runs whenever the flavour changes
-    flavour = os.path.join(OBJ, ".flavour")
-    prev = open(flavour).read() if os.path.exists(flavour) else ""
-    relink = prev != ("diag" if is_diag else "release")
     for k in KERNELS:
         src = os.path.join(kdir, k + ".hip")
         obj = os.path.join(OBJ, k + (".diag.o" if is_diag else ".o"))
@@ -96,12 +93,10 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
         for res in ex.map(_run, jobs_list):
             if verbose and res:
                 print(res)
-    if force or relink or _newer(out, objs):
+    if force or _newer(out, objs):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out,
               "-L", torch_lib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
               f"-Wl,-rpath,{torch_lib}"])
-        with open(flavour, "w") as f:
-            f.write("diag" if is_diag else "release")
     return out
 
 

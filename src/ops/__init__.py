@@ -18,7 +18,17 @@ from . import reference as ref
 _C = None
 _C_ERR: Optional[BaseException] = None
 try:
-    from src import _C  # type: ignore  # noqa: F811
+    if os.environ.get("DIE_C_DIAG") == "1":  # the diagnostics build (DIE_KERNEL_DIAG=1 python -m src._build)
+        import importlib.util
+        import sysconfig
+
+        _p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                          "_Cdiag" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+        _spec = importlib.util.spec_from_file_location("src._C", _p)
+        _C = importlib.util.module_from_spec(_spec)
+        _spec.loader.exec_module(_C)
+    else:
+        from src import _C  # type: ignore  # noqa: F811
 except Exception as e:  # pragma: no cover - depends on build state
     _C_ERR = e
 
