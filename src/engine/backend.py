@@ -205,9 +205,26 @@ class LLMBackend:
         from src.engine.disagg import sampling_to_dict
         from src.parallel.kv_transfer import KVPacket
 
-        pseq = await self.async_engine.submit(rid, gi.prompt_token_ids, gi.sampling,
-                                              user_data={"export_kv": True})
+        # reserve the decode worker's landing-zone slot first: the prefill engine's export then gathers the
+        # prompt's blocks straight into it (one pass over xGMI, no staging tensor, no second copy)
+        slot = None
+        if self.engine.device.type == "cuda" and os.environ.get("DIE_KV_DIRECT", "1") == "1":
+            from src.parallel.kv_transfer import packet_shape
+
+            nb = self.engine.blocks.blocks_needed(len(gi.prompt_token_ids))
+            slot = await self._decode_link.reserve(self.engine.device, packet_shape(self.engine.pool.planes(), nb))
+        ud = {"export_kv": True}
+        if slot is not None:
+            ud["export_dst"] = slot["dst"]
+        try:
+            pseq = await self.async_engine.submit(rid, gi.prompt_token_ids, gi.sampling, user_data=ud)
+        except BaseException:
+            if slot is not None:  # the prompt never ran to the export (or its gather may still be queued)
+                await self._decode_link.abandon(slot, None)
+            raise
         if pseq.finish_reason == "stop":
+            if slot is not None:
+                await self._decode_link.abandon(slot, getattr(pseq, "kv_export_ready", None))
             return build_llm_output(pseq.output_ids, self.tokenizer, prompt_len=pseq.prompt_len,
                                     finish_reason="stop", ttft_ms=pseq.ttft_ms(), latency_ms=pseq.latency_ms(),
                                     return_text=gi.return_text)
@@ -215,7 +232,10 @@ class LLMBackend:
                           sampling_to_dict(gi.sampling), ttft_ms=pseq.ttft_ms(),
                           ready=getattr(pseq, "kv_export_ready", None))
         pseq.kv_export = None
-        rep = await self._decode_link.send(packet)
+        if slot is not None:
+            rep = await self._decode_link.send_reserved(packet, slot)
+        else:
+            rep = await self._decode_link.send(packet)
         if not rep.get("success"):
             raise RuntimeError(f"decode worker failed: {rep.get('error')}")
         out = rep["outputs"]
@@ -228,7 +248,7 @@ class LLMBackend:
             from src.parallel.kv_transfer import IPCLandingZone
 
             cap = int((self.config.overrides or {}).get("kv_landing_zone_bytes",
-                                                         os.environ.get("DIE_KV_ZONE_BYTES", 1 << 30)))
+                                                         os.environ.get("DIE_KV_ZONE_BYTES", 4 << 30)))
             self._zone = IPCLandingZone(self.engine.device, cap,
                                         uncached=os.environ.get("DIE_KV_ZONE_UNCACHED", "0") == "1")
         return self._zone
@@ -289,12 +309,12 @@ class LLMBackend:
             if self.engine.device.type != "cuda":
                 return {"success": False, "error": "no GPU landing zone on a CPU engine"}
             z = self._landing_zone()
-            return {"success": True, "handle": z.handle, "capacity": z.capacity, "device": str(z.device),
-                    "pid": os.getpid()}
+            return {"success": True, "handle": z.handle, "handles": z.handles, "seg_bytes": z.seg_bytes,
+                    "capacity": z.capacity, "device": str(z.device), "pid": os.getpid()}
         if op == "kv_reserve":  # optionally wait up to wait_s for slots to come back (no host sync: polling)
             zone, n = self._landing_zone(), int(msg["nbytes"])
-            if n > zone.capacity:
-                return {"success": False, "offset": None, "error": "packet larger than the landing zone"}
+            if n > zone.seg_bytes:
+                return {"success": False, "offset": None, "error": "packet larger than a landing-zone segment"}
             deadline = time.monotonic() + float(msg.get("wait_s") or 0.0)
             off = zone.reserve(n)
             while off is None and time.monotonic() < deadline:

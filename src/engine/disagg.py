@@ -95,6 +95,7 @@ class RemoteDecodeLink:
         self._ipc = None
         self._ipc_lock = asyncio.Lock()
         self.ipc_packets = 0
+        self.direct_packets = 0   # gathered by the prefill engine straight into a reserved slot
         self.wire_packets = 0
 
     async def _channel(self, device):
@@ -112,7 +113,8 @@ class RemoteDecodeLink:
                 elif rep.get("success"):
                     from src.parallel.kv_transfer import IPCSender
 
-                    self._ipc = IPCSender(rep["handle"], rep["capacity"], device)
+                    self._ipc = IPCSender(rep.get("handles") or rep["handle"], rep.get("seg_bytes", rep["capacity"]),
+                                          device)
                     logger.info("KV IPC channel to %s mapped (%d MiB landing zone)", self.address,
                                 rep["capacity"] >> 20)
                 else:
@@ -121,6 +123,54 @@ class RemoteDecodeLink:
                 logger.info("KV IPC channel to %s unavailable (%s); using the RPC payload path", self.address, e)
                 self.use_ipc = False
         return self._ipc
+
+    async def reserve(self, device, shape: List[int]) -> Optional[Dict[str, Any]]:
+        """Reserve a landing-zone slot for a packet of ``shape`` BEFORE its prompt runs: returns
+        ``{"offset", "gen", "dst"}`` (``dst`` a bf16 view of the slot for the prefill engine's gather to
+        write into), or None (no IPC channel / zone full: the packet then takes the staged path)."""
+        ch = await self._channel(device)
+        if ch is None:
+            return None
+        nbytes = 2
+        for d in shape:
+            nbytes *= int(d)
+        rep = await self.rpc.call(self.address, {"op": "kv_reserve", "model": self.model, "nbytes": nbytes,
+                                                 "wait_s": self.reserve_wait_s}, self.timeout)
+        if not rep.get("success"):
+            return None
+        try:
+            dst = ch.dst(rep["offset"], shape)
+        except ValueError:
+            await self._release(rep["offset"], rep.get("gen"))
+            return None
+        return {"offset": rep["offset"], "gen": rep.get("gen"), "dst": dst}
+
+    async def send_reserved(self, packet: KVPacket, slot: Dict[str, Any]) -> Dict[str, Any]:
+        """The packet's KV was gathered straight into ``slot`` (see :meth:`reserve`): wait for that gather
+        (its event, polled) and hand the slot over with ONE kv_import. If that fails before the decode
+        worker owns the slot, the slot is released — after the gather has finished writing it."""
+        off, gen = slot["offset"], slot["gen"]
+        imported = False
+        try:
+            await self._ipc.wait_ready(packet.ready)
+            wire = dict(packet_meta(packet), ipc={"offset": off, "gen": gen})
+            self.ipc_packets += 1
+            self.direct_packets += 1
+            imported = True
+            return await self.rpc.call(self.address, {"op": "kv_import", "model": self.model, "packet": wire},
+                                       self.timeout)
+        except BaseException:
+            if not imported:
+                await self.abandon(slot, packet.ready)
+            raise
+
+    async def abandon(self, slot: Dict[str, Any], ready=None) -> None:
+        """Give a reserved slot back (the prompt failed or was cancelled): once ``ready`` (the gather into
+        it, if one was issued) has completed, so no later owner of the slot is overwritten."""
+        if ready is not None and not ready.query():
+            asyncio.ensure_future(self._release_after_copy(slot["offset"], slot["gen"], ready))
+        else:
+            await self._release(slot["offset"], slot["gen"])
 
     async def send(self, packet: KVPacket) -> Dict[str, Any]:
         ch = await self._channel(packet.kv.device)

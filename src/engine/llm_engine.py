@@ -362,7 +362,11 @@ class LLMEngine:
                 from src.parallel.kv_transfer import export_blocks
 
                 nb = self.blocks.blocks_needed(seq.prompt_len)
-                seq.kv_export = export_blocks(self.pool.planes(), seq.block_table[:nb])  # type: ignore[attr-defined]
+                # export_dst: a slot of the decode worker's landing zone reserved before the prompt ran (the
+                # gather writes straight into it); else a local staging tensor
+                ud = seq.user_data if isinstance(seq.user_data, dict) else {}
+                seq.kv_export = export_blocks(self.pool.planes(), seq.block_table[:nb],  # type: ignore[attr-defined]
+                                              out=ud.get("export_dst"))
                 if seq.kv_export.is_cuda:  # consumers wait on this instead of a host sync
                     ev = torch.cuda.Event()
                     ev.record()

@@ -51,10 +51,17 @@ class KVPacket:
         return self.kv.numel() * self.kv.element_size()
 
 
-def export_blocks(pool_planes: torch.Tensor, block_ids: List[int]) -> torch.Tensor:
-    """Gather ``block_ids`` of every (layer, K/V) plane into a staging tensor."""
+def export_blocks(pool_planes: torch.Tensor, block_ids: List[int], out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Gather ``block_ids`` of every (layer, K/V) plane into a staging tensor, or into ``out`` (e.g. a
+    peer's IPC landing-zone slot: the gather then writes straight over xGMI, no second copy)."""
     ids = torch.tensor(block_ids, dtype=torch.int64, device=pool_planes.device)
-    return ops.gather_blocks(pool_planes, ids)
+    return ops.gather_blocks(pool_planes, ids, buf=out)
+
+
+def packet_shape(pool_planes: torch.Tensor, n_blocks: int) -> List[int]:
+    """[n_blocks, planes, slab] of a packet gathered from ``pool_planes`` ([planes, num_blocks, ...])."""
+    planes, nb = pool_planes.shape[0], pool_planes.shape[1]
+    return [int(n_blocks), int(planes), int(pool_planes.numel() // (planes * nb))]
 
 
 def import_blocks(pool_planes: torch.Tensor, block_ids: List[int], buf: torch.Tensor) -> None:
@@ -99,43 +106,59 @@ def ship(buf: torch.Tensor, device, ready=None):
 
 
 class IPCLandingZone:
-    """Decode-worker side of cross-process KV shipping on one node: ONE IPC-shareable device buffer
-    (plain hipMalloc, so this GPU reads it through its caches) that prefill workers map
-    (hipIpcOpenMemHandle) and fill with device-to-device copies over xGMI — the packed prompt KV never
-    touches host memory or the RPC socket, which then carries only the metadata.
+    """Decode-worker side of cross-process KV shipping on one node: IPC-shareable device segments (plain
+    hipMalloc, so this GPU reads them through its caches) that prefill workers map (hipIpcOpenMemHandle)
+    and fill over xGMI — the packed prompt KV never touches host memory or the RPC socket, which then
+    carries only the metadata. A prefill worker that reserved its slot before the prompt ran gathers the
+    prompt's blocks from its paged pool STRAIGHT into the slot (one pass, no staging copy); the decode
+    engine then scatters from the slot into its own pool.
 
     Lifecycle of a slot (no host synchronisation anywhere):
-    ``reserve`` (kv_reserve RPC, first fit) → the sender copies and tells us (kv_import) → ``claim``
+    ``reserve`` (kv_reserve RPC, first fit) → the sender fills it and tells us (kv_import) → ``claim``
     hands the engine a VIEW of the slot (no clone) → the engine thread scatters it straight into its
     paged pool with ``move_blocks`` and calls ``release_after`` with an event recorded behind the
     scatter → the slot returns to the free list once that event has completed (checked without
     blocking whenever space is reserved). A reservation that is never imported (sender failed, client
     gone) is returned by ``release`` (kv_release RPC) or expires after ``reserve_ttl_s``.
 
-    The zone stays below 2 GiB: on this ROCm (7.2, dmabuf IPC) hipIpcOpenMemHandle of a 2 GiB
-    allocation never returns in the importing process, while 256 MiB..1 GiB open in < 10 ms
-    (measured, scripts/repro_ipc_kv.py). 1 GiB holds 16 in-flight 512-token Llama-3-8B prompts."""
+    Offsets are global over the segments (segment s covers [s * seg_bytes, (s + 1) * seg_bytes)); a slot
+    never spans two. Each segment stays below 2 GiB: on this ROCm (7.2, dmabuf IPC) hipIpcOpenMemHandle of
+    a 2 GiB allocation never returns in the importing process, while 256 MiB..1 GiB open in < 10 ms
+    (measured, scripts/repro_ipc_kv.py). The default 4 x 1 GiB holds 64 in-flight 512-token Llama-3-8B
+    prompts: a whole bench wave of 32 (with one segment, half the wave waited for the other half's
+    scatter)."""
 
     ALIGN = 1 << 16
-    MAX_BYTES = (1 << 31) - (1 << 20)
+    MAX_BYTES = (1 << 31) - (1 << 20)   # per segment
+    SEG_BYTES = 1 << 30
 
-    def __init__(self, device, capacity: int = 1 << 30, uncached: bool = False, reserve_ttl_s: float = 120.0):
+    def __init__(self, device, capacity: int = 4 << 30, uncached: bool = False, reserve_ttl_s: float = 120.0,
+                 seg_bytes: int = SEG_BYTES):
         from src import _C
 
         self.device = torch.device(device)
-        self.capacity = int(capacity)
-        if not 0 < self.capacity <= self.MAX_BYTES:
-            raise ValueError(f"landing zone of {self.capacity} bytes: must be in (0, {self.MAX_BYTES}]")
+        self.seg_bytes = int(min(seg_bytes, capacity))
+        if not 0 < self.seg_bytes <= self.MAX_BYTES or self.seg_bytes % self.ALIGN:
+            raise ValueError(f"landing-zone segments of {self.seg_bytes} bytes: must be a multiple of "
+                             f"{self.ALIGN} in (0, {self.MAX_BYTES}]")
+        nseg = max(1, -(-int(capacity) // self.seg_bytes))
+        self.capacity = nseg * self.seg_bytes
+        self.ptrs, self.views, self.handles = [], [], []
         with torch.cuda.device(self.device):
-            self.ptr = _C.car_alloc(self.capacity, uncached)
-            self.view = _C.car_tensor(self.ptr, self.capacity, self.device.index or 0)
-        self.handle = _C.car_handle(self.ptr).hex()
+            for _ in range(nseg):
+                ptr = _C.car_alloc(self.seg_bytes, uncached)
+                self.ptrs.append(ptr)
+                self.views.append(_C.car_tensor(ptr, self.seg_bytes, self.device.index or 0))
+                self.handles.append(_C.car_handle(ptr).hex())
+        self.handle = self.handles[0]
         self._init_book(reserve_ttl_s)
 
     def _init_book(self, reserve_ttl_s: float) -> None:
         """Slot bookkeeping (host only; CPU-testable without a device buffer)."""
         self.reserve_ttl_s = reserve_ttl_s
-        self._free: List[List[int]] = [[0, self.capacity]]  # sorted [start, end) ranges
+        if not getattr(self, "seg_bytes", None):
+            self.seg_bytes = self.capacity
+        self._free: List[List[int]] = [[o, o + self.seg_bytes] for o in range(0, self.capacity, self.seg_bytes)]
         self._used: Dict[int, int] = {}
         # generation of each reservation: a late kv_import / kv_release of an expired reservation whose
         # offset was handed out again must not touch the new owner's slot
@@ -196,7 +219,7 @@ class IPCLandingZone:
             self._free.sort()
             merged: List[List[int]] = []
             for r in self._free:
-                if merged and merged[-1][1] == r[0]:
+                if merged and merged[-1][1] == r[0] and r[0] % self.seg_bytes:  # never across segments
                     merged[-1][1] = r[1]
                 else:
                     merged.append(r)
@@ -216,7 +239,8 @@ class IPCLandingZone:
                 raise ValueError(f"kv_import of a stale reservation at {offset} (generation {gen}, "
                                  f"slot now {self._gen_of.get(offset)})")
             self._reserved_at.pop(offset, None)  # imported: no longer expires
-        return self.view[offset: offset + n].view(torch.bfloat16).view(*shape)
+        seg, loc = divmod(offset, self.seg_bytes)
+        return self.views[seg][loc: loc + n].view(torch.bfloat16).view(*shape)
 
     def release_after(self, offset: int, event=None) -> None:
         """Free the slot once ``event`` (recorded behind the consumer's scatter) has completed."""
@@ -234,36 +258,59 @@ class IPCLandingZone:
     def close(self) -> None:
         from src import _C
 
-        self.view = None
-        _C.car_release(self.ptr)
+        self.views = []
+        for p in self.ptrs:
+            _C.car_release(p)
+        self.ptrs = []
 
 
 class IPCSender:
-    """Prefill-worker side: maps a decode worker's :class:`IPCLandingZone` into this GPU's address
-    space once, then each packet is one device-to-device copy into it on a dedicated transfer stream,
-    ordered after the prefill engine's gather by its event. ``write`` returns that copy's completion
-    event; ``write_async`` awaits it by polling (the asyncio thread never blocks on the GPU).
+    """Prefill-worker side: maps a decode worker's :class:`IPCLandingZone` segments into this GPU's address
+    space once. A slot reserved before the prompt ran is handed to the prefill engine as a tensor view
+    (:meth:`dst`): the engine's export gathers the prompt's blocks straight into it. Otherwise a packed
+    packet is copied in on a dedicated transfer stream (:meth:`write`), ordered after the engine's gather
+    by its event; ``write_async`` / :meth:`wait_ready` await completion by polling (the asyncio thread
+    never blocks on the GPU).
 
     ``DIE_KV_COPY=dma`` copies with hipMemcpyAsync (copy engines; compute keeps all CUs) instead of the
     default shader-store copy kernel (bench/micro_ipc_copy.py measures both)."""
 
-    def __init__(self, handle_hex: str, capacity: int, device):
+    def __init__(self, handles, seg_bytes: int, device):
         import os
 
         from src import _C
 
+        if isinstance(handles, str):
+            handles = [handles]
         self.device = torch.device(device)
+        self.seg_bytes = int(seg_bytes)
+        self.ptrs, self.views = [], []
         with torch.cuda.device(self.device):
-            self.ptr = _C.car_open(bytes.fromhex(handle_hex))
-            self.view = _C.car_tensor(self.ptr, int(capacity), self.device.index or 0)
+            for h in handles:
+                ptr = _C.car_open(bytes.fromhex(h))
+                self.ptrs.append(ptr)
+                self.views.append(_C.car_tensor(ptr, self.seg_bytes, self.device.index or 0))
             self.stream = torch.cuda.Stream(device=self.device)
         self.dma = os.environ.get("DIE_KV_COPY", "shader") == "dma"
         self.bytes_sent = 0
+
+    def _loc(self, offset: int, nbytes: int):
+        seg, loc = divmod(int(offset), self.seg_bytes)
+        if seg >= len(self.ptrs) or loc + nbytes > self.seg_bytes:
+            raise ValueError(f"slot at {offset} (+{nbytes} B) is outside the mapped landing zone")
+        return seg, loc
+
+    def dst(self, offset: int, shape: List[int]) -> torch.Tensor:
+        """A bf16 view of the reserved slot (for the prefill engine's gather to write into)."""
+        n = int(np.prod(shape)) * 2
+        seg, loc = self._loc(offset, n)
+        return self.views[seg][loc: loc + n].view(torch.bfloat16).view(*shape)
 
     def write(self, offset: int, kv: torch.Tensor, ready=None):
         from src import _C
 
         flat = kv.contiguous().view(torch.uint8).view(-1)
+        seg, loc = self._loc(offset, flat.numel())
         s = self.stream
         with torch.cuda.device(self.device), torch.cuda.stream(s):
             if ready is not None:
@@ -271,33 +318,39 @@ class IPCSender:
             else:
                 s.wait_stream(torch.cuda.current_stream(self.device))
             if self.dma:
-                self.view[int(offset): int(offset) + flat.numel()].copy_(flat, non_blocking=True)
+                self.views[seg][loc: loc + flat.numel()].copy_(flat, non_blocking=True)
             else:  # shader stores into the mapped peer buffer
-                _C.car_copy_to(self.ptr + int(offset), flat)
+                _C.car_copy_to(self.ptrs[seg] + loc, flat)
             done = torch.cuda.Event()
             done.record(s)
         flat.record_stream(s)  # the staging tensor lives until the copy has read it
         self.bytes_sent += flat.numel()
         return done
 
+    @staticmethod
+    async def wait_ready(ev, poll_s: float = 2e-4) -> None:
+        import asyncio
+
+        while ev is not None and not ev.query():
+            await asyncio.sleep(poll_s)
+
     async def write_async(self, offset: int, kv: torch.Tensor, ready=None, poll_s: float = 2e-4,
                           issued: Optional[Dict[str, Any]] = None) -> None:
         """Copy and wait for delivery without blocking the event loop. ``issued["event"]`` is set to the
         copy's completion event as soon as the copy is queued, so a caller that is cancelled while
         waiting knows the copy may still be writing into the slot."""
-        import asyncio
-
         done = self.write(offset, kv, ready)
         if issued is not None:
             issued["event"] = done
-        while not done.query():
-            await asyncio.sleep(poll_s)
+        await self.wait_ready(done, poll_s)
 
     def close(self) -> None:
         from src import _C
 
-        self.view = None
-        _C.car_close(self.ptr)
+        self.views = []
+        for p in self.ptrs:
+            _C.car_close(p)
+        self.ptrs = []
 
 
 def packet_meta(p: KVPacket) -> Dict[str, Any]:

@@ -10,10 +10,11 @@ import torch
 from src.parallel.kv_transfer import IPCLandingZone
 
 
-def zone(cap=1 << 20, ttl=120.0):
+def zone(cap=1 << 20, ttl=120.0, seg=None):
     z = object.__new__(IPCLandingZone)
     z.capacity = cap
-    z.view = torch.zeros(cap, dtype=torch.uint8)
+    z.seg_bytes = seg or cap
+    z.views = [torch.zeros(z.seg_bytes, dtype=torch.uint8) for _ in range(cap // z.seg_bytes)]
     z._init_book(ttl)
     return z
 
@@ -41,3 +42,29 @@ def test_release_without_generation_still_works():
     z = zone()
     o = z.reserve(4096)
     assert z.release(o) and not z.release(o)
+
+
+def test_segments_slots_never_span_and_free_lists_stay_per_segment():
+    """A multi-segment zone (several < 2 GiB IPC allocations): a slot lies inside one segment, claims map to
+    that segment's buffer, and freeing never merges ranges across a segment boundary."""
+    seg = 4 * IPCLandingZone.ALIGN
+    z = zone(cap=3 * seg, seg=seg)
+    a = z.reserve(3 * IPCLandingZone.ALIGN)          # segment 0, leaves one unit free there
+    b = z.reserve(2 * IPCLandingZone.ALIGN)          # does not fit the rest of segment 0: segment 1
+    c = z.reserve(IPCLandingZone.ALIGN)              # first fit: the tail of segment 0
+    assert (a, b, c) == (0, seg, 3 * IPCLandingZone.ALIGN)
+    assert z.reserve(5 * IPCLandingZone.ALIGN) is None   # larger than a segment: never
+    kv = z.claim(b, [IPCLandingZone.ALIGN], z.generation(b))
+    kv.fill_(1.0)
+    assert z.views[1][: 2 * IPCLandingZone.ALIGN].view(torch.bfloat16).eq(1.0).all()
+    assert z.views[0].eq(0).all()
+    for o in (a, b, c):
+        assert z.release(o)
+    assert z._free == [[0, seg], [seg, 2 * seg], [2 * seg, 3 * seg]]
+    # a whole bench wave of 32 x 64 MiB packets fits the default 4 x 1 GiB (one segment held only 16)
+    # (bookkeeping only: no 4 GiB host buffer)
+    z2 = object.__new__(IPCLandingZone)
+    z2.capacity, z2.seg_bytes = 4 << 30, 1 << 30
+    z2._init_book(120.0)
+    offs = [z2.reserve(64 << 20) for _ in range(32)]
+    assert None not in offs and len(set(offs)) == 32 and z2.reserve(2 << 30) is None

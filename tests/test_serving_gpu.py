@@ -149,29 +149,54 @@ def test_gpu_disaggregated_ipc_landing_zone():
                 assert a["outputs"]["disaggregated"]
                 assert a["outputs"]["token_ids"] == b["outputs"]["token_ids"]
             link = pre.models["mini"]._decode_link
-            assert link.ipc_packets == 3 and link.wire_packets == 0, (link.ipc_packets, link.wire_packets)
+            # every packet was gathered by the prefill engine straight into a slot reserved before its prompt
+            # ran (one pass, no staging tensor, no second copy)
+            assert link.ipc_packets == 3 and link.direct_packets == 3 and link.wire_packets == 0, \
+                (link.ipc_packets, link.direct_packets, link.wire_packets)
             cd = InferenceClient(f"127.0.0.1:{dport}")
 
             async def zone():
                 st = await cd.call({"op": "engine_stats", "model": "mini"})
                 return st["stats"]["kv_zone"]
 
+            async def drained():  # a slot given back by a failed sender returns once its gather finished
+                for _ in range(100):
+                    z = await zone()
+                    if z["slots_used"] == 0 and z["reserved"] == 0:
+                        return z
+                    await asyncio.sleep(0.05)
+                return z
+
             z = await zone()  # every imported slot went back behind the decode engine's scatter
             assert z["slots_used"] == 0 and z["pending_release"] == 0, z
-            # a sender whose copy fails after kv_reserve hands the slot back (kv_release), no leak
-            real = link._ipc.write_async
 
             async def broken(*a, **k):
-                raise RuntimeError("injected copy failure")
-            link._ipc.write_async = broken
+                raise RuntimeError("injected transfer failure")
             req = {"prompt_token_ids": list(range(9, 200)), "max_tokens": 8, "ignore_eos": True}
+            # the hand-off fails after the prompt's blocks were gathered into the reserved slot: the sender
+            # releases the slot behind that gather, no leak
+            link._ipc.wait_ready = broken
             r = await asyncio.wait_for(cp.call({"model": "mini", "inputs": req}), 60)
             assert not r["success"]
-            z = await zone()
+            z = await drained()
             assert z["slots_used"] == 0 and z["reserved"] == 0, z
-            link._ipc.write_async = real
+            del link._ipc.wait_ready
+            # the staged path (DIE_KV_DIRECT=0: packed copy into the slot after kv_reserve) with a failing copy
+            os.environ["DIE_KV_DIRECT"] = "0"
+            try:
+                link._ipc.write_async = broken
+                r = await asyncio.wait_for(cp.call({"model": "mini", "inputs": req}), 60)
+                assert not r["success"]
+                z = await drained()
+                assert z["slots_used"] == 0 and z["reserved"] == 0, z
+                del link._ipc.write_async
+                r = await asyncio.wait_for(cp.call({"model": "mini", "inputs": req}), 60)
+                assert r["success"] and r["outputs"]["disaggregated"]
+            finally:
+                os.environ.pop("DIE_KV_DIRECT", None)
             r = await asyncio.wait_for(cp.call({"model": "mini", "inputs": req}), 60)
             assert r["success"] and r["outputs"]["disaggregated"]
+            assert link.wire_packets == 0 and link.direct_packets == 4, (link.wire_packets, link.direct_packets)
             cd.close()
             for x in (cp, cs):
                 x.close()
