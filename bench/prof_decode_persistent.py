@@ -2,10 +2,10 @@
 when the workgroups entered their task, had its data, finished the compute and finished the epilogue
 (100 MHz clock, microseconds from the earliest stamp). Llama-3-8B shapes at batch 32, random init.
 
-python bench/prof_decode_persistent.py [layers] [switches, e.g. 0,1,2,4]
+DIE_C_DIAG=1 python bench/prof_decode_persistent.py [layers]
 
-Switches (DIE_DP_DBG, diagnostic builds; results are garbage except with 0): 1 activation loads cached
-(not sc1), 2 no activation loads, 4 no weight / KV loads.
+(ready_wait = task entry -> its first chunk's data in LDS: the dependency wait, the late activation loads
+and the first chunk; compute = the chunk stream; epi = the epilogue and publish.)
 """
 import json
 import os
@@ -39,36 +39,27 @@ def main():
     sc = m.alloc_decode_scratch(M)
     assert m.prepare_persistent(pool, sc)
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    pbuf = torch.zeros(ncu * (layers * 5 * 4 + 32), dtype=torch.int64, device=dev)
-    prof = pbuf[: ncu * layers * 20].view(ncu, layers * 5, 4)
-    stages = pbuf[ncu * layers * 20:].view(ncu, 4, 8)
+    pbuf = torch.zeros(ncu * layers * 5 * 4, dtype=torch.int64, device=dev)
+    prof = pbuf.view(ncu, layers * 5, 4)
     sc["persistent"]["prof"] = pbuf
     maxp = ops.decode_partials(max_ctx)
     meta = AttnMetadata(False, slots, bt, ctx, max_ctx=max_ctx, scratch=sc,
                         part_o=torch.empty(M * m.hq * maxp * 128, dtype=torch.float32, device=dev),
                         part_ml=torch.empty(M * m.hq * maxp * 2, dtype=torch.float32, device=dev),
                         attn_cnt=torch.zeros(M * m.hkv, dtype=torch.int32, device=dev))
-    variants = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "0").split(",")]
-    for dbg in variants:
-        os.environ["DIE_DP_DBG"] = str(dbg)
-        with torch.inference_mode():
-            for _ in range(3):
-                pbuf.zero_()
-                m.forward(ids, pos, meta, pool)
-            torch.cuda.synchronize()
-        summarize(prof.cpu(), layers, dbg, int(sc["persistent"]["err"].item()))
-        st = stages.double().cpu()
-        names = ("compute_prev", "issue_w", "issue_x_or_dep", "vm_wait", "barrier1", "compute", "poll", "barrier2")
-        for w in range(4):  # per wave: kilo-cycles (shader clock) per stage, median over workgroups
-            print(json.dumps({"wave": w, **{n: round(float(st[:, w, i].median()) / 1e3, 1)
-                                             for i, n in enumerate(names)}}), flush=True)
+    with torch.inference_mode():
+        for _ in range(3):
+            pbuf.zero_()
+            m.forward(ids, pos, meta, pool)
+        torch.cuda.synchronize()
+    summarize(prof.cpu(), layers, int(sc["persistent"]["err"].item()))
 
 
-def summarize(p, layers, dbg, err):
+def summarize(p, layers, err):
     valid = p[..., 0] > 0
     t0 = p[..., 0][valid].min().item()
     us = (p.double() - t0) / 100.0  # 100 MHz -> us
-    print(json.dumps({"switches": dbg, "err": err, "stamped_tasks": int(valid.sum()),
+    print(json.dumps({"err": err, "stamped_tasks": int(valid.sum()),
                       "total_us": round(us[..., 3][valid].max().item(), 1),
                       "us_per_layer": round(us[..., 3][valid].max().item() / layers, 1)}), flush=True)
     for q in range(layers * 5):

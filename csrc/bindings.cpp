@@ -827,8 +827,7 @@ void decode_persistent(Tensor ws, Tensor table, Tensor h, Tensor ssp0, Tensor bl
     TORCH_CHECK(prof->is_cuda() && prof->scalar_type() == at::kLong && prof->is_contiguous() &&
                     prof->numel() >= (int64_t)ncu * ((l1 - l0) * 5 * 4 + 32), "prof [grid, phases * 4 + 32] int64");
     a.prof = reinterpret_cast<uint64_t*>(prof->data_ptr());
-    const char* dbg = std::getenv("DIE_DP_DBG");  // experiment switches, read only by diagnostic builds
-    a.dbg = dbg ? std::atoi(dbg) : 0;
+    a.dbg = 0;
   }
   DIE_HIP(die::launch_decode_persistent(a, cur_stream()));
 }

@@ -203,13 +203,7 @@ struct WS {
 
 struct Rt {  // run-time uniforms (layers [0, l1): the launcher requires l0 = 0)
   int P, b, M, l1;
-  int dbg;  // diagnostic builds: experiment switches (DpArgs::dbg); 0 otherwise
 };
-#ifdef DIE_KERNEL_DIAG
-#define DP_DBG(r) ((r).dbg)
-#else
-#define DP_DBG(r) 0
-#endif
 template <class C>
 __device__ __forceinline__ int ntasks(const Rt& r, int p) {
   switch (p) {
@@ -1057,7 +1051,6 @@ __global__ void __launch_bounds__(NTH, 1) decode_persistent_kernel(DpArgs a) {
   r.b = blockIdx.x;
   r.M = a.M;
   r.l1 = a.l1;
-  r.dbg = a.dbg;
   const int lane0 = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   Eng<C> e(a, r, dp_smem, wave, lane0);

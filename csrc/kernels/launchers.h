@@ -148,7 +148,7 @@ struct DpArgs {
   float scale_log2, eps, inv_h;
   int H, I, hq, hkv;       // the model shape (selects the instantiation; checked by the launcher)
   uint64_t* prof;          // diagnostic builds: timeline stamps [grid][phases][4] (nullptr: none)
-  int dbg;                 // diagnostic builds: experiment switches (DIE_DP_DBG)
+  int dbg;                 // reserved (0)
 };
 // the instantiation for a model shape: cfg7 = {wrq, skq, wro, sko, wrg, wrd, skd} and the workspace layout
 // lay4[9] = {bytes for `layers` layers, offsets of: the error word, the counters, slab_q, attn, slab_od, act,

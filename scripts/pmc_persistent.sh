@@ -13,7 +13,7 @@ P3="SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE
 i=0
 for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o p$i -- python3 $R/bench/prof_decode_persistent.py 4 0 > $OUT/p$i.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o p$i -- python3 $R/bench/prof_decode_persistent.py 4 > $OUT/p$i.log 2>&1
   echo "pass $i rc=$?"
 done
 find $OUT -name "*counter_collection*.csv" | sort

@@ -58,6 +58,7 @@ class Batch:
     created_at: float
     max_batch_size: int
     max_latency: float
+    last_arrival: float = 0.0   # time.monotonic() of the latest request (idle-gap flush)
 
 
 class Batcher:
@@ -70,6 +71,7 @@ class Batcher:
         split: Optional[Callable[[Any, int], List[Any]]] = None,
         max_inflight_batches: Optional[int] = None,
         eager_when_idle: bool = False,
+        idle_flush_ms: Optional[float] = None,
     ):
         if max_batch_size < 1:
             raise ValueError("max_batch_size must be at least 1")
@@ -77,6 +79,11 @@ class Batcher:
             raise ValueError("max_latency_ms must be greater than 0")
         self.max_batch_size = max_batch_size
         self.max_latency = max_latency_ms / 1000.0
+        # idle_flush_ms: a partial batch is also flushed once no request has arrived for this long
+        # (max_latency stays the bound). Closed-loop clients that are all waiting on this batch send nothing
+        # until it returns: without it, every such batch (e.g. 16 clients per coordinator process under
+        # SO_REUSEPORT, batch size 32) waited the full max_latency.
+        self.idle_flush = (idle_flush_ms / 1000.0) if idle_flush_ms else None
         self.batch_callback = batch_callback
         self.coalesce = coalesce
         self.split = split
@@ -161,6 +168,7 @@ class Batcher:
                 self._batches[key] = batch
                 self._flush_tasks[key] = asyncio.create_task(self._timer(key, batch))
             batch.requests.append(req)
+            batch.last_arrival = time.monotonic()
             self.total_requests += 1
             if len(batch.requests) >= self.max_batch_size:
                 to_flush = self._detach(key, batch)
@@ -228,7 +236,16 @@ class Batcher:
 
     async def _timer(self, key: str, batch: Batch) -> None:
         try:
-            await asyncio.sleep(batch.max_latency)
+            if self.idle_flush is None:
+                await asyncio.sleep(batch.max_latency)
+            else:  # flush at max_latency, or earlier once arrivals have paused for idle_flush
+                t_end = time.monotonic() + batch.max_latency
+                while True:
+                    now = time.monotonic()
+                    wake = min(t_end, (batch.last_arrival or now) + self.idle_flush)
+                    if wake <= now:
+                        break
+                    await asyncio.sleep(wake - now)
         except asyncio.CancelledError:
             return
         async with self._lock:

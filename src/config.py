@@ -134,6 +134,8 @@ class DeploymentConfig:
     strategy: str = "round_robin"
     batch_max_size: int = 32
     batch_max_latency_ms: float = 10.0
+    # flush a partial batch once arrivals pause this long (closed-loop clients all waiting on it); 0: off
+    batch_idle_flush_ms: float = 1.0
     cache_size: int = 10000
     cache_policy: str = "lru"
     cache_ttl_s: Optional[float] = None

@@ -66,6 +66,7 @@ class Coordinator:
         strategy: str = "round_robin",
         max_batch_size: int = 32,
         max_latency_ms: float = 10.0,
+        batch_idle_flush_ms: Optional[float] = 1.0,
         cache_size: int = 10000,
         cache_policy: str = "lru",
         cache_ttl_s: Optional[float] = None,
@@ -93,7 +94,8 @@ class Coordinator:
         # eager_when_idle: an idle shard gets a request immediately; max_latency only
         # applies while a previous batch for that shard is still in flight.
         self.batcher = Batcher(max_batch_size=max_batch_size, max_latency_ms=max_latency_ms,
-                               batch_callback=self._batch_callback, eager_when_idle=True)
+                               batch_callback=self._batch_callback, eager_when_idle=True,
+                               idle_flush_ms=batch_idle_flush_ms)
         # coordinator -> worker frames in msgpack (C codec: ~3x cheaper than json per hop); clients keep JSON
         self.rpc = RPCClient(max_idle_per_host=512, codec=CODEC_MSGPACK)
         self.tracer = GLOBAL_TRACER
@@ -108,7 +110,8 @@ class Coordinator:
     def from_config(cls, cfg: DeploymentConfig) -> "Coordinator":
         return cls(host=cfg.listen_host, port=cfg.listen_port, strategy=cfg.strategy,
                    max_batch_size=cfg.batch_max_size, max_latency_ms=cfg.batch_max_latency_ms,
-                   cache_size=cfg.cache_size, cache_policy=cfg.cache_policy, cache_ttl_s=cfg.cache_ttl_s,
+                   batch_idle_flush_ms=cfg.batch_idle_flush_ms, cache_size=cfg.cache_size,
+                   cache_policy=cfg.cache_policy, cache_ttl_s=cfg.cache_ttl_s,
                    max_retries=cfg.max_retries, request_timeout_s=cfg.request_timeout_s,
                    health_check_interval=cfg.health_check_interval)
 

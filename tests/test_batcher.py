@@ -159,3 +159,38 @@ def test_validation():
         Batcher(max_batch_size=0)
     with pytest.raises(ValueError):
         Batcher(max_latency_ms=0)
+
+
+def test_idle_gap_flush_does_not_wait_max_latency():
+    """idle_flush_ms: a partial batch goes out once arrivals pause (closed-loop clients all waiting on it),
+    long before max_latency; a steady stream of arrivals still batches up to max_latency / max_batch."""
+    import asyncio
+    import time
+
+    from src.batcher import Batcher
+
+    async def main():
+        sizes = []
+
+        async def cb(model, version, inputs):
+            sizes.append(len(inputs))
+            return inputs
+
+        b = Batcher(max_batch_size=32, max_latency_ms=200.0, batch_callback=cb, idle_flush_ms=2.0)
+        await b.start()
+        t0 = time.perf_counter()
+        futs = [await b.add_request("m", "1", i) for i in range(5)]
+        await asyncio.gather(*futs)
+        quick = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        futs = []
+        for i in range(10):  # arrivals 1 ms apart: under the idle gap, so they keep batching
+            futs.append(await b.add_request("m", "1", i))
+            await asyncio.sleep(0.001)
+        await asyncio.gather(*futs)
+        await b.stop()
+        return quick, sizes
+
+    quick, sizes = asyncio.run(main())
+    assert quick < 0.1, quick          # not the 200 ms max_latency
+    assert sizes[0] == 5 and sum(sizes) == 15 and max(sizes[1:]) >= 5, sizes
