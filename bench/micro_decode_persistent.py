@@ -3,7 +3,7 @@ decode-step kernel (csrc/kernels/decode_persistent.hip, all 32 layers in one lau
 fused path (5 launches per layer) — with the production tiles and with the persistent kernel's own tiles.
 Each variant is captured in a hipGraph; the timed region is graph replays (layers + final norm, no LM head).
 
-python bench/micro_decode_persistent.py [layers] [reps]
+python bench/micro_decode_persistent.py [layers] [reps] [rows]
 """
 import json
 import os
@@ -23,7 +23,8 @@ def main():
     layers = int(sys.argv[1]) if len(sys.argv) > 1 else 32
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     dev = torch.device("cuda:0")
-    M, bs, max_ctx = 32, 16, 1024
+    M = int(sys.argv[3]) if len(sys.argv) > 3 else 32
+    bs, max_ctx = 16, 1024
     m = CausalLM(get_preset("llama3-8b", num_layers=layers), dev, seed=0, max_position=max_ctx + 16)
     nbps = max_ctx // bs
     nblocks = M * nbps + 8
