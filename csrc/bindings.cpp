@@ -538,6 +538,26 @@ void decode_advance(Tensor out, Tensor ids, Tensor pos, Tensor ctx, Tensor slots
                                      (int)block_size, (int)tokens.size(0), cur_stream()));
 }
 
+// Decode-step embedding gather + first-norm statistics (norm_act.hip): out [M, H] = table[ids], ssp[0][m] = sum of
+// squares of out[m]
+void embed_sumsq(Tensor out, Tensor ssp, Tensor table, Tensor ids) {
+  DIE_CHECK_CUDA(table);
+  DIE_CHECK_BF16(table);
+  DIE_CHECK_BF16(out);
+  DIE_CHECK_CONTIG(table);
+  DIE_CHECK_CONTIG(out);
+  DIE_CHECK_DTYPE(ids, at::kLong);
+  DIE_CHECK_CONTIG(ids);
+  DIE_CHECK_DTYPE(ssp, at::kFloat);
+  DIE_CHECK_CONTIG(ssp);
+  const int64_t M = ids.numel(), H = table.size(1);
+  TORCH_CHECK(table.dim() == 2 && out.dim() == 2 && out.size(0) == M && out.size(1) == H, "out [M, H], table [V, H]");
+  TORCH_CHECK(M >= 1 && M <= die::DECODE_SSP_LD && ssp.numel() >= die::DECODE_SSP_LD && H % 8 == 0,
+              "embed_sumsq: 1 <= M <= 128 rows, ssp [1, 128], H % 8 == 0");
+  DIE_HIP(die::launch_embed_sumsq(bf(out), ssp.data_ptr<float>(), bf(table), ids.data_ptr<int64_t>(), (int)M, (int)H,
+                                  cur_stream()));
+}
+
 void residual_add_sumsq(Tensor ssp, Tensor resid, Tensor x) {
   DIE_CHECK_CUDA(x);
   DIE_CHECK_BF16(x);
@@ -859,6 +879,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("row_sumsq", &row_sumsq);
   m.def("residual_add_sumsq", &residual_add_sumsq);
   m.def("decode_advance", &decode_advance);
+  m.def("embed_sumsq", &embed_sumsq);
   m.def("moe_route", &moe_route);
   m.def("moe_combine_residual", &moe_combine_residual);
   m.def("gemm_decode_grouped", &gemm_decode_grouped);

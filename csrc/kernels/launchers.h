@@ -155,6 +155,8 @@ struct DpArgs {
 // ssp_o, ssp_d}; false if the shape has none
 bool decode_persistent_config(int H, int I, int hq, int hkv, int layers, int* cfg7, int64_t* lay4);
 hipError_t launch_decode_persistent(const DpArgs& a, hipStream_t s);
+hipError_t launch_embed_sumsq(bf16_t* out, float* ssp, const bf16_t* table, const int64_t* ids, int rows, int hidden,
+                              hipStream_t s);
 hipError_t launch_ipc_copy(void* dst, const void* src, int64_t nbytes, hipStream_t s);
 hipError_t car_free(void* p);
 hipError_t car_ipc_handle(void* p, void* handle64);

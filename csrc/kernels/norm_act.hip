@@ -196,6 +196,40 @@ __global__ void __launch_bounds__(256) row_sumsq_kernel(float* __restrict__ ssp,
   if (threadIdx.x == 0) ssp[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
+// Decode-step input: out[row] = table[ids[row]] (the embedding gather) and ssp[row] = its sum of squares (the
+// first layer's RMSNorm statistics) in one pass — the gather and row_sumsq were two launches per step.
+// grid = rows (<= 128), block = 256.
+__global__ void __launch_bounds__(256) embed_sumsq_kernel(bf16_t* __restrict__ out, float* __restrict__ ssp,
+                                                          const bf16_t* __restrict__ table,
+                                                          const int64_t* __restrict__ ids, int hidden) {
+  __shared__ float red[4];
+  const int64_t id = ids[blockIdx.x];
+  const uint4* src = reinterpret_cast<const uint4*>(table + id * hidden);
+  uint4* dst = reinterpret_cast<uint4*>(out + (int64_t)blockIdx.x * hidden);
+  float ss = 0.f;
+  for (int c = threadIdx.x; c < (hidden >> 3); c += 256) {
+    const uint4 u = src[c];
+    dst[c] = u;
+    float v[8];
+    unpack8(u, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  if (threadIdx.x == 0) ssp[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+hipError_t launch_embed_sumsq(bf16_t* out, float* ssp, const bf16_t* table, const int64_t* ids, int rows, int hidden,
+                              hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  if (hidden % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(embed_sumsq_kernel, dim3(rows), dim3(256), 0, s, out, ssp, table, ids, hidden);
+  return hipGetLastError();
+}
+
 // resid[row] += x[row] (bf16, in place) and ssp[row] = sum of squares of the new residual:
 // the tensor-parallel form of the decode GEMM's residual epilogue (mode 3), run after the
 // row-parallel projection's all-reduce. grid = rows (<= 128), block = 256.

@@ -118,12 +118,25 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
   const int k = top_k ? top_k[r] : 0;
   const float p = top_p ? top_p[r] : 1.f;
 
+  // the argmax pass (all a greedy row needs): AU 16-B loads per lane in flight at once instead of one
+  // dependent round trip per 16 KiB of the row (11.9 -> see docs/performance.md, 32 x 128K rows)
+  constexpr int AU = 8;
   ArgMax best{-INFINITY, 0x7fffffff};
-  for (int i = threadIdx.x * 8; i < vocab; i += SNT * 8) {
-    float z[8];
-    unpack8(*reinterpret_cast<const uint4*>(row + i), z);
+  for (int i0 = threadIdx.x * 8; i0 < vocab; i0 += SNT * 8 * AU) {
+    uint4 v[AU];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) best = better(best, ArgMax{z[j], i + j});
+    for (int u = 0; u < AU; ++u) {
+      const int i = i0 + u * SNT * 8;
+      v[u] = i < vocab ? *reinterpret_cast<const uint4*>(row + i) : make_uint4(0xff80ff80u, 0xff80ff80u, 0xff80ff80u, 0xff80ff80u);
+    }
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+      float z[8];
+      unpack8(v[u], z);
+      const int i = i0 + u * SNT * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) best = better(best, ArgMax{z[j], i + j});
+    }
   }
   best = block_argmax(best, red);
   // an all-NaN / all -inf row (e.g. a padded graph row over uninitialised KV) still yields a

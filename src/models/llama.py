@@ -333,10 +333,13 @@ class CausalLM:
         """Returns the final-norm hidden states [T, H]. ``kv_pool`` is
         [layers, 2, num_blocks, hkv, block_size, head_dim]."""
         eps = self.arch.rms_eps
+        if (self._slab_path(input_ids) and meta.scratch is not None and not meta.is_prefill
+                and self._fused_decode_ok(kv_pool, input_ids.shape[0])):
+            # the embedding gather and the first norm's row statistics in one launch
+            residual, ssp0 = ops.embed_sumsq(input_ids, self.embed, meta.scratch["ssp0"])
+            return self._forward_decode_fused(residual, positions, meta, kv_pool, ssp0=ssp0)
         residual = F.embedding(input_ids, self.embed)
         if self._slab_path(input_ids):
-            if meta.scratch is not None and not meta.is_prefill and self._fused_decode_ok(kv_pool, input_ids.shape[0]):
-                return self._forward_decode_fused(residual, positions, meta, kv_pool)
             if not self.tp.enabled and not self.arch.is_moe:  # the slab fallback is dense-only
                 return self._forward_decode_slab(residual, positions, meta, kv_pool)
         if self.sequence_parallel and meta.is_prefill:
@@ -573,7 +576,7 @@ class CausalLM:
                 and ((sq * (g + 2) + 1) // 2) * 1024 + 1536 <= V3_MERGE_BYTES)
 
     def _forward_decode_fused(self, h: torch.Tensor, positions: torch.Tensor, meta: AttnMetadata,
-                              kv_pool: torch.Tensor) -> torch.Tensor:
+                              kv_pool: torch.Tensor, ssp0: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Decode layer = 5 launches: qkv (split-K slabs) -> attention (norm scale + slab sum + RoPE
         + KV write in its prologue) -> o (slabs, last arriver adds into the residual and writes the
         next norm's row statistics) -> gate/up (norm as a row scale, SiLU*mul) -> down (as o).
@@ -594,7 +597,7 @@ class CausalLM:
             t = lw.tiled.get((name, wr, kc))
             return (getattr(lw, name), False) if t is None else (t, True)
 
-        ssp_prev = ops.row_sumsq(h, out=sc["ssp0"])
+        ssp_prev = ssp0 if ssp0 is not None else ops.row_sumsq(h, out=sc["ssp0"])
         ps = sc.get("persistent")
         if ps is not None and h.shape[0] <= 32 and ps["pool_ptr"] == kv_pool.data_ptr():
             # every layer in one persistent launch (weight / KV stream kept running across op boundaries)

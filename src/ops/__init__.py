@@ -357,6 +357,17 @@ def residual_add_sumsq(resid: torch.Tensor, x: torch.Tensor, out: torch.Tensor) 
     return out
 
 
+def embed_sumsq(ids: torch.Tensor, table: torch.Tensor, ssp: torch.Tensor):
+    """(table[ids] [M, H], ssp): the decode step's embedding gather and its per-row sums of squares (the first
+    layer's RMSNorm statistics, ssp [1, SSP_LD]) in one launch."""
+    if not table.is_cuda:
+        h = torch.nn.functional.embedding(ids, table)
+        return h, row_sumsq(h, out=ssp)
+    h = torch.empty(ids.shape[0], table.shape[1], dtype=table.dtype, device=table.device)
+    _kern().embed_sumsq(h, ssp, table, ids)
+    return h, ssp
+
+
 def row_sumsq(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[1, SSP_LD] fp32 per-row sums of squares of x [M <= SSP_LD, H] (RMSNorm statistics)."""
     if out is None:

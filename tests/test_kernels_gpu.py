@@ -249,6 +249,15 @@ def test_sampling_greedy_and_filters(dev):
     logits = torch.randn(6, v, device=dev, dtype=torch.bfloat16) * 3
     out = ops.sample(logits)
     assert torch.equal(out.cpu(), logits.float().argmax(-1).cpu())
+    # the batched argmax pass at vocabularies below / between its load batches, ties to the lowest index,
+    # and an all -inf row (-> token 0, never an out-of-range id)
+    for vs in (8, 1000, 8192 * 8 + 8):
+        lg = (torch.randn(3, vs, device=dev) * 3).to(torch.bfloat16)
+        lg[1, vs // 2] = lg[1, vs - 1] = 100.0
+        lg[2] = float("-inf")
+        got = ops.sample(lg).cpu()
+        want = lg.float().argmax(-1).cpu()
+        assert got[0] == want[0] and got[1] == vs // 2 and got[2] == 0, (vs, got, want)
     temp = torch.full((6,), 0.8, device=dev)
     topk = torch.tensor([1, 5, 5, 0, 0, 50], dtype=torch.int32, device=dev)
     topp = torch.tensor([1.0, 1.0, 0.5, 1e-6, 0.9, 0.9], device=dev)
