@@ -219,8 +219,12 @@ class LLMBackend:
         try:
             pseq = await self.async_engine.submit(rid, gi.prompt_token_ids, gi.sampling, user_data=ud)
         except BaseException:
-            if slot is not None:  # the prompt never ran to the export (or its gather may still be queued)
-                await self._decode_link.abandon(slot, None)
+            if slot is not None:
+                # a cancelled await does not stop the prompt: revoke the destination (the engine reads it when
+                # it exports; this dict is the one it holds) and leave the slot to the decode worker's
+                # reservation TTL — releasing it now could hand it to another sender while a gather that read
+                # the destination just before the revocation still writes into it
+                ud["export_dst"] = None
             raise
         if pseq.finish_reason == "stop":
             if slot is not None:
