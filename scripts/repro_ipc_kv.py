@@ -33,8 +33,8 @@ async def main():
     print("kv_channel", {k: v for k, v in rep.items() if k != "handle"}, flush=True)
     torch.zeros(1, device="cuda:0")
     print("opening", flush=True); t_open = time.time()
-    s = IPCSender(rep["handle"], rep["capacity"], torch.device("cuda:0"))
-    print("opened", hex(s.ptr), round(time.time() - t_open, 2), "s", flush=True)
+    s = IPCSender(rep.get("handles") or rep["handle"], rep.get("seg_bytes", rep["capacity"]), torch.device("cuda:0"))
+    print("opened", [hex(p) for p in s.ptrs], round(time.time() - t_open, 2), "s", flush=True)
     r = await c.call({"op": "kv_reserve", "model": "mini", "nbytes": 1 << 20})
     print("reserve", r, flush=True)
     x = torch.arange(1 << 19, device="cuda:0", dtype=torch.int16).view(torch.bfloat16)
