@@ -593,3 +593,19 @@ def test_gemm_decode_large_m_slabs_and_tiled(dev, m, wr, kc, sk):
     wt = ops.gd_pack_weights(w, wr, kc=kc)
     b = ops.gemm_decode(x, wt, 2 | 32, wr, sk, kc=kc)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("rows", [1, 7, 32, 128])
+def test_embed_sumsq_matches_gather_and_fp32_sumsq(dev, rows):
+    """The decode step's fused embedding gather + first-norm statistics (norm_act.hip embed_sumsq) against
+    torch's gather and an fp32 sum of squares of the gathered bf16 rows; the statistics row is [1, 128]."""
+    table = (torch.randn(5000, 4096, device=dev) * 0.05).to(torch.bfloat16)
+    ids = torch.randint(0, 5000, (rows,), device=dev)
+    ssp = torch.full((1, ops.SSP_LD), -1.0, device=dev)
+    h, s = ops.embed_sumsq(ids, table, ssp)
+    assert s is ssp
+    want = torch.nn.functional.embedding(ids, table)
+    assert torch.equal(h, want)
+    ref = want.float().pow(2).sum(-1)
+    torch.testing.assert_close(ssp[0, :rows], ref, rtol=1e-5, atol=1e-5)
+    assert torch.all(ssp[0, rows:] == -1.0)  # rows past M untouched
