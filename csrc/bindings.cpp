@@ -414,10 +414,10 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
   const int64_t M = x.size(0), K = x.size(1);
   TORCH_CHECK(M >= 1 && M <= 128, "gemm_decode: 1 <= M <= 128");
   TORCH_CHECK(gd_tile_ok(wr, kc), "gemm_decode: unsupported (wr, kc) tile");
-  TORCH_CHECK(mode >= 0 && mode <= 4, "mode");
+  TORCH_CHECK(mode >= 0 && mode <= 6 && mode != 5, "mode");
   const int64_t wrr = wr;  // rows per workgroup
   TORCH_CHECK(K % (kc * sk) == 0, "gemm_decode: K must be a multiple of kc * sk");
-  const bool silu = mode == 1 || mode == 4;
+  const bool silu = mode == 1 || mode == 4 || mode == 6;
   int64_t N, ldy;
   if (mode == 2 || mode == 3) {
     DIE_CHECK_DTYPE(y, at::kFloat);
@@ -428,7 +428,7 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
   } else {
     DIE_CHECK_BF16(y);
     check_rows(y, "y");
-    TORCH_CHECK(sk == 1 && y.size(0) == M, "bf16 output: sk == 1, y [M, N]");
+    TORCH_CHECK((sk == 1 || mode == 6) && y.size(0) == M, "bf16 output: sk == 1 (mode 6: any), y [M, N]");
     N = y.size(1);
     ldy = y.stride(0);
   }
@@ -455,7 +455,17 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
       fz.counters = counters.data_ptr<int>();
     }
   }
-  if (mode == 4) {
+  if (mode == 6 && sk > 1) {  // split-K SiLU: ssp_out carries the fp32 partial slab [sk, M, 2N], counters the tickets
+    DIE_CHECK_DTYPE(ssp_out, at::kFloat);
+    DIE_CHECK_CONTIG(ssp_out);
+    TORCH_CHECK(ssp_out.numel() >= sk * M * 2 * N && sk * M * 2 * N * 4 < ((int64_t)1 << 31), "mode 6 slab [sk, M, 2N]");
+    DIE_CHECK_DTYPE(counters, at::kInt);
+    TORCH_CHECK(counters.is_cuda() && counters.numel() >= N / (wrr / 2), "mode 6 counters [N / (wr / 2)] int32");
+    fz.slab6 = ssp_out.data_ptr<float>();
+    fz.ld_slab6 = 2 * N;
+    fz.counters = counters.data_ptr<int>();
+  }
+  if (mode == 4 || mode == 6) {
     DIE_CHECK_DTYPE(ssp_in, at::kFloat);
     DIE_CHECK_CONTIG(ssp_in);
     TORCH_CHECK(ssp_in.dim() == 2 && ssp_in.size(1) == die::DECODE_SSP_LD && ssp_in.size(0) >= 1 &&

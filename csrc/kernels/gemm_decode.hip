@@ -95,7 +95,7 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
   constexpr int ROWB = KC * 2;                 // bytes per image row
   constexpr int CPR = KC / 8;                  // 16-byte chunks per row
   constexpr int RPP = 64 / CPR;                // rows per 1-KiB DMA piece
-  constexpr bool SILU = EPI == 1 || EPI == 4;
+  constexpr bool SILU = EPI == 1 || EPI == 4 || EPI == 6;
   constexpr int NO = SILU ? WR / 2 : WR;       // output columns per workgroup
   constexpr int SLOT = (WR + XR) * ROWB;       // bytes per ring slot
   constexpr int INSTR = (WR + XR) / RPP;       // 1-KiB DMA pieces per chunk
@@ -179,8 +179,8 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
   // inside the weight stream. Index clamped, masked later (no branches).
   constexpr int NSL = NTH / RR;                // tile slices
   constexpr int NPF = (128 + NSL - 1) / NSL;   // prefetched statistics per thread (<= 128 tiles)
-  float ssv[EPI == 4 ? NPF : 1];
-  if constexpr (EPI == 4) {
+  float ssv[EPI == 4 || EPI == 6 ? NPF : 1];
+  if constexpr (EPI == 4 || EPI == 6) {
 #pragma unroll
     for (int i = 0; i < NPF; ++i)
       ssv[i] = fz.ssp_in[min(tid / RR + NSL * i, fz.ssp_tiles - 1) * SSP_LD + (tid % RR)];
@@ -352,7 +352,7 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
     if (!single && tid == 0) __hip_atomic_store(fz.counters + bx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
-  if constexpr (EPI == 4) {
+  if constexpr (EPI == 4 || EPI == 6) {
     // row scale r[m] = rsqrt(sum_t ssp[t][m] / n + eps) (the RMSNorm whose weight is folded into W)
     float* part = reinterpret_cast<float*>(escr);  // [NSL][RR]
     float* rs = part + NTH;
@@ -368,6 +368,79 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
       rs[tid] = rsqrtf(t * fz.inv_n + fz.eps);
     }
     __syncthreads();
+  }
+  if constexpr (EPI == 6) {
+    // split-K form of mode 4: this slice's (gate, up) partial sums go to the fp32 slab fz.slab6
+    // [sk][M][2 N_out] (tile-local columns: gate at bx*WR + j, up at bx*WR + NO + j, write-through); the
+    // last arriver of the tile (agent-scope ticket, re-armed) adds the other slices in slice order, applies
+    // the row scale and SiLU(gate) * up and writes the bf16 output. Lets a narrow-N projection (a TP
+    // shard's gate/up) use wide tiles — less activation re-read per weight byte — at a full grid.
+    constexpr int EPT = (RR * NO + NTH - 1) / NTH;
+    const float* rsv = reinterpret_cast<const float*>(escr) + NTH;
+    int* ctl = reinterpret_cast<int*>(escr) + NTH + RR;
+    float g[EPT], u[EPT];
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = min(tid + i * NTH, RR * NO - 1), m = e / NO, j = e % NO;
+      float gv = 0.f, uv = 0.f;
+#pragma unroll
+      for (int w = 0; w < NRED; ++w) {
+        gv += red[(w * RR + m) * WR + j];
+        uv += red[(w * RR + m) * WR + NO + j];
+      }
+      g[i] = gv;
+      u[i] = uv;
+    }
+    const int64_t lds6 = fz.ld_slab6;  // floats per slab row (2 N_out)
+    __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(fz.slab6, 0, 0x7fffffff, 0x00020000);
+    if (ny > 1) {
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) {
+        const int e = tid + i * NTH, m = e / NO, j = e % NO;
+        if (e < RR * NO && m < M) {
+          const int64_t o = ((int64_t)by * M + m) * lds6 + (int64_t)bx * WR + j;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g[i]), rsl, (int)(o * 4), 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(u[i]), rsl, (int)((o + NO) * 4), 0, 16);
+        }
+      }
+      wait_vm<0>();
+      __syncthreads();
+      if (tid == 0)
+        ctl[0] = __hip_atomic_fetch_add(fz.counters + bx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ny - 1;
+      __syncthreads();
+      if (!ctl[0]) return;
+      // last arriver: every other slice's partials (write-through stores above, sc1 loads here), in slice order
+      float gs[EPT], us[EPT];
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) gs[i] = us[i] = 0.f;
+      for (int k = 0; k < ny; ++k) {
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+          const int e = min(tid + i * NTH, RR * NO - 1), m = min(e / NO, M - 1), j = e % NO;
+          const int64_t o = ((int64_t)k * M + m) * lds6 + (int64_t)bx * WR + j;
+          const float gk = k == by ? g[i] : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsl, (int)(o * 4), 0, 16));
+          const float uk = k == by ? u[i] : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsl, (int)((o + NO) * 4), 0, 16));
+          gs[i] += gk;
+          us[i] += uk;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) {
+        g[i] = gs[i];
+        u[i] = us[i];
+      }
+      if (tid == 0) __hip_atomic_store(fz.counters + bx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tid + i * NTH, m = e / NO, j = e % NO;
+      if (e < RR * NO && m < M) {
+        const float r = rsv[m];
+        const float gv = g[i] * r, uv = u[i] * r;
+        reinterpret_cast<bf16_t*>(Yv)[(int64_t)m * ldy + n0 + j] = f2bf(gv / (1.f + __expf(-gv)) * uv);
+      }
+    }
+    return;
   }
   for (int e = tid; e < RR * NO; e += NTH) {
     const int m = e / NO, j = e % NO;
@@ -437,7 +510,7 @@ static hipError_t launch_gd_xr(void* Y, int64_t ldy, const bf16_t* X, int64_t ld
   } else {
     constexpr int S = ring_slots(WR, XR, KC);
     constexpr size_t lds = gd_lds(WR, XR, KC, S);
-    const dim3 grid(N_out / ((EPI == 1 || EPI == 4) ? WR / 2 : WR), sk, fz.grp_n);
+    const dim3 grid(N_out / ((EPI == 1 || EPI == 4 || EPI == 6) ? WR / 2 : WR), sk, fz.grp_n);
     if (nt)
       hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, true, KC, XR, SKC>), grid, dim3(NTH), lds, s, Y, ldy, X, ldx,
                          W, M, N_out, K, fz);
@@ -451,7 +524,7 @@ static hipError_t launch_gd_xr(void* Y, int64_t ldy, const bf16_t* X, int64_t ld
 template <int WR, int EPI, int KC, int SKC = 0>
 static hipError_t launch_gd(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N_out,
                             int K, int sk, bool nt, const GemmDecodeFuse& fz, hipStream_t s) {
-  constexpr int NO = (EPI == 1 || EPI == 4) ? WR / 2 : WR;
+  constexpr int NO = (EPI == 1 || EPI == 4 || EPI == 6) ? WR / 2 : WR;
   if (N_out % NO || K % sk || (K / sk) % KC) return hipErrorInvalidValue;
   // Activation image: the smallest of 16 / 32 / 64 / 128 rows that holds M and exists for this tile
   // (16 only on the nt path). Measured (profiles/micro_gemm_decode_xr16_r1.jsonl): dense 8B projections
@@ -479,6 +552,7 @@ static hipError_t launch_modes(void* Y, int64_t ldy, const bf16_t* X, int64_t ld
     case 1: return launch_gd<WR, 1, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
     case 2: return launch_gd<WR, 2, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
     case 4: return launch_gd<WR, 4, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
+    case 6: return launch_gd<WR, 6, KC>(Y, ldy, X, ldx, W, M, N, K, sk, nt, fz, s);
     case 3:
       if constexpr (WR == 32 || WR == 64 || WR == 128) {
         switch (sk) {  // compile-time split count: the last arriver issues every slab load at once
@@ -497,7 +571,9 @@ static hipError_t launch_modes(void* Y, int64_t ldy, const bf16_t* X, int64_t ld
 // mode 3: fp32 slabs + last-arriver residual update (fz.resid += sum of slabs, bf16) and per-tile
 //         row sums of squares fz.ssp_out [N / wr][SSP_LD] (the next RMSNorm's statistics);
 // mode 4: mode 1 with the rows scaled by rsqrt(sum_t fz.ssp_in[t][m] * inv_n + eps) (RMSNorm with
-//         its weight folded into W).
+//         its weight folded into W);
+// mode 6: mode 4 split over sk K slices: fp32 partials in fz.slab6 [sk][M][2 N], the tile's last arriver
+//         finishes (fz.counters [N / (wr / 2)] tickets, zero, re-armed).
 // (wr, kc): weight rows per workgroup and K elements per ring slot (gemm_decode_tile_ok), so that
 // (N / columns) * sk can be made a multiple of the CU count for the model's shapes (e.g. 8B gate/up:
 // 14336 / 56 = 256 workgroups at wr = 112). Small K slots (64 / 32) are for M > 32: they keep the
@@ -506,8 +582,10 @@ hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx
                               int K, int mode, int wr, int kc, int sk, bool nt, const GemmDecodeFuse& fz,
                               hipStream_t s) {
   if (M <= 0) return hipSuccess;
-  if (M > 128 || sk < 1 || (mode != 2 && mode != 3 && sk != 1)) return hipErrorInvalidValue;
-  if (mode == 4 && (fz.ssp_in == nullptr || fz.ssp_tiles < 1 || fz.ssp_tiles > 128)) return hipErrorInvalidValue;
+  if (M > 128 || sk < 1 || (mode != 2 && mode != 3 && mode != 6 && sk != 1)) return hipErrorInvalidValue;
+  if ((mode == 4 || mode == 6) && (fz.ssp_in == nullptr || fz.ssp_tiles < 1 || fz.ssp_tiles > 128))
+    return hipErrorInvalidValue;
+  if (mode == 6 && sk > 1 && (fz.slab6 == nullptr || fz.counters == nullptr)) return hipErrorInvalidValue;
   if (mode == 3 && (fz.resid == nullptr || fz.ssp_out == nullptr || (sk > 1 && fz.counters == nullptr)))
     return hipErrorInvalidValue;
 #define DIE_GD(WR, KC) \

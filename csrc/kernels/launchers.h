@@ -89,6 +89,8 @@ struct GemmDecodeFuse {
   const int* grp_rows = nullptr; //   optional gather: X row j of the sorted order is token grp_rows[j] / grp_k
   int grp_k = 1;                 //   (X is then the un-permuted [T, K] activations; Y stays in sorted order)
   int tiled = 0;                 // W pre-packed into the kernel's tile order (gd_pack_weights)
+  float* slab6 = nullptr;        // mode 6: split-K (gate, up) partials [sk][M][ld_slab6 = 2 N_out]
+  int64_t ld_slab6 = 0;
   long long* ts = nullptr;       // diagnostics: per-workgroup [start, end, xcc] s_memrealtime stamps (or null)
 };
 hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,

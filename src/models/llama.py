@@ -460,8 +460,9 @@ class CausalLM:
         else:                # residual-updating split-K (mode 3)
             o = ops.decode_tile(h, self.hq * d, 3, b)
             down = ops.decode_tile(h, self.inter, 3, b) if not self.arch.is_moe else None
-        gu = ops.decode_tile(self.inter, h, 4, b)[:2] if not self.arch.is_moe else None
-        return {"qkv": qkv, "o": o, "down": down, "gate_up": gu}
+        gu = ops.decode_tile_silu(self.inter, h, b) if not self.arch.is_moe else None
+        return {"qkv": qkv, "o": o, "down": down, "gate_up": gu[:2] if gu else None,
+                "gate_up_sk": gu[2] if gu else 1}
 
     def _packed_layouts(self, buckets) -> set:
         """(projection, wr, kc) tile-order copies the fused path uses for these row buckets."""
@@ -530,6 +531,11 @@ class CausalLM:
         self.pack_decode_weights(buckets)
         ld = ops.SSP_LD
         sc = {"plans": plans, "ssp0": torch.zeros(1, ld, dtype=f32, device=dev),
+              # split-K gate/up (mode 6): fp32 partial slab + per-tile tickets, sized for the largest bucket
+              "slab6": torch.empty(max((p["gate_up_sk"] * b * 2 * self.inter if p["gate_up_sk"] > 1 else 0)
+                                       for b, p in plans.items()), dtype=f32, device=dev),
+              "cnt6": torch.zeros(max((self.inter // (p["gate_up"][0] // 2) if p["gate_up"] else 0)
+                                      for p in plans.values()), dtype=i32, device=dev),
               "ssp_a": torch.zeros(to, ld, dtype=f32, device=dev), "cnt_a": torch.zeros(to, dtype=i32, device=dev),
               "ssp_b": torch.zeros(td, ld, dtype=f32, device=dev), "cnt_b": torch.zeros(td, dtype=i32, device=dev)}
         return sc
@@ -625,18 +631,21 @@ class CausalLM:
                     ops.moe_forward_routed(x, lw.w13, lw.w2, wr_, ids_, residual=h, ssp=ssp_b)
             else:
                 wg, kg = plan["gate_up"]
+                gsk = plan.get("gate_up_sk", 1)
                 wgu, tg = tw(lw, "gate_up", wg, kg)
                 if self.tp.enabled:  # row-parallel partial sums -> all-reduce -> residual + statistics (one
                     # launch on the one-shot IPC path, see TPContext.all_reduce_residual)
                     self.tp.all_reduce_residual(self._row_parallel(attn, lw, "o", plan), h, ssp_a)
-                    act = ops.linear_silu_mul_rownorm(h, wgu, ssp_a, eps, wg, tiled=tg, kc=kg)
+                    act = ops.linear_silu_mul_rownorm(h, wgu, ssp_a, eps, wg, tiled=tg, kc=kg, sk=gsk,
+                                                      slab=sc["slab6"], counters=sc["cnt6"])
                     self.tp.all_reduce_residual(self._row_parallel(act, lw, "down", plan), h, ssp_b)
                 else:
                     wdn_, kd, sd = plan["down"]
                     wo_t, to_ = tw(lw, "o", wo, ko)
                     wd_t, td_ = tw(lw, "down", wdn_, kd)
                     ops.linear_slab_residual(attn, wo_t, h, ssp_a, sc["cnt_a"], wo, so, tiled=to_, kc=ko)
-                    act = ops.linear_silu_mul_rownorm(h, wgu, ssp_a, eps, wg, tiled=tg, kc=kg)
+                    act = ops.linear_silu_mul_rownorm(h, wgu, ssp_a, eps, wg, tiled=tg, kc=kg, sk=gsk,
+                                                      slab=sc["slab6"], counters=sc["cnt6"])
                     ops.linear_slab_residual(act, wd_t, h, ssp_b, sc["cnt_b"], wdn_, sd, tiled=td_, kc=kd)
             ssp_prev = ssp_b
         return ops.rms_norm(h, self.norm, eps)

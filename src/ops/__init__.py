@@ -332,18 +332,45 @@ def linear_slab_residual(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, 
 
 
 def linear_silu_mul_rownorm(x: torch.Tensor, w_gate_up: torch.Tensor, ssp_in: torch.Tensor, eps: float,
-                            wr: Optional[int] = None, tiled: bool = False, kc: Optional[int] = None) -> torch.Tensor:
+                            wr: Optional[int] = None, tiled: bool = False, kc: Optional[int] = None, sk: int = 1,
+                            slab: Optional[torch.Tensor] = None,
+                            counters: Optional[torch.Tensor] = None) -> torch.Tensor:
     """silu(r * x @ gate^T) * (r * x @ up^T) with r = rsqrt(sum_t ssp_in[t] / K + eps) per row:
-    RMSNorm (weight folded into w_gate_up) + gate/up + SiLU*mul in one weight stream."""
+    RMSNorm (weight folded into w_gate_up) + gate/up + SiLU*mul in one weight stream. sk > 1 (mode 6): K
+    split over sk workgroups per tile with fp32 partials in ``slab`` (>= sk * rows * 2N floats) and the tile's
+    last arriver finishing (``counters``: >= N / (wr / 2) int32, zero; re-armed by the kernel)."""
     n = w_gate_up.shape[0] // 2
     if wr is None:
         wr, kc, _ = decode_tile(n, x.shape[1], 4, _bucket(x.shape[0]))
     wr, kc = gd_tile(wr, kc)
     out = torch.empty(x.shape[0], n, dtype=x.dtype, device=x.device)
     e = _empty(x.device)
+    if sk > 1:
+        if slab is None or counters is None:
+            raise ValueError("split-K gate/up (sk > 1) needs its slab and counters")
+        _kern().gemm_decode(out, x, w_gate_up, 6 | (32 if tiled else 0), wr, kc, sk, DECODE_GEMM_NT, e, slab, counters,
+                            ssp_in, float(eps))
+        return out
     _kern().gemm_decode(out, x, w_gate_up, 4 | (32 if tiled else 0), wr, kc, 1, DECODE_GEMM_NT, e, e, e, ssp_in,
                         float(eps))
     return out
+
+
+# (N_out, K, row bucket) -> (wr, kc, sk) of the split-K gate/up (mode 6), where the full-K form's grid forces
+# narrow tiles (bench/micro_gd_splitk_silu.py, profiles/micro_gd_splitk_silu_r3.jsonl): Llama-3-70B's TP=8
+# shard 27.1 us vs 30.0 for the best full-K tile (32, 256). Dense 8B shapes lose with split-K (not listed).
+DECODE_SILU_SPLITK_CFG = {
+    (3584, 8192, 32): (64, 256, 2),
+}
+
+
+def decode_tile_silu(n: int, k: int, bucket: int = 32):
+    """(wr, kc, sk) of the norm-scaled SiLU gate/up decode GEMM: a split-K tile where one was measured faster,
+    else the full-K tile (sk = 1). DIE_GD_SILU_SPLITK=0 keeps every shape on the full-K form."""
+    c = DECODE_SILU_SPLITK_CFG.get((n, k, bucket))
+    if c is not None and os.environ.get("DIE_GD_SILU_SPLITK", "1") != "0":
+        return c
+    return (*decode_tile(n, k, 4, bucket)[:2], 1)
 
 
 def residual_add_sumsq(resid: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:

@@ -609,3 +609,29 @@ def test_embed_sumsq_matches_gather_and_fp32_sumsq(dev, rows):
     ref = want.float().pow(2).sum(-1)
     torch.testing.assert_close(ssp[0, :rows], ref, rtol=1e-5, atol=1e-5)
     assert torch.all(ssp[0, rows:] == -1.0)  # rows past M untouched
+
+
+@pytest.mark.parametrize("n,k,wr,kc,sk,m", [(3584, 8192, 64, 256, 2, 32), (3584, 8192, 64, 256, 2, 7),
+                                           (2048, 1024, 64, 128, 4, 32), (2048, 1024, 128, 64, 2, 1)])
+def test_gate_up_split_k_silu_matches_full_k(dev, n, k, wr, kc, sk, m):
+    """Mode 6 (the norm-scaled SiLU gate/up with K split over sk workgroups, fp32 partial slabs, last-arriver
+    finish) against mode 4 (one pass) and an fp32 reference; the tickets are re-armed for the next launch."""
+    w = (torch.randn(2 * n, k, device=dev) * 0.02).to(torch.bfloat16)
+    x = torch.randn(m, k, device=dev).to(torch.bfloat16)
+    ssp = (torch.rand(3, ops.SSP_LD, device=dev) * k * 0.1).float()
+    wt = ops.gd_pack_weights(w, wr, silu=True, kc=kc)
+    slab = torch.empty(sk * m * 2 * n, dtype=torch.float32, device=dev)
+    cnt = torch.zeros(n // (wr // 2), dtype=torch.int32, device=dev)
+    got = ops.linear_silu_mul_rownorm(x, wt, ssp, 1e-5, wr, tiled=True, kc=kc, sk=sk, slab=slab, counters=cnt)
+    again = ops.linear_silu_mul_rownorm(x, wt, ssp, 1e-5, wr, tiled=True, kc=kc, sk=sk, slab=slab, counters=cnt)
+    one = ops.linear_silu_mul_rownorm(x, wt, ssp, 1e-5, wr, tiled=True, kc=kc)
+    torch.cuda.synchronize()
+    assert int(cnt.abs().sum()) == 0
+    assert torch.equal(got, again)  # deterministic (slices summed in slice order)
+    r = torch.rsqrt(ssp[:, :m].sum(0) / k + 1e-5)[:, None]
+    y = (x.float() @ w.float().t()) * r
+    ref = torch.nn.functional.silu(y[:, :n]) * y[:, n:]
+    for out in (got, one):
+        err = float((out.float() - ref).norm() / ref.norm())
+        assert err < 1e-2, err
+    assert float((got.float() - one.float()).norm() / one.float().norm()) < 5e-3
