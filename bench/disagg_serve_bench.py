@@ -32,7 +32,8 @@ def spawn(args, role, extra):
     cmd = [sys.executable, "-m", "src.worker", "--worker-id", f"{role}-w", "--host", "127.0.0.1", "--port", "0",
            "--port-file", pf, "--model", "llama", "--arch", "llama", "--preset", args.preset, "--role", role,
            "--max-batch-size", str(args.batch), "--max-model-len", "1024", "--num-kv-blocks", str(args.kv_blocks),
-           "--max-latency-ms", "10"] + extra
+           "--max-latency-ms", "10",
+           "--device", args.prefill_device if role == "prefill" else args.decode_device] + extra
     log = open(f"{args.log_dir}/disagg_{role}.log", "w")
     proc = subprocess.Popen(cmd, cwd=ROOT, stdout=log, stderr=subprocess.STDOUT)
     t0 = time.time()
@@ -70,14 +71,20 @@ async def run(args, pport, dport):
     lat = sorted(x[0] * 1e3 for x in res)
     ttft = sorted(x[1] for x in res if x[1] is not None)
     st = await InferenceClient(f"127.0.0.1:{dport}").call({"op": "engine_stats", "model": "llama"})
+    link = (await c.call({"op": "engine_stats", "model": "llama"}))["stats"].get("kv_link") or {}
     c.close()
+    # the point of config 3 is that the KV never crosses the socket: a silent fallback to bytes is a failure
+    if link.get("wire_packets", 0) or not link.get("ipc"):
+        raise SystemExit(f"disaggregation fell back to the RPC byte path: {link}")
     return {"bench": "disagg_two_process", "preset": args.preset, "req_per_s": round(len(res) / el, 2),
             "p50_latency_ms": round(statistics.median(lat), 1), "p99_latency_ms": round(lat[int(0.99 * len(lat)) - 1], 1),
             "ttft_p50_ms": round(statistics.median(ttft), 1) if ttft else None,
             "ttft_p99_ms": round(ttft[int(0.99 * len(ttft)) - 1], 1) if ttft else None,
             "batch": args.batch, "waves": args.steps, "prompt_len": args.prompt_len, "gen_len": args.gen_len,
             "kv_zone": st.get("stats", {}).get("kv_zone"), "kv_copy": os.environ.get("DIE_KV_COPY", "shader"),
-            "kv_path": "staged" if os.environ.get("DIE_KV_DIRECT", "1") == "0" else "direct-gather"}
+            "kv_link": link, "kv_path": link.get("kv_path"),
+            "zone_uncached": os.environ.get("DIE_KV_ZONE_UNCACHED", "1") == "1",
+            "devices": {"prefill": args.prefill_device, "decode": args.decode_device}}
 
 
 def main():
@@ -90,6 +97,8 @@ def main():
     ap.add_argument("--gen-len", type=int, default=128)
     ap.add_argument("--kv-blocks", type=int, default=16384)
     ap.add_argument("--log-dir", default="/tmp")
+    ap.add_argument("--prefill-device", default="cuda:0")
+    ap.add_argument("--decode-device", default="cuda:0", help="cuda:1 on a multi-GPU node: the KV rides xGMI")
     args = ap.parse_args()
     dproc, dport = spawn(args, "decode", [])
     try:

@@ -778,7 +778,9 @@ void car_all_reduce(Tensor in, Tensor out, int64_t rank, std::vector<int64_t> bu
 
 }  // namespace
 
-// Persistent decode step (decode_persistent.hip): the instantiation's tiles and workspace layout for a shape.
+#ifdef DIE_KERNEL_DIAG
+// Persistent decode step (decode_persistent.hip; diagnostics build only — measured slower than the five-launch
+// layer, docs/performance.md): the instantiation's tiles and workspace layout for a shape.
 std::vector<int64_t> decode_persistent_config(int64_t H, int64_t I, int64_t hq, int64_t hkv, int64_t layers) {
   int cfg[7];
   int64_t lay[9];
@@ -861,6 +863,7 @@ void decode_persistent(Tensor ws, Tensor table, Tensor h, Tensor ssp0, Tensor bl
   }
   DIE_HIP(die::launch_decode_persistent(a, cur_stream()));
 }
+#endif  // DIE_KERNEL_DIAG
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "Hand-written gfx950 (MI355X) HIP kernels";
@@ -871,8 +874,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_prefill", &attn_prefill);
   m.def("attn_decode", &attn_decode);
   m.def("attn_decode_fused", &attn_decode_fused);
+#ifdef DIE_KERNEL_DIAG
   m.def("decode_persistent_config", &decode_persistent_config);
   m.def("decode_persistent", &decode_persistent);
+#endif
   m.def("decode_partials", &decode_partials);
   m.def("sample", &sample, py::arg("out"), py::arg("logits"), py::arg("temperature") = py::none(),
         py::arg("top_k") = py::none(), py::arg("top_p") = py::none(), py::arg("seeds") = py::none(),

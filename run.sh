@@ -6,6 +6,8 @@
 #   ARCH=llama PRESET=llama3-8b GPUS=8 ./run.sh      # one Llama-3-8B replica per MI355X
 #   ARCH=llama PRESET=llama3-70b TP=8 ./run.sh       # one TP=8 group (torchrun) as one worker
 #   DISAGG=1 ARCH=llama PRESET=llama3-8b ./run.sh    # prefill worker on GPU0 -> decode worker on GPU1
+#     (PREFILL_GPU / DECODE_GPU pick the ordinals; both workers see every GPU and select theirs with --device,
+#      so the prefill process can map the decode GPU's landing zone and write it over xGMI)
 set -euo pipefail
 cd "$(dirname "$0")"
 ARCH=${ARCH:-mock}
@@ -28,10 +30,12 @@ python -m src.coordinator --listen-port "$PORT" --strategy "$STRATEGY" > "$LOGDI
 pids+=($!)
 
 if [ "${DISAGG:-0}" = 1 ]; then
-  HIP_VISIBLE_DEVICES=1 python -m src.worker --worker-id decode0 --port $((PORT + 2)) --model "$MODEL" \
+  PREFILL_GPU=${PREFILL_GPU:-0}
+  DECODE_GPU=${DECODE_GPU:-1}
+  python -m src.worker --worker-id decode0 --port $((PORT + 2)) --model "$MODEL" --device "cuda:$DECODE_GPU" \
       --arch "$ARCH" --preset "$PRESET" --role decode > "$LOGDIR/decode0.log" 2>&1 &
   pids+=($!)
-  HIP_VISIBLE_DEVICES=0 python -m src.worker --worker-id prefill0 --port $((PORT + 1)) --model "$MODEL" \
+  python -m src.worker --worker-id prefill0 --port $((PORT + 1)) --model "$MODEL" --device "cuda:$PREFILL_GPU" \
       --arch "$ARCH" --preset "$PRESET" --role prefill --decode-worker 127.0.0.1:$((PORT + 2)) \
       --coordinator 127.0.0.1:$PORT > "$LOGDIR/prefill0.log" 2>&1 &
   pids+=($!)

@@ -27,8 +27,10 @@ EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 ARCH = os.environ.get("DIE_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-KERNELS = ["norm_act", "rope_cache", "attention", "sampling", "moe", "gemm_decode", "decode_step", "allreduce",
-           "decode_persistent"]
+KERNELS = ["norm_act", "rope_cache", "attention", "sampling", "moe", "gemm_decode", "decode_step", "allreduce"]
+# kernels the serving path does not use, compiled into the diagnostics build only: the persistent decode step
+# (one launch per step) measured 0.70-0.77x of the five-launch layer (docs/performance.md, round 3)
+DIAG_KERNELS = ["decode_persistent"]
 CONTRACT_ON = {"attention", "gemm_decode", "decode_persistent"}
 
 
@@ -67,7 +69,7 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
     incs, torch_lib, abi = _torch_paths()
     jobs_list = []
     objs = []
-    for k in KERNELS:
+    for k in KERNELS + (DIAG_KERNELS if is_diag else []):
         src = os.path.join(kdir, k + ".hip")
         obj = os.path.join(OBJ, k + (".diag.o" if is_diag else ".o"))
         objs.append(obj)
@@ -79,10 +81,11 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
             jobs_list.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *diag, *contract, "-I",
                               CSRC, "-c", src, "-o", obj])
     bsrc = os.path.join(CSRC, "bindings.cpp")
-    bobj = os.path.join(OBJ, "bindings.o")
+    bobj = os.path.join(OBJ, "bindings.diag.o" if is_diag else "bindings.o")
     objs.append(bobj)
     if force or _newer(bobj, [bsrc] + hdrs):
-        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__=1",
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", *(["-DDIE_KERNEL_DIAG"] if is_diag else []),
+               f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__=1",
                "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
                "-I", CSRC, "-I", "/opt/rocm/include", "-I", sysconfig.get_paths()["include"]]
         for i in incs:
@@ -93,7 +96,7 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
         for res in ex.map(_run, jobs_list):
             if verbose and res:
                 print(res)
-    if force or _newer(out, objs):
+    if force or _newer(out, objs + [os.path.abspath(__file__)]):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out,
               "-L", torch_lib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
               f"-Wl,-rpath,{torch_lib}"])

@@ -162,6 +162,13 @@ class AsyncLLMEngine:
     def _loop(self) -> None:
         eng = self.engine
         try:
+            if eng.device.type == "cuda":
+                # the current device is per thread: the kernels' bindings launch on the current device's
+                # current stream, so a worker serving cuda:N (run.sh DISAGG exposes every GPU to every
+                # worker) must select it on this thread too
+                import torch
+
+                torch.cuda.set_device(eng.device)
             while not self._stop.is_set():
                 self._drain()
                 if not eng.has_work():

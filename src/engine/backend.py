@@ -53,6 +53,9 @@ class LLMBackend:
         device = config.overrides.get("device") if config.overrides else None
         if device is None:
             device = "cuda:0" if torch.cuda.is_available() else "cpu"
+        if str(device).startswith("cuda"):
+            # model build, weight packing and graph capture run on this thread: on the serving GPU
+            torch.cuda.set_device(torch.device(device))
         if engine is None:
             from src.models.loader import is_hf_checkpoint
 
@@ -150,13 +153,19 @@ class LLMBackend:
 
     async def predict_stream(self, inputs: Any, emit, request_id: Optional[str] = None) -> Dict[str, Any]:
         """Streaming generation: ``await emit({"delta_token_ids": [...], "done": False})`` as tokens are
-        produced (bursts of up to ``decode_window`` per host round trip), then return the final output.
-        If ``emit`` fails (client gone) the request is aborted."""
+        produced, then return the final output. If ``emit`` fails (client gone) the request is aborted.
+
+        The first token (the prefill's) always goes out ALONE, as soon as it reaches the event loop — TTFT
+        is what a streaming client is for, and it must not depend on how far the engine thread has run
+        ahead (a small model can finish the whole generation before this coroutine first wakes: coalescing
+        everything queued would then send one frame for the whole request). Later tokens are coalesced per
+        wake-up (bursts of up to ``decode_window`` per host round trip)."""
         q: asyncio.Queue = asyncio.Queue()
         task = asyncio.ensure_future(self.predict(inputs, request_id, on_token=q.put_nowait))
         with_text = not isinstance(inputs, dict) or bool(inputs.get("return_text", True))
         so_far: List[int] = []
         text_sent = 0
+        first = True
 
         async def send(toks: List[int]) -> None:
             nonlocal text_sent
@@ -178,8 +187,9 @@ class LLMBackend:
                     get.cancel()
                     break
                 toks = [get.result()]
-                while not q.empty():
+                while not first and not q.empty():
                     toks.append(q.get_nowait())
+                first = False
                 await send(toks)
             toks = []
             while not q.empty():  # tokens delivered before the completion callback ran
@@ -205,30 +215,35 @@ class LLMBackend:
         from src.engine.disagg import sampling_to_dict
         from src.parallel.kv_transfer import KVPacket
 
-        # reserve the decode worker's landing-zone slot first: the prefill engine's export then gathers the
-        # prompt's blocks straight into it (one pass over xGMI, no staging tensor, no second copy)
+        # try to reserve the decode worker's landing-zone slot first (no waiting: a full zone must not hold the
+        # prompt out of the prefill queue): the prefill engine's export then gathers the prompt's blocks
+        # straight into it (one pass over xGMI, no staging tensor, no second copy). Otherwise the packet takes
+        # the staged path, whose reserve may wait for space AFTER the prompt has run.
         slot = None
         if self.engine.device.type == "cuda" and os.environ.get("DIE_KV_DIRECT", "1") == "1":
             from src.parallel.kv_transfer import packet_shape
 
             nb = self.engine.blocks.blocks_needed(len(gi.prompt_token_ids))
-            slot = await self._decode_link.reserve(self.engine.device, packet_shape(self.engine.pool.planes(), nb))
+            slot = await self._decode_link.reserve_export(self.engine.device,
+                                                          packet_shape(self.engine.pool.planes(), nb))
         ud = {"export_kv": True}
         if slot is not None:
-            ud["export_dst"] = slot["dst"]
+            ud["export_slot"] = slot
         try:
             pseq = await self.async_engine.submit(rid, gi.prompt_token_ids, gi.sampling, user_data=ud)
         except BaseException:
+            # a cancelled await does not stop the prompt by itself: abort it, and give the slot back as soon as
+            # no gather can still write into it (at once if none was queued, else behind its event)
+            self.async_engine.abort(rid)
             if slot is not None:
-                # a cancelled await does not stop the prompt: revoke the destination (the engine reads it when
-                # it exports; this dict is the one it holds) and leave the slot to the decode worker's
-                # reservation TTL — releasing it now could hand it to another sender while a gather that read
-                # the destination just before the revocation still writes into it
-                ud["export_dst"] = None
+                self._decode_link.revoke(slot)
             raise
+        if slot is not None and slot.state != "taken":  # past the reservation's deadline: staged path
+            self._decode_link.revoke(slot)
+            slot = None
         if pseq.finish_reason == "stop":
             if slot is not None:
-                await self._decode_link.abandon(slot, getattr(pseq, "kv_export_ready", None))
+                self._decode_link.revoke(slot)
             return build_llm_output(pseq.output_ids, self.tokenizer, prompt_len=pseq.prompt_len,
                                     finish_reason="stop", ttft_ms=pseq.ttft_ms(), latency_ms=pseq.latency_ms(),
                                     return_text=gi.return_text)
@@ -237,7 +252,7 @@ class LLMBackend:
                           ready=getattr(pseq, "kv_export_ready", None))
         pseq.kv_export = None
         if slot is not None:
-            rep = await self._decode_link.send_reserved(packet, slot)
+            rep = await self._decode_link.send_reserved(packet, slot.res)
         else:
             rep = await self._decode_link.send(packet)
         if not rep.get("success"):
@@ -254,7 +269,7 @@ class LLMBackend:
             cap = int((self.config.overrides or {}).get("kv_landing_zone_bytes",
                                                          os.environ.get("DIE_KV_ZONE_BYTES", 4 << 30)))
             self._zone = IPCLandingZone(self.engine.device, cap,
-                                        uncached=os.environ.get("DIE_KV_ZONE_UNCACHED", "0") == "1")
+                                        uncached=os.environ.get("DIE_KV_ZONE_UNCACHED", "1") == "1")
         return self._zone
 
     async def _kv_import(self, msg: Dict[str, Any]) -> Dict[str, Any]:
@@ -300,6 +315,8 @@ class LLMBackend:
     async def handle_op(self, op: str, msg: Dict[str, Any]) -> Dict[str, Any]:
         if op == "engine_stats":
             st = self.async_engine.stats()
+            if self._decode_link is not None:
+                st["kv_link"] = self._decode_link.stats()
             if self._zone is not None:
                 z = self._zone
                 z._reap()
@@ -324,7 +341,7 @@ class LLMBackend:
             while off is None and time.monotonic() < deadline:
                 await asyncio.sleep(0.0005)
                 off = zone.reserve(n)
-            return {"success": off is not None, "offset": off,
+            return {"success": off is not None, "offset": off, "ttl_s": zone.reserve_ttl_s,
                     "gen": zone.generation(off) if off is not None else None}
         if op == "kv_release":  # a sender gave up on a reserved slot (copy or kv_import failed)
             return {"success": self._landing_zone().release(int(msg["offset"]), msg.get("gen"))}
@@ -338,6 +355,8 @@ class LLMBackend:
             "avg_latency": self.total_latency / self.request_count if self.request_count else 0.0,
             "engine": self.engine.get_stats(),
         }
+        if self._decode_link is not None:  # disaggregated prefill: how the prompt KV has travelled
+            m["kv_link"] = self._decode_link.stats()
         if self.engine.device.type == "cuda":
             free, total = torch.cuda.mem_get_info(self.engine.device)
             m["hbm_used_gib"] = (total - free) / 2**30

@@ -25,7 +25,7 @@ from typing import Any, Dict, List, Optional
 
 from src.engine.async_engine import AsyncLLMEngine
 from src.engine.sequence import Sequence
-from src.parallel.kv_transfer import KVPacket, packet_from_wire, packet_meta, packet_to_wire, ship
+from src.parallel.kv_transfer import ExportSlot, KVPacket, packet_from_wire, packet_meta, packet_to_wire, ship
 from src.preproc import SamplingParams
 from src.rpc import RPCClient
 
@@ -96,7 +96,28 @@ class RemoteDecodeLink:
         self._ipc_lock = asyncio.Lock()
         self.ipc_packets = 0
         self.direct_packets = 0   # gathered by the prefill engine straight into a reserved slot
+        self.staged_packets = 0   # gathered locally, then copied into a slot (zone full at submit / deadline)
         self.wire_packets = 0
+        self._tasks: set = set()  # background releases: held here (the loop keeps only weak references)
+
+    # seconds kept between the local deadline of a direct export and the decode worker's reservation TTL
+    DEADLINE_MARGIN_S = 5.0
+
+    def _spawn(self, coro) -> None:
+        t = asyncio.ensure_future(coro)
+        self._tasks.add(t)
+        t.add_done_callback(self._tasks.discard)
+
+    @property
+    def kv_path(self) -> str:
+        """How packets have travelled so far: direct / staged / wire (or mixed, e.g. "direct+staged")."""
+        parts = [n for n, c in (("direct", self.direct_packets), ("staged", self.staged_packets),
+                                ("wire", self.wire_packets)) if c]
+        return "+".join(parts) or "none"
+
+    def stats(self) -> Dict[str, Any]:
+        return {"kv_path": self.kv_path, "direct_packets": self.direct_packets, "staged_packets": self.staged_packets,
+                "wire_packets": self.wire_packets, "ipc": self._ipc is not None, "decode_worker": self.address}
 
     async def _channel(self, device):
         if self._ipc is not None or not self.use_ipc or device.type != "cuda":
@@ -124,10 +145,10 @@ class RemoteDecodeLink:
                 self.use_ipc = False
         return self._ipc
 
-    async def reserve(self, device, shape: List[int]) -> Optional[Dict[str, Any]]:
-        """Reserve a landing-zone slot for a packet of ``shape`` BEFORE its prompt runs: returns
-        ``{"offset", "gen", "dst"}`` (``dst`` a bf16 view of the slot for the prefill engine's gather to
-        write into), or None (no IPC channel / zone full: the packet then takes the staged path)."""
+    async def reserve(self, device, shape: List[int], wait_s: Optional[float] = None) -> Optional[Dict[str, Any]]:
+        """Reserve a landing-zone slot for a packet of ``shape``: returns ``{"offset", "gen", "dst", "ttl_s"}``
+        (``dst`` a bf16 view of the slot for the prefill engine's gather to write into), or None (no IPC
+        channel / zone full). ``wait_s``: how long the decode worker may wait for space (default: none)."""
         ch = await self._channel(device)
         if ch is None:
             return None
@@ -135,7 +156,7 @@ class RemoteDecodeLink:
         for d in shape:
             nbytes *= int(d)
         rep = await self.rpc.call(self.address, {"op": "kv_reserve", "model": self.model, "nbytes": nbytes,
-                                                 "wait_s": self.reserve_wait_s}, self.timeout)
+                                                 "wait_s": wait_s or 0.0}, self.timeout)
         if not rep.get("success"):
             return None
         try:
@@ -143,7 +164,28 @@ class RemoteDecodeLink:
         except ValueError:
             await self._release(rep["offset"], rep.get("gen"))
             return None
-        return {"offset": rep["offset"], "gen": rep.get("gen"), "dst": dst}
+        return {"offset": rep["offset"], "gen": rep.get("gen"), "dst": dst, "ttl_s": rep.get("ttl_s", 120.0)}
+
+    async def reserve_export(self, device, shape: List[int]) -> Optional[ExportSlot]:
+        """A slot for the prefill engine to gather into, reserved BEFORE the prompt runs and without waiting
+        (a full zone must not keep prompts out of the prefill queue: they take the staged path instead). The
+        slot's local deadline is taken before the RPC, so it ends before the decode worker's TTL can."""
+        t0 = time.monotonic()
+        res = await self.reserve(device, shape)
+        if res is None:
+            return None
+        return ExportSlot(res, t0 + float(res["ttl_s"]) - self.DEADLINE_MARGIN_S)
+
+    def revoke(self, slot: ExportSlot) -> None:
+        """Give an export slot back (cancelled request, stop token, deadline passed): at once when no gather
+        was queued into it, else once that gather's event has completed — a later owner of the slot is never
+        overwritten."""
+        st, ev = slot.revoke()
+        off, gen = slot.res["offset"], slot.res["gen"]
+        if st == "taken" and ev is not None and not ev.query():
+            self._spawn(self._release_after_copy(off, gen, ev))
+        else:
+            self._spawn(self._release(off, gen))
 
     async def send_reserved(self, packet: KVPacket, slot: Dict[str, Any]) -> Dict[str, Any]:
         """The packet's KV was gathered straight into ``slot`` (see :meth:`reserve`): wait for that gather
@@ -168,7 +210,7 @@ class RemoteDecodeLink:
         """Give a reserved slot back (the prompt failed or was cancelled): once ``ready`` (the gather into
         it, if one was issued) has completed, so no later owner of the slot is overwritten."""
         if ready is not None and not ready.query():
-            asyncio.ensure_future(self._release_after_copy(slot["offset"], slot["gen"], ready))
+            self._spawn(self._release_after_copy(slot["offset"], slot["gen"], ready))
         else:
             await self._release(slot["offset"], slot["gen"])
 
@@ -181,6 +223,7 @@ class RemoteDecodeLink:
                                                      "nbytes": packet.nbytes, "wait_s": self.reserve_wait_s},
                                       self.timeout)
             if rep.get("success"):
+                self.staged_packets += 1
                 off, gen = rep["offset"], rep.get("gen")
                 imported = False
                 issued: Dict[str, Any] = {}
@@ -199,7 +242,7 @@ class RemoteDecodeLink:
                         if ev is not None and not ev.query():
                             # cancelled while the copy still writes into the slot: release it only once the
                             # copy has finished, or another sender could get the slot and be overwritten
-                            asyncio.ensure_future(self._release_after_copy(off, gen, ev))
+                            self._spawn(self._release_after_copy(off, gen, ev))
                         else:
                             await self._release(off, gen)
                     raise

@@ -362,14 +362,24 @@ class LLMEngine:
                 from src.parallel.kv_transfer import export_blocks
 
                 nb = self.blocks.blocks_needed(seq.prompt_len)
-                # export_dst: a slot of the decode worker's landing zone reserved before the prompt ran (the
-                # gather writes straight into it); else a local staging tensor
+                planes, ids = self.pool.planes(), seq.block_table[:nb]
+
+                def gather(dst):
+                    buf = export_blocks(planes, ids, out=dst)
+                    ev = None
+                    if buf.is_cuda:  # consumers wait on this instead of a host sync
+                        ev = torch.cuda.Event()
+                        ev.record()
+                    return buf, ev
+
+                # export_slot: a slot of the decode worker's landing zone reserved before the prompt ran (the
+                # gather writes straight into it, unless the reservation is past its deadline or revoked);
+                # else a local staging tensor
                 ud = seq.user_data if isinstance(seq.user_data, dict) else {}
-                seq.kv_export = export_blocks(self.pool.planes(), seq.block_table[:nb],  # type: ignore[attr-defined]
-                                              out=ud.get("export_dst"))
-                if seq.kv_export.is_cuda:  # consumers wait on this instead of a host sync
-                    ev = torch.cuda.Event()
-                    ev.record()
+                slot = ud.get("export_slot")
+                buf, ev = slot.gather(gather) if slot is not None else gather(None)
+                seq.kv_export = buf  # type: ignore[attr-defined]
+                if ev is not None:
                     seq.kv_export_ready = ev  # type: ignore[attr-defined]
             self.scheduler.finish(seq, reason)
             finished.append(seq)

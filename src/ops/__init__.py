@@ -157,8 +157,10 @@ def attn_decode_fused(qkv_slab: torch.Tensor, ssp: torch.Tensor, positions: torc
 
 def decode_persistent_config(hidden: int, inter: int, hq: int, hkv: int, layers: int) -> Optional[dict]:
     """Tiles and workspace layout of the persistent decode-step kernel (csrc/kernels/decode_persistent.hip) for
-    a model shape, or None when it has no instantiation."""
-    if _C is None:
+    a model shape, or None when it has no instantiation. The kernel is compiled into the diagnostics build only
+    (``DIE_KERNEL_DIAG=1 python -m src._build``, loaded with ``DIE_C_DIAG=1``): it measured 0.70-0.77x of the
+    five-launch layer, so the release ``_C`` carries only kernels the serving path runs."""
+    if _C is None or not hasattr(_C, "decode_persistent_config"):
         return None
     v = list(_C.decode_persistent_config(hidden, inter, hq, hkv, layers))
     if not v:

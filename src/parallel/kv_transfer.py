@@ -51,6 +51,48 @@ class KVPacket:
         return self.kv.numel() * self.kv.element_size()
 
 
+class ExportSlot:
+    """A decode worker's landing-zone slot, reserved before a prompt runs, that the prefill engine may gather
+    the prompt's KV straight into — the hand-over between the event-loop thread (which reserved it and may
+    revoke it) and the engine thread (which takes it when the prompt finishes). Thread-safe.
+
+    The decode worker expires an un-imported reservation after its TTL and may then give the offset to another
+    sender; a gather issued after that would overwrite the new owner's KV. So the slot carries a local
+    ``deadline`` (reserve time on THIS side, taken before the reserve RPC, + the decode worker's TTL − a
+    margin): past it the engine gathers into a local staging tensor instead, and the packet takes the staged
+    path. States: ``open`` → ``taken`` (a gather into it was queued; ``event`` marks its completion) or
+    ``expired`` (the deadline passed first) or ``revoked`` (the request was cancelled first)."""
+
+    def __init__(self, reservation: Dict[str, Any], deadline: float):
+        self.res = reservation            # {"offset", "gen", "dst"} from RemoteDecodeLink.reserve
+        self.deadline = deadline          # time.monotonic() on this process
+        self.state = "open"
+        self.event = None
+        self._lock = threading.Lock()
+
+    def gather(self, fn: Callable[[Optional[torch.Tensor]], Any]):
+        """Engine thread: ``fn(dst)`` queues the gather (into the slot, or into a fresh staging tensor when
+        ``dst`` is None) and returns ``(tensor, event)``. The state changes under the lock, together with
+        the issue, so a concurrent :meth:`revoke` sees either no gather or a gather with its event."""
+        with self._lock:
+            if self.state == "open" and time.monotonic() < self.deadline:
+                out, ev = fn(self.res["dst"])
+                self.state, self.event = "taken", ev
+                return out, ev
+            if self.state == "open":
+                self.state = "expired"
+        return fn(None)
+
+    def revoke(self):
+        """Event-loop thread: no gather may start after this. Returns ``(state, event)`` as they were: the
+        slot is free to release at once unless a gather was queued (``taken``: release after ``event``)."""
+        with self._lock:
+            st = self.state
+            if st == "open":
+                self.state = "revoked"
+            return st, self.event
+
+
 def export_blocks(pool_planes: torch.Tensor, block_ids: List[int], out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Gather ``block_ids`` of every (layer, K/V) plane into a staging tensor, or into ``out`` (e.g. a
     peer's IPC landing-zone slot: the gather then writes straight over xGMI, no second copy)."""

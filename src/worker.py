@@ -86,6 +86,8 @@ class Worker:
         self._probe_count = 0
         self._active = 0
         self._conns: set = set()
+        self._bg: set = set()      # background tasks (signal shutdown): held so they are not collected
+        self._waiters = 0
         self._tracer = GLOBAL_TRACER
         self._process = psutil.Process()
 
@@ -95,7 +97,7 @@ class Worker:
         if self.install_signal_handlers:
             for sig in (signal.SIGTERM, signal.SIGINT):
                 with contextlib.suppress(NotImplementedError, RuntimeError, ValueError):
-                    loop.add_signal_handler(sig, lambda s=sig: asyncio.create_task(self.shutdown(s)))
+                    loop.add_signal_handler(sig, self._on_signal, sig)
         for m in self.models.values():
             if hasattr(m, "start"):
                 await m.start()
@@ -136,6 +138,13 @@ class Worker:
         finally:
             client.close()
 
+    def _on_signal(self, sig) -> None:
+        t = asyncio.get_running_loop().create_task(self.shutdown(sig))
+        self._bg.add(t)
+        # a SystemExit raised by shutdown() leaves the loop anyway: retrieve it on the task too, so asyncio
+        # does not log "Task exception was never retrieved" at exit (round 3's SIGTERM noise)
+        t.add_done_callback(lambda t: (self._bg.discard(t), t.cancelled() or t.exception()))
+
     async def shutdown(self, sig=None) -> None:
         if sig:
             logger.info("Received signal %s, shutting down", getattr(sig, "name", sig))
@@ -154,18 +163,25 @@ class Worker:
                     await m.stop()
             self.unload_model(name)
         self._stop_event.set()
-        if sig:
+        if sig and not self._waiters:
+            # the reference exits the process on a signal (`/root/reference/src/worker.py:80-82`); a caller
+            # that awaits wait_closed() (our main) returns normally instead
             sys.exit(0)
 
     async def wait_closed(self) -> None:
-        await self._stop_event.wait()
+        self._waiters += 1
+        try:
+            await self._stop_event.wait()
+        finally:
+            self._waiters -= 1
 
     # -------------------------------------------------------------- network
     IDLE_TIMEOUT_S = 3600.0
 
     async def _handle_connection(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
         self._conns.add(writer)
-        # an idle connection is dropped after IDLE_TIMEOUT_S by ONE timer re-armed per request (asyncio.wait_for
+        # an idle connection is dropped after IDLE_TIMEOUT_S by ONE timer, stopped while a request is being
+        # served (a long streamed generation is not idle) and re-armed once its reply is written (asyncio.wait_for
         # around every read cost a task + a timer per request: the mock worker's largest per-request cost)
         loop = asyncio.get_running_loop()
         idle = [loop.call_later(self.IDLE_TIMEOUT_S, writer.transport.abort)]
@@ -182,7 +198,6 @@ class Worker:
                         await writer.drain()
                     break
                 idle[0].cancel()
-                idle[0] = loop.call_later(self.IDLE_TIMEOUT_S, writer.transport.abort)
                 if mode == "eof":
                     break  # TCP-connect probe: not a request
                 t0 = time.perf_counter()
@@ -203,6 +218,7 @@ class Worker:
                     await writer.drain()
                 except ConnectionError:  # the client went away (e.g. a dropped stream)
                     break
+                idle[0] = loop.call_later(self.IDLE_TIMEOUT_S, writer.transport.abort)
                 logger.debug("request done in %.2f ms", (time.perf_counter() - t0) * 1e3)
         finally:
             idle[0].cancel()

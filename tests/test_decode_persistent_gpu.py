@@ -11,11 +11,16 @@ import os
 import pytest
 import torch
 
-pytestmark = pytest.mark.gpu
-
-os.environ["DIE_PERSISTENT"] = "1"
-
 from src import ops  # noqa: E402
+
+# the persistent step is compiled into the diagnostics build only (round 4: it loses to the five-launch layer,
+# so the release _C does not carry it); run this file with DIE_C_DIAG=1 after `DIE_KERNEL_DIAG=1 python -m src._build`
+_HAVE = ops.native_available() and hasattr(ops._C, "decode_persistent")
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not _HAVE, reason="persistent decode step: diagnostics build only (DIE_C_DIAG=1)")]
+
+if _HAVE:
+    os.environ["DIE_PERSISTENT"] = "1"
 from src.models.llama import AttnMetadata, CausalLM  # noqa: E402
 from src.models.presets import get_preset  # noqa: E402
 

@@ -68,3 +68,62 @@ def test_segments_slots_never_span_and_free_lists_stay_per_segment():
     z2._init_book(120.0)
     offs = [z2.reserve(64 << 20) for _ in range(32)]
     assert None not in offs and len(set(offs)) == 32 and z2.reserve(2 << 30) is None
+
+
+def test_export_slot_deadline_and_revocation():
+    """a direct-export slot whose reservation may have expired on the decode side is never
+    gathered into (the prompt queued / ran past the local deadline: staging tensor instead), and a revoked
+    slot is never gathered into either; a slot revoked after its gather was queued reports the gather's
+    event, so the sender releases it only behind that event."""
+    from src.parallel.kv_transfer import ExportSlot
+
+    calls = []
+
+    def gather(dst):
+        calls.append(dst)
+        return ("slot" if dst is not None else "staging"), ("ev" if dst is not None else None)
+
+    res = {"offset": 0, "gen": 1, "dst": "DST"}
+    s = ExportSlot(res, deadline=time.monotonic() + 60)
+    assert s.gather(gather) == ("slot", "ev") and s.state == "taken"
+    assert s.revoke() == ("taken", "ev")
+    s = ExportSlot(res, deadline=time.monotonic() - 1)       # past its deadline
+    assert s.gather(gather) == ("staging", None) and s.state == "expired"
+    assert s.revoke() == ("expired", None)
+    s = ExportSlot(res, deadline=time.monotonic() + 60)
+    assert s.revoke() == ("open", None) and s.state == "revoked"   # released at once by the sender
+    assert s.gather(gather) == ("staging", None)
+    assert calls == ["DST", None, None]
+
+
+def test_remote_link_reserve_export_never_waits_and_revoke_releases():
+    """The direct path reserves with wait_s=0 (a full zone must not hold prompts out of prefill) and takes
+    its deadline from the decode worker's TTL; revoking an un-gathered slot releases it at once."""
+    import asyncio
+
+    from src.engine.disagg import RemoteDecodeLink
+
+    async def main():
+        link = RemoteDecodeLink("127.0.0.1:1", "m")
+        sent = []
+
+        class Ch:
+            def dst(self, off, shape):
+                return ("view", off)
+
+        class RPC:
+            async def call(self, addr, msg, timeout):
+                sent.append(msg)
+                if msg["op"] == "kv_reserve":
+                    return {"success": True, "offset": 4096, "gen": 7, "ttl_s": 30.0}
+                return {"success": True}
+
+        link._ipc, link.rpc = Ch(), RPC()
+        t0 = time.monotonic()
+        slot = await link.reserve_export(torch.device("cpu"), [2, 4, 8])
+        assert sent[0]["wait_s"] == 0.0 and sent[0]["nbytes"] == 2 * 2 * 4 * 8
+        assert t0 + 30.0 - link.DEADLINE_MARGIN_S <= slot.deadline <= time.monotonic() + 30.0
+        link.revoke(slot)
+        await asyncio.sleep(0.01)
+        assert sent[-1] == {"op": "kv_release", "model": "m", "offset": 4096, "gen": 7} and not link._tasks
+    asyncio.run(main())

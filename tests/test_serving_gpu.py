@@ -59,15 +59,18 @@ def test_gpu_streaming_matches_plain():
         plain = await asyncio.wait_for(cw.call({"op": "infer", "model": "mini", "inputs": req}), 300)
         assert plain["success"], plain
         for client in (cw, cc):
-            deltas, frames, final = [], 0, None
+            deltas, sizes, final = [], [], None
             async for fr in client.infer_stream("mini", req):
                 if fr.get("done") is False:
                     deltas += fr["delta_token_ids"]
-                    frames += 1
+                    if fr["delta_token_ids"]:
+                        sizes.append(len(fr["delta_token_ids"]))
                 else:
                     final = fr
             assert final["success"] and deltas == plain["outputs"]["token_ids"] == final["outputs"]["token_ids"]
-            assert frames >= 2
+            # the prefill's token travels alone, whatever the engine thread's lead over the event loop
+            # (round 3's driver box finished all 40 tokens before the loop's first wake-up: one frame)
+            assert sizes[0] == 1 and len(sizes) >= 2, sizes
         cw.close()
         cc.close()
         await coord.stop()

@@ -58,6 +58,37 @@ def test_stream_matches_plain_worker_and_coordinator():
     asyncio.run(main())
 
 
+def test_first_token_frame_never_coalesced():
+    """The engine thread may run the whole generation before the event loop first wakes (a fast model:
+    round 3's GPU driver run saw ONE frame for 40 tokens). Simulated here by a predict() that delivers
+    every token synchronously before returning: the prefill's token still goes out alone, first."""
+    from src.engine.backend import LLMBackend
+    from src.preproc import ByteTokenizer
+
+    be = object.__new__(LLMBackend)
+    be.tokenizer = ByteTokenizer()
+    toks = list(range(300, 340))
+
+    async def predict(inputs, request_id=None, on_token=None):
+        for t in toks:
+            on_token(t)
+        return {"token_ids": toks, "text": be.tokenizer.decode(toks)}
+
+    be.predict = predict
+
+    async def main():
+        frames = []
+
+        async def emit(fr):
+            frames.append(fr)
+        out = await be.predict_stream({"prompt_token_ids": [5], "max_tokens": 40}, emit)
+        sizes = [len(f["delta_token_ids"]) for f in frames if f["delta_token_ids"]]
+        assert sizes[0] == 1 and len(sizes) >= 2, sizes
+        assert sum((f["delta_token_ids"] for f in frames), []) == toks == out["token_ids"]
+        assert "".join(f.get("delta_text", "") for f in frames) == out["text"]
+    asyncio.run(main())
+
+
 def test_abort_timeout_and_client_disconnect():
     async def main():
         w = Worker("s1", host="127.0.0.1", install_signal_handlers=False)
