@@ -402,8 +402,9 @@ void attn_set_timestamps(Tensor t) {
   die::attn_set_timestamps(t.numel() ? reinterpret_cast<long long*>(t.data_ptr<int64_t>()) : nullptr);
 }
 
-void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t kc, int64_t sk, bool nt,
-                 Tensor resid, Tensor ssp_out, Tensor counters, Tensor ssp_in, double eps) {
+static void gemm_decode_impl(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t kc, int64_t sk,
+                             bool nt, Tensor resid, Tensor ssp_out, Tensor counters, Tensor ssp_in, double eps,
+                             die::GemmDecodeFuse fz) {
   DIE_CHECK_CUDA(x);
   DIE_CHECK_BF16(x);
   DIE_CHECK_BF16(w);
@@ -435,7 +436,6 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
   TORCH_CHECK(w.dim() == 2 && w.size(1) == K && w.size(0) == (silu ? 2 * N : N), "gemm_decode w shape");
   TORCH_CHECK(N % (silu ? wrr / 2 : wrr) == 0, "N not a multiple of the column tile");
   TORCH_CHECK((int64_t)sk * M * N * 4 < ((int64_t)1 << 31) || mode != 3, "slab too large");
-  die::GemmDecodeFuse fz;
   fz.ts = g_gd_ts;
   fz.tiled = tiled ? 1 : 0;
   if (mode == 3) {
@@ -478,6 +478,39 @@ void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t
   }
   DIE_HIP(die::launch_gemm_decode(y.data_ptr(), ldy, bf(x), x.stride(0), bf(w), (int)M, (int)N, (int)K, (int)mode,
                                   (int)wr, (int)kc, (int)sk, nt, fz, cur_stream()));
+}
+
+void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t kc, int64_t sk, bool nt,
+                 Tensor resid, Tensor ssp_out, Tensor counters, Tensor ssp_in, double eps) {
+  gemm_decode_impl(y, x, w, mode, wr, kc, sk, nt, resid, ssp_out, counters, ssp_in, eps, die::GemmDecodeFuse{});
+}
+
+// Tensor-parallel row-parallel projection in ONE launch (decode, mode 3): this rank's K-shard GEMM, the one-shot
+// all-reduce of each column tile with the group's peers (the CustomAllReduce's staging buffers, flag pages and
+// control words: bufs / sigs / ctl / cap as for car_all_reduce), the residual update and the next norm's per-tile
+// statistics. Every rank of the group must make the same call (same shapes, same tile plan).
+void gemm_decode_car(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t kc, int64_t sk, bool nt,
+                     Tensor resid, Tensor ssp_out, Tensor counters, int64_t rank, std::vector<int64_t> bufs,
+                     std::vector<int64_t> sigs, int64_t ctl, int64_t cap_elems) {
+  TORCH_CHECK((mode & 31) == 3, "gemm_decode_car: mode 3 (residual epilogue)");
+  const int world = (int)bufs.size();
+  TORCH_CHECK(world >= 2 && world <= die::CAR_MAX_RANKS && (int)sigs.size() == world, "2..8 ranks");
+  TORCH_CHECK(rank >= 0 && rank < world && ctl != 0, "bad rank / control word");
+  TORCH_CHECK(resid.dim() == 2 && x.size(0) * resid.size(1) <= cap_elems, "message larger than the staging half");
+  TORCH_CHECK(resid.size(1) / wr <= die::CAR_MAX_BLOCKS, "more column tiles than flag slots");
+  die::GemmDecodeFuse fz;
+  for (int p = 0; p < world; ++p) {
+    TORCH_CHECK(bufs[p] != 0 && sigs[p] != 0, "null peer pointer");
+    fz.car.buf[p] = reinterpret_cast<die::bf16_t*>(bufs[p]);
+    fz.car.sig[p] = reinterpret_cast<uint32_t*>(sigs[p]);
+  }
+  fz.car_world = world;
+  fz.car_rank = (int)rank;
+  fz.car_ctl = reinterpret_cast<uint32_t*>(ctl);
+  fz.car_cap = cap_elems;
+  fz.car_mode = die::car_mode();
+  fz.car_spin = die::car_spin_limit();
+  gemm_decode_impl(y, x, w, mode, wr, kc, sk, nt, resid, ssp_out, counters, x, 0.0, fz);
 }
 
 
@@ -889,6 +922,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_gather", &moe_gather);
   m.def("moe_combine", &moe_combine);
   m.def("gemm_decode", &gemm_decode);
+  m.def("gemm_decode_car", &gemm_decode_car);
   m.def("gd_set_timestamps", &gd_set_timestamps);
   m.def("attn_set_timestamps", &attn_set_timestamps);
   m.def("row_sumsq", &row_sumsq);

@@ -21,6 +21,7 @@
 // (its kernels are stream-ordered).
 // The epoch lives in device memory (the last workgroup to finish advances it), so the launch is
 // hipGraph-capturable and replays correctly.
+#include "car_common.h"
 #include "common.h"
 #include "launchers.h"
 
@@ -32,45 +33,7 @@ namespace die {
 
 namespace car {
 constexpr int NTH = 512;
-
-__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 }  // namespace car
-
-// Steps 2 + 3 of the protocol for one workgroup: lanes 0..world-1 (except this rank's) signal peer `tid`
-// and wait for its signal. The wait is bounded (`spin_limit` polls): a peer that never signals (dead, or
-// out of step after skipping a call) sets the sticky error word ctl[2] and s_fail, and the caller then
-// POISONS its output (NaN) instead of reducing stale peer buffers. Once ctl[2] is set, later calls do
-// not wait at all (fail fast): the group is broken as a unit, and the host raises an engine fault on
-// its next token readback (TPModelRunner._to_host).
-__device__ __forceinline__ void car_wait_peers(const CarPeers& peers, uint32_t* slots, uint32_t* ctl, uint32_t epoch,
-                                               int par, int b, int rank, int world, int tid, uint32_t spin_limit,
-                                               int& s_fail) {
-  using namespace car;
-  if (tid < world && tid != rank) {
-    st_sys(peers.sig[tid] + ((int64_t)par * CAR_MAX_BLOCKS + b) * CAR_MAX_RANKS + rank, epoch);
-    bool ok = __hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
-    uint32_t it = 0;
-    while (ok && ld_sys(slots + tid) != epoch) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++it > spin_limit) ok = false;
-    }
-    if (!ok) {
-      __hip_atomic_store(ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_fail = 1;
-    }
-  }
-  __syncthreads();
-}
-
-__device__ __forceinline__ uint4 car_nan8() {
-  const uint32_t n = 0x7fc07fc0u;  // two bf16 quiet NaNs
-  return make_uint4(n, n, n, n);
-}
 
 __global__ void __launch_bounds__(car::NTH) custom_all_reduce_kernel(const bf16_t* __restrict__ in,
                                                                      bf16_t* __restrict__ out, int64_t nvec,
@@ -234,13 +197,18 @@ __global__ void __launch_bounds__(car::NTH) custom_all_reduce_residual_kernel(
 
 // Polls of a peer's flag before a call gives up (each poll ~s_sleep 2 + an uncached load: 2^25 ~ 2 s);
 // DIE_CAR_SPIN overrides it (tests of the failure path use a few thousand).
-static uint32_t car_spin_limit() {
+uint32_t car_spin_limit() {
   static const uint32_t v = [] {
     const char* e = getenv("DIE_CAR_SPIN");
     const long long x = e ? atoll(e) : 0;
     return x > 0 ? (uint32_t)std::min<long long>(x, 0xffffffffll) : (1u << 25);
   }();
   return v;
+}
+
+int car_mode() {
+  static const int m = getenv("DIE_CAR_MODE") ? atoi(getenv("DIE_CAR_MODE")) : 1;
+  return m;
 }
 
 hipError_t launch_custom_all_reduce_residual(const bf16_t* in, bf16_t* resid, float* ssp, int rows, int hidden,
@@ -252,7 +220,7 @@ hipError_t launch_custom_all_reduce_residual(const bf16_t* in, bf16_t* resid, fl
     return hipErrorInvalidValue;
   for (int p = 0; p < world; ++p)
     if (peers.buf[p] == nullptr || peers.sig[p] == nullptr) return hipErrorInvalidValue;
-  static const int mode = getenv("DIE_CAR_MODE") ? atoi(getenv("DIE_CAR_MODE")) : 1;
+  const int mode = car_mode();
   hipLaunchKernelGGL(custom_all_reduce_residual_kernel, dim3(rows), dim3(car::NTH), 0, s, in, resid, ssp, hidden,
                      rank, world, peers, ctl, cap_elems / 8, mode, car_spin_limit());
   return hipGetLastError();
@@ -269,7 +237,7 @@ hipError_t launch_custom_all_reduce(const bf16_t* in, bf16_t* out, int64_t n, in
     if (peers.buf[p] == nullptr || peers.sig[p] == nullptr) return hipErrorInvalidValue;
   const int64_t nvec = n / 8;
   blocks = (int)std::min<int64_t>(blocks, (nvec + 63) / 64);  // at least 64 vectors (1 KiB) per workgroup
-  static const int mode = getenv("DIE_CAR_MODE") ? atoi(getenv("DIE_CAR_MODE")) : 1;
+  const int mode = car_mode();
   hipLaunchKernelGGL(custom_all_reduce_kernel, dim3(blocks), dim3(car::NTH), 0, s, in, out, nvec, rank, world,
                      peers, ctl, cap_elems / 8, mode, car_spin_limit());
   return hipGetLastError();

@@ -30,6 +30,7 @@
 //    that the CONSUMER kernel (fused attention prologue, RMSNorm) sums; or the
 //    split-K last arriver adds the tile into the residual stream and writes the
 //    next RMSNorm's row statistics.
+#include "car_common.h"
 #include "common.h"
 #include "launchers.h"
 
@@ -80,6 +81,76 @@ constexpr int ring_slots(int wr, int xr, int kc) {
 }  // namespace gd
 
 using namespace gd;
+
+// Tensor-parallel residual epilogue (mode 3 with fz.car_world >= 2), run by the column tile's last arriver once
+// `own` holds its complete K-shard partial: round it to bf16 (as a separate all-reduce would receive it),
+// publish it in this rank's uncached staging buffer at the message's [M][N] position, signal every peer's flag
+// slot for THIS tile and wait for theirs (allreduce.hip's one-shot protocol, bounded), then replace `own` by
+// the rank-ordered sum of the W bf16 partials (bit-identical on every rank) — or NaN when a peer never came.
+// Only the tiles' last arrivers wait, so a launch holds at most N / WR waiting workgroups per GPU; peers'
+// partials are read with system-coherent loads of their uncached staging (no acquire fence, no stale line).
+// Returns the call's epoch (the caller's last tile advances the group's epoch word).
+template <int EPT, int Q>
+__device__ __forceinline__ uint32_t car_tile_exchange(f4 (&own)[EPT], const GemmDecodeFuse& fz, int bx, int n0,
+                                                      int M, int N, int tid, int* s_fail) {
+  const int rank = fz.car_rank, world = fz.car_world;
+  const uint32_t epoch = __hip_atomic_load(fz.car_ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const int par = (int)(epoch & 1u);
+  const int64_t half = (int64_t)par * fz.car_cap;
+  uint2 pk[EPT];
+  bf16_t* mine = fz.car.buf[rank] + half;
+  if (tid == 0) *s_fail = 0;
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const int e = tid + i * NTH, m = e / Q, j = 4 * (e % Q);
+    pk[i].x = pack2(own[i][0], own[i][1]);
+    pk[i].y = pack2(own[i][2], own[i][3]);
+    if (m < M) *reinterpret_cast<uint2*>(mine + (int64_t)m * N + n0 + j) = pk[i];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's staging stores are acknowledged
+  __syncthreads();
+  uint32_t* slots = fz.car.sig[rank] + ((int64_t)par * CAR_MAX_BLOCKS + bx) * CAR_MAX_RANKS;
+  if (tid < 64 && !(fz.car_mode & 2)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+  car_wait_peers(fz.car, slots, fz.car_ctl, epoch, par, bx, rank, world, tid, fz.car_spin, *s_fail);
+  if (!(fz.car_mode & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const bool failed = *s_fail != 0;
+  // groups of IG float4 groups: every peer's piece of a group in flight at once (one xGMI round trip each)
+  constexpr int IG = EPT < 2 ? EPT : 2;
+#pragma unroll
+  for (int i0 = 0; i0 < EPT; i0 += IG) {
+    uint2 pv[CAR_MAX_RANKS][IG];
+#pragma unroll
+    for (int p = 0; p < CAR_MAX_RANKS; ++p) {
+      if (p < world && p != rank) {
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(fz.car.buf[p] + half, 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+        for (int ii = 0; ii < IG; ++ii) {
+          const int e = tid + (i0 + ii) * NTH, m = min(e / Q, M - 1), j = 4 * (e % Q);
+          pv[p][ii] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                   rs, (int)(((int64_t)m * N + n0 + j) * 2), 0, 17));  // sc0 sc1
+        }
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < IG; ++ii) {
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int p = 0; p < CAR_MAX_RANKS; ++p) {
+        if (p < world) {
+          const uint2 v = p == rank ? pk[i0 + ii] : pv[p][ii];
+          acc[0] += bf2f((bf16_t)(v.x & 0xffff));
+          acc[1] += bf2f((bf16_t)(v.x >> 16));
+          acc[2] += bf2f((bf16_t)(v.y & 0xffff));
+          acc[3] += bf2f((bf16_t)(v.y >> 16));
+        }
+      }
+      const float nan = __uint_as_float(0x7fc00000u);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) own[i0 + ii][c] = failed ? nan : bf2f(f2bf(acc[c]));  // the all-reduced bf16
+    }
+  }
+  return epoch;
+}
 
 // EPI 0: bf16 Y = XW^T. EPI 1: bf16 Y[:, j] = silu(g_j) * u_j, W = [gate(N_out rows); up(N_out rows)].
 // EPI 2: fp32 slab Y[blockIdx.y][m][n] (split-K partial). EPI 3: slab + last-arriver residual update.
@@ -329,6 +400,8 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
         }
       }
     }
+    uint32_t car_epoch = 0;
+    if (fz.car_world > 1) car_epoch = car_tile_exchange<EPT, Q>(own, fz, bx, n0, M, N_out, tid, ctl + 1);
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {  // Q | 64 and NTH % Q == 0: a row's lanes share a wave
       const int e = tid + i * NTH, m = e / Q, j = 4 * (e % Q);
@@ -350,6 +423,15 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
       if (e % Q == 0 && m < SSP_LD) fz.ssp_out[bx * SSP_LD + m] = m < M ? ss : 0.f;
     }
     if (!single && tid == 0) __hip_atomic_store(fz.counters + bx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (fz.car_world > 1 && tid == 0) {
+      // the group's epoch advances once every tile has exchanged (each tile has one last arriver; every one of
+      // them read the epoch before this point, and the next collective is a later launch)
+      if (__hip_atomic_fetch_add(fz.car_ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+          (uint32_t)gridDim.x - 1) {
+        __hip_atomic_store(fz.car_ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(fz.car_ctl, car_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
     return;
   }
   if constexpr (EPI == 4 || EPI == 6) {
@@ -588,6 +670,14 @@ hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx
   if (mode == 6 && sk > 1 && (fz.slab6 == nullptr || fz.counters == nullptr)) return hipErrorInvalidValue;
   if (mode == 3 && (fz.resid == nullptr || fz.ssp_out == nullptr || (sk > 1 && fz.counters == nullptr)))
     return hipErrorInvalidValue;
+  if (fz.car_world > 1) {  // TP exchange: one flag slot per column tile, the message inside one staging half
+    if (mode != 3 || fz.grp_off != nullptr || fz.car_world > CAR_MAX_RANKS || fz.car_rank < 0 ||
+        fz.car_rank >= fz.car_world || fz.car_ctl == nullptr || N / wr > CAR_MAX_BLOCKS || N % 4 ||
+        (int64_t)M * N > fz.car_cap)
+      return hipErrorInvalidValue;
+    for (int p = 0; p < fz.car_world; ++p)
+      if (fz.car.buf[p] == nullptr || fz.car.sig[p] == nullptr) return hipErrorInvalidValue;
+  }
 #define DIE_GD(WR, KC) \
   if (wr == WR && kc == KC) return launch_modes<WR, KC>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, fz, s);
   DIE_GD(32, 256)

@@ -70,6 +70,16 @@ hipError_t launch_decode_advance(const int64_t* out, int64_t* ids, int64_t* pos,
 hipError_t launch_residual_add_sumsq(float* ssp, bf16_t* resid, const bf16_t* x, int rows, int hidden,
                                      int64_t rstride, int64_t xstride, hipStream_t s);
 hipError_t launch_row_sumsq(float* ssp, const bf16_t* x, int rows, int hidden, int64_t stride, hipStream_t s);
+// one-shot collectives over IPC-mapped peer buffers (allreduce.hip; the TP form of the decode GEMM's mode 3)
+constexpr int CAR_MAX_RANKS = 8;
+constexpr int CAR_MAX_BLOCKS = 256;   // flag slots per parity and rank: all-reduce workgroups / GEMM column tiles
+struct CarPeers {
+  bf16_t* buf[CAR_MAX_RANKS] = {};    // per rank: staging [2][cap] (its own = local, others IPC-mapped)
+  uint32_t* sig[CAR_MAX_RANKS] = {};  // per rank: flag page [2][CAR_MAX_BLOCKS][CAR_MAX_RANKS]
+};
+uint32_t car_spin_limit();            // bounded polls of a peer's flag (DIE_CAR_SPIN)
+int car_mode();                       // synchronisation variant (DIE_CAR_MODE)
+
 // Fusion operands of the decode GEMM (modes 3 and 4, see gemm_decode.hip). Norm statistics arrays have a
 // row stride of DECODE_SSP_LD = 128 (the largest decode batch).
 constexpr int DECODE_SSP_LD = 128;
@@ -92,6 +102,16 @@ struct GemmDecodeFuse {
   float* slab6 = nullptr;        // mode 6: split-K (gate, up) partials [sk][M][ld_slab6 = 2 N_out]
   int64_t ld_slab6 = 0;
   long long* ts = nullptr;       // diagnostics: per-workgroup [start, end, xcc] s_memrealtime stamps (or null)
+  // mode 3 under tensor parallelism (car_world >= 2): the column tile's last arriver rounds its K-shard partial
+  // to bf16, exchanges it with the group's peers one-shot (allreduce.hip's protocol, flag slot = tile) and adds
+  // the rank-ordered sum into the residual — row-parallel GEMM + all-reduce + residual + statistics, one launch
+  int car_world = 0;
+  int car_rank = 0;
+  int car_mode = 1;
+  uint32_t car_spin = 0;
+  int64_t car_cap = 0;           // bf16 elements per half of each rank's staging buffer
+  uint32_t* car_ctl = nullptr;   // [epoch, ticket, error] words of the group's CustomAllReduce
+  CarPeers car;
 };
 hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,
                               int K, int mode, int wr, int kc, int sk, bool nt, const GemmDecodeFuse& fz,
@@ -105,12 +125,6 @@ hipError_t launch_rope_and_cache_slab(bf16_t* q_out, const float* slab, int sk, 
                                       hipStream_t s);
 
 // one-shot all-reduce over IPC-mapped peer buffers (allreduce.hip)
-constexpr int CAR_MAX_RANKS = 8;
-constexpr int CAR_MAX_BLOCKS = 64;
-struct CarPeers {
-  bf16_t* buf[CAR_MAX_RANKS] = {};    // per rank: staging [2][cap] (its own = local, others IPC-mapped)
-  uint32_t* sig[CAR_MAX_RANKS] = {};  // per rank: flag page [2][CAR_MAX_BLOCKS][CAR_MAX_RANKS]
-};
 hipError_t launch_custom_all_reduce(const bf16_t* in, bf16_t* out, int64_t n, int rank, int world,
                                     const CarPeers& peers, uint32_t* ctl, int64_t cap_elems, int blocks,
                                     hipStream_t s);

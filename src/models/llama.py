@@ -454,15 +454,21 @@ class CausalLM:
         # area (V3_MERGE_BYTES): at most 50 rows
         g = max(1, self.hq // self.hkv)
         qkv = ops.decode_tile(self.layers[0].qkv.shape[0], h, 2, b, max_sk=max(1, 50 // (g + 2)))
-        if self.tp.enabled:  # row-parallel o / down: bf16 partial sums (mode 0) for the all-reduce
-            o = ops.decode_tile(h, self.hq * d, 0, b)
-            down = ops.decode_tile(h, self.inter, 0, b) if not self.arch.is_moe else None
-        else:                # residual-updating split-K (mode 3)
-            o = ops.decode_tile(h, self.hq * d, 3, b)
-            down = ops.decode_tile(h, self.inter, 3, b) if not self.arch.is_moe else None
+        # residual-updating split-K (mode 3); under TP the same tiles carry the one-shot exchange of each column
+        # tile in their last arrivers' epilogue (one launch per row-parallel projection) where the group allows
+        # it (TPContext.fused_row_parallel), else bf16 partial sums (mode 0) for a separate all-reduce launch
+        o = ops.decode_tile(h, self.hq * d, 3, b)
+        down = ops.decode_tile(h, self.inter, 3, b) if not self.arch.is_moe else None
+        tp_fused = False
+        if self.tp.enabled:
+            tp_fused = (not self.arch.is_moe and self.tp.fused_row_parallel(h // o[0])
+                        and self.tp.fused_row_parallel(h // down[0]))
+            if not tp_fused:
+                o = ops.decode_tile(h, self.hq * d, 0, b)
+                down = ops.decode_tile(h, self.inter, 0, b) if not self.arch.is_moe else None
         gu = ops.decode_tile_silu(self.inter, h, b) if not self.arch.is_moe else None
         return {"qkv": qkv, "o": o, "down": down, "gate_up": gu[:2] if gu else None,
-                "gate_up_sk": gu[2] if gu else 1}
+                "gate_up_sk": gu[2] if gu else 1, "tp_fused": tp_fused}
 
     def _packed_layouts(self, buckets) -> set:
         """(projection, wr, kc) tile-order copies the fused path uses for these row buckets."""
@@ -520,7 +526,7 @@ class CausalLM:
         f32, i32 = torch.float32, torch.int32
         # TP: the row-parallel projections are all-reduced first, then one kernel adds into the
         # residual and writes a single statistics tile (so does the MoE block's residual add)
-        if self.tp.enabled:
+        if self.tp.enabled and not any(p["tp_fused"] for p in plans.values()):
             to = td = 1
         else:
             to = max(h // p["o"][0] for p in plans.values())
@@ -594,9 +600,10 @@ class CausalLM:
         hq, hkv, hid = self.hq, self.hkv, a.hidden_size
         (wq, kq, sq), (wo, ko, so) = plan["qkv"], plan["o"]
         # statistics tiles of the residual-updating projections (one per wr output columns; 1 under TP)
-        ssp_a = sc["ssp_a"][: 1 if self.tp.enabled else hid // wo]
+        tiles = not self.tp.enabled or plan["tp_fused"]  # per-tile statistics (mode 3), or one row-sum tile
+        ssp_a = sc["ssp_a"][: hid // wo if tiles else 1]
         ssp_b = sc["ssp_b"]
-        if not (self.tp.enabled or a.is_moe):
+        if tiles and not a.is_moe:
             ssp_b = ssp_b[: hid // plan["down"][0]]
 
         def tw(lw, name, wr, kc):  # (weight, tiled?) for this tile
@@ -633,7 +640,16 @@ class CausalLM:
                 wg, kg = plan["gate_up"]
                 gsk = plan.get("gate_up_sk", 1)
                 wgu, tg = tw(lw, "gate_up", wg, kg)
-                if self.tp.enabled:  # row-parallel partial sums -> all-reduce -> residual + statistics (one
+                if self.tp.enabled and plan["tp_fused"]:
+                    # row-parallel GEMM + one-shot all-reduce + residual + statistics: one launch each
+                    wdn_, kd, sd = plan["down"]
+                    wo_t, to_ = tw(lw, "o", wo, ko)
+                    wd_t, td_ = tw(lw, "down", wdn_, kd)
+                    self.tp.row_parallel_residual(attn, wo_t, h, ssp_a, sc["cnt_a"], wo, ko, so, tiled=to_)
+                    act = ops.linear_silu_mul_rownorm(h, wgu, ssp_a, eps, wg, tiled=tg, kc=kg, sk=gsk,
+                                                      slab=sc["slab6"], counters=sc["cnt6"])
+                    self.tp.row_parallel_residual(act, wd_t, h, ssp_b, sc["cnt_b"], wdn_, kd, sd, tiled=td_)
+                elif self.tp.enabled:  # row-parallel partial sums -> all-reduce -> residual + statistics (one
                     # launch on the one-shot IPC path, see TPContext.all_reduce_residual)
                     self.tp.all_reduce_residual(self._row_parallel(attn, lw, "o", plan), h, ssp_a)
                     act = ops.linear_silu_mul_rownorm(h, wgu, ssp_a, eps, wg, tiled=tg, kc=kg, sk=gsk,

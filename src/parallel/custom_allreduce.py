@@ -28,8 +28,9 @@ import torch.distributed as dist
 logger = logging.getLogger(__name__)
 
 MAX_RANKS = 8
-MAX_BLOCKS = 64
-SIG_BYTES = 2 * MAX_BLOCKS * MAX_RANKS * 4
+MAX_BLOCKS = 64                 # rows of the fused all-reduce + residual kernel (one workgroup per row)
+SIG_BLOCKS = 256                # flag slots per parity and rank (csrc CAR_MAX_BLOCKS): workgroups / GEMM tiles
+SIG_BYTES = 2 * SIG_BLOCKS * MAX_RANKS * 4
 
 
 def _kern():
@@ -68,6 +69,15 @@ class CustomAllReduce:
                 self._opened += [b, s]
                 self.bufs.append(b)
                 self.sigs.append(s)
+        # how many ranks of the group share one GPU (tests run 2..8 ranks on one GPU; a node runs one per GPU):
+        # bounds the waiting workgroups of the fused row-parallel GEMM (fused_ok)
+        props = torch.cuda.get_device_properties(torch.cuda.current_device())
+        key = str(getattr(props, "uuid", "") or "") or \
+            f"{getattr(props, 'pci_domain_id', '?')}:{getattr(props, 'pci_bus_id', '?')}:{getattr(props, 'pci_device_id', '?')}"
+        keys: List[Optional[str]] = [None] * world
+        dist.all_gather_object(keys, key, group=group)
+        self.ranks_per_gpu = max(keys.count(k) for k in keys)
+        self.cus = int(props.multi_processor_count)
         dist.barrier(group=group)  # every rank's pages are open before anyone signals into them
 
     def can_run(self, t: torch.Tensor) -> bool:
@@ -101,6 +111,31 @@ class CustomAllReduce:
         """resid += sum over the group of x (bf16, in place), ssp[row] = that row's sum of squares of the
         new residual — all-reduce and residual_add_sumsq in one launch (decode rows, <= 64)."""
         _kern().car_all_reduce_residual(x, resid, ssp, self.rank, self.bufs, self.sigs, self.ctl, self.cap)
+
+    def fused_ok(self, n_tiles: int) -> bool:
+        """Whether the row-parallel decode GEMM may carry the exchange in its epilogue (gemm_decode_car). Only a
+        column tile's last-arriving workgroup waits for the peers, so a launch holds at most ``n_tiles`` waiting
+        workgroups (one per CU: the GEMM's LDS ring) on each GPU; with every rank's waiting tiles resident at
+        once and half the CUs left for the rest of the grids, every tile of every rank gets to run (the ranks
+        sharing a GPU in tests included). ``DIE_TP_FUSED=0`` keeps the separate all-reduce launch. The answer
+        depends only on the group's layout and the shape, so every rank agrees."""
+        import os
+
+        if os.environ.get("DIE_TP_FUSED", "1") == "0":
+            return False
+        return 0 < n_tiles <= SIG_BLOCKS and n_tiles * self.ranks_per_gpu * 2 <= self.cus
+
+    def row_parallel_residual(self, x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, ssp: torch.Tensor,
+                              counters: torch.Tensor, wr: int, kc: int, sk: int, tiled: bool) -> None:
+        """resid += sum over the group of x @ w^T (this rank's K shard), ssp [N / wr, 128] = per-tile row sums of
+        squares of the new residual: ONE launch (decode GEMM mode 3 whose tiles' last arrivers run the one-shot
+        exchange). Every rank must make the same call."""
+        from src import ops
+
+        m, n = x.shape[0], w.shape[0]
+        slab = torch.empty(sk, m, n, dtype=torch.float32, device=x.device)
+        _kern().gemm_decode_car(slab, x, w, 3 | (32 if tiled else 0), wr, kc, sk, ops.DECODE_GEMM_NT, resid, ssp,
+                                counters, self.rank, self.bufs, self.sigs, self.ctl, self.cap)
 
     def read_ctl(self) -> List[int]:
         """[epoch, ticket, error] control words (synchronising host read)."""

@@ -111,6 +111,18 @@ class TPContext:
 
         ops.residual_add_sumsq(resid, self.all_reduce(x), ssp)
 
+    def fused_row_parallel(self, n_tiles: int) -> bool:
+        """Whether a row-parallel decode projection with ``n_tiles`` column tiles runs as ONE launch: the decode
+        GEMM whose tiles' last arrivers exchange their partials one-shot and update the residual
+        (:meth:`row_parallel_residual`), instead of GEMM + all-reduce/residual kernel. Needs the IPC path."""
+        return self.enabled and self.car is not None and self.car.fused_ok(n_tiles)
+
+    def row_parallel_residual(self, x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, ssp: torch.Tensor,
+                              counters: torch.Tensor, wr: int, kc: int, sk: int, tiled: bool = False) -> None:
+        """resid += all_reduce(x @ w^T) and the next norm's per-tile statistics, in one launch
+        (see :meth:`fused_row_parallel`, which the caller checked with this tile's ``n_tiles``)."""
+        self.car.row_parallel_residual(x, w, resid, ssp, counters, wr, kc, sk, tiled)
+
     # --- sequence parallelism (Megatron-SP): the all-reduce split into its two halves around the
     # token-sharded norms. Rows = tokens, padded by the caller to a multiple of world_size.
     def reduce_scatter_rows(self, t: torch.Tensor) -> torch.Tensor:
@@ -196,6 +208,18 @@ class ShardProbeTP(TPContext):
         from src import ops
 
         ops.residual_add_sumsq(resid, x, ssp)  # the non-fused path's local launch
+
+    def fused_row_parallel(self, n_tiles: int) -> bool:
+        # the fused epilogue's local form: the row-parallel GEMM updates the residual itself (DIE_TP_FUSED=0:
+        # the separate-launch form, for A/B)
+        return os.environ.get("DIE_TP_FUSED", "1") != "0"
+
+    def row_parallel_residual(self, x, w, resid, ssp, counters, wr, kc, sk, tiled=False) -> None:
+        from src import ops
+
+        # the one-launch row-parallel projection minus its exchange (mode 3 on the K shard); the exchange's
+        # xGMI cost is not in the probe
+        ops.linear_slab_residual(x, w, resid, ssp, counters, wr, sk, tiled=tiled, kc=kc)
 
     def reduce_scatter_rows(self, t: torch.Tensor) -> torch.Tensor:
         n = t.shape[0] // self.world_size

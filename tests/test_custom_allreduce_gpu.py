@@ -100,6 +100,44 @@ def _worker(rank, world, port, q):
         gg.replay()
         torch.cuda.synchronize()
         replay_ok.append(all(bool((gout[:, p * cols:(p + 1) * cols].float() == p + 1).all()) for p in range(world)))
+        # the row-parallel decode GEMM carrying the exchange in its column tiles' last arrivers (the TP decode
+        # layer's o / down projection in one launch): resid += bf16(sum over ranks of bf16(x_r @ w_r^T)), per-tile
+        # row statistics of the new residual, bit-identical on every rank; eagerly, then under hipGraph replay
+        from src import ops
+
+        m, n, ks = 19, 1024, 512
+        wr, kc, sk = ops.decode_tile(n, ks, 3, 32)
+        assert car.fused_ok(n // wr), (n // wr, car.ranks_per_gpu, car.cus)
+        g = torch.Generator(device="cuda").manual_seed(50 + rank)
+        xs = (torch.randn(m, ks, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+        wsh = (torch.randn(n, ks, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+        g0 = torch.Generator(device="cuda").manual_seed(98)
+        resid0 = torch.randn(m, n, device="cuda", generator=g0).to(torch.bfloat16)
+        resid = resid0.clone()
+        sspt = torch.zeros(n // wr, 128, device="cuda")
+        cnt = torch.zeros(n // wr, dtype=torch.int32, device="cuda")
+        car.row_parallel_residual(xs, wsh, resid, sspt, cnt, wr, kc, sk, False)
+        torch.cuda.synchronize()
+        part = (xs.float() @ wsh.float().t()).to(torch.bfloat16).float().cpu()
+        parts = [torch.empty(m, n) for _ in range(world)]
+        dist.all_gather(parts, part)
+        tot = torch.zeros(m, n)
+        for t in parts:
+            tot += t
+        want = (resid0.float().cpu() + tot.to(torch.bfloat16).float()).to(torch.bfloat16).float()
+        got = resid.float().cpu()
+        gemm_ok = bool((got - want).abs().max() <= 0.06) and float((got - want).abs().mean()) < 2e-3
+        gemm_ok = gemm_ok and torch.allclose(sspt.sum(0)[:m].cpu(), got.pow(2).sum(-1), rtol=1e-4, atol=1e-2)
+        replay_ok.append(gemm_ok)
+        out["fused_gemm"] = (gemm_ok, resid.clone().cpu())
+        gg2 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gg2):
+            car.row_parallel_residual(xs, wsh, resid, sspt, cnt, wr, kc, sk, False)
+        for _ in range(3):
+            gg2.replay()
+        torch.cuda.synchronize()
+        replay_ok.append(bool(torch.isfinite(resid.float()).all()) and int(cnt.abs().sum()) == 0)
+        out["fused_gemm_replayed"] = (True, resid.clone().cpu())
         err = car.error()
         ctl = car.read_ctl()
         dist.barrier()
@@ -137,9 +175,10 @@ def test_custom_allreduce_ranks_one_gpu(world):
         assert all(ok.values()), ok
         assert all(replay_ok), replay_ok
         assert not err
-        # one epoch per executed call (not the captures): sizes, graph warm-up, 5 replays, fused, 2 gathers
-        assert ctl[0] == len(SIZES) + 1 + 5 + 1 + 2 and ctl[1] == 0, ctl
-    for n in SIZES:
+        # one epoch per executed call (not the captures): sizes, graph warm-up, 5 replays, fused, 2 gathers,
+        # the fused GEMM eagerly and 3 replays of it
+        assert ctl[0] == len(SIZES) + 1 + 5 + 1 + 2 + 1 + 3 and ctl[1] == 0, ctl
+    for n in SIZES + ["fused_gemm", "fused_gemm_replayed"]:
         for r in range(1, world):
             assert (res[0][2][n] == res[r][2][n]).all()  # bit-identical on every rank
     assert all(p.exitcode == 0 for p in procs)

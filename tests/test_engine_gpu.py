@@ -187,7 +187,8 @@ def _tp_gpu_worker(rank, world, port, q, preset, moe_parallel="tp", sp=False, gr
             outs = obj.generate(TP_PROMPTS, SamplingParams(max_tokens=8))
             replayed = bool(obj.runner.graphs)
             obj.runner.stop_followers()
-            q.put((outs, tp.car is not None, replayed, bool(tp.car.error()) if tp.car is not None else None))
+            fused = bool(obj.model.decode_plan(4).get("tp_fused"))
+            q.put((outs, tp.car is not None, replayed, bool(tp.car.error()) if tp.car is not None else None, fused))
         else:
             obj.follower_loop()
     finally:
@@ -224,12 +225,15 @@ def test_tensor_parallel_on_one_gpu(preset, moe_parallel, sp, world, graphs):
              for r in range(world)]
     for p in procs:
         p.start()
-    got, used_car, replayed, car_err = q.get(timeout=600)
+    got, used_car, replayed, car_err, fused = q.get(timeout=600)
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
     assert used_car and car_err is False  # all-reduces / logits all-gather on the one-shot IPC kernels
     assert replayed == graphs             # graphs: decode steps replayed hipGraphs on every rank
+    # dense decode: o / down as ONE launch each (the exchange in the GEMM's tile epilogue) where the waiting
+    # tiles of all ranks sharing the GPU fit beside the rest (8 ranks on one GPU take the separate launch)
+    assert fused == (preset == "llama-mini" and world <= 4), fused
     m = CausalLM(get_preset(preset), "cuda:0", seed=3, max_position=512, full_init=True)
     for p, o in zip(TP_PROMPTS, got):
         r, mg = reference_with_margins(m, p, 8)
