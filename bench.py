@@ -124,6 +124,7 @@ def main():
     from src.engine import LLMEngine
     from src.engine.async_engine import AsyncLLMEngine
     from src.preproc import normalize_request
+    from src.utils.tracing import prof_marker
 
     cfg = EngineConfig(max_num_seqs=args.batch, max_num_batched_tokens=max(16384, args.prompt_len),
                        max_latency_ms=args.max_latency_ms, use_cuda_graph=not args.no_graph,
@@ -186,6 +187,7 @@ def main():
         if world > 1:
             dist.barrier()
         sync()
+        prof_marker()
         stats0 = dict(engine.stats)
         t0 = time.perf_counter()
         lats = []
@@ -193,6 +195,7 @@ def main():
             lats += await serve_wave(batcher, waves[s], args.gen_len, args.temperature)
             if args.verbose and rank == 0:
                 print(f"step {s}: {time.perf_counter() - t0:.2f}s", file=sys.stderr, flush=True)
+        prof_marker()
         sync()
         if tp is not None:
             engine.runner.stop_followers()

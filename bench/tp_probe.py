@@ -29,6 +29,7 @@ from src.config import EngineConfig  # noqa: E402
 from src.parallel.tp import ShardProbeTP  # noqa: E402
 from src.parallel.tp_runner import build_tp_engine  # noqa: E402
 from src.preproc import SamplingParams  # noqa: E402
+from src.utils.tracing import prof_marker  # noqa: E402
 
 
 def main(argv=None):
@@ -64,10 +65,12 @@ def main(argv=None):
     for _ in range(a.warmup):
         wave()
     sync()
+    prof_marker()
     s0 = dict(eng.stats)
     t1 = time.perf_counter()
     for _ in range(a.steps):
         wave()
+    prof_marker()
     sync()
     el = time.perf_counter() - t1
     st = eng.stats

@@ -4,7 +4,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_custom_allreduce_gpu.py tests/test_engine_gpu.py tests/test_rccl_gpu.py -k "allreduce or tensor_parallel or tp_ or rccl" -x -v --timeout 400 --timeout-method thread > gpurun_out/r4_tp_tests.log 2>&1 || { echo "TESTS FAILED"; tail -40 gpurun_out/r4_tp_tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_engine_gpu.py tests/test_rccl_gpu.py -k "tp_group or rccl or evicted" -x -v --timeout 400 --timeout-method thread > gpurun_out/r4_tp_tests.log 2>&1 || { echo "TESTS FAILED"; tail -40 gpurun_out/r4_tp_tests.log; exit 1; }
 grep -E "PASSED|FAILED" gpurun_out/r4_tp_tests.log
 timeout -k 10 500 python -u bench/tp_probe.py --preset llama3-70b --tp 8 --steps 2 --warmup 1 > gpurun_out/r4_tp_probe_70b.log 2>&1 || exit 2
 grep -h '^{' gpurun_out/r4_tp_probe_70b.log

@@ -99,6 +99,7 @@ class RemoteDecodeLink:
         self.staged_packets = 0   # gathered locally, then copied into a slot (zone full at submit / deadline)
         self.wire_packets = 0
         self._tasks: set = set()  # background releases: held here (the loop keeps only weak references)
+        self.slot_offsets: List[int] = []  # landing-zone offset of every direct packet (slot reuse, tests)
 
     # seconds kept between the local deadline of a direct export and the decode worker's reservation TTL
     DEADLINE_MARGIN_S = 5.0
@@ -193,6 +194,7 @@ class RemoteDecodeLink:
         worker owns the slot, the slot is released — after the gather has finished writing it."""
         off, gen = slot["offset"], slot["gen"]
         imported = False
+        self.slot_offsets.append(off)
         try:
             await self._ipc.wait_ready(packet.ready)
             wire = dict(packet_meta(packet), ipc={"offset": off, "gen": gen})

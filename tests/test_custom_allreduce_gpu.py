@@ -103,10 +103,8 @@ def _worker(rank, world, port, q):
         # the row-parallel decode GEMM carrying the exchange in its column tiles' last arrivers (the TP decode
         # layer's o / down projection in one launch): resid += bf16(sum over ranks of bf16(x_r @ w_r^T)), per-tile
         # row statistics of the new residual, bit-identical on every rank; eagerly, then under hipGraph replay
-        from src import ops
-
         m, n, ks = 19, 1024, 512
-        wr, kc, sk = ops.decode_tile(n, ks, 3, 32)
+        wr, kc, sk = 64, 256, 2  # 16 column tiles: every rank's waiting tiles fit beside the rest, even at 8 ranks
         assert car.fused_ok(n // wr), (n // wr, car.ranks_per_gpu, car.cus)
         g = torch.Generator(device="cuda").manual_seed(50 + rank)
         xs = (torch.randn(m, ks, device="cuda", generator=g) * 0.5).to(torch.bfloat16)

@@ -399,14 +399,18 @@ def _tp_fault_worker(rank, world, port, q):
             obj.runner.stop_followers()
         else:
             car = tp.car
-            real = car.all_reduce_residual
             calls = [0]
 
-            def skip_one(*a, **k):  # the 5th residual all-reduce (first decode step) never happens here
-                calls[0] += 1
-                if calls[0] != 5:
-                    real(*a, **k)
-            car.all_reduce_residual = skip_one
+            def skipping(real):
+                def skip_one(*a, **k):  # the 5th residual all-reduce (first decode step) never happens here
+                    calls[0] += 1
+                    if calls[0] != 5:
+                        real(*a, **k)
+                return skip_one
+            # decode's row-parallel exchanges: the separate all-reduce + residual launch, or the one fused into
+            # the o / down GEMM (whichever the layer runs; the count is over both)
+            car.all_reduce_residual = skipping(car.all_reduce_residual)
+            car.row_parallel_residual = skipping(car.row_parallel_residual)
             obj.follower_loop()
     finally:
         dist.destroy_process_group()
@@ -439,3 +443,34 @@ def test_tp_group_fails_as_a_unit():
     before, after = toks
     assert before is not None and before == after, toks  # the faulting step appended no token
     assert all(p.exitcode == 0 for p in procs)
+
+
+def test_prefix_blocks_evicted_under_pressure_then_reprefilled():
+    """Config 5's LRU KV eviction at small scale (`/root/reference/src/kvstore.py:82-102`): a pool of 64 blocks,
+    prompts with distinct 320-token prefixes. A repeat while its prefix is cached hits the prefix cache; after
+    enough other prefixes have gone through, the first prefix's blocks have been evicted (LRU of released
+    blocks) and the same prompt is prefilled again from scratch. Every output agrees with the no-cache
+    reference (greedy recompute, up to near-ties), whether it was served from cached or re-computed blocks."""
+    cfg = EngineConfig(max_num_seqs=2, max_num_batched_tokens=512, num_kv_blocks=64, max_latency_ms=0.0,
+                       graph_batch_sizes=[1, 2], enable_prefix_caching=True)
+    eng = LLMEngine.from_preset("llama-mini", device="cuda:0", cfg=cfg, max_model_len=1024)
+    eng.eos_token_id = None
+    rng = random.Random(11)
+    prefixes = [[rng.randrange(3, 32000) for _ in range(320)] for _ in range(5)]
+    prompts = [p + [rng.randrange(3, 32000) for _ in range(9)] for p in prefixes]
+    sp = SamplingParams(max_tokens=6)
+    a0 = eng.generate([prompts[0]], sp)[0]
+    hits0 = eng.stats["prefix_hit_tokens"]
+    a1 = eng.generate([prompts[0]], sp)[0]                 # still cached: served from the prefix cache
+    assert eng.stats["prefix_hit_tokens"] - hits0 == 320
+    ev0 = eng.get_stats()["kv"]["evictions"]
+    others = eng.generate(prompts[1:], sp)                 # 4 x 21 blocks through a 64-block pool
+    assert eng.get_stats()["kv"]["evictions"] > ev0        # cached prefix blocks were reclaimed (LRU)
+    hits1 = eng.stats["prefix_hit_tokens"]
+    a2 = eng.generate([prompts[0]], sp)[0]                 # prefix 0 was evicted: prefilled again
+    assert eng.stats["prefix_hit_tokens"] == hits1
+    assert eng.get_stats()["kv"]["used"] == 0
+    for p, outs in ((prompts[0], (a0, a1, a2)), *((q, (o,)) for q, o in zip(prompts[1:], others))):
+        r, m = reference_with_margins(eng.model, p, 6)
+        for o in outs:
+            assert agree(o, r, m), (o, r, m)

@@ -144,8 +144,15 @@ def test_gpu_disaggregated_ipc_landing_zone():
             assert solo.load_model(gpu_cfg())
             sport = await solo.start()
             cp, cs = InferenceClient(f"127.0.0.1:{pport}"), InferenceClient(f"127.0.0.1:{sport}")
-            for plen in (37, 300, 511):
-                req = {"prompt_token_ids": list(range(7, 7 + plen)), "max_tokens": 16, "ignore_eos": True}
+            import collections
+            import random as _random
+
+            rng = _random.Random(5)
+            # different prompts one after the other: each reuses the slot the previous one gave back (first fit at
+            # the zone's start) — a reused slot must never hand the decode engine a previous occupant's bytes
+            for plen in (37, 300, 511, 300, 64):
+                req = {"prompt_token_ids": [rng.randrange(3, 32000) for _ in range(plen)], "max_tokens": 16,
+                       "ignore_eos": True}
                 a = await asyncio.wait_for(cp.call({"model": "mini", "inputs": req}), 60)
                 b = await asyncio.wait_for(cs.call({"model": "mini", "inputs": req}), 60)
                 assert a["success"] and b["success"], (a, b)
@@ -154,8 +161,10 @@ def test_gpu_disaggregated_ipc_landing_zone():
             link = pre.models["mini"]._decode_link
             # every packet was gathered by the prefill engine straight into a slot reserved before its prompt
             # ran (one pass, no staging tensor, no second copy)
-            assert link.ipc_packets == 3 and link.direct_packets == 3 and link.wire_packets == 0, \
+            assert link.ipc_packets == 5 and link.direct_packets == 5 and link.wire_packets == 0, \
                 (link.ipc_packets, link.direct_packets, link.wire_packets)
+            assert max(collections.Counter(link.slot_offsets).values()) >= 3, link.slot_offsets
+            assert link.kv_path == "direct", link.stats()
             cd = InferenceClient(f"127.0.0.1:{dport}")
 
             async def zone():
@@ -199,7 +208,7 @@ def test_gpu_disaggregated_ipc_landing_zone():
                 os.environ.pop("DIE_KV_DIRECT", None)
             r = await asyncio.wait_for(cp.call({"model": "mini", "inputs": req}), 60)
             assert r["success"] and r["outputs"]["disaggregated"]
-            assert link.wire_packets == 0 and link.direct_packets == 4, (link.wire_packets, link.direct_packets)
+            assert link.wire_packets == 0 and link.direct_packets == 6, (link.wire_packets, link.direct_packets)
             cd.close()
             for x in (cp, cs):
                 x.close()
