@@ -461,8 +461,8 @@ class CausalLM:
         down = ops.decode_tile(h, self.inter, 3, b) if not self.arch.is_moe else None
         tp_fused = False
         if self.tp.enabled:
-            tp_fused = (not self.arch.is_moe and self.tp.fused_row_parallel(h // o[0])
-                        and self.tp.fused_row_parallel(h // down[0]))
+            tp_fused = (not self.arch.is_moe and self.tp.fused_row_parallel(h // o[0], h // o[0] * o[2])
+                        and self.tp.fused_row_parallel(h // down[0], h // down[0] * down[2]))
             if not tp_fused:
                 o = ops.decode_tile(h, self.hq * d, 0, b)
                 down = ops.decode_tile(h, self.inter, 0, b) if not self.arch.is_moe else None

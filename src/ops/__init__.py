@@ -362,7 +362,7 @@ def linear_silu_mul_rownorm(x: torch.Tensor, w_gate_up: torch.Tensor, ssp_in: to
 # narrow tiles (bench/micro_gd_splitk_silu.py, profiles/micro_gd_splitk_silu_r3.jsonl): Llama-3-70B's TP=8
 # shard 27.1 us vs 30.0 for the best full-K tile (32, 256). Dense 8B shapes lose with split-K (not listed).
 DECODE_SILU_SPLITK_CFG = {
-    (3584, 8192, 32): (64, 256, 2),
+    (3584, 8192, 32): (64, 128, 2),   # round 4 sweep (micro_tp_tiles_r4): 26.84 us vs 30.36 for (64, 256, 2) cold
 }
 
 
@@ -481,6 +481,13 @@ DECODE_TILE_CFG = {
     (14336, 4096, 4, 128): (128, 64, 1),   #                 57.2 vs 54.7
     (4096, 14336, 3, 64): (64, 128, 4),    # down  28.3 vs 40.0
     (4096, 14336, 3, 128): (128, 64, 8),   #       38.3 vs 75.3
+    # tensor-parallel shards, 32 rows (bench/micro_tp_tiles.py, profiles/micro_tp_tiles_r4.jsonl, cold, us):
+    (8192, 1024, 3, 32): (32, 128, 1),     # 70B TP=8 o      9.96 vs 12.12 for (64, 256, 2)
+    (8192, 3584, 3, 32): (32, 128, 1),     # 70B TP=8 down  17.12 vs 18.48
+    (4096, 2048, 3, 32): (32, 128, 2),     # 8B TP=2 o      11.48 vs 12.68
+    (4096, 7168, 3, 32): (64, 128, 4),     # 8B TP=2 down   18.40 vs 18.88
+    (3072, 4096, 2, 32): (48, 128, 4),     # 8B TP=2 qkv    11.08 vs 11.80
+    (7168, 4096, 4, 32): (64, 128, 1),     # 8B TP=2 gate/up 24.84 vs 25.68
 }
 _GENERIC_TILES = ((64, 128), (128, 64), (32, 128), (64, 64), (128, 32), (64, 32), (112, 128), (96, 128), (48, 128),
                   (128, 128))

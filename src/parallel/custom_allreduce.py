@@ -112,18 +112,20 @@ class CustomAllReduce:
         new residual — all-reduce and residual_add_sumsq in one launch (decode rows, <= 64)."""
         _kern().car_all_reduce_residual(x, resid, ssp, self.rank, self.bufs, self.sigs, self.ctl, self.cap)
 
-    def fused_ok(self, n_tiles: int) -> bool:
+    def fused_ok(self, n_tiles: int, grid: int = 0) -> bool:
         """Whether the row-parallel decode GEMM may carry the exchange in its epilogue (gemm_decode_car). Only a
         column tile's last-arriving workgroup waits for the peers, so a launch holds at most ``n_tiles`` waiting
-        workgroups (one per CU: the GEMM's LDS ring) on each GPU; with every rank's waiting tiles resident at
-        once and half the CUs left for the rest of the grids, every tile of every rank gets to run (the ranks
-        sharing a GPU in tests included). ``DIE_TP_FUSED=0`` keeps the separate all-reduce launch. The answer
+        workgroups (one per CU: the GEMM's LDS ring) on each GPU. Every tile of every rank gets to run when the
+        whole ``grid`` of every rank sharing the GPU is resident at once, or when the waiting tiles leave half the
+        CUs to the rest of the grids (the ranks sharing a GPU in tests included). ``DIE_TP_FUSED=0`` keeps the separate all-reduce launch. The answer
         depends only on the group's layout and the shape, so every rank agrees."""
         import os
 
-        if os.environ.get("DIE_TP_FUSED", "1") == "0":
+        if os.environ.get("DIE_TP_FUSED", "1") == "0" or not 0 < n_tiles <= SIG_BLOCKS:
             return False
-        return 0 < n_tiles <= SIG_BLOCKS and n_tiles * self.ranks_per_gpu * 2 <= self.cus
+        # every workgroup of every rank sharing the GPU resident at once (one per CU), or at most half the CUs
+        # held by waiting last arrivers
+        return (0 < grid and grid * self.ranks_per_gpu <= self.cus) or n_tiles * self.ranks_per_gpu * 2 <= self.cus
 
     def row_parallel_residual(self, x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, ssp: torch.Tensor,
                               counters: torch.Tensor, wr: int, kc: int, sk: int, tiled: bool) -> None:

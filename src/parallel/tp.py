@@ -111,11 +111,12 @@ class TPContext:
 
         ops.residual_add_sumsq(resid, self.all_reduce(x), ssp)
 
-    def fused_row_parallel(self, n_tiles: int) -> bool:
-        """Whether a row-parallel decode projection with ``n_tiles`` column tiles runs as ONE launch: the decode
+    def fused_row_parallel(self, n_tiles: int, grid: int = 0) -> bool:
+        """Whether a row-parallel decode projection with ``n_tiles`` column tiles (``grid`` workgroups) runs as ONE
+        launch: the decode
         GEMM whose tiles' last arrivers exchange their partials one-shot and update the residual
         (:meth:`row_parallel_residual`), instead of GEMM + all-reduce/residual kernel. Needs the IPC path."""
-        return self.enabled and self.car is not None and self.car.fused_ok(n_tiles)
+        return self.enabled and self.car is not None and self.car.fused_ok(n_tiles, grid)
 
     def row_parallel_residual(self, x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, ssp: torch.Tensor,
                               counters: torch.Tensor, wr: int, kc: int, sk: int, tiled: bool = False) -> None:
@@ -209,7 +210,7 @@ class ShardProbeTP(TPContext):
 
         ops.residual_add_sumsq(resid, x, ssp)  # the non-fused path's local launch
 
-    def fused_row_parallel(self, n_tiles: int) -> bool:
+    def fused_row_parallel(self, n_tiles: int, grid: int = 0) -> bool:
         # the fused epilogue's local form: the row-parallel GEMM updates the residual itself (DIE_TP_FUSED=0:
         # the separate-launch form, for A/B)
         return os.environ.get("DIE_TP_FUSED", "1") != "0"

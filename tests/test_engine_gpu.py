@@ -231,9 +231,9 @@ def test_tensor_parallel_on_one_gpu(preset, moe_parallel, sp, world, graphs):
         assert p.exitcode == 0
     assert used_car and car_err is False  # all-reduces / logits all-gather on the one-shot IPC kernels
     assert replayed == graphs             # graphs: decode steps replayed hipGraphs on every rank
-    # dense decode: o / down as ONE launch each (the exchange in the GEMM's tile epilogue) where the waiting
-    # tiles of all ranks sharing the GPU fit beside the rest (8 ranks on one GPU take the separate launch)
-    assert fused == (preset == "llama-mini" and world <= 4), fused
+    # dense decode: o / down as ONE launch each (the exchange in the GEMM's tile epilogue): the grids of all
+    # ranks sharing the GPU fit on it at once (llama-mini: 16-128 workgroups per rank)
+    assert fused == (preset == "llama-mini"), fused
     m = CausalLM(get_preset(preset), "cuda:0", seed=3, max_position=512, full_init=True)
     for p, o in zip(TP_PROMPTS, got):
         r, mg = reference_with_margins(m, p, 8)
