@@ -46,12 +46,10 @@ from src.rpc import RPCClient, RPCError  # noqa: E402
 from src.utils import (  # noqa: E402
     CODEC_MSGPACK,
     GLOBAL_TRACER,
-    ProtocolError,
     new_request_id,
-    pack_frame,
-    read_message,
     setup_logging,
 )
+from src.utils.frameserver import start_frame_server  # noqa: E402
 
 logger = logging.getLogger(__name__)
 
@@ -122,8 +120,9 @@ class Coordinator:
         for lb in self.lbs.values():
             await lb.start()
         # backlog: a burst of >100 new client connections must not hit SYN retransmits (1 s stalls)
-        self.server = await asyncio.start_server(self._handle_connection, self.host, self.port, limit=1 << 26,
-                                                 backlog=4096, reuse_port=self.reuse_port or None)
+        # protocol-level framing (src/utils/frameserver.py): no reader task per request on the front door
+        self.server = await start_frame_server(self.handle_message, self.host, self.port, backlog=4096,
+                                               reuse_port=self.reuse_port or None)
         self.port = self.server.sockets[0].getsockname()[1]
         logger.info("Coordinator listening on %s:%d", self.host, self.port)
         return self.port
@@ -131,7 +130,7 @@ class Coordinator:
     async def start_peer_server(self) -> str:
         """A private listener on which sibling coordinator processes reach THIS process (forwarded
         registrations); returns its address."""
-        self.peer_server = await asyncio.start_server(self._handle_connection, self.host, 0, limit=1 << 26)
+        self.peer_server = await start_frame_server(self.handle_message, self.host, 0)
         return f"{self.host}:{self.peer_server.sockets[0].getsockname()[1]}"
 
     async def _forward(self, msg: Dict[str, Any]) -> None:
@@ -212,38 +211,6 @@ class Coordinator:
         return False
 
     # --------------------------------------------------------------- serve
-    async def _handle_connection(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
-        try:
-            while True:
-                try:
-                    msg, mode, codec = await read_message(reader)
-                except (asyncio.IncompleteReadError, ConnectionError):
-                    break
-                except (ProtocolError, ValueError) as e:
-                    with contextlib.suppress(Exception):
-                        writer.write(pack_frame({"error": f"bad request: {e}", "success": False}))
-                        await writer.drain()
-                    break
-                if mode == "eof":
-                    break
-                async def emit(frame, codec=codec):  # token deltas of a streamed request
-                    writer.write(pack_frame(frame, codec))
-                    await writer.drain()
-
-                resp = await self.handle_message(msg, emit=emit if mode != "legacy" else None)
-                if mode == "legacy":
-                    writer.write(json.dumps(resp).encode())
-                    await writer.drain()
-                    break
-                try:
-                    writer.write(pack_frame(resp, codec))
-                    await writer.drain()
-                except ConnectionError:  # the client went away
-                    break
-        finally:
-            with contextlib.suppress(Exception):
-                writer.close()
-
     async def handle_message(self, msg: Any, emit=None) -> Dict[str, Any]:
         if not isinstance(msg, dict):
             return {"error": "Request must be a JSON object", "success": False}

@@ -18,6 +18,7 @@ from collections import defaultdict
 from typing import Any, Dict, List, Optional, Tuple
 
 from src.utils import CODEC_JSON, parse_address, read_frame, pack_frame
+from src.utils.frameserver import FrameClientProtocol
 
 
 class RPCError(Exception):
@@ -47,26 +48,34 @@ class RPCClient:
         r, w = await asyncio.wait_for(asyncio.open_connection(host, port, limit=1 << 26), timeout)
         return _Conn(r, w)
 
+    async def _open_proto(self, address: str, timeout: float) -> FrameClientProtocol:
+        host, port = parse_address(address)
+        loop = asyncio.get_running_loop()
+        _, proto = await asyncio.wait_for(loop.create_connection(FrameClientProtocol, host, port), timeout)
+        return proto
+
     async def call(self, address: str, msg: Any, timeout: Optional[float] = 600.0) -> Any:
-        """Send one framed request and await its framed reply."""
+        """Send one framed request and await its framed reply (a pooled protocol-level connection: the reply
+        frame is cut out of the receive buffer by the connection's callback, no reader task per call)."""
         pool = self._idle[address]
-        conn = pool.pop() if pool else None
+        conn = None
+        while pool and conn is None:
+            c = pool.pop()
+            conn = None if c.closed else c
         fresh = conn is None
         if conn is None:
-            conn = await self._open(address, timeout or 30.0)
+            conn = await self._open_proto(address, timeout or 30.0)
         # the reply timeout aborts the connection from a timer instead of wrapping the read in
         # asyncio.wait_for (a task + a timer per call on Python 3.10: the RPC hot path's largest cost)
         timer, expired = None, []
         if timeout:
-            def _expire(w=conn.writer):
+            def _expire(t=conn.transport):
                 expired.append(True)
-                w.transport.abort()
+                t.abort()
             timer = asyncio.get_running_loop().call_later(timeout, _expire)
         try:
-            conn.writer.write(pack_frame(msg, self.codec))
-            await conn.writer.drain()
-            reply, _ = await read_frame(conn.reader)
-        except (ConnectionError, asyncio.IncompleteReadError, OSError) as e:
+            reply = await conn.request(pack_frame(msg, self.codec))
+        except (ConnectionError, OSError) as e:
             conn.close()
             if expired:
                 raise asyncio.TimeoutError(f"rpc to {address}: no reply within {timeout} s") from e
@@ -82,7 +91,7 @@ class RPCClient:
         finally:
             if timer is not None:
                 timer.cancel()
-        if len(pool) < self.max_idle:
+        if len(pool) < self.max_idle and not conn.closed:
             pool.append(conn)
         else:
             conn.close()

@@ -1,0 +1,285 @@
+"""
+Protocol-level (callback) framing for the control plane's hot hops: the coordinator's and the worker's
+listeners (:func:`start_frame_server`) and the pooled RPC client connection (:class:`FrameClientProtocol`).
+
+The stream API (``asyncio.StreamReader``/``StreamWriter``) costs a reader future and a task wake-up per read
+and a ``drain()`` per write; at concurrency 1 through client → coordinator → worker those were most of the
+coordinator's per-request time in this sandbox (1.85k req/s against 3.3k for the single hop). Here
+``data_received`` cuts frames straight out of the receive buffer, a reply is one ``transport.write``, and
+``drain`` only waits while the transport has actually paused writing. The wire format is unchanged
+(:mod:`src.utils.framing`: u32 length + codec byte + payload), and so is the legacy path of the reference's
+clients (`/root/reference/src/worker.py:93,116-124`): a connection whose first byte is ``{`` is read as one
+unframed JSON document, answered unframed, and closed.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import collections
+import json
+import logging
+from typing import Any, Awaitable, Callable, Optional
+
+from .framing import _HDR, MAX_FRAME, ProtocolError, _JsonObjectEnd, deserialize, pack_frame
+
+logger = logging.getLogger(__name__)
+
+# handler(msg, emit) -> reply dict; emit(frame) (async) writes an intermediate frame (streaming), or is None
+Handler = Callable[[Any, Optional[Callable[[Any], Awaitable[None]]]], Awaitable[Any]]
+
+
+class _FlowControl:
+    """drain() for a Protocol: waits only while the transport has paused writing."""
+
+    def __init__(self) -> None:
+        self._paused = False
+        self._waiters: "collections.deque[asyncio.Future]" = collections.deque()
+
+    def pause_writing(self) -> None:
+        self._paused = True
+
+    def resume_writing(self) -> None:
+        self._paused = False
+        while self._waiters:
+            w = self._waiters.popleft()
+            if not w.done():
+                w.set_result(None)
+
+    def wake_all(self, exc: Optional[BaseException]) -> None:
+        while self._waiters:
+            w = self._waiters.popleft()
+            if not w.done():
+                if exc is None:
+                    w.set_result(None)
+                else:
+                    w.set_exception(exc)
+
+    async def drain(self) -> None:
+        if self._paused:
+            w = asyncio.get_running_loop().create_future()
+            self._waiters.append(w)
+            await w
+
+
+class FrameServerProtocol(asyncio.Protocol):
+    """One server connection: frames in, one handler call at a time (replies in request order), frames out.
+    ``idle_timeout``: the connection is dropped after that long with no request being served (the timer is
+    stopped while a request runs — a long streamed generation is not idle)."""
+
+    def __init__(self, handler: Handler, idle_timeout: Optional[float] = None, conns: Optional[set] = None,
+                 allow_pickle: bool = False):
+        self.handler = handler
+        self.idle_timeout = idle_timeout
+        self.conns = conns
+        self.allow_pickle = allow_pickle
+        self.transport: Optional[asyncio.Transport] = None
+        self._buf = bytearray()
+        self._queue: "collections.deque" = collections.deque()
+        self._busy = False
+        self._closed = False
+        self._legacy: Optional[_JsonObjectEnd] = None
+        self._idle: Optional[asyncio.TimerHandle] = None
+        self._flow = _FlowControl()
+        self._loop = asyncio.get_event_loop()
+
+    # ---------------------------------------------------------------- lifecycle
+    def connection_made(self, transport) -> None:
+        self.transport = transport
+        if self.conns is not None:
+            self.conns.add(transport)
+        self._arm_idle()
+
+    def connection_lost(self, exc) -> None:
+        self._closed = True
+        if self.conns is not None:
+            self.conns.discard(self.transport)
+        if self._idle is not None:
+            self._idle.cancel()
+        self._flow.wake_all(ConnectionResetError("connection lost"))
+
+    def pause_writing(self) -> None:
+        self._flow.pause_writing()
+
+    def resume_writing(self) -> None:
+        self._flow.resume_writing()
+
+    def _arm_idle(self) -> None:
+        if self.idle_timeout and not self._closed:
+            if self._idle is not None:
+                self._idle.cancel()
+            self._idle = self._loop.call_later(self.idle_timeout, self.transport.abort)
+
+    # ------------------------------------------------------------------- input
+    def data_received(self, data: bytes) -> None:
+        if self._legacy is not None:
+            self._feed_legacy(data)
+            return
+        buf = self._buf
+        if not buf and not self._queue and not self._busy and data[:1] == b"{":
+            # a legacy (unframed) request: '{' can never start a valid frame header (0x7B << 24 > MAX_FRAME)
+            self._legacy = _JsonObjectEnd()
+            self._feed_legacy(data)
+            return
+        buf += data
+        try:
+            while len(buf) >= 4:
+                (n,) = _HDR.unpack_from(buf)
+                if n == 0 or n > MAX_FRAME:
+                    raise ProtocolError(f"bad frame length {n}")
+                if len(buf) < 4 + n:
+                    break
+                body = bytes(buf[4:4 + n])
+                del buf[:4 + n]
+                self._queue.append((deserialize(body, allow_pickle=self.allow_pickle), body[:1]))
+        except (ProtocolError, ValueError) as e:
+            self._reject(e)
+            return
+        if not self._busy and self._queue:
+            self._next()
+
+    def _feed_legacy(self, data: bytes) -> None:
+        base = len(self._buf)
+        self._buf += data
+        if len(self._buf) > MAX_FRAME:
+            self._reject(ProtocolError("legacy request too large"))
+            return
+        end = self._legacy.feed(data, base)
+        if end >= 0 and not self._busy:
+            try:
+                msg = json.loads(bytes(self._buf[:end]).decode())
+            except ValueError as e:
+                self._reject(e)
+                return
+            self._busy = True
+            self._loop.create_task(self._serve(msg, None, legacy=True))
+
+    def eof_received(self) -> bool:
+        if self._legacy is not None and not self._busy:  # an unterminated legacy document: decode what came
+            try:
+                msg = json.loads(bytes(self._buf).decode())
+            except ValueError as e:
+                self._reject(e)
+                return False
+            self._busy = True
+            self._loop.create_task(self._serve(msg, None, legacy=True))
+            return True  # keep the transport open for the reply
+        return False
+
+    def _reject(self, e: BaseException) -> None:
+        if self.transport is not None and not self._closed:
+            try:
+                self.transport.write(pack_frame({"error": f"bad request: {e}", "success": False}))
+            finally:
+                self.transport.close()
+
+    # ------------------------------------------------------------------ serving
+    def _next(self) -> None:
+        msg, codec = self._queue.popleft()
+        self._busy = True
+        if self._idle is not None:
+            self._idle.cancel()
+            self._idle = None
+        self._loop.create_task(self._serve(msg, codec))
+
+    async def emit(self, frame: Any, codec: bytes) -> None:
+        if self._closed or self.transport.is_closing():
+            raise ConnectionResetError("client went away")
+        self.transport.write(pack_frame(frame, codec))
+        await self._flow.drain()
+
+    async def _serve(self, msg: Any, codec: Optional[bytes], legacy: bool = False) -> None:
+        emit = None
+        if not legacy:
+            async def emit(frame, codec=codec):  # intermediate frames of a streamed reply
+                await self.emit(frame, codec)
+        try:
+            resp = await self.handler(msg, emit)
+        except Exception as e:  # a handler bug must not kill the connection silently
+            logger.exception("request handler failed")
+            resp = {"error": str(e) or type(e).__name__, "success": False}
+        if self._closed:
+            return
+        if legacy:
+            self.transport.write(json.dumps(resp).encode())
+            self.transport.close()
+            return
+        self.transport.write(pack_frame(resp, codec))
+        self._busy = False
+        if self._queue:
+            self._next()
+        else:
+            self._arm_idle()
+
+
+async def start_frame_server(handler: Handler, host: str, port: int, *, idle_timeout: Optional[float] = None,
+                             conns: Optional[set] = None, backlog: int = 4096,
+                             reuse_port: Optional[bool] = None) -> asyncio.AbstractServer:
+    loop = asyncio.get_running_loop()
+    return await loop.create_server(lambda: FrameServerProtocol(handler, idle_timeout, conns), host, port,
+                                    backlog=backlog, reuse_port=reuse_port)
+
+
+class FrameClientProtocol(asyncio.Protocol):
+    """A pooled RPC connection: one request in flight; its reply frame resolves ``waiter``."""
+
+    def __init__(self) -> None:
+        self.transport: Optional[asyncio.Transport] = None
+        self.waiter: Optional[asyncio.Future] = None
+        self.closed = False
+        self._buf = bytearray()
+        self._flow = _FlowControl()
+
+    def connection_made(self, transport) -> None:
+        self.transport = transport
+
+    def connection_lost(self, exc) -> None:
+        self.closed = True
+        w, self.waiter = self.waiter, None
+        if w is not None and not w.done():
+            w.set_exception(ConnectionResetError(f"connection lost: {exc}"))
+        self._flow.wake_all(ConnectionResetError("connection lost"))
+
+    def pause_writing(self) -> None:
+        self._flow.pause_writing()
+
+    def resume_writing(self) -> None:
+        self._flow.resume_writing()
+
+    def data_received(self, data: bytes) -> None:
+        buf = self._buf
+        buf += data
+        while len(buf) >= 4:
+            (n,) = _HDR.unpack_from(buf)
+            if n == 0 or n > MAX_FRAME:
+                self._fail(ProtocolError(f"bad frame length {n}"))
+                return
+            if len(buf) < 4 + n:
+                return
+            body = bytes(buf[4:4 + n])
+            del buf[:4 + n]
+            w, self.waiter = self.waiter, None
+            if w is None or w.done():  # an unsolicited frame: the connection is out of step
+                self._fail(ProtocolError("unexpected frame"))
+                return
+            try:
+                w.set_result(deserialize(body))
+            except (ProtocolError, ValueError) as e:
+                w.set_exception(e)
+
+    def _fail(self, e: BaseException) -> None:
+        w, self.waiter = self.waiter, None
+        if w is not None and not w.done():
+            w.set_exception(e)
+        if self.transport is not None:
+            self.transport.abort()
+
+    async def request(self, frame: bytes) -> Any:
+        loop = asyncio.get_running_loop()
+        self.waiter = w = loop.create_future()
+        self.transport.write(frame)
+        await self._flow.drain()
+        return await w
+
+    def close(self) -> None:
+        if self.transport is not None:
+            self.transport.close()

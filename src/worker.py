@@ -45,13 +45,8 @@ import psutil  # noqa: E402
 from src.config import ModelConfig  # noqa: E402
 from src.mock_models import FakeModel  # noqa: E402
 from src.rpc import RPCClient  # noqa: E402
-from src.utils import (  # noqa: E402
-    GLOBAL_TRACER,
-    ProtocolError,
-    pack_frame,
-    read_message,
-    setup_logging,
-)
+from src.utils import GLOBAL_TRACER, setup_logging  # noqa: E402
+from src.utils.frameserver import start_frame_server  # noqa: E402
 
 logger = logging.getLogger(__name__)
 
@@ -101,8 +96,10 @@ class Worker:
         for m in self.models.values():
             if hasattr(m, "start"):
                 await m.start()
-        self.server = await asyncio.start_server(self._handle_connection, host=self.host, port=self.port, backlog=4096,
-                                                 limit=1 << 26)
+        # protocol-level framing (src/utils/frameserver.py); an idle connection is dropped after IDLE_TIMEOUT_S
+        # (the timer stops while a request is being served: a long streamed generation is not idle)
+        self.server = await start_frame_server(self.handle_message, self.host, self.port, backlog=4096,
+                                               idle_timeout=self.IDLE_TIMEOUT_S, conns=self._conns)
         self.port = self.server.sockets[0].getsockname()[1]
         logger.info("Worker %s listening on %s:%d", self.worker_id, self.host, self.port)
         if self.coordinator:
@@ -175,56 +172,7 @@ class Worker:
         finally:
             self._waiters -= 1
 
-    # -------------------------------------------------------------- network
     IDLE_TIMEOUT_S = 3600.0
-
-    async def _handle_connection(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
-        self._conns.add(writer)
-        # an idle connection is dropped after IDLE_TIMEOUT_S by ONE timer, stopped while a request is being
-        # served (a long streamed generation is not idle) and re-armed once its reply is written (asyncio.wait_for
-        # around every read cost a task + a timer per request: the mock worker's largest per-request cost)
-        loop = asyncio.get_running_loop()
-        idle = [loop.call_later(self.IDLE_TIMEOUT_S, writer.transport.abort)]
-        try:
-            while True:
-                try:
-                    msg, mode, codec = await read_message(reader)
-                except (asyncio.IncompleteReadError, ConnectionError):
-                    break
-                except (ProtocolError, ValueError) as e:
-                    self._error_count += 1
-                    with contextlib.suppress(Exception):
-                        writer.write(pack_frame({"error": f"bad request: {e}", "success": False}))
-                        await writer.drain()
-                    break
-                idle[0].cancel()
-                if mode == "eof":
-                    break  # TCP-connect probe: not a request
-                t0 = time.perf_counter()
-
-                async def emit(frame, codec=codec):  # intermediate frames of a streamed reply
-                    writer.write(pack_frame(frame, codec))
-                    await writer.drain()
-
-                resp = await self.handle_message(msg, emit=emit if mode != "legacy" else None)
-                if mode == "legacy":
-                    import json
-
-                    writer.write(json.dumps(resp).encode())
-                    await writer.drain()
-                    break
-                try:
-                    writer.write(pack_frame(resp, codec))
-                    await writer.drain()
-                except ConnectionError:  # the client went away (e.g. a dropped stream)
-                    break
-                idle[0] = loop.call_later(self.IDLE_TIMEOUT_S, writer.transport.abort)
-                logger.debug("request done in %.2f ms", (time.perf_counter() - t0) * 1e3)
-        finally:
-            idle[0].cancel()
-            self._conns.discard(writer)
-            with contextlib.suppress(Exception):
-                writer.close()
 
     async def handle_message(self, msg: Any, emit=None) -> Dict[str, Any]:
         """One RPC. ``emit``: writes an intermediate frame on the caller's connection — streamed
