@@ -289,6 +289,22 @@ void move_blocks(Tensor pool, Tensor buf, Tensor ids, bool gather) {
                                   gather, cur_stream()));
 }
 
+// pool [planes, blocks, ...]: planes [plane0, plane0 + nplanes) of blocks ids[i] into the packet row at address
+// dst[i] (int64 device array; each row holds `planes` slabs). The caller keeps the destinations alive and sized.
+void gather_blocks_rows(Tensor pool, Tensor ids, Tensor dst, int64_t plane0, int64_t nplanes) {
+  DIE_CHECK_CUDA(pool);
+  DIE_CHECK_BF16(pool);
+  DIE_CHECK_CONTIG(pool);
+  DIE_CHECK_DTYPE(ids, at::kLong);
+  DIE_CHECK_DTYPE(dst, at::kLong);
+  TORCH_CHECK(ids.is_cuda() && dst.is_cuda() && ids.is_contiguous() && dst.is_contiguous() &&
+                  ids.numel() == dst.numel(), "ids / dst: int64 device arrays of one length");
+  const int64_t planes = pool.size(0), nb = pool.size(1), slab = pool.numel() / (planes * nb);
+  TORCH_CHECK(plane0 >= 0 && nplanes >= 0 && plane0 + nplanes <= planes, "plane range outside the pool");
+  DIE_HIP(die::launch_gather_blocks_rows(bf(pool), ids.data_ptr<int64_t>(), dst.data_ptr<int64_t>(), (int)ids.numel(),
+                                         (int)plane0, (int)nplanes, nb, slab, cur_stream()));
+}
+
 void topk_softmax(Tensor w, Tensor ids, Tensor gating, bool renorm) {
   DIE_CHECK_CUDA(gating);
   DIE_CHECK_BF16(gating);
@@ -917,6 +933,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("steps") = py::none());
   m.def("copy_blocks", &copy_blocks);
   m.def("move_blocks", &move_blocks);
+  m.def("gather_blocks_rows", &gather_blocks_rows);
   m.def("topk_softmax", &topk_softmax);
   m.def("moe_align", &moe_align);
   m.def("moe_gather", &moe_gather);

@@ -23,6 +23,9 @@ hipError_t launch_copy_blocks(bf16_t* pool, const int64_t* pairs, int num_pairs,
                               int64_t slab, hipStream_t s);
 hipError_t launch_move_blocks(bf16_t* pool, bf16_t* buf, const int64_t* ids, int n, int planes, int64_t num_blocks,
                               int64_t slab, bool gather, hipStream_t s);
+// planes [plane0, plane0 + nplanes) of pool blocks ids[i] -> the [planes, slab] row at address dst[i] (int64)
+hipError_t launch_gather_blocks_rows(const bf16_t* pool, const int64_t* ids, const int64_t* dst, int n, int plane0,
+                                     int nplanes, int64_t num_blocks, int64_t slab, hipStream_t s);
 
 hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, const bf16_t* k_cache,
                                const bf16_t* v_cache, const int* block_tables, int bt_stride, const int* cu_q,

@@ -218,6 +218,30 @@ __global__ void __launch_bounds__(256) move_blocks_kernel(bf16_t* __restrict__ p
     for (int64_t k = threadIdx.x; k < slab / 8; k += blockDim.x) p[k] = b[k];
 }
 
+// Overlapped disaggregated export: gather planes [plane0, plane0 + gridDim.y) of n pool blocks, block i of the
+// list going to its own destination row dst[i] (a packet's [planes, slab] row of one block — packets of several
+// sequences, e.g. other GPUs' landing-zone slots over xGMI, in one launch). Launched on a transfer stream
+// behind the prefill forward's layer groups.
+__global__ void __launch_bounds__(256) gather_blocks_rows_kernel(const bf16_t* __restrict__ pool,
+                                                                 const int64_t* __restrict__ ids,
+                                                                 const int64_t* __restrict__ dst, int64_t num_blocks,
+                                                                 int64_t slab, int plane0) {
+  const int64_t i = blockIdx.x;
+  const int64_t plane = plane0 + blockIdx.y;
+  const uint4* p = reinterpret_cast<const uint4*>(pool + (plane * num_blocks + ids[i]) * slab);
+  uint4* b = reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(dst[i]) + plane * slab);
+  for (int64_t k = threadIdx.x; k < slab / 8; k += blockDim.x) b[k] = p[k];
+}
+
+hipError_t launch_gather_blocks_rows(const bf16_t* pool, const int64_t* ids, const int64_t* dst, int n, int plane0,
+                                     int nplanes, int64_t num_blocks, int64_t slab, hipStream_t s) {
+  if (n == 0 || nplanes == 0) return hipSuccess;
+  if (slab % 8 || nplanes < 0 || plane0 < 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gather_blocks_rows_kernel, dim3(n, nplanes), dim3(256), 0, s, pool, ids, dst, num_blocks, slab,
+                     plane0);
+  return hipGetLastError();
+}
+
 hipError_t launch_move_blocks(bf16_t* pool, bf16_t* buf, const int64_t* ids, int n, int planes, int64_t num_blocks,
                               int64_t slab, bool gather, hipStream_t s) {
   if (n == 0) return hipSuccess;

@@ -183,7 +183,9 @@ class RemoteDecodeLink:
         overwritten."""
         st, ev = slot.revoke()
         off, gen = slot.res["offset"], slot.res["gen"]
-        if st == "taken" and ev is not None and not ev.query():
+        if st == "taken" and ev is None:  # an overlapped export still queueing its layer groups
+            self._spawn(self._release_after_slot_event(slot))
+        elif st == "taken" and not ev.query():
             self._spawn(self._release_after_copy(off, gen, ev))
         else:
             self._spawn(self._release(off, gen))
@@ -260,6 +262,15 @@ class RemoteDecodeLink:
                                 30.0)
         except Exception:
             logger.warning("kv_release of slot %d on %s failed", off, self.address)
+
+    async def _release_after_slot_event(self, slot: ExportSlot, poll_s: float = 1e-3, limit_s: float = 60.0) -> None:
+        t0 = time.monotonic()
+        while slot.event is None:
+            if time.monotonic() - t0 > limit_s:  # the engine never finished the export: leave it to the TTL
+                logger.warning("export into slot %d never completed; slot left to expire", slot.res["offset"])
+                return
+            await asyncio.sleep(poll_s)
+        await self._release_after_copy(slot.res["offset"], slot.res["gen"], slot.event)
 
     async def _release_after_copy(self, off: int, gen, ev, poll_s: float = 2e-4, limit_s: float = 60.0) -> None:
         t0 = time.monotonic()

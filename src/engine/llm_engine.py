@@ -226,7 +226,10 @@ class LLMEngine:
         if out.prefill:
             # a prefill step, or a mixed step: the decode rows as 1-token chunks in the same ragged batch
             chunks = out.chunks() if out.decode else out.prefill
-            toks = self.runner.prefill(chunks)
+            exporter = self._start_export(chunks)
+            toks = self.runner.prefill(chunks, kv_hook=exporter.on_layer if exporter is not None else None)
+            if exporter is not None:
+                self._finish_export(exporter)
             now = time.perf_counter()
             self.stats["mixed_time" if out.decode else "prefill_time"] = \
                 self.stats.get("mixed_time" if out.decode else "prefill_time", 0.0) + now - t0
@@ -262,6 +265,54 @@ class LLMEngine:
         if self.cfg.kv_block_ttl_s:
             self.blocks.evict_expired()
         return finished
+
+    def _start_export(self, chunks):
+        """Disaggregated prefill: the prompts that complete in this step and export their KV get their packets
+        now (a reserved landing-zone slot — taken under its lock, see ExportSlot — or a staging tensor), and a
+        LayerGroupExporter copies each group of layers into them while the rest of the forward runs. None when
+        nothing exports (or off the GPU, under TP, or with DIE_KV_OVERLAP=0: the export then gathers everything
+        after the step, in _append)."""
+        import os
+
+        from src.parallel.kv_transfer import LayerGroupExporter, packet_shape
+
+        if self.device.type != "cuda" or os.environ.get("DIE_KV_OVERLAP", "1") == "0":
+            return None
+        if getattr(self.model, "tp", None) is not None and self.model.tp.enabled:
+            return None
+        planes = self.pool.planes()
+        targets = []
+        for c in chunks:
+            seq = c.seq
+            if c.decode or not c.completes_prompt or not getattr(seq, "export_kv", False):
+                continue
+            nb = self.blocks.blocks_needed(seq.prompt_len)
+            ud = seq.user_data if isinstance(seq.user_data, dict) else {}
+            slot = ud.get("export_slot")
+
+            def dest(dst, nb=nb):
+                buf = dst if dst is not None else torch.empty(packet_shape(planes, nb), dtype=planes.dtype,
+                                                              device=planes.device)
+                return buf, None
+            buf, _ = slot.gather(dest) if slot is not None else dest(None)
+            seq.kv_export = buf  # type: ignore[attr-defined]
+            seq._export_slot_taken = slot if (slot is not None and slot.state == "taken") else None  # type: ignore
+            targets.append((seq, list(seq.block_table[:nb]), buf))
+        if not targets:
+            return None
+        ex = LayerGroupExporter(planes, self.arch.num_layers, [(ids, buf) for _, ids, buf in targets],
+                                group=int(os.environ.get("DIE_KV_OVERLAP_GROUP", "4")))
+        ex.seqs = [s for s, _, _ in targets]
+        return ex
+
+    def _finish_export(self, ex) -> None:
+        ev = ex.finish()
+        for seq in ex.seqs:
+            seq.kv_export_ready = ev  # type: ignore[attr-defined]
+            slot = getattr(seq, "_export_slot_taken", None)
+            if slot is not None:
+                slot.set_event(ev)
+        self.stats["overlapped_exports"] = self.stats.get("overlapped_exports", 0) + len(ex.seqs)
 
     def _run_swaps(self, out: SchedulerOutput) -> None:
         """Queue the step's KV swaps on the compute stream ahead of its forward: swap-outs pack
@@ -358,7 +409,7 @@ class LLMEngine:
         elif len(seq) >= self.max_model_len:
             reason = "length"
         if reason:
-            if getattr(seq, "export_kv", False):
+            if getattr(seq, "export_kv", False) and getattr(seq, "kv_export", None) is None:
                 from src.parallel.kv_transfer import export_blocks
 
                 nb = self.blocks.blocks_needed(seq.prompt_len)

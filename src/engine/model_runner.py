@@ -222,7 +222,7 @@ class ModelRunner:
         (see :class:`src.parallel.tp_runner.TPModelRunner`). No-op at TP=1."""
 
     @torch.inference_mode()
-    def prefill(self, chunks: List[PrefillChunk]) -> List[Optional[int]]:
+    def prefill(self, chunks: List[PrefillChunk], kv_hook=None) -> List[Optional[int]]:
         """Run one ragged prefill batch — or a mixed step, whose decode rows are 1-token chunks —
         and return the sampled token for every chunk that completes its prompt or decodes
         (None for partial prompt chunks)."""
@@ -243,7 +243,7 @@ class ModelRunner:
         self._h2d(t, n, with_cu=True)
         max_q = max(c.length for c in chunks)
         self._sync_step(self.KIND_PREFILL, t, n, max_q, nd)
-        ids = self._exec_prefill(t, n, max_q, nd, greedy)
+        ids = self._exec_prefill(t, n, max_q, nd, greedy, kv_hook=kv_hook)
         res: List[Optional[int]] = [None] * n
         if nd:
             vals = self._to_host(ids, nd)
@@ -255,9 +255,9 @@ class ModelRunner:
             self._raise_on_fault()
         return res
 
-    def _exec_prefill(self, t: int, n: int, max_q: int, nd: int, greedy: bool) -> Optional[torch.Tensor]:
+    def _exec_prefill(self, t: int, n: int, max_q: int, nd: int, greedy: bool, kv_hook=None) -> Optional[torch.Tensor]:
         meta = AttnMetadata(is_prefill=True, slot_mapping=self.d_slots[:t], block_tables=self.d_bt[:n],
-                            ctx_lens=self.d_ctx[:n], cu_q=self.d_cu[: n + 1], max_q_len=max_q)
+                            ctx_lens=self.d_ctx[:n], cu_q=self.d_cu[: n + 1], max_q_len=max_q, kv_hook=kv_hook)
         hidden = self.model.forward(self.d_ids[:t], self.d_pos[:t], meta, self.pool.tensor)
         if not nd:
             return None

@@ -23,7 +23,7 @@ from __future__ import annotations
 import math
 import os
 from dataclasses import dataclass
-from typing import Dict, List, Optional
+from typing import Callable, Dict, List, Optional
 
 import torch
 import torch.nn.functional as F
@@ -49,6 +49,7 @@ class AttnMetadata:
     part_ml: Optional[torch.Tensor] = None
     attn_cnt: Optional[torch.Tensor] = None  # decode attention merge tickets (int32, zeroed once)
     scratch: Optional[dict] = None  # fused decode path buffers (CausalLM.alloc_decode_scratch)
+    kv_hook: Optional[Callable[[int], None]] = None  # prefill: called once layer i's KV writes are queued
 
 
 class LayerWeights:
@@ -350,6 +351,8 @@ class CausalLM:
             if li > 0:
                 x = ops.fused_add_rms_norm(h, residual, lw.ln1, eps)
             attn = self._attention(li, lw, x, positions, meta, kv_pool)
+            if meta.kv_hook is not None:  # layer li's KV is written: e.g. queue its overlapped export
+                meta.kv_hook(li)
             o = self.tp.all_reduce(ops.linear(attn, lw.o))
             x = ops.fused_add_rms_norm(o, residual, lw.ln2, eps)
             h = self.tp.all_reduce(self._mlp(lw, x))

@@ -218,6 +218,12 @@ def gather_blocks(pool: torch.Tensor, ids: torch.Tensor, buf: Optional[torch.Ten
     return buf
 
 
+def gather_blocks_rows(pool: torch.Tensor, ids: torch.Tensor, dst: torch.Tensor, plane0: int, nplanes: int) -> None:
+    """Planes [plane0, plane0 + nplanes) of pool blocks ``ids`` into the packet rows at device addresses ``dst``
+    (int64, one per block; each row [planes, slab]) — the overlapped disaggregated export (LayerGroupExporter)."""
+    _kern().gather_blocks_rows(pool, ids, dst, plane0, nplanes)
+
+
 def scatter_blocks(pool: torch.Tensor, ids: torch.Tensor, buf: torch.Tensor) -> None:
     planes, nb = pool.shape[0], pool.shape[1]
     slab = pool.numel() // (planes * nb)

@@ -83,6 +83,11 @@ class ExportSlot:
                 self.state = "expired"
         return fn(None)
 
+    def set_event(self, ev) -> None:
+        """Engine thread: the completion event of a gather queued in pieces (overlapped export)."""
+        with self._lock:
+            self.event = ev
+
     def revoke(self):
         """Event-loop thread: no gather may start after this. Returns ``(state, event)`` as they were: the
         slot is free to release at once unless a gather was queued (``taken``: release after ``event``)."""
@@ -91,6 +96,67 @@ class ExportSlot:
             if st == "open":
                 self.state = "revoked"
             return st, self.event
+
+
+_EXPORT_STREAMS: Dict[Any, Any] = {}
+
+
+class LayerGroupExporter:
+    """Overlapped export of the prompts that finish in a prefill step (disaggregated prefill → decode): as soon as
+    the forward has queued the KV writes of each group of ``group`` layers, the gather of those layers' planes
+    (every finishing prompt's blocks, each into its own packet: a decode worker's landing-zone slot over xGMI, or
+    a staging tensor) is queued on a separate export stream behind an event — the copies run while the
+    remaining layers compute, and only the last group's copy is left after the forward. ``finish()`` queues
+    whatever is left (a forward without layer callbacks exports everything there), returns the completion event
+    and makes the compute stream wait for it, so no later kernel can reuse the exported blocks before they
+    were read."""
+
+    def __init__(self, pool_planes: torch.Tensor, num_layers: int, targets: List[Any], group: int = 4):
+        self.pool = pool_planes
+        self.device = pool_planes.device
+        self.planes = pool_planes.shape[0]
+        self.per_layer = self.planes // num_layers
+        self.num_layers = num_layers
+        self.group = max(1, group)
+        self.done = 0
+        ids, dst = [], []
+        row = self.planes * (pool_planes.numel() // (self.planes * pool_planes.shape[1])) * pool_planes.element_size()
+        self.targets = targets                # [(block_ids, packet [nb, planes, slab])], kept alive until finish
+        for block_ids, buf in targets:
+            base = buf.data_ptr()
+            for j, b in enumerate(block_ids):
+                ids.append(int(b))
+                dst.append(base + j * row)
+        self.ids = torch.tensor(ids, dtype=torch.int64, device=self.device)
+        self.dst = torch.tensor(dst, dtype=torch.int64, device=self.device)
+        s = _EXPORT_STREAMS.get(self.device)
+        if s is None:
+            s = _EXPORT_STREAMS[self.device] = torch.cuda.Stream(device=self.device)
+        self.stream = s
+
+    def on_layer(self, li: int) -> None:
+        """Called by the forward once layer ``li``'s KV writes are queued on the current stream."""
+        if (li + 1) % self.group == 0 or li + 1 == self.num_layers:
+            self._gather_upto((li + 1) * self.per_layer)
+
+    def _gather_upto(self, p1: int) -> None:
+        if p1 <= self.done:
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.stream):
+            self.stream.wait_event(ev)
+            ops.gather_blocks_rows(self.pool, self.ids, self.dst, self.done, p1 - self.done)
+        self.done = p1
+
+    def finish(self):
+        self._gather_upto(self.planes)
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        torch.cuda.current_stream(self.device).wait_event(ev)
+        for t in (self.ids, self.dst, *(b for _, b in self.targets)):
+            t.record_stream(self.stream)
+        return ev
 
 
 def export_blocks(pool_planes: torch.Tensor, block_ids: List[int], out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -166,6 +166,36 @@ def test_kv_export_import_exact(engine):
     dec.abort("kvx")
 
 
+def test_overlapped_layer_group_export_matches_post_step_gather(engine, monkeypatch):
+    """Disaggregated prefill export overlapped with the forward (LayerGroupExporter: each group of 4 layers
+    copied into the packets on a separate stream while the rest of the forward runs) gives the same packet
+    bytes as the gather after the step (DIE_KV_OVERLAP=0), for several prompts finishing in one ragged prefill
+    step, one of them a second chunk of a long prompt."""
+    cfg = EngineConfig(max_num_seqs=8, max_num_batched_tokens=512, num_kv_blocks=256, max_latency_ms=0.0,
+                       use_cuda_graph=False, enable_prefix_caching=False)
+    eng = LLMEngine(engine.model, cfg, 1024)
+    rng = random.Random(4)
+    prompts = [[rng.randrange(3, 32000) for _ in range(n)] for n in (700, 150, 260, 33)]
+
+    def run(tag):
+        got = {}
+        for i, p in enumerate(prompts):
+            eng.add_request(f"{tag}{i}", p, SamplingParams(max_tokens=4), export_kv=True,
+                            on_finish=lambda q, i=i: got.__setitem__(i, q))
+        while eng.has_work():
+            eng.step()
+        torch.cuda.synchronize()
+        return [(got[i].output_ids, got[i].kv_export.clone()) for i in range(len(prompts))]
+    n0 = eng.stats.get("overlapped_exports", 0)
+    a = run("ov")
+    assert eng.stats.get("overlapped_exports", 0) - n0 == len(prompts)
+    monkeypatch.setenv("DIE_KV_OVERLAP", "0")
+    b = run("pg")
+    assert eng.stats.get("overlapped_exports", 0) - n0 == len(prompts)
+    for (ta, ka), (tb, kb) in zip(a, b):
+        assert ta == tb and ka.shape == kb.shape and torch.equal(ka, kb)
+
+
 def _tp_gpu_worker(rank, world, port, q, preset, moe_parallel="tp", sp=False, graphs=False):
     import os
 
