@@ -23,6 +23,8 @@ SHAPES = {  # name -> [(projection, N, K, modes)]
                 ("down", 8192, 3584, (3,))],
     "8b_tp2": [("qkv", 3072, 4096, (2,)), ("o", 4096, 2048, (3,)), ("gate_up", 7168, 4096, (4, 6)),
                ("down", 4096, 7168, (3,))],
+    "8b": [("qkv", 6144, 4096, (2,)), ("o", 4096, 4096, (3,)), ("gate_up", 14336, 4096, (4, 6)),
+           ("down", 4096, 14336, (3,))],
     "8b_tp4": [("qkv", 1536, 4096, (2,)), ("o", 4096, 1024, (3,)), ("gate_up", 3584, 4096, (4, 6)),
                ("down", 4096, 3584, (3,))],
 }

@@ -227,7 +227,8 @@ class LLMEngine:
             # a prefill step, or a mixed step: the decode rows as 1-token chunks in the same ragged batch
             chunks = out.chunks() if out.decode else out.prefill
             exporter = self._start_export(chunks)
-            toks = self.runner.prefill(chunks, kv_hook=exporter.on_layer if exporter is not None else None)
+            toks = (self.runner.prefill(chunks) if exporter is None
+                    else self.runner.prefill(chunks, kv_hook=exporter.on_layer))
             if exporter is not None:
                 self._finish_export(exporter)
             now = time.perf_counter()

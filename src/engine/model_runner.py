@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import bisect
 import logging
+import os
 from typing import Dict, List, Optional, Sequence as Seq
 
 import torch
@@ -65,6 +66,8 @@ class ModelRunner:
         self.pool = pool
         self.cfg = cfg
         self.device = model.device
+        # prefill's last layer only for the sampled rows (CausalLM._last_layer_kept_rows; DIE_PRUNE_LAST=0: all)
+        self.prune_last = os.environ.get("DIE_PRUNE_LAST", "1") != "0"
         self.is_cuda = self.device.type == "cuda"
         self.bs = pool.block_size
         self.max_model_len = max_model_len
@@ -256,12 +259,17 @@ class ModelRunner:
         return res
 
     def _exec_prefill(self, t: int, n: int, max_q: int, nd: int, greedy: bool, kv_hook=None) -> Optional[torch.Tensor]:
+        # the last layer runs only for the sampled rows (CausalLM._last_layer_kept_rows; DIE_PRUNE_LAST=0: all)
+        keep = self.d_last[:nd] if self.prune_last else None
         meta = AttnMetadata(is_prefill=True, slot_mapping=self.d_slots[:t], block_tables=self.d_bt[:n],
-                            ctx_lens=self.d_ctx[:n], cu_q=self.d_cu[: n + 1], max_q_len=max_q, kv_hook=kv_hook)
+                            ctx_lens=self.d_ctx[:n], cu_q=self.d_cu[: n + 1], max_q_len=max_q, kv_hook=kv_hook,
+                            keep_rows=keep)
         hidden = self.model.forward(self.d_ids[:t], self.d_pos[:t], meta, self.pool.tensor)
         if not nd:
             return None
-        logits = self.model.compute_logits(hidden.index_select(0, self.d_last[:nd]))
+        if hidden.shape[0] != nd:  # a path that computed every row (e.g. the slab path of small steps)
+            hidden = hidden.index_select(0, self.d_last[:nd])
+        logits = self.model.compute_logits(hidden)
         return self._sample(logits, nd, greedy, self.d_out)
 
     # ------------------------------------------------------------- decode

@@ -50,6 +50,10 @@ class AttnMetadata:
     attn_cnt: Optional[torch.Tensor] = None  # decode attention merge tickets (int32, zeroed once)
     scratch: Optional[dict] = None  # fused decode path buffers (CausalLM.alloc_decode_scratch)
     kv_hook: Optional[Callable[[int], None]] = None  # prefill: called once layer i's KV writes are queued
+    # prefill: the only rows whose final hidden state is used (each sampled chunk's last token, [n] int64): the
+    # last layer computes its KV for every token but attention / o / MLP / final norm only for these rows, and
+    # forward() returns [n, H] in this order (None: every row)
+    keep_rows: Optional[torch.Tensor] = None
 
 
 class LayerWeights:
@@ -347,9 +351,12 @@ class CausalLM:
             return self._forward_sp(residual, positions, meta, kv_pool)
         x = ops.rms_norm(residual, self.layers[0].ln1, eps)
         h = None
+        last = len(self.layers) - 1
         for li, lw in enumerate(self.layers):
             if li > 0:
                 x = ops.fused_add_rms_norm(h, residual, lw.ln1, eps)
+            if li == last and meta.is_prefill and meta.keep_rows is not None:
+                return self._last_layer_kept_rows(lw, x, residual, positions, meta, kv_pool)
             attn = self._attention(li, lw, x, positions, meta, kv_pool)
             if meta.kv_hook is not None:  # layer li's KV is written: e.g. queue its overlapped export
                 meta.kv_hook(li)
@@ -357,6 +364,40 @@ class CausalLM:
             x = ops.fused_add_rms_norm(o, residual, lw.ln2, eps)
             h = self.tp.all_reduce(self._mlp(lw, x))
         return ops.fused_add_rms_norm(h, residual, self.norm, eps)
+
+    def _last_layer_kept_rows(self, lw: LayerWeights, x: torch.Tensor, residual: torch.Tensor,
+                              positions: torch.Tensor, meta: AttnMetadata, kv_pool: torch.Tensor) -> torch.Tensor:
+        """Prefill's last layer, pruned to the rows whose hidden state is sampled: K / V of every token are
+        still projected and written to the cache (later steps attend to them), but the query, attention, o, MLP
+        and final norm run for one row per sampled sequence — the other rows' last-layer outputs would be
+        discarded (a 16,384-token prefill of 32 prompts keeps 32 rows: ~1/32 of a layer's GEMM work for the
+        sampled rows instead of a whole layer). The kept rows are each sequence's last token, so the attention is
+        a 1-query-per-sequence prefill attention over the full context."""
+        eps, d, hq, hkv = self.arch.rms_eps, self.head_dim, self.hq, self.hkv
+        li = len(self.layers) - 1
+        keep = meta.keep_rows
+        n = keep.numel()
+        qkv = ops.linear(x, lw.qkv)
+        k_cache, v_cache = kv_pool[li, 0], kv_pool[li, 1]
+        fuse_q = qkv.is_cuda
+        ops.rope_and_cache(qkv, positions, self.cos_sin, meta.slot_mapping, k_cache, v_cache, hq, hkv, d,
+                           rot_q=not fuse_q)
+        if meta.kv_hook is not None:
+            meta.kv_hook(li)
+        if n == 0:
+            return residual[:0]
+        # the sequence of each kept row (rows of sequence i: [cu_q[i], cu_q[i + 1]))
+        seq = torch.searchsorted(meta.cu_q[1:].to(torch.int64), keep, right=True)
+        q = qkv.index_select(0, keep)[:, : hq * d].contiguous()
+        cu1 = torch.arange(n + 1, dtype=torch.int32, device=q.device)
+        attn = ops.attn_prefill(q, k_cache, v_cache, meta.block_tables.index_select(0, seq),
+                                cu1, meta.ctx_lens.index_select(0, seq), 1, hq, hkv, self.scale,
+                                cos_sin=self.cos_sin if fuse_q else None)
+        res = residual.index_select(0, keep)
+        o = self.tp.all_reduce(ops.linear(attn, lw.o))
+        x2 = ops.fused_add_rms_norm(o, res, lw.ln2, eps)
+        h = self.tp.all_reduce(self._mlp(lw, x2))
+        return ops.fused_add_rms_norm(h, res, self.norm, eps)
 
     def _attention(self, li: int, lw: LayerWeights, x: torch.Tensor, positions: torch.Tensor, meta: AttnMetadata,
                    kv_pool: torch.Tensor) -> torch.Tensor:
