@@ -1099,6 +1099,18 @@ static bool cfg_matches(const DpArgs& a) {
 
 template <class C>
 static hipError_t launch_cfg(const DpArgs& a, hipStream_t s) {
+  // every workgroup waits on others (dependency counters): the whole grid must be resident at once. Check the
+  // occupancy the hardware reports for this kernel (a plain launch gives no such check); work on
+  // other streams or processes can still delay residency — the bounded waits then set the error word — so the
+  // engine never runs this step beside the KV-transfer streams (diagnostics build only).
+  static const hipError_t fits = [] {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_persistent_kernel<C>, NTH, LDS_TOTAL) !=
+        hipSuccess)
+      return hipErrorInvalidValue;
+    return per_cu >= 1 ? hipSuccess : hipErrorCooperativeLaunchTooLarge;
+  }();
+  if (fits != hipSuccess) return fits;
   hipLaunchKernelGGL(decode_persistent_kernel<C>, dim3(num_cus()), dim3(NTH), LDS_TOTAL, s, a);
   return hipGetLastError();
 }
