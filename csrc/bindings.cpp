@@ -243,7 +243,8 @@ void attn_decode_fused(Tensor out, Tensor part_o, Tensor part_ml, Tensor counter
 int64_t decode_partials(int64_t max_ctx) { return die::attn_decode_max_partials((int)max_ctx); }
 
 void sample(Tensor out, Tensor logits, c10::optional<Tensor> temperature, c10::optional<Tensor> top_k,
-            c10::optional<Tensor> top_p, c10::optional<Tensor> seeds, c10::optional<Tensor> steps) {
+            c10::optional<Tensor> top_p, c10::optional<Tensor> seeds, c10::optional<Tensor> steps,
+            c10::optional<Tensor> part, c10::optional<Tensor> cnt) {
   DIE_CHECK_CUDA(logits);
   DIE_CHECK_BF16(logits);
   check_rows(logits, "logits");
@@ -256,11 +257,23 @@ void sample(Tensor out, Tensor logits, c10::optional<Tensor> temperature, c10::o
     TORCH_CHECK(t->scalar_type() == d && t->is_cuda() && t->numel() >= rows, n, ": wrong dtype/device/size");
     return t->data_ptr();
   };
+  // split greedy argmax: a row per `splits` workgroups, so that the grid reaches ~256 workgroups
+  int splits = 1;
+  uint32_t* pp = nullptr;
+  int* cp = nullptr;
+  if (part.has_value() && cnt.has_value()) {
+    splits = (int)std::max<int64_t>(1, std::min<int64_t>(die::SAMPLE_MAX_SPLITS, 256 / std::max<int64_t>(1, rows)));
+    TORCH_CHECK(part->is_cuda() && part->scalar_type() == at::kInt && part->numel() >= rows * splits * 2,
+                "sample part scratch [rows * 16 * 2] int32");
+    TORCH_CHECK(cnt->is_cuda() && cnt->scalar_type() == at::kInt && cnt->numel() >= rows, "sample cnt [rows] int32");
+    pp = reinterpret_cast<uint32_t*>(part->data_ptr<int>());
+    cp = cnt->data_ptr<int>();
+  }
   DIE_HIP(die::launch_sample(out.data_ptr<int64_t>(), bf(logits), logits.stride(0), (int)rows, (int)logits.size(1),
                              (const float*)opt(temperature, at::kFloat, "temperature"),
                              (const int*)opt(top_k, at::kInt, "top_k"), (const float*)opt(top_p, at::kFloat, "top_p"),
                              (const int64_t*)opt(seeds, at::kLong, "seeds"),
-                             (const int64_t*)opt(steps, at::kLong, "steps"), cur_stream()));
+                             (const int64_t*)opt(steps, at::kLong, "steps"), cur_stream(), pp, cp, splits));
 }
 
 // pool viewed as [planes, num_blocks, slab]
@@ -930,7 +943,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("decode_partials", &decode_partials);
   m.def("sample", &sample, py::arg("out"), py::arg("logits"), py::arg("temperature") = py::none(),
         py::arg("top_k") = py::none(), py::arg("top_p") = py::none(), py::arg("seeds") = py::none(),
-        py::arg("steps") = py::none());
+        py::arg("steps") = py::none(), py::arg("part") = py::none(), py::arg("cnt") = py::none());
   m.def("copy_blocks", &copy_blocks);
   m.def("move_blocks", &move_blocks);
   m.def("gather_blocks_rows", &gather_blocks_rows);

@@ -52,9 +52,13 @@ hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* c
                               int head_dim, int block_size, float scale, const AttnDecodeFuse* fz, hipStream_t s);
 int attn_decode_max_partials(int max_ctx);
 
+// splits > 1: greedy rows are argmax'ed by `splits` workgroups each (part [rows][splits][2] u32 scratch, cnt [rows]
+// int32 tickets, zero, re-armed by the kernel)
+constexpr int SAMPLE_MAX_SPLITS = 16;
 hipError_t launch_sample(int64_t* out, const bf16_t* logits, int64_t stride, int rows, int vocab,
                          const float* temperature, const int* top_k, const float* top_p, const int64_t* seeds,
-                         const int64_t* steps, hipStream_t s);
+                         const int64_t* steps, hipStream_t s, uint32_t* part = nullptr, int* cnt = nullptr,
+                         int splits = 1);
 
 hipError_t launch_topk_softmax(float* w, int* ids, const bf16_t* gating, int T, int E, int K, bool renorm,
                                hipStream_t s);

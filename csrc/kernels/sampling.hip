@@ -103,31 +103,17 @@ __device__ uint32_t radix_threshold(const bf16_t* row, int vocab, float inv_t, f
   return prefix;
 }
 
-__global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, const bf16_t* __restrict__ logits,
-                                                     int64_t stride, int vocab, const float* __restrict__ temperature,
-                                                     const int* __restrict__ top_k, const float* __restrict__ top_p,
-                                                     const int64_t* __restrict__ seeds,
-                                                     const int64_t* __restrict__ steps) {
-  __shared__ ArgMax red[SNT / 64];
-  __shared__ float redf[SNT / 64];
-  __shared__ float hist[256];
-  __shared__ uint32_t sh[2];
-  const int r = blockIdx.x;
-  const bf16_t* row = logits + (int64_t)r * stride;
-  const float temp = temperature ? temperature[r] : 0.f;
-  const int k = top_k ? top_k[r] : 0;
-  const float p = top_p ? top_p[r] : 1.f;
-
-  // the argmax pass (all a greedy row needs): AU 16-B loads per lane in flight at once instead of one
-  // dependent round trip per 16 KiB of the row (11.9 -> see docs/performance.md, 32 x 128K rows)
+// argmax over row[lo, hi) (lo a multiple of 8): AU 16-B loads per lane in flight at once instead of one
+// dependent round trip per 16 KiB of the row
+__device__ __forceinline__ ArgMax row_argmax(const bf16_t* row, int lo, int hi, ArgMax* red) {
   constexpr int AU = 8;
   ArgMax best{-INFINITY, 0x7fffffff};
-  for (int i0 = threadIdx.x * 8; i0 < vocab; i0 += SNT * 8 * AU) {
+  for (int i0 = lo + threadIdx.x * 8; i0 < hi; i0 += SNT * 8 * AU) {
     uint4 v[AU];
 #pragma unroll
     for (int u = 0; u < AU; ++u) {
       const int i = i0 + u * SNT * 8;
-      v[u] = i < vocab ? *reinterpret_cast<const uint4*>(row + i) : make_uint4(0xff80ff80u, 0xff80ff80u, 0xff80ff80u, 0xff80ff80u);
+      v[u] = i < hi ? *reinterpret_cast<const uint4*>(row + i) : make_uint4(0xff80ff80u, 0xff80ff80u, 0xff80ff80u, 0xff80ff80u);
     }
 #pragma unroll
     for (int u = 0; u < AU; ++u) {
@@ -138,11 +124,62 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
       for (int j = 0; j < 8; ++j) best = better(best, ArgMax{z[j], i + j});
     }
   }
-  best = block_argmax(best, red);
+  return block_argmax(best, red);
+}
+
+// grid = (rows, splits). splits > 1: a GREEDY row is cut into `splits` slices, one workgroup each (a decode
+// step's 32 rows then use 256 CUs instead of 32: the argmax is bound by the CUs that read the row); each
+// slice's (max, index) goes to part[r][split] with write-through stores and the slice's last arriver (agent-
+// scope ticket cnt[r], re-armed) picks the row's winner — MI355X_MICROARCH.md inter-workgroup table, first
+// row. A sampled (non-greedy) row is handled whole by split 0, the others exit.
+__global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, const bf16_t* __restrict__ logits,
+                                                     int64_t stride, int vocab, const float* __restrict__ temperature,
+                                                     const int* __restrict__ top_k, const float* __restrict__ top_p,
+                                                     const int64_t* __restrict__ seeds,
+                                                     const int64_t* __restrict__ steps, uint32_t* __restrict__ part,
+                                                     int* __restrict__ cnt) {
+  __shared__ ArgMax red[SNT / 64];
+  __shared__ float redf[SNT / 64];
+  __shared__ float hist[256];
+  __shared__ uint32_t sh[2];
+  const int r = blockIdx.x, splits = gridDim.y, sp = blockIdx.y;
+  const bf16_t* row = logits + (int64_t)r * stride;
+  const float temp = temperature ? temperature[r] : 0.f;
+  const int k = top_k ? top_k[r] : 0;
+  const float p = top_p ? top_p[r] : 1.f;
+  const bool greedy = temp <= 0.f || k == 1;
+
+  if (splits > 1) {
+    if (!greedy && sp != 0) return;
+    if (greedy) {
+      const int per = ((vocab / 8 + splits - 1) / splits) * 8;
+      const int lo = min(vocab, sp * per), hi = min(vocab, lo + per);
+      const ArgMax b = row_argmax(row, lo, hi, red);
+      if (threadIdx.x == 0) {
+        uint32_t* pr = part + ((int64_t)r * splits + sp) * 2;
+        __hip_atomic_store(pr, __float_as_uint(b.v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pr + 1, (uint32_t)b.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (__hip_atomic_fetch_add(cnt + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == splits - 1) {
+          ArgMax w{-INFINITY, 0x7fffffff};
+          for (int q = 0; q < splits; ++q) {  // slices in order: ties keep the lowest index
+            const uint32_t* pq = part + ((int64_t)r * splits + q) * 2;
+            const ArgMax c{__uint_as_float(__hip_atomic_load(pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                           (int)__hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
+            w = better(w, c);
+          }
+          out[r] = w.i < vocab ? w.i : 0;
+          __hip_atomic_store(cnt + r, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      return;
+    }
+  }
+  ArgMax best = row_argmax(row, 0, vocab, red);
   // an all-NaN / all -inf row (e.g. a padded graph row over uninitialised KV) still yields a
   // valid token id: an out-of-range id would turn into an out-of-bounds embedding read next step
   if (best.i >= vocab) best.i = 0;
-  if (temp <= 0.f || k == 1) {
+  if (greedy) {
     if (threadIdx.x == 0) out[r] = best.i;
     return;
   }
@@ -186,11 +223,12 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
 
 hipError_t launch_sample(int64_t* out, const bf16_t* logits, int64_t stride, int rows, int vocab,
                          const float* temperature, const int* top_k, const float* top_p, const int64_t* seeds,
-                         const int64_t* steps, hipStream_t s) {
+                         const int64_t* steps, hipStream_t s, uint32_t* part, int* cnt, int splits) {
   if (rows == 0) return hipSuccess;
-  if (vocab % 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(sample_kernel, dim3(rows), dim3(SNT), 0, s, out, logits, stride, vocab, temperature, top_k,
-                     top_p, seeds, steps);
+  if (vocab % 8 || splits < 1 || splits > SAMPLE_MAX_SPLITS || (splits > 1 && (part == nullptr || cnt == nullptr)))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sample_kernel, dim3(rows, splits), dim3(SNT), 0, s, out, logits, stride, vocab, temperature,
+                     top_k, top_p, seeds, steps, part, cnt);
   return hipGetLastError();
 }
 

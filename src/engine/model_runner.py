@@ -123,6 +123,9 @@ class ModelRunner:
         self.d_seed = torch.zeros(self.max_seqs, dtype=i64, device=dev)
         self.d_step = torch.zeros(self.max_seqs, dtype=i64, device=dev)
         self.d_out = torch.zeros(self.max_seqs, dtype=i64, device=dev)
+        # split greedy argmax scratch (ops.sample): per-slice (max, index) and per-row tickets, re-armed in-kernel
+        self.d_samp = (torch.zeros(self.max_seqs * 32, dtype=torch.int32, device=dev),
+                       torch.zeros(self.max_seqs, dtype=torch.int32, device=dev))
         self.d_tokens = torch.zeros(2 * self.k_max, self.max_seqs, dtype=i64, device=dev)
         self.d_ctl = torch.zeros(2, dtype=i32, device=dev)
         if self.is_cuda:
@@ -189,9 +192,9 @@ class ModelRunner:
 
     def _sample(self, logits: torch.Tensor, n: int, greedy: bool, out: torch.Tensor) -> torch.Tensor:
         if greedy:
-            return ops.sample(logits, out=out[:n]) if self.is_cuda else ops.sample(logits)
+            return ops.sample(logits, out=out[:n], scratch=self.d_samp) if self.is_cuda else ops.sample(logits)
         args = (self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n], self.d_step[:n])
-        return ops.sample(logits, *args, out=out[:n]) if self.is_cuda else ops.sample(logits, *args)
+        return ops.sample(logits, *args, out=out[:n], scratch=self.d_samp) if self.is_cuda else ops.sample(logits, *args)
 
     def _to_host(self, ids: torch.Tensor, n: int) -> List[int]:
         if self.is_cuda:
@@ -283,7 +286,7 @@ class ModelRunner:
             return ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
                               self.d_step[:n])
         out = ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
-                         self.d_step[:n], out=self.d_out[:n])
+                         self.d_step[:n], out=self.d_out[:n], scratch=self.d_samp)
         if self.supports_multistep:
             # next step's inputs from this step's samples, on the device (multi-step windows)
             ops.decode_advance(self.d_out, self.d_ids, self.d_pos, self.d_ctx, self.d_slots, self.d_bt, self.d_step,

@@ -187,12 +187,16 @@ def decode_advance(out, ids, pos, ctx, slots, bt, step, tokens, cnt, n_real, row
 
 
 def sample(logits, temperature=None, top_k=None, top_p=None, seeds=None, steps=None,
-           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+           out: Optional[torch.Tensor] = None, scratch=None) -> torch.Tensor:
+    """``scratch`` = (part int32 [>= rows * 32], cnt int32 [>= rows], zero): greedy rows are split over several
+    workgroups each (a decode step's argmax on ~256 CUs instead of one per row); keep it for the engine's life
+    (the tickets are re-armed by the kernel, so it is graph-capturable)."""
     if not logits.is_cuda:
         return ref.sample(logits, temperature, top_k, top_p, seeds, steps)
     if out is None:
         out = torch.empty(logits.shape[0], dtype=torch.long, device=logits.device)
-    _kern().sample(out, logits, temperature, top_k, top_p, seeds, steps)
+    part, cnt = scratch if scratch is not None else (None, None)
+    _kern().sample(out, logits, temperature, top_k, top_p, seeds, steps, part, cnt)
     return out
 
 

@@ -277,6 +277,36 @@ def test_sampling_greedy_and_filters(dev):
     assert torch.equal(a, b)
 
 
+def test_sampling_split_greedy_argmax(dev):
+    """The split greedy argmax (ops.sample with scratch: each greedy row argmax'ed by up to 16 workgroups whose
+    slice winners the last arriver combines) equals torch's argmax at 1 / 7 / 32 / 128 rows — ties to the lowest
+    index across slices, all -inf rows to 0 — mixes with sampled rows (handled whole by one workgroup), and
+    re-arms its tickets (repeated calls, as under graph replay)."""
+    v = 128256
+    part = torch.zeros(128 * 32, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(128, dtype=torch.int32, device=dev)
+    for rows in (1, 7, 32, 128):
+        lg = (torch.randn(rows, v, device=dev) * 3).to(torch.bfloat16)
+        lg[0, 5] = lg[0, v - 3] = 100.0           # a tie in the first and last slices: the first wins
+        if rows > 1:
+            lg[1] = float("-inf")
+        for _ in range(3):
+            got = ops.sample(lg, scratch=(part, cnt)).cpu()
+            want = lg.float().argmax(-1).cpu()
+            if rows > 1:
+                want[1] = 0
+            assert torch.equal(got, want), (rows, got[:8], want[:8])
+        assert int(cnt.abs().sum()) == 0
+    lg = (torch.randn(32, v, device=dev) * 3).to(torch.bfloat16)
+    temp = torch.where(torch.arange(32, device=dev) % 2 == 0, 0.0, 0.7).float()
+    seeds = torch.arange(32, device=dev, dtype=torch.long)
+    steps = torch.zeros(32, device=dev, dtype=torch.long)
+    a = ops.sample(lg, temp, None, None, seeds, steps, scratch=(part, cnt)).cpu()
+    b = ops.sample(lg, temp, None, None, seeds, steps).cpu()   # one workgroup per row
+    assert torch.equal(a, b)
+    assert torch.equal(a[::2], lg.float().argmax(-1).cpu()[::2])
+
+
 def test_sampling_distribution(dev):
     v = 1024
     probs = torch.zeros(v)
