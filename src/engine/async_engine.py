@@ -168,7 +168,8 @@ class AsyncLLMEngine:
                 # worker) must select it on this thread too
                 import torch
 
-                torch.cuda.set_device(eng.device)
+                if eng.device.index is not None:
+                    torch.cuda.set_device(eng.device)
             while not self._stop.is_set():
                 self._drain()
                 if not eng.has_work():

@@ -53,7 +53,7 @@ class LLMBackend:
         device = config.overrides.get("device") if config.overrides else None
         if device is None:
             device = "cuda:0" if torch.cuda.is_available() else "cpu"
-        if str(device).startswith("cuda"):
+        if str(device).startswith("cuda") and torch.device(device).index is not None:
             # model build, weight packing and graph capture run on this thread: on the serving GPU
             torch.cuda.set_device(torch.device(device))
         if engine is None:
