@@ -280,7 +280,15 @@ class LLMBackend:
         d = msg["packet"]
         handed: List[bool] = []
         off = -1
-        if d.get("ipc") is not None:  # payload already delivered into the landing zone by the sender's copy
+        ready = None
+        if d.get("ipc") is not None and d["ipc"].get("event") is not None:
+            # the sender's copies may still be in flight: our stream waits on its IPC completion event
+            try:
+                ready = torch.cuda.Event.from_ipc_handle(self.engine.device, bytes(d["ipc"]["event"]))
+            except Exception as e:  # the slot stays the sender's: it polls and re-sends without the event
+                logger.info("cannot open an IPC event (%s): asking the sender to poll", e)
+                return {"success": False, "event_unsupported": True}
+        if d.get("ipc") is not None:  # payload delivered (or being delivered) into the landing zone by the sender
             zone, off = self._landing_zone(), int(d["ipc"]["offset"])
             kv = zone.claim(off, d["shape"], d["ipc"].get("gen"))  # a view: the engine scatters from the zone
 
@@ -290,7 +298,7 @@ class LLMBackend:
 
             packet = KVPacket(d["request_id"], list(d["prompt_ids"]), int(d["first_token"]), kv,
                               int(d["block_size"]), dict(d.get("sampling") or {}), d.get("ttft_ms"),
-                              on_imported=on_imported)
+                              ready=ready, on_imported=on_imported)
             self.ipc_imports += 1
         else:
             packet = packet_for_import(d, self.engine.device)

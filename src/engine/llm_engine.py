@@ -307,7 +307,13 @@ class LLMEngine:
         return ex
 
     def _finish_export(self, ex) -> None:
-        ev = ex.finish()
+        import os
+
+        # an IPC completion event where a packet goes to another process's landing zone: the decode worker's
+        # stream waits on it directly (DIE_KV_IPC_EVENT=0: the sender polls completion, then signals by RPC)
+        ipc = os.environ.get("DIE_KV_IPC_EVENT", "1") != "0" and any(
+            getattr(s, "_export_slot_taken", None) is not None for s in ex.seqs)
+        ev = ex.finish(interprocess=ipc)
         for seq in ex.seqs:
             seq.kv_export_ready = ev  # type: ignore[attr-defined]
             slot = getattr(seq, "_export_slot_taken", None)

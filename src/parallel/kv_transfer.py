@@ -149,9 +149,18 @@ class LayerGroupExporter:
             ops.gather_blocks_rows(self.pool, self.ids, self.dst, self.done, p1 - self.done)
         self.done = p1
 
-    def finish(self):
+    def finish(self, interprocess: bool = False):
+        """``interprocess``: the completion event is an IPC event (its handle lets another process's stream wait
+        for the copies — the decode worker's scatter — with no host round trip in between)."""
         self._gather_upto(self.planes)
-        ev = torch.cuda.Event()
+        ev = None
+        if interprocess:
+            try:
+                ev = torch.cuda.Event(interprocess=True)
+            except Exception:  # no IPC events on this runtime: a plain event, the sender polls it
+                ev = None
+        if ev is None:
+            ev = torch.cuda.Event()
         ev.record(self.stream)
         torch.cuda.current_stream(self.device).wait_event(ev)
         for t in (self.ids, self.dst, *(b for _, b in self.targets)):

@@ -165,6 +165,11 @@ def test_gpu_disaggregated_ipc_landing_zone():
                 (link.ipc_packets, link.direct_packets, link.wire_packets)
             assert max(collections.Counter(link.slot_offsets).values()) >= 3, link.slot_offsets
             assert link.kv_path == "direct", link.stats()
+            # completion handed over as an IPC event (the decode stream waits on the sender's copies), unless the
+            # runtime refused one — then every packet fell back to poll + RPC, still direct
+            print("kv link:", link.stats(), "ipc events:", link.ipc_events, flush=True)
+            assert link.event_handoffs in (0, 5) and (link.event_handoffs == 5) == link.ipc_events, link.stats()
+            link.ipc_events = False  # the injected failures below are in the poll path
             cd = InferenceClient(f"127.0.0.1:{dport}")
 
             async def zone():
