@@ -192,8 +192,13 @@ def test_overlapped_layer_group_export_matches_post_step_gather(engine, monkeypa
     monkeypatch.setenv("DIE_KV_OVERLAP", "0")
     b = run("pg")
     assert eng.stats.get("overlapped_exports", 0) - n0 == len(prompts)
-    for (ta, ka), (tb, kb) in zip(a, b):
-        assert ta == tb and ka.shape == kb.shape and torch.equal(ka, kb)
+    for p, (ta, ka), (tb, kb) in zip(prompts, a, b):
+        assert ta == tb and ka.shape == kb.shape
+        # the prompt's token slots (the last block's slots past the prompt hold whatever the pool block held)
+        nb, planes = ka.shape[0], ka.shape[1]
+        va = ka.view(nb, planes, -1, 16, 128).transpose(1, 3).reshape(nb * 16, -1)[: len(p)]
+        vb = kb.view(nb, planes, -1, 16, 128).transpose(1, 3).reshape(nb * 16, -1)[: len(p)]
+        assert torch.equal(va, vb)
 
 
 def _tp_gpu_worker(rank, world, port, q, preset, moe_parallel="tp", sp=False, graphs=False):
