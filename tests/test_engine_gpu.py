@@ -403,7 +403,9 @@ def _tp_fault_worker(rank, world, port, q):
     """One rank skips a one-shot collective (out of step, as a rank that died mid-step would be)."""
     import os
 
-    os.environ["DIE_CAR_SPIN"] = "200000"  # bounded waits of well under a second (read at the first launch)
+    # bounded waits of a few seconds (read at the first launch): long enough for a cold rank to reach a collective
+    # (first-use module loads), short enough for the injected fault to surface quickly
+    os.environ["DIE_CAR_SPIN"] = "3000000"
     import torch.distributed as dist
 
     from src.parallel.tp import TPContext
