@@ -145,7 +145,9 @@ class RemoteDecodeLink:
                 else:
                     self.use_ipc = False
             except Exception as e:  # different node / no IPC: bytes over the socket from now on
-                logger.info("KV IPC channel to %s unavailable (%s); using the RPC payload path", self.address, e)
+                # loud: on one node this is a misconfiguration (e.g. the decode GPU not visible to this process)
+                logger.warning("KV IPC channel to %s unavailable (%s): prompt KV will travel as BYTES over the RPC "
+                               "socket (kv_path 'wire')", self.address, e)
                 self.use_ipc = False
         return self._ipc
 
