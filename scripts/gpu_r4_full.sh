@@ -18,3 +18,7 @@ DIE_KV_OVERLAP=0 timeout -k 10 600 python -u bench/disagg_serve_bench.py --steps
 cat gpurun_out/r4f_disagg_noov.jsonl
 timeout -k 10 500 python -u bench/micro_tp_tiles.py --shapes 8b > gpurun_out/r4f_8b_tiles.jsonl 2>&1 || exit 8
 grep best gpurun_out/r4f_8b_tiles.jsonl
+timeout -k 10 300 python -u bench/micro_prefill_tail.py > gpurun_out/r4f_prefill_tail.jsonl 2>&1 || exit 9
+cat gpurun_out/r4f_prefill_tail.jsonl
+DIE_PREFILL_RESID_GEMM=1 timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/r4f_bench_resid.log 2>&1 || { tail -5 gpurun_out/r4f_bench_resid.log; exit 10; }
+grep '^{' gpurun_out/r4f_bench_resid.log

@@ -349,6 +349,8 @@ class CausalLM:
                 return self._forward_decode_slab(residual, positions, meta, kv_pool)
         if self.sequence_parallel and meta.is_prefill:
             return self._forward_sp(residual, positions, meta, kv_pool)
+        if meta.is_prefill and self._resid_gemm_ok(residual):
+            return self._forward_prefill_resid(residual, positions, meta, kv_pool)
         x = ops.rms_norm(residual, self.layers[0].ln1, eps)
         h = None
         last = len(self.layers) - 1
@@ -364,6 +366,34 @@ class CausalLM:
             x = ops.fused_add_rms_norm(o, residual, lw.ln2, eps)
             h = self.tp.all_reduce(self._mlp(lw, x))
         return ops.fused_add_rms_norm(h, residual, self.norm, eps)
+
+    def _resid_gemm_ok(self, residual: torch.Tensor) -> bool:
+        """Prefill on one GPU (no TP exchange between a projection and its residual add), dense FFN."""
+        return (residual.is_cuda and not self.tp.enabled and not self.arch.is_moe
+                and os.environ.get("DIE_PREFILL_RESID_GEMM", "0") != "0")
+
+    def _forward_prefill_resid(self, residual: torch.Tensor, positions: torch.Tensor, meta: AttnMetadata,
+                               kv_pool: torch.Tensor) -> torch.Tensor:
+        """Prefill with the residual adds in the GEMM epilogues: o and down accumulate straight into the
+        residual stream (``residual.addmm_``: hipBLASLt's beta = 1 epilogue reads C = residual and adds it in
+        fp32 before the one bf16 rounding), so each norm is a plain rms_norm — read the residual, write x —
+        instead of fused_add_rms_norm's read h, read residual, write residual, write x. At the bench's
+        16,384-row wave that drops two [T, H] passes (2 x 134 MB) per norm, 64 norms a wave; the projection
+        output tensors are not allocated at all. The norm weights are folded into Wqkv / Wgate_up
+        (fold_norm_weights), so only the row statistics remain to apply."""
+        eps = self.arch.rms_eps
+        last = len(self.layers) - 1
+        for li, lw in enumerate(self.layers):
+            x = ops.rms_norm(residual, lw.ln1, eps)
+            if li == last and meta.keep_rows is not None:
+                return self._last_layer_kept_rows(lw, x, residual, positions, meta, kv_pool)
+            attn = self._attention(li, lw, x, positions, meta, kv_pool)
+            if meta.kv_hook is not None:
+                meta.kv_hook(li)
+            residual.addmm_(attn, lw.o.t())
+            x = ops.rms_norm(residual, lw.ln2, eps)
+            residual.addmm_(ops.silu_and_mul(F.linear(x, lw.gate_up)), lw.down.t())
+        return ops.rms_norm(residual, self.norm, eps)
 
     def _last_layer_kept_rows(self, lw: LayerWeights, x: torch.Tensor, residual: torch.Tensor,
                               positions: torch.Tensor, meta: AttnMetadata, kv_pool: torch.Tensor) -> torch.Tensor:
