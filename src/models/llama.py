@@ -383,6 +383,14 @@ class CausalLM:
         (fold_norm_weights), so only the row statistics remain to apply."""
         eps = self.arch.rms_eps
         last = len(self.layers) - 1
+        t = residual.shape[0]
+        # DIE_PREFILL_MLP_CHUNK=N: the FFN runs over N-row chunks, so a chunk's gate/up output and SiLU*mul
+        # output (N x 2I and N x I bf16) can stay in the Infinity Cache between the three kernels
+        chunk = int(os.environ.get("DIE_PREFILL_MLP_CHUNK", "0"))
+        bufs = None
+        if 0 < chunk < t:
+            bufs = (torch.empty(chunk, 2 * self.inter, dtype=residual.dtype, device=residual.device),
+                    torch.empty(chunk, self.inter, dtype=residual.dtype, device=residual.device))
         for li, lw in enumerate(self.layers):
             x = ops.rms_norm(residual, lw.ln1, eps)
             if li == last and meta.keep_rows is not None:
@@ -392,7 +400,15 @@ class CausalLM:
                 meta.kv_hook(li)
             residual.addmm_(attn, lw.o.t())
             x = ops.rms_norm(residual, lw.ln2, eps)
-            residual.addmm_(ops.silu_and_mul(F.linear(x, lw.gate_up)), lw.down.t())
+            if bufs is None:
+                residual.addmm_(ops.silu_and_mul(F.linear(x, lw.gate_up)), lw.down.t())
+                continue
+            gu, act = bufs
+            for s in range(0, t, chunk):
+                n = min(t, s + chunk) - s
+                F.linear(x[s:s + n], lw.gate_up, out=gu[:n])
+                ops.silu_and_mul(gu[:n], out=act[:n])
+                residual[s:s + n].addmm_(act[:n], lw.down.t())
         return ops.rms_norm(residual, self.norm, eps)
 
     def _last_layer_kept_rows(self, lw: LayerWeights, x: torch.Tensor, residual: torch.Tensor,
