@@ -420,12 +420,19 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
   for (int t = blockIdx.x; t < n_tasks; t += gridDim.x) {
     const int pair = t % pairs, part = t / pairs;
     const int seq = pair / hkv, kvh = pair - seq * hkv;
-    const int ctx = __builtin_amdgcn_readfirstlane(ctx_lens[seq]);
-    const int nch = (ctx + DEC_KEYS - 1) / DEC_KEYS;
     const int c0 = part * C;
+    const int* bt = block_tables + (int64_t)seq * bt_stride;
+    // the first chunk's two block ids of this wave, read speculatively (clamped to the table row) BEFORE the
+    // context length: the two scalar loads are in flight together, so the first chunk's DMA waits for one
+    // dependent round trip instead of two (ctx, then the table) — micro_attn_timeline's 7.1 us first chunk
+    const int f0 = bt[__builtin_amdgcn_readfirstlane(min(c0 * 8 + 2 * wave, bt_stride - 1))];
+    const int f1 = bt[__builtin_amdgcn_readfirstlane(min(c0 * 8 + 2 * wave + 1, bt_stride - 1))];
+    const int ctx = __builtin_amdgcn_readfirstlane(ctx_lens[seq]);
+    // consumed here, so the compiler cannot sink the table loads past the branch below (one lgkmcnt wait)
+    asm volatile("" ::"s"(f0), "s"(f1), "s"(ctx));
+    const int nch = (ctx + DEC_KEYS - 1) / DEC_KEYS;
     if (c0 >= nch) continue;  // uniform
     const int c1 = min(c0 + C, nch);
-    const int* bt = block_tables + (int64_t)seq * bt_stride;
     const int last_blk = (ctx - 1) >> 4;
 
     // LDS-DMA chunk c (K and V rows of 128 keys) into buffer b: 16 instructions per lane.
@@ -435,8 +442,8 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
       // this wave's two 16-key blocks of the chunk; the table row is read speculatively
       // (clamped to the row, not to the context) so the loads do not wait for ctx
       const int j0 = c * 8 + 2 * wave;
-      const int e0 = bt[__builtin_amdgcn_readfirstlane(min(j0, bt_stride - 1))];
-      const int e1 = bt[__builtin_amdgcn_readfirstlane(min(j0 + 1, bt_stride - 1))];
+      const int e0 = c == c0 ? f0 : bt[__builtin_amdgcn_readfirstlane(min(j0, bt_stride - 1))];
+      const int e1 = c == c0 ? f1 : bt[__builtin_amdgcn_readfirstlane(min(j0 + 1, bt_stride - 1))];
       const int el = j0 + 1 > last_blk ? bt[last_blk] : 0;  // only the context's last chunk needs it
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
