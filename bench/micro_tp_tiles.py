@@ -57,8 +57,8 @@ def main():
                         cols = wr // 2 if silu else wr
                         if n % cols or k % (kc * sk) or not ops.gd_tile_valid(wr, kc, 32):
                             continue
-                        if mode == 3 and wr not in (32, 64, 128):
-                            continue
+                        if mode == 3 and (wr not in (32, 64, 128) or n // wr > 128):
+                            continue  # the fused path's consumers take <= 128 statistics tiles
                         if mode == 6 and sk == 1:
                             continue
                         ntiles = n // cols

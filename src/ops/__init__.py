@@ -492,14 +492,29 @@ DECODE_TILE_CFG = {
     (4096, 14336, 3, 64): (64, 128, 4),    # down  28.3 vs 40.0
     (4096, 14336, 3, 128): (128, 64, 8),   #       38.3 vs 75.3
     # tensor-parallel shards, 32 rows (bench/micro_tp_tiles.py, profiles/micro_tp_tiles_r4.jsonl, cold, us):
-    (8192, 1024, 3, 32): (32, 128, 1),     # 70B TP=8 o      9.96 vs 12.12 for (64, 256, 2)
-    (8192, 3584, 3, 32): (32, 128, 1),     # 70B TP=8 down  17.12 vs 18.48
+    # (mode 3 needs N / wr <= 128 statistics tiles: the 70B shard's wr = 32 winners, 9.96 / 17.12 us, would
+    # disable the fused decode path, so the best wr >= 64 tiles)
+    (8192, 1024, 3, 32): (64, 256, 1),     # 70B TP=8 o     11.28 vs 12.12 for (64, 256, 2)
+    (8192, 3584, 3, 32): (64, 128, 2),     # 70B TP=8 down  17.96 vs 18.48 for (64, 256, 2)
     (4096, 2048, 3, 32): (32, 128, 2),     # 8B TP=2 o      11.48 vs 12.68
     (4096, 7168, 3, 32): (64, 128, 4),     # 8B TP=2 down   18.40 vs 18.88
     (3072, 4096, 2, 32): (48, 128, 4),     # 8B TP=2 qkv    11.08 vs 11.80
     (7168, 4096, 4, 32): (64, 128, 1),     # 8B TP=2 gate/up 24.84 vs 25.68
 }
-_GENERIC_TILES = ((64, 128), (128, 64), (32, 128), (64, 64), (128, 32), (64, 32), (112, 128), (96, 128), (48, 128),
+
+
+def _tile_overrides(spec: str) -> dict:
+    """DIE_TILE_OVERRIDE="N,K,mode,bucket=wr,kc,sk;...": decode-GEMM tiles to try in the real graph (A/B runs of
+    a micro-bench winner) without editing DECODE_TILE_CFG."""
+    out = {}
+    for item in filter(None, (s.strip() for s in spec.split(";"))):
+        key, val = item.split("=")
+        out[tuple(int(v) for v in key.split(","))] = tuple(int(v) for v in val.split(","))
+    return out
+
+
+DECODE_TILE_CFG.update(_tile_overrides(os.environ.get("DIE_TILE_OVERRIDE", "")))
+_GENERIC_TILES = ((64, 128),(128, 64), (32, 128), (64, 64), (128, 32), (64, 32), (112, 128), (96, 128), (48, 128),
                   (128, 128))
 
 
@@ -509,7 +524,8 @@ def decode_tile(n: int, k: int, mode: int, bucket: int = 32, max_sk: int = 8):
     import math
 
     c = DECODE_TILE_CFG.get((n, k, mode, bucket))
-    if c is not None and c[2] <= max_sk:
+    # mode 3 writes one statistics tile per wr columns; its consumers take at most 128 of them
+    if c is not None and c[2] <= max_sk and (mode != 3 or n // c[0] <= 128):
         return c
     if bucket <= 32:
         if mode == 3:

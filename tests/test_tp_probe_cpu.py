@@ -21,3 +21,23 @@ def test_tp_probe_runs_shard_on_cpu(tp):
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["bench"] == "tp_shard_probe" and d["tp"] == tp and d["decode_ms_per_step"] > 0
     assert "all-reduce" in d["not_included"]
+
+
+def test_decode_tile_table_keeps_statistics_tiles_within_the_consumers():
+    """Mode 3 (residual update) writes one row-statistics tile per wr output columns; the fused attention
+    prologue and the gate/up row scale read at most 128 of them (a 70B TP=8 shard with wr = 32 would have 256
+    and turn the whole fused decode path off)."""
+    from src import ops
+
+    for (n, k, mode, bucket) in ops.DECODE_TILE_CFG:
+        wr, kc, sk = ops.decode_tile(n, k, mode, bucket)
+        if mode == 3:
+            assert n // wr <= 128, (n, k, bucket, wr)
+    assert ops.decode_tile(8192, 1024, 3, 32)[0] >= 64 and ops.decode_tile(8192, 3584, 3, 32)[0] >= 64
+
+
+def test_tile_override_parser():
+    from src import ops
+
+    assert ops._tile_overrides("4096,4096,3,32=32,256,2; 14336,4096,4,32=128,128,1") == {
+        (4096, 4096, 3, 32): (32, 256, 2), (14336, 4096, 4, 32): (128, 128, 1)}
