@@ -309,9 +309,12 @@ class LLMEngine:
     def _finish_export(self, ex) -> None:
         import os
 
-        # an IPC completion event where a packet goes to another process's landing zone: the decode worker's
-        # stream waits on it directly (DIE_KV_IPC_EVENT=0: the sender polls completion, then signals by RPC)
-        ipc = os.environ.get("DIE_KV_IPC_EVENT", "1") != "0" and any(
+        # DIE_KV_IPC_EVENT=1: an IPC completion event where a packet goes to another process's landing zone, the
+        # decode worker's stream waits on it directly. Default off: the sender polls completion, then signals by
+        # RPC — measured faster on MI355X (two-process bench 49.55 vs 49.01 req/s,
+        # profiles/disagg_r4_ipc_event_ab.jsonl: opening an IPC event and a stream wait on it cost the decode
+        # worker more than the poll + one RPC the event saves)
+        ipc = os.environ.get("DIE_KV_IPC_EVENT", "0") == "1" and any(
             getattr(s, "_export_slot_taken", None) is not None for s in ex.seqs)
         ev = ex.finish(interprocess=ipc)
         for seq in ex.seqs:

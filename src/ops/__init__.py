@@ -491,6 +491,12 @@ DECODE_TILE_CFG = {
     (14336, 4096, 4, 128): (128, 64, 1),   #                 57.2 vs 54.7
     (4096, 14336, 3, 64): (64, 128, 4),    # down  28.3 vs 40.0
     (4096, 14336, 3, 128): (128, 64, 8),   #       38.3 vs 75.3
+    # the bench's 32-row bucket, round-4 sweep (bench/micro_tp_tiles.py --shapes 8b, profiles/micro_8b_tiles_r4.jsonl,
+    # cold us) confirmed in the real graph: bench 50.49 -> 51.45 req/s with all three, same box
+    # (profiles/bench_r4_tile_ab.jsonl; gate/up alone 50.94, o alone 50.44)
+    (4096, 4096, 3, 32): (32, 256, 2),     # o      13.96 vs 15.44 for (64, 256, 4)
+    (14336, 4096, 4, 32): (128, 128, 1),   # gate/up + SiLU 42.08 vs 43.96 for (112, 128, 1)
+    (4096, 14336, 3, 32): (64, 128, 4),    # down   29.6 vs 30.2 for (64, 256, 4)
     # tensor-parallel shards, 32 rows (bench/micro_tp_tiles.py, profiles/micro_tp_tiles_r4.jsonl, cold, us):
     # (mode 3 needs N / wr <= 128 statistics tiles: the 70B shard's wr = 32 winners, 9.96 / 17.12 us, would
     # disable the fused decode path, so the best wr >= 64 tiles)

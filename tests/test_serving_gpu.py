@@ -106,11 +106,12 @@ def test_gpu_disaggregated_workers_over_rpc():
     asyncio.run(main())
 
 
-def test_gpu_disaggregated_ipc_landing_zone():
+def test_gpu_disaggregated_ipc_landing_zone(monkeypatch):
     """Prefill worker (this process) -> decode worker (a separate process on the same GPU): the
     packed prompt KV goes by device-to-device copy into the decode worker's IPC landing zone (the
     xGMI path between two GPUs of a node) and only metadata crosses the socket; tokens match a
-    colocated worker."""
+    colocated worker. The completion hand-off runs as an IPC event here (opt-in: DIE_KV_IPC_EVENT=1)."""
+    monkeypatch.setenv("DIE_KV_IPC_EVENT", "1")
     import os
     import subprocess
     import sys
