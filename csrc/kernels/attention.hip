@@ -402,7 +402,6 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
     int hkv, float scale_log2, int maxp, int dbg, AttnDecodeFuse fz, const int64_t* __restrict__ slot_mapping) {
   constexpr int QI = (G * 256 + 1023) / 1024;  // LDS-DMA instructions for the query rows
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  warm_kernargs<208>();  // the explicit arguments end at 208 (slot_mapping, after the 88-byte fz at 96)
   float* ml = reinterpret_cast<float*>(smem + 2 * V3_BUF);
   float* ob = reinterpret_cast<float*>(smem + 2 * V3_BUF + V3_ML);
   int* ctl = reinterpret_cast<int*>(smem + 2 * V3_BUF + V3_MERGE);

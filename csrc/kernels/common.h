@@ -120,20 +120,6 @@ __device__ __forceinline__ float hash_uniform(uint64_t seed, uint64_t a, uint64_
   return ((float)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);
 }
 
-// Kernel entry: one scalar load from every 64-byte line of the first BYTES of the kernel-argument segment, all
-// in flight together behind ONE wait. The compiler otherwise loads each argument at its first use and waits
-// there, so a kernel that branches on a few arguments before its first memory operation pays several serial
-// round trips to wherever the launch's argument block sits (L2 / MALL / HBM) before any data moves; after this
-// every later argument load hits the scalar cache. BYTES must not exceed the explicit arguments' size.
-template <int BYTES>
-__device__ __forceinline__ void warm_kernargs() {
-  const uint32_t* ka = reinterpret_cast<const uint32_t*>(__builtin_amdgcn_kernarg_segment_ptr());
-  uint32_t acc = 0;
-#pragma unroll
-  for (int o = 0; o < BYTES; o += 64) acc ^= ka[o / 4];
-  asm volatile("" ::"s"(acc));
-}
-
 // Compute units of the current device (256 on MI355X), cached per device: persistent and
 // self-merging kernels size their grids by it.
 static inline int num_cus() {

@@ -554,7 +554,6 @@ __global__ void __launch_bounds__(NTH) gemm_decode_kernel(void* __restrict__ Yv,
                                                           const bf16_t* __restrict__ W, int M, int N_out, int K,
                                                           GemmDecodeFuse fz) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  warm_kernargs<56 + (int)sizeof(GemmDecodeFuse)>();  // Y .. K = 56 bytes, then fz
   long long t0 = 0;
   if (fz.ts != nullptr) t0 = __builtin_amdgcn_s_memrealtime();
   gd_body<WR, EPI, S, NT, KC, XR, SKC>(smem, Yv, ldy, X, ldx, W, M, N_out, K, fz, blockIdx.x, blockIdx.y, gridDim.y);
