@@ -155,22 +155,36 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
       const int per = ((vocab / 8 + splits - 1) / splits) * 8;
       const int lo = min(vocab, sp * per), hi = min(vocab, lo + per);
       const ArgMax b = row_argmax(row, lo, hi, red);
+      __shared__ int is_last;
       if (threadIdx.x == 0) {
         uint32_t* pr = part + ((int64_t)r * splits + sp) * 2;
         __hip_atomic_store(pr, __float_as_uint(b.v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(pr + 1, (uint32_t)b.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (__hip_atomic_fetch_add(cnt + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == splits - 1) {
-          ArgMax w{-INFINITY, 0x7fffffff};
-          for (int q = 0; q < splits; ++q) {  // slices in order: ties keep the lowest index
-            const uint32_t* pq = part + ((int64_t)r * splits + q) * 2;
-            const ArgMax c{__uint_as_float(__hip_atomic_load(pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
-                           (int)__hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
-            w = better(w, c);
-          }
-          out[r] = w.i < vocab ? w.i : 0;
-          __hip_atomic_store(cnt + r, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        is_last = __hip_atomic_fetch_add(cnt + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == splits - 1;
+      }
+      __syncthreads();
+      if (!is_last || threadIdx.x >= 64) return;
+      // last arriver: lane q loads slice q's (max, index) — every slice in ONE round trip (a loop over the slices
+      // in one lane waited for each agent-scope load in turn: ~11 us for 8 slices) — reduced in the wave;
+      // better() is a total order (value, then lowest index), so the result does not depend on the order
+      const int lane = threadIdx.x;
+      ArgMax w{-INFINITY, 0x7fffffff};
+      if (lane < splits) {
+        const uint32_t* pq = part + ((int64_t)r * splits + lane) * 2;
+        w = ArgMax{__uint_as_float(__hip_atomic_load(pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                   (int)__hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        ArgMax y;
+        y.v = __shfl_xor(w.v, o, 64);
+        y.i = __shfl_xor(w.i, o, 64);
+        w = better(w, y);
+      }
+      if (lane == 0) {
+        out[r] = w.i < vocab ? w.i : 0;
+        __hip_atomic_store(cnt + r, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return;
     }
