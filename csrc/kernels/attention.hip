@@ -674,19 +674,32 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
           const int64_t s0 = ((int64_t)seq * hq + head) * maxp;
           float M = NEG_BIG, L = 0.f;
           float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-          for (int p = 0; p < nparts; ++p) {
-            const auto mv =
-                __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rm, (int)((s0 + p) * 2) * 4, 0, 16));
-            const auto ov = __builtin_bit_cast(
-                float4, __builtin_amdgcn_raw_buffer_load_b128(ro, (int)((s0 + p) * D + d) * 4, 0, 16));
-            const float Mn = fmaxf(M, mv.x);
-            const float a = exp2f(M - Mn), bb = exp2f(mv.x - Mn);
-            L = L * a + mv.y * bb;
-            acc.x = acc.x * a + ov.x * bb;
-            acc.y = acc.y * a + ov.y * bb;
-            acc.z = acc.z * a + ov.z * bb;
-            acc.w = acc.w * a + ov.w * bb;
-            M = Mn;
+          // the parts' loads go out PB at a time (indices clamped, the surplus masked below): one round trip
+          // per PB parts instead of one per part (Llama-3-70B's TP=8 shard merges 5 parts per pair)
+          constexpr int PB = 8;
+          for (int p0 = 0; p0 < nparts; p0 += PB) {
+            float2 mv[PB];
+            float4 ov[PB];
+#pragma unroll
+            for (int j = 0; j < PB; ++j) {
+              const int p = min(p0 + j, nparts - 1);
+              mv[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rm, (int)((s0 + p) * 2) * 4, 0, 16));
+              ov[j] = __builtin_bit_cast(float4,
+                                         __builtin_amdgcn_raw_buffer_load_b128(ro, (int)((s0 + p) * D + d) * 4, 0, 16));
+            }
+#pragma unroll
+            for (int j = 0; j < PB; ++j) {  // branch-free (a break would let the loads sink back to their uses)
+              const bool ok = p0 + j < nparts;
+              const float mx = ok ? mv[j].x : NEG_BIG;
+              const float Mn = fmaxf(M, mx);
+              const float a = exp2f(M - Mn), bb = ok ? exp2f(mx - Mn) : 0.f;
+              L = L * a + mv[j].y * bb;
+              acc.x = acc.x * a + ov[j].x * bb;
+              acc.y = acc.y * a + ov[j].y * bb;
+              acc.z = acc.z * a + ov[j].z * bb;
+              acc.w = acc.w * a + ov[j].w * bb;
+              M = Mn;
+            }
           }
           const float inv = L > 0.f ? 1.f / L : 0.f;
           uint2 pk;
