@@ -12,3 +12,5 @@ timeout -k 10 300 python -u bench/tp_probe.py --preset llama3-8b --tp 2 --steps 
 grep -h '^{' gpurun_out/tl_tp8.log
 timeout -k 10 400 python bench.py --steps 10 --warmup 2 > gpurun_out/tl_bench.log 2>&1 || { tail -5 gpurun_out/tl_bench.log; exit 3; }
 grep '^{' gpurun_out/tl_bench.log
+DIE_TILE_OVERRIDE="4096,4096,3,32=64,256,4" timeout -k 10 400 python bench.py --steps 10 --warmup 2 > gpurun_out/tl_bench_o64.log 2>&1 || { tail -5 gpurun_out/tl_bench_o64.log; exit 6; }
+grep '^{' gpurun_out/tl_bench_o64.log
