@@ -221,6 +221,7 @@ def main():
         lats = [x for g in gathered for x in g]
     total_req = args.steps * args.batch * replicas
     rps = total_req / elapsed
+    res = None
     if rank == 0:
         label = model_label(args.preset)
         res = {
@@ -260,10 +261,62 @@ def main():
                 "engine_init_s": round(init_s, 1),
             },
         }
-        print(json.dumps(res), flush=True)
+    dog = None
+    if world > 1 and on_gpu and tp is None and os.environ.get("DIE_XGPU_PROBE", "1") != "0":
+        # after the timed region: RCCL / one-shot IPC all-reduce / landing-zone KV hop between the real GPUs
+        # (src/parallel/xgpu_probe.py), reported in notes. A watchdog armed until the process group is gone
+        # prints the result without the probe (once) and ends the rank if anything after the timed region stalls.
+        dog = _Watchdog(res, rank, 150.0)
+        try:
+            from src.parallel.xgpu_probe import xgpu_probe
+
+            probe = xgpu_probe(rank, world, dev)
+        except Exception as e:  # noqa: BLE001 — the bench result stands on its own
+            probe = {"error": str(e)[:200]}
+        if rank == 0:
+            res["notes"]["xgpu_probe"] = probe
+    if rank == 0:
+        if dog is not None:
+            dog.emit()
+        else:
+            print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if dog is not None:
+        dog.cancel()
+
+
+class _Watchdog:
+    """Prints rank 0's result line exactly once — normally (emit), or from the timer with the probe marked as
+    stalled — and on expiry ends the process (os._exit) so that no rank waits on a peer forever."""
+
+    def __init__(self, res, rank: int, budget_s: float):
+        import threading
+
+        self.res, self.rank, self.budget_s = res, rank, budget_s
+        self._lock = threading.Lock()
+        self._printed = False
+        self._timer = threading.Timer(budget_s, self._expire)
+        self._timer.daemon = True
+        self._timer.start()
+
+    def emit(self) -> None:
+        with self._lock:
+            if not self._printed and self.rank == 0:
+                print(json.dumps(self.res), flush=True)
+            self._printed = True
+
+    def _expire(self) -> None:
+        with self._lock:
+            if not self._printed and self.rank == 0:
+                self.res["notes"].setdefault("xgpu_probe", {"error": f"no result within {self.budget_s:.0f} s"})
+                print(json.dumps(self.res), flush=True)
+            self._printed = True
+        os._exit(0)
+
+    def cancel(self) -> None:
+        self._timer.cancel()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,186 @@
+"""
+Cross-GPU probe run by a multi-GPU ``bench.py`` after its timed region: the data movements the serving
+configurations rely on, measured between real GPUs of the node (one process per GPU) instead of between
+two processes sharing one GPU.
+
+* ``rccl_allreduce``: RCCL (``torch.distributed`` backend "nccl") all-reduce of a 256 MiB bf16 tensor —
+  algorithm and bus bandwidth (bus = 2 (n - 1) / n x bytes / time, the per-link figure a ring over xGMI is
+  bound by).
+* ``ipc_allreduce``: the one-shot IPC all-reduce of the tensor-parallel decode path
+  (:class:`src.parallel.custom_allreduce.CustomAllReduce`, the protocol the fused row-parallel GEMM epilogue
+  uses) at decode sizes (32 rows x 4,096 / 8,192 bf16): latency, and its sum checked against RCCL's.
+* ``kv_hop``: the disaggregated prefill -> decode KV hand-off — rank 2k gathers a 128 MiB packet straight
+  into rank 2k+1's IPC landing zone (:class:`IPCLandingZone` / :class:`IPCSender`, shader stores over
+  xGMI), rank 2k+1 checks every byte; GB/s of the copy.
+
+Everything is bounded: the caller runs this under a watchdog (bench.py), every device wait is an event
+poll or a collective, and each part reports an error string instead of raising. Reference: the reference
+has no GPU path; these are the transports behind its placement / disaggregation claims
+(`/root/reference/README.md:14-15`, `/root/reference/src/router.py:140-184`).
+
+Rehearsal with N ranks on ONE GPU (no RCCL: it refuses two ranks on one device; gloo coordinates)::
+
+    python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 \\
+        -m src.parallel.xgpu_probe --same-device
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import time
+from typing import Any, Dict, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def _events():
+    return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+
+def _rccl_allreduce(dev, world: int, group=None) -> Dict[str, Any]:
+    n = 128 << 20  # 128 M bf16 = 256 MiB
+    t = torch.ones(n, dtype=torch.bfloat16, device=dev)
+    for _ in range(2):
+        dist.all_reduce(t, group=group)
+    torch.cuda.synchronize(dev)
+    iters = 5
+    e0, e1 = _events()
+    dist.barrier(group=group)
+    e0.record()
+    for _ in range(iters):
+        dist.all_reduce(t, group=group)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    s = e0.elapsed_time(e1) / 1e3 / iters
+    nbytes = n * 2
+    return {"bytes": nbytes, "ms": round(s * 1e3, 3), "algbw_GBps": round(nbytes / s / 1e9, 1),
+            "busbw_GBps": round(2 * (world - 1) / world * nbytes / s / 1e9, 1)}
+
+
+def _ipc_allreduce(rank: int, world: int, dev, group=None, rccl_group=None) -> Dict[str, Any]:
+    from src.parallel.custom_allreduce import CustomAllReduce
+
+    car = CustomAllReduce(rank, world, group=group)
+    out: Dict[str, Any] = {}
+    try:
+        g = torch.Generator(device="cpu").manual_seed(17 + rank)
+        for rows, hid in ((32, 4096), (32, 8192)):
+            x = (torch.randn(rows, hid, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+            y = car.all_reduce(x)
+            torch.cuda.synchronize(dev)
+            ok = None
+            if rccl_group is not False:  # the reference sum: RCCL over the same inputs (fp32 accumulate)
+                ref = x.float()
+                dist.all_reduce(ref, group=rccl_group)
+                ok = bool(torch.allclose(y.float(), ref, rtol=2e-2, atol=2e-2))
+            for _ in range(5):
+                car.all_reduce(x, out=y)
+            torch.cuda.synchronize(dev)
+            iters = 50
+            dist.barrier(group=group)
+            e0, e1 = _events()
+            e0.record()
+            for _ in range(iters):
+                car.all_reduce(x, out=y)
+            e1.record()
+            torch.cuda.synchronize(dev)
+            out[f"{rows}x{hid}"] = {"bytes": rows * hid * 2, "us": round(e0.elapsed_time(e1) * 1e3 / iters, 2),
+                                    "matches_rccl": ok}
+        out["error_word"] = bool(car.error())
+    finally:
+        dist.barrier(group=group)
+        car.close()
+    return out
+
+
+def _kv_hop(rank: int, world: int, dev, group=None) -> Dict[str, Any]:
+    from src.parallel.kv_transfer import IPCLandingZone, IPCSender
+
+    nbytes = 128 << 20
+    recv = rank % 2 == 1
+    paired = rank ^ 1 < world
+    zone = IPCLandingZone(dev, capacity=256 << 20, uncached=True) if (recv and paired) else None
+    info = {"handle": zone.handle, "seg": zone.seg_bytes} if zone is not None else None
+    allinfo = [None] * world
+    dist.all_gather_object(allinfo, info, group=group)
+    res: Dict[str, Any] = {"bytes": nbytes, "pairs": world // 2}
+    g = torch.Generator(device="cpu").manual_seed(99)
+    payload = torch.randint(-30000, 30000, (nbytes // 2,), dtype=torch.int16, generator=g)
+    sender = None
+    try:
+        if not recv and paired:
+            peer = allinfo[rank + 1]
+            sender = IPCSender(peer["handle"], peer["seg"], dev)
+            src = payload.to(dev).view(torch.bfloat16)
+            sender.write(0, src)  # warm the mapping
+            torch.cuda.synchronize(dev)
+            e0, e1 = _events()
+            e0.record(sender.stream)
+            done = sender.write(0, src)
+            e1.record(sender.stream)
+            done.synchronize()
+            res["send_ms"] = round(e0.elapsed_time(e1), 3)
+            res["GBps"] = round(nbytes / (e0.elapsed_time(e1) / 1e3) / 1e9, 1)
+        dist.barrier(group=group)  # the sender's copy is complete before the receiver reads its zone
+        if zone is not None:
+            got = zone.views[0][:nbytes].view(torch.int16).cpu()
+            res["receiver_bytes_match"] = bool(torch.equal(got, payload))
+        else:
+            res["receiver_bytes_match"] = None
+        flags = [None] * world
+        dist.all_gather_object(flags, {k: res.get(k) for k in ("GBps", "receiver_bytes_match")}, group=group)
+        res["per_rank"] = flags
+    finally:
+        dist.barrier(group=group)
+        if sender is not None:
+            sender.close()
+        if zone is not None:
+            zone.close()
+    return res
+
+
+def xgpu_probe(rank: int, world: int, dev, rccl: bool = True, group=None) -> Dict[str, Any]:
+    """Run the three parts (each catching its own failure); returns rank 0's view (the same dict on every
+    rank for the RCCL part; the KV hop reports every pair through ``per_rank``)."""
+    out: Dict[str, Any] = {"world": world}
+    t0 = time.perf_counter()
+    if rccl:
+        try:
+            out["rccl_allreduce"] = _rccl_allreduce(dev, world, group)
+        except Exception as e:  # noqa: BLE001 — reported, not raised: the bench result stands on its own
+            out["rccl_allreduce"] = {"error": str(e)[:200]}
+    try:
+        out["ipc_allreduce"] = _ipc_allreduce(rank, world, dev, group, None if rccl else False)
+    except Exception as e:  # noqa: BLE001
+        out["ipc_allreduce"] = {"error": str(e)[:200]}
+    try:
+        out["kv_hop"] = _kv_hop(rank, world, dev, group)
+    except Exception as e:  # noqa: BLE001
+        out["kv_hop"] = {"error": str(e)[:200]}
+    out["probe_s"] = round(time.perf_counter() - t0, 2)
+    return out
+
+
+def main() -> None:
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on cuda:0 (a one-GPU rehearsal; gloo coordinates, no RCCL part)")
+    a = ap.parse_args()
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", 0 if a.same_device else local)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo" if a.same_device else "nccl")
+    res = xgpu_probe(rank, world, dev, rccl=not a.same_device)
+    if rank == 0:
+        print(json.dumps({"bench": "xgpu_probe", **res}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
