@@ -96,48 +96,61 @@ def _ipc_allreduce(rank: int, world: int, dev, group=None, rccl_group=None) -> D
 
 
 def _kv_hop(rank: int, world: int, dev, group=None) -> Dict[str, Any]:
+    """Every rank runs the same collectives in the same order whatever fails locally (a local error is
+    recorded and reported through the final gather, never raised between two collectives)."""
     from src.parallel.kv_transfer import IPCLandingZone, IPCSender
 
     nbytes = 128 << 20
     recv = rank % 2 == 1
-    paired = rank ^ 1 < world
-    zone = IPCLandingZone(dev, capacity=256 << 20, uncached=True) if (recv and paired) else None
-    info = {"handle": zone.handle, "seg": zone.seg_bytes} if zone is not None else None
-    allinfo = [None] * world
-    dist.all_gather_object(allinfo, info, group=group)
+    paired = (rank ^ 1) < world
     res: Dict[str, Any] = {"bytes": nbytes, "pairs": world // 2}
+    err: Optional[str] = None
+    zone = sender = None
+    info = None
+    try:
+        if recv and paired:
+            zone = IPCLandingZone(dev, capacity=256 << 20, uncached=True)
+            info = {"handle": zone.handle, "seg": zone.seg_bytes}
+    except Exception as e:  # noqa: BLE001
+        err = f"zone: {e}"[:200]
+    allinfo: list = [None] * world
+    dist.all_gather_object(allinfo, info, group=group)
     g = torch.Generator(device="cpu").manual_seed(99)
     payload = torch.randint(-30000, 30000, (nbytes // 2,), dtype=torch.int16, generator=g)
-    sender = None
     try:
-        if not recv and paired:
+        if not recv and paired and allinfo[rank + 1] is not None:
             peer = allinfo[rank + 1]
             sender = IPCSender(peer["handle"], peer["seg"], dev)
             src = payload.to(dev).view(torch.bfloat16)
-            sender.write(0, src)  # warm the mapping
-            torch.cuda.synchronize(dev)
+            sender.write(0, src).synchronize()  # warm the mapping
             e0, e1 = _events()
             e0.record(sender.stream)
-            done = sender.write(0, src)
+            sender.write(0, src)
             e1.record(sender.stream)
-            done.synchronize()
-            res["send_ms"] = round(e0.elapsed_time(e1), 3)
-            res["GBps"] = round(nbytes / (e0.elapsed_time(e1) / 1e3) / 1e9, 1)
-        dist.barrier(group=group)  # the sender's copy is complete before the receiver reads its zone
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            res["send_ms"] = round(ms, 3)
+            res["GBps"] = round(nbytes / (ms / 1e3) / 1e9, 1)
+    except Exception as e:  # noqa: BLE001
+        err = f"send: {e}"[:200]
+    dist.barrier(group=group)  # the sender's copy is complete before the receiver reads its zone
+    match = None
+    try:
         if zone is not None:
-            got = zone.views[0][:nbytes].view(torch.int16).cpu()
-            res["receiver_bytes_match"] = bool(torch.equal(got, payload))
-        else:
-            res["receiver_bytes_match"] = None
-        flags = [None] * world
-        dist.all_gather_object(flags, {k: res.get(k) for k in ("GBps", "receiver_bytes_match")}, group=group)
-        res["per_rank"] = flags
-    finally:
-        dist.barrier(group=group)
-        if sender is not None:
-            sender.close()
-        if zone is not None:
-            zone.close()
+            match = bool(torch.equal(zone.views[0][:nbytes].view(torch.int16).cpu(), payload))
+    except Exception as e:  # noqa: BLE001
+        err = f"check: {e}"[:200]
+    flags: list = [None] * world
+    dist.all_gather_object(flags, {"GBps": res.get("GBps"), "receiver_bytes_match": match, "error": err},
+                           group=group)
+    res["per_rank"] = flags
+    dist.barrier(group=group)
+    for obj in (sender, zone):
+        try:
+            if obj is not None:
+                obj.close()
+        except Exception:  # noqa: BLE001
+            pass
     return res
 
 
