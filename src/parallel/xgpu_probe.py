@@ -88,11 +88,67 @@ def _ipc_allreduce(rank: int, world: int, dev, group=None, rccl_group=None) -> D
             torch.cuda.synchronize(dev)
             out[f"{rows}x{hid}"] = {"bytes": rows * hid * 2, "us": round(e0.elapsed_time(e1) * 1e3 / iters, 2),
                                     "matches_rccl": ok}
+        out["fused_row_parallel"] = _fused_row_parallel(rank, world, dev, car, group, rccl_group)
         out["error_word"] = bool(car.error())
     finally:
         dist.barrier(group=group)
         car.close()
     return out
+
+
+def _timed(fn, dev, group, iters: int = 20) -> float:
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize(dev)
+    dist.barrier(group=group)
+    e0, e1 = _events()
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    return e0.elapsed_time(e1) * 1e3 / iters
+
+
+def _fused_row_parallel(rank: int, world: int, dev, car, group=None, rccl_group=None) -> Dict[str, Any]:
+    """The tensor-parallel decode layer's row-parallel projections at Llama-3-70B's shard shapes for this group
+    size (o: K = 8,192 / world, down: K = 28,672 / world, N = 8,192, 32 rows): ONE launch whose column tiles'
+    last arrivers exchange over the group (gemm_decode_car) against the same GEMM without the exchange
+    (mode 3 on the local K shard) — the difference is what the one-shot exchange costs over the links."""
+    from src import ops
+
+    res: Dict[str, Any] = {}
+    shapes = [("o", 8192 // world, 8192), ("down", 28672 // world, 8192)]
+    if car.ranks_per_gpu > 1:  # a one-GPU rehearsal: a shape whose waiting tiles leave room for every rank's grid
+        shapes = [("rehearsal", 1024, 2048)]
+    for name, k, n in shapes:
+        if k % 256:
+            res[name] = {"skipped": f"K = {k}"}
+            continue
+        wr, kc, sk = ops.decode_tile(n, k, 3, 32)
+        if not car.fused_ok(n // wr, (n // wr) * sk):
+            res[name] = {"skipped": "fused_ok"}
+            continue
+        g = torch.Generator(device="cpu").manual_seed(5 + rank)
+        x = (torch.randn(32, k, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+        w = (torch.randn(n, k, generator=g) * 0.02).to(torch.bfloat16).to(dev)
+        resid = torch.zeros(32, n, dtype=torch.bfloat16, device=dev)
+        ssp = torch.zeros(n // wr, ops.SSP_LD, dtype=torch.float32, device=dev)
+        cnt = torch.zeros(n // wr, dtype=torch.int32, device=dev)
+        car.row_parallel_residual(x, w, resid, ssp, cnt, wr, kc, sk, tiled=False)
+        torch.cuda.synchronize(dev)
+        ok = None
+        if rccl_group is not False:
+            ref = x.float() @ w.float().t()
+            dist.all_reduce(ref, group=rccl_group)
+            ok = bool(torch.allclose(resid.float(), ref, rtol=3e-2, atol=3e-2))
+        fused = _timed(lambda: car.row_parallel_residual(x, w, resid, ssp, cnt, wr, kc, sk, tiled=False), dev, group)
+        resid2 = torch.zeros_like(resid)
+        ssp2, cnt2 = torch.zeros_like(ssp), torch.zeros_like(cnt)
+        local = _timed(lambda: ops.linear_slab_residual(x, w, resid2, ssp2, cnt2, wr, sk, kc=kc), dev, group)
+        res[name] = {"K": k, "tile": [wr, kc, sk], "fused_us": round(fused, 2), "local_us": round(local, 2),
+                     "exchange_us": round(fused - local, 2), "matches_rccl": ok}
+    return res
 
 
 def _kv_hop(rank: int, world: int, dev, group=None) -> Dict[str, Any]:
