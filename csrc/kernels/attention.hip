@@ -407,21 +407,8 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
   int* ctl = reinterpret_cast<int*>(smem + 2 * V3_BUF + V3_MERGE);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, row = lane & 31;
   const int pairs = num_seqs * hkv;
-  // chunks per part: from the step's ACTUAL longest context when there are fewer pairs than workgroups (a TP
-  // shard: Llama-3-70B TP=8 has 32 pairs, and the graph-static max_ctx of 2,048 made every part 2 chunks long
-  // with 96 of 256 workgroups busy at 576 keys; the real bound gives 1-chunk parts on 160). Every workgroup
-  // computes the same C (a part count is implied by it in the merge). One vector round trip over ctx_lens; with
-  // a pair per workgroup or more (Llama-3-8B, 256 pairs) the static bound gives the same split without it.
-  int maxc = maxp;
-  if (pairs < (int)gridDim.x) {
-    int mx = 1;
-    for (int i = lane; i < num_seqs; i += 64) mx = max(mx, ctx_lens[i]);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
-    maxc = min(maxp, (__builtin_amdgcn_readfirstlane(mx) + DEC_KEYS - 1) / DEC_KEYS);
-  }
-  const int C = max(1, min(maxc, (maxc * pairs + (int)gridDim.x - 1) / (int)gridDim.x));
-  const int np = (maxc + C - 1) / C;
+  const int C = max(1, min(maxp, (maxp * pairs + (int)gridDim.x - 1) / (int)gridDim.x));
+  const int np = (maxp + C - 1) / C;
   const int n_tasks = pairs * np;
   const int pch = lane & 15;
   // diagnostics (bench/micro_attn_timeline.py): [entry, first chunk landed, prologue done, stream done,
