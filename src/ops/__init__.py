@@ -373,6 +373,9 @@ def linear_silu_mul_rownorm(x: torch.Tensor, w_gate_up: torch.Tensor, ssp_in: to
 # shard 27.1 us vs 30.0 for the best full-K tile (32, 256). Dense 8B shapes lose with split-K (not listed).
 DECODE_SILU_SPLITK_CFG = {
     (3584, 8192, 32): (64, 128, 2),   # round 4 sweep (micro_tp_tiles_r4): 26.84 us vs 30.36 for (64, 256, 2) cold
+    # 64 / 128 rows (micro_tp_tiles --rows 64 / 128, profiles/micro_tp_tiles_r4_rows64_128.jsonl, cold us)
+    (3584, 8192, 64): (112, 128, 4),  # 34.76 vs 41.28 for the full-K (32, 128)
+    (3584, 8192, 128): (64, 128, 2),  # 46.36 vs 52.12
 }
 
 
@@ -506,6 +509,8 @@ DECODE_TILE_CFG = {
     (4096, 7168, 3, 32): (64, 128, 4),     # 8B TP=2 down   18.40 vs 18.88
     (3072, 4096, 2, 32): (48, 128, 4),     # 8B TP=2 qkv    11.08 vs 11.80
     (7168, 4096, 4, 32): (64, 128, 1),     # 8B TP=2 gate/up 24.84 vs 25.68
+    (1280, 8192, 2, 64): (32, 256, 4),     # 70B TP=8 qkv at 64 rows  13.80 vs 14.40 for (32, 128, 4)
+    (8192, 1024, 3, 128): (64, 64, 2),     # 70B TP=8 o at 128 rows   17.52 vs 18.20 for (64, 128, 2)
 }
 
 

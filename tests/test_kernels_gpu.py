@@ -642,7 +642,10 @@ def test_embed_sumsq_matches_gather_and_fp32_sumsq(dev, rows):
 
 
 @pytest.mark.parametrize("n,k,wr,kc,sk,m", [(3584, 8192, 64, 256, 2, 32), (3584, 8192, 64, 256, 2, 7),
-                                           (2048, 1024, 64, 128, 4, 32), (2048, 1024, 128, 64, 2, 1)])
+                                           (2048, 1024, 64, 128, 4, 32), (2048, 1024, 128, 64, 2, 1),
+                                           # the 70B TP=8 shard's 64- / 128-row tiles (DECODE_SILU_SPLITK_CFG)
+                                           (3584, 8192, 112, 128, 4, 64), (3584, 8192, 112, 128, 4, 50),
+                                           (3584, 8192, 64, 128, 2, 128), (3584, 8192, 64, 128, 2, 100)])
 def test_gate_up_split_k_silu_matches_full_k(dev, n, k, wr, kc, sk, m):
     """Mode 6 (the norm-scaled SiLU gate/up with K split over sk workgroups, fp32 partial slabs, last-arriver
     finish) against mode 4 (one pass) and an fp32 reference; the tickets are re-armed for the next launch."""
