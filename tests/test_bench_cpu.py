@@ -57,3 +57,26 @@ def test_bench_json_contract(nproc, extra, par, replicas):
     # value is the whole-job request rate: steps x batch x replicas over the (max-over-ranks) time
     assert res["value"] == pytest.approx(2 * 4 * replicas / (res["ms_per_step"] * 2 / 1e3), rel=0.02)
     assert res["p50_latency_ms"] > 0
+
+
+def test_bench_watchdog_prints_the_line_once_and_ends_a_stalled_rank():
+    """bench.py's watchdog around the cross-GPU probe: a stall after the timed region still prints rank 0's
+    result line (probe marked as stalled) and ends the process with status 0; a normal emit prints once."""
+    import json
+    import subprocess
+    import sys
+    import time
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "d = bench._Watchdog({'value': 1.0, 'notes': {}}, 0, 0.5); time.sleep(30)") % root
+    t0 = time.time()
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0 and time.time() - t0 < 20, (p.returncode, p.stderr[-2000:])
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1 and "error" in lines[0]["notes"]["xgpu_probe"], p.stdout
+    code = ("import sys; sys.path.insert(0, %r); import bench; "
+            "d = bench._Watchdog({'value': 2.0, 'notes': {}}, 0, 30); d.emit(); d.emit(); d.cancel()") % root
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert p.returncode == 0 and len(lines) == 1 and lines[0]["value"] == 2.0, p.stdout
