@@ -49,18 +49,25 @@ __global__ void topk_softmax_kernel(float* __restrict__ w_out, int* __restrict__
 // thread owns 8-element slices of H for all E experts (Wg, E x H bf16, stays in L2 across tokens).
 // Replaces a hipBLASLt [T, H] x [E, H]^T launch (~10 us at T = 32, E = 8) plus topk_softmax_kernel.
 constexpr int ROUTE_MAX_E = 16;
+// EM: compile-time expert count bound (8 or 16). Every slice's EM router rows are loaded before any is used
+// (rows past E clamped to E - 1 and masked): a `break` at e >= E let the compiler sink each load to its use,
+// one dependent L2 round trip per expert (12.7 us per Mixtral decode layer in the timed window).
+template <int EM>
 __global__ void __launch_bounds__(256) moe_route_kernel(float* __restrict__ w_out, int* __restrict__ id_out,
                                                         const bf16_t* __restrict__ x, int64_t ldx,
                                                         const bf16_t* __restrict__ wg, int H, int E, int K,
                                                         int renorm) {
   __shared__ float red[4][ROUTE_MAX_E];
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float acc[ROUTE_MAX_E];
+  float acc[EM];
 #pragma unroll
-  for (int e = 0; e < ROUTE_MAX_E; ++e) acc[e] = 0.f;
+  for (int e = 0; e < EM; ++e) acc[e] = 0.f;
   const bf16_t* xr = x + (int64_t)t * ldx;
   for (int j = tid * 8; j < H; j += 256 * 8) {
     const uint4 xv = *reinterpret_cast<const uint4*>(xr + j);
+    uint4 wv[EM];
+#pragma unroll
+    for (int e = 0; e < EM; ++e) wv[e] = *reinterpret_cast<const uint4*>(wg + (int64_t)min(e, E - 1) * H + j);
     float xf[8];
     const unsigned xw[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
@@ -69,10 +76,8 @@ __global__ void __launch_bounds__(256) moe_route_kernel(float* __restrict__ w_ou
       xf[2 * i + 1] = bf2f((bf16_t)(xw[i] >> 16));
     }
 #pragma unroll
-    for (int e = 0; e < ROUTE_MAX_E; ++e) {
-      if (e >= E) break;
-      const uint4 wv = *reinterpret_cast<const uint4*>(wg + (int64_t)e * H + j);
-      const unsigned ww[4] = {wv.x, wv.y, wv.z, wv.w};
+    for (int e = 0; e < EM; ++e) {
+      const unsigned ww[4] = {wv[e].x, wv[e].y, wv[e].z, wv[e].w};
       float a = 0.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -81,8 +86,7 @@ __global__ void __launch_bounds__(256) moe_route_kernel(float* __restrict__ w_ou
     }
   }
 #pragma unroll
-  for (int e = 0; e < ROUTE_MAX_E; ++e) {
-    if (e >= E) break;
+  for (int e = 0; e < EM; ++e) {
     float v = acc[e];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -129,7 +133,10 @@ hipError_t launch_moe_route(float* w, int* ids, const bf16_t* x, int64_t ldx, co
   if (E < 1 || E > ROUTE_MAX_E || K < 1 || K > E || H % 8 || ldx % 8 ||
       (reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(wg) & 15))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(moe_route_kernel, dim3(T), dim3(256), 0, s, w, ids, x, ldx, wg, H, E, K, renorm ? 1 : 0);
+  if (E <= 8)
+    hipLaunchKernelGGL(moe_route_kernel<8>, dim3(T), dim3(256), 0, s, w, ids, x, ldx, wg, H, E, K, renorm ? 1 : 0);
+  else
+    hipLaunchKernelGGL(moe_route_kernel<16>, dim3(T), dim3(256), 0, s, w, ids, x, ldx, wg, H, E, K, renorm ? 1 : 0);
   return hipGetLastError();
 }
 
