@@ -17,9 +17,14 @@ def test_xgpu_probe_two_ranks_one_gpu():
 
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    import socket
+
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-           "--master-port", "29531", "-m", "src.parallel.xgpu_probe", "--same-device"]
+           "--master-port", str(port), "-m", "src.parallel.xgpu_probe", "--same-device"]
     p = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     line = [x for x in p.stdout.splitlines() if x.startswith('{"bench": "xgpu_probe"')]
