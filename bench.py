@@ -149,6 +149,7 @@ def main():
             dist.barrier()
             t = torch.zeros(1, device=dev, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dist.all_gather_object([None] * world, 0.0)  # the leader's per-rank elapsed
             dist.all_gather_object([None] * world, [])
             dist.barrier()
             dist.destroy_process_group()
@@ -212,9 +213,12 @@ def main():
     gen_tok = st["generated_tokens"] - stats0["generated_tokens"]
     prefill_s = st["prefill_time"] - stats0["prefill_time"]
     decode_s = st["decode_time"] - stats0["decode_time"]
+    rank_elapsed = [elapsed]
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        rank_elapsed = [None] * world
+        dist.all_gather_object(rank_elapsed, elapsed)
         elapsed = float(t.item())
         gathered = [None] * world
         dist.all_gather_object(gathered, lats)
@@ -261,6 +265,8 @@ def main():
                 "engine_init_s": round(init_s, 1),
             },
         }
+        if world > 1 and tp is None:  # the value uses the slowest replica; the spread shows stragglers
+            res["notes"]["rank_elapsed_s"] = [round(x, 3) for x in rank_elapsed]
     dog = None
     if world > 1 and on_gpu and tp is None and os.environ.get("DIE_XGPU_PROBE", "1") != "0":
         # after the timed region: RCCL / one-shot IPC all-reduce / landing-zone KV hop between the real GPUs
