@@ -78,6 +78,13 @@ class LLMEngine:
         self.scheduler = Scheduler(cfg, self.blocks, self.max_model_len, swap_capacity_blocks=swap_blocks)
         self.seqs: Dict[str, Sequence] = {}
         self._step_est = 0.004  # EMA of one decode step (s): sizes windows that must end by a deadline
+        # disaggregated decode: imported prompts join the running batch directly (no waiting queue), so a burst of
+        # imports would otherwise join one decode WINDOW late each; while imports keep arriving (the last one less
+        # than this long ago) the engine runs single steps so the next import joins at the next step
+        import os
+
+        self._import_settle_s = float(os.environ.get("DIE_IMPORT_SETTLE_MS", "3")) / 1e3
+        self._last_import = -1e9
         self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "finished": 0, "prefill_time": 0.0,
                       "decode_time": 0.0, "steps": 0, "prefix_hit_tokens": 0}
         logger.info("KV pool: %d blocks x %d tokens = %.1f GiB (%d tokens)", nblocks, cfg.block_size,
@@ -154,6 +161,7 @@ class LLMEngine:
 
         if packet.block_size != self.cfg.block_size:
             raise ValueError("block size mismatch between prefill and decode workers")
+        self._last_import = time.perf_counter()
         seq = Sequence(packet.request_id, list(packet.prompt_ids), dataclasses.replace(sampling),
                        on_finish=on_finish, imported_kv=True)
         seq.output_ids = [int(packet.first_token)]
@@ -364,7 +372,7 @@ class LLMEngine:
         if not self.cfg.async_decode or not getattr(self.runner, "supports_multistep", False):
             return 0
         sch = self.scheduler
-        if sch.waiting or sch.swapped or len(sch.running) != len(seqs):
+        if sch.waiting or sch.swapped or len(sch.running) != len(seqs) or self._importing():
             return 0
         ids = {id(s) for s in seqs}
         if any(id(s) not in ids or s.status != SeqStatus.RUNNING or s.in_prefill for s in sch.running):
@@ -379,13 +387,17 @@ class LLMEngine:
                 return 0
         return k
 
+    def _importing(self) -> bool:
+        """A burst of imported (disaggregated) prompts is still arriving."""
+        return time.perf_counter() - self._last_import < self._import_settle_s
+
     def _decode_window(self, seqs: List[Sequence]) -> int:
         """How many decode steps to run before the host looks again: 1 while requests wait for
         admission (they must not sit behind a window), otherwise up to cfg.decode_window, no
         further than the longest remaining generation and the context limit, and only if KV
         slots for the whole window can be reserved now."""
         kmax = int(getattr(self.cfg, "decode_window", 1))
-        if kmax <= 1 or not getattr(self.runner, "supports_multistep", False):
+        if kmax <= 1 or not getattr(self.runner, "supports_multistep", False) or self._importing():
             return 1
         if self.scheduler.waiting:
             # prompts held for a larger prefill step (Scheduler._defer_prefill): a window that ends by
