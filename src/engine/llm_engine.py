@@ -15,6 +15,7 @@ finish and LRU/TTL eviction only starts under real memory pressure.
 
 from __future__ import annotations
 
+import collections
 import dataclasses
 import logging
 import time
@@ -85,6 +86,11 @@ class LLMEngine:
 
         self._import_settle_s = float(os.environ.get("DIE_IMPORT_SETTLE_MS", "3")) / 1e3
         self._last_import = -1e9
+        # open-loop arrivals: times of the requests that arrived while sequences were decoding (a closed-loop wave
+        # arrives while the engine is idle and is not counted); they cap the decode window so that a new prompt
+        # waits about half an inter-arrival gap for admission, not a whole window plus a queued continuation
+        self._dec_arrivals: "collections.deque[float]" = collections.deque(maxlen=64)
+        self._arrival_lookback_s = float(os.environ.get("DIE_ARRIVAL_WINDOW_MS", "250")) / 1e3
         self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "finished": 0, "prefill_time": 0.0,
                       "decode_time": 0.0, "steps": 0, "prefix_hit_tokens": 0}
         logger.info("KV pool: %d blocks x %d tokens = %.1f GiB (%d tokens)", nblocks, cfg.block_size,
@@ -136,6 +142,8 @@ class LLMEngine:
             seq.sampling.max_tokens = 1
             seq.export_kv = True  # type: ignore[attr-defined]
         self.seqs[request_id] = seq
+        if self.scheduler.running:
+            self._dec_arrivals.append(time.perf_counter())
         self.scheduler.add(seq)
         self.stats["prompt_tokens"] += len(prompt_ids)
         return seq
@@ -377,7 +385,7 @@ class LLMEngine:
         ids = {id(s) for s in seqs}
         if any(id(s) not in ids or s.status != SeqStatus.RUNNING or s.in_prefill for s in sch.running):
             return 0
-        k = min(int(self.cfg.decode_window),
+        k = min(int(self.cfg.decode_window), self._arrival_cap(),
                 min(s.sampling.max_tokens - len(s.output_ids) - pending for s in seqs),
                 min(self.max_model_len - (len(s) + pending) + 1 for s in seqs))
         if k <= 1:
@@ -386,6 +394,18 @@ class LLMEngine:
             if not self.blocks.ensure_slots(s, len(s) + pending + k - 1):
                 return 0
         return k
+
+    def _arrival_cap(self) -> int:
+        """Window cap from the recent arrival rate during decode: half the mean gap between arrivals, in steps
+        (a large number when nothing arrived in the lookback)."""
+        if self._arrival_lookback_s <= 0 or len(self._dec_arrivals) < 2:
+            return 1 << 30
+        now = time.perf_counter()
+        recent = [t for t in self._dec_arrivals if now - t < self._arrival_lookback_s]
+        if len(recent) < 2:
+            return 1 << 30
+        gap = (recent[-1] - recent[0]) / (len(recent) - 1)
+        return max(1, int(0.5 * gap / max(self._step_est, 1e-4)))
 
     def _importing(self) -> bool:
         """A burst of imported (disaggregated) prompts is still arriving."""
@@ -406,7 +426,7 @@ class LLMEngine:
             if dl is None:
                 return 1
             kmax = min(kmax, int((dl - time.perf_counter()) / max(self._step_est, 1e-4)))
-        k = min(kmax, max(s.sampling.max_tokens - len(s.output_ids) for s in seqs),
+        k = min(kmax, self._arrival_cap(), max(s.sampling.max_tokens - len(s.output_ids) for s in seqs),
                 min(self.max_model_len - len(s) + 1 for s in seqs))
         if k <= 1:
             return 1
