@@ -93,6 +93,9 @@ class LLMEngine:
         # 5.24 -> 5.52 ms and e2e p50 707 -> 727 ms (profiles/poisson_r4_arrival_cap_ab.jsonl)
         self._dec_arrivals: "collections.deque[float]" = collections.deque(maxlen=64)
         self._arrival_lookback_s = float(os.environ.get("DIE_ARRIVAL_WINDOW_MS", "0")) / 1e3
+        # "cap": shorter windows; "noqueue": full windows, but no continuation queued behind a running one while
+        # prompts keep arriving (an arrival then waits for the rest of ONE window)
+        self._arrival_mode = os.environ.get("DIE_ARRIVAL_MODE", "cap")
         self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "finished": 0, "prefill_time": 0.0,
                       "decode_time": 0.0, "steps": 0, "prefix_hit_tokens": 0}
         logger.info("KV pool: %d blocks x %d tokens = %.1f GiB (%d tokens)", nblocks, cfg.block_size,
@@ -387,7 +390,7 @@ class LLMEngine:
         ids = {id(s) for s in seqs}
         if any(id(s) not in ids or s.status != SeqStatus.RUNNING or s.in_prefill for s in sch.running):
             return 0
-        k = min(int(self.cfg.decode_window), self._arrival_cap(),
+        k = min(int(self.cfg.decode_window), self._arrival_cap(continuation=True),
                 min(s.sampling.max_tokens - len(s.output_ids) - pending for s in seqs),
                 min(self.max_model_len - (len(s) + pending) + 1 for s in seqs))
         if k <= 1:
@@ -397,15 +400,21 @@ class LLMEngine:
                 return 0
         return k
 
-    def _arrival_cap(self) -> int:
-        """Window cap from the recent arrival rate during decode: half the mean gap between arrivals, in steps
-        (a large number when nothing arrived in the lookback)."""
+    def _recent_arrivals(self) -> List[float]:
         if self._arrival_lookback_s <= 0 or len(self._dec_arrivals) < 2:
-            return 1 << 30
+            return []
         now = time.perf_counter()
-        recent = [t for t in self._dec_arrivals if now - t < self._arrival_lookback_s]
+        return [t for t in self._dec_arrivals if now - t < self._arrival_lookback_s]
+
+    def _arrival_cap(self, continuation: bool = False) -> int:
+        """Window cap from the recent arrival rate during decode: half the mean gap between arrivals, in steps
+        (a large number when nothing arrived in the lookback). In "noqueue" mode only continuations are
+        affected: none is queued while prompts keep arriving."""
+        recent = self._recent_arrivals()
         if len(recent) < 2:
             return 1 << 30
+        if self._arrival_mode == "noqueue":
+            return 0 if continuation else 1 << 30
         gap = (recent[-1] - recent[0]) / (len(recent) - 1)
         return max(1, int(0.5 * gap / max(self._step_est, 1e-4)))
 
