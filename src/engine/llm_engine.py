@@ -86,16 +86,15 @@ class LLMEngine:
 
         self._import_settle_s = float(os.environ.get("DIE_IMPORT_SETTLE_MS", "3")) / 1e3
         self._last_import = -1e9
-        # open-loop arrivals (DIE_ARRIVAL_WINDOW_MS > 0, off by default): times of the requests that arrived while
-        # sequences were decoding (a closed-loop wave arrives while the engine is idle and is not counted) cap the
-        # decode window so that a new prompt waits about half an inter-arrival gap for admission, not a whole window
-        # plus a queued continuation. A TTFT / TPOT trade: Poisson 40 req/s TTFT p50 36.5 -> 24.2 ms, but TPOT p50
-        # 5.24 -> 5.52 ms and e2e p50 707 -> 727 ms (profiles/poisson_r4_arrival_cap_ab.jsonl)
+        # open-loop arrivals: times of the requests that arrived while sequences were decoding (a closed-loop wave
+        # arrives while the engine is idle and is not counted). While two or more arrived within the lookback
+        # (DIE_ARRIVAL_WINDOW_MS, 0 = off) the engine queues no continuation window behind a running one
+        # (DIE_ARRIVAL_MODE=noqueue, default), so a new prompt waits for the rest of ONE window, not a window plus a
+        # queued continuation: Poisson 40 req/s TTFT p50 38.6 -> 29.8 ms, p99 84 -> 58 ms at equal e2e p50
+        # (profiles/poisson_r4_arrival_ab.jsonl). "cap" shortens the windows instead (TTFT p50 24 ms, TPOT +5 %).
         self._dec_arrivals: "collections.deque[float]" = collections.deque(maxlen=64)
-        self._arrival_lookback_s = float(os.environ.get("DIE_ARRIVAL_WINDOW_MS", "0")) / 1e3
-        # "cap": shorter windows; "noqueue": full windows, but no continuation queued behind a running one while
-        # prompts keep arriving (an arrival then waits for the rest of ONE window)
-        self._arrival_mode = os.environ.get("DIE_ARRIVAL_MODE", "cap")
+        self._arrival_lookback_s = float(os.environ.get("DIE_ARRIVAL_WINDOW_MS", "250")) / 1e3
+        self._arrival_mode = os.environ.get("DIE_ARRIVAL_MODE", "noqueue")
         self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "finished": 0, "prefill_time": 0.0,
                       "decode_time": 0.0, "steps": 0, "prefix_hit_tokens": 0}
         logger.info("KV pool: %d blocks x %d tokens = %.1f GiB (%d tokens)", nblocks, cfg.block_size,
