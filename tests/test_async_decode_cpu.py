@@ -149,3 +149,37 @@ def test_no_queued_window_when_blocks_run_short():
     a, b = make_engine(False, blocks=40), make_engine(True, blocks=40)
     ra, rb = run(a, reqs_for()), run(b, reqs_for())
     assert ra == rb
+
+
+def test_open_loop_arrivals_stop_queued_continuations_but_not_closed_loop_waves():
+    """Requests arriving while sequences decode (open-loop traffic) stop the engine from queueing a continuation
+    window behind the running one, so the next arrival waits for at most one window; a closed-loop wave (its
+    requests arrive while the engine is idle) never counts. Tokens are unchanged either way."""
+    import time
+
+    eng = make_engine(True)
+    base = run(make_engine(True), reqs_for())
+    reqs = reqs_for()
+    for i, (p, sp) in enumerate(reqs):  # idle engine: a closed-loop wave
+        eng.add_request(f"r{i}", p, sp)
+    assert len(eng._dec_arrivals) == 0 and eng._arrival_cap(continuation=True) > 1
+    eng.step()  # prefill: the wave is running now
+    late = [[5 + i, 6, 7, 8, 9] for i in range(2)]
+    for j, p in enumerate(late):  # two open-loop arrivals while decoding
+        eng.add_request(f"late{j}", p, SamplingParams(max_tokens=3))
+    assert len(eng._dec_arrivals) == 2
+    assert eng._arrival_cap(continuation=True) == 0 and eng._arrival_cap() > 1  # noqueue: only continuations
+    eng._dec_arrivals.clear()
+    eng._dec_arrivals.extend([time.perf_counter() - 10.0] * 2)  # older than the lookback: no effect
+    assert eng._arrival_cap(continuation=True) > 1
+    res = {}
+    eng2 = make_engine(True)
+    for i, (p, sp) in enumerate(reqs):
+        eng2.add_request(f"r{i}", p, sp, on_finish=lambda s, i=i: res.__setitem__(i, list(s.output_ids)))
+    steps = 0
+    while eng2.has_work():
+        eng2.step()
+        steps += 1
+        if steps in (2, 3):
+            eng2.add_request(f"x{steps}", [3, 4, 5, 6], SamplingParams(max_tokens=4))
+    assert res == base  # the policy changes when windows run, not what they compute
