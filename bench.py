@@ -274,7 +274,7 @@ def main():
         # after the timed region: RCCL / one-shot IPC all-reduce / landing-zone KV hop between the real GPUs
         # (src/parallel/xgpu_probe.py), reported in notes. A watchdog armed until the process group is gone
         # prints the result without the probe (once) and ends the rank if anything after the timed region stalls.
-        dog = _Watchdog(res, rank, 120.0)
+        dog = _Watchdog(res, rank, 300.0)
         try:
             from src.parallel.xgpu_probe import xgpu_probe
 

@@ -13,6 +13,9 @@ two processes sharing one GPU.
   into rank 2k+1's IPC landing zone (:class:`IPCLandingZone` / :class:`IPCSender`, shader stores over
   xGMI), rank 2k+1 checks every byte; GB/s of the copy.
 
+* ``tp_engine``: a TP=N engine (llama-mini) over all ranks — hipGraph decode windows with the exchange in the
+  row-parallel GEMM epilogue over the links — whose greedy tokens are checked against a TP=1 recompute.
+
 Everything is bounded: the caller runs this under a watchdog (bench.py), every device wait is an event
 poll or a collective, and each part reports an error string instead of raising. Reference: the reference
 has no GPU path; these are the transports behind its placement / disaggregation claims
@@ -210,6 +213,79 @@ def _kv_hop(rank: int, world: int, dev, group=None) -> Dict[str, Any]:
     return res
 
 
+TP_PROMPTS = [[5, 9, 33, 12, 7] * 9, [100, 200, 300], list(range(3, 140))]
+
+
+def _greedy_reference(model, prompt, n):
+    """Greedy no-cache recompute on one GPU; also the top1-top2 logit margin per step."""
+    from src.models.llama import AttnMetadata
+
+    d = model.device
+    ids, toks, margins = list(prompt), [], []
+    nb = (len(prompt) + n + 15) // 16
+    pool = torch.zeros(model.arch.num_layers, 2, nb, model.hkv, 16, 128, dtype=model.dtype, device=d)
+    for _ in range(n):
+        t = len(ids)
+        pos = torch.arange(t, device=d)
+        meta = AttnMetadata(True, pos.clone(), torch.arange(nb, dtype=torch.int32, device=d)[None],
+                            torch.tensor([t], dtype=torch.int32, device=d),
+                            torch.tensor([0, t], dtype=torch.int32, device=d), t)
+        lg = model.compute_logits(model.forward(torch.tensor(ids, device=d), pos, meta, pool)[-1:])[0].float()
+        top = torch.topk(lg, 2)
+        toks.append(int(top.indices[0]))
+        margins.append(float(top.values[0] - top.values[1]))
+        ids.append(toks[-1])
+    return toks, margins
+
+
+def _tp_engine(rank: int, world: int, dev, steps: int = 16) -> Dict[str, Any]:
+    """A tensor-parallel engine over every rank of the job (llama-mini, Megatron-split, hipGraph decode windows,
+    the one-shot exchange in the row-parallel GEMM epilogue over the links): rank 0 serves three prompts, its
+    greedy tokens are checked against a TP=1 no-cache recompute of the same full-size weights on rank 0's GPU
+    (agreement up to the reference's first near-tie, as tests/test_engine_gpu.py does on one GPU)."""
+    from src.config import EngineConfig
+    from src.models.llama import CausalLM
+    from src.models.presets import get_preset
+    from src.parallel.tp import TPContext
+    from src.parallel.tp_runner import build_tp_engine
+    from src.preproc import SamplingParams
+
+    cpu = dist.new_group(list(range(world)), backend="gloo") if dist.get_backend() != "gloo" else None
+    tp = TPContext(rank=rank, world_size=world, cpu_group=cpu)
+    cfg = EngineConfig(max_num_seqs=4, max_num_batched_tokens=256, num_kv_blocks=128, max_latency_ms=0.0,
+                       use_cuda_graph=True, graph_batch_sizes=[1, 2, 4])
+    obj = build_tp_engine("llama-mini", tp, str(dev), cfg=cfg, max_model_len=512, capture=True, full_init=True,
+                          seed=3)
+    res: Dict[str, Any] = {"preset": "llama-mini", "tp": world}
+    if rank != 0:
+        obj.follower_loop()
+        return res
+    obj.eos_token_id = None
+    obj.generate(TP_PROMPTS[:1], SamplingParams(max_tokens=4))  # warm-up
+    t0 = time.perf_counter()
+    outs = obj.generate(TP_PROMPTS, SamplingParams(max_tokens=steps))
+    res["generate_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+    res["decode_steps"] = steps - 1
+    res["graphs_replayed"] = bool(obj.runner.graphs)
+    res["fused_exchange"] = bool(obj.model.decode_plan(4).get("tp_fused"))
+    res["one_shot_error"] = bool(tp.car.error()) if tp.car is not None else None
+    obj.runner.stop_followers()
+    ref = CausalLM(get_preset("llama-mini"), str(dev), seed=3, max_position=512, full_init=True)
+    agree = []
+    for p, o in zip(TP_PROMPTS, outs):
+        r, mg = _greedy_reference(ref, p, steps)
+        ok = True
+        for a, b, m in zip(o, r, mg):
+            if m < 0.25:
+                break
+            if a != b:
+                ok = False
+                break
+        agree.append(ok)
+    res["tokens_agree_with_tp1"] = agree
+    return res
+
+
 def xgpu_probe(rank: int, world: int, dev, rccl: bool = True, group=None) -> Dict[str, Any]:
     """Run the three parts (each catching its own failure); returns rank 0's view (the same dict on every
     rank for the RCCL part; the KV hop reports every pair through ``per_rank``)."""
@@ -228,6 +304,11 @@ def xgpu_probe(rank: int, world: int, dev, rccl: bool = True, group=None) -> Dic
         out["kv_hop"] = _kv_hop(rank, world, dev, group)
     except Exception as e:  # noqa: BLE001
         out["kv_hop"] = {"error": str(e)[:200]}
+    if 2 <= world <= 8 and os.environ.get("DIE_XGPU_TP", "1") != "0":
+        try:
+            out["tp_engine"] = _tp_engine(rank, world, dev)
+        except Exception as e:  # noqa: BLE001
+            out["tp_engine"] = {"error": str(e)[:200]}
     out["probe_s"] = round(time.perf_counter() - t0, 2)
     return out
 
