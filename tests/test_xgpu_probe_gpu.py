@@ -1,6 +1,7 @@
 """The cross-GPU probe a multi-GPU bench.py runs after its timed region (src/parallel/xgpu_probe.py), rehearsed
 with 2 ranks on this one GPU (gloo coordinates; RCCL refuses two ranks on one device): the one-shot IPC
-all-reduce runs without raising its error word and the landing-zone KV hop delivers every byte."""
+all-reduce runs without raising its error word, the landing-zone KV hop delivers every byte and a TP=2
+engine across the two ranks serves tokens that agree with a TP=1 recompute."""
 
 import json
 import os
@@ -35,3 +36,6 @@ def test_xgpu_probe_two_ranks_one_gpu():
     hop = r["kv_hop"]
     assert hop["per_rank"][1]["receiver_bytes_match"] is True, hop
     assert hop["GBps"] > 0 and all(x["error"] is None for x in hop["per_rank"]), hop
+    tpe = r["tp_engine"]  # TP=2 llama-mini over both ranks: graph windows, fused exchange, tokens vs TP=1
+    assert tpe.get("graphs_replayed") and tpe.get("fused_exchange") and tpe.get("one_shot_error") is False, tpe
+    assert all(tpe["tokens_agree_with_tp1"]), tpe
