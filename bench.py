@@ -3,9 +3,9 @@
 Headline benchmark (BASELINE.json): req/s + p50 end-to-end latency of
 Llama-3-8B batched serving on 1/2/4/8 MI355X.
 
-Each rank (one per GPU, launched by torch.distributed.run for N > 1) runs a
-full serving replica — data parallel, the right layout for an 8B model that
-fits one 288 GB GPU many times over — and the whole serving path minus TCP:
+Each rank (one per GPU, under torch.distributed.run for N > 1) runs a full
+serving replica — data parallel, the right layout for an 8B model that fits one
+288 GB GPU many times over — and the whole serving path minus TCP:
 
     Batcher(max_batch=32, max_latency=10 ms)  →  AsyncLLMEngine (engine thread)
       → continuous-batching scheduler → paged-KV Llama-3-8B (random-init bf16)
@@ -15,10 +15,25 @@ One "step" = one wave of ``--batch`` (32) synthetic requests per GPU, each a
 distinct random 512-token prompt generating 128 tokens (ignore_eos), submitted
 together and served to completion (prefill + 128 decode iterations, sampling
 included). Weak scaling: per-GPU work is fixed as N grows. ``value`` is the
-whole-job request rate (all GPUs); ``p50_latency_ms`` is the median
-submit→finish latency over every timed request.
+whole-job request rate over the ranks that actually ran (``notes.world_size_seen``,
+``notes.devices``); ``p50_latency_ms`` is the median submit→finish latency over
+every timed request.
+
+``--gpus N`` (N > 1) without a launcher starts ``torch.distributed.run`` with N
+ranks as a CHILD process and relays its result line and exit status; it never
+counts replicas that did not run. Under a launcher, ``--gpus`` must equal
+WORLD_SIZE.
+
+After the timed region of a multi-GPU run (its engines freed, under a watchdog)
+the node measures BASELINE configs 3 and 4 and the links they use
+(``notes.cross_gpu``, status also at the top level as ``cross_gpu_status``):
+cross-GPU transports (src/parallel/xgpu_probe.py), 8B disaggregated serving
+with prefill on rank 2k and decode on rank 2k+1 (N >= 2), and a Llama-3-70B
+TP=N engine serving one wave (N == 8) (src/parallel/node_bench.py). A stall
+prints the result with ``cross_gpu_status: "stalled ..."`` and exits 3.
 
     python bench.py                      # 1 GPU, 3 timed steps, 1 warmup
+    python bench.py --gpus 8 --steps 3   # spawns the 8-rank launcher itself
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29500 bench.py --gpus 8 --steps 3 --warmup 1
 """
@@ -30,8 +45,11 @@ import asyncio
 import json
 import os
 import random
+import socket
 import statistics
+import subprocess
 import sys
+import threading
 import time
 
 import torch
@@ -42,6 +60,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 METRIC_FMT = "req/sec + p50 end-to-end latency, {model} batched serving at 1/2/4/8 MI355X"
+STALL_EXIT = 3
 
 
 def model_label(preset: str) -> str:
@@ -56,7 +75,7 @@ def model_label(preset: str) -> str:
     return name.replace("-8b", "-8B").replace("-70b", "-70B").replace("x7b", "x7B")
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=None)
     p.add_argument("--steps", type=int, default=3)
@@ -76,10 +95,57 @@ def parse():
     p.add_argument("--sequence-parallel", action="store_true", help="Megatron-SP prefill under --tp")
     p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                    help="cpu: reference-op engine over gloo (tests the multi-rank plumbing, not a measurement)")
+    p.add_argument("--kv-blocks", type=int, default=None,
+                   help="KV pool blocks per replica (default: the HBM left after the weights; --same-device: enough "
+                        "for one wave, so the ranks sharing the GPU do not each claim its HBM)")
+    p.add_argument("--same-device", action="store_true",
+                   help="rehearsal: every rank on cuda:0, gloo coordinates (no RCCL; numbers are not a scaling point)")
+    # the post-timed-region node section (configs 3 / 4 and the cross-GPU transports)
+    p.add_argument("--cross-gpu", choices=["auto", "on", "off"], default="auto",
+                   help="auto: on for multi-rank GPU runs; on: also on CPU (plumbing tests)")
+    p.add_argument("--cross-gpu-budget-s", type=float, default=420.0, help="watchdog for the whole node section")
+    p.add_argument("--disagg-preset", default=None, help="config 3 model (default: --preset)")
+    p.add_argument("--tp-wave-preset", default="llama3-70b", help="config 4 model")
+    p.add_argument("--tp-wave-min-world", type=int, default=8, help="run the config-4 TP wave from this many ranks")
     p.add_argument("--verbose", action="store_true")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
+# ------------------------------------------------------------------------------------------------ launch guard
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def needs_launcher(args) -> bool:
+    """--gpus N > 1 outside torch.distributed.run: this process would be ONE replica."""
+    return bool(args.gpus and args.gpus > 1 and "WORLD_SIZE" not in os.environ)
+
+
+def self_launch(args, argv) -> int:
+    """Run this script under torch.distributed.run with ``args.gpus`` ranks as a child process (no exec: this
+    process has not touched the GPU and never will), relay rank 0's single JSON line to stdout and return the
+    launcher's exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    for ln in p.stdout.splitlines():
+        if not ln.startswith("{"):
+            print(ln, file=sys.stderr)
+    if len(lines) != 1:
+        print(f"bench.py: the {args.gpus}-rank run printed {len(lines)} result lines (rc {p.returncode})",
+              file=sys.stderr)
+        return p.returncode or 1
+    print(lines[0], flush=True)
+    return p.returncode
+
+
+# ------------------------------------------------------------------------------------------------ serving
 def make_prompts(rng, n, prompt_len, vocab):
     """One wave's synthetic prompts (client-side data, generated before the clock starts)."""
     return [[rng.randrange(3, vocab) for _ in range(prompt_len)] for _ in range(n)]
@@ -103,23 +169,9 @@ async def serve_wave(batcher, prompts, gen_len, temperature):
     return lat
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    n_gpus = args.gpus or world
-    on_gpu = args.device == "cuda"
-    if world > 1:
-        if on_gpu:
-            torch.cuda.set_device(local)
-        dist.init_process_group("nccl" if on_gpu else "gloo")  # nccl = RCCL over xGMI
-    dev = torch.device(f"cuda:{local}" if on_gpu else "cpu")
-
-    def sync():
-        if on_gpu:
-            torch.cuda.synchronize(dev)
-
+def serve_timed(args, rank, world, dev, on_gpu):
+    """Build this rank's replica (or TP group member), run warmup + timed waves, return the measurements.
+    Every engine object is local to this function, so its HBM is released when it returns."""
     from src.batcher import Batcher
     from src.config import EngineConfig
     from src.engine import LLMEngine
@@ -127,8 +179,15 @@ def main():
     from src.preproc import normalize_request
     from src.utils.tracing import prof_marker
 
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize(dev)
+
+    kv_blocks = args.kv_blocks
+    if kv_blocks is None and args.same_device:
+        kv_blocks = args.batch * -(-args.max_model_len // 16) + 64
     cfg = EngineConfig(max_num_seqs=args.batch, max_num_batched_tokens=max(16384, args.prompt_len),
-                       max_latency_ms=args.max_latency_ms, use_cuda_graph=not args.no_graph,
+                       num_kv_blocks=kv_blocks, max_latency_ms=args.max_latency_ms, use_cuda_graph=not args.no_graph,
                        graph_batch_sizes=[1, 2, 4, 8, 16, 24, 32, args.batch],
                        async_decode=not args.no_async_decode,
                        **({"decode_window": args.decode_window} if args.decode_window else {}))
@@ -149,19 +208,12 @@ def main():
             obj.follower_loop()
             sync()
             dist.barrier()
-            t = torch.zeros(1, device=dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dist.all_gather_object([None] * world, 0.0)  # the leader's per-rank elapsed
-            dist.all_gather_object([None] * world, [])
-            dist.barrier()
-            dist.destroy_process_group()
-            return
+            return {"elapsed": 0.0, "lats": [], "follower": True}
         engine = obj
     else:
         engine = LLMEngine.from_preset(args.preset, device=dev, cfg=cfg, max_model_len=args.max_model_len,
                                        seed=1234, capture=not args.no_graph)
     engine.eos_token_id = None
-    replicas = n_gpus // args.tp
     init_s = time.perf_counter() - t_init
     aeng = AsyncLLMEngine(engine)
     aeng.start()
@@ -180,7 +232,7 @@ def main():
         batcher = Batcher(max_batch_size=args.batch, max_latency_ms=args.max_latency_ms, batch_callback=callback)
         await batcher.start()
         vocab = engine.arch.vocab_size
-        for w in range(args.warmup):
+        for _ in range(args.warmup):
             await serve_wave(batcher, make_prompts(rng, args.batch, args.prompt_len, vocab), args.gen_len,
                              args.temperature)
         waves = [make_prompts(rng, args.batch, args.prompt_len, vocab) for _ in range(args.steps)]
@@ -212,10 +264,134 @@ def main():
     elapsed, lats, stats0 = asyncio.run(run())
     aeng.stop()
     st = engine.stats
-    gen_tok = st["generated_tokens"] - stats0["generated_tokens"]
-    prefill_s = st["prefill_time"] - stats0["prefill_time"]
-    decode_s = st["decode_time"] - stats0["decode_time"]
+    return {"elapsed": elapsed, "lats": lats, "init_s": init_s,
+            "gen_tok": st["generated_tokens"] - stats0["generated_tokens"],
+            "prefill_s": st["prefill_time"] - stats0["prefill_time"],
+            "decode_s": st["decode_time"] - stats0["decode_time"]}
+
+
+# ------------------------------------------------------------------------------------------------ node section
+def cross_gpu_section(args, rank, world, dev, on_gpu, state) -> dict:
+    """Configs 3 / 4 and the transports, after the timed region. Every rank runs every part in the same order;
+    ``state["part"]`` names the running part for the watchdog."""
+    from src.parallel.node_bench import NodeBenchArgs, disagg_part, free_device_memory, tp_wave_part
+
+    free_device_memory()  # the timed replicas' weights, KV pools and graphs
+    cpu = dist.new_group(list(range(world)), backend="gloo") if dist.get_backend() != "gloo" else None
+    out: dict = {}
+    nb = NodeBenchArgs(preset=args.disagg_preset or args.preset, tp_preset=args.tp_wave_preset, batch=args.batch,
+                       prompt_len=args.prompt_len, gen_len=args.gen_len, max_model_len=args.max_model_len,
+                       max_latency_ms=args.max_latency_ms, graphs=not args.no_graph)
+    parts = []
+    if on_gpu:
+        parts.append("xgpu_probe")
+    parts.append("disagg")
+    if world >= args.tp_wave_min_world:
+        parts.append("tp_wave")
+    for part in parts:
+        state["part"] = part
+        t0 = time.perf_counter()
+        try:
+            if part == "xgpu_probe":
+                from src.parallel.xgpu_probe import xgpu_probe
+
+                r = xgpu_probe(rank, world, dev, rccl=not args.same_device)
+            elif part == "disagg":
+                r = disagg_part(nb, rank, world, dev, cpu)
+            else:
+                r = tp_wave_part(nb, rank, world, dev)
+        except Exception as e:  # noqa: BLE001 — reported; the timed result stands on its own
+            r = {"error": f"{type(e).__name__}: {e}"[:300]}
+        if isinstance(r, dict):
+            r.setdefault("part_s", round(time.perf_counter() - t0, 1))
+        out[part] = r
+        state.setdefault("done", {})[part] = r
+        free_device_memory()
+        dist.barrier(group=cpu)
+    state["part"] = None
+    return out
+
+
+def _part_errors(cross: dict) -> list:
+    errs = []
+    for name, r in cross.items():
+        if not isinstance(r, dict):
+            continue
+        if r.get("error"):
+            errs.append(name)
+        elif name == "xgpu_probe" and any(isinstance(v, dict) and v.get("error") for v in r.values()):
+            errs.append(name)
+    return errs
+
+
+class _Watchdog:
+    """Prints rank 0's result line exactly once — normally (emit), or from the timer with the node section marked
+    as stalled — and on expiry ends the process with status STALL_EXIT (3), so a stall can never look like a
+    successful run."""
+
+    def __init__(self, res, rank: int, budget_s: float, state=None):
+        self.res, self.rank, self.budget_s = res, rank, budget_s
+        self.state = state if state is not None else {}
+        self._lock = threading.Lock()
+        self._printed = False
+        self._timer = threading.Timer(budget_s, self._expire)
+        self._timer.daemon = True
+        self._timer.start()
+
+    def emit(self) -> None:
+        with self._lock:
+            if not self._printed and self.rank == 0:
+                print(json.dumps(self.res), flush=True)
+            self._printed = True
+
+    def _expire(self) -> None:
+        with self._lock:
+            if not self._printed and self.rank == 0:
+                part = self.state.get("part")
+                msg = f"stalled in {part or 'teardown'}: no result within {self.budget_s:.0f} s"
+                self.res["cross_gpu_status"] = msg
+                cross = self.res.setdefault("notes", {}).setdefault("cross_gpu", {})
+                cross["status"] = STALL_EXIT
+                cross["stalled_part"] = part
+                # the parts that finished before the stall (state["done"], written by rank 0 as it goes)
+                for k, v in (self.state.get("done") or {}).items():
+                    cross.setdefault(k, v)
+                print(json.dumps(self.res), flush=True)
+            self._printed = True
+        os._exit(STALL_EXIT)
+
+    def cancel(self) -> None:
+        self._timer.cancel()
+
+
+# ------------------------------------------------------------------------------------------------ main
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    if needs_launcher(args):
+        return self_launch(args, argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; refusing to report replicas that do not run",
+              file=sys.stderr)
+        return 2
+    n_gpus = world
+    on_gpu = args.device == "cuda"
+    if world > 1:
+        if on_gpu:
+            torch.cuda.set_device(0 if args.same_device else local)
+        dist.init_process_group("nccl" if on_gpu and not args.same_device else "gloo")  # nccl = RCCL over xGMI
+    dev = torch.device(f"cuda:{0 if args.same_device else local}" if on_gpu else "cpu")
+
+    from src.parallel.node_bench import device_identity, distinct_devices
+
+    m = serve_timed(args, rank, world, dev, on_gpu)
+    elapsed, lats = m["elapsed"], m["lats"]
+    ident = device_identity(dev)
     rank_elapsed = [elapsed]
+    idents = [ident]
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -225,14 +401,17 @@ def main():
         gathered = [None] * world
         dist.all_gather_object(gathered, lats)
         lats = [x for g in gathered for x in g]
+        idents = [None] * world
+        dist.all_gather_object(idents, ident)
+    tp = args.tp if args.tp > 1 else None
+    replicas = world // args.tp
     total_req = args.steps * args.batch * replicas
-    rps = total_req / elapsed
     res = None
     if rank == 0:
         label = model_label(args.preset)
         res = {
             "metric": METRIC_FMT.format(model=label),
-            "value": round(rps, 3),
+            "value": round(total_req / elapsed, 3),
             "unit": "req/s",
             "n_gpus": n_gpus,
             "steps": args.steps,
@@ -245,7 +424,7 @@ def main():
             "data": "synthetic",
             "p50_latency_ms": round(1e3 * statistics.median(lats), 2),
             "p99_latency_ms": round(1e3 * sorted(lats)[max(0, int(0.99 * len(lats)) - 1)], 2),
-            "output_tok_per_s": round(gen_tok * replicas / elapsed, 1),
+            "output_tok_per_s": round(m["gen_tok"] * replicas / elapsed, 1),
             "config": {
                 "model": label,
                 "global_batch": args.batch * replicas,
@@ -262,27 +441,31 @@ def main():
             },
             "notes": {
                 "baseline": "reference publishes no numbers and has no GPU path (BASELINE.md); vs_baseline=null",
-                "rank0_prefill_s": round(prefill_s, 3),
-                "rank0_decode_s": round(decode_s, 3),
-                "engine_init_s": round(init_s, 1),
+                "rank0_prefill_s": round(m["prefill_s"], 3),
+                "rank0_decode_s": round(m["decode_s"], 3),
+                "engine_init_s": round(m["init_s"], 1),
+                "world_size_seen": dist.get_world_size() if world > 1 else 1,
+                "distinct_devices": distinct_devices(idents),
+                "devices": idents,
             },
         }
+        if args.same_device:
+            res["notes"]["rehearsal"] = "every rank on cuda:0: not a scaling point"
         if world > 1 and tp is None:  # the value uses the slowest replica; the spread shows stragglers
             res["notes"]["rank_elapsed_s"] = [round(x, 3) for x in rank_elapsed]
+    m = None
+    run_node = world > 1 and tp is None and (args.cross_gpu == "on" or (args.cross_gpu == "auto" and on_gpu))
     dog = None
-    if world > 1 and on_gpu and tp is None and os.environ.get("DIE_XGPU_PROBE", "1") != "0":
-        # after the timed region: RCCL / one-shot IPC all-reduce / landing-zone KV hop between the real GPUs
-        # (src/parallel/xgpu_probe.py), reported in notes. A watchdog armed until the process group is gone
-        # prints the result without the probe (once) and ends the rank if anything after the timed region stalls.
-        dog = _Watchdog(res, rank, 300.0)
-        try:
-            from src.parallel.xgpu_probe import xgpu_probe
-
-            probe = xgpu_probe(rank, world, dev)
-        except Exception as e:  # noqa: BLE001 — the bench result stands on its own
-            probe = {"error": str(e)[:200]}
+    rc = 0
+    if run_node:
+        state: dict = {"part": None, "done": {}}
+        dog = _Watchdog(res, rank, args.cross_gpu_budget_s, state)
+        cross = cross_gpu_section(args, rank, world, dev, on_gpu, state)
         if rank == 0:
-            res["notes"]["xgpu_probe"] = probe
+            errs = _part_errors(cross)
+            cross["status"] = 1 if errs else 0
+            res["notes"]["cross_gpu"] = cross
+            res["cross_gpu_status"] = ("error in " + ", ".join(errs)) if errs else "ok"
     if rank == 0:
         if dog is not None:
             dog.emit()
@@ -293,39 +476,8 @@ def main():
         dist.destroy_process_group()
     if dog is not None:
         dog.cancel()
-
-
-class _Watchdog:
-    """Prints rank 0's result line exactly once — normally (emit), or from the timer with the probe marked as
-    stalled — and on expiry ends the process (os._exit) so that no rank waits on a peer forever."""
-
-    def __init__(self, res, rank: int, budget_s: float):
-        import threading
-
-        self.res, self.rank, self.budget_s = res, rank, budget_s
-        self._lock = threading.Lock()
-        self._printed = False
-        self._timer = threading.Timer(budget_s, self._expire)
-        self._timer.daemon = True
-        self._timer.start()
-
-    def emit(self) -> None:
-        with self._lock:
-            if not self._printed and self.rank == 0:
-                print(json.dumps(self.res), flush=True)
-            self._printed = True
-
-    def _expire(self) -> None:
-        with self._lock:
-            if not self._printed and self.rank == 0:
-                self.res["notes"].setdefault("xgpu_probe", {"error": f"no result within {self.budget_s:.0f} s"})
-                print(json.dumps(self.res), flush=True)
-            self._printed = True
-        os._exit(0)
-
-    def cancel(self) -> None:
-        self._timer.cancel()
+    return rc
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -115,17 +115,17 @@ class CustomAllReduce:
     def fused_ok(self, n_tiles: int, grid: int = 0) -> bool:
         """Whether the row-parallel decode GEMM may carry the exchange in its epilogue (gemm_decode_car). Only a
         column tile's last-arriving workgroup waits for the peers, so a launch holds at most ``n_tiles`` waiting
-        workgroups (one per CU: the GEMM's LDS ring) on each GPU. Every tile of every rank gets to run when the
-        whole ``grid`` of every rank sharing the GPU is resident at once, or when the waiting tiles leave half the
-        CUs to the rest of the grids (the ranks sharing a GPU in tests included). ``DIE_TP_FUSED=0`` keeps the separate all-reduce launch. The answer
-        depends only on the group's layout and the shape, so every rank agrees."""
+        workgroups on each GPU (times the ranks sharing it, in one-GPU tests). Every other workgroup finishes
+        without waiting, so the grid always drains when the waiting ones can hold at most HALF the CUs — whatever
+        the kernel's occupancy per CU and whatever else shares the GPU for a while (the former
+        "whole grid resident at one workgroup per CU" clause assumed both). ``grid`` is kept for callers.
+        ``DIE_TP_FUSED=0`` keeps the separate all-reduce launch. The answer depends only on the group's layout
+        and the shape, so every rank agrees."""
         import os
 
         if os.environ.get("DIE_TP_FUSED", "1") == "0" or not 0 < n_tiles <= SIG_BLOCKS:
             return False
-        # every workgroup of every rank sharing the GPU resident at once (one per CU), or at most half the CUs
-        # held by waiting last arrivers
-        return (0 < grid and grid * self.ranks_per_gpu <= self.cus) or n_tiles * self.ranks_per_gpu * 2 <= self.cus
+        return n_tiles * self.ranks_per_gpu * 2 <= self.cus
 
     def row_parallel_residual(self, x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, ssp: torch.Tensor,
                               counters: torch.Tensor, wr: int, kc: int, sk: int, tiled: bool) -> None:
