@@ -247,10 +247,15 @@ class LLMEngine:
             # a prefill step, or a mixed step: the decode rows as 1-token chunks in the same ragged batch
             chunks = out.chunks() if out.decode else out.prefill
             exporter = self._start_export(chunks)
-            toks = (self.runner.prefill(chunks) if exporter is None
-                    else self.runner.prefill(chunks, kv_hook=exporter.on_layer))
-            if exporter is not None:
-                self._finish_export(exporter)
+            try:
+                toks = (self.runner.prefill(chunks) if exporter is None
+                        else self.runner.prefill(chunks, kv_hook=exporter.on_layer))
+            finally:
+                # even when the forward fails: every slot the export took gets its completion event (a revoke then
+                # releases it behind the queued gathers instead of polling until the TTL) and the compute stream
+                # waits for those gathers before any later kernel can reuse the exported blocks
+                if exporter is not None:
+                    self._finish_export_safely(exporter)
             now = time.perf_counter()
             self.stats["mixed_time" if out.decode else "prefill_time"] = \
                 self.stats.get("mixed_time" if out.decode else "prefill_time", 0.0) + now - t0
@@ -343,6 +348,17 @@ class LLMEngine:
             if slot is not None:
                 slot.set_event(ev)
         self.stats["overlapped_exports"] = self.stats.get("overlapped_exports", 0) + len(ex.seqs)
+
+    def _finish_export_safely(self, ex) -> None:
+        import sys
+
+        if sys.exc_info()[0] is None:
+            self._finish_export(ex)
+            return
+        try:  # the forward already raised: its exception is the one that propagates
+            self._finish_export(ex)
+        except Exception:  # noqa: BLE001
+            logger.exception("finishing the KV export after a failed prefill step")
 
     def _run_swaps(self, out: SchedulerOutput) -> None:
         """Queue the step's KV swaps on the compute stream ahead of its forward: swap-outs pack

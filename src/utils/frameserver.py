@@ -66,9 +66,15 @@ class FrameServerProtocol(asyncio.Protocol):
     ``idle_timeout``: the connection is dropped after that long with no request being served (the timer is
     stopped while a request runs — a long streamed generation is not idle)."""
 
+    # a pipelining client may queue this many decoded requests before the transport stops reading (TCP
+    # backpressure then holds the rest in the client's socket buffers instead of this process's memory)
+    MAX_QUEUED = 64
+
     def __init__(self, handler: Handler, idle_timeout: Optional[float] = None, conns: Optional[set] = None,
-                 allow_pickle: bool = False):
+                 allow_pickle: bool = False, on_error: Optional[Callable[[BaseException], None]] = None):
         self.handler = handler
+        self.on_error = on_error
+        self._reading_paused = False
         self.idle_timeout = idle_timeout
         self.conns = conns
         self.allow_pickle = allow_pickle
@@ -121,8 +127,17 @@ class FrameServerProtocol(asyncio.Protocol):
             self._feed_legacy(data)
             return
         buf += data
+        if not self._parse():
+            return
+        if not self._busy and self._queue:
+            self._next()
+
+    def _parse(self) -> bool:
+        """Decode the buffered frames into the request queue, at most MAX_QUEUED of them; past that the transport
+        stops reading and the rest stays raw in the buffer (at most one read's worth). False: rejected."""
+        buf = self._buf
         try:
-            while len(buf) >= 4:
+            while len(buf) >= 4 and len(self._queue) < self.MAX_QUEUED:
                 (n,) = _HDR.unpack_from(buf)
                 if n == 0 or n > MAX_FRAME:
                     raise ProtocolError(f"bad frame length {n}")
@@ -133,9 +148,11 @@ class FrameServerProtocol(asyncio.Protocol):
                 self._queue.append((deserialize(body, allow_pickle=self.allow_pickle), body[:1]))
         except (ProtocolError, ValueError) as e:
             self._reject(e)
-            return
-        if not self._busy and self._queue:
-            self._next()
+            return False
+        if len(self._queue) >= self.MAX_QUEUED and not self._reading_paused and not self._closed:
+            self._reading_paused = True
+            self.transport.pause_reading()
+        return True
 
     def _feed_legacy(self, data: bytes) -> None:
         base = len(self._buf)
@@ -166,6 +183,11 @@ class FrameServerProtocol(asyncio.Protocol):
         return False
 
     def _reject(self, e: BaseException) -> None:
+        if self.on_error is not None:  # e.g. the worker's error_count: a malformed request is an error too
+            try:
+                self.on_error(e)
+            except Exception:  # pragma: no cover - a counter must not break the reply
+                pass
         if self.transport is not None and not self._closed:
             try:
                 self.transport.write(pack_frame({"error": f"bad request: {e}", "success": False}))
@@ -175,6 +197,10 @@ class FrameServerProtocol(asyncio.Protocol):
     # ------------------------------------------------------------------ serving
     def _next(self) -> None:
         msg, codec = self._queue.popleft()
+        if self._reading_paused and len(self._queue) < self.MAX_QUEUED // 2 and not self._closed:
+            if self._parse() and len(self._queue) < self.MAX_QUEUED:  # the frames held back in the buffer first
+                self._reading_paused = False
+                self.transport.resume_reading()
         self._busy = True
         if self._idle is not None:
             self._idle.cancel()
@@ -212,11 +238,12 @@ class FrameServerProtocol(asyncio.Protocol):
 
 
 async def start_frame_server(handler: Handler, host: str, port: int, *, idle_timeout: Optional[float] = None,
-                             conns: Optional[set] = None, backlog: int = 4096,
-                             reuse_port: Optional[bool] = None) -> asyncio.AbstractServer:
+                             conns: Optional[set] = None, backlog: int = 4096, reuse_port: Optional[bool] = None,
+                             on_error: Optional[Callable[[BaseException], None]] = None) -> asyncio.AbstractServer:
+    """``on_error(exc)``: called for every request the protocol layer rejects (malformed frame / JSON)."""
     loop = asyncio.get_running_loop()
-    return await loop.create_server(lambda: FrameServerProtocol(handler, idle_timeout, conns), host, port,
-                                    backlog=backlog, reuse_port=reuse_port)
+    return await loop.create_server(lambda: FrameServerProtocol(handler, idle_timeout, conns, on_error=on_error),
+                                    host, port, backlog=backlog, reuse_port=reuse_port)
 
 
 class FrameClientProtocol(asyncio.Protocol):

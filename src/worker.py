@@ -99,12 +99,19 @@ class Worker:
         # protocol-level framing (src/utils/frameserver.py); an idle connection is dropped after IDLE_TIMEOUT_S
         # (the timer stops while a request is being served: a long streamed generation is not idle)
         self.server = await start_frame_server(self.handle_message, self.host, self.port, backlog=4096,
-                                               idle_timeout=self.IDLE_TIMEOUT_S, conns=self._conns)
+                                               idle_timeout=self.IDLE_TIMEOUT_S, conns=self._conns,
+                                               on_error=self._on_protocol_error)
         self.port = self.server.sockets[0].getsockname()[1]
         logger.info("Worker %s listening on %s:%d", self.worker_id, self.host, self.port)
         if self.coordinator:
             asyncio.create_task(self._register_with_coordinator())
         return self.port
+
+    def _on_protocol_error(self, exc: BaseException) -> None:
+        """A request the framing layer rejected (bad frame, malformed JSON): counted as a request and an error,
+        as the reference's handler counted a failed json.loads (`/root/reference/src/worker.py:87,99-101`)."""
+        self._request_count += 1
+        self._error_count += 1
 
     @property
     def address(self) -> str:

@@ -48,3 +48,33 @@ def test_packet_wire_roundtrip():
     q = packet_from_wire(packet_to_wire(p))
     assert torch.equal(q.kv.view(torch.int16), kv.view(torch.int16))
     assert (q.prompt_ids, q.first_token, q.block_size, q.ttft_ms) == ([1, 2, 3], 9, 16, 12.5)
+
+
+def test_failed_prefill_still_finishes_the_overlapped_export():
+    """if the forward raises after an overlapped export took its slots, the export is still finished
+    (its slots get their completion event, the compute stream waits for the queued gathers) and the forward's
+    exception is the one that propagates."""
+    import pytest
+
+    from src.preproc import SamplingParams
+
+    e = eng()
+    finished = []
+
+    class FakeExporter:
+        seqs = []
+
+        def on_layer(self, li):
+            pass
+
+    e._start_export = lambda chunks: FakeExporter()
+    e._finish_export = lambda ex: finished.append(ex)
+
+    def boom(chunks, kv_hook=None):
+        raise RuntimeError("forward failed")
+
+    e.runner.prefill = boom
+    e.add_request("r0", [5, 6, 7, 8], SamplingParams(max_tokens=4))
+    with pytest.raises(RuntimeError, match="forward failed"):
+        e.step()
+    assert len(finished) == 1 and isinstance(finished[0], FakeExporter)
