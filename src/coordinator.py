@@ -41,6 +41,7 @@ from src.config import DeploymentConfig  # noqa: E402
 from src.kvstore import KVCache  # noqa: E402
 from src.load_balancer import LoadBalancer, LoadBalancerStrategy  # noqa: E402
 from src.model_registry import ModelRegistry, rendezvous_score  # noqa: E402
+from src.preproc import request_cost  # noqa: E402
 from src.router import Router, WorkerHealth  # noqa: E402
 from src.rpc import RPCClient, RPCError  # noqa: E402
 from src.utils import (  # noqa: E402
@@ -352,12 +353,13 @@ class Coordinator:
         lb = self._lb(model, version)
         wmsg = {"op": "infer", "model": model, "inputs": inputs, "request_id": rid}
         last_err = "no worker available"
-        for i, (wid, addr) in enumerate(self._candidates(model, version, shard.shard_id, key)):
+        cost = request_cost(inputs)
+        for i, (wid, addr) in enumerate(self._candidates(model, version, shard.shard_id, key, cost)):
             if i > self.max_retries:
                 break
             relayed = False
             try:
-                async with lb.track(wid):
+                async with lb.track(wid, cost):
                     async for frame in self.rpc.stream(addr, wmsg, timeout=self.request_timeout_s):
                         if isinstance(frame, dict) and frame.get("done") is False:
                             relayed = True
@@ -365,6 +367,7 @@ class Coordinator:
                             continue
                         self.router.mark_worker_success(wid)
                         if isinstance(frame, dict):
+                            lb.observe(wid, frame.pop("engine_load", None))
                             frame.setdefault("request_id", rid)
                         return frame
             except (RPCError, OSError, asyncio.TimeoutError) as e:
@@ -382,13 +385,13 @@ class Coordinator:
             return self.dispatch_override
         return "batch" if self._model_arch.get(model, "mock") == "mock" else "stream"
 
-    def _candidates(self, model: str, version: str, shard_id: int, key: str):
+    def _candidates(self, model: str, version: str, shard_id: int, key: str, cost=None):
         """Ordered worker candidates, generated lazily (the fallbacks are only computed after a failure):
         LB choice in the routed shard first, then the shard's other healthy workers, then other healthy
-        shards by key affinity."""
+        shards by key affinity. ``cost``: (prompt tokens, output tokens) for the least_latency score."""
         lb = self._lb(model, version)
         seen: List[Tuple[str, str]] = []
-        first = lb.pick(group=str(shard_id))
+        first = lb.pick(group=str(shard_id), cost=cost)
         if first:
             seen.append(first)
             yield first
@@ -399,7 +402,7 @@ class Coordinator:
         others = [s for s in self.router.healthy_shards(model, version) if s.shard_id != shard_id]
         others.sort(key=lambda s: -rendezvous_score(key, s.shard_id))
         for s in others:
-            p = lb.pick(group=str(s.shard_id))
+            p = lb.pick(group=str(s.shard_id), cost=cost)
             if p and p not in seen:
                 seen.append(p)
                 yield p
@@ -413,7 +416,8 @@ class Coordinator:
         tried = 0
         if deadline is None:
             deadline = time.monotonic() + self.request_timeout_s
-        for wid, addr in self._candidates(model, version, shard_id, key):
+        cost = request_cost(msg.get("inputs")) if msg.get("op") == "infer" else None
+        for wid, addr in self._candidates(model, version, shard_id, key, cost):
             if tried > self.max_retries:
                 break
             left = deadline - time.monotonic()
@@ -424,10 +428,11 @@ class Coordinator:
                 self.stats["retries"] += 1
             tried += 1
             try:
-                async with lb.track(wid):
+                async with lb.track(wid, cost):
                     rep = await self.rpc.call(addr, msg, timeout=min(self.request_timeout_s, left))
                     if not isinstance(rep, dict):
                         raise RPCError("malformed reply")
+                    lb.observe(wid, rep.pop("engine_load", None))
                     if not rep.get("success") and rep.get("retryable"):
                         raise RPCError(rep.get("error", "worker error"))
                 self.router.mark_worker_success(wid)

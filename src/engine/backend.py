@@ -105,6 +105,16 @@ class LLMBackend:
         s = self.engine.scheduler
         return (len(s.running) + len(s.waiting)) / max(1, self.engine.cfg.max_num_seqs)
 
+    def load_report(self) -> Dict[str, Any]:
+        """Engine state for the load balancer (piggybacked on every reply and health answer by the worker): the
+        engine thread's last snapshot, plus the submissions its loop has not drained yet."""
+        r = dict(self.engine.load_snapshot)
+        if not r:
+            r = {"running": 0, "waiting": 0, "waiting_prompt_tokens": 0, "max_num_seqs": self.engine.cfg.max_num_seqs,
+                 "kv_used_frac": 0.0, "step_ms": round(self.engine._step_est * 1e3, 4), "prefill_us_per_token": 0.0}
+        r["waiting"] = r.get("waiting", 0) + self.async_engine._q.qsize()
+        return r
+
     async def predict(self, inputs: Any, request_id: Optional[str] = None,
                       on_token=None) -> Dict[str, Any]:
         """One generation. ``inputs["timeout_s"]`` bounds it (the request is aborted in the engine and the

@@ -79,6 +79,8 @@ class LLMEngine:
         self.scheduler = Scheduler(cfg, self.blocks, self.max_model_len, swap_capacity_blocks=swap_blocks)
         self.seqs: Dict[str, Sequence] = {}
         self._step_est = 0.004  # EMA of one decode step (s): sizes windows that must end by a deadline
+        self._pf_tok_est = 0.0  # EMA of prefill time per prompt token (s), 0 until the first prefill step
+        self.load_snapshot: dict = {}
         # disaggregated decode: imported prompts join the running batch directly (no waiting queue), so a burst of
         # imports would otherwise join one decode WINDOW late each; while imports keep arriving (the last one less
         # than this long ago) the engine runs single steps so the next import joins at the next step
@@ -259,6 +261,10 @@ class LLMEngine:
             now = time.perf_counter()
             self.stats["mixed_time" if out.decode else "prefill_time"] = \
                 self.stats.get("mixed_time" if out.decode else "prefill_time", 0.0) + now - t0
+            ntok = sum(c.length for c in chunks if not c.decode)
+            if ntok and not out.decode:
+                per = (now - t0) / ntok
+                self._pf_tok_est = per if not self._pf_tok_est else 0.8 * self._pf_tok_est + 0.2 * per
             for c, tok in zip(chunks, toks):
                 seq = c.seq
                 if c.decode:
@@ -290,7 +296,25 @@ class LLMEngine:
         self.stats["steps"] += 1
         if self.cfg.kv_block_ttl_s:
             self.blocks.evict_expired()
+        self._update_load_snapshot()
         return finished
+
+    def _update_load_snapshot(self) -> None:
+        """The engine state a load balancer scores this worker by (src/load_balancer.py, least_latency), rebuilt
+        by the engine thread after each step and swapped in whole (readers on other threads never see a
+        half-built dict): sequences running / waiting, prompt tokens not yet prefilled, the batch cap, KV pool
+        occupancy, and the EWMA decode step time and prefill time per prompt token."""
+        sch = self.scheduler
+        wt = 0
+        for q in (sch.waiting, sch.running):
+            for sq in q:
+                if sq.num_computed < sq.prompt_len:
+                    wt += sq.prompt_len - sq.num_computed
+        self.load_snapshot = {"running": len(sch.running), "waiting": len(sch.waiting) + len(sch.swapped),
+                              "waiting_prompt_tokens": wt, "max_num_seqs": self.cfg.max_num_seqs,
+                              "kv_used_frac": round(self.blocks.usage(), 4),
+                              "step_ms": round(self._step_est * 1e3, 4),
+                              "prefill_us_per_token": round(self._pf_tok_est * 1e6, 3)}
 
     def _start_export(self, chunks):
         """Disaggregated prefill: the prompts that complete in this step and export their KV get their packets

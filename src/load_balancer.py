@@ -13,6 +13,20 @@ uses an EWMA (``latency_alpha``) so a worker that got slow is noticed, and
 an unmeasured worker is tried first exactly once (cold-start exploration).
 Optional ``groups`` partition workers (e.g. per shard / per role) so the
 coordinator can ask for "a healthy decode worker of shard 3".
+
+``least_latency`` for LLM workers (round 5): an end-to-end latency average
+mostly measures the sizes of the requests a worker happened to get (a worker
+that just served long generations looks slow), so it is not the signal. LLM
+workers piggyback their engine state on every reply and health answer
+(``engine_load``: running / waiting sequences, prompt tokens still to prefill,
+the batch cap, KV occupancy, the EWMA decode step time and prefill time per
+token — :meth:`src.engine.llm_engine.LLMEngine.load_snapshot`), and the balancer
+scores each candidate by the time the NEW request is expected to take there:
+the prefill backlog ahead of it, its own prompt at that worker's prefill rate,
+and its output tokens at that worker's decode step time, stretched when the
+running batch is over its cap. Work dispatched since the worker's last report is
+added on top. Workers that report nothing (mock models) keep the latency EWMA
+× (1 + active requests) score. Reference: `/root/reference/src/load_balancer.py:276-291`.
 """
 
 from __future__ import annotations
@@ -48,6 +62,9 @@ class WorkerStats:
     ewma_latency: Optional[float] = None
     probe_count: int = 0
     probe_latency: float = 0.0
+    report: Optional[Dict[str, Any]] = None   # the worker's last engine_load (see module doc)
+    unreported_requests: int = 0              # dispatched here since that report
+    unreported_prompt_tokens: int = 0
 
     @property
     def avg_latency(self) -> float:
@@ -79,6 +96,8 @@ class LoadBalancer:
         self.groups: Dict[str, str] = {}
         self._rr: Dict[Optional[str], int] = {}
         self._rng = random.Random(seed)
+        self._cost: Optional[Tuple[int, int]] = None
+        self._cost_ewma: Optional[Tuple[float, float]] = None
         self._running = False
         self._health_check_task: Optional[asyncio.Task] = None
         self._rpc = RPCClient(max_idle_per_host=1)
@@ -132,8 +151,10 @@ class LoadBalancer:
         return self.pick(worker_id, group, exclude)
 
     def pick(self, worker_id: Optional[str] = None, group: Optional[str] = None,
-             exclude: Optional[List[str]] = None) -> Optional[Tuple[str, str]]:
-        """Synchronous selection (the coordinator's hot path)."""
+             exclude: Optional[List[str]] = None, cost: Optional[Tuple[int, int]] = None) -> Optional[Tuple[str, str]]:
+        """Synchronous selection (the coordinator's hot path). ``cost``: (prompt tokens, max output tokens) of the
+        request, when known (least_latency uses it; see the module doc)."""
+        self._cost = cost
         if not self.workers:
             return None
         if worker_id:
@@ -162,24 +183,72 @@ class LoadBalancer:
         return self._rng.choice(ids)
 
     def _least_latency(self, ids: List[str], group: Optional[str] = None) -> str:
+        reported = [w for w in ids if self.worker_stats[w].report is not None]
+        if reported:
+            # engine-state scoring over the workers that report it; a silent one (just registered, not yet
+            # probed) is tried once while it has nothing in flight
+            silent = [w for w in ids if self.worker_stats[w].report is None
+                      and self.worker_stats[w].active_connections == 0]
+            if silent:
+                return silent[0]
+            cost = self._cost or self._default_cost()
+            return min(reported, key=lambda w: self.expected_ms(w, cost))
         cold = [w for w in ids if self.worker_stats[w].ewma_latency is None
                 and self.worker_stats[w].active_connections == 0]
         if cold:
             return cold[0]
 
-        def score(w: str) -> float:
+        def score(w: str) -> float:  # workers without an engine report (mock models)
             s = self.worker_stats[w]
             lat = s.ewma_latency if s.ewma_latency is not None else 0.0
-            # Expected wait grows with queued work on that worker.
             return lat * (1.0 + s.active_connections)
 
         return min(ids, key=score)
 
+    def _default_cost(self) -> Tuple[int, int]:
+        return self._cost_ewma if self._cost_ewma is not None else (0, 1)
+
+    def expected_ms(self, worker_id: str, cost: Tuple[int, int]) -> float:
+        """Expected time (ms) for a request of ``cost`` = (prompt tokens, output tokens) on this worker, from its
+        last engine report plus what was dispatched to it since."""
+        s = self.worker_stats[worker_id]
+        r = s.report or {}
+        p, g = cost
+        pf = float(r.get("prefill_us_per_token") or 0.0) / 1e3   # ms per prompt token
+        step = float(r.get("step_ms") or 0.0)
+        backlog = int(r.get("waiting_prompt_tokens", 0)) + s.unreported_prompt_tokens
+        seqs = int(r.get("running", 0)) + int(r.get("waiting", 0)) + s.unreported_requests + 1
+        cap = max(1, int(r.get("max_num_seqs") or 1))
+        # the decode batch is over its cap: sequences take turns (the new one also waits for a slot)
+        share = max(1.0, seqs / cap)
+        # a KV pool near full preempts / delays admission
+        kv = float(r.get("kv_used_frac") or 0.0)
+        kv_pen = 1.0 + max(0.0, kv - 0.9) * 10.0
+        return ((backlog + p) * pf + g * step * share) * kv_pen
+
     # ------------------------------------------------------ accounting
-    def acquire(self, worker_id: str) -> None:
+    def acquire(self, worker_id: str, cost: Optional[Tuple[int, int]] = None) -> None:
         s = self.worker_stats.get(worker_id)
         if s is not None:
             s.active_connections += 1
+            s.unreported_requests += 1
+            if cost:
+                s.unreported_prompt_tokens += int(cost[0])
+        if cost:
+            c = self._cost_ewma
+            self._cost_ewma = tuple(cost) if c is None else (0.9 * c[0] + 0.1 * cost[0], 0.9 * c[1] + 0.1 * cost[1])
+
+    def observe(self, worker_id: str, report: Optional[Dict[str, Any]]) -> None:
+        """A worker's engine state (``engine_load`` of a reply or a health answer): replaces the last one; what was
+        dispatched before it is in it."""
+        if not isinstance(report, dict):
+            return
+        s = self.worker_stats.get(worker_id)
+        if s is None:
+            return
+        s.report = report
+        s.unreported_requests = 0
+        s.unreported_prompt_tokens = 0
 
     def release(self, worker_id: str) -> None:
         s = self.worker_stats.get(worker_id)
@@ -187,10 +256,10 @@ class LoadBalancer:
             s.active_connections -= 1
 
     @contextlib.asynccontextmanager
-    async def track(self, worker_id: str):
+    async def track(self, worker_id: str, cost: Optional[Tuple[int, int]] = None):
         """``async with lb.track(w): ...`` — counts an active request and
         records its outcome and latency."""
-        self.acquire(worker_id)
+        self.acquire(worker_id, cost)
         t0 = time.perf_counter()
         ok = False
         try:
@@ -236,6 +305,7 @@ class LoadBalancer:
             "avg_probe_latency": s.probe_latency / s.probe_count if s.probe_count else 0.0,
             "last_seen": s.last_seen,
             "healthy": self.is_healthy(worker_id),
+            "engine_load": s.report,
         }
 
     def get_all_stats(self) -> Dict[str, Dict[str, Any]]:
@@ -266,7 +336,9 @@ class LoadBalancer:
         if self.probe == "tcp":
             ok, lat = await tcp_connect_probe(addr, self.health_check_timeout)
         else:
-            ok, lat, _ = await self._rpc.probe(addr, self.health_check_timeout)
+            ok, lat, reply = await self._rpc.probe(addr, self.health_check_timeout)
+            if ok and isinstance(reply, dict):
+                self.observe(worker_id, reply.get("engine_load"))
         s = self.worker_stats.get(worker_id)
         if s is None:
             return

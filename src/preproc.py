@@ -18,7 +18,7 @@ from __future__ import annotations
 import asyncio
 import concurrent.futures as cf
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional, Sequence
+from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 PAD_ID, BOS_ID, EOS_ID = 0, 1, 2
 _BYTE_OFFSET = 3
@@ -162,3 +162,23 @@ def preprocess(inputs: Dict[str, Any]) -> Dict[str, Any]:
     if isinstance(inputs, str):
         return inputs.strip()  # type: ignore[return-value]
     return inputs
+
+
+def request_cost(inputs: Any) -> Optional[Tuple[int, int]]:
+    """(prompt tokens, max output tokens) of an LLM request as a load balancer can estimate it without the
+    worker's tokenizer (text prompts: ~4 bytes per token), or None for other payloads."""
+    if not isinstance(inputs, dict):
+        return None
+    ids = inputs.get("prompt_token_ids")
+    if isinstance(ids, list):
+        p = len(ids)
+    elif isinstance(inputs.get("prompt"), str):
+        p = len(inputs["prompt"].encode()) // 4 + 1
+    else:
+        return None
+    try:
+        g = int(inputs.get("max_tokens", SamplingParams.max_tokens))
+    except (TypeError, ValueError):
+        g = SamplingParams.max_tokens
+    return p, max(1, g)
+

@@ -193,6 +193,7 @@ class Worker:
             self._probe_count += 1
             failed = self.failed_models()
             return {"success": not failed, "worker_id": self.worker_id, "load": self.load(), "failed_models": failed,
+                    "engine_load": self.engine_load(),
                     "models": list(self.models),
                     "archs": {n: getattr(getattr(m, "config", None), "arch", "mock") for n, m in self.models.items()}}
         if op == "metrics":
@@ -226,6 +227,9 @@ class Worker:
                 self._active -= 1
             if not resp.get("success"):
                 self._error_count += 1
+            el = self.engine_load(msg.get("model"))
+            if el is not None:  # piggybacked for the coordinator's load balancer (least_latency)
+                resp["engine_load"] = el
             return resp
         if op in ("kv_export", "kv_import", "kv_channel", "kv_reserve", "kv_release", "engine_stats"):
             m = self.models.get(msg.get("model"))
@@ -326,6 +330,17 @@ class Worker:
     def load(self) -> float:
         loads = [m.load() for m in self.models.values() if hasattr(m, "load")]
         return max(loads) if loads else float(self._active)
+
+    def engine_load(self, model: Optional[str] = None) -> Optional[Dict[str, Any]]:
+        """The engine-state report of ``model`` (default: the first model that has one), or None."""
+        ms = [self.models[model]] if model in self.models else list(self.models.values())
+        for m in ms:
+            if hasattr(m, "load_report"):
+                try:
+                    return m.load_report()
+                except Exception:  # noqa: BLE001 - a report must never fail a request
+                    return None
+        return None
 
     def get_metrics(self) -> Dict[str, Any]:
         mem = self._process.memory_info()

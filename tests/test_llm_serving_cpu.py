@@ -39,6 +39,13 @@ def test_llm_through_coordinator():
         assert again.get("cached") and again["outputs"]["token_ids"] == rs[0]["outputs"]["token_ids"]
         m = await c.call({"op": "stats"})
         assert m["success"]
+        # every LLM reply carried the worker's engine state; the balancer keeps it (least_latency's signal) and
+        # the coordinator strips it from what the client sees
+        assert "engine_load" not in rs[0]
+        lbst = [st for lbs in m["stats"]["load_balancers"].values() for st in lbs.values()] if "stats" in m else \
+            [st for lbs in m["load_balancers"].values() for st in lbs.values()]
+        el = lbst[0]["engine_load"]
+        assert el["max_num_seqs"] == 4 and el["step_ms"] > 0 and el["prefill_us_per_token"] > 0, el
         c.close()
         await coord.stop()
         await w.shutdown()
