@@ -81,9 +81,7 @@ async def run(args, pport, dport):
             "ttft_p50_ms": round(statistics.median(ttft), 1) if ttft else None,
             "ttft_p99_ms": round(ttft[int(0.99 * len(ttft)) - 1], 1) if ttft else None,
             "batch": args.batch, "waves": args.steps, "prompt_len": args.prompt_len, "gen_len": args.gen_len,
-            "kv_zone": st.get("stats", {}).get("kv_zone"), "kv_copy": os.environ.get("DIE_KV_COPY", "shader"),
-            "kv_link": link, "kv_path": link.get("kv_path"),
-            "zone_uncached": os.environ.get("DIE_KV_ZONE_UNCACHED", "1") == "1",
+            "kv_zone": st.get("stats", {}).get("kv_zone"), "kv_link": link, "kv_path": link.get("kv_path"),
             "devices": {"prefill": args.prefill_device, "decode": args.decode_device}}
 
 

@@ -17,11 +17,11 @@ inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(
 
 inline die::bf16_t* bf(const Tensor& t) { return reinterpret_cast<die::bf16_t*>(t.data_ptr()); }
 
-#define DIE_CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
-#define DIE_CHECK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bfloat16")
-#define DIE_CHECK_DTYPE(x, d) TORCH_CHECK((x).scalar_type() == (d), #x " has wrong dtype")
-#define DIE_CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
-#define DIE_HIP(call)                                                                 \
+#define CHK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bfloat16")
+#define CHK_DTYPE(x, d) TORCH_CHECK((x).scalar_type() == (d), #x " has wrong dtype")
+#define CHK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+#define HIP_OK(call)                                                                 \
   do {                                                                                \
     hipError_t e_ = (call);                                                           \
     TORCH_CHECK(e_ == hipSuccess, "HIP launch failed: ", hipGetErrorString(e_), " (", \
@@ -36,103 +36,103 @@ inline void check_rows(const Tensor& t, const char* name) {
 }
 
 void rms_norm(Tensor out, Tensor x, Tensor w, double eps) {
-  DIE_CHECK_CUDA(x);
-  DIE_CHECK_BF16(x);
-  DIE_CHECK_BF16(out);
-  DIE_CHECK_BF16(w);
+  CHK_CUDA(x);
+  CHK_BF16(x);
+  CHK_BF16(out);
+  CHK_BF16(w);
   check_rows(x, "x");
   check_rows(out, "out");
   TORCH_CHECK(out.size(0) == x.size(0) && out.size(1) == x.size(1) && w.numel() == x.size(1), "rms_norm shapes");
   TORCH_CHECK(x.size(1) <= 8 * 256 * 8, "hidden too large");
-  DIE_HIP(die::launch_rms_norm(bf(out), bf(x), bf(w), (float)eps, (int)x.size(0), (int)x.size(1), x.stride(0),
+  HIP_OK(die::launch_rms_norm(bf(out), bf(x), bf(w), (float)eps, (int)x.size(0), (int)x.size(1), x.stride(0),
                                out.stride(0), cur_stream()));
 }
 
 void fused_add_rms_norm(Tensor out, Tensor x, Tensor residual, Tensor w, double eps) {
-  DIE_CHECK_CUDA(x);
-  DIE_CHECK_BF16(x);
-  DIE_CHECK_BF16(out);
-  DIE_CHECK_BF16(residual);
-  DIE_CHECK_BF16(w);
+  CHK_CUDA(x);
+  CHK_BF16(x);
+  CHK_BF16(out);
+  CHK_BF16(residual);
+  CHK_BF16(w);
   check_rows(x, "x");
   check_rows(out, "out");
-  DIE_CHECK_CONTIG(residual);
+  CHK_CONTIG(residual);
   TORCH_CHECK(residual.size(0) == x.size(0) && residual.size(1) == x.size(1), "residual shape");
   TORCH_CHECK(out.size(0) == x.size(0) && out.size(1) == x.size(1) && w.numel() == x.size(1), "norm shapes");
   TORCH_CHECK(x.size(1) <= 8 * 256 * 8, "hidden too large");
-  DIE_HIP(die::launch_fused_add_rms_norm(bf(out), bf(x), bf(residual), bf(w), (float)eps, (int)x.size(0),
+  HIP_OK(die::launch_fused_add_rms_norm(bf(out), bf(x), bf(residual), bf(w), (float)eps, (int)x.size(0),
                                          (int)x.size(1), x.stride(0), out.stride(0), cur_stream()));
 }
 
 void silu_and_mul(Tensor out, Tensor x) {
-  DIE_CHECK_CUDA(x);
-  DIE_CHECK_BF16(x);
-  DIE_CHECK_BF16(out);
-  DIE_CHECK_CONTIG(x);
-  DIE_CHECK_CONTIG(out);
+  CHK_CUDA(x);
+  CHK_BF16(x);
+  CHK_BF16(out);
+  CHK_CONTIG(x);
+  CHK_CONTIG(out);
   TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.size(1) == 2 * out.size(1) && x.size(0) == out.size(0),
               "silu_and_mul: x [T, 2I], out [T, I]");
   TORCH_CHECK(out.size(1) % 8 == 0, "intermediate size must be a multiple of 8");
-  DIE_HIP(die::launch_silu_and_mul(bf(out), bf(x), (int)x.size(0), (int)out.size(1), cur_stream()));
+  HIP_OK(die::launch_silu_and_mul(bf(out), bf(x), (int)x.size(0), (int)out.size(1), cur_stream()));
 }
 
 void check_cache(const Tensor& c, int64_t hkv, int64_t head_dim, const char* name) {
-  DIE_CHECK_CUDA(c);
-  DIE_CHECK_BF16(c);
-  DIE_CHECK_CONTIG(c);
+  CHK_CUDA(c);
+  CHK_BF16(c);
+  CHK_CONTIG(c);
   TORCH_CHECK(c.dim() == 4 && c.size(1) == hkv && c.size(3) == head_dim, name,
               " must be [num_blocks, num_kv_heads, block_size, head_dim]");
 }
 
 void rope_and_cache(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor slot_mapping, Tensor k_cache,
                     Tensor v_cache, int64_t hq, int64_t hkv, int64_t head_dim, bool rot_q) {
-  DIE_CHECK_CUDA(qkv);
-  DIE_CHECK_BF16(qkv);
+  CHK_CUDA(qkv);
+  CHK_BF16(qkv);
   check_rows(qkv, "qkv");
   TORCH_CHECK(qkv.size(1) >= (hq + 2 * hkv) * head_dim, "qkv width < (hq + 2*hkv) * head_dim");
-  DIE_CHECK_DTYPE(positions, at::kLong);
-  DIE_CHECK_DTYPE(slot_mapping, at::kLong);
-  DIE_CHECK_DTYPE(cos_sin, at::kFloat);
-  DIE_CHECK_CONTIG(cos_sin);
+  CHK_DTYPE(positions, at::kLong);
+  CHK_DTYPE(slot_mapping, at::kLong);
+  CHK_DTYPE(cos_sin, at::kFloat);
+  CHK_CONTIG(cos_sin);
   TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == head_dim, "cos_sin must be [max_pos, head_dim]");
   TORCH_CHECK(positions.numel() >= qkv.size(0) && slot_mapping.numel() >= qkv.size(0), "positions/slots too short");
   check_cache(k_cache, hkv, head_dim, "k_cache");
   check_cache(v_cache, hkv, head_dim, "v_cache");
   TORCH_CHECK(k_cache.sizes() == v_cache.sizes(), "k/v cache shapes differ");
-  DIE_HIP(die::launch_rope_and_cache(bf(qkv), qkv.stride(0), positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
+  HIP_OK(die::launch_rope_and_cache(bf(qkv), qkv.stride(0), positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
                                      slot_mapping.data_ptr<int64_t>(), bf(k_cache), bf(v_cache), (int)qkv.size(0),
                                      (int)hq, (int)hkv, (int)head_dim, (int)k_cache.size(2), cur_stream(), rot_q));
 }
 
 void attn_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor cu_q,
                   Tensor ctx_lens, int64_t max_q_len, int64_t hq, int64_t hkv, double scale, Tensor cos_sin) {
-  DIE_CHECK_CUDA(q);
-  DIE_CHECK_BF16(q);
-  DIE_CHECK_BF16(out);
+  CHK_CUDA(q);
+  CHK_BF16(q);
+  CHK_BF16(out);
   check_rows(q, "q");
-  DIE_CHECK_CONTIG(out);
+  CHK_CONTIG(out);
   const int64_t D = 128;
   TORCH_CHECK(q.size(1) >= hq * D, "q width < hq*128 (head_dim must be 128)");
   TORCH_CHECK(out.numel() >= q.size(0) * hq * D, "out too small");
   TORCH_CHECK(hq % hkv == 0 && (hq / hkv) <= 32 && (32 % (hq / hkv)) == 0, "hq/hkv must divide 32");
   check_cache(k_cache, hkv, D, "k_cache");
   check_cache(v_cache, hkv, D, "v_cache");
-  DIE_CHECK_DTYPE(block_tables, at::kInt);
-  DIE_CHECK_DTYPE(cu_q, at::kInt);
-  DIE_CHECK_DTYPE(ctx_lens, at::kInt);
-  DIE_CHECK_CONTIG(block_tables);
+  CHK_DTYPE(block_tables, at::kInt);
+  CHK_DTYPE(cu_q, at::kInt);
+  CHK_DTYPE(ctx_lens, at::kInt);
+  CHK_CONTIG(block_tables);
   const int64_t nseq = ctx_lens.numel();
   TORCH_CHECK(cu_q.numel() >= nseq + 1 && block_tables.dim() == 2 && block_tables.size(0) >= nseq,
               "cu_q / block_tables sizes");
   // cos_sin (optional, numel 0 = absent): [max_pos, 128] fp32; Q rows are rotated on load (unrotated q)
   const bool rot = cos_sin.numel() > 0;
   if (rot) {
-    DIE_CHECK_DTYPE(cos_sin, at::kFloat);
-    DIE_CHECK_CONTIG(cos_sin);
+    CHK_DTYPE(cos_sin, at::kFloat);
+    CHK_CONTIG(cos_sin);
     TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == D && cos_sin.device() == q.device(),
                 "cos_sin must be [max_pos, 128] on q's device");
   }
-  DIE_HIP(die::launch_attn_prefill(bf(out), bf(q), q.stride(0), bf(k_cache), bf(v_cache),
+  HIP_OK(die::launch_attn_prefill(bf(out), bf(q), q.stride(0), bf(k_cache), bf(v_cache),
                                    block_tables.data_ptr<int>(), (int)block_tables.size(1), cu_q.data_ptr<int>(),
                                    ctx_lens.data_ptr<int>(), (int)nseq, (int)max_q_len, (int)hq, (int)hkv, (int)D,
                                    (int)k_cache.size(2), (float)scale, cur_stream(),
@@ -143,11 +143,11 @@ void attn_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor b
 // selects the two-kernel path (partials + merge launch).
 void attn_decode(Tensor out, Tensor part_o, Tensor part_ml, Tensor counters, Tensor q, Tensor k_cache, Tensor v_cache,
                  Tensor block_tables, Tensor ctx_lens, int64_t max_ctx, int64_t hq, int64_t hkv, double scale) {
-  DIE_CHECK_CUDA(q);
-  DIE_CHECK_BF16(q);
-  DIE_CHECK_BF16(out);
+  CHK_CUDA(q);
+  CHK_BF16(q);
+  CHK_BF16(out);
   check_rows(q, "q");
-  DIE_CHECK_CONTIG(out);
+  CHK_CONTIG(out);
   const int64_t D = 128;
   const int64_t nseq = ctx_lens.numel();
   TORCH_CHECK(q.size(0) >= nseq && q.size(1) >= hq * D, "q shape");
@@ -155,23 +155,23 @@ void attn_decode(Tensor out, Tensor part_o, Tensor part_ml, Tensor counters, Ten
   TORCH_CHECK(hq % hkv == 0 && (hq / hkv) <= 32, "hq/hkv <= 32");
   check_cache(k_cache, hkv, D, "k_cache");
   check_cache(v_cache, hkv, D, "v_cache");
-  DIE_CHECK_DTYPE(block_tables, at::kInt);
-  DIE_CHECK_DTYPE(ctx_lens, at::kInt);
-  DIE_CHECK_CONTIG(block_tables);
+  CHK_DTYPE(block_tables, at::kInt);
+  CHK_DTYPE(ctx_lens, at::kInt);
+  CHK_CONTIG(block_tables);
   TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= nseq, "block_tables shape");
   TORCH_CHECK(block_tables.size(1) * k_cache.size(2) >= max_ctx, "block table narrower than max_ctx");
   const int maxp = die::attn_decode_max_partials((int)max_ctx);
-  DIE_CHECK_DTYPE(part_o, at::kFloat);
-  DIE_CHECK_DTYPE(part_ml, at::kFloat);
+  CHK_DTYPE(part_o, at::kFloat);
+  CHK_DTYPE(part_ml, at::kFloat);
   TORCH_CHECK(part_o.numel() >= nseq * hq * maxp * D && part_ml.numel() >= nseq * hq * maxp * 2,
               "partial buffers too small for max_ctx");
   int* cnt = nullptr;
   if (counters.numel() > 0) {
-    DIE_CHECK_DTYPE(counters, at::kInt);
+    CHK_DTYPE(counters, at::kInt);
     TORCH_CHECK(counters.is_cuda() && counters.numel() >= nseq * hkv, "attn counters: int32 [>= num_seqs*hkv]");
     cnt = counters.data_ptr<int>();
   }
-  DIE_HIP(die::launch_attn_decode(bf(out), part_o.data_ptr<float>(), part_ml.data_ptr<float>(), cnt, bf(q), q.stride(0),
+  HIP_OK(die::launch_attn_decode(bf(out), part_o.data_ptr<float>(), part_ml.data_ptr<float>(), cnt, bf(q), q.stride(0),
                                   bf(k_cache), bf(v_cache), block_tables.data_ptr<int>(), (int)block_tables.size(1),
                                   ctx_lens.data_ptr<int>(), (int)nseq, (int)max_ctx, (int)hq, (int)hkv, (int)D,
                                   (int)k_cache.size(2), (float)scale, nullptr, cur_stream()));
@@ -184,11 +184,11 @@ void attn_decode_fused(Tensor out, Tensor part_o, Tensor part_ml, Tensor counter
                        Tensor positions, Tensor cos_sin, Tensor slot_mapping, Tensor k_cache, Tensor v_cache,
                        Tensor block_tables, Tensor ctx_lens, int64_t max_ctx, int64_t hq, int64_t hkv, double scale,
                        double eps, int64_t hidden) {
-  DIE_CHECK_CUDA(slab);
-  DIE_CHECK_DTYPE(slab, at::kFloat);
-  DIE_CHECK_CONTIG(slab);
-  DIE_CHECK_BF16(out);
-  DIE_CHECK_CONTIG(out);
+  CHK_CUDA(slab);
+  CHK_DTYPE(slab, at::kFloat);
+  CHK_CONTIG(slab);
+  CHK_BF16(out);
+  CHK_CONTIG(out);
   const int64_t D = 128;
   const int64_t nseq = ctx_lens.numel();
   TORCH_CHECK(slab.dim() == 3 && slab.size(1) >= nseq && slab.size(2) == (hq + 2 * hkv) * D, "slab [sk, M, width]");
@@ -199,28 +199,28 @@ void attn_decode_fused(Tensor out, Tensor part_o, Tensor part_ml, Tensor counter
   check_cache(k_cache, hkv, D, "k_cache");
   check_cache(v_cache, hkv, D, "v_cache");
   TORCH_CHECK(k_cache.size(2) == 16, "fused decode attention: block_size 16");
-  DIE_CHECK_DTYPE(block_tables, at::kInt);
-  DIE_CHECK_DTYPE(ctx_lens, at::kInt);
-  DIE_CHECK_CONTIG(block_tables);
+  CHK_DTYPE(block_tables, at::kInt);
+  CHK_DTYPE(ctx_lens, at::kInt);
+  CHK_CONTIG(block_tables);
   TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= nseq, "block_tables shape");
   TORCH_CHECK(block_tables.size(1) * 16 >= max_ctx, "block table narrower than max_ctx");
-  DIE_CHECK_DTYPE(ssp, at::kFloat);
-  DIE_CHECK_CONTIG(ssp);
+  CHK_DTYPE(ssp, at::kFloat);
+  CHK_CONTIG(ssp);
   TORCH_CHECK(ssp.dim() == 2 && ssp.size(1) == die::DECODE_SSP_LD && ssp.size(0) >= 1 && ssp.size(0) <= 128,
               "ssp [T <= 128, 128]");
-  DIE_CHECK_DTYPE(positions, at::kLong);
-  DIE_CHECK_DTYPE(slot_mapping, at::kLong);
-  DIE_CHECK_DTYPE(cos_sin, at::kFloat);
-  DIE_CHECK_CONTIG(cos_sin);
+  CHK_DTYPE(positions, at::kLong);
+  CHK_DTYPE(slot_mapping, at::kLong);
+  CHK_DTYPE(cos_sin, at::kFloat);
+  CHK_CONTIG(cos_sin);
   TORCH_CHECK(cos_sin.size(1) == D, "cos_sin [max_pos, 128]");
   TORCH_CHECK(positions.numel() >= nseq && slot_mapping.numel() >= nseq, "positions / slot_mapping");
   // decode: every sequence's new token sits at position ctx_len - 1 (the kernel uses that)
   const int maxp = die::attn_decode_max_partials((int)max_ctx);
-  DIE_CHECK_DTYPE(part_o, at::kFloat);
-  DIE_CHECK_DTYPE(part_ml, at::kFloat);
+  CHK_DTYPE(part_o, at::kFloat);
+  CHK_DTYPE(part_ml, at::kFloat);
   TORCH_CHECK(part_o.numel() >= nseq * hq * maxp * D && part_ml.numel() >= nseq * hq * maxp * 2,
               "partial buffers too small for max_ctx");
-  DIE_CHECK_DTYPE(counters, at::kInt);
+  CHK_DTYPE(counters, at::kInt);
   TORCH_CHECK(counters.is_cuda() && counters.numel() >= nseq * hkv, "attn counters: int32 [>= num_seqs*hkv]");
   die::AttnDecodeFuse fz;
   fz.slab = slab.data_ptr<float>();
@@ -233,7 +233,7 @@ void attn_decode_fused(Tensor out, Tensor part_o, Tensor part_ml, Tensor counter
   fz.eps = (float)eps;
   fz.cos_sin = cos_sin.data_ptr<float>();
   fz.slot_mapping = slot_mapping.data_ptr<int64_t>();
-  DIE_HIP(die::launch_attn_decode(bf(out), part_o.data_ptr<float>(), part_ml.data_ptr<float>(),
+  HIP_OK(die::launch_attn_decode(bf(out), part_o.data_ptr<float>(), part_ml.data_ptr<float>(),
                                   counters.data_ptr<int>(), nullptr, 0, bf(k_cache), bf(v_cache),
                                   block_tables.data_ptr<int>(), (int)block_tables.size(1), ctx_lens.data_ptr<int>(),
                                   (int)nseq, (int)max_ctx, (int)hq, (int)hkv, (int)D, 16, (float)scale, &fz,
@@ -245,10 +245,10 @@ int64_t decode_partials(int64_t max_ctx) { return die::attn_decode_max_partials(
 void sample(Tensor out, Tensor logits, c10::optional<Tensor> temperature, c10::optional<Tensor> top_k,
             c10::optional<Tensor> top_p, c10::optional<Tensor> seeds, c10::optional<Tensor> steps,
             c10::optional<Tensor> part, c10::optional<Tensor> cnt) {
-  DIE_CHECK_CUDA(logits);
-  DIE_CHECK_BF16(logits);
+  CHK_CUDA(logits);
+  CHK_BF16(logits);
   check_rows(logits, "logits");
-  DIE_CHECK_DTYPE(out, at::kLong);
+  CHK_DTYPE(out, at::kLong);
   const int64_t rows = logits.size(0);
   TORCH_CHECK(out.numel() >= rows, "out too small");
   TORCH_CHECK(logits.size(1) % 8 == 0, "vocab must be a multiple of 8");
@@ -269,7 +269,7 @@ void sample(Tensor out, Tensor logits, c10::optional<Tensor> temperature, c10::o
     pp = reinterpret_cast<uint32_t*>(part->data_ptr<int>());
     cp = cnt->data_ptr<int>();
   }
-  DIE_HIP(die::launch_sample(out.data_ptr<int64_t>(), bf(logits), logits.stride(0), (int)rows, (int)logits.size(1),
+  HIP_OK(die::launch_sample(out.data_ptr<int64_t>(), bf(logits), logits.stride(0), (int)rows, (int)logits.size(1),
                              (const float*)opt(temperature, at::kFloat, "temperature"),
                              (const int*)opt(top_k, at::kInt, "top_k"), (const float*)opt(top_p, at::kFloat, "top_p"),
                              (const int64_t*)opt(seeds, at::kLong, "seeds"),
@@ -278,130 +278,130 @@ void sample(Tensor out, Tensor logits, c10::optional<Tensor> temperature, c10::o
 
 // pool viewed as [planes, num_blocks, slab]
 void copy_blocks(Tensor pool, Tensor pairs) {
-  DIE_CHECK_CUDA(pool);
-  DIE_CHECK_BF16(pool);
-  DIE_CHECK_CONTIG(pool);
-  DIE_CHECK_DTYPE(pairs, at::kLong);
+  CHK_CUDA(pool);
+  CHK_BF16(pool);
+  CHK_CONTIG(pool);
+  CHK_DTYPE(pairs, at::kLong);
   TORCH_CHECK(pool.dim() >= 3, "pool must be [planes, num_blocks, ...]");
   TORCH_CHECK(pairs.dim() == 2 && pairs.size(1) == 2, "pairs must be [n, 2]");
   const int64_t planes = pool.size(0), nb = pool.size(1), slab = pool.numel() / (planes * nb);
-  DIE_HIP(die::launch_copy_blocks(bf(pool), pairs.data_ptr<int64_t>(), (int)pairs.size(0), (int)planes, nb, slab,
+  HIP_OK(die::launch_copy_blocks(bf(pool), pairs.data_ptr<int64_t>(), (int)pairs.size(0), (int)planes, nb, slab,
                                   cur_stream()));
 }
 
 void move_blocks(Tensor pool, Tensor buf, Tensor ids, bool gather) {
-  DIE_CHECK_CUDA(pool);
-  DIE_CHECK_BF16(pool);
-  DIE_CHECK_BF16(buf);
-  DIE_CHECK_CONTIG(pool);
-  DIE_CHECK_CONTIG(buf);
-  DIE_CHECK_DTYPE(ids, at::kLong);
+  CHK_CUDA(pool);
+  CHK_BF16(pool);
+  CHK_BF16(buf);
+  CHK_CONTIG(pool);
+  CHK_CONTIG(buf);
+  CHK_DTYPE(ids, at::kLong);
   const int64_t planes = pool.size(0), nb = pool.size(1), slab = pool.numel() / (planes * nb);
   TORCH_CHECK(buf.numel() >= ids.numel() * planes * slab, "staging buffer too small");
-  DIE_HIP(die::launch_move_blocks(bf(pool), bf(buf), ids.data_ptr<int64_t>(), (int)ids.numel(), (int)planes, nb, slab,
+  HIP_OK(die::launch_move_blocks(bf(pool), bf(buf), ids.data_ptr<int64_t>(), (int)ids.numel(), (int)planes, nb, slab,
                                   gather, cur_stream()));
 }
 
 // pool [planes, blocks, ...]: planes [plane0, plane0 + nplanes) of blocks ids[i] into the packet row at address
 // dst[i] (int64 device array; each row holds `planes` slabs). The caller keeps the destinations alive and sized.
 void gather_blocks_rows(Tensor pool, Tensor ids, Tensor dst, int64_t plane0, int64_t nplanes) {
-  DIE_CHECK_CUDA(pool);
-  DIE_CHECK_BF16(pool);
-  DIE_CHECK_CONTIG(pool);
-  DIE_CHECK_DTYPE(ids, at::kLong);
-  DIE_CHECK_DTYPE(dst, at::kLong);
+  CHK_CUDA(pool);
+  CHK_BF16(pool);
+  CHK_CONTIG(pool);
+  CHK_DTYPE(ids, at::kLong);
+  CHK_DTYPE(dst, at::kLong);
   TORCH_CHECK(ids.is_cuda() && dst.is_cuda() && ids.is_contiguous() && dst.is_contiguous() &&
                   ids.numel() == dst.numel(), "ids / dst: int64 device arrays of one length");
   const int64_t planes = pool.size(0), nb = pool.size(1), slab = pool.numel() / (planes * nb);
   TORCH_CHECK(plane0 >= 0 && nplanes >= 0 && plane0 + nplanes <= planes, "plane range outside the pool");
-  DIE_HIP(die::launch_gather_blocks_rows(bf(pool), ids.data_ptr<int64_t>(), dst.data_ptr<int64_t>(), (int)ids.numel(),
+  HIP_OK(die::launch_gather_blocks_rows(bf(pool), ids.data_ptr<int64_t>(), dst.data_ptr<int64_t>(), (int)ids.numel(),
                                          (int)plane0, (int)nplanes, nb, slab, cur_stream()));
 }
 
 void topk_softmax(Tensor w, Tensor ids, Tensor gating, bool renorm) {
-  DIE_CHECK_CUDA(gating);
-  DIE_CHECK_BF16(gating);
-  DIE_CHECK_CONTIG(gating);
-  DIE_CHECK_DTYPE(w, at::kFloat);
-  DIE_CHECK_DTYPE(ids, at::kInt);
+  CHK_CUDA(gating);
+  CHK_BF16(gating);
+  CHK_CONTIG(gating);
+  CHK_DTYPE(w, at::kFloat);
+  CHK_DTYPE(ids, at::kInt);
   TORCH_CHECK(w.sizes() == ids.sizes() && w.size(0) == gating.size(0), "topk_softmax shapes");
-  DIE_HIP(die::launch_topk_softmax(w.data_ptr<float>(), ids.data_ptr<int>(), bf(gating), (int)gating.size(0),
+  HIP_OK(die::launch_topk_softmax(w.data_ptr<float>(), ids.data_ptr<int>(), bf(gating), (int)gating.size(0),
                                    (int)gating.size(1), (int)w.size(1), renorm, cur_stream()));
 }
 
 void moe_align(Tensor offsets, Tensor sorted, Tensor pos, Tensor ids, int64_t num_experts) {
-  DIE_CHECK_DTYPE(offsets, at::kInt);
-  DIE_CHECK_DTYPE(sorted, at::kInt);
-  DIE_CHECK_DTYPE(pos, at::kInt);
-  DIE_CHECK_DTYPE(ids, at::kInt);
+  CHK_DTYPE(offsets, at::kInt);
+  CHK_DTYPE(sorted, at::kInt);
+  CHK_DTYPE(pos, at::kInt);
+  CHK_DTYPE(ids, at::kInt);
   TORCH_CHECK(offsets.numel() >= num_experts + 1 && sorted.numel() >= ids.numel() && pos.numel() >= ids.numel(),
               "moe_align buffers");
-  DIE_HIP(die::launch_moe_align(offsets.data_ptr<int>(), sorted.data_ptr<int>(), pos.data_ptr<int>(),
+  HIP_OK(die::launch_moe_align(offsets.data_ptr<int>(), sorted.data_ptr<int>(), pos.data_ptr<int>(),
                                 ids.data_ptr<int>(), (int)ids.numel(), (int)num_experts, cur_stream()));
 }
 
 void moe_gather(Tensor xs, Tensor x, Tensor sorted, int64_t topk) {
-  DIE_CHECK_BF16(xs);
-  DIE_CHECK_BF16(x);
-  DIE_CHECK_CONTIG(xs);
-  DIE_CHECK_CONTIG(x);
-  DIE_CHECK_DTYPE(sorted, at::kInt);
+  CHK_BF16(xs);
+  CHK_BF16(x);
+  CHK_CONTIG(xs);
+  CHK_CONTIG(x);
+  CHK_DTYPE(sorted, at::kInt);
   TORCH_CHECK(xs.size(0) == sorted.numel() && xs.size(1) == x.size(1) && sorted.numel() == x.size(0) * topk,
               "moe_gather shapes");
-  DIE_HIP(die::launch_moe_gather(bf(xs), bf(x), sorted.data_ptr<int>(), (int)xs.size(0), (int)topk, (int)x.size(1),
+  HIP_OK(die::launch_moe_gather(bf(xs), bf(x), sorted.data_ptr<int>(), (int)xs.size(0), (int)topk, (int)x.size(1),
                                  cur_stream()));
 }
 
 void moe_combine(Tensor out, Tensor ys, Tensor pos, Tensor w) {
-  DIE_CHECK_BF16(out);
-  DIE_CHECK_BF16(ys);
-  DIE_CHECK_CONTIG(out);
-  DIE_CHECK_CONTIG(ys);
-  DIE_CHECK_DTYPE(pos, at::kInt);
-  DIE_CHECK_DTYPE(w, at::kFloat);
+  CHK_BF16(out);
+  CHK_BF16(ys);
+  CHK_CONTIG(out);
+  CHK_CONTIG(ys);
+  CHK_DTYPE(pos, at::kInt);
+  CHK_DTYPE(w, at::kFloat);
   const int64_t T = out.size(0), K = w.size(1);
   TORCH_CHECK(w.size(0) == T && pos.numel() == T * K && ys.size(0) == T * K && ys.size(1) == out.size(1),
               "moe_combine shapes");
-  DIE_HIP(die::launch_moe_combine(bf(out), bf(ys), pos.data_ptr<int>(), w.data_ptr<float>(), (int)T, (int)K,
+  HIP_OK(die::launch_moe_combine(bf(out), bf(ys), pos.data_ptr<int>(), w.data_ptr<float>(), (int)T, (int)K,
                                   (int)out.size(1), cur_stream()));
 }
 
 // Fused decode routing: w [T, K] fp32, ids [T, K] int32 from x [T, H] (row stride ldx) and the router
 // weights wg [E, H] bf16 (moe.hip moe_route_kernel).
 void moe_route(Tensor w, Tensor ids, Tensor x, Tensor wg, bool renorm) {
-  DIE_CHECK_CUDA(x);
-  DIE_CHECK_BF16(x);
-  DIE_CHECK_BF16(wg);
-  DIE_CHECK_CONTIG(wg);
-  DIE_CHECK_CONTIG(w);
-  DIE_CHECK_CONTIG(ids);
-  DIE_CHECK_DTYPE(w, at::kFloat);
-  DIE_CHECK_DTYPE(ids, at::kInt);
+  CHK_CUDA(x);
+  CHK_BF16(x);
+  CHK_BF16(wg);
+  CHK_CONTIG(wg);
+  CHK_CONTIG(w);
+  CHK_CONTIG(ids);
+  CHK_DTYPE(w, at::kFloat);
+  CHK_DTYPE(ids, at::kInt);
   check_rows(x, "x");
   TORCH_CHECK(wg.dim() == 2 && wg.size(1) == x.size(1), "moe_route: wg [E, H]");
   TORCH_CHECK(w.dim() == 2 && w.size(0) == x.size(0) && ids.sizes() == w.sizes(), "moe_route: w, ids [T, K]");
-  DIE_HIP(die::launch_moe_route(w.data_ptr<float>(), ids.data_ptr<int>(), bf(x), x.stride(0), bf(wg),
+  HIP_OK(die::launch_moe_route(w.data_ptr<float>(), ids.data_ptr<int>(), bf(x), x.stride(0), bf(wg),
                                 (int)x.size(0), (int)x.size(1), (int)wg.size(0), (int)w.size(1), renorm,
                                 cur_stream()));
 }
 
 // resid [T, H] += combine(ys, pos, w); ssp [>= T] fp32 = row sums of squares of the new residual.
 void moe_combine_residual(Tensor ssp, Tensor resid, Tensor ys, Tensor pos, Tensor w) {
-  DIE_CHECK_CUDA(resid);
-  DIE_CHECK_BF16(resid);
-  DIE_CHECK_BF16(ys);
-  DIE_CHECK_CONTIG(ys);
-  DIE_CHECK_CONTIG(pos);
-  DIE_CHECK_CONTIG(w);
-  DIE_CHECK_CONTIG(ssp);
-  DIE_CHECK_DTYPE(ssp, at::kFloat);
-  DIE_CHECK_DTYPE(pos, at::kInt);
-  DIE_CHECK_DTYPE(w, at::kFloat);
+  CHK_CUDA(resid);
+  CHK_BF16(resid);
+  CHK_BF16(ys);
+  CHK_CONTIG(ys);
+  CHK_CONTIG(pos);
+  CHK_CONTIG(w);
+  CHK_CONTIG(ssp);
+  CHK_DTYPE(ssp, at::kFloat);
+  CHK_DTYPE(pos, at::kInt);
+  CHK_DTYPE(w, at::kFloat);
   check_rows(resid, "resid");
   const int64_t T = resid.size(0), H = resid.size(1), K = w.size(1);
   TORCH_CHECK(w.size(0) == T && pos.numel() == T * K && ys.size(0) == T * K && ys.size(1) == H && ssp.numel() >= T,
               "moe_combine_residual shapes");
-  DIE_HIP(die::launch_moe_combine_residual(ssp.data_ptr<float>(), bf(resid), resid.stride(0), bf(ys),
+  HIP_OK(die::launch_moe_combine_residual(ssp.data_ptr<float>(), bf(resid), resid.stride(0), bf(ys),
                                            pos.data_ptr<int>(), w.data_ptr<float>(), (int)T, (int)K, (int)H,
                                            cur_stream()));
 }
@@ -434,10 +434,10 @@ void attn_set_timestamps(Tensor t) {
 static void gemm_decode_impl(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t kc, int64_t sk,
                              bool nt, Tensor resid, Tensor ssp_out, Tensor counters, Tensor ssp_in, double eps,
                              die::GemmDecodeFuse fz) {
-  DIE_CHECK_CUDA(x);
-  DIE_CHECK_BF16(x);
-  DIE_CHECK_BF16(w);
-  DIE_CHECK_CONTIG(w);
+  CHK_CUDA(x);
+  CHK_BF16(x);
+  CHK_BF16(w);
+  CHK_CONTIG(w);
   check_rows(x, "x");
   const bool tiled = (mode & 32) != 0;  // w pre-packed by ops.gd_pack_weights for this (mode, wr)
   mode &= 31;
@@ -450,13 +450,13 @@ static void gemm_decode_impl(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t
   const bool silu = mode == 1 || mode == 4 || mode == 6;
   int64_t N, ldy;
   if (mode == 2 || mode == 3) {
-    DIE_CHECK_DTYPE(y, at::kFloat);
-    DIE_CHECK_CONTIG(y);
+    CHK_DTYPE(y, at::kFloat);
+    CHK_CONTIG(y);
     TORCH_CHECK(y.dim() == 3 && y.size(0) == sk && y.size(1) == M, "slab y must be [sk, M, N]");
     N = y.size(2);
     ldy = N;
   } else {
-    DIE_CHECK_BF16(y);
+    CHK_BF16(y);
     check_rows(y, "y");
     TORCH_CHECK((sk == 1 || mode == 6) && y.size(0) == M, "bf16 output: sk == 1 (mode 6: any), y [M, N]");
     N = y.size(1);
@@ -469,34 +469,34 @@ static void gemm_decode_impl(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t
   fz.tiled = tiled ? 1 : 0;
   if (mode == 3) {
     TORCH_CHECK(wrr == 32 || wrr == 64 || wrr == 128, "mode 3: wr in {32, 64, 128}");
-    DIE_CHECK_BF16(resid);
+    CHK_BF16(resid);
     check_rows(resid, "resid");
     TORCH_CHECK(resid.size(0) >= M && resid.size(1) == N, "resid [M, N]");
-    DIE_CHECK_DTYPE(ssp_out, at::kFloat);
-    DIE_CHECK_CONTIG(ssp_out);
+    CHK_DTYPE(ssp_out, at::kFloat);
+    CHK_CONTIG(ssp_out);
     TORCH_CHECK(ssp_out.numel() >= (N / wrr) * die::DECODE_SSP_LD, "ssp_out [N/wr, 128]");
     fz.resid = bf(resid);
     fz.ld_resid = resid.stride(0);
     fz.ssp_out = ssp_out.data_ptr<float>();
     if (sk > 1) {
-      DIE_CHECK_DTYPE(counters, at::kInt);
+      CHK_DTYPE(counters, at::kInt);
       TORCH_CHECK(counters.is_cuda() && counters.numel() >= N / wrr, "counters [N/wr] int32");
       fz.counters = counters.data_ptr<int>();
     }
   }
   if (mode == 6 && sk > 1) {  // split-K SiLU: ssp_out carries the fp32 partial slab [sk, M, 2N], counters the tickets
-    DIE_CHECK_DTYPE(ssp_out, at::kFloat);
-    DIE_CHECK_CONTIG(ssp_out);
+    CHK_DTYPE(ssp_out, at::kFloat);
+    CHK_CONTIG(ssp_out);
     TORCH_CHECK(ssp_out.numel() >= sk * M * 2 * N && sk * M * 2 * N * 4 < ((int64_t)1 << 31), "mode 6 slab [sk, M, 2N]");
-    DIE_CHECK_DTYPE(counters, at::kInt);
+    CHK_DTYPE(counters, at::kInt);
     TORCH_CHECK(counters.is_cuda() && counters.numel() >= N / (wrr / 2), "mode 6 counters [N / (wr / 2)] int32");
     fz.slab6 = ssp_out.data_ptr<float>();
     fz.ld_slab6 = 2 * N;
     fz.counters = counters.data_ptr<int>();
   }
   if (mode == 4 || mode == 6) {
-    DIE_CHECK_DTYPE(ssp_in, at::kFloat);
-    DIE_CHECK_CONTIG(ssp_in);
+    CHK_DTYPE(ssp_in, at::kFloat);
+    CHK_CONTIG(ssp_in);
     TORCH_CHECK(ssp_in.dim() == 2 && ssp_in.size(1) == die::DECODE_SSP_LD && ssp_in.size(0) >= 1 &&
                     ssp_in.size(0) <= 128,
                 "ssp_in [T <= 128, 128]");
@@ -505,7 +505,7 @@ static void gemm_decode_impl(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t
     fz.inv_n = 1.f / (float)K;
     fz.eps = (float)eps;
   }
-  DIE_HIP(die::launch_gemm_decode(y.data_ptr(), ldy, bf(x), x.stride(0), bf(w), (int)M, (int)N, (int)K, (int)mode,
+  HIP_OK(die::launch_gemm_decode(y.data_ptr(), ldy, bf(x), x.stride(0), bf(w), (int)M, (int)N, (int)K, (int)mode,
                                   (int)wr, (int)kc, (int)sk, nt, fz, cur_stream()));
 }
 
@@ -549,14 +549,14 @@ void gemm_decode_car(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int
 // mode 0: plain. Experts with no rows stream no weights.
 void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t mode, int64_t wr, int64_t kc,
                          Tensor rows, int64_t k, int64_t max_rows, int64_t segs) {
-  DIE_CHECK_CUDA(x);
-  DIE_CHECK_BF16(x);
-  DIE_CHECK_BF16(w);
-  DIE_CHECK_BF16(y);
-  DIE_CHECK_CONTIG(w);
+  CHK_CUDA(x);
+  CHK_BF16(x);
+  CHK_BF16(w);
+  CHK_BF16(y);
+  CHK_CONTIG(w);
   check_rows(x, "x");
   check_rows(y, "y");
-  DIE_CHECK_DTYPE(offsets, at::kInt);
+  CHK_DTYPE(offsets, at::kInt);
   TORCH_CHECK(mode == 0 || mode == 1, "grouped: mode 0 or 1");
   TORCH_CHECK(w.dim() == 3 && w.size(2) == x.size(1), "w [E, rows, K]");
   const int64_t E = w.size(0), K = x.size(1);
@@ -566,8 +566,8 @@ void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t m
   const int64_t N = mode == 1 ? w.size(1) / 2 : w.size(1);
   const bool gather = rows.numel() > 0;  // x in token order, row j of the sorted order = rows[j] / k
   if (gather) {
-    DIE_CHECK_DTYPE(rows, at::kInt);
-    DIE_CHECK_CONTIG(rows);
+    CHK_DTYPE(rows, at::kInt);
+    CHK_CONTIG(rows);
     TORCH_CHECK(k >= 1 && rows.numel() == y.size(0) && x.size(0) * k == y.size(0), "grouped gather: rows [T*k]");
   }
   TORCH_CHECK((gather || y.size(0) == x.size(0)) && y.size(1) == N, "y [R, N]");
@@ -586,7 +586,7 @@ void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t m
     fz.grp_k = (int)k;
   }
   TORCH_CHECK(y.size(0) >= 1, "grouped: at least one row");
-  DIE_HIP(die::launch_gemm_decode(y.data_ptr(), y.stride(0), bf(x), x.stride(0), bf(w),
+  HIP_OK(die::launch_gemm_decode(y.data_ptr(), y.stride(0), bf(x), x.stride(0), bf(w),
                                   (int)std::min<int64_t>(y.size(0), max_rows), (int)N, (int)K, (int)mode, (int)wr,
                                   (int)kc, 1, true, fz, cur_stream()));
 }
@@ -594,16 +594,16 @@ void gemm_decode_grouped(Tensor y, Tensor x, Tensor w, Tensor offsets, int64_t m
 // Decode-step input advance (decode_step.hip), for multi-step decode windows.
 void decode_advance(Tensor out, Tensor ids, Tensor pos, Tensor ctx, Tensor slots, Tensor bt, Tensor step,
                     Tensor tokens, Tensor cnt, Tensor n_real, int64_t rows, int64_t block_size) {
-  DIE_CHECK_CUDA(out);
-  for (const Tensor* t : {&out, &ids, &pos, &slots, &step, &tokens}) DIE_CHECK_DTYPE((*t), at::kLong);
-  for (const Tensor* t : {&ctx, &bt, &cnt, &n_real}) DIE_CHECK_DTYPE((*t), at::kInt);
-  DIE_CHECK_CONTIG(bt);
-  DIE_CHECK_CONTIG(tokens);
+  CHK_CUDA(out);
+  for (const Tensor* t : {&out, &ids, &pos, &slots, &step, &tokens}) CHK_DTYPE((*t), at::kLong);
+  for (const Tensor* t : {&ctx, &bt, &cnt, &n_real}) CHK_DTYPE((*t), at::kInt);
+  CHK_CONTIG(bt);
+  CHK_CONTIG(tokens);
   TORCH_CHECK(rows <= out.numel() && rows <= ids.numel() && rows <= pos.numel() && rows <= ctx.numel() &&
                   rows <= slots.numel() && rows <= step.numel() && rows <= bt.size(0) && rows <= tokens.size(1),
               "decode_advance: buffers smaller than rows");
   TORCH_CHECK(tokens.dim() == 2 && bt.dim() == 2, "tokens [K, S], bt [S, W]");
-  DIE_HIP(die::launch_decode_advance(out.data_ptr<int64_t>(), ids.data_ptr<int64_t>(), pos.data_ptr<int64_t>(),
+  HIP_OK(die::launch_decode_advance(out.data_ptr<int64_t>(), ids.data_ptr<int64_t>(), pos.data_ptr<int64_t>(),
                                      ctx.data_ptr<int>(), slots.data_ptr<int64_t>(), bt.data_ptr<int>(),
                                      (int)bt.size(1), step.data_ptr<int64_t>(), tokens.data_ptr<int64_t>(),
                                      (int)tokens.size(1), cnt.data_ptr<int>(), n_real.data_ptr<int>(), (int)rows,
@@ -613,84 +613,84 @@ void decode_advance(Tensor out, Tensor ids, Tensor pos, Tensor ctx, Tensor slots
 // Decode-step embedding gather + first-norm statistics (norm_act.hip): out [M, H] = table[ids], ssp[0][m] = sum of
 // squares of out[m]
 void embed_sumsq(Tensor out, Tensor ssp, Tensor table, Tensor ids) {
-  DIE_CHECK_CUDA(table);
-  DIE_CHECK_BF16(table);
-  DIE_CHECK_BF16(out);
-  DIE_CHECK_CONTIG(table);
-  DIE_CHECK_CONTIG(out);
-  DIE_CHECK_DTYPE(ids, at::kLong);
-  DIE_CHECK_CONTIG(ids);
-  DIE_CHECK_DTYPE(ssp, at::kFloat);
-  DIE_CHECK_CONTIG(ssp);
+  CHK_CUDA(table);
+  CHK_BF16(table);
+  CHK_BF16(out);
+  CHK_CONTIG(table);
+  CHK_CONTIG(out);
+  CHK_DTYPE(ids, at::kLong);
+  CHK_CONTIG(ids);
+  CHK_DTYPE(ssp, at::kFloat);
+  CHK_CONTIG(ssp);
   const int64_t M = ids.numel(), H = table.size(1);
   TORCH_CHECK(table.dim() == 2 && out.dim() == 2 && out.size(0) == M && out.size(1) == H, "out [M, H], table [V, H]");
   TORCH_CHECK(M >= 1 && M <= die::DECODE_SSP_LD && ssp.numel() >= die::DECODE_SSP_LD && H % 8 == 0,
               "embed_sumsq: 1 <= M <= 128 rows, ssp [1, 128], H % 8 == 0");
-  DIE_HIP(die::launch_embed_sumsq(bf(out), ssp.data_ptr<float>(), bf(table), ids.data_ptr<int64_t>(), (int)M, (int)H,
+  HIP_OK(die::launch_embed_sumsq(bf(out), ssp.data_ptr<float>(), bf(table), ids.data_ptr<int64_t>(), (int)M, (int)H,
                                   cur_stream()));
 }
 
 void residual_add_sumsq(Tensor ssp, Tensor resid, Tensor x) {
-  DIE_CHECK_CUDA(x);
-  DIE_CHECK_BF16(x);
-  DIE_CHECK_BF16(resid);
+  CHK_CUDA(x);
+  CHK_BF16(x);
+  CHK_BF16(resid);
   check_rows(x, "x");
   check_rows(resid, "resid");
-  DIE_CHECK_DTYPE(ssp, at::kFloat);
-  DIE_CHECK_CONTIG(ssp);
+  CHK_DTYPE(ssp, at::kFloat);
+  CHK_CONTIG(ssp);
   TORCH_CHECK(x.sizes() == resid.sizes() && x.size(0) <= die::DECODE_SSP_LD && ssp.numel() >= x.size(0),
               "residual_add_sumsq shapes");
-  DIE_HIP(die::launch_residual_add_sumsq(ssp.data_ptr<float>(), bf(resid), bf(x), (int)x.size(0), (int)x.size(1),
+  HIP_OK(die::launch_residual_add_sumsq(ssp.data_ptr<float>(), bf(resid), bf(x), (int)x.size(0), (int)x.size(1),
                                          resid.stride(0), x.stride(0), cur_stream()));
 }
 
 void row_sumsq(Tensor ssp, Tensor x) {
-  DIE_CHECK_CUDA(x);
-  DIE_CHECK_BF16(x);
+  CHK_CUDA(x);
+  CHK_BF16(x);
   check_rows(x, "x");
-  DIE_CHECK_DTYPE(ssp, at::kFloat);
-  DIE_CHECK_CONTIG(ssp);
+  CHK_DTYPE(ssp, at::kFloat);
+  CHK_CONTIG(ssp);
   TORCH_CHECK(x.size(0) <= die::DECODE_SSP_LD && ssp.numel() >= x.size(0), "row_sumsq: x [<= 128, H], ssp [1, 128]");
-  DIE_HIP(die::launch_row_sumsq(ssp.data_ptr<float>(), bf(x), (int)x.size(0), (int)x.size(1), x.stride(0),
+  HIP_OK(die::launch_row_sumsq(ssp.data_ptr<float>(), bf(x), (int)x.size(0), (int)x.size(1), x.stride(0),
                                 cur_stream()));
 }
 
 void fused_add_rms_norm_slab(Tensor out, Tensor slab, Tensor residual, Tensor w, double eps) {
-  DIE_CHECK_CUDA(slab);
-  DIE_CHECK_DTYPE(slab, at::kFloat);
-  DIE_CHECK_CONTIG(slab);
-  DIE_CHECK_BF16(out);
-  DIE_CHECK_BF16(residual);
-  DIE_CHECK_CONTIG(residual);
+  CHK_CUDA(slab);
+  CHK_DTYPE(slab, at::kFloat);
+  CHK_CONTIG(slab);
+  CHK_BF16(out);
+  CHK_BF16(residual);
+  CHK_CONTIG(residual);
   check_rows(out, "out");
   TORCH_CHECK(slab.dim() == 3 && slab.size(1) == residual.size(0) && slab.size(2) == residual.size(1),
               "slab [sk, rows, hidden] must match residual");
   TORCH_CHECK(out.size(0) == residual.size(0) && out.size(1) == residual.size(1) && w.numel() == residual.size(1),
               "shapes");
   TORCH_CHECK(residual.size(1) <= 8 * 256 * 8 && residual.size(1) % 8 == 0, "hidden");
-  DIE_HIP(die::launch_fused_add_rms_norm_slab(bf(out), slab.data_ptr<float>(), (int)slab.size(0), bf(residual), bf(w),
+  HIP_OK(die::launch_fused_add_rms_norm_slab(bf(out), slab.data_ptr<float>(), (int)slab.size(0), bf(residual), bf(w),
                                               (float)eps, (int)residual.size(0), (int)residual.size(1),
                                               out.stride(0), cur_stream()));
 }
 
 void rope_and_cache_slab(Tensor q_out, Tensor slab, Tensor positions, Tensor cos_sin, Tensor slot_mapping,
                          Tensor k_cache, Tensor v_cache, int64_t hq, int64_t hkv, int64_t head_dim) {
-  DIE_CHECK_CUDA(slab);
-  DIE_CHECK_DTYPE(slab, at::kFloat);
-  DIE_CHECK_CONTIG(slab);
-  DIE_CHECK_BF16(q_out);
-  DIE_CHECK_CONTIG(q_out);
+  CHK_CUDA(slab);
+  CHK_DTYPE(slab, at::kFloat);
+  CHK_CONTIG(slab);
+  CHK_BF16(q_out);
+  CHK_CONTIG(q_out);
   const int64_t T = slab.size(1);
   TORCH_CHECK(slab.dim() == 3 && slab.size(2) == (hq + 2 * hkv) * head_dim, "slab [sk, T, (hq+2hkv)*D]");
   TORCH_CHECK(q_out.numel() >= T * hq * head_dim, "q_out too small");
-  DIE_CHECK_DTYPE(positions, at::kLong);
-  DIE_CHECK_DTYPE(slot_mapping, at::kLong);
-  DIE_CHECK_DTYPE(cos_sin, at::kFloat);
+  CHK_DTYPE(positions, at::kLong);
+  CHK_DTYPE(slot_mapping, at::kLong);
+  CHK_DTYPE(cos_sin, at::kFloat);
   TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == head_dim, "cos_sin must be [max_pos, head_dim]");
   TORCH_CHECK(positions.numel() >= T && slot_mapping.numel() >= T, "positions/slots too short");
   check_cache(k_cache, hkv, head_dim, "k_cache");
   check_cache(v_cache, hkv, head_dim, "v_cache");
-  DIE_HIP(die::launch_rope_and_cache_slab(bf(q_out), slab.data_ptr<float>(), (int)slab.size(0),
+  HIP_OK(die::launch_rope_and_cache_slab(bf(q_out), slab.data_ptr<float>(), (int)slab.size(0),
                                           positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
                                           slot_mapping.data_ptr<int64_t>(), bf(k_cache), bf(v_cache), (int)T,
                                           (int)hq, (int)hkv, (int)head_dim, (int)k_cache.size(2), cur_stream()));
@@ -700,18 +700,18 @@ void rope_and_cache_slab(Tensor q_out, Tensor slab, Tensor positions, Tensor cos
 int64_t car_alloc(int64_t bytes, bool uncached) {
   TORCH_CHECK(bytes > 0 && bytes % 256 == 0, "car_alloc: bytes must be a positive multiple of 256");
   void* p = nullptr;
-  DIE_HIP(die::car_malloc(&p, (size_t)bytes, uncached));
+  HIP_OK(die::car_malloc(&p, (size_t)bytes, uncached));
   return reinterpret_cast<int64_t>(p);
 }
 
 // dst_ptr (raw device pointer, e.g. an IPC-mapped peer buffer) <- src (contiguous GPU tensor), by a
 // copy kernel on the current stream
 void car_copy_to(int64_t dst_ptr, Tensor src) {
-  DIE_CHECK_CUDA(src);
-  DIE_CHECK_CONTIG(src);
+  CHK_CUDA(src);
+  CHK_CONTIG(src);
   const int64_t nbytes = src.numel() * src.element_size();
   TORCH_CHECK(dst_ptr != 0 && nbytes % 16 == 0, "car_copy_to: null destination or size not a multiple of 16");
-  DIE_HIP(die::launch_ipc_copy(reinterpret_cast<void*>(dst_ptr), src.data_ptr(), nbytes, cur_stream()));
+  HIP_OK(die::launch_ipc_copy(reinterpret_cast<void*>(dst_ptr), src.data_ptr(), nbytes, cur_stream()));
 }
 
 // A byte tensor over raw device memory we own or mapped (IPC landing zones); no deleter: the owner
@@ -722,11 +722,11 @@ Tensor car_tensor(int64_t ptr, int64_t nbytes, int64_t device) {
                           torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, (int)device));
 }
 
-void car_release(int64_t ptr) { DIE_HIP(die::car_free(reinterpret_cast<void*>(ptr))); }
+void car_release(int64_t ptr) { HIP_OK(die::car_free(reinterpret_cast<void*>(ptr))); }
 
 py::bytes car_handle(int64_t ptr) {
   char h[sizeof(hipIpcMemHandle_t)];
-  DIE_HIP(die::car_ipc_handle(reinterpret_cast<void*>(ptr), h));
+  HIP_OK(die::car_ipc_handle(reinterpret_cast<void*>(ptr), h));
   return py::bytes(h, sizeof(h));
 }
 
@@ -742,17 +742,17 @@ int64_t car_open(py::bytes handle) {
   return reinterpret_cast<int64_t>(p);
 }
 
-void car_close(int64_t ptr) { DIE_HIP(die::car_ipc_close(reinterpret_cast<void*>(ptr))); }
+void car_close(int64_t ptr) { HIP_OK(die::car_ipc_close(reinterpret_cast<void*>(ptr))); }
 
 void car_all_reduce_residual(Tensor x, Tensor resid, Tensor ssp, int64_t rank, std::vector<int64_t> bufs,
                              std::vector<int64_t> sigs, int64_t ctl, int64_t cap_elems) {
-  DIE_CHECK_CUDA(x);
-  DIE_CHECK_BF16(x);
-  DIE_CHECK_BF16(resid);
-  DIE_CHECK_CONTIG(x);
-  DIE_CHECK_CONTIG(resid);
-  DIE_CHECK_DTYPE(ssp, at::kFloat);
-  DIE_CHECK_CONTIG(ssp);
+  CHK_CUDA(x);
+  CHK_BF16(x);
+  CHK_BF16(resid);
+  CHK_CONTIG(x);
+  CHK_CONTIG(resid);
+  CHK_DTYPE(ssp, at::kFloat);
+  CHK_CONTIG(ssp);
   TORCH_CHECK(x.dim() == 2 && resid.sizes() == x.sizes(), "x and resid must both be [rows, hidden]");
   const int64_t rows = x.size(0), hidden = x.size(1);
   TORCH_CHECK(hidden % 8 == 0 && rows <= die::CAR_MAX_BLOCKS && rows * hidden <= cap_elems,
@@ -769,7 +769,7 @@ void car_all_reduce_residual(Tensor x, Tensor resid, Tensor ssp, int64_t rank, s
     peers.buf[p] = reinterpret_cast<die::bf16_t*>(bufs[p]);
     peers.sig[p] = reinterpret_cast<uint32_t*>(sigs[p]);
   }
-  DIE_HIP(die::launch_custom_all_reduce_residual(bf(x), bf(resid), ssp.data_ptr<float>(), (int)rows, (int)hidden,
+  HIP_OK(die::launch_custom_all_reduce_residual(bf(x), bf(resid), ssp.data_ptr<float>(), (int)rows, (int)hidden,
                                                  (int)rank, world, peers, reinterpret_cast<uint32_t*>(ctl), cap_elems,
                                                  cur_stream()));
 }
@@ -777,8 +777,8 @@ void car_all_reduce_residual(Tensor x, Tensor resid, Tensor ssp, int64_t rank, s
 std::vector<int64_t> car_read_words(int64_t ptr, int64_t n) {  // synchronising host read of uint32 words
   TORCH_CHECK(n > 0 && n <= 64, "car_read_words: 1..64 words");
   std::vector<uint32_t> h((size_t)n);
-  DIE_HIP(hipDeviceSynchronize());
-  DIE_HIP(hipMemcpy(h.data(), reinterpret_cast<void*>(ptr), (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(h.data(), reinterpret_cast<void*>(ptr), (size_t)n * 4, hipMemcpyDeviceToHost));
   return std::vector<int64_t>(h.begin(), h.end());
 }
 
@@ -797,11 +797,11 @@ static die::CarPeers car_peers(const std::vector<int64_t>& bufs, const std::vect
 // out [rows, world * cols] = concatenation of every rank's in [rows, cols] along the last dim
 void car_all_gather(Tensor in, Tensor out, int64_t rank, std::vector<int64_t> bufs, std::vector<int64_t> sigs,
                     int64_t ctl, int64_t cap_elems, int64_t blocks) {
-  DIE_CHECK_CUDA(in);
-  DIE_CHECK_BF16(in);
-  DIE_CHECK_BF16(out);
-  DIE_CHECK_CONTIG(in);
-  DIE_CHECK_CONTIG(out);
+  CHK_CUDA(in);
+  CHK_BF16(in);
+  CHK_BF16(out);
+  CHK_CONTIG(in);
+  CHK_CONTIG(out);
   const int world = (int)bufs.size();
   TORCH_CHECK(in.dim() == 2 && out.dim() == 2 && out.size(0) == in.size(0) && out.size(1) == world * in.size(1),
               "all_gather: in [rows, cols], out [rows, world * cols]");
@@ -809,18 +809,18 @@ void car_all_gather(Tensor in, Tensor out, int64_t rank, std::vector<int64_t> bu
   TORCH_CHECK(reinterpret_cast<uintptr_t>(in.data_ptr()) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "all_gather: 16-byte alignment");
   TORCH_CHECK(rank >= 0 && rank < world && ctl != 0, "all_gather: bad rank / control word");
-  DIE_HIP(die::launch_custom_all_gather(bf(in), bf(out), in.size(0), in.size(1), (int)rank, world,
+  HIP_OK(die::launch_custom_all_gather(bf(in), bf(out), in.size(0), in.size(1), (int)rank, world,
                                         car_peers(bufs, sigs), reinterpret_cast<uint32_t*>(ctl), cap_elems,
                                         (int)blocks, cur_stream()));
 }
 
 void car_all_reduce(Tensor in, Tensor out, int64_t rank, std::vector<int64_t> bufs, std::vector<int64_t> sigs,
                     int64_t ctl, int64_t cap_elems, int64_t blocks) {
-  DIE_CHECK_CUDA(in);
-  DIE_CHECK_BF16(in);
-  DIE_CHECK_BF16(out);
-  DIE_CHECK_CONTIG(in);
-  DIE_CHECK_CONTIG(out);
+  CHK_CUDA(in);
+  CHK_BF16(in);
+  CHK_BF16(out);
+  CHK_CONTIG(in);
+  CHK_CONTIG(out);
   TORCH_CHECK(in.numel() == out.numel(), "all_reduce: in/out sizes differ");
   TORCH_CHECK(in.numel() % 8 == 0 && in.numel() <= cap_elems, "all_reduce: numel must be a multiple of 8 <= cap");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(in.data_ptr()) % 16 == 0 &&
@@ -834,98 +834,12 @@ void car_all_reduce(Tensor in, Tensor out, int64_t rank, std::vector<int64_t> bu
     peers.buf[p] = reinterpret_cast<die::bf16_t*>(bufs[p]);
     peers.sig[p] = reinterpret_cast<uint32_t*>(sigs[p]);
   }
-  DIE_HIP(die::launch_custom_all_reduce(bf(in), bf(out), in.numel(), (int)rank, world, peers,
+  HIP_OK(die::launch_custom_all_reduce(bf(in), bf(out), in.numel(), (int)rank, world, peers,
                                         reinterpret_cast<uint32_t*>(ctl), cap_elems, (int)blocks, cur_stream()));
 }
 
 }  // namespace
 
-#ifdef DIE_KERNEL_DIAG
-// Persistent decode step (decode_persistent.hip; diagnostics build only — measured slower than the five-launch
-// layer, docs/performance.md): the instantiation's tiles and workspace layout for a shape.
-std::vector<int64_t> decode_persistent_config(int64_t H, int64_t I, int64_t hq, int64_t hkv, int64_t layers) {
-  int cfg[7];
-  int64_t lay[9];
-  if (!die::decode_persistent_config((int)H, (int)I, (int)hq, (int)hkv, (int)layers, cfg, lay)) return {};
-  std::vector<int64_t> v(cfg, cfg + 7);
-  v.insert(v.end(), lay, lay + 9);
-  return v;
-}
-
-// layers [l0, l1) of a dense decode step in one launch. `table` [L, 6] int64 = per layer the device pointers of
-// the tile-packed qkv / o / gate_up / down weights and of the layer's K / V cache (built by the model from
-// tensors it keeps alive); `pool` [L, 2, blocks, hkv, 16, 128] is only checked against the table's geometry.
-void decode_persistent(Tensor ws, Tensor table, Tensor h, Tensor ssp0, Tensor block_tables, Tensor ctx_lens,
-                       Tensor slot_mapping, Tensor cos_sin, Tensor pool, int64_t l0, int64_t l1, int64_t I,
-                       int64_t hq, int64_t hkv, double scale, double eps, c10::optional<Tensor> prof) {
-  DIE_CHECK_CUDA(h);
-  DIE_CHECK_BF16(h);
-  DIE_CHECK_CONTIG(h);
-  TORCH_CHECK(h.dim() == 2 && h.size(0) >= 1 && h.size(0) <= 32, "h [M <= 32, H]");
-  const int64_t M = h.size(0), H = h.size(1), L = table.size(0);
-  int cfg[7];
-  int64_t lay[9];
-  TORCH_CHECK(die::decode_persistent_config((int)H, (int)I, (int)hq, (int)hkv, (int)L, cfg, lay),
-              "decode_persistent: no instantiation for this model shape");
-  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.is_contiguous() && table.dim() == 2 &&
-                  table.size(1) == 6, "table [L, 6] int64 on the GPU");
-  // the workspace's dependency counters are never reset (each launch advances them by a fixed amount): one
-  // workspace serves one layer range, the whole table
-  TORCH_CHECK(l0 == 0 && l1 == L, "decode_persistent runs every layer of its table (l0 = 0, l1 = L)");
-  TORCH_CHECK(ws.is_cuda() && ws.is_contiguous() && ws.numel() * ws.element_size() >= lay[0] &&
-                  reinterpret_cast<uintptr_t>(ws.data_ptr()) % 256 == 0, "workspace too small or misaligned");
-  DIE_CHECK_CUDA(pool);
-  DIE_CHECK_BF16(pool);
-  DIE_CHECK_CONTIG(pool);
-  TORCH_CHECK(pool.dim() == 6 && pool.size(0) == L && pool.size(1) == 2 && pool.size(3) == hkv && pool.size(4) == 16 &&
-                  pool.size(5) == 128, "pool [L, 2, blocks, hkv, 16, 128]");
-  DIE_CHECK_DTYPE(ssp0, at::kFloat);
-  DIE_CHECK_CONTIG(ssp0);
-  TORCH_CHECK(ssp0.dim() == 2 && ssp0.size(1) == die::DECODE_SSP_LD && ssp0.size(0) >= 1 && ssp0.size(0) <= 128,
-              "ssp0 [tiles <= 128, 128]");
-  DIE_CHECK_DTYPE(block_tables, at::kInt);
-  DIE_CHECK_CONTIG(block_tables);
-  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= M, "block_tables [>= M, width]");
-  DIE_CHECK_DTYPE(ctx_lens, at::kInt);
-  TORCH_CHECK(ctx_lens.is_contiguous() && ctx_lens.numel() >= M, "ctx_lens [>= M]");
-  DIE_CHECK_DTYPE(slot_mapping, at::kLong);
-  TORCH_CHECK(slot_mapping.is_contiguous() && slot_mapping.numel() >= M, "slot_mapping [>= M]");
-  DIE_CHECK_DTYPE(cos_sin, at::kFloat);
-  DIE_CHECK_CONTIG(cos_sin);
-  TORCH_CHECK(cos_sin.dim() == 2 && cos_sin.size(1) == 128, "cos_sin [max_pos, 128]");
-  die::DpArgs a{};
-  a.layers = reinterpret_cast<const die::DpLayerW*>(table.data_ptr());
-  a.ws = reinterpret_cast<char*>(ws.data_ptr());
-  a.h = bf(h);
-  a.ssp0 = ssp0.data_ptr<float>();
-  a.bt = block_tables.data_ptr<int>();
-  a.ctx = ctx_lens.data_ptr<int>();
-  a.slots = slot_mapping.data_ptr<int64_t>();
-  a.cos_sin = cos_sin.data_ptr<float>();
-  a.l0 = (int)l0;
-  a.l1 = (int)l1;
-  a.M = (int)M;
-  a.bt_stride = (int)block_tables.stride(0);
-  a.ssp0_tiles = (int)ssp0.size(0);
-  a.scale_log2 = (float)scale * 1.4426950408889634f;  // as the attention launchers round it
-  a.eps = (float)eps;
-  a.inv_h = 1.f / (float)H;
-  a.H = (int)H;
-  a.I = (int)I;
-  a.hq = (int)hq;
-  a.hkv = (int)hkv;
-  if (prof.has_value()) {  // timeline stamps (written only by DIE_KERNEL_DIAG builds)
-    int dev = 0, ncu = 0;
-    DIE_HIP(hipGetDevice(&dev));
-    DIE_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    TORCH_CHECK(prof->is_cuda() && prof->scalar_type() == at::kLong && prof->is_contiguous() &&
-                    prof->numel() >= (int64_t)ncu * ((l1 - l0) * 5 * 4 + 32), "prof [grid, phases * 4 + 32] int64");
-    a.prof = reinterpret_cast<uint64_t*>(prof->data_ptr());
-    a.dbg = 0;
-  }
-  DIE_HIP(die::launch_decode_persistent(a, cur_stream()));
-}
-#endif  // DIE_KERNEL_DIAG
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "Hand-written gfx950 (MI355X) HIP kernels";
@@ -936,10 +850,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_prefill", &attn_prefill);
   m.def("attn_decode", &attn_decode);
   m.def("attn_decode_fused", &attn_decode_fused);
-#ifdef DIE_KERNEL_DIAG
-  m.def("decode_persistent_config", &decode_persistent_config);
-  m.def("decode_persistent", &decode_persistent);
-#endif
   m.def("decode_partials", &decode_partials);
   m.def("sample", &sample, py::arg("out"), py::arg("logits"), py::arg("temperature") = py::none(),
         py::arg("top_k") = py::none(), py::arg("top_p") = py::none(), py::arg("seeds") = py::none(),

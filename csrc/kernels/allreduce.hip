@@ -206,10 +206,10 @@ uint32_t car_spin_limit() {
   return v;
 }
 
-int car_mode() {
-  static const int m = getenv("DIE_CAR_MODE") ? atoi(getenv("DIE_CAR_MODE")) : 1;
-  return m;
-}
+// Synchronisation variant of the one-shot protocol: bit 0 = peers' staging read with system-coherent (sc0 sc1)
+// loads instead of an acquire fence, bit 1 = no release fence before the flag store. 1 is the measured and
+// validated form (round 1: uncached staging + system-scope release + sc0 sc1 loads).
+int car_mode() { return 1; }
 
 hipError_t launch_custom_all_reduce_residual(const bf16_t* in, bf16_t* resid, float* ssp, int rows, int hidden,
                                              int rank, int world, const CarPeers& peers, uint32_t* ctl,

@@ -34,15 +34,6 @@
 #include "common.h"
 #include "launchers.h"
 
-// Diagnostic bisection bits (DIE_ATTN_DBG for decode, DIE_PF_XCD bits 1-2 for prefill) exist only in a
-// diagnostics build (-DDIE_KERNEL_DIAG, `DIE_KERNEL_DIAG=1 python -m src._build --force`); in the production
-// build DIAG(x) is the constant 0 and those branches are compiled out.
-#ifdef DIE_KERNEL_DIAG
-#define DIAG(x) (x)
-#else
-#define DIAG(x) 0
-#endif
-
 namespace die {
 
 using namespace attn;
@@ -61,7 +52,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
                                                            const int* __restrict__ block_tables, int bt_stride,
                                                            const int* __restrict__ cu_q,
                                                            const int* __restrict__ ctx_lens, int hq, int hkv,
-                                                           int block_size, float scale_log2, int xcd_swz,
+                                                           int block_size, float scale_log2,
                                                            const float* __restrict__ cos_sin, int n_pos) {
   constexpr int TPW = 32 / G;   // tokens per wave
   constexpr int TPB = NW * TPW;  // tokens per workgroup
@@ -73,7 +64,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
   const int gx = gridDim.x, gy = gridDim.y;
   const int hw = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
   const int nwg = gx * gy * gridDim.z, xq = nwg >> 3, xr = nwg & 7, xcd = hw & 7;
-  const int lid = (xcd_swz & 1) ? (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (hw >> 3) : hw;
+  const int lid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (hw >> 3);
   const int bx = lid % gx, seq = (lid / gx) % gy, kvh = lid / (gx * gy);
   const int qbeg = cu_q[seq], qlen = cu_q[seq + 1] - qbeg;
   const int t0 = (gx - 1 - bx) * TPB;  // heaviest (latest) tiles of a group launch first
@@ -97,9 +88,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
   const int* bt = block_tables + (int64_t)seq * bt_stride;
 
   bf16x8_t qf[8];
-  // xcd_swz bit 1 (diagnostic): every row reads the Q row of token 0 (an L2 hit) instead of its own
-  load_q(qf, row_valid ? q + (DIAG(xcd_swz & 2) ? (int64_t)head * D : (int64_t)(qbeg + tok) * q_stride + (int64_t)head * D)
-                       : nullptr, h);
+  load_q(qf, row_valid ? q + (int64_t)(qbeg + tok) * q_stride + (int64_t)head * D : nullptr, h);
   if (cos_sin != nullptr && row_valid) {
     // RoPE (neox pairs (i, i + 64)) on the Q row as it is loaded: qf[kk] holds dims 16 kk + 8 h + [0, 8)
     // and qf[kk + 4] their partners, so the rotation is lane-local (the rope kernel skips q)
@@ -152,8 +141,8 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
     *reinterpret_cast<u32x4_t*>(kl + (ks % KT + kr) * K_PITCH + c * 16) = kreg[i];
     *reinterpret_cast<u32x4_t*>(vl + (ks % KT + kr) * V_PITCH + c * 16) = vreg[i];
   };
-#define DIE_LOAD_STAGE(kt, K, V) static_for<NP>([&](auto I) { load_one(kt, I, K, V); })
-#define DIE_STORE_STAGE(buf, K, V) static_for<NP>([&](auto I) { store_one(buf, I, K, V); })
+#define LOAD_STAGE(kt, K, V) static_for<NP>([&](auto I) { load_one(kt, I, K, V); })
+#define STORE_STAGE(buf, K, V) static_for<NP>([&](auto I) { store_one(buf, I, K, V); })
   auto compute = [&](int kt, int cur) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
@@ -171,9 +160,9 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
   };
 
   // stage s lives in register set A (s even) or B (s odd), then in LDS buffer s & 1
-  DIE_LOAD_STAGE(0, kA, vA);
-  DIE_LOAD_STAGE(min(1, ntiles - 1), kB, vB);  // past the last stage: a harmless re-read, never stored
-  DIE_STORE_STAGE(0, kA, vA);
+  LOAD_STAGE(0, kA, vA);
+  LOAD_STAGE(min(1, ntiles - 1), kB, vB);  // past the last stage: a harmless re-read, never stored
+  STORE_STAGE(0, kA, vA);
   __syncthreads();
   // the per-stage barrier orders the LDS writes and reads only: no vmcnt(0) (a __syncthreads here would
   // drain the prefetch that is meant to stay in flight across it)
@@ -183,25 +172,25 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
   };
 #pragma unroll 1
   for (int kt = 0; kt < ntiles; kt += 2) {
-    DIE_LOAD_STAGE(min(kt + 2, ntiles - 1), kA, vA);  // set A is free: stage kt is in LDS buffer 0
+    LOAD_STAGE(min(kt + 2, ntiles - 1), kA, vA);  // set A is free: stage kt is in LDS buffer 0
     compute(kt, 0);
-    if (kt + 1 < ntiles) DIE_STORE_STAGE(1, kB, vB);       // buffer 1 was last read two stages ago
+    if (kt + 1 < ntiles) STORE_STAGE(1, kB, vB);       // buffer 1 was last read two stages ago
     stage_barrier();
     if (kt + 1 >= ntiles) break;
-    DIE_LOAD_STAGE(min(kt + 3, ntiles - 1), kB, vB);
+    LOAD_STAGE(min(kt + 3, ntiles - 1), kB, vB);
     compute(kt + 1, 1);
-    if (kt + 2 < ntiles) DIE_STORE_STAGE(0, kA, vA);
+    if (kt + 2 < ntiles) STORE_STAGE(0, kA, vA);
     stage_barrier();
   }
-#undef DIE_LOAD_STAGE
-#undef DIE_STORE_STAGE
+#undef LOAD_STAGE
+#undef STORE_STAGE
 
   // Epilogue: O staged through LDS and stored as whole rows. Stored straight from the MFMA layout, every
   // 8-byte lane store touched 32 rows (32 partial lines per instruction) and the store tail cost ~45 us
   // of a 32 x 512 prefill (micro_attn_prefill_xcd_r2.txt); a row of 256 B is 16 lanes x 16 B, so each
   // wave stores its 32 x 128 tile in 8 instructions of 4 full rows. The loop ended on a barrier that
   // follows every wave's last LDS read, so the ring is free; each wave uses its own 32-row region.
-  if (!DIAG(xcd_swz & 4)) {  // bit 2 (diagnostic): no O store
+  {
     constexpr int OP = 272;  // staging row pitch (bytes): 2-way conflicts at most on the b64 writes
     char* ob = smem + wave * 32 * OP;
     const float inv = 1.f / st.l;
@@ -399,7 +388,7 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters,
     const bf16_t* __restrict__ q, int64_t q_stride, bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, int num_seqs, int hq,
-    int hkv, float scale_log2, int maxp, int dbg, AttnDecodeFuse fz, const int64_t* __restrict__ slot_mapping) {
+    int hkv, float scale_log2, int maxp, AttnDecodeFuse fz, const int64_t* __restrict__ slot_mapping) {
   constexpr int QI = (G * 256 + 1023) / 1024;  // LDS-DMA instructions for the query rows
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* ml = reinterpret_cast<float*>(smem + 2 * V3_BUF);
@@ -437,7 +426,6 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
 
     // LDS-DMA chunk c (K and V rows of 128 keys) into buffer b: 16 instructions per lane.
     auto issue = [&](int c, int b) {
-      if (DIAG(dbg & 2)) return;
       char* base = smem + b * V3_BUF;
       // this wave's two 16-key blocks of the chunk; the table row is read speculatively
       // (clamped to the row, not to the context) so the loads do not wait for ctx
@@ -465,7 +453,7 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
     // sum, norm scale, RoPE, KV write) runs while the chunk streams in; only a counted vmcnt separates
     // them (the chunk stays in flight).
     if constexpr (FUSED) {
-      if (!DIAG(dbg & 2)) {
+      {
         const float* srow = fz.slab + (int64_t)seq * fz.width;
         for (int i = wave; i < (frows + 1) / 2; i += 4) {
           const int ri = min(2 * i + (lane >> 5), frows - 1);
@@ -481,7 +469,7 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
         if (wave == 1)  // decode: the new token sits at position ctx - 1
           glds16(fz.cos_sin + (int64_t)(ctx - 1) * D + (lane & 31) * 4, fa + fs_off + 512);
       }
-    } else if (wave == 0 && !DIAG(dbg & 2)) {  // the G query rows of this (seq, kv head), 256 B each
+    } else if (wave == 0) {  // the G query rows of this (seq, kv head), 256 B each
       const bf16_t* qb = q + (int64_t)seq * q_stride + (int64_t)kvh * G * D;
 #pragma unroll
       for (int i = 0; i < QI; ++i) {
@@ -586,7 +574,7 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
                            : zero_frag();
         if (fz.ts != nullptr) tsv[2] = __builtin_amdgcn_s_memrealtime();
       }
-      if (!DIAG(dbg & 1)) {
+      {
         const int kb = c * DEC_KEYS + 32 * wave;  // keys >= ctx: clamped rows, masked to -inf
         f32x16_t s = qk_lds_swz(base + 32 * wave * DEC_ROW, qf, lane);
         softmax_tile_lazy(s, st, kb, ctx, scale_log2, h);
@@ -596,7 +584,6 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     if (fz.ts != nullptr) tsv[3] = __builtin_amdgcn_s_memrealtime();
-    if (DIAG(dbg & 32)) continue;
 
     // merge the 4 waves' (m, l, O) through LDS
     if (row < G) {
@@ -752,37 +739,26 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
   if (head_dim != D || hq % hkv || block_size % 16) return hipErrorInvalidValue;
   const int G = hq / hkv;
   const float sl2 = scale * 1.4426950408889634f;
-  static const int nw = [] {
-    const char* e = getenv("DIE_PF_NW");
-    return e && atoi(e) == 4 ? 4 : 8;
-  }();
-  static const int xcd_swz = [] {
-    const char* e = getenv("DIE_PF_XCD");  // bit 0: XCD-aware order (default on); bits 1-2: diagnostics
-    return e ? atoi(e) : 1;
-  }();
-  const int tpb = nw * (32 / (G > 32 ? 32 : G));
-  dim3 grid((max_q_len + tpb - 1) / tpb, num_seqs, hkv), block(64 * nw);
+  constexpr int NW = 8;  // one 512-thread workgroup per CU (two 4-wave workgroups measured slower, round 2)
+  const int tpb = NW * (32 / (G > 32 ? 32 : G));
+  dim3 grid((max_q_len + tpb - 1) / tpb, num_seqs, hkv), block(64 * NW);
   const size_t lds = 2 * 2 * KV_TILE;
-#define DIE_PF(GG)                                                                                             \
+#define PF_CASE(GG)                                                                                            \
   case GG:                                                                                                     \
-    if (nw == 8)                                                                                               \
-      hipLaunchKernelGGL((attn_prefill_kernel<GG, 2, 8>), grid, block, lds, s, out, q, q_stride, k_cache,      \
-                         v_cache, block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2, xcd_swz, cos_sin, n_pos);          \
-    else                                                                                                       \
-      hipLaunchKernelGGL((attn_prefill_kernel<GG, 2, 4>), grid, block, lds, s, out, q, q_stride, k_cache,      \
-                         v_cache, block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2, xcd_swz, cos_sin, n_pos);          \
+    hipLaunchKernelGGL((attn_prefill_kernel<GG, 2, NW>), grid, block, lds, s, out, q, q_stride, k_cache,       \
+                       v_cache, block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2, cos_sin, n_pos); \
     break;
   switch (G) {
-    DIE_PF(1)
-    DIE_PF(2)
-    DIE_PF(4)
-    DIE_PF(8)
-    DIE_PF(16)
-    DIE_PF(32)
+    PF_CASE(1)
+    PF_CASE(2)
+    PF_CASE(4)
+    PF_CASE(8)
+    PF_CASE(16)
+    PF_CASE(32)
     default:
       return hipErrorInvalidValue;
   }
-#undef DIE_PF
+#undef PF_CASE
   return hipGetLastError();
 }
 
@@ -809,11 +785,6 @@ hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* c
     const float sl2 = scale * 1.4426950408889634f;
     const int tasks = num_seqs * hkv * maxp3;
     const int ncu = num_cus();
-#ifdef DIE_KERNEL_DIAG
-    static const int dbg = getenv("DIE_ATTN_DBG") ? atoi(getenv("DIE_ATTN_DBG")) : 0;  // perf experiments only
-#else
-    constexpr int dbg = 0;
-#endif
     dim3 grid(tasks < ncu ? tasks : ncu), block(256);
     AttnDecodeFuse none{};
     none.ts = g_attn_ts;
@@ -823,24 +794,24 @@ hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* c
       fzc.ts = g_attn_ts;
       fz = &fzc;
     }
-#define DIE_D3(GG)                                                                                              \
+#define D3_CASE(GG)                                                                                              \
   case GG:                                                                                                      \
     if (fz)                                                                                                     \
       hipLaunchKernelGGL((attn_decode_v3_kernel<GG, true>), grid, block, V3_LDS, s, out, part_o, part_ml,       \
                          counters, q, q_stride, k_cache, v_cache, block_tables, bt_stride, ctx_lens, num_seqs, hq, \
-                         hkv, sl2, maxp3, dbg, *fz, fz->slot_mapping);                                          \
+                         hkv, sl2, maxp3, *fz, fz->slot_mapping);                                          \
     else                                                                                                        \
       hipLaunchKernelGGL((attn_decode_v3_kernel<GG, false>), grid, block, V3_LDS, s, out, part_o, part_ml,      \
                          counters, q, q_stride, k_cache, v_cache, block_tables, bt_stride, ctx_lens, num_seqs, hq, \
-                         hkv, sl2, maxp3, dbg, none, nullptr);                                                  \
+                         hkv, sl2, maxp3, none, nullptr);                                                  \
     break;
     switch (G) {
-      DIE_D3(1)
-      DIE_D3(2)
-      DIE_D3(4)
-      DIE_D3(8)
+      D3_CASE(1)
+      D3_CASE(2)
+      D3_CASE(4)
+      D3_CASE(8)
     }
-#undef DIE_D3
+#undef D3_CASE
     return hipGetLastError();
   }
   if (G > 32 || G * D * 4 * 4 + 4 * 32 * 2 * 4 > DEC_LDS) return hipErrorInvalidValue;
@@ -848,22 +819,22 @@ hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* c
   const int maxp = (max_ctx + DEC_KEYS - 1) / DEC_KEYS;
   const int tasks = num_seqs * hkv * maxp;
   dim3 grid(tasks < 512 ? tasks : 512), block(256);
-#define DIE_DC(GG)                                                                                          \
+#define DC_CASE(GG)                                                                                          \
   case GG:                                                                                                  \
     hipLaunchKernelGGL(attn_decode_kernel<GG>, grid, block, DEC_LDS + 16, s, part_o, part_ml, q, q_stride,      \
                        k_cache, v_cache, block_tables, bt_stride, ctx_lens, num_seqs, hq, hkv, block_size, sl2, maxp); \
     break;
   switch (G) {
-    DIE_DC(1)
-    DIE_DC(2)
-    DIE_DC(4)
-    DIE_DC(8)
-    DIE_DC(16)
-    DIE_DC(32)
+    DC_CASE(1)
+    DC_CASE(2)
+    DC_CASE(4)
+    DC_CASE(8)
+    DC_CASE(16)
+    DC_CASE(32)
     default:
       return hipErrorInvalidValue;
   }
-#undef DIE_DC
+#undef DC_CASE
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(num_seqs, hq), dim3(128), 0, s, out, part_o, part_ml,

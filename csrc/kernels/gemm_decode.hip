@@ -611,11 +611,7 @@ static hipError_t launch_gd(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, 
   // Activation image: the smallest of 16 / 32 / 64 / 128 rows that holds M and exists for this tile
   // (16 only on the nt path). Measured (profiles/micro_gemm_decode_xr16_r1.jsonl): dense 8B projections
   // at M = 8 / 16 ~1.5 % faster with 16 rows than 32; Mixtral grouped experts a tie.
-  static const bool xr16 = [] {
-    const char* e = std::getenv("DIE_GD_XR16");  // A/B knob: 0 = never the 16-row image
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  if (M <= 16 && xr16 && nt && gd_valid(WR, 16, KC))
+  if (M <= 16 && nt && gd_valid(WR, 16, KC))
     return launch_gd_xr<WR, EPI, KC, 16, SKC>(Y, ldy, X, ldx, W, M, N_out, K, sk, nt, fz, s);
   if (M <= 32 && gd_valid(WR, 32, KC))
     return launch_gd_xr<WR, EPI, KC, 32, SKC>(Y, ldy, X, ldx, W, M, N_out, K, sk, nt, fz, s);
@@ -678,22 +674,22 @@ hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx
     for (int p = 0; p < fz.car_world; ++p)
       if (fz.car.buf[p] == nullptr || fz.car.sig[p] == nullptr) return hipErrorInvalidValue;
   }
-#define DIE_GD(WR, KC) \
+#define GD_TILE(WR, KC) \
   if (wr == WR && kc == KC) return launch_modes<WR, KC>(Y, ldy, X, ldx, W, M, N, K, mode, sk, nt, fz, s);
-  DIE_GD(32, 256)
-  DIE_GD(48, 256)
-  DIE_GD(64, 256)
-  DIE_GD(32, 128)
-  DIE_GD(48, 128)
-  DIE_GD(64, 128)
-  DIE_GD(96, 128)
-  DIE_GD(112, 128)
-  DIE_GD(128, 128)
-  DIE_GD(64, 64)
-  DIE_GD(128, 64)
-  DIE_GD(64, 32)
-  DIE_GD(128, 32)
-#undef DIE_GD
+  GD_TILE(32, 256)
+  GD_TILE(48, 256)
+  GD_TILE(64, 256)
+  GD_TILE(32, 128)
+  GD_TILE(48, 128)
+  GD_TILE(64, 128)
+  GD_TILE(96, 128)
+  GD_TILE(112, 128)
+  GD_TILE(128, 128)
+  GD_TILE(64, 64)
+  GD_TILE(128, 64)
+  GD_TILE(64, 32)
+  GD_TILE(128, 32)
+#undef GD_TILE
   return hipErrorInvalidValue;
 }
 

@@ -85,7 +85,7 @@ struct CarPeers {
   uint32_t* sig[CAR_MAX_RANKS] = {};  // per rank: flag page [2][CAR_MAX_BLOCKS][CAR_MAX_RANKS]
 };
 uint32_t car_spin_limit();            // bounded polls of a peer's flag (DIE_CAR_SPIN)
-int car_mode();                       // synchronisation variant (DIE_CAR_MODE)
+int car_mode();                       // synchronisation variant of the one-shot protocol (allreduce.hip)
 
 // Fusion operands of the decode GEMM (modes 3 and 4, see gemm_decode.hip). Norm statistics arrays have a
 // row stride of DECODE_SSP_LD = 128 (the largest decode batch).
@@ -145,39 +145,6 @@ hipError_t launch_custom_all_gather(const bf16_t* in, bf16_t* out, int64_t rows,
                                     hipStream_t s);
 hipError_t car_malloc(void** p, size_t bytes, bool uncached = true);
 
-// Persistent decode step (decode_persistent.hip): layers [l0, l1) of a dense Llama decode step in one launch.
-struct DpLayerW {
-  const bf16_t* qkv;  // tile-packed (gd_pack_weights) for (wrq, kc 128)
-  const bf16_t* o;    // (wro, 128)
-  const bf16_t* gu;   // (wrg, 128), silu layout
-  const bf16_t* dn;   // (wrd, 128)
-  bf16_t* kc;         // the layer's paged K / V cache [blocks][hkv][16][128]
-  bf16_t* vc;
-};
-constexpr int DP_SYNC_LD = 5 * 16 * 32;  // dependency counter words per layer: 5 phases x 16 shards x 128 B
-// Scratch of the persistent step lives in ONE workspace (compile-time offsets per model shape, rows padded
-// to 32): qkv slabs, attention output, o / down slabs, SiLU output, norm statistics, split-K tickets, the
-// error word and the per-layer dependency counters (decode_persistent_layout gives the offsets).
-struct DpArgs {
-  const DpLayerW* layers;  // device array, indexed by absolute layer
-  char* ws;                // workspace (zero-initialised once; its counters only ever advance)
-  bf16_t* h;               // residual stream [M][H] (in / out)
-  const float* ssp0;       // statistics of h at entry [ssp0_tiles][128]
-  const int* bt;           // block tables [M][bt_stride]
-  const int* ctx;          // KV length after this step [M]
-  const int64_t* slots;    // the new token's cache slot [M] (-1: none)
-  const float* cos_sin;    // [max_pos][128]
-  int l0, l1, M, bt_stride, ssp0_tiles;
-  float scale_log2, eps, inv_h;
-  int H, I, hq, hkv;       // the model shape (selects the instantiation; checked by the launcher)
-  uint64_t* prof;          // diagnostic builds: timeline stamps [grid][phases][4] (nullptr: none)
-  int dbg;                 // reserved (0)
-};
-// the instantiation for a model shape: cfg7 = {wrq, skq, wro, sko, wrg, wrd, skd} and the workspace layout
-// lay4[9] = {bytes for `layers` layers, offsets of: the error word, the counters, slab_q, attn, slab_od, act,
-// ssp_o, ssp_d}; false if the shape has none
-bool decode_persistent_config(int H, int I, int hq, int hkv, int layers, int* cfg7, int64_t* lay4);
-hipError_t launch_decode_persistent(const DpArgs& a, hipStream_t s);
 hipError_t launch_embed_sumsq(bf16_t* out, float* ssp, const bf16_t* table, const int64_t* ids, int rows, int hidden,
                               hipStream_t s);
 hipError_t launch_ipc_copy(void* dst, const void* src, int64_t nbytes, hipStream_t s);

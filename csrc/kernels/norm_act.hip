@@ -64,24 +64,24 @@ static hipError_t rms_dispatch(bf16_t* out, const bf16_t* in, bf16_t* residual, 
                                int rows, int hidden, int64_t in_stride, int64_t out_stride, hipStream_t s) {
   const int nc = (hidden / 8 + NT - 1) / NT;
   dim3 grid(rows), block(NT);
-#define DIE_RMS_CASE(N)                                                                               \
+#define RMS_CASE(N)                                                                               \
   case N:                                                                                             \
     hipLaunchKernelGGL((rmsnorm_kernel<NT, N, FUSED>), grid, block, 0, s, out, in, residual, w, eps, \
                        hidden, in_stride, out_stride);                                                \
     break;
   switch (nc) {
-    DIE_RMS_CASE(1)
-    DIE_RMS_CASE(2)
-    DIE_RMS_CASE(3)
-    DIE_RMS_CASE(4)
-    DIE_RMS_CASE(5)
-    DIE_RMS_CASE(6)
-    DIE_RMS_CASE(7)
-    DIE_RMS_CASE(8)
+    RMS_CASE(1)
+    RMS_CASE(2)
+    RMS_CASE(3)
+    RMS_CASE(4)
+    RMS_CASE(5)
+    RMS_CASE(6)
+    RMS_CASE(7)
+    RMS_CASE(8)
     default:
       return hipErrorInvalidValue;
   }
-#undef DIE_RMS_CASE
+#undef RMS_CASE
   return hipGetLastError();
 }
 
@@ -155,20 +155,20 @@ hipError_t launch_fused_add_rms_norm_slab(bf16_t* out, const float* slab, int sk
   const int nc = (hidden / 8 + 255) / 256;
   dim3 grid(rows), block(256);
   switch (nc) {
-#define DIE_RS(N)                                                                                              \
+#define RS_CASE(N)                                                                                              \
   case N:                                                                                                      \
     hipLaunchKernelGGL((rmsnorm_slab_kernel<256, N>), grid, block, 0, s, out, slab, sk, residual, w, eps, rows, \
                        hidden, out_stride);                                                                    \
     break;
-    DIE_RS(1)
-    DIE_RS(2)
-    DIE_RS(3)
-    DIE_RS(4)
-    DIE_RS(5)
-    DIE_RS(6)
-    DIE_RS(7)
-    DIE_RS(8)
-#undef DIE_RS
+    RS_CASE(1)
+    RS_CASE(2)
+    RS_CASE(3)
+    RS_CASE(4)
+    RS_CASE(5)
+    RS_CASE(6)
+    RS_CASE(7)
+    RS_CASE(8)
+#undef RS_CASE
     default:
       return hipErrorInvalidValue;
   }

@@ -5,7 +5,6 @@ kernels and the torch bindings into ``src/_C*.so`` and the host runtime
 
     python -m src._build            # incremental
     python -m src._build --force
-    DIE_KERNEL_DIAG=1 python -m src._build   # diagnostics build -> src/_Cdiag*.so (DIE_C_DIAG=1 loads it)
 
 The kernels are compiled once here with ``hipcc --offload-arch=gfx950`` and the
 ``.so`` files travel with the repo snapshot to the GPU box.
@@ -28,10 +27,7 @@ ARCH = os.environ.get("DIE_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 KERNELS = ["norm_act", "rope_cache", "attention", "sampling", "moe", "gemm_decode", "decode_step", "allreduce"]
-# kernels the serving path does not use, compiled into the diagnostics build only: the persistent decode step
-# (one launch per step) measured 0.70-0.77x of the five-launch layer (docs/performance.md, round 3)
-DIAG_KERNELS = ["decode_persistent"]
-CONTRACT_ON = {"attention", "gemm_decode", "decode_persistent"}
+CONTRACT_ON = {"attention", "gemm_decode"}
 
 
 def _torch_paths():
@@ -61,30 +57,26 @@ def _headers(d: str):
 
 def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
     os.makedirs(OBJ, exist_ok=True)
-    is_diag = os.environ.get("DIE_KERNEL_DIAG") == "1"
-    # the diagnostics build is a separate file (loaded instead of _C with DIE_C_DIAG=1): both travel
-    out = os.path.join(ROOT, "src", ("_Cdiag" if is_diag else "_C") + EXT_SUFFIX)
+    out = os.path.join(ROOT, "src", "_C" + EXT_SUFFIX)
     kdir = os.path.join(CSRC, "kernels")
     hdrs = _headers(kdir)
     incs, torch_lib, abi = _torch_paths()
     jobs_list = []
     objs = []
-    for k in KERNELS + (DIAG_KERNELS if is_diag else []):
+    for k in KERNELS:
         src = os.path.join(kdir, k + ".hip")
-        obj = os.path.join(OBJ, k + (".diag.o" if is_diag else ".o"))
+        obj = os.path.join(OBJ, k + ".o")
         objs.append(obj)
         if force or _newer(obj, [src] + hdrs + [os.path.abspath(__file__)]):
-            diag = ["-DDIE_KERNEL_DIAG"] if is_diag else []
-            # the decode kernels fuse multiply-adds per source expression only (not across statements): the
-            # persistent decode step and the multi-launch path then round identically (bit-exact tests)
+            # the decode kernels fuse multiply-adds per source expression only (not across statements)
             contract = ["-ffp-contract=on"] if k in CONTRACT_ON else []
-            jobs_list.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *diag, *contract, "-I",
+            jobs_list.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *contract, "-I",
                               CSRC, "-c", src, "-o", obj])
     bsrc = os.path.join(CSRC, "bindings.cpp")
-    bobj = os.path.join(OBJ, "bindings.diag.o" if is_diag else "bindings.o")
+    bobj = os.path.join(OBJ, "bindings.o")
     objs.append(bobj)
     if force or _newer(bobj, [bsrc] + hdrs):
-        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", *(["-DDIE_KERNEL_DIAG"] if is_diag else []),
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC",
                f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__=1",
                "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
                "-I", CSRC, "-I", "/opt/rocm/include", "-I", sysconfig.get_paths()["include"]]

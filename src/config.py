@@ -114,6 +114,19 @@ class EngineConfig:
     # 2,048), so decode is interrupted less; TTFT pays up to the wait. 0 disables.
     prefill_batch_tokens: int = 0
     prefill_batch_wait_ms: float = 60.0
+    # disaggregated prefill: export each finishing prompt's KV per group of kv_export_group layers while the rest
+    # of the forward runs (False: one gather after the step). Overlapped 48.95 vs 47.31 req/s
+    # (profiles/disagg_r4_overlap_vs_not.jsonl)
+    kv_export_overlap: bool = True
+    kv_export_group: int = 4
+    # disaggregated decode: single-step windows while imported prompts keep arriving (the last one less than
+    # this long ago), so each joins at the next step instead of the next window (50.02 -> 50.65 req/s,
+    # profiles/disagg_r4_import_settle_ab.jsonl). 0: off
+    import_settle_ms: float = 3.0
+    # open-loop arrivals: with two or more prompts arrived during decode within this lookback, no continuation
+    # window is queued behind the running one (Poisson 40 req/s TTFT p50 38.6 -> 29.8 ms at equal e2e,
+    # profiles/poisson_r4_arrival_ab.jsonl). 0: off
+    arrival_window_ms: float = 250.0
 
 
 @dataclass

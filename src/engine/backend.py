@@ -85,6 +85,11 @@ class LLMBackend:
         self.total_latency = 0.0
         self._live: Dict[str, str] = {}  # client request_id -> engine request id (abort)
         self._zone = None                # IPC landing zone for shipped KV (decode role, lazily)
+        ov = config.overrides or {}
+        # prefill role: gather each prompt's KV straight into a slot of the decode worker's landing zone reserved
+        # before the prompt runs (False: gather locally, then copy into a slot — the staged path, A/B only)
+        self.kv_direct = bool(ov.get("kv_direct", True))
+        self.kv_zone_bytes = int(ov.get("kv_landing_zone_bytes", 4 << 30))
         self.ipc_imports = 0
 
     async def start(self) -> None:
@@ -230,7 +235,7 @@ class LLMBackend:
         # straight into it (one pass over xGMI, no staging tensor, no second copy). Otherwise the packet takes
         # the staged path, whose reserve may wait for space AFTER the prompt has run.
         slot = None
-        if self.engine.device.type == "cuda" and os.environ.get("DIE_KV_DIRECT", "1") == "1":
+        if self.engine.device.type == "cuda" and self.kv_direct:
             from src.parallel.kv_transfer import packet_shape
 
             nb = self.engine.blocks.blocks_needed(len(gi.prompt_token_ids))
@@ -276,10 +281,9 @@ class LLMBackend:
         if self._zone is None:
             from src.parallel.kv_transfer import IPCLandingZone
 
-            cap = int((self.config.overrides or {}).get("kv_landing_zone_bytes",
-                                                         os.environ.get("DIE_KV_ZONE_BYTES", 4 << 30)))
-            self._zone = IPCLandingZone(self.engine.device, cap,
-                                        uncached=os.environ.get("DIE_KV_ZONE_UNCACHED", "1") == "1")
+            # uncached (fine-grained) segments: a peer GPU's stores over xGMI are not cached in this GPU's L2
+            # under a stale line (coherence; no measurable cost, profiles/r4_disagg_zone_uncached_vs_cached.jsonl)
+            self._zone = IPCLandingZone(self.engine.device, self.kv_zone_bytes, uncached=True)
         return self._zone
 
     async def _kv_import(self, msg: Dict[str, Any]) -> Dict[str, Any]:
@@ -291,13 +295,6 @@ class LLMBackend:
         handed: List[bool] = []
         off = -1
         ready = None
-        if d.get("ipc") is not None and d["ipc"].get("event") is not None:
-            # the sender's copies may still be in flight: our stream waits on its IPC completion event
-            try:
-                ready = torch.cuda.Event.from_ipc_handle(self.engine.device, bytes(d["ipc"]["event"]))
-            except Exception as e:  # the slot stays the sender's: it polls and re-sends without the event
-                logger.info("cannot open an IPC event (%s): asking the sender to poll", e)
-                return {"success": False, "event_unsupported": True}
         if d.get("ipc") is not None:  # payload delivered (or being delivered) into the landing zone by the sender
             zone, off = self._landing_zone(), int(d["ipc"]["offset"])
             kv = zone.claim(off, d["shape"], d["ipc"].get("gen"))  # a view: the engine scatters from the zone

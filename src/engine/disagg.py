@@ -100,8 +100,6 @@ class RemoteDecodeLink:
         self.wire_packets = 0
         self._tasks: set = set()  # background releases: held here (the loop keeps only weak references)
         self.slot_offsets: List[int] = []  # landing-zone offset of every direct packet (slot reuse, tests)
-        self.ipc_events = True     # hand completion over as an IPC event (until the decode side refuses one)
-        self.event_handoffs = 0
 
     # seconds kept between the local deadline of a direct export and the decode worker's reservation TTL
     DEADLINE_MARGIN_S = 5.0
@@ -120,8 +118,7 @@ class RemoteDecodeLink:
 
     def stats(self) -> Dict[str, Any]:
         return {"kv_path": self.kv_path, "direct_packets": self.direct_packets, "staged_packets": self.staged_packets,
-                "wire_packets": self.wire_packets, "ipc": self._ipc is not None, "event_handoffs": self.event_handoffs,
-                "decode_worker": self.address}
+                "wire_packets": self.wire_packets, "ipc": self._ipc is not None, "decode_worker": self.address}
 
     async def _channel(self, device):
         if self._ipc is not None or not self.use_ipc or device.type != "cuda":
@@ -203,20 +200,6 @@ class RemoteDecodeLink:
         imported = False
         self.slot_offsets.append(off)
         try:
-            handle = self._event_handle(packet.ready)
-            if handle is not None:
-                # IPC event hand-off: the decode worker's stream waits for the copies itself — the import goes out
-                # while the last layer group may still be in flight (no poll, no host round trip in between)
-                wire = dict(packet_meta(packet), ipc={"offset": off, "gen": gen, "event": handle})
-                rep = await self.rpc.call(self.address, {"op": "kv_import", "model": self.model, "packet": wire},
-                                          self.timeout)
-                if not rep.get("event_unsupported"):
-                    self.ipc_packets += 1
-                    self.direct_packets += 1
-                    self.event_handoffs += 1
-                    imported = True
-                    return rep
-                self.ipc_events = False  # the decode side cannot open IPC events: poll from now on
             await self._ipc.wait_ready(packet.ready)
             wire = dict(packet_meta(packet), ipc={"offset": off, "gen": gen})
             self.ipc_packets += 1
@@ -228,15 +211,6 @@ class RemoteDecodeLink:
             if not imported:
                 await self.abandon(slot, packet.ready)
             raise
-
-    def _event_handle(self, ev) -> Optional[bytes]:
-        """The IPC handle of an interprocess completion event (None: a plain event, or IPC events off)."""
-        if ev is None or not self.ipc_events:
-            return None
-        try:
-            return bytes(ev.ipc_handle())
-        except Exception:  # not an interprocess event
-            return None
 
     async def abandon(self, slot: Dict[str, Any], ready=None) -> None:
         """Give a reserved slot back (the prompt failed or was cancelled): once ``ready`` (the gather into

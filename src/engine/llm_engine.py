@@ -83,20 +83,13 @@ class LLMEngine:
         self.load_snapshot: dict = {}
         # disaggregated decode: imported prompts join the running batch directly (no waiting queue), so a burst of
         # imports would otherwise join one decode WINDOW late each; while imports keep arriving (the last one less
-        # than this long ago) the engine runs single steps so the next import joins at the next step
-        import os
-
-        self._import_settle_s = float(os.environ.get("DIE_IMPORT_SETTLE_MS", "3")) / 1e3
+        # than cfg.import_settle_ms ago) the engine runs single steps so the next import joins at the next step
+        self._import_settle_s = float(cfg.import_settle_ms) / 1e3
         self._last_import = -1e9
         # open-loop arrivals: times of the requests that arrived while sequences were decoding (a closed-loop wave
-        # arrives while the engine is idle and is not counted). While two or more arrived within the lookback
-        # (DIE_ARRIVAL_WINDOW_MS, 0 = off) the engine queues no continuation window behind a running one
-        # (DIE_ARRIVAL_MODE=noqueue, default), so a new prompt waits for the rest of ONE window, not a window plus a
-        # queued continuation: Poisson 40 req/s TTFT p50 38.6 -> 29.8 ms, p99 84 -> 58 ms at equal e2e p50
-        # (profiles/poisson_r4_arrival_ab.jsonl). "cap" shortens the windows instead (TTFT p50 24 ms, TPOT +5 %).
+        # arrives while the engine is idle and is not counted); see EngineConfig.arrival_window_ms
         self._dec_arrivals: "collections.deque[float]" = collections.deque(maxlen=64)
-        self._arrival_lookback_s = float(os.environ.get("DIE_ARRIVAL_WINDOW_MS", "250")) / 1e3
-        self._arrival_mode = os.environ.get("DIE_ARRIVAL_MODE", "noqueue")
+        self._arrival_lookback_s = float(cfg.arrival_window_ms) / 1e3
         self.stats = {"prompt_tokens": 0, "generated_tokens": 0, "finished": 0, "prefill_time": 0.0,
                       "decode_time": 0.0, "steps": 0, "prefix_hit_tokens": 0}
         logger.info("KV pool: %d blocks x %d tokens = %.1f GiB (%d tokens)", nblocks, cfg.block_size,
@@ -320,13 +313,11 @@ class LLMEngine:
         """Disaggregated prefill: the prompts that complete in this step and export their KV get their packets
         now (a reserved landing-zone slot — taken under its lock, see ExportSlot — or a staging tensor), and a
         LayerGroupExporter copies each group of layers into them while the rest of the forward runs. None when
-        nothing exports (or off the GPU, under TP, or with DIE_KV_OVERLAP=0: the export then gathers everything
-        after the step, in _append)."""
-        import os
-
+        nothing exports (or off the GPU, under TP, or with cfg.kv_export_overlap off: the export then gathers
+        everything after the step, in _append)."""
         from src.parallel.kv_transfer import LayerGroupExporter, packet_shape
 
-        if self.device.type != "cuda" or os.environ.get("DIE_KV_OVERLAP", "1") == "0":
+        if self.device.type != "cuda" or not self.cfg.kv_export_overlap:
             return None
         if getattr(self.model, "tp", None) is not None and self.model.tp.enabled:
             return None
@@ -351,21 +342,14 @@ class LLMEngine:
         if not targets:
             return None
         ex = LayerGroupExporter(planes, self.arch.num_layers, [(ids, buf) for _, ids, buf in targets],
-                                group=int(os.environ.get("DIE_KV_OVERLAP_GROUP", "4")))
+                                group=self.cfg.kv_export_group)
         ex.seqs = [s for s, _, _ in targets]
         return ex
 
     def _finish_export(self, ex) -> None:
-        import os
-
-        # DIE_KV_IPC_EVENT=1: an IPC completion event where a packet goes to another process's landing zone, the
-        # decode worker's stream waits on it directly. Default off: the sender polls completion, then signals by
-        # RPC — measured faster on MI355X (two-process bench 49.55 vs 49.01 req/s,
-        # profiles/disagg_r4_ipc_event_ab.jsonl: opening an IPC event and a stream wait on it cost the decode
-        # worker more than the poll + one RPC the event saves)
-        ipc = os.environ.get("DIE_KV_IPC_EVENT", "0") == "1" and any(
-            getattr(s, "_export_slot_taken", None) is not None for s in ex.seqs)
-        ev = ex.finish(interprocess=ipc)
+        # the sender polls the completion event, then signals by RPC (an IPC completion event the decode worker's
+        # stream waits on measured slower: 49.01 vs 49.55 req/s, profiles/disagg_r4_ipc_event_ab.jsonl)
+        ev = ex.finish()
         for seq in ex.seqs:
             seq.kv_export_ready = ev  # type: ignore[attr-defined]
             slot = getattr(seq, "_export_slot_taken", None)
@@ -446,16 +430,12 @@ class LLMEngine:
         return [t for t in self._dec_arrivals if now - t < self._arrival_lookback_s]
 
     def _arrival_cap(self, continuation: bool = False) -> int:
-        """Window cap from the recent arrival rate during decode: half the mean gap between arrivals, in steps
-        (a large number when nothing arrived in the lookback). In "noqueue" mode only continuations are
-        affected: none is queued while prompts keep arriving."""
-        recent = self._recent_arrivals()
-        if len(recent) < 2:
+        """While prompts keep arriving during decode (two or more in the lookback), no continuation window is
+        queued behind the running one: a new prompt then waits for the rest of ONE window. (Shortening the
+        windows to half the arrival gap instead gave TTFT p50 24 ms but TPOT +5 %, e2e +3 %: not kept.)"""
+        if len(self._recent_arrivals()) < 2:
             return 1 << 30
-        if self._arrival_mode == "noqueue":
-            return 0 if continuation else 1 << 30
-        gap = (recent[-1] - recent[0]) / (len(recent) - 1)
-        return max(1, int(0.5 * gap / max(self._step_est, 1e-4)))
+        return 0 if continuation else 1 << 30
 
     def _importing(self) -> bool:
         """A burst of imported (disaggregated) prompts is still arriving."""

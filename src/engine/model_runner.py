@@ -18,7 +18,6 @@ from __future__ import annotations
 
 import bisect
 import logging
-import os
 from typing import Dict, List, Optional, Sequence as Seq
 
 import torch
@@ -66,8 +65,8 @@ class ModelRunner:
         self.pool = pool
         self.cfg = cfg
         self.device = model.device
-        # prefill's last layer only for the sampled rows (CausalLM._last_layer_kept_rows; DIE_PRUNE_LAST=0: all)
-        self.prune_last = os.environ.get("DIE_PRUNE_LAST", "1") != "0"
+        # prefill's last layer only for the sampled rows (CausalLM._last_layer_kept_rows)
+        self.prune_last = True
         self.is_cuda = self.device.type == "cuda"
         self.bs = pool.block_size
         self.max_model_len = max_model_len
@@ -103,7 +102,6 @@ class ModelRunner:
         self._cpar = 0
         self.inflight: Optional[Dict[str, object]] = None  # a queued window whose tokens are not yet read
         self.h_ctl = torch.zeros(2, dtype=i32, pin_memory=pin)   # [window step counter, real rows]
-        self.h_perr = torch.zeros(1, dtype=i32, pin_memory=pin)  # persistent decode kernel's error word
         # numpy views over the pinned buffers (zero-copy) for cheap bulk writes
         self.n_ids, self.n_temp, self.n_topk = self.h_ids.numpy(), self.h_temp.numpy(), self.h_topk.numpy()
         self.n_topp, self.n_seed, self.n_step = self.h_topp.numpy(), self.h_seed.numpy(), self.h_step.numpy()
@@ -136,9 +134,6 @@ class ModelRunner:
             self.attn_cnt = torch.zeros(self.max_seqs * model.hkv, dtype=i32, device=dev)
             self.dec_scratch = (model.alloc_decode_scratch(self.max_seqs) if hasattr(model, "alloc_decode_scratch")
                                 else None)
-            # every decode layer in one persistent launch where the model shape has an instantiation
-            if self.dec_scratch is not None and hasattr(model, "prepare_persistent"):
-                model.prepare_persistent(pool.tensor, self.dec_scratch)
         else:
             self.part_o = self.part_ml = self.attn_cnt = self.dec_scratch = None
         self.supports_swap = type(self)._sync_step is ModelRunner._sync_step
@@ -206,16 +201,11 @@ class ModelRunner:
         return ids[:n].tolist()
 
     def _queue_fault_readback(self) -> None:
-        """Queue device-side error words behind the step (read with the tokens, same sync): the persistent
-        decode kernel's timeout word."""
-        ps = self.dec_scratch.get("persistent") if self.dec_scratch else None
-        if ps is not None:
-            self.h_perr.copy_(ps["err"], non_blocking=True)
+        """Queue device-side error words behind the step (read with the tokens, same sync). None on one GPU;
+        the TP runner reads the one-shot collectives' sticky error word."""
 
     def _raise_on_fault(self) -> None:
         """Raise if an error word read by :meth:`_queue_fault_readback` is set."""
-        if self.dec_scratch and self.dec_scratch.get("persistent") is not None and int(self.h_perr[0]):
-            raise RuntimeError("persistent decode step: a dependency wait timed out (outputs invalid)")
 
     # ------------------------------------------------------------ prefill
     KIND_STOP, KIND_PREFILL, KIND_DECODE, KIND_HEARTBEAT = 0, 1, 2, 3

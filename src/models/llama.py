@@ -21,7 +21,6 @@ The same module runs CPU tensors through :mod:`src.ops.reference` for tests.
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional
 
@@ -115,6 +114,7 @@ class CausalLM:
         self.max_position = max_position or a.max_position
         self.full_init = full_init
         self.sequence_parallel = bool(sequence_parallel and self.tp.enabled)
+        self.tiled_decode_weights = True  # decode GEMMs on tile-order copies (pack_decode_weights)
         self.layers: List[LayerWeights] = []
         self._init_random(seed, init_std)
         self.cos_sin = rope_cos_sin(self.max_position, a.head_dim, a.rope_theta, self.device, a.rope_scaling)
@@ -349,8 +349,6 @@ class CausalLM:
                 return self._forward_decode_slab(residual, positions, meta, kv_pool)
         if self.sequence_parallel and meta.is_prefill:
             return self._forward_sp(residual, positions, meta, kv_pool)
-        if meta.is_prefill and self._resid_gemm_ok(residual):
-            return self._forward_prefill_resid(residual, positions, meta, kv_pool)
         x = ops.rms_norm(residual, self.layers[0].ln1, eps)
         h = None
         last = len(self.layers) - 1
@@ -366,50 +364,6 @@ class CausalLM:
             x = ops.fused_add_rms_norm(o, residual, lw.ln2, eps)
             h = self.tp.all_reduce(self._mlp(lw, x))
         return ops.fused_add_rms_norm(h, residual, self.norm, eps)
-
-    def _resid_gemm_ok(self, residual: torch.Tensor) -> bool:
-        """Prefill on one GPU (no TP exchange between a projection and its residual add), dense FFN."""
-        return (residual.is_cuda and not self.tp.enabled and not self.arch.is_moe
-                and os.environ.get("DIE_PREFILL_RESID_GEMM", "0") != "0")
-
-    def _forward_prefill_resid(self, residual: torch.Tensor, positions: torch.Tensor, meta: AttnMetadata,
-                               kv_pool: torch.Tensor) -> torch.Tensor:
-        """Prefill with the residual adds in the GEMM epilogues: o and down accumulate straight into the
-        residual stream (``residual.addmm_``: hipBLASLt's beta = 1 epilogue reads C = residual and adds it in
-        fp32 before the one bf16 rounding), so each norm is a plain rms_norm — read the residual, write x —
-        instead of fused_add_rms_norm's read h, read residual, write residual, write x. At the bench's
-        16,384-row wave that drops two [T, H] passes (2 x 134 MB) per norm, 64 norms a wave; the projection
-        output tensors are not allocated at all. The norm weights are folded into Wqkv / Wgate_up
-        (fold_norm_weights), so only the row statistics remain to apply."""
-        eps = self.arch.rms_eps
-        last = len(self.layers) - 1
-        t = residual.shape[0]
-        # DIE_PREFILL_MLP_CHUNK=N: the FFN runs over N-row chunks, so a chunk's gate/up output and SiLU*mul
-        # output (N x 2I and N x I bf16) can stay in the Infinity Cache between the three kernels
-        chunk = int(os.environ.get("DIE_PREFILL_MLP_CHUNK", "0"))
-        bufs = None
-        if 0 < chunk < t:
-            bufs = (torch.empty(chunk, 2 * self.inter, dtype=residual.dtype, device=residual.device),
-                    torch.empty(chunk, self.inter, dtype=residual.dtype, device=residual.device))
-        for li, lw in enumerate(self.layers):
-            x = ops.rms_norm(residual, lw.ln1, eps)
-            if li == last and meta.keep_rows is not None:
-                return self._last_layer_kept_rows(lw, x, residual, positions, meta, kv_pool)
-            attn = self._attention(li, lw, x, positions, meta, kv_pool)
-            if meta.kv_hook is not None:
-                meta.kv_hook(li)
-            residual.addmm_(attn, lw.o.t())
-            x = ops.rms_norm(residual, lw.ln2, eps)
-            if bufs is None:
-                residual.addmm_(ops.silu_and_mul(F.linear(x, lw.gate_up)), lw.down.t())
-                continue
-            gu, act = bufs
-            for s in range(0, t, chunk):
-                n = min(t, s + chunk) - s
-                F.linear(x[s:s + n], lw.gate_up, out=gu[:n])
-                ops.silu_and_mul(gu[:n], out=act[:n])
-                residual[s:s + n].addmm_(act[:n], lw.down.t())
-        return ops.rms_norm(residual, self.norm, eps)
 
     def _last_layer_kept_rows(self, lw: LayerWeights, x: torch.Tensor, residual: torch.Tensor,
                               positions: torch.Tensor, meta: AttnMetadata, kv_pool: torch.Tensor) -> torch.Tensor:
@@ -577,8 +531,9 @@ class CausalLM:
         every LDS-DMA piece one linear 1-KiB read) for the fused decode path — one per (wr, kc) tile the
         row buckets' plans use; prefill keeps the row-major copies for hipBLASLt. Only done while the
         weights and their copies take <= 1/2 of the device memory (8B at batch <= 32: +13 GiB of 288 GB;
-        at batch 128: +34 GiB). DIE_GD_TILED=0 disables it."""
-        if os.environ.get("DIE_GD_TILED", "1") == "0" or self.arch.is_moe or not self.norms_folded:
+        at batch 128: +34 GiB). ``self.tiled_decode_weights = False`` keeps the decode GEMMs on the row-major
+        weights (4 % slower bench, profiles/r5_decode_weight_layout_ab.txt)."""
+        if not self.tiled_decode_weights or self.arch.is_moe or not self.norms_folded:
             return False
         if not (self.device.type == "cuda" and ops.native_available()):
             return False
@@ -636,41 +591,6 @@ class CausalLM:
               "ssp_b": torch.zeros(td, ld, dtype=f32, device=dev), "cnt_b": torch.zeros(td, dtype=i32, device=dev)}
         return sc
 
-    def persistent_config(self) -> Optional[dict]:
-        """Tiles / workspace of the persistent decode-step kernel for this model, or None (TP, MoE, unfolded
-        norms, a shape without an instantiation, or DIE_PERSISTENT=0)."""
-        if os.environ.get("DIE_PERSISTENT", "0") == "0" or self.tp.enabled or self.arch.is_moe:
-            return None
-        if not (self.device.type == "cuda" and ops.native_available() and self.norms_folded and self.head_dim == 128):
-            return None
-        return ops.decode_persistent_config(self.arch.hidden_size, self.inter, self.hq, self.hkv, len(self.layers))
-
-    def prepare_persistent(self, kv_pool: torch.Tensor, scratch: Optional[dict]) -> bool:
-        """Set up the persistent decode step for ``kv_pool`` (block size 16): tile-order weight copies for its
-        tiles (KC 128), the per-layer pointer table and the zeroed workspace, kept in ``scratch``. Call before
-        any hipGraph capture (it allocates)."""
-        cfg = self.persistent_config()
-        if cfg is None or scratch is None or kv_pool.shape[4] != 16 or self.hq // self.hkv not in (1, 2, 4, 8):
-            return False
-        tiles = {"qkv": cfg["wrq"], "o": cfg["wro"], "gate_up": cfg["wrg"], "down": cfg["wrd"]}
-        rows = []
-        for li, lw in enumerate(self.layers):
-            ptrs = []
-            for name, wr in tiles.items():
-                key = (name, wr, 128)
-                if key not in lw.tiled:
-                    lw.tiled[key] = ops.gd_pack_weights(getattr(lw, name), wr, silu=name == "gate_up", kc=128)
-                ptrs.append(lw.tiled[key].data_ptr())
-            ptrs += [kv_pool[li, 0].data_ptr(), kv_pool[li, 1].data_ptr()]
-            rows.append(ptrs)
-        table = torch.tensor(rows, dtype=torch.int64, device=self.device)
-        ws = torch.zeros(cfg["ws_bytes"], dtype=torch.uint8, device=self.device)
-        scratch["persistent"] = {"cfg": cfg, "table": table, "ws": ws, "pool_ptr": kv_pool.data_ptr(),
-                                 "err": ws[cfg["err_off"]:cfg["err_off"] + 4].view(torch.int32),
-                                 # {err, waiting workgroup, layer * 8 + phase, producers seen} after a timeout
-                                 "err_info": ws[cfg["err_off"]:cfg["err_off"] + 16].view(torch.int32)}
-        return True
-
     def _fused_decode_ok(self, kv_pool: torch.Tensor, m: int = 32) -> bool:
         g = self.hq // self.hkv
         sq = self.decode_plan(m)["qkv"][2]
@@ -701,13 +621,6 @@ class CausalLM:
             return (getattr(lw, name), False) if t is None else (t, True)
 
         ssp_prev = ssp0 if ssp0 is not None else ops.row_sumsq(h, out=sc["ssp0"])
-        ps = sc.get("persistent")
-        if ps is not None and h.shape[0] <= 32 and ps["pool_ptr"] == kv_pool.data_ptr():
-            # every layer in one persistent launch (weight / KV stream kept running across op boundaries)
-            ops.decode_persistent(ps["ws"], ps["table"], h, ssp_prev, meta.block_tables, meta.ctx_lens,
-                                  meta.slot_mapping, self.cos_sin, kv_pool, 0, len(self.layers), self.inter, hq,
-                                  hkv, self.scale, eps, ps.get("prof"))
-            return ops.rms_norm(h, self.norm, eps)
         for li, lw in enumerate(self.layers):
             k_cache, v_cache = kv_pool[li, 0], kv_pool[li, 1]
             wqkv, tq = tw(lw, "qkv", wq, kq)

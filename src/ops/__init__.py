@@ -18,17 +18,7 @@ from . import reference as ref
 _C = None
 _C_ERR: Optional[BaseException] = None
 try:
-    if os.environ.get("DIE_C_DIAG") == "1":  # the diagnostics build (DIE_KERNEL_DIAG=1 python -m src._build)
-        import importlib.util
-        import sysconfig
-
-        _p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                          "_Cdiag" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
-        _spec = importlib.util.spec_from_file_location("src._C", _p)
-        _C = importlib.util.module_from_spec(_spec)
-        _spec.loader.exec_module(_C)
-    else:
-        from src import _C  # type: ignore  # noqa: F811
+    from src import _C  # type: ignore  # noqa: F811
 except Exception as e:  # pragma: no cover - depends on build state
     _C_ERR = e
 
@@ -155,32 +145,6 @@ def attn_decode_fused(qkv_slab: torch.Tensor, ssp: torch.Tensor, positions: torc
     return out
 
 
-def decode_persistent_config(hidden: int, inter: int, hq: int, hkv: int, layers: int) -> Optional[dict]:
-    """Tiles and workspace layout of the persistent decode-step kernel (csrc/kernels/decode_persistent.hip) for
-    a model shape, or None when it has no instantiation. The kernel is compiled into the diagnostics build only
-    (``DIE_KERNEL_DIAG=1 python -m src._build``, loaded with ``DIE_C_DIAG=1``): it measured 0.70-0.77x of the
-    five-launch layer, so the release ``_C`` carries only kernels the serving path runs."""
-    if _C is None or not hasattr(_C, "decode_persistent_config"):
-        return None
-    v = list(_C.decode_persistent_config(hidden, inter, hq, hkv, layers))
-    if not v:
-        return None
-    keys = ("wrq", "skq", "wro", "sko", "wrg", "wrd", "skd", "ws_bytes", "err_off", "sync_off", "slabq_off",
-            "attn_off", "slabod_off", "act_off", "sspo_off", "sspd_off")
-    return dict(zip(keys, v))
-
-
-def decode_persistent(ws: torch.Tensor, table: torch.Tensor, h: torch.Tensor, ssp0: torch.Tensor,
-                      block_tables: torch.Tensor, ctx_lens: torch.Tensor, slot_mapping: torch.Tensor,
-                      cos_sin: torch.Tensor, pool: torch.Tensor, l0: int, l1: int, inter: int, hq: int, hkv: int,
-                      scale: float, eps: float, prof: Optional[torch.Tensor] = None) -> None:
-    """Layers [l0, l1) of a dense decode step in ONE persistent launch (h updated in place, the new tokens'
-    K / V written to the pool). ``table`` [L, 6] int64: the layers' packed weight and cache pointers.
-    ``prof`` (int64 [CUs, phases, 4]) receives timeline stamps in DIE_KERNEL_DIAG builds."""
-    _kern().decode_persistent(ws, table, h, ssp0, block_tables, ctx_lens, slot_mapping, cos_sin, pool, l0, l1,
-                              inter, hq, hkv, scale, eps, prof)
-
-
 def decode_advance(out, ids, pos, ctx, slots, bt, step, tokens, cnt, n_real, rows: int, block_size: int) -> None:
     """Device-side advance of the decode inputs (decode_step.hip); see ModelRunner.decode_multi."""
     _kern().decode_advance(out, ids, pos, ctx, slots, bt, step, tokens, cnt, n_real, rows, block_size)
@@ -239,8 +203,8 @@ def scatter_blocks(pool: torch.Tensor, ids: torch.Tensor, buf: torch.Tensor) -> 
 
 DECODE_GEMM_MAX_M = 128   # weight-streaming decode GEMM / fused decode path (gemm_decode.hip)
 # expert-streaming grouped decode GEMM up to this many tokens (<= 128 rows per expert: 16/32/64/128-row
-# images); DIE_MOE_DECODE_MAX_T=32 restores round 1's limit for A/B (above it: <= 128-row segments)
-MOE_DECODE_MAX_T = min(128, int(os.environ.get("DIE_MOE_DECODE_MAX_T", "128")))
+# images; above it: <= 128-row segments). 32 (round 1's limit) measured 14.9 vs 18.1 req/s at batch 64
+MOE_DECODE_MAX_T = 128
 SSP_LD = 128              # row stride of the norm-statistics arrays [tiles, SSP_LD]
 
 
@@ -381,9 +345,9 @@ DECODE_SILU_SPLITK_CFG = {
 
 def decode_tile_silu(n: int, k: int, bucket: int = 32):
     """(wr, kc, sk) of the norm-scaled SiLU gate/up decode GEMM: a split-K tile where one was measured faster,
-    else the full-K tile (sk = 1). DIE_GD_SILU_SPLITK=0 keeps every shape on the full-K form."""
+    else the full-K tile (sk = 1)."""
     c = DECODE_SILU_SPLITK_CFG.get((n, k, bucket))
-    if c is not None and os.environ.get("DIE_GD_SILU_SPLITK", "1") != "0":
+    if c is not None:
         return c
     return (*decode_tile(n, k, 4, bucket)[:2], 1)
 

@@ -115,17 +115,18 @@ class CustomAllReduce:
     def fused_ok(self, n_tiles: int, grid: int = 0) -> bool:
         """Whether the row-parallel decode GEMM may carry the exchange in its epilogue (gemm_decode_car). Only a
         column tile's last-arriving workgroup waits for the peers, so a launch holds at most ``n_tiles`` waiting
-        workgroups on each GPU (times the ranks sharing it, in one-GPU tests). Every other workgroup finishes
-        without waiting, so the grid always drains when the waiting ones can hold at most HALF the CUs — whatever
-        the kernel's occupancy per CU and whatever else shares the GPU for a while (the former
-        "whole grid resident at one workgroup per CU" clause assumed both). ``grid`` is kept for callers.
-        ``DIE_TP_FUSED=0`` keeps the separate all-reduce launch. The answer depends only on the group's layout
-        and the shape, so every rank agrees."""
+        workgroups on each GPU (times the ranks sharing it, in one-GPU tests). The grid always drains when
+        either (a) every workgroup of every rank sharing the GPU is resident at once — ``grid`` x ranks <= CUs,
+        at least one workgroup per CU whatever the kernel's occupancy — or (b) the waiting ones can hold at most
+        HALF the CUs, so the others always find a CU and finish. Both assume no long-running kernel of another
+        stream holds CUs meanwhile (a TP rank runs its decode on one stream). ``DIE_TP_FUSED=0`` keeps the
+        separate all-reduce launch. The answer depends only on the group's layout and the shape, so every rank
+        agrees."""
         import os
 
         if os.environ.get("DIE_TP_FUSED", "1") == "0" or not 0 < n_tiles <= SIG_BLOCKS:
             return False
-        return n_tiles * self.ranks_per_gpu * 2 <= self.cus
+        return (0 < grid and grid * self.ranks_per_gpu <= self.cus) or n_tiles * self.ranks_per_gpu * 2 <= self.cus
 
     def row_parallel_residual(self, x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, ssp: torch.Tensor,
                               counters: torch.Tensor, wr: int, kc: int, sk: int, tiled: bool) -> None:

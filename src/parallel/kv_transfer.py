@@ -149,18 +149,9 @@ class LayerGroupExporter:
             ops.gather_blocks_rows(self.pool, self.ids, self.dst, self.done, p1 - self.done)
         self.done = p1
 
-    def finish(self, interprocess: bool = False):
-        """``interprocess``: the completion event is an IPC event (its handle lets another process's stream wait
-        for the copies — the decode worker's scatter — with no host round trip in between)."""
+    def finish(self):
         self._gather_upto(self.planes)
-        ev = None
-        if interprocess:
-            try:
-                ev = torch.cuda.Event(interprocess=True)
-            except Exception:  # no IPC events on this runtime: a plain event, the sender polls it
-                ev = None
-        if ev is None:
-            ev = torch.cuda.Event()
+        ev = torch.cuda.Event()
         ev.record(self.stream)
         torch.cuda.current_stream(self.device).wait_event(ev)
         for t in (self.ids, self.dst, *(b for _, b in self.targets)):
@@ -389,12 +380,10 @@ class IPCSender:
     by its event; ``write_async`` / :meth:`wait_ready` await completion by polling (the asyncio thread
     never blocks on the GPU).
 
-    ``DIE_KV_COPY=dma`` copies with hipMemcpyAsync (copy engines; compute keeps all CUs) instead of the
-    default shader-store copy kernel (bench/micro_ipc_copy.py measures both)."""
+    ``dma = True`` copies with hipMemcpyAsync (copy engines) instead of the shader-store copy kernel: measured
+    slower, and it slows a concurrent GEMM loop more (bench/micro_ipc_copy.py, profiles/micro_ipc_copy_r2.jsonl)."""
 
     def __init__(self, handles, seg_bytes: int, device):
-        import os
-
         from src import _C
 
         if isinstance(handles, str):
@@ -408,7 +397,7 @@ class IPCSender:
                 self.ptrs.append(ptr)
                 self.views.append(_C.car_tensor(ptr, self.seg_bytes, self.device.index or 0))
             self.stream = torch.cuda.Stream(device=self.device)
-        self.dma = os.environ.get("DIE_KV_COPY", "shader") == "dma"
+        self.dma = False
         self.bytes_sent = 0
 
     def _loc(self, offset: int, nbytes: int):

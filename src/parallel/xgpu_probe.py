@@ -304,7 +304,7 @@ def xgpu_probe(rank: int, world: int, dev, rccl: bool = True, group=None) -> Dic
         out["kv_hop"] = _kv_hop(rank, world, dev, group)
     except Exception as e:  # noqa: BLE001
         out["kv_hop"] = {"error": str(e)[:200]}
-    if 2 <= world <= 8 and os.environ.get("DIE_XGPU_TP", "1") != "0":
+    if 2 <= world <= 8:
         try:
             out["tp_engine"] = _tp_engine(rank, world, dev)
         except Exception as e:  # noqa: BLE001

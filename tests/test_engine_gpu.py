@@ -169,7 +169,7 @@ def test_kv_export_import_exact(engine):
 def test_overlapped_layer_group_export_matches_post_step_gather(engine, monkeypatch):
     """Disaggregated prefill export overlapped with the forward (LayerGroupExporter: each group of 4 layers
     copied into the packets on a separate stream while the rest of the forward runs) gives the same packet
-    bytes as the gather after the step (DIE_KV_OVERLAP=0), for several prompts finishing in one ragged prefill
+    bytes as the gather after the step (EngineConfig.kv_export_overlap off), for several prompts finishing in one ragged prefill
     step, one of them a second chunk of a long prompt."""
     cfg = EngineConfig(max_num_seqs=8, max_num_batched_tokens=512, num_kv_blocks=256, max_latency_ms=0.0,
                        use_cuda_graph=False, enable_prefix_caching=False)
@@ -189,7 +189,7 @@ def test_overlapped_layer_group_export_matches_post_step_gather(engine, monkeypa
     n0 = eng.stats.get("overlapped_exports", 0)
     a = run("ov")
     assert eng.stats.get("overlapped_exports", 0) - n0 == len(prompts)
-    monkeypatch.setenv("DIE_KV_OVERLAP", "0")
+    eng.cfg.kv_export_overlap = False
     b = run("pg")
     assert eng.stats.get("overlapped_exports", 0) - n0 == len(prompts)
     for p, (ta, ka), (tb, kb) in zip(prompts, a, b):

@@ -129,22 +129,16 @@ def test_remote_link_reserve_export_never_waits_and_revoke_releases():
     asyncio.run(main())
 
 
-def test_remote_link_ipc_event_handoff_and_fallback():
-    """A direct packet's completion goes to the decode worker as an IPC event handle (no poll before the
-    kv_import); a decode worker that cannot open IPC events answers event_unsupported without claiming the
-    slot, and the sender then polls its event and re-sends the import without it — for every later packet too."""
+def test_remote_link_send_reserved_polls_then_imports():
+    """A packet gathered straight into a reserved slot: the sender polls the gather's event (never blocks the
+    event loop), then hands the slot over with ONE kv_import carrying only metadata (no event handle: the
+    IPC-event hand-off measured slower and was removed in round 5)."""
     import asyncio
 
     from src.engine.disagg import RemoteDecodeLink
     from src.parallel.kv_transfer import KVPacket
 
     class Ev:
-        def __init__(self, h):
-            self.h = h
-
-        def ipc_handle(self):
-            return self.h
-
         def query(self):
             return True
 
@@ -157,26 +151,15 @@ def test_remote_link_ipc_event_handoff_and_fallback():
                 polled.append(ev)
 
         class RPC:
-            def __init__(self, support):
-                self.support = support
-
             async def call(self, addr, msg, timeout):
                 sent.append(msg)
-                if msg["op"] == "kv_import" and "event" in msg["packet"]["ipc"] and not self.support:
-                    return {"success": False, "event_unsupported": True}
                 return {"success": True, "outputs": {}}
 
         link._ipc = IPC()
-        slot = {"offset": 0, "gen": 3}
-        pk = KVPacket("r", [1, 2], 5, torch.zeros(1, 2, 4, dtype=torch.bfloat16), 16, ready=Ev(b"h" * 64))
-        link.rpc = RPC(True)
-        rep = await link.send_reserved(pk, slot)
-        assert rep["success"] and sent[-1]["packet"]["ipc"]["event"] == b"h" * 64 and not polled
-        assert link.event_handoffs == 1 and link.direct_packets == 1
-        link.rpc = RPC(False)
-        rep = await link.send_reserved(pk, slot)
-        assert rep["success"] and "event" not in sent[-1]["packet"]["ipc"] and polled == [pk.ready]
-        assert not link.ipc_events and link.direct_packets == 2 and link.event_handoffs == 1
-        await link.send_reserved(pk, slot)          # no further attempt with an event
-        assert "event" not in sent[-1]["packet"]["ipc"] and sum("event" in m["packet"]["ipc"] for m in sent) == 2
+        link.rpc = RPC()
+        pk = KVPacket("r", [1, 2], 5, torch.zeros(1, 2, 4, dtype=torch.bfloat16), 16, ready=Ev())
+        rep = await link.send_reserved(pk, {"offset": 0, "gen": 3})
+        assert rep["success"] and polled == [pk.ready] and len(sent) == 1
+        assert sent[0]["op"] == "kv_import" and sent[0]["packet"]["ipc"] == {"offset": 0, "gen": 3}
+        assert link.direct_packets == 1 and link.kv_path == "direct"
     asyncio.run(main())

@@ -110,8 +110,7 @@ def test_gpu_disaggregated_ipc_landing_zone(monkeypatch):
     """Prefill worker (this process) -> decode worker (a separate process on the same GPU): the
     packed prompt KV goes by device-to-device copy into the decode worker's IPC landing zone (the
     xGMI path between two GPUs of a node) and only metadata crosses the socket; tokens match a
-    colocated worker. The completion hand-off runs as an IPC event here (opt-in: DIE_KV_IPC_EVENT=1)."""
-    monkeypatch.setenv("DIE_KV_IPC_EVENT", "1")
+    colocated worker."""
     import os
     import subprocess
     import sys
@@ -166,11 +165,6 @@ def test_gpu_disaggregated_ipc_landing_zone(monkeypatch):
                 (link.ipc_packets, link.direct_packets, link.wire_packets)
             assert max(collections.Counter(link.slot_offsets).values()) >= 3, link.slot_offsets
             assert link.kv_path == "direct", link.stats()
-            # completion handed over as an IPC event (the decode stream waits on the sender's copies), unless the
-            # runtime refused one — then every packet fell back to poll + RPC, still direct
-            print("kv link:", link.stats(), "ipc events:", link.ipc_events, flush=True)
-            assert link.event_handoffs in (0, 5) and (link.event_handoffs == 5) == link.ipc_events, link.stats()
-            link.ipc_events = False  # the injected failures below are in the poll path
             cd = InferenceClient(f"127.0.0.1:{dport}")
 
             async def zone():
@@ -199,8 +193,8 @@ def test_gpu_disaggregated_ipc_landing_zone(monkeypatch):
             z = await drained()
             assert z["slots_used"] == 0 and z["reserved"] == 0, z
             del link._ipc.wait_ready
-            # the staged path (DIE_KV_DIRECT=0: packed copy into the slot after kv_reserve) with a failing copy
-            os.environ["DIE_KV_DIRECT"] = "0"
+            # the staged path (kv_direct off: packed copy into the slot after kv_reserve) with a failing copy
+            pre.models["mini"].kv_direct = False
             try:
                 link._ipc.write_async = broken
                 r = await asyncio.wait_for(cp.call({"model": "mini", "inputs": req}), 60)
@@ -211,7 +205,7 @@ def test_gpu_disaggregated_ipc_landing_zone(monkeypatch):
                 r = await asyncio.wait_for(cp.call({"model": "mini", "inputs": req}), 60)
                 assert r["success"] and r["outputs"]["disaggregated"]
             finally:
-                os.environ.pop("DIE_KV_DIRECT", None)
+                pre.models["mini"].kv_direct = True
             r = await asyncio.wait_for(cp.call({"model": "mini", "inputs": req}), 60)
             assert r["success"] and r["outputs"]["disaggregated"]
             assert link.wire_packets == 0 and link.direct_packets == 6, (link.wire_packets, link.direct_packets)
