@@ -290,6 +290,8 @@ def cross_gpu_section(args, rank, world, dev, on_gpu, state) -> dict:
         parts.append("tp_wave")
     for part in parts:
         state["part"] = part
+        if args.verbose:
+            print(f"[rank {rank}] node section: {part}", file=sys.stderr, flush=True)
         t0 = time.perf_counter()
         try:
             if part == "xgpu_probe":
