@@ -1,8 +1,10 @@
 """Diagnostic: per-workgroup phase timeline of the fused decode attention (attn_decode_v3_kernel,
-FUSED prologue) at the headline shape — 32 sequences x 8 kv heads (Llama-3-8B: 32 q heads x 128),
-contexts 512..640, KV blocks allocated contiguously per sequence as the engine's block manager
-does, cold KV (a new pool slice per call). Stamps (s_memrealtime, 100 MHz): entry, first chunk
-landed, prologue done, stream done, end. Prints the median phase durations and the kernel span."""
+FUSED prologue) — by default the headline shape, 32 sequences x 8 kv heads (Llama-3-8B: 32 q heads x 128),
+contexts 512..640; ``--shape 70b_tp8`` is a Llama-3-70B TP=8 rank (1 kv head, 8 q heads), ``--ctx N`` gives
+every sequence the same context (as in a bench wave), ``--max-ctx`` the static bound that sizes the parts
+(C = chunks per task). KV blocks allocated contiguously per sequence as the engine's block manager does, cold
+KV (a new pool slice per call). Stamps (s_memrealtime, 100 MHz): entry, first chunk landed, prologue done,
+stream done, end. Prints the median phase durations, the kernel span and the event-timed us per call."""
 
 import json
 import os
@@ -17,13 +19,22 @@ from src.ops import reference as ref  # noqa: E402
 
 
 def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="8b", choices=["8b", "70b_tp8"])
+    ap.add_argument("--ctx", type=int, default=0, help="every sequence's context (0: 512 + 4 i)")
+    ap.add_argument("--max-ctx", type=int, default=2048)
+    ap.add_argument("--batch", type=int, default=32)
+    a = ap.parse_args()
     dev = torch.device("cuda:0")
-    n, hkv, g, bs, d, hid = 32, 8, 4, 16, 128, 4096
+    n, bs, d = a.batch, 16, 128
+    hkv, g, hid = (8, 4, 4096) if a.shape == "8b" else (1, 8, 8192)
     hq = hkv * g
-    ctxs = [512 + 4 * i for i in range(n)]
-    max_ctx = 2048
+    ctxs = [a.ctx] * n if a.ctx else [512 + 4 * i for i in range(n)]
+    max_ctx = a.max_ctx
     per_seq = max_ctx // bs
-    copies = 12                                    # 12 x 75 MB of KV >> the 256 MB Infinity Cache
+    copies = 12 if a.shape == "8b" else 40         # >> the 256 MB Infinity Cache
     nb = copies * n * per_seq
     kc = torch.randn(nb, hkv, bs, d, device=dev, dtype=torch.bfloat16)
     vc = torch.randn(nb, hkv, bs, d, device=dev, dtype=torch.bfloat16)
@@ -59,6 +70,15 @@ def main():
         call(c)
     k_.attn_set_timestamps(torch.empty(0, dtype=torch.int64, device=dev))
     torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    reps = 3
+    for _ in range(reps):
+        for c in range(copies):
+            call(c)
+    e1.record()
+    torch.cuda.synchronize()
+    us_call = e0.elapsed_time(e1) * 1e3 / (reps * copies)
     t = ts.view(copies, ncu, 6).cpu().double()
     res = {k: [] for k in ("span", "first_chunk", "prologue", "stream", "merge_out", "start_skew", "tail")}
     for c in range(2, copies):
@@ -75,7 +95,10 @@ def main():
         res["merge_out"].append(float((tt[:, 4] - tt[:, 3]).median()) * 10e-3)
     out = {k: round(statistics.median(v), 2) for k, v in res.items()}
     out["kv_TBps_span"] = round(kv_bytes / out["span"] / 1e6, 2)
-    print(json.dumps({"bench": "attn_decode_timeline", "batch": n, "ctx": [ctxs[0], ctxs[-1]], **out}), flush=True)
+    out["us_per_call"] = round(us_call, 2)
+    out["kv_TBps_call"] = round(kv_bytes / us_call / 1e6, 2)
+    print(json.dumps({"bench": "attn_decode_timeline", "shape": a.shape, "batch": n, "ctx": [ctxs[0], ctxs[-1]],
+                      "max_ctx": max_ctx, **out}), flush=True)
 
 
 if __name__ == "__main__":
