@@ -36,6 +36,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="70b_tp8,8b_tp2")
     ap.add_argument("--rows", type=int, default=32)
+    ap.add_argument("--proj", default="", help="comma-separated projections to sweep (default: all)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     kern = ops._kern()
@@ -45,6 +46,8 @@ def main():
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     for sname in a.shapes.split(","):
         for proj, n, k, modes in SHAPES[sname]:
+            if a.proj and proj not in a.proj.split(","):
+                continue
             silu = proj == "gate_up"
             w = (torch.randn(2 * n if silu else n, k, device=dev) * 0.02).to(torch.bfloat16)
             x = torch.randn(m, k, device=dev).to(torch.bfloat16)
@@ -57,8 +60,9 @@ def main():
                         cols = wr // 2 if silu else wr
                         if n % cols or k % (kc * sk) or not ops.gd_tile_valid(wr, kc, 32):
                             continue
-                        if mode == 3 and (wr not in (32, 64, 128) or n // wr > 128):
-                            continue  # the fused path's consumers take <= 128 statistics tiles
+                        lim = ops.SSP_MAX_TILES if m <= 32 else ops.SSP_MAX_TILES_WIDE
+                        if mode == 3 and (wr not in (32, 64, 128) or n // wr > lim):
+                            continue  # the fused path's consumers take <= 256 (<= 128 above 32 rows) tiles
                         if mode == 6 and sk == 1:
                             continue
                         ntiles = n // cols

@@ -206,8 +206,9 @@ void attn_decode_fused(Tensor out, Tensor part_o, Tensor part_ml, Tensor counter
   TORCH_CHECK(block_tables.size(1) * 16 >= max_ctx, "block table narrower than max_ctx");
   CHK_DTYPE(ssp, at::kFloat);
   CHK_CONTIG(ssp);
-  TORCH_CHECK(ssp.dim() == 2 && ssp.size(1) == die::DECODE_SSP_LD && ssp.size(0) >= 1 && ssp.size(0) <= 128,
-              "ssp [T <= 128, 128]");
+  TORCH_CHECK(ssp.dim() == 2 && ssp.size(1) == die::DECODE_SSP_LD && ssp.size(0) >= 1 &&
+                  ssp.size(0) <= die::DECODE_SSP_MAX_TILES,
+              "ssp [tiles <= 256, 128]");
   CHK_DTYPE(positions, at::kLong);
   CHK_DTYPE(slot_mapping, at::kLong);
   CHK_DTYPE(cos_sin, at::kFloat);
@@ -498,8 +499,8 @@ static void gemm_decode_impl(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t
     CHK_DTYPE(ssp_in, at::kFloat);
     CHK_CONTIG(ssp_in);
     TORCH_CHECK(ssp_in.dim() == 2 && ssp_in.size(1) == die::DECODE_SSP_LD && ssp_in.size(0) >= 1 &&
-                    ssp_in.size(0) <= 128,
-                "ssp_in [T <= 128, 128]");
+                    ssp_in.size(0) <= (M <= 32 ? die::DECODE_SSP_MAX_TILES : die::DECODE_SSP_MAX_TILES_WIDE),
+                "ssp_in [tiles <= 256 (<= 128 above 32 rows), 128]");
     fz.ssp_in = ssp_in.data_ptr<float>();
     fz.ssp_tiles = (int)ssp_in.size(0);
     fz.inv_n = 1.f / (float)K;

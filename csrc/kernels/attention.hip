@@ -461,13 +461,14 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
           const int col = j < G ? (kvh * G + j) * D : (j == G ? (hq + kvh) * D : (hq + hkv + kvh) * D);
           glds16(srow + sl * fz.slab_stride + col + (lane & 31) * 4, fa + i * 1024);
         }
-        if (wave == 0) {
+        if (wave == 0) {  // the statistics tiles (<= 256: 4 x 64 lanes; the upper two only when present)
 #pragma unroll
-          for (int i = 0; i < 2; ++i)
-            glds4(fz.ssp + min(lane + 64 * i, fz.ssp_tiles - 1) * DECODE_SSP_LD + seq, fa + fs_off + i * 256);
+          for (int i = 0; i < 4; ++i)
+            if (i < 2 || 64 * i < fz.ssp_tiles)
+              glds4(fz.ssp + min(lane + 64 * i, fz.ssp_tiles - 1) * DECODE_SSP_LD + seq, fa + fs_off + i * 256);
         }
         if (wave == 1)  // decode: the new token sits at position ctx - 1
-          glds16(fz.cos_sin + (int64_t)(ctx - 1) * D + (lane & 31) * 4, fa + fs_off + 512);
+          glds16(fz.cos_sin + (int64_t)(ctx - 1) * D + (lane & 31) * 4, fa + fs_off + 1024);
       }
     } else if (wave == 0) {  // the G query rows of this (seq, kv head), 256 B each
       const bf16_t* qb = q + (int64_t)seq * q_stride + (int64_t)kvh * G * D;
@@ -491,12 +492,12 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
       // r = rsqrt(mean(h^2) + eps) of this sequence's row
       float ssum = 0.f;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 4; ++i)
         ssum += lane + 64 * i < fz.ssp_tiles ? lds_ld32(lds_addr(fa + fs_off + 4 * (lane + 64 * i))) : 0.f;
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) ssum += __shfl_xor(ssum, o, 64);
       const float rn = rsqrtf(ssum * fz.inv_n + fz.eps);
-      const uint32_t cs = lds_addr(fa + fs_off + 512);
+      const uint32_t cs = lds_addr(fa + fs_off + 1024);
       auto slab_sum = [&](int j, int d) {
         float v = 0.f;
         for (int sl = 0; sl < fz.sk; ++sl) v += lds_ld32(lds_addr(fa + ((sl * (G + 2) + j) * D + d) * 4));
@@ -777,8 +778,8 @@ hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* c
   const bool v3_ok = counters != nullptr && block_size == 16 && (G == 1 || G == 2 || G == 4 || G == 8) &&
                      part_bytes < ((int64_t)1 << 31);
   if (fz != nullptr) {  // fused prologue: only the v3 kernel has it
-    if (!v3_ok || fz->sk < 1 || fz->ssp_tiles < 1 || fz->ssp_tiles > 128 ||
-        ((fz->sk * (G + 2) + 1) / 2) * 1024 + 1536 > V3_MERGE)
+    if (!v3_ok || fz->sk < 1 || fz->ssp_tiles < 1 || fz->ssp_tiles > DECODE_SSP_MAX_TILES ||
+        ((fz->sk * (G + 2) + 1) / 2) * 1024 + 2048 > V3_MERGE)
       return hipErrorInvalidValue;
   }
   if (v3_ok) {

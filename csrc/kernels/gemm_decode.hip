@@ -249,7 +249,8 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
   // tid / RR + NSL * i), loaded before any LDS-DMA and first used in the epilogue, so no wait lands
   // inside the weight stream. Index clamped, masked later (no branches).
   constexpr int NSL = NTH / RR;                // tile slices
-  constexpr int NPF = (128 + NSL - 1) / NSL;   // prefetched statistics per thread (<= 128 tiles)
+  constexpr int MAXT = RR <= 32 ? DECODE_SSP_MAX_TILES : DECODE_SSP_MAX_TILES_WIDE;
+  constexpr int NPF = (MAXT + NSL - 1) / NSL;  // prefetched statistics per thread (<= MAXT tiles)
   float ssv[EPI == 4 || EPI == 6 ? NPF : 1];
   if constexpr (EPI == 4 || EPI == 6) {
 #pragma unroll
@@ -661,7 +662,9 @@ hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx
                               hipStream_t s) {
   if (M <= 0) return hipSuccess;
   if (M > 128 || sk < 1 || (mode != 2 && mode != 3 && mode != 6 && sk != 1)) return hipErrorInvalidValue;
-  if ((mode == 4 || mode == 6) && (fz.ssp_in == nullptr || fz.ssp_tiles < 1 || fz.ssp_tiles > 128))
+  if ((mode == 4 || mode == 6) &&
+      (fz.ssp_in == nullptr || fz.ssp_tiles < 1 ||
+       fz.ssp_tiles > (M <= 32 ? DECODE_SSP_MAX_TILES : DECODE_SSP_MAX_TILES_WIDE)))
     return hipErrorInvalidValue;
   if (mode == 6 && sk > 1 && (fz.slab6 == nullptr || fz.counters == nullptr)) return hipErrorInvalidValue;
   if (mode == 3 && (fz.resid == nullptr || fz.ssp_out == nullptr || (sk > 1 && fz.counters == nullptr)))

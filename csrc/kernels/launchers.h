@@ -90,6 +90,10 @@ int car_mode();                       // synchronisation variant of the one-shot
 // Fusion operands of the decode GEMM (modes 3 and 4, see gemm_decode.hip). Norm statistics arrays have a
 // row stride of DECODE_SSP_LD = 128 (the largest decode batch).
 constexpr int DECODE_SSP_LD = 128;
+// norm-statistics tiles a consumer accepts: 256 at <= 32 decode rows (one tile per 32 output columns of an
+// 8,192-wide residual, e.g. Llama-3-70B's TP shard projections at wr = 32), 128 above
+constexpr int DECODE_SSP_MAX_TILES = 256;
+constexpr int DECODE_SSP_MAX_TILES_WIDE = 128;
 struct GemmDecodeFuse {
   bf16_t* resid = nullptr;       // mode 3: residual stream [M][ld_resid], updated in place
   int64_t ld_resid = 0;

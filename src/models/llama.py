@@ -494,7 +494,7 @@ class CausalLM:
         norm-statistics tile per wr output columns), (wr, kc) of the gate/up projection."""
         h, d = self.arch.hidden_size, self.head_dim
         b = self.decode_bucket(m)
-        # the fused attention stages sk x (G + 2) slab rows of 512 B (+ 1.5 KiB) in its 27 KiB merge
+        # the fused attention stages sk x (G + 2) slab rows of 512 B (+ 2 KiB) in its 27 KiB merge
         # area (V3_MERGE_BYTES): at most 50 rows
         g = max(1, self.hq // self.hkv)
         qkv = ops.decode_tile(self.layers[0].qkv.shape[0], h, 2, b, max_sk=max(1, 50 // (g + 2)))
@@ -576,8 +576,12 @@ class CausalLM:
         else:
             to = max(h // p["o"][0] for p in plans.values())
             td = 1 if self.arch.is_moe else max(h // p["down"][0] for p in plans.values())
-        if max(to, td) > 128:
-            return None
+        # consumers take <= 256 statistics tiles at <= 32 rows, <= 128 above (gemm_decode.hip / attention.hip)
+        for b, p in plans.items():
+            lim = ops.SSP_MAX_TILES if b <= 32 else ops.SSP_MAX_TILES_WIDE
+            if not (self.tp.enabled and not p["tp_fused"]) and max(h // p["o"][0],
+                                                                   0 if self.arch.is_moe else h // p["down"][0]) > lim:
+                return None
         dev = self.device
         self.pack_decode_weights(buckets)
         ld = ops.SSP_LD
@@ -595,7 +599,7 @@ class CausalLM:
         g = self.hq // self.hkv
         sq = self.decode_plan(m)["qkv"][2]
         return (self.norms_folded and self.head_dim == 128 and kv_pool.shape[4] == 16 and g in (1, 2, 4, 8)
-                and ((sq * (g + 2) + 1) // 2) * 1024 + 1536 <= V3_MERGE_BYTES)
+                and ((sq * (g + 2) + 1) // 2) * 1024 + 2048 <= V3_MERGE_BYTES)
 
     def _forward_decode_fused(self, h: torch.Tensor, positions: torch.Tensor, meta: AttnMetadata,
                               kv_pool: torch.Tensor, ssp0: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -206,6 +206,8 @@ DECODE_GEMM_MAX_M = 128   # weight-streaming decode GEMM / fused decode path (ge
 # images; above it: <= 128-row segments). 32 (round 1's limit) measured 14.9 vs 18.1 req/s at batch 64
 MOE_DECODE_MAX_T = 128
 SSP_LD = 128              # row stride of the norm-statistics arrays [tiles, SSP_LD]
+SSP_MAX_TILES = 256       # statistics tiles a consumer takes at <= 32 decode rows (launchers.h)
+SSP_MAX_TILES_WIDE = 128  # ... above 32 rows
 
 
 def _decode_gemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -464,11 +466,12 @@ DECODE_TILE_CFG = {
     (4096, 4096, 3, 32): (32, 256, 2),     # o      13.96 vs 15.44 for (64, 256, 4)
     (14336, 4096, 4, 32): (128, 128, 1),   # gate/up + SiLU 42.08 vs 43.96 for (112, 128, 1)
     (4096, 14336, 3, 32): (64, 128, 4),    # down   29.6 vs 30.2 for (64, 256, 4)
-    # tensor-parallel shards, 32 rows (bench/micro_tp_tiles.py, profiles/micro_tp_tiles_r4.jsonl, cold, us):
-    # (mode 3 needs N / wr <= 128 statistics tiles: the 70B shard's wr = 32 winners, 9.96 / 17.12 us, would
-    # disable the fused decode path, so the best wr >= 64 tiles)
-    (8192, 1024, 3, 32): (64, 256, 1),     # 70B TP=8 o     11.28 vs 12.12 for (64, 256, 2)
-    (8192, 3584, 3, 32): (64, 128, 2),     # 70B TP=8 down  17.96 vs 18.48 for (64, 256, 2)
+    # tensor-parallel shards, 32 rows (bench/micro_tp_tiles.py, profiles/micro_tp_tiles_r4.jsonl, cold, us)
+    # round 5: consumers take 256 statistics tiles at <= 32 rows, so the 70B shard's wr = 32 tiles (one workgroup
+    # per CU, no split-K) are usable (bench/micro_tp_tiles.py --proj o,down, profiles/r5_tp8_tiles_wr32.jsonl):
+    # o 10.00 vs 11.28 us for (64, 256, 1), down 17.20 vs 17.96 for (64, 128, 2); probe 5.74 -> 5.58 ms/step
+    (8192, 1024, 3, 32): (32, 128, 1),     # 70B TP=8 o
+    (8192, 3584, 3, 32): (32, 256, 1),     # 70B TP=8 down
     (4096, 2048, 3, 32): (32, 128, 2),     # 8B TP=2 o      11.48 vs 12.68
     (4096, 7168, 3, 32): (64, 128, 4),     # 8B TP=2 down   18.40 vs 18.88
     (3072, 4096, 2, 32): (48, 128, 4),     # 8B TP=2 qkv    11.08 vs 11.80
@@ -500,7 +503,8 @@ def decode_tile(n: int, k: int, mode: int, bucket: int = 32, max_sk: int = 8):
 
     c = DECODE_TILE_CFG.get((n, k, mode, bucket))
     # mode 3 writes one statistics tile per wr columns; its consumers take at most 128 of them
-    if c is not None and c[2] <= max_sk and (mode != 3 or n // c[0] <= 128):
+    if c is not None and c[2] <= max_sk and (mode != 3 or n // c[0] <= (SSP_MAX_TILES if bucket <= 32
+                                                                         else SSP_MAX_TILES_WIDE)):
         return c
     if bucket <= 32:
         if mode == 3:

@@ -487,14 +487,17 @@ def test_gemm_decode_residual_mode(dev, wr, sk, k, m, kc):
         assert int(cnt.abs().sum()) == 0
 
 
-@pytest.mark.parametrize("m,inter,k,wr", [(32, 14336, 4096, 112), (7, 2048, 1024, 64), (100, 14336, 4096, 112),
-                                         (64, 2048, 1024, 64)])
-def test_gemm_decode_rownorm_silu(dev, m, inter, k, wr):
-    """mode 4: RMSNorm (weight folded into W) as a per-row scale + gate/up + SiLU*mul."""
+@pytest.mark.parametrize("m,inter,k,wr,t", [(32, 14336, 4096, 112, 64), (7, 2048, 1024, 64, 64),
+                                           (100, 14336, 4096, 112, 64), (64, 2048, 1024, 64, 64),
+                                           (32, 3584, 8192, 64, 256), (19, 3584, 8192, 64, 200)])
+def test_gemm_decode_rownorm_silu(dev, m, inter, k, wr, t):
+    """mode 4: RMSNorm (weight folded into W) as a per-row scale + gate/up + SiLU*mul; the statistics arrive as
+    t per-tile partial sums (up to 256 tiles at <= 32 rows: a residual written by wr = 32 tiles of 8,192)."""
     x = torch.randn(m, k, device=dev, dtype=torch.bfloat16) * 3
     w = torch.randn(2 * inter, k, device=dev, dtype=torch.bfloat16) / math.sqrt(k)
     ss = x.float().pow(2)
-    t = 64 if k % 64 == 0 else 1
+    if k % t:
+        t = 1
     ssp = torch.zeros(t, ops.SSP_LD, device=dev)
     ssp[:, :m] = ss.view(m, t, -1).sum(-1).t()
     y = ops.linear_silu_mul_rownorm(x, w, ssp, 1e-5, wr)
@@ -528,10 +531,11 @@ def test_gemm_decode_tiled_weights(dev, mode, n, k, wr, sk):
         close(a, x.float() @ w.float().t(), atol=2e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("g,hkv,big", [(4, 8, False), (8, 1, False), (1, 4, False), (4, 8, True)])
-def test_attn_decode_fused(dev, g, hkv, big):
+@pytest.mark.parametrize("g,hkv,big,tiles", [(4, 8, False, 4), (8, 1, False, 4), (1, 4, False, 4), (4, 8, True, 4),
+                                             (8, 1, False, 256), (4, 8, True, 130)])
+def test_attn_decode_fused(dev, g, hkv, big, tiles):
     """Fused prologue: norm scale + qkv slab sum + RoPE at ctx-1 + KV write, then attention.
-    big: 32 sequences x 8 kv heads."""
+    big: 32 sequences x 8 kv heads. tiles: norm-statistics tiles (up to 256)."""
     hq, sk, bs, d = hkv * g, 2, 16, 128
     hid = 1024
     ctxs = [1, 17, 200, 777, 2049]
@@ -545,8 +549,8 @@ def test_attn_decode_fused(dev, g, hkv, big):
     bt_wide[:, : bt.shape[1]] = bt
     slab = torch.randn(sk, n, width, device=dev) * 0.7   # normalised q/k/v ~ N(0, 1): realistic scores
     ssv = (torch.rand(n, device=dev) + 0.5) * hid
-    ssp = torch.zeros(4, ops.SSP_LD, device=dev)
-    ssp[:, :n] = (ssv / 4)[None, :]                     # 4 tiles summing to ssv
+    ssp = torch.zeros(tiles, ops.SSP_LD, device=dev)
+    ssp[:, :n] = (ssv / tiles)[None, :]                 # `tiles` tiles summing to ssv
     slots = torch.tensor([int(bt[i, (c - 1) // bs]) * bs + (c - 1) % bs for i, c in enumerate(ctxs)],
                          dtype=torch.long, device=dev)
     slots[1] = -1                                        # a padded row: no cache write
