@@ -327,7 +327,7 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
   __syncthreads();
   char* escr = smem + NRED * RR * WR * 4;  // epilogue scratch after the partials
   if constexpr (EPI == 3) {
-    // split-K partial -> last arriver: h += sum of partials (bf16), per-tile row sums of squares.
+    // split-K partial -> last arriver: h += sum of partials in slice order (bf16), per-tile row sums of squares.
     // Every thread owns EPT float4 groups (row m, columns j..j+3); its own workgroup's partial stays in
     // registers, so the last arriver reads only the OTHER ny-1 slabs, all of them issued back to back
     // (SKC = compile-time ny: no per-slab round trip) together with the residual rows.
@@ -385,19 +385,33 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
                                                       ry, (int)((((int64_t)k * M + m) * ldy + n0 + j) * 4), 0, 16));
             }
           }
+          // summed in slice order whichever slice arrived last: the result is run-to-run deterministic
 #pragma unroll
-          for (int ii = 0; ii < IG; ++ii)
+          for (int ii = 0; ii < IG; ++ii) {
+            f4 sum = own[i0 + ii];
 #pragma unroll
-            for (int kk = 0; kk < SKC - 1; ++kk) own[i0 + ii] += pv[ii][kk];
+            for (int k = 0; k < SKC; ++k) {
+              f4 v;
+              if (k == 0) v = by == 0 ? own[i0 + ii] : pv[ii][0];
+              else if (k == SKC - 1) v = by == SKC - 1 ? own[i0 + ii] : pv[ii][SKC - 2];
+              else v = k < by ? pv[ii][k] : (k == by ? own[i0 + ii] : pv[ii][k - 1]);
+              sum = k == 0 ? v : sum + v;
+            }
+            own[i0 + ii] = sum;
+          }
         }
       } else {
 #pragma unroll
         for (int i = 0; i < EPT; ++i) {
           const int e = tid + i * NTH, m = min(e / Q, M - 1), j = 4 * (e % Q);
-          for (int k = 0; k < ny; ++k)
-            if (k != by)
-              own[i] += __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                   ry, (int)((((int64_t)k * M + m) * ldy + n0 + j) * 4), 0, 16));
+          f4 sum = own[i];
+          for (int k = 0; k < ny; ++k) {
+            const f4 v = k == by ? own[i]
+                                 : __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                              ry, (int)((((int64_t)k * M + m) * ldy + n0 + j) * 4), 0, 16));
+            sum = k == 0 ? v : sum + v;
+          }
+          own[i] = sum;
         }
       }
     }

@@ -487,6 +487,26 @@ def test_gemm_decode_residual_mode(dev, wr, sk, k, m, kc):
         assert int(cnt.abs().sum()) == 0
 
 
+@pytest.mark.parametrize("sk", [4, 3])
+def test_gemm_decode_residual_mode_is_deterministic(dev, sk):
+    """The split-K last arriver sums the slices in slice order whichever slice arrived last: repeated launches
+    from the same residual are bit-identical (compile-time and runtime split counts). (Summed in arrival order
+    they differed in the last bit of a few elements per launch: profiles/r5_down_qkv_pair_negative.jsonl.)"""
+    m, h, k = 19, 4096, 3072 * 4 if sk == 4 else 3072
+    x = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(h, k, device=dev, dtype=torch.bfloat16) / math.sqrt(k)
+    res0 = torch.randn(m, h, device=dev, dtype=torch.bfloat16)
+    ssp = torch.zeros(h // 64, ops.SSP_LD, device=dev)
+    cnt = torch.zeros(h // 64, dtype=torch.int32, device=dev)
+    outs = []
+    for _ in range(8):
+        r = res0.clone()
+        ops.linear_slab_residual(x, w, r, ssp, cnt, 64, sk)
+        outs.append((r, ssp.clone()))
+    for r, s in outs[1:]:
+        assert torch.equal(r, outs[0][0]) and torch.equal(s, outs[0][1])
+
+
 @pytest.mark.parametrize("m,inter,k,wr,t", [(32, 14336, 4096, 112, 64), (7, 2048, 1024, 64, 64),
                                            (100, 14336, 4096, 112, 64), (64, 2048, 1024, 64, 64),
                                            (32, 3584, 8192, 64, 256), (19, 3584, 8192, 64, 200)])
