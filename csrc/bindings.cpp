@@ -64,7 +64,17 @@ void fused_add_rms_norm(Tensor out, Tensor x, Tensor residual, Tensor w, double 
                                          (int)x.size(1), x.stride(0), out.stride(0), cur_stream()));
 }
 
-void silu_and_mul(Tensor out, Tensor x) {
+// row_scale (optional, numel 0 = absent): fp32 [T] RMSNorm row scale applied to gate and up (prefill with the
+// norm weight folded into Wgate_up)
+static const float* opt_row_scale(const Tensor& rs, int64_t rows, const Tensor& like, const char* name) {
+  if (rs.numel() == 0) return nullptr;
+  CHK_DTYPE(rs, at::kFloat);
+  CHK_CONTIG(rs);
+  TORCH_CHECK(rs.device() == like.device() && rs.numel() >= rows, name, ": row scale [T] fp32 on the same device");
+  return rs.data_ptr<float>();
+}
+
+void silu_and_mul(Tensor out, Tensor x, Tensor row_scale) {
   CHK_CUDA(x);
   CHK_BF16(x);
   CHK_BF16(out);
@@ -73,7 +83,28 @@ void silu_and_mul(Tensor out, Tensor x) {
   TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.size(1) == 2 * out.size(1) && x.size(0) == out.size(0),
               "silu_and_mul: x [T, 2I], out [T, I]");
   TORCH_CHECK(out.size(1) % 8 == 0, "intermediate size must be a multiple of 8");
-  HIP_OK(die::launch_silu_and_mul(bf(out), bf(x), (int)x.size(0), (int)out.size(1), cur_stream()));
+  HIP_OK(die::launch_silu_and_mul(bf(out), bf(x), (int)x.size(0), (int)out.size(1), cur_stream(),
+                                  opt_row_scale(row_scale, x.size(0), x, "silu_and_mul")));
+}
+
+// Prefill RMSNorm as a row scale: resid += x (x empty: no add) and rs [T] = rsqrt(mean(resid^2) + eps).
+void rms_row_scale(Tensor rs, Tensor resid, Tensor x, double eps) {
+  CHK_CUDA(resid);
+  CHK_BF16(resid);
+  check_rows(resid, "resid");
+  CHK_DTYPE(rs, at::kFloat);
+  CHK_CONTIG(rs);
+  TORCH_CHECK(rs.device() == resid.device() && rs.numel() >= resid.size(0), "rs [T] fp32");
+  const bool add = x.numel() > 0;
+  if (add) {
+    CHK_BF16(x);
+    check_rows(x, "x");
+    TORCH_CHECK(x.sizes() == resid.sizes() && x.device() == resid.device(), "x like resid");
+  }
+  TORCH_CHECK(resid.size(1) <= 8192, "hidden <= 8192");
+  HIP_OK(die::launch_rms_row_scale(rs.data_ptr<float>(), bf(resid), add ? bf(x) : nullptr, (int)resid.size(0),
+                                   (int)resid.size(1), resid.stride(0), add ? x.stride(0) : 0, (float)eps,
+                                   cur_stream()));
 }
 
 void check_cache(const Tensor& c, int64_t hkv, int64_t head_dim, const char* name) {
@@ -85,7 +116,7 @@ void check_cache(const Tensor& c, int64_t hkv, int64_t head_dim, const char* nam
 }
 
 void rope_and_cache(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor slot_mapping, Tensor k_cache,
-                    Tensor v_cache, int64_t hq, int64_t hkv, int64_t head_dim, bool rot_q) {
+                    Tensor v_cache, int64_t hq, int64_t hkv, int64_t head_dim, bool rot_q, Tensor row_scale) {
   CHK_CUDA(qkv);
   CHK_BF16(qkv);
   check_rows(qkv, "qkv");
@@ -101,11 +132,13 @@ void rope_and_cache(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor slot_ma
   TORCH_CHECK(k_cache.sizes() == v_cache.sizes(), "k/v cache shapes differ");
   HIP_OK(die::launch_rope_and_cache(bf(qkv), qkv.stride(0), positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
                                      slot_mapping.data_ptr<int64_t>(), bf(k_cache), bf(v_cache), (int)qkv.size(0),
-                                     (int)hq, (int)hkv, (int)head_dim, (int)k_cache.size(2), cur_stream(), rot_q));
+                                     (int)hq, (int)hkv, (int)head_dim, (int)k_cache.size(2), cur_stream(), rot_q,
+                                     opt_row_scale(row_scale, qkv.size(0), qkv, "rope_and_cache")));
 }
 
 void attn_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor cu_q,
-                  Tensor ctx_lens, int64_t max_q_len, int64_t hq, int64_t hkv, double scale, Tensor cos_sin) {
+                  Tensor ctx_lens, int64_t max_q_len, int64_t hq, int64_t hkv, double scale, Tensor cos_sin,
+                  Tensor q_scale) {
   CHK_CUDA(q);
   CHK_BF16(q);
   CHK_BF16(out);
@@ -136,7 +169,8 @@ void attn_prefill(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor b
                                    block_tables.data_ptr<int>(), (int)block_tables.size(1), cu_q.data_ptr<int>(),
                                    ctx_lens.data_ptr<int>(), (int)nseq, (int)max_q_len, (int)hq, (int)hkv, (int)D,
                                    (int)k_cache.size(2), (float)scale, cur_stream(),
-                                   rot ? cos_sin.data_ptr<float>() : nullptr, rot ? (int)cos_sin.size(0) : 0));
+                                   rot ? cos_sin.data_ptr<float>() : nullptr, rot ? (int)cos_sin.size(0) : 0,
+                                   opt_row_scale(q_scale, q.size(0), q, "attn_prefill")));
 }
 
 // counters: int32 [>= num_seqs * hkv], zero before first use (the kernel re-arms them); an empty tensor
@@ -864,6 +898,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_combine", &moe_combine);
   m.def("gemm_decode", &gemm_decode);
   m.def("gemm_decode_car", &gemm_decode_car);
+  m.def("rms_row_scale", &rms_row_scale);
   m.def("gd_set_timestamps", &gd_set_timestamps);
   m.def("attn_set_timestamps", &attn_set_timestamps);
   m.def("row_sumsq", &row_sumsq);

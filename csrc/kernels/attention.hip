@@ -28,6 +28,7 @@
 //    a wave-private LDS tile), writes an unnormalised partial; a second kernel
 //    merges partials (flash-decoding). Grid sized by the max context so the
 //    launch is hipGraph-capturable; surplus workgroups exit immediately.
+#include <algorithm>
 #include <cstdlib>
 
 #include "attn_common.h"
@@ -53,7 +54,8 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
                                                            const int* __restrict__ cu_q,
                                                            const int* __restrict__ ctx_lens, int hq, int hkv,
                                                            int block_size, float scale_log2,
-                                                           const float* __restrict__ cos_sin, int n_pos) {
+                                                           const float* __restrict__ cos_sin, int n_pos,
+                                                           const float* __restrict__ q_scale) {
   constexpr int TPW = 32 / G;   // tokens per wave
   constexpr int TPB = NW * TPW;  // tokens per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -93,6 +95,9 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
     // RoPE (neox pairs (i, i + 64)) on the Q row as it is loaded: qf[kk] holds dims 16 kk + 8 h + [0, 8)
     // and qf[kk + 4] their partners, so the rotation is lane-local (the rope kernel skips q)
     const float* cs = cos_sin + (int64_t)min(pos0 + tok, n_pos - 1) * D;
+    // q_scale: the token's RMSNorm row scale (the norm weight is folded into Wqkv and the projection ran
+    // on the raw residual), applied with the rotation (both are linear)
+    const float qs = q_scale != nullptr ? q_scale[qbeg + tok] : 1.f;
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       float a[8], b[8], ya[8], yb[8];
@@ -101,7 +106,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) attn_prefill_kernel(bf16_t* _
       const int i0 = 16 * kk + 8 * h;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float co = cs[i0 + j], si = cs[D / 2 + i0 + j];
+        const float co = cs[i0 + j] * qs, si = cs[D / 2 + i0 + j] * qs;
         ya[j] = a[j] * co - b[j] * si;
         yb[j] = b[j] * co + a[j] * si;
       }
@@ -388,7 +393,7 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters,
     const bf16_t* __restrict__ q, int64_t q_stride, bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, int num_seqs, int hq,
-    int hkv, float scale_log2, int maxp, AttnDecodeFuse fz, const int64_t* __restrict__ slot_mapping) {
+    int hkv, float scale_log2, int maxp, int cpp, AttnDecodeFuse fz, const int64_t* __restrict__ slot_mapping) {
   constexpr int QI = (G * 256 + 1023) / 1024;  // LDS-DMA instructions for the query rows
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* ml = reinterpret_cast<float*>(smem + 2 * V3_BUF);
@@ -396,7 +401,7 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
   int* ctl = reinterpret_cast<int*>(smem + 2 * V3_BUF + V3_MERGE);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, row = lane & 31;
   const int pairs = num_seqs * hkv;
-  const int C = max(1, min(maxp, (maxp * pairs + (int)gridDim.x - 1) / (int)gridDim.x));
+  const int C = cpp;  // chunks per part (host: launch_attn_decode)
   const int np = (maxp + C - 1) / C;
   const int n_tasks = pairs * np;
   const int pch = lane & 15;
@@ -405,11 +410,22 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
   long long tsv[5] = {0, 0, 0, 0, 0};
   if (fz.ts != nullptr) tsv[0] = __builtin_amdgcn_s_memrealtime();
 
+  int ctx_pf = -1;  // the context length of task t, loaded during the previous task (-1: not loaded)
 #pragma unroll 1
   for (int t = blockIdx.x; t < n_tasks; t += gridDim.x) {
     const int pair = t % pairs, part = t / pairs;
     const int seq = pair / hkv, kvh = pair - seq * hkv;
     const int c0 = part * C;
+    // the next task's context length, in flight with this task's scalar loads: a next task past its
+    // sequence's context is then skipped at this one's end without another round trip (single-chunk parts
+    // give a workgroup two or more tasks, most of them past a short context)
+    const int tn = t + (int)gridDim.x;
+    const int ctx_next = tn < n_tasks ? ctx_lens[__builtin_amdgcn_readfirstlane((tn % pairs) / hkv)] : 0;
+    if (ctx_pf >= 0 && c0 >= (ctx_pf + DEC_KEYS - 1) / DEC_KEYS) {  // uniform
+      ctx_pf = ctx_next;
+      continue;
+    }
+    ctx_pf = ctx_next;
     const int* bt = block_tables + (int64_t)seq * bt_stride;
     // the first chunk's two block ids of this wave, read speculatively (clamped to the table row) BEFORE the
     // context length: the two scalar loads are in flight together, so the first chunk's DMA waits for one
@@ -447,7 +463,9 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
 
     const bool has_new = FUSED && c1 == nch;  // this part holds the step's new token (key ctx-1)
     char* fa = smem + 2 * V3_BUF;            // FUSED staging (merge area, idle at a task start)
-    const int frows = fz.sk * (G + 2);       // slab rows: [s][q heads..., k, v] x 128 fp32
+    // slab rows x 128 fp32: [s][q heads] then [s][k, v]; a part without the new token stages only the q rows
+    const int frows = fz.sk * (G + 2);
+    const int qrows = fz.sk * G;
     const int fs_off = ((frows + 1) / 2) * 1024;
     // Issue order: the prologue's small operands first, then chunk c0, so the prologue (FUSED: slab
     // sum, norm scale, RoPE, KV write) runs while the chunk streams in; only a counted vmcnt separates
@@ -455,9 +473,17 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
     if constexpr (FUSED) {
       {
         const float* srow = fz.slab + (int64_t)seq * fz.width;
-        for (int i = wave; i < (frows + 1) / 2; i += 4) {
-          const int ri = min(2 * i + (lane >> 5), frows - 1);
-          const int sl = ri / (G + 2), j = ri - sl * (G + 2);
+        const int nrows = has_new ? frows : qrows;
+        for (int i = wave; i < (nrows + 1) / 2; i += 4) {
+          const int ri = min(2 * i + (lane >> 5), nrows - 1);
+          int sl, j;
+          if (ri < qrows) {
+            sl = ri / G;
+            j = ri - sl * G;
+          } else {
+            sl = (ri - qrows) >> 1;
+            j = G + ((ri - qrows) & 1);
+          }
           const int col = j < G ? (kvh * G + j) * D : (j == G ? (hq + kvh) * D : (hq + hkv + kvh) * D);
           glds16(srow + sl * fz.slab_stride + col + (lane & 31) * 4, fa + i * 1024);
         }
@@ -498,9 +524,10 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
       for (int o = 32; o > 0; o >>= 1) ssum += __shfl_xor(ssum, o, 64);
       const float rn = rsqrtf(ssum * fz.inv_n + fz.eps);
       const uint32_t cs = lds_addr(fa + fs_off + 1024);
-      auto slab_sum = [&](int j, int d) {
+      auto slab_sum = [&](int j, int d) {  // staged row of split sl: q head j at sl * G + j, k / v at qrows + 2 sl
         float v = 0.f;
-        for (int sl = 0; sl < fz.sk; ++sl) v += lds_ld32(lds_addr(fa + ((sl * (G + 2) + j) * D + d) * 4));
+        for (int sl = 0; sl < fz.sk; ++sl)
+          v += lds_ld32(lds_addr(fa + (((j < G ? sl * G : qrows + 2 * sl - G) + j) * D + d) * 4));
         return v * rn;
       };
       for (int it = tid; it < G * 64; it += 256) {  // rotated query rows -> q image (bf16)
@@ -511,7 +538,8 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
         lds_st16(qa + 2 * p, f2bf(a * co - bq * si));
         lds_st16(qa + 2 * (p + 64), f2bf(bq * co + a * si));
       }
-      if (tid < 64) {  // new key, rotated
+      if (!has_new) {
+      } else if (tid < 64) {  // new key, rotated
         const float a = slab_sum(G, tid), bq = slab_sum(G, tid + 64);
         const float co = lds_ld32(cs + 4 * tid), si = lds_ld32(cs + 4 * (tid + 64));
         nk0 = f2bf(a * co - bq * si);
@@ -734,9 +762,11 @@ __global__ void __launch_bounds__(128) attn_decode_reduce_kernel(bf16_t* __restr
 hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, const bf16_t* k_cache,
                                const bf16_t* v_cache, const int* block_tables, int bt_stride, const int* cu_q,
                                const int* ctx_lens, int num_seqs, int max_q_len, int hq, int hkv, int head_dim,
-                               int block_size, float scale, hipStream_t s, const float* cos_sin, int n_pos) {
+                               int block_size, float scale, hipStream_t s, const float* cos_sin, int n_pos,
+                               const float* q_scale) {
   if (num_seqs == 0 || max_q_len == 0) return hipSuccess;
   if (cos_sin != nullptr && n_pos < 1) return hipErrorInvalidValue;
+  if (q_scale != nullptr && cos_sin == nullptr) return hipErrorInvalidValue;  // applied with the rotation
   if (head_dim != D || hq % hkv || block_size % 16) return hipErrorInvalidValue;
   const int G = hq / hkv;
   const float sl2 = scale * 1.4426950408889634f;
@@ -747,7 +777,8 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
 #define PF_CASE(GG)                                                                                            \
   case GG:                                                                                                     \
     hipLaunchKernelGGL((attn_prefill_kernel<GG, 2, NW>), grid, block, lds, s, out, q, q_stride, k_cache,       \
-                       v_cache, block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2, cos_sin, n_pos); \
+                       v_cache, block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2, cos_sin, n_pos, \
+                       q_scale);                                                                               \
     break;
   switch (G) {
     PF_CASE(1)
@@ -784,9 +815,16 @@ hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* c
   }
   if (v3_ok) {
     const float sl2 = scale * 1.4426950408889634f;
-    const int tasks = num_seqs * hkv * maxp3;
+    const int pairs = num_seqs * hkv;
+    const int tasks = pairs * maxp3;
     const int ncu = num_cus();
     dim3 grid(tasks < ncu ? tasks : ncu), block(256);
+    // chunks per part: pairs x parts ~ the grid; with few (sequence, kv head) pairs (tensor-parallel shards:
+    // Llama-3-70B TP=8 has 32 at batch 32) every part is ONE chunk and a workgroup takes up to two tasks, so a
+    // short context spreads over several CUs instead of streaming several chunks through one CU's miss slots
+    int cpp = std::max(1, std::min(maxp3, (maxp3 * pairs + (int)grid.x - 1) / (int)grid.x));
+    static const bool ab_old = getenv("DIE_AB_ATTN_OLD") != nullptr;  // TEMP A/B
+    if (tasks <= 2 * (int)grid.x && !ab_old) cpp = 1;
     AttnDecodeFuse none{};
     none.ts = g_attn_ts;
     AttnDecodeFuse fzc{};
@@ -800,11 +838,11 @@ hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* c
     if (fz)                                                                                                     \
       hipLaunchKernelGGL((attn_decode_v3_kernel<GG, true>), grid, block, V3_LDS, s, out, part_o, part_ml,       \
                          counters, q, q_stride, k_cache, v_cache, block_tables, bt_stride, ctx_lens, num_seqs, hq, \
-                         hkv, sl2, maxp3, *fz, fz->slot_mapping);                                          \
+                         hkv, sl2, maxp3, cpp, *fz, fz->slot_mapping);                                     \
     else                                                                                                        \
       hipLaunchKernelGGL((attn_decode_v3_kernel<GG, false>), grid, block, V3_LDS, s, out, part_o, part_ml,      \
                          counters, q, q_stride, k_cache, v_cache, block_tables, bt_stride, ctx_lens, num_seqs, hq, \
-                         hkv, sl2, maxp3, none, nullptr);                                                  \
+                         hkv, sl2, maxp3, cpp, none, nullptr);                                             \
     break;
     switch (G) {
       D3_CASE(1)

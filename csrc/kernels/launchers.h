@@ -14,11 +14,19 @@ hipError_t launch_rms_norm(bf16_t* out, const bf16_t* in, const bf16_t* w, float
                            int64_t in_stride, int64_t out_stride, hipStream_t s);
 hipError_t launch_fused_add_rms_norm(bf16_t* out, const bf16_t* in, bf16_t* residual, const bf16_t* w, float eps,
                                      int rows, int hidden, int64_t in_stride, int64_t out_stride, hipStream_t s);
-hipError_t launch_silu_and_mul(bf16_t* out, const bf16_t* in, int rows, int inter, hipStream_t s);
+// row_scale (optional, fp32 [rows]): silu(r g) * (r u) — the prefill RMSNorm applied as a row scale after a
+// projection of the raw residual (norm weight folded into the weights)
+hipError_t launch_silu_and_mul(bf16_t* out, const bf16_t* in, int rows, int inter, hipStream_t s,
+                               const float* row_scale = nullptr);
+// prefill RMSNorm as a row scale: resid += x (x optional; bf16, in place) and rs[row] = rsqrt(mean(resid^2) + eps)
+// of the rounded residual. Any number of rows; grid = rows
+hipError_t launch_rms_row_scale(float* rs, bf16_t* resid, const bf16_t* x, int rows, int hidden, int64_t rstride,
+                                int64_t xstride, float eps, hipStream_t s);
 
 hipError_t launch_rope_and_cache(bf16_t* qkv, int64_t qkv_stride, const int64_t* positions, const float* cos_sin,
                                  const int64_t* slot_mapping, bf16_t* k_cache, bf16_t* v_cache, int num_tokens,
-                                 int hq, int hkv, int head_dim, int block_size, hipStream_t s, bool rot_q = true);
+                                 int hq, int hkv, int head_dim, int block_size, hipStream_t s, bool rot_q = true,
+                                 const float* row_scale = nullptr);
 hipError_t launch_copy_blocks(bf16_t* pool, const int64_t* pairs, int num_pairs, int planes, int64_t num_blocks,
                               int64_t slab, hipStream_t s);
 hipError_t launch_move_blocks(bf16_t* pool, bf16_t* buf, const int64_t* ids, int n, int planes, int64_t num_blocks,
@@ -31,7 +39,7 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
                                const bf16_t* v_cache, const int* block_tables, int bt_stride, const int* cu_q,
                                const int* ctx_lens, int num_seqs, int max_q_len, int hq, int hkv, int head_dim,
                                int block_size, float scale, hipStream_t s, const float* cos_sin = nullptr,
-                               int n_pos = 0);
+                               int n_pos = 0, const float* q_scale = nullptr);
 // Fused decode-attention prologue (attention.hip, attn_decode_v3_kernel<G, true>).
 struct AttnDecodeFuse {
   const float* slab = nullptr;      // qkv projection split-K slabs [sk][M][width] fp32

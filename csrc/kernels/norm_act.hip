@@ -282,8 +282,9 @@ hipError_t launch_row_sumsq(float* ssp, const bf16_t* x, int rows, int hidden, i
 // form: 114,688 workgroups at 16K x 14,336) was 1.6 % slower.
 template <int SM_PER>
 __global__ void __launch_bounds__(256) silu_mul_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ in,
-                                                       int inter) {
+                                                       int inter, const float* __restrict__ row_scale) {
   const int64_t row = blockIdx.x;
+  const float r = row_scale != nullptr ? row_scale[row] : 1.f;
   const int nc = inter >> 3;
   const int c0 = blockIdx.y * 256 * SM_PER + threadIdx.x;
   const uint4* g = reinterpret_cast<const uint4*>(in + row * 2 * (int64_t)inter);
@@ -303,17 +304,97 @@ __global__ void __launch_bounds__(256) silu_mul_kernel(bf16_t* __restrict__ out,
     unpack8(gv[i], a);
     unpack8(uv[i], b);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) y[j] = a[j] * __builtin_amdgcn_rcpf(1.f + __expf(-a[j])) * b[j];
+    for (int j = 0; j < 8; ++j) {
+      const float ga = a[j] * r;
+      y[j] = ga * __builtin_amdgcn_rcpf(1.f + __expf(-ga)) * (b[j] * r);
+    }
     if (c < nc) o[c] = pack8(y);
   }
 }
 
-hipError_t launch_silu_and_mul(bf16_t* out, const bf16_t* in, int rows, int inter, hipStream_t s) {
+hipError_t launch_silu_and_mul(bf16_t* out, const bf16_t* in, int rows, int inter, hipStream_t s,
+                               const float* row_scale) {
   if (inter % 8 != 0) return hipErrorInvalidValue;
   if (rows == 0) return hipSuccess;
   constexpr int per = 4;  // 4 vs 1 chunk per lane: 268 vs 272 us at 16K x 14,336 (bench/micro_silu_mul.py)
   dim3 grid(rows, (inter / 8 + 256 * per - 1) / (256 * per)), block(256);
-  hipLaunchKernelGGL(silu_mul_kernel<per>, grid, block, 0, s, out, in, inter);
+  hipLaunchKernelGGL(silu_mul_kernel<per>, grid, block, 0, s, out, in, inter, row_scale);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------
+// Prefill RMSNorm as a row scale (the norm weight folded into Wqkv / Wgate_up): resid += x (optional, bf16,
+// in place) and rs[row] = rsqrt(mean(resid^2) + eps) of the rounded residual. The consumers apply rs to the
+// projection's output rows (RoPE / KV write, the attention's Q load, SiLU * up), so no normalised copy of
+// the residual is written: 2 (3 with the add) x hidden x 2 bytes per row instead of 3 (4).
+// One workgroup per row; NC 16-byte chunks per thread, every load of the row in flight before the first use.
+template <int NC, bool ADD>
+__global__ void __launch_bounds__(256) rms_row_scale_kernel(float* __restrict__ rs, bf16_t* __restrict__ resid,
+                                                            const bf16_t* __restrict__ x, int hidden, int64_t rstride,
+                                                            int64_t xstride, float eps) {
+  __shared__ float red[4];
+  const int64_t row = blockIdx.x;
+  uint4* r = reinterpret_cast<uint4*>(resid + row * rstride);
+  const uint4* src = ADD ? reinterpret_cast<const uint4*>(x + row * xstride) : nullptr;
+  const int nchunk = hidden >> 3;
+  uint4 rv[NC], xv[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int idx = min((int)threadIdx.x + c * 256, nchunk - 1);  // clamped, masked below
+    rv[c] = r[idx];
+    if (ADD) xv[c] = src[idx];
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int idx = threadIdx.x + c * 256;
+    if (idx < nchunk) {
+      float a[8];
+      unpack8(rv[c], a);
+      if (ADD) {
+        float b[8];
+        unpack8(xv[c], b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += b[j];
+        const uint4 p = pack8(a);
+        r[idx] = p;
+        unpack8(p, a);  // statistics of the rounded residual
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += a[j] * a[j];
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  if (threadIdx.x == 0) rs[row] = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)hidden + eps);
+}
+
+hipError_t launch_rms_row_scale(float* rs, bf16_t* resid, const bf16_t* x, int rows, int hidden, int64_t rstride,
+                                int64_t xstride, float eps, hipStream_t s) {
+  if (rows == 0) return hipSuccess;
+  if (hidden % 8) return hipErrorInvalidValue;
+  const int nc = (hidden / 8 + 255) / 256;
+  dim3 grid(rows), block(256);
+#define RR_CASE(N)                                                                                             \
+  case N:                                                                                                     \
+    if (x != nullptr)                                                                                         \
+      hipLaunchKernelGGL((rms_row_scale_kernel<N, true>), grid, block, 0, s, rs, resid, x, hidden, rstride,     \
+                         xstride, eps);                                                                       \
+    else                                                                                                      \
+      hipLaunchKernelGGL((rms_row_scale_kernel<N, false>), grid, block, 0, s, rs, resid, x, hidden, rstride,    \
+                         xstride, eps);                                                                       \
+    break;
+  switch (nc) {
+    RR_CASE(1)
+    RR_CASE(2)
+    RR_CASE(3)
+    RR_CASE(4)
+    default:
+      return hipErrorInvalidValue;  // hidden <= 8,192
+  }
+#undef RR_CASE
   return hipGetLastError();
 }
 

@@ -19,7 +19,8 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16_t* __restrict__ qk
                                                          const float* __restrict__ cos_sin,
                                                          const int64_t* __restrict__ slot_mapping,
                                                          bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
-                                                         int hq, int hkv, int block_size, int rot_q) {
+                                                         int hq, int hkv, int block_size, int rot_q,
+                                                         const float* __restrict__ row_scale) {
   constexpr int HALF = D / 2;
   constexpr int RC = HALF / 8;  // 8-wide rotation chunks per head
   constexpr int VC = D / 8;     // 16-byte chunks per head
@@ -28,6 +29,9 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16_t* __restrict__ qk
   const int64_t pos = positions[tok];
   const int64_t slot = slot_mapping ? slot_mapping[tok] : -1;
   const float* cs = cos_sin + pos * D;
+  // row_scale: the token's RMSNorm scale (prefill with the norm weight folded into Wqkv: the projection ran on
+  // the raw residual); applied to k with the rotation and to v, never to q (the attention scales its Q rows)
+  const float rsc = row_scale != nullptr ? row_scale[tok] : 1.f;
   // rot_q = 0: q is left as it is (prefill attention rotates its Q rows itself when it loads them)
   const int h0 = rot_q ? 0 : hq;
   const int n_rot = (hq + hkv - h0) * RC;
@@ -43,10 +47,11 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16_t* __restrict__ qk
       *reinterpret_cast<float4*>(co + 4) = *reinterpret_cast<const float4*>(cs + c * 8 + 4);
       *reinterpret_cast<float4*>(si) = *reinterpret_cast<const float4*>(cs + HALF + c * 8);
       *reinterpret_cast<float4*>(si + 4) = *reinterpret_cast<const float4*>(cs + HALF + c * 8 + 4);
+      const float sc = head < hq ? 1.f : rsc;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        ya[j] = a[j] * co[j] - b[j] * si[j];
-        yb[j] = b[j] * co[j] + a[j] * si[j];
+        ya[j] = (a[j] * co[j] - b[j] * si[j]) * sc;
+        yb[j] = (b[j] * co[j] + a[j] * si[j]) * sc;
       }
       const uint4 pa = pack8(ya), pb = pack8(yb);
       if (head < hq) {
@@ -62,7 +67,14 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16_t* __restrict__ qk
     } else if (slot >= 0) {
       const int v = it - n_rot;
       const int kh = v / VC, c = v % VC;
-      const uint4 val = *reinterpret_cast<const uint4*>(row + (hq + hkv + kh) * D + c * 8);
+      uint4 val = *reinterpret_cast<const uint4*>(row + (hq + hkv + kh) * D + c * 8);
+      if (row_scale != nullptr) {
+        float f[8];
+        unpack8(val, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] *= rsc;
+        val = pack8(f);
+      }
       const int64_t blk = slot / block_size, off = slot % block_size;
       *reinterpret_cast<uint4*>(v_cache + ((blk * hkv + kh) * block_size + off) * D + c * 8) = val;
     }
@@ -71,17 +83,18 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(bf16_t* __restrict__ qk
 
 hipError_t launch_rope_and_cache(bf16_t* qkv, int64_t qkv_stride, const int64_t* positions, const float* cos_sin,
                                  const int64_t* slot_mapping, bf16_t* k_cache, bf16_t* v_cache, int num_tokens,
-                                 int hq, int hkv, int head_dim, int block_size, hipStream_t s, bool rot_q) {
+                                 int hq, int hkv, int head_dim, int block_size, hipStream_t s, bool rot_q,
+                                 const float* row_scale) {
   if (num_tokens == 0) return hipSuccess;
   dim3 grid(num_tokens), block(256);
   switch (head_dim) {
     case 64:
       hipLaunchKernelGGL(rope_cache_kernel<64>, grid, block, 0, s, qkv, qkv_stride, positions, cos_sin,
-                         slot_mapping, k_cache, v_cache, hq, hkv, block_size, (int)rot_q);
+                         slot_mapping, k_cache, v_cache, hq, hkv, block_size, (int)rot_q, row_scale);
       break;
     case 128:
       hipLaunchKernelGGL(rope_cache_kernel<128>, grid, block, 0, s, qkv, qkv_stride, positions, cos_sin,
-                         slot_mapping, k_cache, v_cache, hq, hkv, block_size, (int)rot_q);
+                         slot_mapping, k_cache, v_cache, hq, hkv, block_size, (int)rot_q, row_scale);
       break;
     default:
       return hipErrorInvalidValue;

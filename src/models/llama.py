@@ -349,6 +349,8 @@ class CausalLM:
                 return self._forward_decode_slab(residual, positions, meta, kv_pool)
         if self.sequence_parallel and meta.is_prefill:
             return self._forward_sp(residual, positions, meta, kv_pool)
+        if self._prefill_row_scale(residual, meta):
+            return self._forward_prefill_row_scale(residual, positions, meta, kv_pool)
         x = ops.rms_norm(residual, self.layers[0].ln1, eps)
         h = None
         last = len(self.layers) - 1
@@ -365,14 +367,52 @@ class CausalLM:
             h = self.tp.all_reduce(self._mlp(lw, x))
         return ops.fused_add_rms_norm(h, residual, self.norm, eps)
 
+    def _prefill_row_scale(self, residual: torch.Tensor, meta: AttnMetadata) -> bool:
+        """GPU prefill steps above decode sizes with the norm weights folded run the RMSNorms as row scales."""
+        import os  # TEMP A/B
+        return (meta.is_prefill and residual.is_cuda and self.norms_folded and self.head_dim == 128
+                and residual.shape[0] > ops.DECODE_GEMM_MAX_M and not os.environ.get("DIE_AB_PF_OLD"))
+
+    def _forward_prefill_row_scale(self, residual: torch.Tensor, positions: torch.Tensor, meta: AttnMetadata,
+                                   kv_pool: torch.Tensor) -> torch.Tensor:
+        """Prefill with every folded RMSNorm as a per-token row scale: one pass adds the block output into the
+        residual and writes rs = rsqrt(mean(residual^2) + eps) (``ops.rms_row_scale``); the qkv and gate/up
+        projections run on the raw residual (their norm weights are folded in) and the consumers of their
+        outputs apply rs — k / v in the RoPE + KV-write kernel, q in the attention's Q load, gate / up in SiLU *
+        up. No normalised copy of the residual is written or read back: two [T, hidden] bf16 passes less per
+        norm. Mixtral keeps its explicit ln2 (it also feeds the router)."""
+        a, eps = self.arch, self.arch.rms_eps
+        rs = ops.rms_row_scale(residual, None, eps)
+        h = None
+        last = len(self.layers) - 1
+        for li, lw in enumerate(self.layers):
+            if li > 0:
+                rs = ops.rms_row_scale(residual, h, eps, out=rs)
+            if li == last and meta.keep_rows is not None:
+                return self._last_layer_kept_rows(lw, residual, residual, positions, meta, kv_pool, rs=rs)
+            attn = self._attention(li, lw, residual, positions, meta, kv_pool, rs=rs)
+            if meta.kv_hook is not None:
+                meta.kv_hook(li)
+            o = self.tp.all_reduce(ops.linear(attn, lw.o))
+            if a.is_moe:
+                x = ops.fused_add_rms_norm(o, residual, lw.ln2, eps)
+                h = self.tp.all_reduce(self._mlp(lw, x))
+            else:
+                rs2 = ops.rms_row_scale(residual, o, eps)
+                act = ops.silu_and_mul(ops.linear(residual, lw.gate_up), row_scale=rs2)
+                h = self.tp.all_reduce(ops.linear(act, lw.down))
+        return ops.fused_add_rms_norm(h, residual, self.norm, eps)
+
     def _last_layer_kept_rows(self, lw: LayerWeights, x: torch.Tensor, residual: torch.Tensor,
-                              positions: torch.Tensor, meta: AttnMetadata, kv_pool: torch.Tensor) -> torch.Tensor:
+                              positions: torch.Tensor, meta: AttnMetadata, kv_pool: torch.Tensor,
+                              rs: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Prefill's last layer, pruned to the rows whose hidden state is sampled: K / V of every token are
         still projected and written to the cache (later steps attend to them), but the query, attention, o, MLP
         and final norm run for one row per sampled sequence — the other rows' last-layer outputs would be
         discarded (a 16,384-token prefill of 32 prompts keeps 32 rows: ~1/32 of a layer's GEMM work for the
         sampled rows instead of a whole layer). The kept rows are each sequence's last token, so the attention is
-        a 1-query-per-sequence prefill attention over the full context."""
+        a 1-query-per-sequence prefill attention over the full context. rs: x is the raw residual and rs its
+        RMSNorm row scales (:meth:`_forward_prefill_row_scale`)."""
         eps, d, hq, hkv = self.arch.rms_eps, self.head_dim, self.hq, self.hkv
         li = len(self.layers) - 1
         keep = meta.keep_rows
@@ -381,7 +421,7 @@ class CausalLM:
         k_cache, v_cache = kv_pool[li, 0], kv_pool[li, 1]
         fuse_q = qkv.is_cuda
         ops.rope_and_cache(qkv, positions, self.cos_sin, meta.slot_mapping, k_cache, v_cache, hq, hkv, d,
-                           rot_q=not fuse_q)
+                           rot_q=not fuse_q, row_scale=rs)
         if meta.kv_hook is not None:
             meta.kv_hook(li)
         if n == 0:
@@ -392,7 +432,8 @@ class CausalLM:
         cu1 = torch.arange(n + 1, dtype=torch.int32, device=q.device)
         attn = ops.attn_prefill(q, k_cache, v_cache, meta.block_tables.index_select(0, seq),
                                 cu1, meta.ctx_lens.index_select(0, seq), 1, hq, hkv, self.scale,
-                                cos_sin=self.cos_sin if fuse_q else None)
+                                cos_sin=self.cos_sin if fuse_q else None,
+                                q_scale=rs.index_select(0, keep) if rs is not None else None)
         res = residual.index_select(0, keep)
         o = self.tp.all_reduce(ops.linear(attn, lw.o))
         x2 = ops.fused_add_rms_norm(o, res, lw.ln2, eps)
@@ -400,19 +441,22 @@ class CausalLM:
         return ops.fused_add_rms_norm(h, res, self.norm, eps)
 
     def _attention(self, li: int, lw: LayerWeights, x: torch.Tensor, positions: torch.Tensor, meta: AttnMetadata,
-                   kv_pool: torch.Tensor) -> torch.Tensor:
-        """qkv projection, RoPE + paged KV write, paged attention (prefill or decode) -> [T, hq*d]."""
+                   kv_pool: torch.Tensor, rs: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """qkv projection, RoPE + paged KV write, paged attention (prefill or decode) -> [T, hq*d].
+        rs (GPU prefill): x is the raw residual and rs its per-token RMSNorm scale, applied to k / v in the
+        KV write and to q in the attention's Q load."""
         d, hq, hkv = self.head_dim, self.hq, self.hkv
         qkv = ops.linear(x, lw.qkv)
         k_cache, v_cache = kv_pool[li, 0], kv_pool[li, 1]
         # prefill on the GPU: q's RoPE happens in the attention kernel's Q load (no q round trip through HBM)
         fuse_q = meta.is_prefill and qkv.is_cuda
         ops.rope_and_cache(qkv, positions, self.cos_sin, meta.slot_mapping, k_cache, v_cache, hq, hkv, d,
-                           rot_q=not fuse_q)
+                           rot_q=not fuse_q, row_scale=rs)
         q = qkv[:, : hq * d]
         if meta.is_prefill:
             return ops.attn_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_q, meta.ctx_lens,
-                                    meta.max_q_len, hq, hkv, self.scale, cos_sin=self.cos_sin if fuse_q else None)
+                                    meta.max_q_len, hq, hkv, self.scale, cos_sin=self.cos_sin if fuse_q else None,
+                                    q_scale=rs)
         return ops.attn_decode(q, k_cache, v_cache, meta.block_tables, meta.ctx_lens, meta.max_ctx, hq, hkv,
                                self.scale, part_o=meta.part_o, part_ml=meta.part_ml, counters=meta.attn_cnt)
 

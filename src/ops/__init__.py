@@ -64,37 +64,67 @@ def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
     return out
 
 
-def silu_and_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def silu_and_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None,
+                 row_scale: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(gate) * up for x = [gate | up]; row_scale (fp32 [T]): silu(r gate) * (r up) — the prefill RMSNorm
+    applied after a projection of the raw residual (:func:`rms_row_scale`)."""
     if not x.is_cuda:
+        if row_scale is not None:
+            x = (x.float() * row_scale[:, None]).to(x.dtype)
         return ref.silu_and_mul(x)
     if out is None:
         out = torch.empty(x.shape[0], x.shape[1] // 2, dtype=x.dtype, device=x.device)
-    _kern().silu_and_mul(out, x)
+    _kern().silu_and_mul(out, x, row_scale if row_scale is not None else _empty(x.device))
+    return out
+
+
+def rms_row_scale(resid: torch.Tensor, x: Optional[torch.Tensor], eps: float,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Prefill RMSNorm as a row scale (norm weight folded into the consuming projection): resid += x (bf16,
+    in place; x None: no add) and returns rs [T] fp32 = rsqrt(mean(resid^2) + eps). The projections then run
+    on the raw residual and their consumers scale the output rows (rope_and_cache / attn_prefill /
+    silu_and_mul ``row_scale``): no normalised copy of the residual is written."""
+    t = resid.shape[0]
+    if out is None:
+        out = torch.empty(t, dtype=torch.float32, device=resid.device)
+    if not resid.is_cuda:
+        if x is not None:
+            resid.copy_((resid.float() + x.float()).to(resid.dtype))
+        out.copy_(torch.rsqrt(resid.float().pow(2).mean(-1) + eps))
+        return out
+    _kern().rms_row_scale(out, resid, x if x is not None else _empty(resid.device), float(eps))
     return out
 
 
 def rope_and_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq: int, hkv: int, head_dim: int,
-                   rot_q: bool = True) -> None:
+                   rot_q: bool = True, row_scale: Optional[torch.Tensor] = None) -> None:
     """Rotate k (and q unless rot_q=False: prefill attention then rotates its Q rows on load, see
-    attn_prefill's cos_sin) and write k / v into the paged cache."""
+    attn_prefill's cos_sin) and write k / v into the paged cache. row_scale (fp32 [T], with rot_q=False):
+    k and v rows are scaled by the token's RMSNorm scale (:func:`rms_row_scale`); q is left to the attention."""
     if not qkv.is_cuda:
-        assert rot_q, "the CPU reference path rotates q here"
+        assert rot_q and row_scale is None, "the CPU reference path rotates q here"
         ref.rope_and_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq, hkv, head_dim)
         return
-    _kern().rope_and_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq, hkv, head_dim, rot_q)
+    assert row_scale is None or not rot_q, "a row scale is applied with the attention's Q rotation"
+    _kern().rope_and_cache(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, hq, hkv, head_dim, rot_q,
+                           row_scale if row_scale is not None else _empty(qkv.device))
 
 
 def attn_prefill(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_q_len: int, hq: int, hkv: int,
-                 scale: float, out: Optional[torch.Tensor] = None, cos_sin: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 scale: float, out: Optional[torch.Tensor] = None, cos_sin: Optional[torch.Tensor] = None,
+                 q_scale: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Causal paged prefill attention. cos_sin ([max_pos, 128] fp32): q is NOT yet rotated, the kernel
-    applies RoPE to each Q row as it loads it (token positions ctx - q_len + i)."""
+    applies RoPE to each Q row as it loads it (token positions ctx - q_len + i). q_scale (fp32 [T], with
+    cos_sin): each Q row is also scaled by its token's RMSNorm scale (:func:`rms_row_scale`)."""
     if not q.is_cuda:
-        assert cos_sin is None, "the CPU reference path takes a rotated q"
+        assert cos_sin is None and q_scale is None, "the CPU reference path takes a rotated q"
         return ref.attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, hq, hkv, scale).reshape(q.shape[0], -1)
     if out is None:
         out = torch.empty(q.shape[0], hq * 128, dtype=q.dtype, device=q.device)
+    assert q_scale is None or cos_sin is not None, "the Q row scale is applied with the rotation"
+    e = _empty(q.device)
     _kern().attn_prefill(out, q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_q_len, hq, hkv, scale,
-                         cos_sin if cos_sin is not None else _empty(q.device))
+                         cos_sin if cos_sin is not None else e, q_scale if q_scale is not None else e)
     return out
 
 

@@ -183,6 +183,64 @@ def test_rope_and_cache_keeps_q(dev):
     assert torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
 
 
+# ---------------------------------------------------------------- prefill RMSNorm as a row scale
+@pytest.mark.parametrize("t,h,add", [(700, 4096, True), (300, 8192, True), (129, 4096, False), (5, 1024, True)])
+def test_rms_row_scale(dev, t, h, add):
+    """resid += x (bf16) and rs = rsqrt(mean(resid^2) + eps) of the rounded residual, against fp32."""
+    res = torch.randn(t, h, device=dev, dtype=torch.bfloat16) * 3
+    x = torch.randn(t, h, device=dev, dtype=torch.bfloat16) if add else None
+    expect = (res.float() + x.float()).to(torch.bfloat16) if add else res.clone()
+    rs = ops.rms_row_scale(res, x, 1e-5)
+    assert torch.equal(res, expect)
+    close(rs, torch.rsqrt(expect.float().pow(2).mean(-1) + 1e-5), atol=1e-5, rtol=1e-4)
+
+
+def test_silu_and_mul_row_scale(dev):
+    t, inter = 37, 3584
+    x = torch.randn(t, 2 * inter, device=dev, dtype=torch.bfloat16) * 4
+    rs = torch.rand(t, device=dev) + 0.1
+    xs = x.float() * rs[:, None]
+    r = torch.nn.functional.silu(xs[:, :inter]) * xs[:, inter:]
+    close(ops.silu_and_mul(x, row_scale=rs), r, atol=3e-2, rtol=2e-2)
+
+
+def test_rope_and_cache_row_scale(dev):
+    """row_scale: k (rotated) and v are cached scaled by the token's factor; q stays untouched."""
+    hq, hkv, t, bs, nb = 32, 8, 45, 16, 16
+    qkv = torch.randn(t, (hq + 2 * hkv) * 128, device=dev, dtype=torch.bfloat16)
+    rs = torch.rand(t, device=dev) + 0.25
+    pos = torch.randint(0, 4000, (t,), device=dev)
+    slots = torch.randperm(nb * bs, device=dev)[:t]
+    cs = ref.rope_cos_sin(4096, 128, 500000.0, dev)
+    kc1, vc1 = _paged(nb, hkv, bs, dev)
+    kc2, vc2 = _paged(nb, hkv, bs, dev)
+    scaled = qkv.float()
+    scaled[:, hq * 128:] *= rs[:, None]
+    q1, q2 = scaled.to(torch.bfloat16), qkv.clone()
+    ops.rope_and_cache(q1, pos, cs, slots, kc1, vc1, hq, hkv, 128, rot_q=False)
+    ops.rope_and_cache(q2, pos, cs, slots, kc2, vc2, hq, hkv, 128, rot_q=False, row_scale=rs)
+    assert torch.equal(q2[:, : hq * 128], qkv[:, : hq * 128])
+    close(kc2, kc1, atol=2e-2, rtol=1e-2)
+    close(vc2, vc1, atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("g", [4, 8])
+def test_attn_prefill_q_scale(dev, g):
+    """q_scale: the Q rows are scaled by their token's factor together with the rotation on load — the same as
+    attention over the pre-scaled q."""
+    hkv = 8 if g == 4 else 1
+    qlens = [1, 37, 128, 200, 64]
+    ctxs = [1, 37, 300, 200, 1000]
+    q, kc, vc, bt, cu, ctx, hq = _make_seqs(qlens, ctxs, hkv, 16, dev, g)
+    cs = ref.rope_cos_sin(4096, 128, 500000.0, dev)
+    rs = torch.rand(q.shape[0], device=dev) + 0.25
+    qs = (q.float() * rs[:, None]).to(torch.bfloat16)
+    scale = 1 / math.sqrt(128)
+    a = ops.attn_prefill(q, kc, vc, bt, cu, ctx, max(qlens), hq, hkv, scale, cos_sin=cs, q_scale=rs)
+    b = ops.attn_prefill(qs, kc, vc, bt, cu, ctx, max(qlens), hq, hkv, scale, cos_sin=cs)
+    close(a, b, atol=2e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("g,bs,merge", [(4, 16, False), (8, 16, False), (4, 32, False), (1, 16, False),
                                          (2, 16, False), (4, 16, True)])
 def test_attn_decode(dev, g, bs, merge):
@@ -551,20 +609,26 @@ def test_gemm_decode_tiled_weights(dev, mode, n, k, wr, sk):
         close(a, x.float() @ w.float().t(), atol=2e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("g,hkv,big,tiles", [(4, 8, False, 4), (8, 1, False, 4), (1, 4, False, 4), (4, 8, True, 4),
-                                             (8, 1, False, 256), (4, 8, True, 130)])
-def test_attn_decode_fused(dev, g, hkv, big, tiles):
+@pytest.mark.parametrize("g,hkv,big,tiles,sk", [(4, 8, False, 4, 2), (8, 1, False, 4, 2), (1, 4, False, 4, 2),
+                                                (4, 8, True, 4, 2), (8, 1, False, 256, 2), (4, 8, True, 130, 2),
+                                                (8, 1, "tp8", 128, 4), (8, 1, "tp8", 256, 2)])
+def test_attn_decode_fused(dev, g, hkv, big, tiles, sk):
     """Fused prologue: norm scale + qkv slab sum + RoPE at ctx-1 + KV write, then attention.
-    big: 32 sequences x 8 kv heads. tiles: norm-statistics tiles (up to 256)."""
-    hq, sk, bs, d = hkv * g, 2, 16, 128
+    big: 32 sequences x 8 kv heads. "tp8": a Llama-3-70B TP=8 shard (32 sequences x 1 kv head, max context
+    2,048): single-chunk parts, two tasks per workgroup, most second tasks past their context and skipped.
+    tiles: norm-statistics tiles (up to 256). sk: qkv split-K slabs."""
+    hq, bs, d = hkv * g, 16, 128
     hid = 1024
     ctxs = [1, 17, 200, 777, 2049]
-    if big:
+    max_ctx = 4096
+    if big == "tp8":
+        ctxs = [1, 17, 64, 65, 129, 200, 1024, 1025, 2048] + [400 + 29 * i for i in range(23)]
+        max_ctx = 2048
+    elif big:
         ctxs = [1, 17, 64, 65, 129, 200, 777, 2049] + [400 + 29 * i for i in range(24)]
     n = len(ctxs)
     width = (hq + 2 * hkv) * d
     _, kc, vc, bt, _, ctx, _ = _make_seqs([1] * n, ctxs, hkv, bs, dev, g)
-    max_ctx = 4096
     bt_wide = torch.zeros(n, max_ctx // bs, dtype=torch.int32, device=dev)
     bt_wide[:, : bt.shape[1]] = bt
     slab = torch.randn(sk, n, width, device=dev) * 0.7   # normalised q/k/v ~ N(0, 1): realistic scores
