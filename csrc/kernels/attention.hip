@@ -410,22 +410,11 @@ __global__ void __launch_bounds__(256, 1) attn_decode_v3_kernel(
   long long tsv[5] = {0, 0, 0, 0, 0};
   if (fz.ts != nullptr) tsv[0] = __builtin_amdgcn_s_memrealtime();
 
-  int ctx_pf = -1;  // the context length of task t, loaded during the previous task (-1: not loaded)
 #pragma unroll 1
   for (int t = blockIdx.x; t < n_tasks; t += gridDim.x) {
     const int pair = t % pairs, part = t / pairs;
     const int seq = pair / hkv, kvh = pair - seq * hkv;
     const int c0 = part * C;
-    // the next task's context length, in flight with this task's scalar loads: a next task past its
-    // sequence's context is then skipped at this one's end without another round trip (single-chunk parts
-    // give a workgroup two or more tasks, most of them past a short context)
-    const int tn = t + (int)gridDim.x;
-    const int ctx_next = tn < n_tasks ? ctx_lens[__builtin_amdgcn_readfirstlane((tn % pairs) / hkv)] : 0;
-    if (ctx_pf >= 0 && c0 >= (ctx_pf + DEC_KEYS - 1) / DEC_KEYS) {  // uniform
-      ctx_pf = ctx_next;
-      continue;
-    }
-    ctx_pf = ctx_next;
     const int* bt = block_tables + (int64_t)seq * bt_stride;
     // the first chunk's two block ids of this wave, read speculatively (clamped to the table row) BEFORE the
     // context length: the two scalar loads are in flight together, so the first chunk's DMA waits for one
@@ -819,12 +808,11 @@ hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* c
     const int tasks = pairs * maxp3;
     const int ncu = num_cus();
     dim3 grid(tasks < ncu ? tasks : ncu), block(256);
-    // chunks per part: pairs x parts ~ the grid; with few (sequence, kv head) pairs (tensor-parallel shards:
-    // Llama-3-70B TP=8 has 32 at batch 32) every part is ONE chunk and a workgroup takes up to two tasks, so a
-    // short context spreads over several CUs instead of streaming several chunks through one CU's miss slots
-    int cpp = std::max(1, std::min(maxp3, (maxp3 * pairs + (int)grid.x - 1) / (int)grid.x));
-    static const bool ab_old = getenv("DIE_AB_ATTN_OLD") != nullptr;  // TEMP A/B
-    if (tasks <= 2 * (int)grid.x && !ab_old) cpp = 1;
+    // chunks per part, from the static max context: pairs x parts ~ the grid. (Single-chunk parts for the few
+    // pairs of a tensor-parallel shard — Llama-3-70B TP=8: 32 at batch 32, two tasks per workgroup — measured
+    // neutral: 12.69 vs 12.75 us per layer, the part's time is a chain of dependent round trips, not its
+    // CU's bandwidth; profiles/r5_tp8_attn_single_chunk_parts.txt)
+    const int cpp = std::max(1, std::min(maxp3, (maxp3 * pairs + (int)grid.x - 1) / (int)grid.x));
     AttnDecodeFuse none{};
     none.ts = g_attn_ts;
     AttnDecodeFuse fzc{};

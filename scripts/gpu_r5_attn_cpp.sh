@@ -1,5 +1,6 @@
 # round 5: single-chunk attention parts for few (sequence, kv head) pairs + prefill RMSNorm as row scales —
 # tests, then the 70B TP=8 probe A/B and the bench A/B
+# (the DIE_AB_* switches were temporary: removed once the A/B was recorded in profiles/r5_*)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp

@@ -369,9 +369,8 @@ class CausalLM:
 
     def _prefill_row_scale(self, residual: torch.Tensor, meta: AttnMetadata) -> bool:
         """GPU prefill steps above decode sizes with the norm weights folded run the RMSNorms as row scales."""
-        import os  # TEMP A/B
         return (meta.is_prefill and residual.is_cuda and self.norms_folded and self.head_dim == 128
-                and residual.shape[0] > ops.DECODE_GEMM_MAX_M and not os.environ.get("DIE_AB_PF_OLD"))
+                and residual.shape[0] > ops.DECODE_GEMM_MAX_M)
 
     def _forward_prefill_row_scale(self, residual: torch.Tensor, positions: torch.Tensor, meta: AttnMetadata,
                                    kv_pool: torch.Tensor) -> torch.Tensor:

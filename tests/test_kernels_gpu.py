@@ -615,8 +615,8 @@ def test_gemm_decode_tiled_weights(dev, mode, n, k, wr, sk):
 def test_attn_decode_fused(dev, g, hkv, big, tiles, sk):
     """Fused prologue: norm scale + qkv slab sum + RoPE at ctx-1 + KV write, then attention.
     big: 32 sequences x 8 kv heads. "tp8": a Llama-3-70B TP=8 shard (32 sequences x 1 kv head, max context
-    2,048): single-chunk parts, two tasks per workgroup, most second tasks past their context and skipped.
-    tiles: norm-statistics tiles (up to 256). sk: qkv split-K slabs."""
+    2,048: two-chunk parts, up to 16 parts merged per pair; parts without the new token stage only the q rows
+    of the slabs). tiles: norm-statistics tiles (up to 256). sk: qkv split-K slabs."""
     hq, bs, d = hkv * g, 16, 128
     hid = 1024
     ctxs = [1, 17, 200, 777, 2049]
@@ -629,7 +629,7 @@ def test_attn_decode_fused(dev, g, hkv, big, tiles, sk):
     n = len(ctxs)
     width = (hq + 2 * hkv) * d
     _, kc, vc, bt, _, ctx, _ = _make_seqs([1] * n, ctxs, hkv, bs, dev, g)
-    bt_wide = torch.zeros(n, max_ctx // bs, dtype=torch.int32, device=dev)
+    bt_wide = torch.zeros(n, max(max_ctx // bs, bt.shape[1]), dtype=torch.int32, device=dev)
     bt_wide[:, : bt.shape[1]] = bt
     slab = torch.randn(sk, n, width, device=dev) * 0.7   # normalised q/k/v ~ N(0, 1): realistic scores
     ssv = (torch.rand(n, device=dev) + 0.5) * hid
