@@ -27,6 +27,9 @@ SHAPES = {  # name -> [(projection, N, K, modes)]
            ("down", 4096, 14336, (3,))],
     "8b_tp4": [("qkv", 1536, 4096, (2,)), ("o", 4096, 1024, (3,)), ("gate_up", 3584, 4096, (4, 6)),
                ("down", 4096, 3584, (3,))],
+    # the decode step's LM head (Llama-3 vocabulary): mode 0, bf16 logits; row-major weight ("tiled": False)
+    # as the engine stores it today, and tile-order
+    "lm_head": [("lm_head", 128256, 4096, (0,))],
 }
 TILES = [(32, 256), (48, 256), (64, 256), (32, 128), (48, 128), (64, 128), (96, 128), (112, 128), (128, 128),
          (64, 64), (128, 64)]
@@ -55,7 +58,8 @@ def main():
             best = None
             for mode in modes:
                 sks = (1,) if mode == 4 else (1, 2, 4, 8)
-                for wr, kc in TILES:
+                for (wr, kc), tiled in [(t, True) for t in TILES] + ([(t, False) for t in TILES]
+                                                                      if proj == "lm_head" else []):
                     for sk in sks:
                         cols = wr // 2 if silu else wr
                         if n % cols or k % (kc * sk) or not ops.gd_tile_valid(wr, kc, 32):
@@ -66,14 +70,20 @@ def main():
                         if mode == 6 and sk == 1:
                             continue
                         ntiles = n // cols
-                        if ntiles * sk > 4 * cus:
+                        if ntiles * sk > 4 * cus and proj != "lm_head":
+                            continue
+                        if mode == 0 and sk > 1:
                             continue
                         try:
-                            wt = ops.gd_pack_weights(w, wr, silu=silu, kc=kc)
+                            wt = ops.gd_pack_weights(w, wr, silu=silu, kc=kc) if tiled else w
                         except AssertionError:
                             continue
                         cnt = torch.zeros(max(1, ntiles), dtype=torch.int32, device=dev)
-                        if mode == 2:
+                        tb = 32 if tiled else 0
+                        if mode == 0:
+                            y = torch.empty(m, n, dtype=torch.bfloat16, device=dev)
+                            args = (y, x, wt, tb, wr, kc, 1, True, e, e, e, e, 0.0)
+                        elif mode == 2:
                             y = torch.empty(sk, m, n, dtype=torch.float32, device=dev)
                             args = (y, x, wt, 2 | 32, wr, kc, sk, True, e, e, e, e, 0.0)
                         elif mode == 3:
@@ -105,7 +115,8 @@ def main():
                         us = ts[len(ts) // 2]
                         wbytes = w.numel() * 2
                         rec = {"shape": sname, "proj": proj, "N": n, "K": k, "mode": mode, "tile": [wr, kc, sk],
-                               "grid": ntiles * sk, "us": round(us, 2), "TBps": round(wbytes / us / 1e6, 2)}
+                               "tiled": tiled, "grid": ntiles * sk, "us": round(us, 2),
+                               "TBps": round(wbytes / us / 1e6, 2)}
                         print(json.dumps(rec), flush=True)
                         if best is None or us < best["us"]:
                             best = rec

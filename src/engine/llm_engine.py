@@ -65,6 +65,8 @@ class LLMEngine:
         if hasattr(model, "pack_decode_weights") and hasattr(model, "decode_buckets"):
             # the decode GEMMs' tile-order weight copies are made before the KV pool takes the free HBM
             model.pack_decode_weights(model.decode_buckets(cfg.max_num_seqs))
+        if hasattr(model, "pack_lm_head"):
+            model.pack_lm_head()
         nblocks = plan_kv_blocks(self.arch, model, cfg, self.device)
         self.pool = KVPool(self.arch.num_layers, nblocks, model.hkv, cfg.block_size, self.arch.head_dim,
                            self.device, dtype=model.dtype)

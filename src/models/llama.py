@@ -115,6 +115,7 @@ class CausalLM:
         self.full_init = full_init
         self.sequence_parallel = bool(sequence_parallel and self.tp.enabled)
         self.tiled_decode_weights = True  # decode GEMMs on tile-order copies (pack_decode_weights)
+        self.lm_head_tile = None          # (wr, kc) once the LM head is re-laid in place in tile order
         self.layers: List[LayerWeights] = []
         self._init_random(seed, init_std)
         self.cos_sin = rope_cos_sin(self.max_position, a.head_dim, a.rope_theta, self.device, a.rope_scaling)
@@ -221,6 +222,32 @@ class CausalLM:
                 lw.ln2.fill_(1)
         self.norms_folded = True
 
+    # LM head tiles tried in order (bench/micro_tp_tiles.py --shapes lm_head, cold, 32 rows: tile-order
+    # (128, 128) 171.8 us vs the row-major (64, 256) 187.0 us for Llama-3's 128,256 x 4,096)
+    LM_HEAD_TILES = ((128, 128), (64, 256), (64, 128))
+
+    def pack_lm_head(self) -> bool:
+        """Re-lay the LM head IN PLACE in the decode GEMM's tile order (one copy: its only consumer is the
+        decode GEMM — logits are computed for the sampled rows, in <= 128-row chunks). Returns whether packed."""
+        if self.lm_head_tile is not None:
+            return True
+        if not (self.tiled_decode_weights and self.device.type == "cuda" and ops.native_available()):
+            return False
+        rows, k = self.lm_head.shape
+        for wr, kc in self.LM_HEAD_TILES:
+            if rows % wr == 0 and k % kc == 0 and ops.gd_tile_valid(wr, kc, 32):
+                self.lm_head.copy_(ops.gd_pack_weights(self.lm_head, wr, kc=kc))
+                self.lm_head_tile = (wr, kc)
+                torch.cuda.empty_cache()  # the packing transients, before the KV pool is sized
+                return True
+        return False
+
+    def lm_head_rows(self) -> torch.Tensor:
+        """The LM head in its row-major layout (a copy when it is kept in tile order)."""
+        if self.lm_head_tile is None:
+            return self.lm_head
+        return ops.gd_unpack_weights(self.lm_head, *self.lm_head_tile)
+
     def load_state_dict(self, tensors: Dict[str, torch.Tensor], fold: bool = True) -> int:
         """Load HuggingFace-named Llama / Mixtral tensors at their FULL (unsharded) shapes; this
         rank's Megatron slice is cut here, so a checkpoint shard file can be streamed in as is and
@@ -229,6 +256,9 @@ class CausalLM:
         False while streaming several files, then call :meth:`fold_norm_weights` once)."""
         for lw in self.layers:  # decode tile-order copies go stale: re-packed by alloc_decode_scratch
             lw.tiled = {}
+        if self.lm_head_tile is not None:  # back to row-major for the checkpoint's rows (re-packed likewise)
+            self.lm_head.copy_(self.lm_head_rows())
+            self.lm_head_tile = None
         a, d, r, ws = self.arch, self.head_dim, self.tp.rank, self.tp.world_size
         hq, hkv, inter = self.hq, self.hkv, self.inter
         kv_idx = (r * hkv) if a.num_kv_heads >= ws else r // (ws // a.num_kv_heads)
@@ -313,7 +343,8 @@ class CausalLM:
         def conv(t):
             return None if t is None else t.detach().to(device=device, dtype=dtype)
 
-        m.embed, m.norm, m.lm_head = conv(self.embed), conv(self.norm), conv(self.lm_head)
+        m.embed, m.norm, m.lm_head = conv(self.embed), conv(self.norm), conv(self.lm_head_rows())
+        m.lm_head_tile = None
         m.layers = []
         for lw in self.layers:
             nl = LayerWeights()
@@ -627,6 +658,7 @@ class CausalLM:
                 return None
         dev = self.device
         self.pack_decode_weights(buckets)
+        self.pack_lm_head()
         ld = ops.SSP_LD
         sc = {"plans": plans, "ssp0": torch.zeros(1, ld, dtype=f32, device=dev),
               # split-K gate/up (mode 6): fp32 partial slab + per-tile tickets, sized for the largest bucket
@@ -725,7 +757,14 @@ class CausalLM:
         return ops.linear(x, getattr(lw, name)) if t is None else ops.linear_tiled(x, t, wr, kc)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
-        logits = ops.linear(hidden, self.lm_head)
+        if self.lm_head_tile is not None and hidden.shape[0] > 0:  # tile order: the decode GEMM, <= 128 rows
+            wr, kc = self.lm_head_tile
+            mx = ops.DECODE_GEMM_MAX_M
+            logits = (ops.linear_tiled(hidden, self.lm_head, wr, kc) if hidden.shape[0] <= mx else
+                      torch.cat([ops.linear_tiled(hidden[i:i + mx], self.lm_head, wr, kc)
+                                 for i in range(0, hidden.shape[0], mx)]))
+        else:
+            logits = ops.linear(hidden, self.lm_head)
         if self.vocab_parallel:
             logits = self.tp.all_gather_last(logits)
         return logits

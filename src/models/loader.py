@@ -79,7 +79,7 @@ def hf_state_dict(model) -> Dict[str, torch.Tensor]:
     a, d = model.arch, model.head_dim
     hq, hkv, inter = model.hq, model.hkv, model.inter
     out = {"model.embed_tokens.weight": model.embed, "model.norm.weight": model.norm,
-           "lm_head.weight": model.lm_head}
+           "lm_head.weight": model.lm_head_rows()}
     for i, lw in enumerate(model.layers):
         p = f"model.layers.{i}."
         out[p + "self_attn.q_proj.weight"] = lw.qkv[: hq * d]

@@ -313,6 +313,20 @@ def gd_pack_weights(w: torch.Tensor, wr: int, silu: bool = False, kc: Optional[i
     return wt.permute(0, 2, 1, 3, 4).contiguous().view(rows, k)
 
 
+def gd_unpack_weights(wt: torch.Tensor, wr: int, kc: Optional[int] = None) -> torch.Tensor:
+    """Inverse of :func:`gd_pack_weights` (plain projections, not the SiLU pairing): the row-major weight."""
+    rows, k = wt.shape
+    wrr, kc = gd_tile(wr, kc)
+    cpr = kc // 8
+    assert rows % wrr == 0 and k % kc == 0
+    nt, nch = rows // wrr, k // kc
+    w = wt.view(nt, nch, wrr, cpr, 8).permute(0, 2, 1, 3, 4)
+    r = torch.arange(wrr, device=wt.device).view(1, wrr, 1, 1, 1)
+    q = torch.arange(cpr, device=wt.device).view(1, 1, 1, cpr, 1)
+    sw = (q ^ gd_swizzle(r, kc)).expand(nt, wrr, nch, cpr, 8)  # the XOR swizzle is its own inverse
+    return torch.gather(w, 3, sw).contiguous().view(rows, k)
+
+
 _EMPTY: dict = {}
 
 

@@ -44,3 +44,17 @@ def test_tile_override_parser():
 
     assert ops._tile_overrides("4096,4096,3,32=32,256,2; 14336,4096,4,32=128,128,1") == {
         (4096, 4096, 3, 32): (32, 256, 2), (14336, 4096, 4, 32): (128, 128, 1)}
+
+
+def test_tile_order_pack_unpack_round_trip():
+    """ops.gd_pack_weights / gd_unpack_weights (the decode GEMM's tile order; the LM head is kept in it in
+    place, and unpacked for checkpoint export and the fp32 reference copy) are exact inverses."""
+    import torch
+
+    from src import ops
+
+    for wr, kc, rows, k in ((128, 128, 1024, 512), (64, 256, 640, 1024), (64, 128, 256, 4096), (32, 256, 96, 512)):
+        w = torch.randn(rows, k).to(torch.bfloat16)
+        p = ops.gd_pack_weights(w, wr, kc=kc)
+        assert p.shape == w.shape and not torch.equal(p, w)
+        assert torch.equal(ops.gd_unpack_weights(p, wr, kc=kc), w), (wr, kc)
