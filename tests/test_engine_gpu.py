@@ -390,11 +390,19 @@ def test_queued_decode_windows_match_synchronous():
     b2 = _run_requests(engs[False], reqs)
     o2 = _run_requests(engs[True], reqs)
     assert o2 == b2 and len(o2[0]) == first + 1
-    # a prompt arriving while windows are queued: the chain ends, the prompt is admitted
+    # a prompt arriving while windows are queued: the chain ends, the prompt is admitted. The modes need not
+    # admit it at the same decode step (the queued window runs first), so a row's token may come from a mixed
+    # prefill step in one mode and from a decode step in the other — two kernel paths that round differently:
+    # tokens must agree up to the first near-tie of the no-cache greedy reference (a near-tie flip at the last
+    # token of a 70-token request was seen once the prefill norms became row scales)
     late = (prompts[2][:30], SamplingParams(max_tokens=20))
     b3 = _run_requests(engs[False], [(p, SamplingParams(max_tokens=n)) for p, n in zip(prompts, lens)], late)
     o3 = _run_requests(engs[True], [(p, SamplingParams(max_tokens=n)) for p, n in zip(prompts, lens)], late)
-    assert o3 == b3 and len(o3) == len(prompts) + 1
+    assert len(o3) == len(b3) == len(prompts) + 1 and [len(x) for x in o3] == [len(x) for x in b3]
+    for i, (p, n) in enumerate(zip(prompts + [late[0]], lens + [20])):
+        if o3[i] != b3[i]:
+            r, m = reference_with_margins(engs[True].model, p, n)
+            assert agree(o3[i], r, m) and agree(b3[i], r, m), (i, o3[i], b3[i], r, m)
     # the queued windows leak no KV blocks
     assert engs[True].blocks.bm.num_available() == engs[False].blocks.bm.num_available()
 
