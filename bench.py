@@ -89,6 +89,7 @@ def parse(argv=None):
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-async-decode", action="store_true", help="synchronous decode windows (A/B)")
     p.add_argument("--temperature", type=float, default=0.0)
+    p.add_argument("--no-gemm-table", action="store_true", help="prefill GEMMs on the library defaults (A/B)")
     p.add_argument("--decode-window", type=int, default=None, help="decode steps per hipGraph window (engine default)")
     p.add_argument("--tp", type=int, default=1, help="tensor-parallel degree per replica (70B: --tp 8)")
     p.add_argument("--moe-parallel", choices=["tp", "ep"], default="tp", help="MoE layout under --tp")
@@ -189,7 +190,7 @@ def serve_timed(args, rank, world, dev, on_gpu):
     cfg = EngineConfig(max_num_seqs=args.batch, max_num_batched_tokens=max(16384, args.prompt_len),
                        num_kv_blocks=kv_blocks, max_latency_ms=args.max_latency_ms, use_cuda_graph=not args.no_graph,
                        graph_batch_sizes=[1, 2, 4, 8, 16, 24, 32, args.batch],
-                       async_decode=not args.no_async_decode,
+                       async_decode=not args.no_async_decode, tuned_gemm_table=not args.no_gemm_table,
                        **({"decode_window": args.decode_window} if args.decode_window else {}))
     t_init = time.perf_counter()
     tp = None

@@ -127,6 +127,8 @@ class EngineConfig:
     # window is queued behind the running one (Poisson 40 req/s TTFT p50 38.6 -> 29.8 ms at equal e2e,
     # profiles/poisson_r4_arrival_ab.jsonl). 0: off
     arrival_window_ms: float = 250.0
+    # prefill GEMMs: the measured solution table for the serving shapes (src/ops/gemm_table.py), read-only
+    tuned_gemm_table: bool = True
 
 
 @dataclass

@@ -62,6 +62,10 @@ class LLMEngine:
         self.device = model.device
         self.max_model_len = min(max_model_len, model.max_position)
         self.eos_token_id = eos_token_id
+        if self.device.type == "cuda" and getattr(cfg, "tuned_gemm_table", True):
+            from src.ops.gemm_table import enable_prefill_gemm_table
+
+            enable_prefill_gemm_table()
         if hasattr(model, "pack_decode_weights") and hasattr(model, "decode_buckets"):
             # the decode GEMMs' tile-order weight copies are made before the KV pool takes the free HBM
             model.pack_decode_weights(model.decode_buckets(cfg.max_num_seqs))

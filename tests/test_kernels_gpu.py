@@ -756,3 +756,19 @@ def test_gate_up_split_k_silu_matches_full_k(dev, n, k, wr, kc, sk, m):
         err = float((out.float() - ref).norm() / ref.norm())
         assert err < 1e-2, err
     assert float((got.float() - one.float()).norm() / one.float().norm()) < 5e-3
+
+
+def test_prefill_gemm_table_loads_and_matches_fp32(dev):
+    """The prefill GEMM table (src/ops/gemm_table.py) loads read-only on this stack (TunableOp on, tuning off)
+    and a listed shape (Llama-3-8B qkv at 2,048 tokens) still matches the fp32 product."""
+    from src.ops.gemm_table import enable_prefill_gemm_table, table_entries
+
+    import torch.cuda.tunable as tun
+
+    assert enable_prefill_gemm_table(), "table rejected by this PyTorch / ROCm stack"
+    assert tun.is_enabled() and not tun.tuning_is_enabled()
+    assert (6144, 2048, 4096) in table_entries()
+    x = torch.randn(2048, 4096, device=dev).to(torch.bfloat16)
+    w = (torch.randn(6144, 4096, device=dev) * 0.02).to(torch.bfloat16)
+    y = torch.nn.functional.linear(x, w)
+    close(y, x.float() @ w.float().t(), atol=3e-2, rtol=2e-2)

@@ -58,3 +58,23 @@ def test_tile_order_pack_unpack_round_trip():
         p = ops.gd_pack_weights(w, wr, kc=kc)
         assert p.shape == w.shape and not torch.equal(p, w)
         assert torch.equal(ops.gd_unpack_weights(p, wr, kc=kc), w), (wr, kc)
+
+
+def test_prefill_gemm_table_is_well_formed():
+    """The shipped prefill GEMM table (src/ops/gemm_table.py): validators for the stack it was measured on,
+    only TN bf16 entries with a named solution (no 'Default' rows: those shapes keep the library path), the
+    Llama-3-8B bench wave's qkv / o / gate-up shapes present; loading it is a no-op without a GPU."""
+    from src.ops import gemm_table
+
+    lines = open(gemm_table.TABLE).read().splitlines()
+    vals = {l.split(",")[1] for l in lines if l.startswith("Validator,")}
+    assert {"PT_VERSION", "HIP_VERSION", "HIPBLASLT_VERSION", "GCN_ARCH_NAME", "ROCBLAS_VERSION"} <= vals
+    assert any("gfx950" in l for l in lines if l.startswith("Validator,GCN_ARCH_NAME"))
+    ent = gemm_table.table_entries()
+    assert ent and all(s != "Default" for s in ent.values())
+    for n, k in ((6144, 4096), (4096, 4096), (28672, 4096)):
+        assert (n, 16384, k) in ent
+    import torch
+
+    if not torch.cuda.is_available():
+        assert gemm_table.enable_prefill_gemm_table() is False
