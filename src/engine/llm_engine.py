@@ -65,7 +65,7 @@ class LLMEngine:
         if self.device.type == "cuda" and getattr(cfg, "tuned_gemm_table", True):
             from src.ops.gemm_table import enable_prefill_gemm_table
 
-            enable_prefill_gemm_table()
+            enable_prefill_gemm_table(self.device)
         if hasattr(model, "pack_decode_weights") and hasattr(model, "decode_buckets"):
             # the decode GEMMs' tile-order weight copies are made before the KV pool takes the free HBM
             model.pack_decode_weights(model.decode_buckets(cfg.max_num_seqs))

@@ -34,8 +34,24 @@ def table_entries(path: str = TABLE) -> dict:
     return out
 
 
-def enable_prefill_gemm_table(path: str = TABLE) -> bool:
-    """Load the table read-only into PyTorch TunableOp (once per process). Returns whether it is active."""
+def warm_table(device, path: str = TABLE) -> None:
+    """Run every listed GEMM once on ``device`` (operands uninitialised; results discarded). The table names
+    rocBLAS as well as hipBLASLt solutions: the first call into a library (handle creation, code-object
+    loads) can take a second or more, and a tensor-parallel rank that pays it inside its first prefill step
+    while its peers already wait in a one-shot collective would trip their bounded wait (a spurious TP fault).
+    Paying it here, before serving, keeps the first prefill step as fast as the others."""
+    for (n, m, k) in sorted(table_entries(path), key=lambda e: e[0] * e[1] * e[2]):
+        x = torch.empty(m, k, dtype=torch.bfloat16, device=device)
+        w = torch.empty(n, k, dtype=torch.bfloat16, device=device)
+        torch.nn.functional.linear(x, w)
+        del x, w
+    torch.cuda.synchronize(device)
+    torch.cuda.empty_cache()
+
+
+def enable_prefill_gemm_table(device=None, path: str = TABLE) -> bool:
+    """Load the table read-only into PyTorch TunableOp (once per process) and warm its libraries on ``device``
+    (default: the current device). Returns whether it is active."""
     global _loaded
     if _loaded is not None:
         return _loaded
@@ -51,6 +67,8 @@ def enable_prefill_gemm_table(path: str = TABLE) -> bool:
         _loaded = bool(tun.read_file(path))
         if not _loaded:
             tun.enable(False)
+        else:
+            warm_table(device if device is not None else torch.device("cuda", torch.cuda.current_device()), path)
     except Exception as e:  # a stack the table was not made on: keep the library defaults
         logger.warning("prefill GEMM table not loaded: %s", e)
         _loaded = False
