@@ -441,6 +441,7 @@ def main(argv=None) -> int:
                 "max_latency_ms": args.max_latency_ms,
                 "weights": "random-init",
                 "hip_graph_decode": not args.no_graph,
+                "prefill_gemm_table": not args.no_gemm_table,
             },
             "notes": {
                 "baseline": "reference publishes no numbers and has no GPU path (BASELINE.md); vs_baseline=null",
