@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--shapes", default="70b_tp8,8b_tp2")
     ap.add_argument("--rows", type=int, default=32)
     ap.add_argument("--proj", default="", help="comma-separated projections to sweep (default: all)")
+    ap.add_argument("--splits", default="1,2,4,8", help="split-K counts to try (uneven splits allowed: 3,5,6)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     kern = ops._kern()
@@ -57,12 +58,12 @@ def main():
             ssp = (torch.rand(4, 128, device=dev) * k * 0.1).float()
             best = None
             for mode in modes:
-                sks = (1,) if mode == 4 else (1, 2, 4, 8)
+                sks = (1,) if mode == 4 else tuple(int(v) for v in a.splits.split(","))
                 for (wr, kc), tiled in [(t, True) for t in TILES] + ([(t, False) for t in TILES]
                                                                       if proj == "lm_head" else []):
                     for sk in sks:
                         cols = wr // 2 if silu else wr
-                        if n % cols or k % (kc * sk) or not ops.gd_tile_valid(wr, kc, 32):
+                        if n % cols or k % kc or k // kc < sk or not ops.gd_tile_valid(wr, kc, 32):
                             continue
                         lim = ops.SSP_MAX_TILES if m <= 32 else ops.SSP_MAX_TILES_WIDE
                         if mode == 3 and (wr not in (32, 64, 128) or n // wr > lim):

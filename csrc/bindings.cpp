@@ -481,7 +481,7 @@ static void gemm_decode_impl(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t
   TORCH_CHECK(gd_tile_ok(wr, kc), "gemm_decode: unsupported (wr, kc) tile");
   TORCH_CHECK(mode >= 0 && mode <= 6 && mode != 5, "mode");
   const int64_t wrr = wr;  // rows per workgroup
-  TORCH_CHECK(K % (kc * sk) == 0, "gemm_decode: K must be a multiple of kc * sk");
+  TORCH_CHECK(K % kc == 0 && K / kc >= sk, "gemm_decode: K must be a multiple of kc with >= sk K-slots");
   const bool silu = mode == 1 || mode == 4 || mode == 6;
   int64_t N, ldy;
   if (mode == 2 || mode == 3) {

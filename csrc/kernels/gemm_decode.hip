@@ -199,9 +199,12 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
     Yv = reinterpret_cast<char*>(Yv) + (int64_t)r0 * ldy * (EPI == 2 || EPI == 3 ? 4 : 2);
   }
   const int n0 = bx * NO;
-  const int kper = K / ny;
-  const int k0 = by * kper;
-  const int nch = kper / KC;
+  // split by of ny takes K-chunks [by * tch / ny, (by + 1) * tch / ny): any split count up to tch (uneven
+  // splits differ by one chunk), so grids of e.g. 40 tiles x 5 splits exist for K = 2^13
+  const int tch = K / KC;
+  const int c_lo = by * tch / ny;
+  const int k0 = c_lo * KC;
+  const int nch = (by + 1) * tch / ny - c_lo;
 
   // Per-lane source rows for this wave's DMA pieces (fixed across chunks).
   const bf16_t* src[PER_WAVE];
@@ -622,7 +625,7 @@ template <int WR, int EPI, int KC, int SKC = 0>
 static hipError_t launch_gd(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N_out,
                             int K, int sk, bool nt, const GemmDecodeFuse& fz, hipStream_t s) {
   constexpr int NO = (EPI == 1 || EPI == 4 || EPI == 6) ? WR / 2 : WR;
-  if (N_out % NO || K % sk || (K / sk) % KC) return hipErrorInvalidValue;
+  if (N_out % NO || K % KC || K / KC < sk) return hipErrorInvalidValue;
   // Activation image: the smallest of 16 / 32 / 64 / 128 rows that holds M and exists for this tile
   // (16 only on the nt path). Measured (profiles/micro_gemm_decode_xr16_r1.jsonl): dense 8B projections
   // at M = 8 / 16 ~1.5 % faster with 16 rows than 32; Mixtral grouped experts a tie.

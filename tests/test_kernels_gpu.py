@@ -522,7 +522,7 @@ def test_rope_and_cache_slab(dev):
 @pytest.mark.parametrize("wr,sk,k,m,kc", [(64, 4, 4096, 27, None), (64, 4, 14336, 27, None), (32, 1, 2048, 27, None),
                                           (128, 2, 4096, 27, None), (64, 8, 4096, 27, None), (32, 3, 3072, 27, None),
                                           (64, 4, 4096, 100, 128), (128, 8, 4096, 128, 32), (64, 2, 14336, 64, 256),
-                                          (128, 4, 4096, 77, 64)])
+                                          (128, 4, 4096, 77, 64), (64, 3, 4096, 27, 256), (32, 5, 8192, 32, 256)])
 def test_gemm_decode_residual_mode(dev, wr, sk, k, m, kc):
     """mode 3: resid += x @ w^T with the split-K reduced by the last-arriving workgroup, which
     also writes the per-tile row sums of squares of the new residual."""
@@ -543,6 +543,20 @@ def test_gemm_decode_residual_mode(dev, wr, sk, k, m, kc):
         rr = 32 if m <= 32 else (64 if m <= 64 else 128)  # rows of the activation image: padded rows -> 0
         assert torch.all(ssp[:, m:rr] == 0)
         assert int(cnt.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("n,k,wr,kc,sk,m", [(1280, 8192, 32, 256, 5, 32), (1280, 8192, 32, 128, 6, 7),
+                                            (6144, 4096, 48, 256, 3, 19)])
+def test_gemm_decode_uneven_split_slabs(dev, n, k, wr, kc, sk, m):
+    """Split-K counts that do not divide K's slots (splits differ by one K-slot): the fp32 slabs sum to x @ w^T,
+    row-major and tile-order weights alike."""
+    x = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(n, k, device=dev, dtype=torch.bfloat16) / math.sqrt(k)
+    ref32 = x.float() @ w.float().t()
+    a = ops.gemm_decode(x, w, mode=2, wr=wr, sk=sk, kc=kc)
+    b = ops.gemm_decode(x, ops.gd_pack_weights(w, wr, kc=kc), mode=2 | 32, wr=wr, sk=sk, kc=kc)
+    assert a.shape == (sk, m, n) and torch.equal(a, b)
+    close(a.sum(0), ref32, atol=2e-3, rtol=2e-3)
 
 
 @pytest.mark.parametrize("sk", [4, 3])
