@@ -79,3 +79,22 @@ def test_tp2_matches_tp1(preset, moe_parallel, sp):
         p.join(60)
         assert p.exitcode == 0
     assert got == expect
+
+
+def test_fused_exchange_residency_rule_at_70b_tp8_shapes():
+    """CustomAllReduce.fused_ok: on an 8-GPU node (one rank per GPU, 256 CUs) the 70B TP=8 decode
+    shard's row-parallel projections (wr = 32 tiles: o and down 256 column tiles, grid 256) carry the exchange
+    in their GEMM epilogue because the whole grid is resident; with 8 ranks sharing ONE GPU the same shapes
+    fall back to the separate all-reduce launch (neither the grid nor the waiting tiles fit), while 16 tiles
+    (the one-GPU GPU test's shape) may still fuse."""
+    from src.parallel.custom_allreduce import CustomAllReduce
+
+    node = object.__new__(CustomAllReduce)
+    node.ranks_per_gpu, node.cus = 1, 256
+    assert node.fused_ok(256, grid=256)            # 8192 / 32 tiles, split-K 1
+    assert node.fused_ok(128, grid=256)            # wr = 64, split-K 2
+    assert not node.fused_ok(256, grid=512)        # a grid twice the CUs with every tile waiting: never
+    shared = object.__new__(CustomAllReduce)
+    shared.ranks_per_gpu, shared.cus = 8, 256
+    assert not shared.fused_ok(256, grid=256) and not shared.fused_ok(128, grid=256)
+    assert shared.fused_ok(16, grid=32)
