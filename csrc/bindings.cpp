@@ -87,6 +87,26 @@ void silu_and_mul(Tensor out, Tensor x, Tensor row_scale) {
                                   opt_row_scale(row_scale, x.size(0), x, "silu_and_mul")));
 }
 
+// silu(gate) * up on [T, I] row views (unit column stride, 16-byte aligned rows; gate and up share a row stride).
+void silu_and_mul_views(Tensor out, Tensor gate, Tensor up, Tensor row_scale, int64_t per) {
+  CHK_CUDA(gate);
+  CHK_BF16(gate);
+  CHK_BF16(up);
+  CHK_BF16(out);
+  TORCH_CHECK(gate.dim() == 2 && up.sizes() == gate.sizes() && out.sizes() == gate.sizes(),
+              "silu_and_mul_views: gate, up, out [T, I]");
+  TORCH_CHECK(gate.stride(1) == 1 && up.stride(1) == 1 && out.stride(1) == 1 && up.stride(0) == gate.stride(0),
+              "silu_and_mul_views: unit column strides, one row stride for gate and up");
+  TORCH_CHECK(gate.size(1) % 8 == 0 && gate.stride(0) % 8 == 0 && out.stride(0) % 8 == 0 &&
+                  (reinterpret_cast<uintptr_t>(gate.data_ptr()) | reinterpret_cast<uintptr_t>(up.data_ptr()) |
+                   reinterpret_cast<uintptr_t>(out.data_ptr())) % 16 == 0,
+              "silu_and_mul_views: 16-byte aligned rows");
+  HIP_OK(die::launch_silu_and_mul_views(bf(out), out.stride(0), bf(gate), bf(up), gate.stride(0),
+                                        (int)gate.size(0), (int)gate.size(1), cur_stream(),
+                                        opt_row_scale(row_scale, gate.size(0), gate, "silu_and_mul_views"),
+                                        (int)per));
+}
+
 // Prefill RMSNorm as a row scale: resid += x (x empty: no add) and rs [T] = rsqrt(mean(resid^2) + eps).
 void rms_row_scale(Tensor rs, Tensor resid, Tensor x, double eps) {
   CHK_CUDA(resid);
@@ -881,6 +901,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("rms_norm", &rms_norm);
   m.def("fused_add_rms_norm", &fused_add_rms_norm);
   m.def("silu_and_mul", &silu_and_mul);
+  m.def("silu_and_mul_views", &silu_and_mul_views);
   m.def("rope_and_cache", &rope_and_cache);
   m.def("attn_prefill", &attn_prefill);
   m.def("attn_decode", &attn_decode);

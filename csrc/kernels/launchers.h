@@ -18,6 +18,11 @@ hipError_t launch_fused_add_rms_norm(bf16_t* out, const bf16_t* in, bf16_t* resi
 // projection of the raw residual (norm weight folded into the weights)
 hipError_t launch_silu_and_mul(bf16_t* out, const bf16_t* in, int rows, int inter, hipStream_t s,
                                const float* row_scale = nullptr);
+// silu(gate) * up on strided [rows, inter] views (16-byte aligned rows); per: 16-byte chunks per lane
+// (1..8, 0 = fewest workgroups per row, then fewest idle lanes)
+hipError_t launch_silu_and_mul_views(bf16_t* out, int64_t ostride, const bf16_t* gate, const bf16_t* up,
+                                     int64_t istride, int rows, int inter, hipStream_t s,
+                                     const float* row_scale = nullptr, int per = 0);
 // prefill RMSNorm as a row scale: resid += x (x optional; bf16, in place) and rs[row] = rsqrt(mean(resid^2) + eps)
 // of the rounded residual. Any number of rows; grid = rows
 hipError_t launch_rms_row_scale(float* rs, bf16_t* resid, const bf16_t* x, int rows, int hidden, int64_t rstride,

@@ -275,21 +275,26 @@ hipError_t launch_row_sumsq(float* ssp, const bf16_t* x, int rows, int hidden, i
 }
 
 // ----------------------------------------------------------------------------
-// silu(gate) * up. Input row = [gate(I) | up(I)], output row = I.
+// silu(gate) * up over strided row views: gate / up rows of I elements at row stride istride (the usual
+// input row = [gate(I) | up(I)]: up = gate + I, istride = 2I), output rows of I at ostride (column blocks of
+// a wider activation: bench/micro_ffn_nchunk.py).
 // grid = (rows, ceil(I/8 / (256 * SM_PER))); each lane owns SM_PER 16-byte chunks of a row (stride 256
 // chunks, so every load instruction of the workgroup is contiguous) and issues all of its gate and up
 // loads before the first use: 2 * SM_PER loads in flight per lane. One chunk per lane (the earlier
-// form: 114,688 workgroups at 16K x 14,336) was 1.6 % slower.
+// form: 114,688 workgroups at 16K x 14,336) was 1.6 % slower; at 16K x 14,336 one workgroup per row with 7
+// chunks per lane (the launcher's default) takes 256 us vs 266 us for two workgroups of 4
+// (profiles/r5_silu_per_lane_sweep.jsonl).
 template <int SM_PER>
-__global__ void __launch_bounds__(256) silu_mul_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ in,
-                                                       int inter, const float* __restrict__ row_scale) {
+__global__ void __launch_bounds__(256) silu_mul_kernel(bf16_t* __restrict__ out, int64_t ostride,
+                                                       const bf16_t* __restrict__ gate, const bf16_t* __restrict__ up,
+                                                       int64_t istride, int inter, const float* __restrict__ row_scale) {
   const int64_t row = blockIdx.x;
   const float r = row_scale != nullptr ? row_scale[row] : 1.f;
   const int nc = inter >> 3;
   const int c0 = blockIdx.y * 256 * SM_PER + threadIdx.x;
-  const uint4* g = reinterpret_cast<const uint4*>(in + row * 2 * (int64_t)inter);
-  const uint4* u = reinterpret_cast<const uint4*>(in + row * 2 * (int64_t)inter + inter);
-  uint4* o = reinterpret_cast<uint4*>(out + row * (int64_t)inter);
+  const uint4* g = reinterpret_cast<const uint4*>(gate + row * istride);
+  const uint4* u = reinterpret_cast<const uint4*>(up + row * istride);
+  uint4* o = reinterpret_cast<uint4*>(out + row * ostride);
   uint4 gv[SM_PER], uv[SM_PER];
 #pragma unroll
   for (int i = 0; i < SM_PER; ++i) {
@@ -312,14 +317,38 @@ __global__ void __launch_bounds__(256) silu_mul_kernel(bf16_t* __restrict__ out,
   }
 }
 
+hipError_t launch_silu_and_mul_views(bf16_t* out, int64_t ostride, const bf16_t* gate, const bf16_t* up,
+                                     int64_t istride, int rows, int inter, hipStream_t s, const float* row_scale,
+                                     int per) {
+  if (inter % 8 != 0 || ostride % 8 != 0 || istride % 8 != 0 || per < 0 || per > 8) return hipErrorInvalidValue;
+  if (rows == 0) return hipSuccess;
+  const int nc = inter / 8;
+  if (per == 0) {  // fewest workgroups per row at <= 8 chunks per lane, then the fewest idle lanes
+    const int nb = (nc + 256 * 8 - 1) / (256 * 8);
+    per = (nc + 256 * nb - 1) / (256 * nb);
+  }
+  dim3 grid(rows, (nc + 256 * per - 1) / (256 * per)), block(256);
+#define DIE_SILU_CASE(P)                                                                                       \
+  case P:                                                                                                     \
+    hipLaunchKernelGGL(silu_mul_kernel<P>, grid, block, 0, s, out, ostride, gate, up, istride, inter, row_scale); \
+    break;
+  switch (per) {
+    DIE_SILU_CASE(1)
+    DIE_SILU_CASE(2)
+    DIE_SILU_CASE(3)
+    DIE_SILU_CASE(4)
+    DIE_SILU_CASE(5)
+    DIE_SILU_CASE(6)
+    DIE_SILU_CASE(7)
+    DIE_SILU_CASE(8)
+  }
+#undef DIE_SILU_CASE
+  return hipGetLastError();
+}
+
 hipError_t launch_silu_and_mul(bf16_t* out, const bf16_t* in, int rows, int inter, hipStream_t s,
                                const float* row_scale) {
-  if (inter % 8 != 0) return hipErrorInvalidValue;
-  if (rows == 0) return hipSuccess;
-  constexpr int per = 4;  // 4 vs 1 chunk per lane: 268 vs 272 us at 16K x 14,336 (bench/micro_silu_mul.py)
-  dim3 grid(rows, (inter / 8 + 256 * per - 1) / (256 * per)), block(256);
-  hipLaunchKernelGGL(silu_mul_kernel<per>, grid, block, 0, s, out, in, inter, row_scale);
-  return hipGetLastError();
+  return launch_silu_and_mul_views(out, inter, in, in + inter, 2 * (int64_t)inter, rows, inter, s, row_scale, 0);
 }
 
 // ----------------------------------------------------------------------------

@@ -78,6 +78,21 @@ def silu_and_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None,
     return out
 
 
+def silu_and_mul_views(gate: torch.Tensor, up: torch.Tensor, out: torch.Tensor,
+                       row_scale: Optional[torch.Tensor] = None, per: int = 0) -> torch.Tensor:
+    """out = silu(r gate) * (r up) on [T, I] row views (unit column stride, e.g. column blocks of a wider
+    buffer): the SiLU * up of one FFN column chunk, written into its columns of the [T, inter] activation.
+    per: 16-byte chunks per lane (0: the launcher's choice; micro-benchmarks only)."""
+    if not gate.is_cuda:
+        g, u = gate.float(), up.float()
+        if row_scale is not None:
+            g, u = g * row_scale[:, None], u * row_scale[:, None]
+        out.copy_((torch.nn.functional.silu(g) * u).to(out.dtype))
+        return out
+    _kern().silu_and_mul_views(out, gate, up, row_scale if row_scale is not None else _empty(gate.device), per)
+    return out
+
+
 def rms_row_scale(resid: torch.Tensor, x: Optional[torch.Tensor], eps: float,
                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Prefill RMSNorm as a row scale (norm weight folded into the consuming projection): resid += x (bf16,

@@ -204,6 +204,29 @@ def test_silu_and_mul_row_scale(dev):
     close(ops.silu_and_mul(x, row_scale=rs), r, atol=3e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("per", [0, 1, 3, 7, 8])
+@pytest.mark.parametrize("inter,blocks", [(14336, 2), (7168, 1), (1008, 2), (64, 1)])
+def test_silu_and_mul_views(dev, per, inter, blocks):
+    """SiLU * up of FFN column blocks: gate / up are the two halves of each block's [T, 2c] GEMM output, the
+    result goes into the block's columns of a wider [T, inter] activation (strided rows on both sides), at
+    every chunks-per-lane count; the same bits as the [gate | up] layout's default launch."""
+    t, c = 29, inter // blocks
+    x = torch.randn(t, 2 * inter, device=dev, dtype=torch.bfloat16) * 3
+    rs = torch.rand(t, device=dev) + 0.25
+    want = ops.silu_and_mul(x, row_scale=rs)
+    xs = x.float() * rs[:, None]
+    close(want, torch.nn.functional.silu(xs[:, :inter]) * xs[:, inter:], atol=3e-2, rtol=2e-2)
+    # the same columns re-laid as blocks [gate_i | up_i] of width 2c
+    blk = torch.cat([torch.cat([x[:, c * i:c * (i + 1)], x[:, inter + c * i:inter + c * (i + 1)]], 1)
+                     for i in range(blocks)], 1)
+    out = torch.full((t, inter + 8), 7.0, device=dev, dtype=torch.bfloat16)  # wider rows, 8 guard columns
+    for i in range(blocks):
+        y = blk[:, 2 * c * i:2 * c * (i + 1)]
+        ops.silu_and_mul_views(y[:, :c], y[:, c:], out[:, c * i:c * (i + 1)], rs, per=per)
+    assert torch.equal(out[:, :inter], want)
+    assert bool((out[:, inter:] == 7).all())
+
+
 def test_rope_and_cache_row_scale(dev):
     """row_scale: k (rotated) and v are cached scaled by the token's factor; q stays untouched."""
     hq, hkv, t, bs, nb = 32, 8, 45, 16, 16
