@@ -24,13 +24,16 @@ ranks as a CHILD process and relays its result line and exit status; it never
 counts replicas that did not run. Under a launcher, ``--gpus`` must equal
 WORLD_SIZE.
 
-After the timed region of a multi-GPU run (its engines freed, under a watchdog)
-the node measures BASELINE configs 3 and 4 and the links they use
-(``notes.cross_gpu``, status also at the top level as ``cross_gpu_status``):
-cross-GPU transports (src/parallel/xgpu_probe.py), 8B disaggregated serving
-with prefill on rank 2k and decode on rank 2k+1 (N >= 2), and a Llama-3-70B
-TP=N engine serving one wave (N == 8) (src/parallel/node_bench.py). A stall
-prints the result with ``cross_gpu_status: "stalled ..."`` and exits 3.
+After the timed region of a multi-GPU run (its engines freed) the node measures
+BASELINE configs 3 and 4 and the links they use (``notes.cross_gpu``, status
+also at the top level as ``cross_gpu_status``): cross-GPU transports
+(src/parallel/xgpu_probe.py), 8B disaggregated serving with prefill on rank 2k
+and decode on rank 2k+1 (N >= 2), and a Llama-3-70B TP=N engine serving one
+wave (N == 8) (src/parallel/node_bench.py). That section runs in its OWN
+torch.distributed.run (a child of rank 0, one rank per GPU again), so a crash,
+GPU fault or hang there cannot cost the timed result: rank 0 waits at most
+``--cross-gpu-budget-s``, kills the child's process group on expiry, prints the
+result with ``cross_gpu_status: "stalled ..."`` and exits 3.
 
     python bench.py                      # 1 GPU, 3 timed steps, 1 warmup
     python bench.py --gpus 8 --steps 3   # spawns the 8-rank launcher itself
@@ -45,6 +48,7 @@ import asyncio
 import json
 import os
 import random
+import signal
 import socket
 import statistics
 import subprocess
@@ -108,6 +112,8 @@ def parse(argv=None):
     p.add_argument("--disagg-preset", default=None, help="config 3 model (default: --preset)")
     p.add_argument("--tp-wave-preset", default="llama3-70b", help="config 4 model")
     p.add_argument("--tp-wave-min-world", type=int, default=8, help="run the config-4 TP wave from this many ranks")
+    p.add_argument("--node-section-only", action="store_true",
+                   help="internal: the node section alone (the child run that rank 0 of a multi-rank run starts)")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args(argv)
 
@@ -272,9 +278,10 @@ def serve_timed(args, rank, world, dev, on_gpu):
 
 
 # ------------------------------------------------------------------------------------------------ node section
-def cross_gpu_section(args, rank, world, dev, on_gpu, state) -> dict:
+def cross_gpu_section(args, rank, world, dev, on_gpu, state, progress: bool = False) -> dict:
     """Configs 3 / 4 and the transports, after the timed region. Every rank runs every part in the same order;
-    ``state["part"]`` names the running part for the watchdog."""
+    ``state["part"]`` names the running part. progress (the child run's rank 0): one stdout line as each part
+    starts and ends, so the parent knows what finished if the run dies or stalls."""
     from src.parallel.node_bench import NodeBenchArgs, disagg_part, free_device_memory, tp_wave_part
 
     free_device_memory()  # the timed replicas' weights, KV pools and graphs
@@ -291,6 +298,8 @@ def cross_gpu_section(args, rank, world, dev, on_gpu, state) -> dict:
         parts.append("tp_wave")
     for part in parts:
         state["part"] = part
+        if progress:
+            print(json.dumps({"node_part_start": part}), flush=True)
         if args.verbose:
             print(f"[rank {rank}] node section: {part}", file=sys.stderr, flush=True)
         t0 = time.perf_counter()
@@ -309,10 +318,68 @@ def cross_gpu_section(args, rank, world, dev, on_gpu, state) -> dict:
             r.setdefault("part_s", round(time.perf_counter() - t0, 1))
         out[part] = r
         state.setdefault("done", {})[part] = r
+        if progress:
+            print(json.dumps({"node_part": part, "result": r}, default=str), flush=True)
         free_device_memory()
         dist.barrier(group=cpu)
     state["part"] = None
     return out
+
+
+_LAUNCHER_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                  "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT")
+
+
+def run_node_child(args, argv, world: int, state: dict):
+    """Rank 0: the node section in its own torch.distributed.run with ``world`` ranks (``--node-section-only``;
+    no exec — a child process group). Returns (cross, stalled): the section's results as its rank 0 reported
+    them — every finished part even when the run dies or is killed at the budget — with ``status`` 0 (all parts
+    ok), 1 (a part failed or the run exited non-zero) or STALL_EXIT (killed at the budget; ``stalled_part``)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)]
+    cmd += list(argv) + ["--node-section-only"]
+    env = {k: v for k, v in os.environ.items() if k not in _LAUNCHER_VARS and not k.startswith("TORCHELASTIC_")}
+    env["MASTER_ADDR"] = "127.0.0.1"
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, start_new_session=True)
+    stalled = False
+    try:
+        out, _ = p.communicate(timeout=args.cross_gpu_budget_s)
+    except subprocess.TimeoutExpired:
+        stalled = True
+        try:
+            os.killpg(p.pid, signal.SIGKILL)  # the launcher and every rank it started
+        except ProcessLookupError:
+            pass
+        out, _ = p.communicate()
+    done, final, started = {}, None, None
+    for ln in (out or "").splitlines():
+        d = None
+        if ln.startswith("{"):
+            try:
+                d = json.loads(ln)
+            except ValueError:
+                d = None
+        if not isinstance(d, dict):
+            print(ln, file=sys.stderr)
+        elif "node_part_start" in d:
+            started = state["part"] = d["node_part_start"]
+        elif "node_part" in d:
+            done[d["node_part"]] = d["result"]
+            state.setdefault("done", {})[d["node_part"]] = d["result"]
+            started = state["part"] = None
+        elif "node_section" in d:
+            final = d["node_section"]
+    if final is not None and not stalled and p.returncode == 0:
+        errs = _part_errors(final)
+        final["status"] = 1 if errs else 0
+        return final, False
+    cross = dict(done)
+    if stalled:
+        cross.update(status=STALL_EXIT, stalled_part=started)
+    else:
+        cross.update(status=1, error=f"node section run exited {p.returncode}"
+                     + (f" in {started}" if started else ""), failed_part=started)
+    return cross, stalled
 
 
 def _part_errors(cross: dict) -> list:
@@ -387,8 +454,15 @@ def main(argv=None) -> int:
             torch.cuda.set_device(0 if args.same_device else local)
         dist.init_process_group("nccl" if on_gpu and not args.same_device else "gloo")  # nccl = RCCL over xGMI
     dev = torch.device(f"cuda:{0 if args.same_device else local}" if on_gpu else "cpu")
+    if args.node_section_only:  # the child run of a multi-rank bench (run_node_child)
+        cross = cross_gpu_section(args, rank, world, dev, on_gpu, {"part": None, "done": {}}, progress=rank == 0)
+        if rank == 0:
+            print(json.dumps({"node_section": cross}, default=str), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return 0
 
-    from src.parallel.node_bench import device_identity, distinct_devices
+    from src.parallel.node_bench import device_identity, distinct_devices, free_device_memory
 
     m = serve_timed(args, rank, world, dev, on_gpu)
     elapsed, lats = m["elapsed"], m["lats"]
@@ -461,22 +535,38 @@ def main(argv=None) -> int:
     run_node = world > 1 and tp is None and (args.cross_gpu == "on" or (args.cross_gpu == "auto" and on_gpu))
     dog = None
     rc = 0
+    cpu = None
     if run_node:
         state: dict = {"part": None, "done": {}}
-        dog = _Watchdog(res, rank, args.cross_gpu_budget_s, state)
-        cross = cross_gpu_section(args, rank, world, dev, on_gpu, state)
+        # outer guard: the child run is bounded by the budget; this covers this process's own teardown
+        dog = _Watchdog(res, rank, args.cross_gpu_budget_s + 180.0, state)
+        free_device_memory()  # the timed replicas' weights, KV pools and graphs, before the child takes the GPUs
+        if dist.get_backend() != "gloo":
+            import datetime
+
+            cpu = dist.new_group(list(range(world)), backend="gloo",
+                                 timeout=datetime.timedelta(seconds=args.cross_gpu_budget_s + 600))
+        dist.barrier(group=cpu)
         if rank == 0:
-            errs = _part_errors(cross)
-            cross["status"] = 1 if errs else 0
+            cross, stalled = run_node_child(args, argv, world, state)
             res["notes"]["cross_gpu"] = cross
-            res["cross_gpu_status"] = ("error in " + ", ".join(errs)) if errs else "ok"
+            if stalled:
+                res["cross_gpu_status"] = (f"stalled in {cross.get('stalled_part') or 'teardown'}: no result within "
+                                           f"{args.cross_gpu_budget_s:.0f} s")
+                rc = STALL_EXIT
+            elif cross["status"]:
+                errs = _part_errors(cross) or [cross.get("failed_part") or "the node section run"]
+                res["cross_gpu_status"] = "error in " + ", ".join(errs)
+            else:
+                res["cross_gpu_status"] = "ok"
+        dist.barrier(group=cpu)  # the other ranks wait here (CPU) while rank 0's child run has the GPUs
     if rank == 0:
         if dog is not None:
             dog.emit()
         else:
             print(json.dumps(res), flush=True)
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=cpu)
         dist.destroy_process_group()
     if dog is not None:
         dog.cancel()

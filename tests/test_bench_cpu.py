@@ -132,3 +132,19 @@ def test_bench_node_section_configs_3_and_4_on_cpu():
     assert d["pairs"] == 1 and d["req_s_total"] > 0 and d["kv_path"] == "wire" and d["ttft_p50_ms"] > 0
     t = cross["tp_wave"]
     assert t["tp"] == 2 and t["requests"] == 4 and t["all_tokens"] and t["req_s"] > 0
+
+
+def test_bench_node_section_child_run_failure_and_stall():
+    """The node section runs in its own launcher (rank 0's child): a run that dies is reported as an error
+    (status 1, the exit code), a run past the budget is killed with its process group and reported as a stall
+    (status 3) — in both cases rank 0 still has the timed result to print."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    state = {"part": None, "done": {}}
+    args = bench.parse(SMALL + ["--cross-gpu", "on", "--cross-gpu-budget-s", "1"])
+    cross, stalled = bench.run_node_child(args, SMALL + ["--cross-gpu", "on"], 1, state)
+    assert stalled and cross["status"] == 3 and "stalled_part" in cross
+    args = bench.parse(SMALL + ["--cross-gpu-budget-s", "200"])
+    cross, stalled = bench.run_node_child(args, SMALL + ["--batch", "not-a-number"], 1, state)
+    assert not stalled and cross["status"] == 1 and "exited" in cross["error"], cross

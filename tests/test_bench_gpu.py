@@ -27,8 +27,8 @@ def test_bench_node_section_rehearsal_two_ranks_one_gpu():
         env.pop(k, None)
     cmd = [sys.executable, "bench.py", "--gpus", "2", "--same-device", "--preset", "llama-mini", "--batch", "8",
            "--prompt-len", "64", "--gen-len", "16", "--max-model-len", "256", "--steps", "1", "--warmup", "1",
-           "--tp-wave-min-world", "2", "--tp-wave-preset", "llama-mini", "--cross-gpu-budget-s", "100", "--verbose"]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
+           "--tp-wave-min-world", "2", "--tp-wave-preset", "llama-mini", "--cross-gpu-budget-s", "150", "--verbose"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
     lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
     # a stall in the node section prints the line with the stalled part (watchdog, exit 3): show it
     assert p.returncode == 0 and len(lines) == 1, (p.returncode, p.stdout[-3000:], p.stderr[-3000:])
