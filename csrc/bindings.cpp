@@ -299,7 +299,7 @@ int64_t decode_partials(int64_t max_ctx) { return die::attn_decode_max_partials(
 
 void sample(Tensor out, Tensor logits, c10::optional<Tensor> temperature, c10::optional<Tensor> top_k,
             c10::optional<Tensor> top_p, c10::optional<Tensor> seeds, c10::optional<Tensor> steps,
-            c10::optional<Tensor> part, c10::optional<Tensor> cnt) {
+            c10::optional<Tensor> part, c10::optional<Tensor> cnt, c10::optional<Tensor> lm_part) {
   CHK_CUDA(logits);
   CHK_BF16(logits);
   check_rows(logits, "logits");
@@ -324,11 +324,22 @@ void sample(Tensor out, Tensor logits, c10::optional<Tensor> temperature, c10::o
     pp = reinterpret_cast<uint32_t*>(part->data_ptr<int>());
     cp = cnt->data_ptr<int>();
   }
+  // lm_part [>= rows, parts, 2] int32: the LM head's per-column-tile greedy candidates (gemm_decode_argmax)
+  const uint32_t* lp = nullptr;
+  int lparts = 0;
+  if (lm_part.has_value()) {
+    TORCH_CHECK(lm_part->is_cuda() && lm_part->scalar_type() == at::kInt && lm_part->dim() == 3 &&
+                    lm_part->size(0) >= rows && lm_part->size(2) == 2 && lm_part->is_contiguous(),
+                "sample lm_part [rows, parts, 2] int32");
+    lp = reinterpret_cast<const uint32_t*>(lm_part->data_ptr<int>());
+    lparts = (int)lm_part->size(1);
+  }
   HIP_OK(die::launch_sample(out.data_ptr<int64_t>(), bf(logits), logits.stride(0), (int)rows, (int)logits.size(1),
                              (const float*)opt(temperature, at::kFloat, "temperature"),
                              (const int*)opt(top_k, at::kInt, "top_k"), (const float*)opt(top_p, at::kFloat, "top_p"),
                              (const int64_t*)opt(seeds, at::kLong, "seeds"),
-                             (const int64_t*)opt(steps, at::kLong, "steps"), cur_stream(), pp, cp, splits));
+                             (const int64_t*)opt(steps, at::kLong, "steps"), cur_stream(), pp, cp, splits,
+                             lp, lparts));
 }
 
 // pool viewed as [planes, num_blocks, slab]
@@ -567,6 +578,21 @@ static void gemm_decode_impl(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t
 void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t kc, int64_t sk, bool nt,
                  Tensor resid, Tensor ssp_out, Tensor counters, Tensor ssp_in, double eps) {
   gemm_decode_impl(y, x, w, mode, wr, kc, sk, nt, resid, ssp_out, counters, ssp_in, eps, die::GemmDecodeFuse{});
+}
+
+// y = x @ w^T (mode 0, bf16) that also writes each column tile's per-row greedy candidate into amax
+// [M, N / wr, 2] int32 (value bits, column): the decode step's LM head, whose argmax then reduces N / wr
+// candidates per row (sample(..., lm_part=amax)) instead of re-reading the logits.
+void gemm_decode_argmax(Tensor y, Tensor x, Tensor w, int64_t wr, int64_t kc, bool tiled, Tensor amax) {
+  CHK_DTYPE(amax, at::kInt);
+  CHK_CONTIG(amax);
+  TORCH_CHECK(amax.is_cuda() && amax.dim() == 3 && amax.size(0) >= x.size(0) && amax.size(2) == 2 &&
+                  y.dim() == 2 && amax.size(1) == y.size(1) / wr,
+              "gemm_decode_argmax: amax [M, N / wr, 2] int32");
+  die::GemmDecodeFuse fz;
+  fz.amax = reinterpret_cast<uint32_t*>(amax.data_ptr<int>());
+  fz.amax_parts = (int)amax.size(1);
+  gemm_decode_impl(y, x, w, tiled ? 32 : 0, wr, kc, 1, true, x, x, x, x, 0.0, fz);
 }
 
 // Tensor-parallel row-parallel projection in ONE launch (decode, mode 3): this rank's K-shard GEMM, the one-shot
@@ -909,7 +935,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("decode_partials", &decode_partials);
   m.def("sample", &sample, py::arg("out"), py::arg("logits"), py::arg("temperature") = py::none(),
         py::arg("top_k") = py::none(), py::arg("top_p") = py::none(), py::arg("seeds") = py::none(),
-        py::arg("steps") = py::none(), py::arg("part") = py::none(), py::arg("cnt") = py::none());
+        py::arg("steps") = py::none(), py::arg("part") = py::none(), py::arg("cnt") = py::none(),
+        py::arg("lm_part") = py::none());
   m.def("copy_blocks", &copy_blocks);
   m.def("move_blocks", &move_blocks);
   m.def("gather_blocks_rows", &gather_blocks_rows);
@@ -918,6 +945,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_gather", &moe_gather);
   m.def("moe_combine", &moe_combine);
   m.def("gemm_decode", &gemm_decode);
+  m.def("gemm_decode_argmax", &gemm_decode_argmax);
   m.def("gemm_decode_car", &gemm_decode_car);
   m.def("rms_row_scale", &rms_row_scale);
   m.def("gd_set_timestamps", &gd_set_timestamps);

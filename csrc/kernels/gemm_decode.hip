@@ -542,6 +542,68 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
     }
     return;
   }
+  if constexpr (EPI == 0) {
+    // bf16 Y in whole 16-byte pieces: CPW lanes per row, 8 columns each (a row's piece of the tile is one
+    // contiguous 2 * NO-byte run per wave instruction). With fz.amax each row's greedy candidate of the tile
+    // (the LM head's share of the step's argmax) is taken over the same rounded values on the way out: ascending
+    // columns within a lane (strict >: the lowest column of a tie), then (value, lower column) across its lanes;
+    // NaN never wins.
+    constexpr int CPW = NO / 8;      // lanes per row (4, 8 or 16)
+    constexpr int RPI = NTH / CPW;   // rows per pass
+    if (((reinterpret_cast<uintptr_t>(Yv) | (uintptr_t)(ldy * 2)) & 15) == 0) {
+      const int q = tid % CPW;
+#pragma unroll 1
+      for (int m0 = 0; m0 < RR; m0 += RPI) {
+        const int m = m0 + tid / CPW;
+        const bool live = m < M && m < RR;
+        float v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = 0.f;
+        if (live) {
+#pragma unroll
+          for (int w = 0; w < NRED; ++w) {
+            const f4 a = *reinterpret_cast<const f4*>(red + (w * RR + m) * WR + 8 * q);
+            const f4 b = *reinterpret_cast<const f4*>(red + (w * RR + m) * WR + 8 * q + 4);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              v[c] += a[c];
+              v[4 + c] += b[c];
+            }
+          }
+          const uint4 o = pack8(v);
+          *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(Yv) + (int64_t)m * ldy + n0 + 8 * q) = o;
+          unpack8(o, v);  // the rounded values, for the candidate
+        }
+        if (fz.amax != nullptr) {
+          float bv = -INFINITY;
+          int bi = 0x7fffffff;
+          if (live) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+              if (v[c] > bv) {
+                bv = v[c];
+                bi = n0 + 8 * q + c;
+              }
+          }
+#pragma unroll
+          for (int o = 1; o < CPW; o <<= 1) {
+            const float ov = __shfl_xor(bv, o, 64);
+            const int oi = __shfl_xor(bi, o, 64);
+            if (ov > bv || (ov == bv && oi < bi)) {
+              bv = ov;
+              bi = oi;
+            }
+          }
+          if (q == 0 && live) {
+            uint32_t* p = fz.amax + ((int64_t)m * fz.amax_parts + bx) * 2;
+            p[0] = __float_as_uint(bv);
+            p[1] = (uint32_t)bi;
+          }
+        }
+      }
+      return;
+    }
+  }
   for (int e = tid; e < RR * NO; e += NTH) {
     const int m = e / NO, j = e % NO;
     if (m >= M) continue;
@@ -563,6 +625,41 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
       reinterpret_cast<float*>(Yv)[((int64_t)by * M + m) * ldy + n0 + j] = v;
     else
       reinterpret_cast<bf16_t*>(Yv)[(int64_t)m * ldy + n0 + j] = f2bf(v);
+  }
+  if constexpr (EPI == 0) {
+    if (fz.amax != nullptr) {
+      // unaligned Y (the scalar stores above): the candidates from a second pass over the partials
+      constexpr int TPR = NTH / RR;
+      const int m = tid / TPR, q = tid % TPR;
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+      if (m < M) {
+        for (int j = q; j < NO; j += TPR) {
+          float v = 0.f;
+#pragma unroll
+          for (int w = 0; w < NRED; ++w) v += red[(w * RR + m) * WR + j];
+          const float z = bf2f(f2bf(v));
+          if (z > bv) {
+            bv = z;
+            bi = n0 + j;
+          }
+        }
+      }
+#pragma unroll
+      for (int o = 1; o < TPR; o <<= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov > bv || (ov == bv && oi < bi)) {
+          bv = ov;
+          bi = oi;
+        }
+      }
+      if (q == 0 && m < M) {
+        uint32_t* p = fz.amax + ((int64_t)m * fz.amax_parts + bx) * 2;
+        p[0] = __float_as_uint(bv);
+        p[1] = (uint32_t)bi;
+      }
+    }
   }
 }
 

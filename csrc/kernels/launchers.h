@@ -71,7 +71,7 @@ constexpr int SAMPLE_MAX_SPLITS = 16;
 hipError_t launch_sample(int64_t* out, const bf16_t* logits, int64_t stride, int rows, int vocab,
                          const float* temperature, const int* top_k, const float* top_p, const int64_t* seeds,
                          const int64_t* steps, hipStream_t s, uint32_t* part = nullptr, int* cnt = nullptr,
-                         int splits = 1);
+                         int splits = 1, const uint32_t* lm_part = nullptr, int lm_parts = 0);
 
 hipError_t launch_topk_softmax(float* w, int* ids, const bf16_t* gating, int T, int E, int K, bool renorm,
                                hipStream_t s);
@@ -126,6 +126,10 @@ struct GemmDecodeFuse {
   float* slab6 = nullptr;        // mode 6: split-K (gate, up) partials [sk][M][ld_slab6 = 2 N_out]
   int64_t ld_slab6 = 0;
   long long* ts = nullptr;       // diagnostics: per-workgroup [start, end, xcc] s_memrealtime stamps (or null)
+  // mode 0: each column tile's per-row greedy candidate (max of the bf16-rounded outputs, lowest column on ties) as
+  // (value bits, column) pairs [M][amax_parts][2] — the LM head's share of the decode step's argmax (sampling.hip)
+  uint32_t* amax = nullptr;
+  int amax_parts = 0;
   // mode 3 under tensor parallelism (car_world >= 2): the column tile's last arriver rounds its K-shard partial
   // to bf16, exchanges it with the group's peers one-shot (allreduce.hip's protocol, flag slot = tile) and adds
   // the rank-ordered sum into the residual — row-parallel GEMM + all-reduce + residual + statistics, one launch

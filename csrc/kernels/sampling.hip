@@ -137,7 +137,8 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
                                                      const int* __restrict__ top_k, const float* __restrict__ top_p,
                                                      const int64_t* __restrict__ seeds,
                                                      const int64_t* __restrict__ steps, uint32_t* __restrict__ part,
-                                                     int* __restrict__ cnt) {
+                                                     int* __restrict__ cnt, const uint32_t* __restrict__ lm_part,
+                                                     int lm_parts) {
   __shared__ ArgMax red[SNT / 64];
   __shared__ float redf[SNT / 64];
   __shared__ float hist[256];
@@ -149,6 +150,20 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
   const float p = top_p ? top_p[r] : 1.f;
   const bool greedy = temp <= 0.f || k == 1;
 
+  if (lm_part != nullptr && greedy) {
+    // the LM head wrote each column tile's (max, lowest column) of this row (gemm_decode mode 0 with fz.amax):
+    // reduce lm_parts candidates (8 B each) instead of re-reading the 128K-entry row
+    if (sp != 0) return;
+    ArgMax best{-INFINITY, 0x7fffffff};
+    const uint32_t* pr = lm_part + (int64_t)r * lm_parts * 2;
+    for (int i = threadIdx.x; i < lm_parts; i += SNT) {
+      const uint2 c = *reinterpret_cast<const uint2*>(pr + 2 * i);
+      best = better(best, ArgMax{__uint_as_float(c.x), (int)c.y});
+    }
+    best = block_argmax(best, red);
+    if (threadIdx.x == 0) out[r] = best.i < vocab ? best.i : 0;
+    return;
+  }
   if (splits > 1) {
     if (!greedy && sp != 0) return;
     if (greedy) {
@@ -237,12 +252,16 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
 
 hipError_t launch_sample(int64_t* out, const bf16_t* logits, int64_t stride, int rows, int vocab,
                          const float* temperature, const int* top_k, const float* top_p, const int64_t* seeds,
-                         const int64_t* steps, hipStream_t s, uint32_t* part, int* cnt, int splits) {
+                         const int64_t* steps, hipStream_t s, uint32_t* part, int* cnt, int splits,
+                         const uint32_t* lm_part, int lm_parts) {
   if (rows == 0) return hipSuccess;
   if (vocab % 8 || splits < 1 || splits > SAMPLE_MAX_SPLITS || (splits > 1 && (part == nullptr || cnt == nullptr)))
     return hipErrorInvalidValue;
+  if (lm_part != nullptr && lm_parts < 1) return hipErrorInvalidValue;
+  // with the LM head's candidates a greedy row is one short reduction: no split (a sampled row is whole anyway)
+  if (lm_part != nullptr) splits = 1;
   hipLaunchKernelGGL(sample_kernel, dim3(rows, splits), dim3(SNT), 0, s, out, logits, stride, vocab, temperature,
-                     top_k, top_p, seeds, steps, part, cnt);
+                     top_k, top_p, seeds, steps, part, cnt, lm_part, lm_parts);
   return hipGetLastError();
 }
 

@@ -134,8 +134,12 @@ class ModelRunner:
             self.attn_cnt = torch.zeros(self.max_seqs * model.hkv, dtype=i32, device=dev)
             self.dec_scratch = (model.alloc_decode_scratch(self.max_seqs) if hasattr(model, "alloc_decode_scratch")
                                 else None)
+            # the LM head's per-column-tile greedy candidates (CausalLM.compute_logits(argmax_parts=...)): a greedy
+            # row's argmax reduces those instead of re-reading its 128K logits (decode steps of <= 128 rows)
+            parts = model.lm_head_argmax_parts() if hasattr(model, "lm_head_argmax_parts") else 0
+            self.d_lmpart = torch.zeros(self.max_seqs, parts, 2, dtype=i32, device=dev) if parts else None
         else:
-            self.part_o = self.part_ml = self.attn_cnt = self.dec_scratch = None
+            self.part_o = self.part_ml = self.attn_cnt = self.dec_scratch = self.d_lmpart = None
         self.supports_swap = type(self)._sync_step is ModelRunner._sync_step
         self.supports_multistep = self.is_cuda and self.k_max > 1 and type(self)._sync_step is ModelRunner._sync_step
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
@@ -271,12 +275,15 @@ class ModelRunner:
                             ctx_lens=self.d_ctx[:n], max_ctx=self.max_model_len, part_o=self.part_o,
                             part_ml=self.part_ml, attn_cnt=self.attn_cnt, scratch=self.dec_scratch)
         hidden = self.model.forward(self.d_ids[:n], self.d_pos[:n], meta, self.pool.tensor)
-        logits = self.model.compute_logits(hidden)
+        amax = self.d_lmpart if self.d_lmpart is not None and n <= ops.DECODE_GEMM_MAX_M else None
+        logits = self.model.compute_logits(hidden, argmax_parts=amax) if amax is not None else \
+            self.model.compute_logits(hidden)
         if not self.is_cuda:
             return ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
                               self.d_step[:n])
         out = ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
-                         self.d_step[:n], out=self.d_out[:n], scratch=self.d_samp)
+                         self.d_step[:n], out=self.d_out[:n], scratch=self.d_samp,
+                         lm_part=amax[:n] if amax is not None else None)
         if self.supports_multistep:
             # next step's inputs from this step's samples, on the device (multi-step windows)
             ops.decode_advance(self.d_out, self.d_ids, self.d_pos, self.d_ctx, self.d_slots, self.d_bt, self.d_step,

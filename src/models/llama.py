@@ -756,10 +756,21 @@ class CausalLM:
         t = lw.tiled.get((name, wr, kc))
         return ops.linear(x, getattr(lw, name)) if t is None else ops.linear_tiled(x, t, wr, kc)
 
-    def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
+    def lm_head_argmax_parts(self) -> int:
+        """Greedy candidates per row the LM head writes with its logits (one per column tile; 0: it cannot — the
+        head is not in tile order, or is split over a TP group's vocabulary)."""
+        if self.lm_head_tile is None or self.vocab_parallel:
+            return 0
+        return self.lm_head.shape[0] // self.lm_head_tile[0]
+
+    def compute_logits(self, hidden: torch.Tensor, argmax_parts: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """argmax_parts [>= rows, lm_head_argmax_parts(), 2] int32 (decode steps, <= 128 rows): also filled with the
+        LM head's per-column-tile greedy candidates, which ops.sample(lm_part=...) reduces for greedy rows."""
         if self.lm_head_tile is not None and hidden.shape[0] > 0:  # tile order: the decode GEMM, <= 128 rows
             wr, kc = self.lm_head_tile
             mx = ops.DECODE_GEMM_MAX_M
+            if argmax_parts is not None and hidden.shape[0] <= mx and not self.vocab_parallel:
+                return ops.linear_tiled_argmax(hidden, self.lm_head, wr, kc, argmax_parts[:hidden.shape[0]])
             logits = (ops.linear_tiled(hidden, self.lm_head, wr, kc) if hidden.shape[0] <= mx else
                       torch.cat([ops.linear_tiled(hidden[i:i + mx], self.lm_head, wr, kc)
                                  for i in range(0, hidden.shape[0], mx)]))

@@ -196,16 +196,17 @@ def decode_advance(out, ids, pos, ctx, slots, bt, step, tokens, cnt, n_real, row
 
 
 def sample(logits, temperature=None, top_k=None, top_p=None, seeds=None, steps=None,
-           out: Optional[torch.Tensor] = None, scratch=None) -> torch.Tensor:
+           out: Optional[torch.Tensor] = None, scratch=None, lm_part: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``scratch`` = (part int32 [>= rows * 32], cnt int32 [>= rows], zero): greedy rows are split over several
     workgroups each (a decode step's argmax on ~256 CUs instead of one per row); keep it for the engine's life
-    (the tickets are re-armed by the kernel, so it is graph-capturable)."""
+    (the tickets are re-armed by the kernel, so it is graph-capturable). ``lm_part`` [rows, parts, 2] int32: the
+    LM head's per-column-tile candidates (:func:`linear_tiled_argmax`) — greedy rows reduce those instead."""
     if not logits.is_cuda:
         return ref.sample(logits, temperature, top_k, top_p, seeds, steps)
     if out is None:
         out = torch.empty(logits.shape[0], dtype=torch.long, device=logits.device)
     part, cnt = scratch if scratch is not None else (None, None)
-    _kern().sample(out, logits, temperature, top_k, top_p, seeds, steps, part, cnt)
+    _kern().sample(out, logits, temperature, top_k, top_p, seeds, steps, part, cnt, lm_part)
     return out
 
 
@@ -622,6 +623,14 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
 def linear_tiled(x: torch.Tensor, w: torch.Tensor, wr: int, kc: int) -> torch.Tensor:
     """y = x @ w^T (bf16, decode sizes) with w packed by gd_pack_weights for the (wr, kc) tile."""
     return gemm_decode(x, w, 0 | 32, wr, 1, kc=kc)
+
+
+def linear_tiled_argmax(x: torch.Tensor, w: torch.Tensor, wr: int, kc: int, amax: torch.Tensor) -> torch.Tensor:
+    """linear_tiled that also writes every wr-column tile's per-row greedy candidate (max of the bf16 outputs,
+    lowest column on ties) into amax [M, N / wr, 2] int32 — the LM head's share of a decode step's argmax."""
+    out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
+    _kern().gemm_decode_argmax(out, x, w, wr, kc, True, amax)
+    return out
 
 
 def linear_slab(x: torch.Tensor, w: torch.Tensor, sk: Optional[int] = None, wr: Optional[int] = None,

@@ -809,3 +809,40 @@ def test_prefill_gemm_table_loads_and_matches_fp32(dev):
     w = (torch.randn(6144, 4096, device=dev) * 0.02).to(torch.bfloat16)
     y = torch.nn.functional.linear(x, w)
     close(y, x.float() @ w.float().t(), atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("m", [1, 7, 32, 128])
+@pytest.mark.parametrize("n,wr,kc", [(128256, 128, 128), (32000, 64, 128)])
+def test_lm_head_argmax_candidates(dev, m, n, wr, kc):
+    """The decode LM head with per-column-tile greedy candidates (ops.linear_tiled_argmax): the same logits bit
+    for bit as the plain tiled GEMM, and the candidates reduce (ops.sample(lm_part=...)) to torch.argmax of those
+    logits — lowest index on a tie (rows 100 and n - 900 are made identical and dominant for every token);
+    sampled rows (temperature > 0) ignore the candidates and draw exactly as without them."""
+    k = 4096
+    g = torch.Generator(device=dev).manual_seed(m + n)
+    x = torch.randn(m, k, device=dev, generator=g).abs().to(torch.bfloat16)
+    w = (torch.randn(n, k, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+    w[100] = 0.05
+    w[n - 900] = 0.05
+    wt = ops.gd_pack_weights(w, wr, kc=kc)
+    parts = torch.zeros(m, n // wr, 2, dtype=torch.int32, device=dev)
+    y = ops.linear_tiled_argmax(x, wt, wr, kc, parts)
+    assert torch.equal(y, ops.linear_tiled(x, wt, wr, kc))
+    want = torch.argmax(y.float(), dim=-1)
+    assert bool((want == 100).all())
+    got = ops.sample(y, lm_part=parts)
+    assert torch.equal(got, want)
+    # without the tie: the plain argmax of random logits, and candidates = per-tile maxima
+    w[100] = w[101]
+    w[n - 900] = w[n - 901]
+    wt = ops.gd_pack_weights(w, wr, kc=kc)
+    y = ops.linear_tiled_argmax(x, wt, wr, kc, parts)
+    assert torch.equal(ops.sample(y, lm_part=parts), torch.argmax(y.float(), dim=-1))
+    tiles = y.float().view(m, n // wr, wr)
+    assert torch.equal(parts[..., 0].view(torch.float32), tiles.max(-1).values)
+    assert torch.equal(parts[..., 1].long(), tiles.argmax(-1) + torch.arange(0, n, wr, device=dev))
+    temp = torch.full((m,), 0.8, device=dev)
+    seeds = torch.arange(m, device=dev, dtype=torch.long)
+    steps = torch.zeros(m, device=dev, dtype=torch.long)
+    assert torch.equal(ops.sample(y, temp, seeds=seeds, steps=steps, lm_part=parts),
+                       ops.sample(y, temp, seeds=seeds, steps=steps))
