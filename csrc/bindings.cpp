@@ -587,8 +587,8 @@ void gemm_decode_argmax(Tensor y, Tensor x, Tensor w, int64_t wr, int64_t kc, bo
   CHK_DTYPE(amax, at::kInt);
   CHK_CONTIG(amax);
   TORCH_CHECK(amax.is_cuda() && amax.dim() == 3 && amax.size(0) >= x.size(0) && amax.size(2) == 2 &&
-                  y.dim() == 2 && amax.size(1) == y.size(1) / wr,
-              "gemm_decode_argmax: amax [M, N / wr, 2] int32");
+                  y.dim() == 2 && amax.size(1) == y.size(1) / wr && y.is_contiguous() && y.size(1) % 8 == 0,
+              "gemm_decode_argmax: amax [M, N / wr, 2] int32 with a contiguous y of N % 8 == 0 columns");
   die::GemmDecodeFuse fz;
   fz.amax = reinterpret_cast<uint32_t*>(amax.data_ptr<int>());
   fz.amax_parts = (int)amax.size(1);

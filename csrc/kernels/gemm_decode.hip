@@ -626,41 +626,6 @@ __device__ __forceinline__ void gd_body(char* smem, void* Yv, int64_t ldy, const
     else
       reinterpret_cast<bf16_t*>(Yv)[(int64_t)m * ldy + n0 + j] = f2bf(v);
   }
-  if constexpr (EPI == 0) {
-    if (fz.amax != nullptr) {
-      // unaligned Y (the scalar stores above): the candidates from a second pass over the partials
-      constexpr int TPR = NTH / RR;
-      const int m = tid / TPR, q = tid % TPR;
-      float bv = -INFINITY;
-      int bi = 0x7fffffff;
-      if (m < M) {
-        for (int j = q; j < NO; j += TPR) {
-          float v = 0.f;
-#pragma unroll
-          for (int w = 0; w < NRED; ++w) v += red[(w * RR + m) * WR + j];
-          const float z = bf2f(f2bf(v));
-          if (z > bv) {
-            bv = z;
-            bi = n0 + j;
-          }
-        }
-      }
-#pragma unroll
-      for (int o = 1; o < TPR; o <<= 1) {
-        const float ov = __shfl_xor(bv, o, 64);
-        const int oi = __shfl_xor(bi, o, 64);
-        if (ov > bv || (ov == bv && oi < bi)) {
-          bv = ov;
-          bi = oi;
-        }
-      }
-      if (q == 0 && m < M) {
-        uint32_t* p = fz.amax + ((int64_t)m * fz.amax_parts + bx) * 2;
-        p[0] = __float_as_uint(bv);
-        p[1] = (uint32_t)bi;
-      }
-    }
-  }
 }
 
 template <int WR, int EPI, int S, bool NT, int KC, int XR, int SKC = 0>
@@ -767,6 +732,7 @@ static hipError_t launch_modes(void* Y, int64_t ldy, const bf16_t* X, int64_t ld
 //         its weight folded into W);
 // mode 6: mode 4 split over sk K slices: fp32 partials in fz.slab6 [sk][M][2 N], the tile's last arriver
 //         finishes (fz.counters [N / (wr / 2)] tickets, zero, re-armed).
+// fz.amax (mode 0, 16-byte aligned Y rows): per-tile greedy candidates [M][N / wr][2].
 // (wr, kc): weight rows per workgroup and K elements per ring slot (gemm_decode_tile_ok), so that
 // (N / columns) * sk can be made a multiple of the CU count for the model's shapes (e.g. 8B gate/up:
 // 14336 / 56 = 256 workgroups at wr = 112). Small K slots (64 / 32) are for M > 32: they keep the
@@ -776,6 +742,9 @@ hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx
                               hipStream_t s) {
   if (M <= 0) return hipSuccess;
   if (M > 128 || sk < 1 || (mode != 2 && mode != 3 && mode != 6 && sk != 1)) return hipErrorInvalidValue;
+  if (fz.amax != nullptr && (mode != 0 || fz.amax_parts < 1 ||
+                             ((reinterpret_cast<uintptr_t>(Y) | (uintptr_t)(ldy * 2)) & 15)))
+    return hipErrorInvalidValue;  // candidates come with mode 0's 16-byte store path
   if ((mode == 4 || mode == 6) &&
       (fz.ssp_in == nullptr || fz.ssp_tiles < 1 ||
        fz.ssp_tiles > (M <= 32 ? DECODE_SSP_MAX_TILES : DECODE_SSP_MAX_TILES_WIDE)))

@@ -7,7 +7,7 @@ R=$GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_kernels_gpu.py -k "argmax or sample or gemm_decode or tiled or grouped or moe" > gpurun_out/r5_lmarg_tests.log 2>&1 || { tail -40 gpurun_out/r5_lmarg_tests.log; exit 1; }
 tail -1 gpurun_out/r5_lmarg_tests.log
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_engine_gpu.py tests/test_oracle_gpu.py > gpurun_out/r5_lmarg_tests2.log 2>&1 || { tail -40 gpurun_out/r5_lmarg_tests2.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_engine_gpu.py tests/test_oracle_gpu.py tests/test_serving_gpu.py tests/test_expert_parallel_gpu.py > gpurun_out/r5_lmarg_tests2.log 2>&1 || { tail -40 gpurun_out/r5_lmarg_tests2.log; exit 1; }
 tail -1 gpurun_out/r5_lmarg_tests2.log
 timeout -k 10 120 python -u bench/micro_lm_head_argmax.py > gpurun_out/r5_lmarg_micro.jsonl 2>&1 || { tail -5 gpurun_out/r5_lmarg_micro.jsonl; exit 2; }
 cat gpurun_out/r5_lmarg_micro.jsonl
