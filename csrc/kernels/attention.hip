@@ -759,28 +759,32 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
   if (head_dim != D || hq % hkv || block_size % 16) return hipErrorInvalidValue;
   const int G = hq / hkv;
   const float sl2 = scale * 1.4426950408889634f;
-  constexpr int NW = 8;  // one 512-thread workgroup per CU (two 4-wave workgroups measured slower, round 2)
-  const int tpb = NW * (32 / (G > 32 ? 32 : G));
-  dim3 grid((max_q_len + tpb - 1) / tpb, num_seqs, hkv), block(64 * NW);
-  const size_t lds = 2 * 2 * KV_TILE;
-#define PF_CASE(GG)                                                                                            \
-  case GG:                                                                                                     \
-    hipLaunchKernelGGL((attn_prefill_kernel<GG, 2, NW>), grid, block, lds, s, out, q, q_stride, k_cache,       \
+  // NW waves x NS 32-key sub-tiles per stage: one 512-thread workgroup per CU with 64-key stages for prompts
+  // above 256 tokens (4 x 4,096: 708 vs 797 us for (4, 1)); two 256-thread workgroups per CU with 32-key stages
+  // for short ones, where more, shorter q tiles fill the chip (64 x 256: 119 vs 132 us; 32 x 512 within 1.5 %:
+  // profiles/r5_prefill_attn_nw_ns.jsonl)
+  const bool short_q = max_q_len <= 256;
+  const int NWr = short_q ? 4 : 8, NSr = short_q ? 1 : 2;
+  const int tpb = NWr * (32 / (G > 32 ? 32 : G));
+  dim3 grid((max_q_len + tpb - 1) / tpb, num_seqs, hkv), block(64 * NWr);
+  const size_t lds = std::max<size_t>(2 * NSr * KV_TILE, (size_t)NWr * 32 * 272);  // ring / O staging
+#define PF_CASE2(GG, NS_, NW_)                                                                                 \
+  if (G == GG && NSr == NS_ && NWr == NW_) {                                                                  \
+    hipLaunchKernelGGL((attn_prefill_kernel<GG, NS_, NW_>), grid, block, lds, s, out, q, q_stride, k_cache,    \
                        v_cache, block_tables, bt_stride, cu_q, ctx_lens, hq, hkv, block_size, sl2, cos_sin, n_pos, \
                        q_scale);                                                                               \
-    break;
-  switch (G) {
-    PF_CASE(1)
-    PF_CASE(2)
-    PF_CASE(4)
-    PF_CASE(8)
-    PF_CASE(16)
-    PF_CASE(32)
-    default:
-      return hipErrorInvalidValue;
+    return hipGetLastError();                                                                                  \
   }
+#define PF_CASE(GG) PF_CASE2(GG, 2, 8) PF_CASE2(GG, 1, 4)
+  PF_CASE(1)
+  PF_CASE(2)
+  PF_CASE(4)
+  PF_CASE(8)
+  PF_CASE(16)
+  PF_CASE(32)
+  return hipErrorInvalidValue;
 #undef PF_CASE
-  return hipGetLastError();
+#undef PF_CASE2
 }
 
 static long long* g_attn_ts = nullptr;
