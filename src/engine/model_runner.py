@@ -275,7 +275,8 @@ class ModelRunner:
                             ctx_lens=self.d_ctx[:n], max_ctx=self.max_model_len, part_o=self.part_o,
                             part_ml=self.part_ml, attn_cnt=self.attn_cnt, scratch=self.dec_scratch)
         hidden = self.model.forward(self.d_ids[:n], self.d_pos[:n], meta, self.pool.tensor)
-        amax = self.d_lmpart if self.d_lmpart is not None and n <= ops.DECODE_GEMM_MAX_M else None
+        amax = (self.d_lmpart if self.d_lmpart is not None and n <= ops.DECODE_GEMM_MAX_M
+                and self.model.lm_head_argmax_parts() == self.d_lmpart.shape[1] else None)
         logits = self.model.compute_logits(hidden, argmax_parts=amax) if amax is not None else \
             self.model.compute_logits(hidden)
         if not self.is_cuda:

@@ -766,11 +766,14 @@ class CausalLM:
     def compute_logits(self, hidden: torch.Tensor, argmax_parts: Optional[torch.Tensor] = None) -> torch.Tensor:
         """argmax_parts [>= rows, lm_head_argmax_parts(), 2] int32 (decode steps, <= 128 rows): also filled with the
         LM head's per-column-tile greedy candidates, which ops.sample(lm_part=...) reduces for greedy rows."""
+        if argmax_parts is not None:  # the caller's argmax reads these candidates: never leave them stale
+            if not (self.lm_head_argmax_parts() == argmax_parts.shape[1] and 0 < hidden.shape[0] <= ops.DECODE_GEMM_MAX_M):
+                raise ValueError("LM-head argmax candidates requested where the head cannot write them")
+            wr, kc = self.lm_head_tile
+            return ops.linear_tiled_argmax(hidden, self.lm_head, wr, kc, argmax_parts[:hidden.shape[0]])
         if self.lm_head_tile is not None and hidden.shape[0] > 0:  # tile order: the decode GEMM, <= 128 rows
             wr, kc = self.lm_head_tile
             mx = ops.DECODE_GEMM_MAX_M
-            if argmax_parts is not None and hidden.shape[0] <= mx and not self.vocab_parallel:
-                return ops.linear_tiled_argmax(hidden, self.lm_head, wr, kc, argmax_parts[:hidden.shape[0]])
             logits = (ops.linear_tiled(hidden, self.lm_head, wr, kc) if hidden.shape[0] <= mx else
                       torch.cat([ops.linear_tiled(hidden[i:i + mx], self.lm_head, wr, kc)
                                  for i in range(0, hidden.shape[0], mx)]))

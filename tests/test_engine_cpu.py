@@ -325,3 +325,18 @@ def test_always_mixed_does_not_starve_prompts_behind_a_large_decode_batch():
     while eng.has_work():
         eng.step()
     assert eng.get_stats()["kv"]["used"] == 0
+
+
+def test_lm_head_argmax_candidates_are_never_left_stale():
+    """compute_logits(argmax_parts=...) promises per-tile greedy candidates that the sampler reads instead of the
+    logits; a head that cannot write them (row-major here: not in tile order) must refuse loudly, and it reports
+    zero candidate tiles so the runner never asks."""
+    from src.models.llama import CausalLM
+    from src.models.presets import get_preset
+
+    m = CausalLM(get_preset("llama-tiny"), "cpu", dtype=torch.float32, seed=1, max_position=256)
+    assert m.lm_head_argmax_parts() == 0
+    h = torch.randn(4, m.arch.hidden_size)
+    with pytest.raises(ValueError):
+        m.compute_logits(h, argmax_parts=torch.zeros(4, 8, 2, dtype=torch.int32))
+    assert m.compute_logits(h).shape == (4, m.arch.vocab_size)
