@@ -342,6 +342,52 @@ void sample(Tensor out, Tensor logits, c10::optional<Tensor> temperature, c10::o
                              lp, lparts));
 }
 
+// A decode step's sampling from the LM head's candidates (sample(..., lm_part)) that also advances the step's
+// inputs as decode_advance does (ids / pos / ctx / slots / step, the window's token row, the step counter cnt[0]),
+// one workgroup per row; ticket: int32 [1], zero, re-armed by the kernel.
+void sample_advance(Tensor out, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds,
+                    Tensor lm_part, Tensor ids, Tensor pos, Tensor ctx, Tensor slots, Tensor bt, Tensor step,
+                    Tensor tokens, Tensor cnt, Tensor n_real, int64_t block_size, Tensor ticket) {
+  CHK_CUDA(logits);
+  CHK_BF16(logits);
+  check_rows(logits, "logits");
+  const int64_t rows = logits.size(0);
+  for (const Tensor* t : {&out, &ids, &pos, &slots, &step, &tokens, &seeds}) CHK_DTYPE((*t), at::kLong);
+  for (const Tensor* t : {&ctx, &bt, &cnt, &n_real, &ticket, &top_k, &lm_part}) CHK_DTYPE((*t), at::kInt);
+  CHK_DTYPE(temperature, at::kFloat);
+  CHK_DTYPE(top_p, at::kFloat);
+  CHK_CONTIG(bt);
+  CHK_CONTIG(tokens);
+  CHK_CONTIG(lm_part);
+  TORCH_CHECK(logits.size(1) % 8 == 0 && lm_part.dim() == 3 && lm_part.size(0) >= rows && lm_part.size(2) == 2,
+              "sample_advance: vocab % 8, lm_part [rows, parts, 2]");
+  TORCH_CHECK(rows <= out.numel() && rows <= ids.numel() && rows <= pos.numel() && rows <= ctx.numel() &&
+                  rows <= slots.numel() && rows <= step.numel() && rows <= seeds.numel() && rows <= temperature.numel() &&
+                  rows <= top_k.numel() && rows <= top_p.numel() && bt.dim() == 2 && rows <= bt.size(0) &&
+                  tokens.dim() == 2 && rows <= tokens.size(1) && cnt.numel() >= 1 && n_real.numel() >= 1 &&
+                  ticket.numel() >= 1,
+              "sample_advance: buffers smaller than rows");
+  die::SampleAdvance adv;
+  adv.ids = ids.data_ptr<int64_t>();
+  adv.pos = pos.data_ptr<int64_t>();
+  adv.ctx = ctx.data_ptr<int>();
+  adv.slots = slots.data_ptr<int64_t>();
+  adv.bt = bt.data_ptr<int>();
+  adv.bt_width = (int)bt.size(1);
+  adv.step = step.data_ptr<int64_t>();
+  adv.tokens = tokens.data_ptr<int64_t>();
+  adv.tok_stride = (int)tokens.size(1);
+  adv.k_max = (int)tokens.size(0);
+  adv.cnt = cnt.data_ptr<int>();
+  adv.n_real = n_real.data_ptr<int>();
+  adv.bs = (int)block_size;
+  adv.ticket = ticket.data_ptr<int>();
+  HIP_OK(die::launch_sample(out.data_ptr<int64_t>(), bf(logits), logits.stride(0), (int)rows, (int)logits.size(1),
+                             temperature.data_ptr<float>(), top_k.data_ptr<int>(), top_p.data_ptr<float>(),
+                             seeds.data_ptr<int64_t>(), step.data_ptr<int64_t>(), cur_stream(), nullptr, nullptr, 1,
+                             reinterpret_cast<const uint32_t*>(lm_part.data_ptr<int>()), (int)lm_part.size(1), adv));
+}
+
 // pool viewed as [planes, num_blocks, slab]
 void copy_blocks(Tensor pool, Tensor pairs) {
   CHK_CUDA(pool);
@@ -938,6 +984,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("steps") = py::none(), py::arg("part") = py::none(), py::arg("cnt") = py::none(),
         py::arg("lm_part") = py::none());
   m.def("copy_blocks", &copy_blocks);
+  m.def("sample_advance", &sample_advance);
   m.def("move_blocks", &move_blocks);
   m.def("gather_blocks_rows", &gather_blocks_rows);
   m.def("topk_softmax", &topk_softmax);

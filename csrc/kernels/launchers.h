@@ -68,10 +68,30 @@ int attn_decode_max_partials(int max_ctx);
 // splits > 1: greedy rows are argmax'ed by `splits` workgroups each (part [rows][splits][2] u32 scratch, cnt [rows]
 // int32 tickets, zero, re-armed by the kernel)
 constexpr int SAMPLE_MAX_SPLITS = 16;
+// the decode step's input advance (decode_step.hip) done by the sampling kernel itself: each row's workgroup
+// writes its token into the window's token rows and advances that row's id / position / context / slot / step;
+// the last row to finish (agent-scope ticket, re-armed) bumps the window's step counter
+struct SampleAdvance {
+  int64_t* ids = nullptr;  // null: no advance
+  int64_t* pos = nullptr;
+  int* ctx = nullptr;
+  int64_t* slots = nullptr;
+  const int* bt = nullptr;
+  int bt_width = 0;
+  int64_t* step = nullptr;
+  int64_t* tokens = nullptr;
+  int tok_stride = 0;
+  int k_max = 0;
+  int* cnt = nullptr;
+  const int* n_real = nullptr;
+  int bs = 16;
+  int* ticket = nullptr;
+};
 hipError_t launch_sample(int64_t* out, const bf16_t* logits, int64_t stride, int rows, int vocab,
                          const float* temperature, const int* top_k, const float* top_p, const int64_t* seeds,
                          const int64_t* steps, hipStream_t s, uint32_t* part = nullptr, int* cnt = nullptr,
-                         int splits = 1, const uint32_t* lm_part = nullptr, int lm_parts = 0);
+                         int splits = 1, const uint32_t* lm_part = nullptr, int lm_parts = 0,
+                         const SampleAdvance& adv = SampleAdvance{});
 
 hipError_t launch_topk_softmax(float* w, int* ids, const bf16_t* gating, int T, int E, int K, bool renorm,
                                hipStream_t s);

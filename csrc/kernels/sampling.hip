@@ -138,13 +138,36 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
                                                      const int64_t* __restrict__ seeds,
                                                      const int64_t* __restrict__ steps, uint32_t* __restrict__ part,
                                                      int* __restrict__ cnt, const uint32_t* __restrict__ lm_part,
-                                                     int lm_parts) {
+                                                     int lm_parts, SampleAdvance adv) {
   __shared__ ArgMax red[SNT / 64];
   __shared__ float redf[SNT / 64];
   __shared__ float hist[256];
   __shared__ uint32_t sh[2];
   const int r = blockIdx.x, splits = gridDim.y, sp = blockIdx.y;
   const bf16_t* row = logits + (int64_t)r * stride;
+  // thread 0: out[r] = t and (adv.ids) this row's share of the step's input advance (decode_advance_kernel)
+  auto finish = [&](int64_t t) {
+    out[r] = t;
+    if (adv.ids == nullptr) return;
+    const int k = __hip_atomic_load(adv.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int n = adv.n_real[0];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // k is read before this row's ticket below
+    if (k < adv.k_max) adv.tokens[(int64_t)k * adv.tok_stride + r] = t;
+    if (r < n) {
+      adv.ids[r] = t;
+      const int64_t p = adv.pos[r] + 1;
+      adv.pos[r] = p;
+      adv.ctx[r] += 1;
+      const int b = (int)(p / adv.bs);
+      adv.slots[r] = b < adv.bt_width ? (int64_t)adv.bt[(int64_t)r * adv.bt_width + b] * adv.bs + p % adv.bs : -1;
+      adv.step[r] += 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (__hip_atomic_fetch_add(adv.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+      __hip_atomic_store(adv.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(adv.cnt, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
   const float temp = temperature ? temperature[r] : 0.f;
   const int k = top_k ? top_k[r] : 0;
   const float p = top_p ? top_p[r] : 1.f;
@@ -161,7 +184,7 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
       best = better(best, ArgMax{__uint_as_float(c.x), (int)c.y});
     }
     best = block_argmax(best, red);
-    if (threadIdx.x == 0) out[r] = best.i < vocab ? best.i : 0;
+    if (threadIdx.x == 0) finish(best.i < vocab ? best.i : 0);
     return;
   }
   if (splits > 1) {
@@ -209,7 +232,7 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
   // valid token id: an out-of-range id would turn into an out-of-bounds embedding read next step
   if (best.i >= vocab) best.i = 0;
   if (greedy) {
-    if (threadIdx.x == 0) out[r] = best.i;
+    if (threadIdx.x == 0) finish(best.i);
     return;
   }
   const float inv_t = 1.f / temp;
@@ -247,21 +270,24 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
     }
   }
   g = block_argmax(g, red);
-  if (threadIdx.x == 0) out[r] = g.i < vocab ? g.i : best.i;
+  if (threadIdx.x == 0) finish(g.i < vocab ? g.i : best.i);
 }
 
 hipError_t launch_sample(int64_t* out, const bf16_t* logits, int64_t stride, int rows, int vocab,
                          const float* temperature, const int* top_k, const float* top_p, const int64_t* seeds,
                          const int64_t* steps, hipStream_t s, uint32_t* part, int* cnt, int splits,
-                         const uint32_t* lm_part, int lm_parts) {
+                         const uint32_t* lm_part, int lm_parts, const SampleAdvance& adv) {
   if (rows == 0) return hipSuccess;
   if (vocab % 8 || splits < 1 || splits > SAMPLE_MAX_SPLITS || (splits > 1 && (part == nullptr || cnt == nullptr)))
     return hipErrorInvalidValue;
   if (lm_part != nullptr && lm_parts < 1) return hipErrorInvalidValue;
+  // the advance rides on one workgroup per row: only with the LM head's candidates (no split argmax)
+  if (adv.ids != nullptr && (lm_part == nullptr || adv.cnt == nullptr || adv.ticket == nullptr || adv.n_real == nullptr))
+    return hipErrorInvalidValue;
   // with the LM head's candidates a greedy row is one short reduction: no split (a sampled row is whole anyway)
   if (lm_part != nullptr) splits = 1;
   hipLaunchKernelGGL(sample_kernel, dim3(rows, splits), dim3(SNT), 0, s, out, logits, stride, vocab, temperature,
-                     top_k, top_p, seeds, steps, part, cnt, lm_part, lm_parts);
+                     top_k, top_p, seeds, steps, part, cnt, lm_part, lm_parts, adv);
   return hipGetLastError();
 }
 

@@ -126,6 +126,7 @@ class ModelRunner:
                        torch.zeros(self.max_seqs, dtype=torch.int32, device=dev))
         self.d_tokens = torch.zeros(2 * self.k_max, self.max_seqs, dtype=i64, device=dev)
         self.d_ctl = torch.zeros(2, dtype=i32, device=dev)
+        self.d_adv_ticket = torch.zeros(1, dtype=i32, device=dev)  # sample_advance's row ticket (re-armed in-kernel)
         if self.is_cuda:
             maxp = ops.decode_partials(max_model_len)
             hq = model.hq
@@ -282,6 +283,12 @@ class ModelRunner:
         if not self.is_cuda:
             return ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
                               self.d_step[:n])
+        if amax is not None and self.supports_multistep:
+            # sampling from the LM head's candidates and the next step's input advance in one launch
+            return ops.sample_advance(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
+                                      self.d_step, self.d_out[:n], amax[:n], self.d_ids, self.d_pos, self.d_ctx,
+                                      self.d_slots, self.d_bt, self.d_tokens, self.d_ctl[0:1], self.d_ctl[1:2],
+                                      self.bs, self.d_adv_ticket)
         out = ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
                          self.d_step[:n], out=self.d_out[:n], scratch=self.d_samp,
                          lm_part=amax[:n] if amax is not None else None)

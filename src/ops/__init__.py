@@ -210,6 +210,17 @@ def sample(logits, temperature=None, top_k=None, top_p=None, seeds=None, steps=N
     return out
 
 
+def sample_advance(logits, temperature, top_k, top_p, seeds, steps, out, lm_part, ids, pos, ctx, slots, bt, tokens,
+                   cnt, n_real, block_size: int, ticket) -> torch.Tensor:
+    """:func:`sample` from the LM head's candidates (``lm_part``) fused with :func:`decode_advance`: every row's
+    workgroup also writes its token into the window's token row ``cnt[0]`` and advances the row's id / position /
+    context / slot / step (``steps`` is read for the draw, then incremented); the last row bumps ``cnt[0]``.
+    ``ticket``: int32 [1], zero, re-armed by the kernel (graph-capturable)."""
+    _kern().sample_advance(out, logits, temperature, top_k, top_p, seeds, lm_part, ids, pos, ctx, slots, bt, steps,
+                           tokens, cnt, n_real, block_size, ticket)
+    return out
+
+
 def copy_blocks(pool: torch.Tensor, pairs: torch.Tensor) -> None:
     """pool viewed [planes, num_blocks, ...]; pairs [n, 2] int64 (src, dst)."""
     if not pool.is_cuda:

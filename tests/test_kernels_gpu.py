@@ -846,3 +846,46 @@ def test_lm_head_argmax_candidates(dev, m, n, wr, kc):
     steps = torch.zeros(m, device=dev, dtype=torch.long)
     assert torch.equal(ops.sample(y, temp, seeds=seeds, steps=steps, lm_part=parts),
                        ops.sample(y, temp, seeds=seeds, steps=steps))
+
+
+@pytest.mark.parametrize("rows,n_real", [(32, 32), (32, 29), (8, 8)])
+def test_sample_advance_matches_sample_then_advance(dev, rows, n_real):
+    """ops.sample_advance (sampling from the LM head's candidates + the decode step's input advance in one launch)
+    leaves every buffer exactly as ops.sample(lm_part=...) followed by ops.decode_advance: tokens, ids, positions,
+    context lengths, slots, steps, the window's token row and step counter — with greedy and sampled rows, padded
+    rows past n_real, and the row ticket re-armed for the next launch (two steps in a row)."""
+    n, wr, kc, k, bs, width, kmax = 32000, 64, 128, 4096, 16, 8, 8
+    g = torch.Generator(device=dev).manual_seed(rows + n_real)
+    x = torch.randn(rows, k, device=dev, generator=g).to(torch.bfloat16)
+    wt = ops.gd_pack_weights((torch.randn(n, k, device=dev, generator=g) * 0.02).to(torch.bfloat16), wr, kc=kc)
+    parts = torch.zeros(rows, n // wr, 2, dtype=torch.int32, device=dev)
+    logits = ops.linear_tiled_argmax(x, wt, wr, kc, parts)
+    temp = torch.zeros(rows, device=dev)
+    temp[1::3] = 0.7  # some sampled rows
+    topk = torch.zeros(rows, dtype=torch.int32, device=dev)
+    topp = torch.ones(rows, device=dev)
+    seeds = torch.arange(rows, dtype=torch.long, device=dev) + 11
+
+    def state():
+        pos = torch.randint(0, width * bs - 2, (rows,), device=dev, generator=g)
+        return {"ids": torch.zeros(rows, dtype=torch.long, device=dev), "pos": pos,
+                "ctx": (pos + 1).to(torch.int32), "slots": torch.zeros(rows, dtype=torch.long, device=dev),
+                "bt": torch.randint(0, 1000, (rows, width), dtype=torch.int32, device=dev, generator=g),
+                "step": torch.randint(0, 50, (rows,), device=dev, generator=g),
+                "tokens": torch.full((2 * kmax, rows), -1, dtype=torch.long, device=dev),
+                "ctl": torch.tensor([3, n_real], dtype=torch.int32, device=dev),
+                "out": torch.zeros(rows, dtype=torch.long, device=dev)}
+
+    a = state()
+    b = {kk: v.clone() for kk, v in a.items()}
+    ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+    for _ in range(2):
+        ops.sample(logits, temp, topk, topp, seeds, a["step"], out=a["out"], lm_part=parts)
+        ops.decode_advance(a["out"], a["ids"], a["pos"], a["ctx"], a["slots"], a["bt"], a["step"], a["tokens"],
+                           a["ctl"][0:1], a["ctl"][1:2], rows, bs)
+        ops.sample_advance(logits, temp, topk, topp, seeds, b["step"], b["out"], parts, b["ids"], b["pos"], b["ctx"],
+                           b["slots"], b["bt"], b["tokens"], b["ctl"][0:1], b["ctl"][1:2], bs, ticket)
+    torch.cuda.synchronize()
+    for kk in a:
+        assert torch.equal(a[kk], b[kk]), kk
+    assert int(ticket.item()) == 0 and int(b["ctl"][0].item()) == 5
