@@ -347,7 +347,8 @@ void sample(Tensor out, Tensor logits, c10::optional<Tensor> temperature, c10::o
 // one workgroup per row; ticket: int32 [1], zero, re-armed by the kernel.
 void sample_advance(Tensor out, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds,
                     Tensor lm_part, Tensor ids, Tensor pos, Tensor ctx, Tensor slots, Tensor bt, Tensor step,
-                    Tensor tokens, Tensor cnt, Tensor n_real, int64_t block_size, Tensor ticket) {
+                    Tensor tokens, Tensor cnt, Tensor n_real, int64_t block_size, Tensor ticket, Tensor table,
+                    Tensor h_out, Tensor ssp_out) {
   CHK_CUDA(logits);
   CHK_BF16(logits);
   check_rows(logits, "logits");
@@ -382,6 +383,20 @@ void sample_advance(Tensor out, Tensor logits, Tensor temperature, Tensor top_k,
   adv.n_real = n_real.data_ptr<int>();
   adv.bs = (int)block_size;
   adv.ticket = ticket.data_ptr<int>();
+  if (table.numel()) {  // also the next step's embedding rows + first-norm statistics (as embed_sumsq)
+    CHK_BF16(table);
+    CHK_BF16(h_out);
+    CHK_CONTIG(table);
+    CHK_CONTIG(h_out);
+    CHK_DTYPE(ssp_out, at::kFloat);
+    TORCH_CHECK(table.dim() == 2 && table.size(1) % 8 == 0 && h_out.dim() == 2 && h_out.size(0) >= rows &&
+                    h_out.size(1) == table.size(1) && ssp_out.numel() >= rows,
+                "sample_advance: table [V, H], h_out [>= rows, H], ssp_out [>= rows]");
+    adv.table = bf(table);
+    adv.h_out = bf(h_out);
+    adv.ssp_out = ssp_out.data_ptr<float>();
+    adv.hidden = (int)table.size(1);
+  }
   HIP_OK(die::launch_sample(out.data_ptr<int64_t>(), bf(logits), logits.stride(0), (int)rows, (int)logits.size(1),
                              temperature.data_ptr<float>(), top_k.data_ptr<int>(), top_p.data_ptr<float>(),
                              seeds.data_ptr<int64_t>(), step.data_ptr<int64_t>(), cur_stream(), nullptr, nullptr, 1,

@@ -86,6 +86,11 @@ struct SampleAdvance {
   const int* n_real = nullptr;
   int bs = 16;
   int* ticket = nullptr;
+  // optional: the next step's embedding rows and first-norm statistics (embed_sumsq) for the advanced ids
+  const bf16_t* table = nullptr;  // null: no embedding
+  bf16_t* h_out = nullptr;        // [rows, hidden]
+  float* ssp_out = nullptr;       // [>= rows]
+  int hidden = 0;
 };
 hipError_t launch_sample(int64_t* out, const bf16_t* logits, int64_t stride, int rows, int vocab,
                          const float* temperature, const int* top_k, const float* top_p, const int64_t* seeds,

@@ -146,11 +146,13 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
   const int r = blockIdx.x, splits = gridDim.y, sp = blockIdx.y;
   const bf16_t* row = logits + (int64_t)r * stride;
   // thread 0: out[r] = t and (adv.ids) this row's share of the step's input advance (decode_advance_kernel)
+  __shared__ int64_t s_next;  // the row's next input id (for the embedding below)
   auto finish = [&](int64_t t) {
     out[r] = t;
     if (adv.ids == nullptr) return;
     const int k = __hip_atomic_load(adv.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int n = adv.n_real[0];
+    s_next = r < n ? t : adv.ids[r];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // k is read before this row's ticket below
     if (k < adv.k_max) adv.tokens[(int64_t)k * adv.tok_stride + r] = t;
     if (r < n) {
@@ -167,6 +169,32 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
       __hip_atomic_store(adv.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(adv.cnt, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+  };
+  // every thread, after finish(): the next step's embedding row and its sum of squares, exactly as embed_sumsq
+  // (the first 256 threads, the same chunk walk and reduction order, so the values are bit-identical)
+  __shared__ float ered[4];
+  auto embed_next = [&]() {
+    if (adv.table == nullptr) return;  // uniform
+    __syncthreads();                   // s_next
+    float ss = 0.f;
+    if (threadIdx.x < 256) {
+      const int64_t id = s_next;
+      const uint4* src = reinterpret_cast<const uint4*>(adv.table + id * adv.hidden);
+      uint4* dst = reinterpret_cast<uint4*>(adv.h_out + (int64_t)r * adv.hidden);
+      for (int c = threadIdx.x; c < (adv.hidden >> 3); c += 256) {
+        const uint4 u = src[c];
+        dst[c] = u;
+        float v[8];
+        unpack8(u, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    if ((threadIdx.x & 63) == 0 && threadIdx.x < 256) ered[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    if (threadIdx.x == 0) adv.ssp_out[r] = ered[0] + ered[1] + ered[2] + ered[3];
   };
   const float temp = temperature ? temperature[r] : 0.f;
   const int k = top_k ? top_k[r] : 0;
@@ -185,6 +213,7 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
     }
     best = block_argmax(best, red);
     if (threadIdx.x == 0) finish(best.i < vocab ? best.i : 0);
+    embed_next();
     return;
   }
   if (splits > 1) {
@@ -233,6 +262,7 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
   if (best.i >= vocab) best.i = 0;
   if (greedy) {
     if (threadIdx.x == 0) finish(best.i);
+    embed_next();
     return;
   }
   const float inv_t = 1.f / temp;
@@ -271,6 +301,7 @@ __global__ void __launch_bounds__(SNT) sample_kernel(int64_t* __restrict__ out, 
   }
   g = block_argmax(g, red);
   if (threadIdx.x == 0) finish(g.i < vocab ? g.i : best.i);
+  embed_next();
 }
 
 hipError_t launch_sample(int64_t* out, const bf16_t* logits, int64_t stride, int rows, int vocab,

@@ -271,10 +271,25 @@ class ModelRunner:
         return self._sample(logits, nd, greedy, self.d_out)
 
     # ------------------------------------------------------------- decode
+    def _fused_tail(self, n: int) -> bool:
+        """Steps of n rows end in ONE launch that samples from the LM head's candidates, advances the inputs and
+        gathers the next step's embedding rows (ops.sample_advance): then the step itself starts from them
+        (AttnMetadata.pre_embedded) and the host writes them before the first step of a window (_pre_embed)."""
+        return bool(self.supports_multistep and self.d_lmpart is not None and n <= ops.DECODE_GEMM_MAX_M
+                    and self.model.lm_head_argmax_parts() == self.d_lmpart.shape[1]
+                    and self.dec_scratch is not None and n <= self.dec_scratch["h_in"].shape[0])
+
+    def _pre_embed(self, pad: int) -> None:
+        if self._fused_tail(pad):
+            sc = self.dec_scratch
+            ops.embed_sumsq(self.d_ids[:pad], self.model.embed, sc["ssp0"], out=sc["h_in"][:pad])
+
     def _decode_forward(self, n: int) -> torch.Tensor:
+        tail = self._fused_tail(n)
         meta = AttnMetadata(is_prefill=False, slot_mapping=self.d_slots[:n], block_tables=self.d_bt[:n],
                             ctx_lens=self.d_ctx[:n], max_ctx=self.max_model_len, part_o=self.part_o,
-                            part_ml=self.part_ml, attn_cnt=self.attn_cnt, scratch=self.dec_scratch)
+                            part_ml=self.part_ml, attn_cnt=self.attn_cnt, scratch=self.dec_scratch,
+                            pre_embedded=tail)
         hidden = self.model.forward(self.d_ids[:n], self.d_pos[:n], meta, self.pool.tensor)
         amax = (self.d_lmpart if self.d_lmpart is not None and n <= ops.DECODE_GEMM_MAX_M
                 and self.model.lm_head_argmax_parts() == self.d_lmpart.shape[1] else None)
@@ -283,12 +298,14 @@ class ModelRunner:
         if not self.is_cuda:
             return ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
                               self.d_step[:n])
-        if amax is not None and self.supports_multistep:
-            # sampling from the LM head's candidates and the next step's input advance in one launch
+        if tail:
+            # sampling from the LM head's candidates, the next step's input advance and its embedding rows in one launch
+            sc = self.dec_scratch
             return ops.sample_advance(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
                                       self.d_step, self.d_out[:n], amax[:n], self.d_ids, self.d_pos, self.d_ctx,
                                       self.d_slots, self.d_bt, self.d_tokens, self.d_ctl[0:1], self.d_ctl[1:2],
-                                      self.bs, self.d_adv_ticket)
+                                      self.bs, self.d_adv_ticket,
+                                      embed=(self.model.embed, sc["h_in"], sc["ssp0"].view(-1)))
         out = ops.sample(logits, self.d_temp[:n], self.d_topk[:n], self.d_topp[:n], self.d_seed[:n],
                          self.d_step[:n], out=self.d_out[:n], scratch=self.d_samp,
                          lm_part=amax[:n] if amax is not None else None)
@@ -337,6 +354,7 @@ class ModelRunner:
                                     self.h_bt.data_ptr(), self.bt_width, pad)
         self._fill_sampling(seqs, pad)
         self._h2d(pad, pad, with_cu=False)
+        self._pre_embed(pad)  # the step starts from these rows when its tail launch writes the next ones
         if self.supports_multistep:  # the graph's input advance must see this step's real rows
             self.h_ctl[0] = 0
             self.h_ctl[1] = n
@@ -370,6 +388,7 @@ class ModelRunner:
                                     self.h_bt.data_ptr(), self.bt_width, pad)
         self._fill_sampling(seqs, pad)
         self._h2d(pad, pad, with_cu=False)
+        self._pre_embed(pad)  # the step starts from these rows when its tail launch writes the next ones
         self.h_ctl[0] = 0
         self.h_ctl[1] = n
         self.d_ctl.copy_(self.h_ctl, non_blocking=True)

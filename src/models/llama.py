@@ -53,6 +53,9 @@ class AttnMetadata:
     # last layer computes its KV for every token but attention / o / MLP / final norm only for these rows, and
     # forward() returns [n, H] in this order (None: every row)
     keep_rows: Optional[torch.Tensor] = None
+    # decode (fused path): the step's embedding rows and first-norm statistics are already in scratch["h_in"] /
+    # scratch["ssp0"] (written by the previous step's sampling launch, or by the runner before a window)
+    pre_embedded: bool = False
 
 
 class LayerWeights:
@@ -371,8 +374,10 @@ class CausalLM:
         eps = self.arch.rms_eps
         if (self._slab_path(input_ids) and meta.scratch is not None and not meta.is_prefill
                 and self._fused_decode_ok(kv_pool, input_ids.shape[0])):
-            # the embedding gather and the first norm's row statistics in one launch
-            residual, ssp0 = ops.embed_sumsq(input_ids, self.embed, meta.scratch["ssp0"])
+            if meta.pre_embedded and "h_in" in meta.scratch:
+                residual, ssp0 = meta.scratch["h_in"][: input_ids.shape[0]], meta.scratch["ssp0"]
+            else:  # the embedding gather and the first norm's row statistics in one launch
+                residual, ssp0 = ops.embed_sumsq(input_ids, self.embed, meta.scratch["ssp0"])
             return self._forward_decode_fused(residual, positions, meta, kv_pool, ssp0=ssp0)
         residual = F.embedding(input_ids, self.embed)
         if self._slab_path(input_ids):
@@ -667,7 +672,9 @@ class CausalLM:
               "cnt6": torch.zeros(max((self.inter // (p["gate_up"][0] // 2) if p["gate_up"] else 0)
                                       for p in plans.values()), dtype=i32, device=dev),
               "ssp_a": torch.zeros(to, ld, dtype=f32, device=dev), "cnt_a": torch.zeros(to, dtype=i32, device=dev),
-              "ssp_b": torch.zeros(td, ld, dtype=f32, device=dev), "cnt_b": torch.zeros(td, dtype=i32, device=dev)}
+              "ssp_b": torch.zeros(td, ld, dtype=f32, device=dev), "cnt_b": torch.zeros(td, dtype=i32, device=dev),
+              # the step's embedding rows when the previous step's sampling launch writes them (AttnMetadata.pre_embedded)
+              "h_in": torch.zeros(max(buckets), h, dtype=self.dtype, device=dev)}
         return sc
 
     def _fused_decode_ok(self, kv_pool: torch.Tensor, m: int = 32) -> bool:

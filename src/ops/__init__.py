@@ -211,13 +211,17 @@ def sample(logits, temperature=None, top_k=None, top_p=None, seeds=None, steps=N
 
 
 def sample_advance(logits, temperature, top_k, top_p, seeds, steps, out, lm_part, ids, pos, ctx, slots, bt, tokens,
-                   cnt, n_real, block_size: int, ticket) -> torch.Tensor:
+                   cnt, n_real, block_size: int, ticket, embed=None) -> torch.Tensor:
     """:func:`sample` from the LM head's candidates (``lm_part``) fused with :func:`decode_advance`: every row's
     workgroup also writes its token into the window's token row ``cnt[0]`` and advances the row's id / position /
     context / slot / step (``steps`` is read for the draw, then incremented); the last row bumps ``cnt[0]``.
-    ``ticket``: int32 [1], zero, re-armed by the kernel (graph-capturable)."""
+    ``ticket``: int32 [1], zero, re-armed by the kernel (graph-capturable). ``embed`` = (table [V, H], h_out
+    [>= rows, H], ssp_out [>= rows] fp32): also writes the next step's embedding rows of the advanced ids and their
+    sums of squares, bit-identical to :func:`embed_sumsq`."""
+    e = _empty(logits.device)
+    table, h_out, ssp_out = embed if embed is not None else (e, e, e)
     _kern().sample_advance(out, logits, temperature, top_k, top_p, seeds, lm_part, ids, pos, ctx, slots, bt, steps,
-                           tokens, cnt, n_real, block_size, ticket)
+                           tokens, cnt, n_real, block_size, ticket, table, h_out, ssp_out)
     return out
 
 
@@ -436,13 +440,15 @@ def residual_add_sumsq(resid: torch.Tensor, x: torch.Tensor, out: torch.Tensor) 
     return out
 
 
-def embed_sumsq(ids: torch.Tensor, table: torch.Tensor, ssp: torch.Tensor):
+def embed_sumsq(ids: torch.Tensor, table: torch.Tensor, ssp: torch.Tensor, out: Optional[torch.Tensor] = None):
     """(table[ids] [M, H], ssp): the decode step's embedding gather and its per-row sums of squares (the first
     layer's RMSNorm statistics, ssp [1, SSP_LD]) in one launch."""
     if not table.is_cuda:
         h = torch.nn.functional.embedding(ids, table)
+        if out is not None:
+            h = out.copy_(h)
         return h, row_sumsq(h, out=ssp)
-    h = torch.empty(ids.shape[0], table.shape[1], dtype=table.dtype, device=table.device)
+    h = out if out is not None else torch.empty(ids.shape[0], table.shape[1], dtype=table.dtype, device=table.device)
     _kern().embed_sumsq(h, ssp, table, ids)
     return h, ssp
 

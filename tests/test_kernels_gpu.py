@@ -879,13 +879,21 @@ def test_sample_advance_matches_sample_then_advance(dev, rows, n_real):
     a = state()
     b = {kk: v.clone() for kk, v in a.items()}
     ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+    table = torch.randn(n, 512, device=dev, generator=g).to(torch.bfloat16)
+    h_out = torch.zeros(rows, 512, dtype=torch.bfloat16, device=dev)
+    ssp_out = torch.zeros(1, ops.SSP_LD, device=dev)
     for _ in range(2):
         ops.sample(logits, temp, topk, topp, seeds, a["step"], out=a["out"], lm_part=parts)
         ops.decode_advance(a["out"], a["ids"], a["pos"], a["ctx"], a["slots"], a["bt"], a["step"], a["tokens"],
                            a["ctl"][0:1], a["ctl"][1:2], rows, bs)
         ops.sample_advance(logits, temp, topk, topp, seeds, b["step"], b["out"], parts, b["ids"], b["pos"], b["ctx"],
-                           b["slots"], b["bt"], b["tokens"], b["ctl"][0:1], b["ctl"][1:2], bs, ticket)
+                           b["slots"], b["bt"], b["tokens"], b["ctl"][0:1], b["ctl"][1:2], bs, ticket,
+                           embed=(table, h_out, ssp_out.view(-1)))
     torch.cuda.synchronize()
     for kk in a:
         assert torch.equal(a[kk], b[kk]), kk
     assert int(ticket.item()) == 0 and int(b["ctl"][0].item()) == 5
+    # the next step's embedding rows and statistics: bit-identical to embed_sumsq of the advanced ids
+    ssp_ref = torch.zeros(1, ops.SSP_LD, device=dev)
+    h_ref, _ = ops.embed_sumsq(a["ids"][:rows], table, ssp_ref)
+    assert torch.equal(h_out, h_ref) and torch.equal(ssp_out[0, :rows], ssp_ref[0, :rows])
