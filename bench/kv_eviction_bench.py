@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--max-batched-tokens", type=int, default=16384)
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--decode-weights", default="auto", choices=("auto", "tiled", "single"),
+                    help="EngineConfig.decode_weight_layout; config 5 is KV-capacity bound, so auto = single")
     ap.add_argument("--dry-run", type=int, default=0, metavar="POOL_BLOCKS",
                     help="host-only LRU simulation over a pool of this many blocks")
     a = ap.parse_args()
@@ -86,7 +88,8 @@ def main():
 
     cfg = EngineConfig(max_num_seqs=a.concurrency, max_num_batched_tokens=a.max_batched_tokens, max_latency_ms=0.0,
                        enable_prefix_caching=not a.no_prefix_cache, kv_block_ttl_s=a.ttl or None,
-                       gpu_memory_fraction=a.gpu_memory_fraction)
+                       gpu_memory_fraction=a.gpu_memory_fraction, kv_capacity_priority=True,
+                       decode_weight_layout=a.decode_weights)
     t0 = time.perf_counter()
     eng = LLMEngine.from_preset(a.preset, device="cuda:0", cfg=cfg, max_model_len=a.prefix_len + a.suffix_len +
                                 a.gen_len + 16)
@@ -138,6 +141,7 @@ def main():
         "pool_gib": round(eng.pool.nbytes / 2**30, 1), "pool_blocks": eng.blocks.num_blocks, "pool_tokens": pool_tokens,
         "hbm_total_gib": round(torch.cuda.get_device_properties(0).total_memory / 2**30, 1),
         "weights_gib": round(eng.model.weight_bytes() / 2**30, 1),
+        "decode_weight_layout": eng.decode_weight_layout,
         "working_set_tokens": distinct * a.prefix_len, "distinct_prefixes": distinct,
         "working_set_over_pool": round(distinct * a.prefix_len / pool_tokens, 2),
         "requests": len(reqs), "elapsed_s": round(el, 1), "req_per_s": round(len(reqs) / el, 2),

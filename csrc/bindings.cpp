@@ -567,6 +567,8 @@ static void gemm_decode_impl(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t
   CHK_CONTIG(w);
   check_rows(x, "x");
   const bool tiled = (mode & 32) != 0;  // w pre-packed by ops.gd_pack_weights for this (mode, wr)
+  // mode bit 64: the half-LDS ring (mode 3, <= 32 rows), two workgroups resident per CU (GemmDecodeFuse.half_ring)
+  fz.half_ring = (mode & 64) != 0 ? 1 : 0;
   mode &= 31;
   const int64_t M = x.size(0), K = x.size(1);
   TORCH_CHECK(M >= 1 && M <= 128, "gemm_decode: 1 <= M <= 128");
@@ -639,6 +641,34 @@ static void gemm_decode_impl(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t
 void gemm_decode(Tensor y, Tensor x, Tensor w, int64_t mode, int64_t wr, int64_t kc, int64_t sk, bool nt,
                  Tensor resid, Tensor ssp_out, Tensor counters, Tensor ssp_in, double eps) {
   gemm_decode_impl(y, x, w, mode, wr, kc, sk, nt, resid, ssp_out, counters, ssp_in, eps, die::GemmDecodeFuse{});
+}
+
+// Resident workgroups per CU of the decode-GEMM instantiation a launch with these parameters would use (mode word
+// as for gemm_decode, bits 32 / 64 included; rows = the step's row count): hipOccupancyMaxActiveBlocksPerMultiprocessor
+// on that kernel with its LDS, no launch. -1 if no such instantiation exists. The TP exchange's residency rule
+// (CustomAllReduce.fused_ok) is built on it.
+int64_t gd_occupancy(int64_t mode, int64_t wr, int64_t kc, int64_t sk, int64_t rows, bool nt) {
+  if (!gd_tile_ok(wr, kc) || rows < 1 || rows > 128 || sk < 1) return -1;
+  die::GemmDecodeFuse fz;
+  fz.half_ring = (mode & 64) != 0 ? 1 : 0;
+  const int m = (int)(mode & 31);
+  // stand-ins for the pointers the launcher validates (never dereferenced: nothing is launched)
+  static char dummy[64];
+  fz.resid = reinterpret_cast<die::bf16_t*>(dummy);
+  fz.ssp_out = reinterpret_cast<float*>(dummy);
+  fz.counters = reinterpret_cast<int*>(dummy);
+  fz.ssp_in = reinterpret_cast<const float*>(dummy);
+  fz.ssp_tiles = 1;
+  fz.slab6 = reinterpret_cast<float*>(dummy);
+  int occ = 0;
+  fz.occupancy = &occ;
+  const int silu = (m == 1 || m == 4 || m == 6);
+  const int n = (int)(silu ? wr / 2 : wr);  // one column tile: the launcher only checks divisibility
+  const int k = (int)(kc * sk);
+  const hipError_t e = die::launch_gemm_decode(dummy, n, reinterpret_cast<const die::bf16_t*>(dummy), k,
+                                               reinterpret_cast<const die::bf16_t*>(dummy), (int)rows, n, k, m,
+                                               (int)wr, (int)kc, (int)sk, nt, fz, cur_stream());
+  return e == hipSuccess ? occ : -1;
 }
 
 // y = x @ w^T (mode 0, bf16) that also writes each column tile's per-row greedy candidate into amax
@@ -1009,6 +1039,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_decode", &gemm_decode);
   m.def("gemm_decode_argmax", &gemm_decode_argmax);
   m.def("gemm_decode_car", &gemm_decode_car);
+  m.def("gd_occupancy", &gd_occupancy);
   m.def("rms_row_scale", &rms_row_scale);
   m.def("gd_set_timestamps", &gd_set_timestamps);
   m.def("attn_set_timestamps", &attn_set_timestamps);

@@ -664,22 +664,58 @@ constexpr bool gd_valid(int wr, int xr, int kc) {
          !(xr < 64 && kc < 128 && wr % 64 != 0) && gd_lds(wr, xr, kc, s) <= 160 * 1024;
 }
 
+// ring depth of the half-LDS form (mode 3, fz.half_ring): at most HALF_RING_BYTES so that two workgroups fit on a
+// CU (160 KiB of LDS). The TP row-parallel projections use it where the grid is about one workgroup per CU: with
+// two resident per CU the whole grid of every GPU is co-resident with room to spare, which the exchange's
+// waiting last arrivers need (CustomAllReduce.fused_ok); 0 = no such form
+constexpr int HALF_RING_BYTES = 76 * 1024;
+constexpr int half_ring_slots(int wr, int xr, int kc) {
+  const int s = ring_slots(wr, xr, kc);
+  const int h = HALF_RING_BYTES / ((wr + xr) * kc * 2);
+  const int r = h < s ? h : s;
+  return r >= 2 ? r : 0;
+}
+
+// launch (or, with fz.occupancy set, only report the resident workgroups per CU of) one instantiation
+template <int WR, int EPI, int S, int KC, int XR, int SKC>
+static hipError_t launch_gd_s(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N_out,
+                              int K, int sk, bool nt, const GemmDecodeFuse& fz, hipStream_t s) {
+  constexpr size_t lds = gd_lds(WR, XR, KC, S);
+  if (fz.occupancy != nullptr)
+    return nt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(fz.occupancy,
+                                                             gemm_decode_kernel<WR, EPI, S, true, KC, XR, SKC>, NTH, lds)
+              : hipOccupancyMaxActiveBlocksPerMultiprocessor(fz.occupancy,
+                                                             gemm_decode_kernel<WR, EPI, S, false, KC, XR, SKC>, NTH,
+                                                             lds);
+  const dim3 grid(N_out / ((EPI == 1 || EPI == 4 || EPI == 6) ? WR / 2 : WR), sk, fz.grp_n);
+  if (nt)
+    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, true, KC, XR, SKC>), grid, dim3(NTH), lds, s, Y, ldy, X, ldx,
+                       W, M, N_out, K, fz);
+  else
+    hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, false, KC, XR, SKC>), grid, dim3(NTH), lds, s, Y, ldy, X,
+                       ldx, W, M, N_out, K, fz);
+  return hipGetLastError();
+}
+
 template <int WR, int EPI, int KC, int XR, int SKC = 0>
 static hipError_t launch_gd_xr(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N_out,
                                int K, int sk, bool nt, const GemmDecodeFuse& fz, hipStream_t s) {
   if constexpr (!gd_valid(WR, XR, KC)) {
     return hipErrorInvalidValue;
   } else {
+    if (fz.half_ring) {
+      // mode 3 at <= 32 rows on the nt path only (the TP shard shapes): bounds the instantiations
+      if constexpr (EPI == 3 && XR <= 32 && half_ring_slots(WR, XR, KC) >= 2 &&
+                    gd_lds(WR, XR, KC, half_ring_slots(WR, XR, KC)) <= HALF_RING_BYTES) {
+        if (!nt) return hipErrorInvalidValue;
+        constexpr int S2 = half_ring_slots(WR, XR, KC);
+        return launch_gd_s<WR, EPI, S2, KC, XR, SKC>(Y, ldy, X, ldx, W, M, N_out, K, sk, true, fz, s);
+      } else {
+        return hipErrorInvalidValue;
+      }
+    }
     constexpr int S = ring_slots(WR, XR, KC);
-    constexpr size_t lds = gd_lds(WR, XR, KC, S);
-    const dim3 grid(N_out / ((EPI == 1 || EPI == 4 || EPI == 6) ? WR / 2 : WR), sk, fz.grp_n);
-    if (nt)
-      hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, true, KC, XR, SKC>), grid, dim3(NTH), lds, s, Y, ldy, X, ldx,
-                         W, M, N_out, K, fz);
-    else
-      hipLaunchKernelGGL((gemm_decode_kernel<WR, EPI, S, false, KC, XR, SKC>), grid, dim3(NTH), lds, s, Y, ldy, X,
-                         ldx, W, M, N_out, K, fz);
-    return hipGetLastError();
+    return launch_gd_s<WR, EPI, S, KC, XR, SKC>(Y, ldy, X, ldx, W, M, N_out, K, sk, nt, fz, s);
   }
 }
 
@@ -745,6 +781,10 @@ hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx
   if (fz.amax != nullptr && (mode != 0 || fz.amax_parts < 1 ||
                              ((reinterpret_cast<uintptr_t>(Y) | (uintptr_t)(ldy * 2)) & 15)))
     return hipErrorInvalidValue;  // candidates come with mode 0's 16-byte store path
+  // the candidate epilogue merges a row's CPW = wr / 8 lanes with xor shuffles: only a power of two keeps every
+  // partner inside the row (wr = 48 / 96 / 112 would mix rows and straddle waves)
+  if (fz.amax != nullptr && (wr % 8 || ((wr / 8) & (wr / 8 - 1)))) return hipErrorInvalidValue;
+  if (fz.half_ring && (mode != 3 || M > 32)) return hipErrorInvalidValue;
   if ((mode == 4 || mode == 6) &&
       (fz.ssp_in == nullptr || fz.ssp_tiles < 1 ||
        fz.ssp_tiles > (M <= 32 ? DECODE_SSP_MAX_TILES : DECODE_SSP_MAX_TILES_WIDE)))

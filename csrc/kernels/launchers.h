@@ -165,6 +165,11 @@ struct GemmDecodeFuse {
   int64_t car_cap = 0;           // bf16 elements per half of each rank's staging buffer
   uint32_t* car_ctl = nullptr;   // [epoch, ticket, error] words of the group's CustomAllReduce
   CarPeers car;
+  // mode 3 at <= 32 rows: a ring of <= 76 KiB so that two workgroups are resident per CU (gemm_decode.hip
+  // half_ring_slots) — the TP exchange's co-residency margin at one-workgroup-per-CU grids
+  int half_ring = 0;
+  // query only: no launch; *occupancy = resident workgroups per CU of the instantiation this call would launch
+  int* occupancy = nullptr;
 };
 hipError_t launch_gemm_decode(void* Y, int64_t ldy, const bf16_t* X, int64_t ldx, const bf16_t* W, int M, int N,
                               int K, int mode, int wr, int kc, int sk, bool nt, const GemmDecodeFuse& fz,

@@ -315,6 +315,10 @@ hipError_t launch_sample(int64_t* out, const bf16_t* logits, int64_t stride, int
   // the advance rides on one workgroup per row: only with the LM head's candidates (no split argmax)
   if (adv.ids != nullptr && (lm_part == nullptr || adv.cnt == nullptr || adv.ticket == nullptr || adv.n_real == nullptr))
     return hipErrorInvalidValue;
+  // the embedding gather reads the advanced id: it needs the advance and its outputs
+  if (adv.table != nullptr &&
+      (adv.ids == nullptr || adv.h_out == nullptr || adv.ssp_out == nullptr || adv.hidden <= 0 || adv.hidden % 8))
+    return hipErrorInvalidValue;
   // with the LM head's candidates a greedy row is one short reduction: no split (a sampled row is whole anyway)
   if (lm_part != nullptr) splits = 1;
   hipLaunchKernelGGL(sample_kernel, dim3(rows, splits), dim3(SNT), 0, s, out, logits, stride, vocab, temperature,

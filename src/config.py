@@ -52,6 +52,9 @@ class ModelConfig:
     max_latency_ms: float = 10.0
     seed: int = 0
     overrides: Dict[str, Any] = field(default_factory=dict)
+    # text prompts / text outputs: 0 = tokenised and detokenised on the worker's event loop; N = in N separate
+    # processes (src.preproc.PreprocPool). Token-id requests never touch the pool.
+    preproc_processes: int = 0
 
     def to_dict(self) -> Dict[str, Any]:
         return asdict(self)
@@ -129,6 +132,15 @@ class EngineConfig:
     arrival_window_ms: float = 250.0
     # prefill GEMMs: the measured solution table for the serving shapes (src/ops/gemm_table.py), read-only
     tuned_gemm_table: bool = True
+    # decode-GEMM weight layout: "tiled" keeps tile-order copies of the dense projections beside prefill's
+    # row-major weights (fastest decode; +13 GiB at Llama-3-8B / 32 rows), "single" runs the decode GEMMs on the
+    # row-major weights (one copy: the bench 4 % slower, profiles/r5_decode_weight_layout_ab.txt, and that HBM goes
+    # to the KV pool), "auto" = "single" when the KV pool is the constraint (kv_capacity_priority, or an explicit
+    # num_kv_blocks that does not fit beside the copies), else "tiled". The choice is logged and in get_stats().
+    decode_weight_layout: str = "auto"
+    # the workload is bound by KV capacity (prefix-cache reuse under eviction: BASELINE config 5): every GiB of
+    # HBM goes to the pool
+    kv_capacity_priority: bool = False
 
 
 @dataclass

@@ -91,6 +91,16 @@ class LLMBackend:
         self.kv_direct = bool(ov.get("kv_direct", True))
         self.kv_zone_bytes = int(ov.get("kv_landing_zone_bytes", 4 << 30))
         self.ipc_imports = 0
+        # text prompts and text outputs tokenised / detokenised in separate processes (ModelConfig.preproc_processes;
+        # the reference's "pre/post-processing in a separate process", /root/reference/README.md:15,96-98). Token-id
+        # requests (the benches' path) never touch the pool; streaming deltas stay incremental on the event loop.
+        self.preproc = None
+        nproc = int(getattr(config, "preproc_processes", 0) or ov.get("preproc_processes", 0) or 0)
+        if nproc > 0:
+            from src.preproc import PreprocPool
+
+            tok_path = None if isinstance(self.tokenizer, ByteTokenizer) else (config.model_path or None)
+            self.preproc = PreprocPool(nproc, engine.arch.vocab_size, tok_path)
 
     async def start(self) -> None:
         self.async_engine.start()
@@ -100,6 +110,28 @@ class LLMBackend:
 
     def close(self) -> None:
         self.async_engine.stop()
+        if self.preproc is not None:
+            self.preproc.close()
+            self.preproc = None
+
+    async def _tokenized(self, inputs: Any) -> Any:
+        """A text prompt's ids from the pre-processing pool (unchanged inputs without a pool or with ids)."""
+        if self.preproc is None:
+            return inputs
+        if isinstance(inputs, str):
+            inputs = {"prompt": inputs}
+        if isinstance(inputs, dict) and inputs.get("prompt_token_ids") is None and isinstance(inputs.get("prompt"), str):
+            ids = await self.preproc.encode_one(inputs["prompt"])
+            inputs = {**inputs, "prompt_token_ids": ids}
+        return inputs
+
+    async def _output(self, ids: List[int], return_text: bool = True, **kw) -> Dict[str, Any]:
+        """build_llm_output, with the text detokenised in the post-processing pool when there is one."""
+        if self.preproc is None or not return_text:
+            return build_llm_output(ids, self.tokenizer, return_text=return_text, **kw)
+        out = build_llm_output(ids, None, return_text=False, **kw)
+        out["text"] = await self.preproc.decode_one(ids)
+        return out
 
     def healthy(self) -> bool:
         """False once the engine loop died (e.g. a HIP fault surfaced as an exception): the worker
@@ -130,6 +162,7 @@ class LLMBackend:
             self.async_engine.start()
         self.request_count += 1
         try:
+            inputs = await self._tokenized(inputs)
             gi = normalize_request(inputs, self.tokenizer, self.engine.max_model_len)
         except ValueError:
             self.error_count += 1
@@ -162,9 +195,8 @@ class LLMBackend:
         lat = (time.perf_counter() - t0) * 1e3
         self.total_latency += lat / 1e3
         reason = "timeout" if timed_out and seq.finish_reason == "abort" else (seq.finish_reason or "length")
-        return build_llm_output(seq.output_ids, self.tokenizer, prompt_len=seq.prompt_len,
-                                finish_reason=reason, ttft_ms=seq.ttft_ms(),
-                                latency_ms=seq.latency_ms(), return_text=gi.return_text)
+        return await self._output(seq.output_ids, gi.return_text, prompt_len=seq.prompt_len, finish_reason=reason,
+                                  ttft_ms=seq.ttft_ms(), latency_ms=seq.latency_ms())
 
     async def predict_stream(self, inputs: Any, emit, request_id: Optional[str] = None) -> Dict[str, Any]:
         """Streaming generation: ``await emit({"delta_token_ids": [...], "done": False})`` as tokens are
@@ -259,9 +291,8 @@ class LLMBackend:
         if pseq.finish_reason == "stop":
             if slot is not None:
                 self._decode_link.revoke(slot)
-            return build_llm_output(pseq.output_ids, self.tokenizer, prompt_len=pseq.prompt_len,
-                                    finish_reason="stop", ttft_ms=pseq.ttft_ms(), latency_ms=pseq.latency_ms(),
-                                    return_text=gi.return_text)
+            return await self._output(pseq.output_ids, gi.return_text, prompt_len=pseq.prompt_len,
+                                      finish_reason="stop", ttft_ms=pseq.ttft_ms(), latency_ms=pseq.latency_ms())
         packet = KVPacket(rid, gi.prompt_token_ids, pseq.output_ids[0], pseq.kv_export, self.engine.cfg.block_size,
                           sampling_to_dict(gi.sampling), ttft_ms=pseq.ttft_ms(),
                           ready=getattr(pseq, "kv_export_ready", None))
@@ -320,8 +351,8 @@ class LLMBackend:
             if packet.on_imported is not None and not handed:
                 self._landing_zone().release(off)
             raise
-        return {"success": True, "outputs": build_llm_output(
-            seq.output_ids, self.tokenizer, prompt_len=seq.prompt_len, finish_reason=seq.finish_reason or "length",
+        return {"success": True, "outputs": await self._output(
+            seq.output_ids, prompt_len=seq.prompt_len, finish_reason=seq.finish_reason or "length",
             ttft_ms=packet.ttft_ms, latency_ms=seq.latency_ms())}
 
     async def predict_batch(self, inputs_list: List[Any]) -> List[Dict[str, Any]]:
@@ -372,6 +403,8 @@ class LLMBackend:
         }
         if self._decode_link is not None:  # disaggregated prefill: how the prompt KV has travelled
             m["kv_link"] = self._decode_link.stats()
+        if self.preproc is not None:  # which processes tokenised / detokenised, in how many calls
+            m["preproc"] = self.preproc.stats()
         if self.engine.device.type == "cuda":
             free, total = torch.cuda.mem_get_info(self.engine.device)
             m["hbm_used_gib"] = (total - free) / 2**30

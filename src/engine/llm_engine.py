@@ -53,6 +53,27 @@ def plan_kv_blocks(arch: ArchConfig, model: CausalLM, cfg: EngineConfig, device:
     return max(16, int(budget // per_block))
 
 
+def choose_decode_weight_layout(model, cfg: EngineConfig, device: torch.device, buckets) -> str:
+    """"tiled" or "single" (EngineConfig.decode_weight_layout): "auto" keeps the tile-order copies unless the KV
+    pool is the constraint — cfg.kv_capacity_priority, or an explicit num_kv_blocks that the HBM left after the
+    copies cannot hold (/root/reference/src/kvstore.py:82-102: capacity is what the LRU evicts for)."""
+    mode = getattr(cfg, "decode_weight_layout", "auto")
+    if mode in ("tiled", "single"):
+        return mode
+    if mode != "auto":
+        raise ValueError(f"decode_weight_layout must be auto / tiled / single, not {mode!r}")
+    if getattr(cfg, "kv_capacity_priority", False):
+        return "single"
+    if cfg.num_kv_blocks and device.type == "cuda" and hasattr(model, "decode_copy_bytes"):
+        extra = model.decode_copy_bytes(buckets)
+        if extra:
+            fits = plan_kv_blocks(model.arch, model, EngineConfig(**{**cfg.__dict__, "num_kv_blocks": None}), device)
+            per_block = KVPool.bytes_per_block(model.arch.num_layers, model.hkv, cfg.block_size, model.arch.head_dim)
+            if cfg.num_kv_blocks > fits - extra // per_block:
+                return "single"
+    return "tiled"
+
+
 class LLMEngine:
     def __init__(self, model: CausalLM, cfg: EngineConfig, max_model_len: int, eos_token_id: Optional[int] = 2,
                  runner_cls=ModelRunner):
@@ -66,9 +87,18 @@ class LLMEngine:
             from src.ops.gemm_table import enable_prefill_gemm_table
 
             enable_prefill_gemm_table(self.device)
+        self.decode_weight_layout = "row-major"
         if hasattr(model, "pack_decode_weights") and hasattr(model, "decode_buckets"):
-            # the decode GEMMs' tile-order weight copies are made before the KV pool takes the free HBM
-            model.pack_decode_weights(model.decode_buckets(cfg.max_num_seqs))
+            # the decode GEMMs' tile-order weight copies are made before the KV pool takes the free HBM — unless
+            # the KV pool is the constraint (EngineConfig.decode_weight_layout)
+            buckets = model.decode_buckets(cfg.max_num_seqs)
+            if choose_decode_weight_layout(model, cfg, self.device, buckets) == "single":
+                model.tiled_decode_weights = False
+            if model.pack_decode_weights(buckets):
+                self.decode_weight_layout = "tiled"
+            logger.info("decode weights: %s (%s)", self.decode_weight_layout,
+                        f"+{model.decode_copy_bytes(buckets) / 2**30:.1f} GiB of tile-order copies"
+                        if self.decode_weight_layout == "tiled" else "one copy, HBM left to the KV pool")
         if hasattr(model, "pack_lm_head"):
             model.pack_lm_head()
         nblocks = plan_kv_blocks(self.arch, model, cfg, self.device)
@@ -542,4 +572,5 @@ class LLMEngine:
         s["kv"] = self.blocks.stats()
         s["kv_pool_gib"] = self.pool.nbytes / 2**30
         s["graphs"] = list(self.runner.graph_sizes)
+        s["decode_weight_layout"] = self.decode_weight_layout
         return s

@@ -60,6 +60,8 @@ class KVPool:
 
 
 class ModelRunner:
+    mirrors_windows = False  # see supports_multistep
+
     def __init__(self, model: CausalLM, pool: KVPool, cfg: EngineConfig, max_model_len: int):
         self.model = model
         self.pool = pool
@@ -106,6 +108,7 @@ class ModelRunner:
         self.n_ids, self.n_temp, self.n_topk = self.h_ids.numpy(), self.h_temp.numpy(), self.h_topk.numpy()
         self.n_topp, self.n_seed, self.n_step = self.h_topp.numpy(), self.h_seed.numpy(), self.h_step.numpy()
         self._samp_key = None
+        self._samp_sent = 0
         dev = self.device
         # device-side static buffers (graph inputs)
         self.d_ids = torch.zeros(self.max_tokens, dtype=i64, device=dev)
@@ -142,7 +145,10 @@ class ModelRunner:
         else:
             self.part_o = self.part_ml = self.attn_cnt = self.dec_scratch = self.d_lmpart = None
         self.supports_swap = type(self)._sync_step is ModelRunner._sync_step
-        self.supports_multistep = self.is_cuda and self.k_max > 1 and type(self)._sync_step is ModelRunner._sync_step
+        # a runner whose steps are mirrored by other ranks (tensor parallelism) must mirror whole windows too:
+        # it declares that with mirrors_windows (TPModelRunner sends one message per window, not per step)
+        self.supports_multistep = self.is_cuda and self.k_max > 1 and (
+            type(self)._sync_step is ModelRunner._sync_step or self.mirrors_windows)
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_sizes: List[int] = []
         self._graph_pool = None
@@ -188,6 +194,7 @@ class ModelRunner:
         for h, d in ((self.h_temp, self.d_temp), (self.h_topk, self.d_topk), (self.h_topp, self.d_topp),
                      (self.h_seed, self.d_seed), (self.h_step, self.d_step)):
             d[:n_pad].copy_(h[:n_pad], non_blocking=nb)
+        self._samp_sent = n_pad  # rows of sampling parameters this step re-sent (TP windows mirror them)
         return greedy
 
     def _sample(self, logits: torch.Tensor, n: int, greedy: bool, out: torch.Tensor) -> torch.Tensor:
@@ -221,6 +228,14 @@ class ModelRunner:
     def _sync_step(self, kind: int, a: int = 0, b: int = 0, c: int = 0, d: int = 0) -> None:
         """Hook for tensor parallelism: rank 0 publishes the step to followers
         (see :class:`src.parallel.tp_runner.TPModelRunner`). No-op at TP=1."""
+
+    def _sync_window(self, n: int, pad: int, k: int) -> None:
+        """Hook: rank 0 publishes a k-step decode window (its first step's inputs, already in the host staging
+        buffers; the graph advances them on every rank). No-op at TP=1."""
+
+    def _sync_continuation(self, par: int, pad: int, k: int, base: int) -> None:
+        """Hook: rank 0 publishes a continuation window queued behind the running one (the re-sent block tables
+        and first-step slots of staging set ``par``, the token-row base). No-op at TP=1."""
 
     @torch.inference_mode()
     def prefill(self, chunks: List[PrefillChunk], kv_hook=None) -> List[Optional[int]]:
@@ -386,12 +401,14 @@ class ModelRunner:
         self.rt.build_decode_inputs([s.block_table for s in seqs], [len(s) for s in seqs], self.bs,
                                     self.h_pos.data_ptr(), self.h_slots.data_ptr(), self.h_ctx.data_ptr(),
                                     self.h_bt.data_ptr(), self.bt_width, pad)
+        self._samp_sent = 0
         self._fill_sampling(seqs, pad)
         self._h2d(pad, pad, with_cu=False)
         self._pre_embed(pad)  # the step starts from these rows when its tail launch writes the next ones
         self.h_ctl[0] = 0
         self.h_ctl[1] = n
         self.d_ctl.copy_(self.h_ctl, non_blocking=True)
+        self._sync_window(n, pad, k)
         for _ in range(k):
             g.replay()
         self.h_tokens[:k].copy_(self.d_tokens[:k], non_blocking=True)
@@ -424,6 +441,7 @@ class ModelRunner:
         self.d_bt[:pad].copy_(hbt[:pad], non_blocking=True)
         self.d_slots[:pad].copy_(hsl[:pad], non_blocking=True)
         self.d_ctl[0:1].fill_(base)  # token rows [base, base + k)
+        self._sync_continuation(par, pad, k, base)
         g = self.graphs[pad]
         for _ in range(k):
             g.replay()

@@ -582,16 +582,38 @@ class CausalLM:
         # it (TPContext.fused_row_parallel), else bf16 partial sums (mode 0) for a separate all-reduce launch
         o = ops.decode_tile(h, self.hq * d, 3, b)
         down = ops.decode_tile(h, self.inter, 3, b) if not self.arch.is_moe else None
-        tp_fused = False
+        tp_fused = o_half = down_half = False
         if self.tp.enabled:
-            tp_fused = (not self.arch.is_moe and self.tp.fused_row_parallel(h // o[0], h // o[0] * o[2])
-                        and self.tp.fused_row_parallel(h // down[0], h // down[0] * down[2]))
-            if not tp_fused:
+            fo = self._tp_fused_tile(h, self.hq * d, b, o) if not self.arch.is_moe else None
+            fd = self._tp_fused_tile(h, self.inter, b, down) if fo is not None else None
+            tp_fused = fo is not None and fd is not None
+            if tp_fused:
+                (o, o_half), (down, down_half) = fo, fd
+            else:
                 o = ops.decode_tile(h, self.hq * d, 0, b)
                 down = ops.decode_tile(h, self.inter, 0, b) if not self.arch.is_moe else None
         gu = ops.decode_tile_silu(self.inter, h, b) if not self.arch.is_moe else None
         return {"qkv": qkv, "o": o, "down": down, "gate_up": gu[:2] if gu else None,
-                "gate_up_sk": gu[2] if gu else 1, "tp_fused": tp_fused}
+                "gate_up_sk": gu[2] if gu else 1, "tp_fused": tp_fused, "o_half": o_half, "down_half": down_half}
+
+    def _tp_fused_tile(self, n: int, k: int, bucket: int, tile):
+        """((wr, kc, sk), half_ring) of a row-parallel projection whose tiles carry the TP exchange, or None. The
+        measured tile first (with its full LDS ring, then — at <= 32 rows — the half-LDS ring that puts two
+        workgroups on a CU), then wider tiles (fewer waiting last arrivers): the first that passes the group's
+        residency rule (custom_allreduce.fused_exchange_ok, on the instantiation's real occupancy)."""
+        lim = ops.SSP_MAX_TILES if bucket <= 32 else ops.SSP_MAX_TILES_WIDE
+        cands = [tuple(tile)] + [c for c in ((64, 256, 1), (64, 128, 1), (64, 128, 2), (128, 128, 1), (128, 128, 2))
+                                 if c != tuple(tile)]
+        for wr, kc, sk in cands:
+            if n % wr or k % (kc * sk) or n // wr > lim or not ops.gd_tile_valid(wr, kc, bucket):
+                continue
+            for half in ((False, True) if bucket <= 32 else (False,)):
+                occ = ops.gd_occupancy(3, wr, kc, sk, bucket, half)
+                if half and occ <= 0:
+                    continue
+                if self.tp.fused_row_parallel(n // wr, n // wr * sk, occ):
+                    return (wr, kc, sk), half
+        return None
 
     def _packed_layouts(self, buckets) -> set:
         """(projection, wr, kc) tile-order copies the fused path uses for these row buckets."""
@@ -616,15 +638,7 @@ class CausalLM:
             return False
         if not (self.device.type == "cuda" and ops.native_available()):
             return False
-        lw0 = self.layers[0]
-
-        def tiles(name, wr, kc):  # the tile covers the (shard's) weight exactly
-            rows, k = getattr(lw0, name).shape
-            silu = name == "gate_up"
-            return k % kc == 0 and (rows // 2 if silu else rows) % (wr // 2 if silu else wr) == 0
-
-        need = {t for t in self._packed_layouts(buckets) if tiles(*t)}
-        extra = sum(getattr(lw0, name).numel() * 2 for name, _, _ in need) * len(self.layers)
+        need, extra = self._decode_copy_plan(buckets)
         total = torch.cuda.get_device_properties(self.device).total_memory
         if self.weight_bytes() + extra > total // 2:
             return False
@@ -634,6 +648,25 @@ class CausalLM:
                     lw.tiled[(name, wr, kc)] = ops.gd_pack_weights(getattr(lw, name), wr, silu=name == "gate_up",
                                                                    kc=kc)
         return True
+
+    def _decode_copy_plan(self, buckets):
+        """(tile layouts, bytes) of the tile-order decode weight copies these row buckets would use."""
+        lw0 = self.layers[0]
+
+        def tiles(name, wr, kc):  # the tile covers the (shard's) weight exactly
+            rows, k = getattr(lw0, name).shape
+            silu = name == "gate_up"
+            return k % kc == 0 and (rows // 2 if silu else rows) % (wr // 2 if silu else wr) == 0
+
+        need = {t for t in self._packed_layouts(buckets) if tiles(*t)}
+        extra = sum(getattr(lw0, name).numel() * lw0.qkv.element_size() for name, _, _ in need) * len(self.layers)
+        return need, extra
+
+    def decode_copy_bytes(self, buckets) -> int:
+        """HBM the tile-order decode weight copies would take (0 where none are made)."""
+        if not self.tiled_decode_weights or self.arch.is_moe or not self.norms_folded:
+            return 0
+        return self._decode_copy_plan(buckets)[1]
 
     @staticmethod
     def decode_buckets(max_rows: int) -> List[int]:
@@ -734,10 +767,12 @@ class CausalLM:
                     wdn_, kd, sd = plan["down"]
                     wo_t, to_ = tw(lw, "o", wo, ko)
                     wd_t, td_ = tw(lw, "down", wdn_, kd)
-                    self.tp.row_parallel_residual(attn, wo_t, h, ssp_a, sc["cnt_a"], wo, ko, so, tiled=to_)
+                    self.tp.row_parallel_residual(attn, wo_t, h, ssp_a, sc["cnt_a"], wo, ko, so, tiled=to_,
+                                                  half_ring=plan["o_half"])
                     act = ops.linear_silu_mul_rownorm(h, wgu, ssp_a, eps, wg, tiled=tg, kc=kg, sk=gsk,
                                                       slab=sc["slab6"], counters=sc["cnt6"])
-                    self.tp.row_parallel_residual(act, wd_t, h, ssp_b, sc["cnt_b"], wdn_, kd, sd, tiled=td_)
+                    self.tp.row_parallel_residual(act, wd_t, h, ssp_b, sc["cnt_b"], wdn_, kd, sd, tiled=td_,
+                                                  half_ring=plan["down_half"])
                 elif self.tp.enabled:  # row-parallel partial sums -> all-reduce -> residual + statistics (one
                     # launch on the one-shot IPC path, see TPContext.all_reduce_residual)
                     self.tp.all_reduce_residual(self._row_parallel(attn, lw, "o", plan), h, ssp_a)

@@ -370,7 +370,7 @@ def _empty(dev) -> torch.Tensor:
 
 def linear_slab_residual(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, ssp_out: torch.Tensor,
                          counters: torch.Tensor, wr: int = 64, sk: int = 4, tiled: bool = False,
-                         kc: Optional[int] = None) -> torch.Tensor:
+                         kc: Optional[int] = None, half_ring: bool = False) -> torch.Tensor:
     """resid += x @ w^T (bf16, in place) with split-K reduced by the last-arriving workgroup of
     each column tile, which also writes the tile's row sums of squares of the new residual to
     ssp_out [N/wr, SSP_LD] — the statistics of the next RMSNorm (whose weight is folded into the
@@ -379,9 +379,25 @@ def linear_slab_residual(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, 
     wr, kc = gd_tile(wr, kc)
     slab = torch.empty(sk, m, n, dtype=torch.float32, device=x.device)
     e = _empty(x.device)
-    _kern().gemm_decode(slab, x, w, 3 | (32 if tiled else 0), wr, kc, sk, DECODE_GEMM_NT, resid, ssp_out, counters,
-                        e, 0.0)
+    _kern().gemm_decode(slab, x, w, 3 | (32 if tiled else 0) | (64 if half_ring else 0), wr, kc, sk, DECODE_GEMM_NT,
+                        resid, ssp_out, counters, e, 0.0)
     return slab
+
+
+_OCC: dict = {}
+
+
+def gd_occupancy(mode: int, wr: int, kc: int, sk: int, rows: int, half_ring: bool = False) -> int:
+    """Resident workgroups per CU of the decode-GEMM launch these parameters select
+    (hipOccupancyMaxActiveBlocksPerMultiprocessor on that instantiation; 0 off the GPU or if none exists)."""
+    if not native_available() or not torch.cuda.is_available():
+        return 0
+    key = (mode, wr, kc, sk, rows, half_ring)
+    v = _OCC.get(key)
+    if v is None:
+        v = max(0, int(_kern().gd_occupancy(mode | (64 if half_ring else 0), wr, kc, sk, rows, DECODE_GEMM_NT)))
+        _OCC[key] = v
+    return v
 
 
 def linear_silu_mul_rownorm(x: torch.Tensor, w_gate_up: torch.Tensor, ssp_in: torch.Tensor, eps: float,

@@ -39,6 +39,32 @@ def _kern():
     return _C
 
 
+def residency_margin(cus: int) -> int:
+    """Workgroup slots rule (a) of :func:`fused_exchange_ok` keeps free: 1/16 of the CUs (16 on MI355X)."""
+    return max(4, cus // 16)
+
+
+def fused_exchange_ok(n_tiles: int, grid: int, per_cu: int, ranks_per_gpu: int, cus: int) -> bool:
+    """Residency rule of the exchange fused into the row-parallel decode GEMM. Only a column tile's last-arriving
+    workgroup waits for the peers (one flag slot per tile), so a launch holds at most ``n_tiles`` waiting
+    workgroups per rank. The grid always drains when either
+
+    (a) every workgroup of every rank sharing the GPU is resident at once WITH a margin: ``grid`` x ranks <=
+        ``per_cu`` x CUs - margin, where ``per_cu`` is the kernel's occupancy (hipOccupancyMaxActiveBlocksPerMultiprocessor
+        on the exact instantiation: LDS ring, registers) — so a few CUs held by another stream's kernel, or a CU
+        mask, still leave room for the whole grid; or
+    (b) the waiting workgroups can hold at most HALF the CUs, so the others always find a CU and finish.
+
+    When neither holds the caller keeps the separate all-reduce launch (never a spin that could only end at the
+    bounded wait). The 70B TP=8 shard's o / down at 32 rows (wr = 32: 256 tiles, grid 256, one workgroup per CU
+    with the full LDS ring) fail both and take the half-LDS ring (two per CU: 256 <= 512 - 16)."""
+    if not 0 < n_tiles <= SIG_BLOCKS:
+        return False
+    if grid > 0 and per_cu > 0 and grid * ranks_per_gpu <= per_cu * cus - residency_margin(cus):
+        return True
+    return n_tiles * ranks_per_gpu * 2 <= cus
+
+
 class CustomAllReduce:
     """IPC-mapped one-shot all-reduce for one TP group (2..8 ranks on one node)."""
 
@@ -112,24 +138,20 @@ class CustomAllReduce:
         new residual — all-reduce and residual_add_sumsq in one launch (decode rows, <= 64)."""
         _kern().car_all_reduce_residual(x, resid, ssp, self.rank, self.bufs, self.sigs, self.ctl, self.cap)
 
-    def fused_ok(self, n_tiles: int, grid: int = 0) -> bool:
-        """Whether the row-parallel decode GEMM may carry the exchange in its epilogue (gemm_decode_car). Only a
-        column tile's last-arriving workgroup waits for the peers, so a launch holds at most ``n_tiles`` waiting
-        workgroups on each GPU (times the ranks sharing it, in one-GPU tests). The grid always drains when
-        either (a) every workgroup of every rank sharing the GPU is resident at once — ``grid`` x ranks <= CUs,
-        at least one workgroup per CU whatever the kernel's occupancy — or (b) the waiting ones can hold at most
-        HALF the CUs, so the others always find a CU and finish. Both assume no long-running kernel of another
-        stream holds CUs meanwhile (a TP rank runs its decode on one stream). ``DIE_TP_FUSED=0`` keeps the
-        separate all-reduce launch. The answer depends only on the group's layout and the shape, so every rank
-        agrees."""
+    def fused_ok(self, n_tiles: int, grid: int = 0, per_cu: int = 0) -> bool:
+        """Whether the row-parallel decode GEMM may carry the exchange in its epilogue (gemm_decode_car); see
+        :func:`fused_exchange_ok` (``per_cu``: the launch's resident workgroups per CU, ops.gd_occupancy).
+        ``DIE_TP_FUSED=0`` keeps the separate all-reduce launch. The answer depends only on the group's layout and
+        the shape, so every rank agrees."""
         import os
 
-        if os.environ.get("DIE_TP_FUSED", "1") == "0" or not 0 < n_tiles <= SIG_BLOCKS:
+        if os.environ.get("DIE_TP_FUSED", "1") == "0":
             return False
-        return (0 < grid and grid * self.ranks_per_gpu <= self.cus) or n_tiles * self.ranks_per_gpu * 2 <= self.cus
+        return fused_exchange_ok(n_tiles, grid, per_cu, self.ranks_per_gpu, self.cus)
 
     def row_parallel_residual(self, x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, ssp: torch.Tensor,
-                              counters: torch.Tensor, wr: int, kc: int, sk: int, tiled: bool) -> None:
+                              counters: torch.Tensor, wr: int, kc: int, sk: int, tiled: bool,
+                              half_ring: bool = False) -> None:
         """resid += sum over the group of x @ w^T (this rank's K shard), ssp [N / wr, 128] = per-tile row sums of
         squares of the new residual: ONE launch (decode GEMM mode 3 whose tiles' last arrivers run the one-shot
         exchange). Every rank must make the same call."""
@@ -137,7 +159,8 @@ class CustomAllReduce:
 
         m, n = x.shape[0], w.shape[0]
         slab = torch.empty(sk, m, n, dtype=torch.float32, device=x.device)
-        _kern().gemm_decode_car(slab, x, w, 3 | (32 if tiled else 0), wr, kc, sk, ops.DECODE_GEMM_NT, resid, ssp,
+        _kern().gemm_decode_car(slab, x, w, 3 | (32 if tiled else 0) | (64 if half_ring else 0), wr, kc, sk,
+                                ops.DECODE_GEMM_NT, resid, ssp,
                                 counters, self.rank, self.bufs, self.sigs, self.ctl, self.cap)
 
     def read_ctl(self) -> List[int]:

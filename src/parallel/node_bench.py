@@ -272,7 +272,9 @@ def tp_wave_part(a: NodeBenchArgs, rank: int, world: int, dev: torch.device) -> 
                 outs += eng.generate(w, sp)
             el = time.perf_counter() - t0
             st = eng.stats
-            steps = max(1, st["steps"] - st0["steps"])
+            # decode steps, not engine iterations: every request's first token comes from its prefill, the
+            # other gen_len - 1 from decode steps (an engine iteration is a whole window of them)
+            steps = max(1, (a.gen_len - 1) * a.waves)
             dec = st["decode_time"] - st0["decode_time"]
             car = tp.car
             res.update({
@@ -287,6 +289,9 @@ def tp_wave_part(a: NodeBenchArgs, rank: int, world: int, dev: torch.device) -> 
                 "one_shot_ipc": car is not None,
                 "error_word": bool(car.error()) if car is not None else None,
                 "graphs_replayed": bool(eng.runner.graphs),
+                "decode_windows": st.get("decode_windows", 0) - st0.get("decode_windows", 0),
+                "queued_windows": st.get("queued_windows", 0) - st0.get("queued_windows", 0),
+                "windows_mirrored": getattr(eng.runner, "windows_synced", 0),
                 "rank_weight_gib": round(eng.model.weight_bytes() / 2**30, 2),
                 "engine_init_s": round(init_s, 1),
             })

@@ -111,18 +111,19 @@ class TPContext:
 
         ops.residual_add_sumsq(resid, self.all_reduce(x), ssp)
 
-    def fused_row_parallel(self, n_tiles: int, grid: int = 0) -> bool:
-        """Whether a row-parallel decode projection with ``n_tiles`` column tiles (``grid`` workgroups) runs as ONE
-        launch: the decode
-        GEMM whose tiles' last arrivers exchange their partials one-shot and update the residual
-        (:meth:`row_parallel_residual`), instead of GEMM + all-reduce/residual kernel. Needs the IPC path."""
-        return self.enabled and self.car is not None and self.car.fused_ok(n_tiles, grid)
+    def fused_row_parallel(self, n_tiles: int, grid: int = 0, per_cu: int = 0) -> bool:
+        """Whether a row-parallel decode projection with ``n_tiles`` column tiles (``grid`` workgroups, ``per_cu``
+        resident per CU) runs as ONE launch: the decode GEMM whose tiles' last arrivers exchange their partials
+        one-shot and update the residual (:meth:`row_parallel_residual`), instead of GEMM + all-reduce/residual
+        kernel. Needs the IPC path and the residency rule (custom_allreduce.fused_exchange_ok)."""
+        return self.enabled and self.car is not None and self.car.fused_ok(n_tiles, grid, per_cu)
 
     def row_parallel_residual(self, x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, ssp: torch.Tensor,
-                              counters: torch.Tensor, wr: int, kc: int, sk: int, tiled: bool = False) -> None:
+                              counters: torch.Tensor, wr: int, kc: int, sk: int, tiled: bool = False,
+                              half_ring: bool = False) -> None:
         """resid += all_reduce(x @ w^T) and the next norm's per-tile statistics, in one launch
         (see :meth:`fused_row_parallel`, which the caller checked with this tile's ``n_tiles``)."""
-        self.car.row_parallel_residual(x, w, resid, ssp, counters, wr, kc, sk, tiled)
+        self.car.row_parallel_residual(x, w, resid, ssp, counters, wr, kc, sk, tiled, half_ring)
 
     # --- sequence parallelism (Megatron-SP): the all-reduce split into its two halves around the
     # token-sharded norms. Rows = tokens, padded by the caller to a multiple of world_size.
@@ -210,17 +211,23 @@ class ShardProbeTP(TPContext):
 
         ops.residual_add_sumsq(resid, x, ssp)  # the non-fused path's local launch
 
-    def fused_row_parallel(self, n_tiles: int, grid: int = 0) -> bool:
-        # the fused epilogue's local form: the row-parallel GEMM updates the residual itself (DIE_TP_FUSED=0:
-        # the separate-launch form, for A/B)
-        return os.environ.get("DIE_TP_FUSED", "1") != "0"
+    def fused_row_parallel(self, n_tiles: int, grid: int = 0, per_cu: int = 0) -> bool:
+        # the fused epilogue's local form, under the same residency rule as a real group of one rank per GPU
+        # (so the probe runs the tiles a node would run; DIE_TP_FUSED=0: the separate-launch form, for A/B)
+        if os.environ.get("DIE_TP_FUSED", "1") == "0":
+            return False
+        from src.parallel.custom_allreduce import fused_exchange_ok
 
-    def row_parallel_residual(self, x, w, resid, ssp, counters, wr, kc, sk, tiled=False) -> None:
+        cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count \
+            if torch.cuda.is_available() else 256
+        return fused_exchange_ok(n_tiles, grid, per_cu, 1, cus)
+
+    def row_parallel_residual(self, x, w, resid, ssp, counters, wr, kc, sk, tiled=False, half_ring=False) -> None:
         from src import ops
 
         # the one-launch row-parallel projection minus its exchange (mode 3 on the K shard); the exchange's
         # xGMI cost is not in the probe
-        ops.linear_slab_residual(x, w, resid, ssp, counters, wr, sk, tiled=tiled, kc=kc)
+        ops.linear_slab_residual(x, w, resid, ssp, counters, wr, sk, tiled=tiled, kc=kc, half_ring=half_ring)
 
     def reduce_scatter_rows(self, t: torch.Tensor) -> torch.Tensor:
         n = t.shape[0] // self.world_size

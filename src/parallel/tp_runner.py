@@ -15,6 +15,17 @@ Step protocol (two messages per step):
    RCCL (xGMI); every rank unpacks it on the device into the runner's static
    input buffers.
 
+Decode windows (round 6): a k-step window is ONE such message (kind WINDOW: the
+first step's inputs, the window's [step counter, real rows] words and — when
+the leader re-sent them — the sampling parameters); a continuation window
+queued behind the running one is another (kind CONTINUE: the grown block
+tables and first-step slots, plus its token-row base). Every rank replays its
+graph k times; the graph's tail samples from the all-gathered logits
+(bit-identical on every rank) and advances the inputs on the device, so the
+followers stay in step without a message per step and the leader reads the
+k x n tokens back once per window — the same host cost as the TP=1 engine's
+queued windows (reference hot loop: /root/reference/src/worker.py:152).
+
 Then all ranks run the identical forward — including replaying the same
 captured decode hipGraph — and meet in the two per-layer all-reduces (one-shot
 IPC kernel at decode sizes, fused with the residual add) and the logits
@@ -36,6 +47,7 @@ import logging
 import time
 from typing import Optional
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -53,6 +65,10 @@ class TPGroupFault(RuntimeError):
 
 class TPModelRunner(ModelRunner):
     HEARTBEAT_S = 20.0
+    # decode windows: the leader sends one message per k-step window (and per queued continuation), every rank
+    # replays its captured graph k times and advances its own inputs on the device from the all-gathered
+    # logits' samples (identical on every rank), so a window costs one host round trip on the leader only
+    mirrors_windows = True
     HDR = 8
 
     def __init__(self, model: CausalLM, pool: KVPool, cfg: EngineConfig, max_model_len: int):
@@ -61,9 +77,12 @@ class TPModelRunner(ModelRunner):
         self._last_sync = time.monotonic()
         self.h_hdr = torch.zeros(self.HDR, dtype=torch.int64)  # host (gloo) header
         cap = 3 * self.max_tokens + self.max_seqs * (self.bt_width + 3) + 1
-        self.h_pkt = torch.zeros(cap, dtype=torch.int64, pin_memory=self.is_cuda)
+        cap += 5 * self.max_seqs + 2  # a window's sampling parameters and step-counter words
+        self.h_pkts = [torch.zeros(cap, dtype=torch.int64, pin_memory=self.is_cuda) for _ in range(2)]
+        self._pkt_par = 0
         self.d_pkt = torch.zeros(cap, dtype=torch.int64, device=self.device)
         self.steps_synced = 0
+        self.windows_synced = 0  # decode windows (and continuations) mirrored as one message each
         # the one-shot collectives' sticky error word (custom_allreduce ctl[2]), read back with the tokens
         self.h_fault = torch.zeros(1, dtype=torch.int32, pin_memory=self.is_cuda)
 
@@ -81,38 +100,55 @@ class TPModelRunner(ModelRunner):
                                "its outputs were poisoned and no token of this step is returned")
 
     # ------------------------------------------------------------ protocol
+    KIND_WINDOW, KIND_CONTINUE = 4, 5
+
     def _fields(self, kind: int, a: int, b: int, d: int):
-        """(device buffer view, rows) of the step's inputs, in payload order."""
+        """(device buffer, host staging buffer, rows) of the step's inputs, in payload order."""
         if kind == self.KIND_PREFILL:
             t, n, nd = a, b, d
-            out = [(self.d_ids, t), (self.d_pos, t), (self.d_slots, t), (self.d_ctx, n), (self.d_bt, n),
-                   (self.d_cu, n + 1)]
-            return out + [(self.d_last, nd)] if nd else out
-        if kind == self.KIND_DECODE:
+            out = [(self.d_ids, self.h_ids, t), (self.d_pos, self.h_pos, t), (self.d_slots, self.h_slots, t),
+                   (self.d_ctx, self.h_ctx, n), (self.d_bt, self.h_bt, n), (self.d_cu, self.h_cu, n + 1)]
+            return out + [(self.d_last, self.h_last, nd)] if nd else out
+        if kind in (self.KIND_DECODE, self.KIND_WINDOW):
             pad = b
-            return [(self.d_ids, pad), (self.d_pos, pad), (self.d_slots, pad), (self.d_ctx, pad), (self.d_bt, pad)]
+            out = [(self.d_ids, self.h_ids, pad), (self.d_pos, self.h_pos, pad), (self.d_slots, self.h_slots, pad),
+                   (self.d_ctx, self.h_ctx, pad), (self.d_bt, self.h_bt, pad)]
+            if self.supports_multistep:  # the graph's input advance reads [step counter, real rows]
+                out.append((self.d_ctl, self.h_ctl, 2))
+            if kind == self.KIND_WINDOW and d:
+                # the window's steps advance and SAMPLE on every rank: non-greedy rows need the same parameters
+                out += [(self.d_temp, self.h_temp, d), (self.d_topk, self.h_topk, d), (self.d_topp, self.h_topp, d),
+                        (self.d_seed, self.h_seed, d), (self.d_step, self.h_step, d)]
+            return out
+        if kind == self.KIND_CONTINUE:
+            pad, par = a, d
+            return [(self.d_bt, self.h_cbt[par], pad), (self.d_slots, self.h_cslots[par], pad)]
         return []
 
-    def _host_of(self, dbuf: torch.Tensor) -> torch.Tensor:
-        return {id(self.d_ids): self.h_ids, id(self.d_pos): self.h_pos, id(self.d_slots): self.h_slots,
-                id(self.d_ctx): self.h_ctx, id(self.d_bt): self.h_bt, id(self.d_cu): self.h_cu,
-                id(self.d_last): self.h_last}[id(dbuf)]
-
     def _pack(self, kind: int, a: int, b: int, d: int) -> int:
-        pkt = self.h_pkt.numpy()
+        # two pinned staging packets used in turn: the leader rewrites one only after the window whose H2D copy
+        # read it has been waited for (at most a running window and its queued continuation are in flight)
+        self._pkt_par ^= 1
+        pkt = self.h_pkts[self._pkt_par].numpy()
         o = 0
-        for dbuf, rows in self._fields(kind, a, b, d):
-            src = self._host_of(dbuf)[:rows].numpy().reshape(-1)
+        for _, hbuf, rows in self._fields(kind, a, b, d):
+            src = hbuf[:rows].numpy().reshape(-1)
+            if src.dtype == np.float32:
+                src = src.view(np.int32)  # float parameters travel as their bit patterns
             pkt[o:o + src.size] = src
             o += src.size
         return o
 
     def _unpack(self, kind: int, a: int, b: int, d: int) -> None:
         o = 0
-        for dbuf, rows in self._fields(kind, a, b, d):
+        for dbuf, _, rows in self._fields(kind, a, b, d):
             view = dbuf[:rows]
             n = view.numel()
-            view.copy_(self.d_pkt[o:o + n].view(view.shape))  # int64 -> int32 where the buffer is int32
+            src = self.d_pkt[o:o + n]
+            if view.dtype == torch.float32:
+                view.copy_(src.to(torch.int32).view(torch.float32).view(view.shape))
+            else:
+                view.copy_(src.view(view.shape))  # int64 -> int32 where the buffer is int32
             o += n
 
     def _bcast(self, t: torch.Tensor) -> None:
@@ -128,9 +164,20 @@ class TPModelRunner(ModelRunner):
         self.h_hdr.copy_(torch.tensor([kind, a, b, c, d, nw, 0, 0], dtype=torch.int64))
         self.tp.broadcast_host(self.h_hdr)
         if nw:
-            self.d_pkt[:nw].copy_(self.h_pkt[:nw], non_blocking=self.is_cuda)
+            self.d_pkt[:nw].copy_(self.h_pkts[self._pkt_par][:nw], non_blocking=self.is_cuda)
             self._bcast(self.d_pkt[:nw])
         self.steps_synced += 1
+
+    def _sync_window(self, n: int, pad: int, k: int) -> None:
+        """One message per k-step window: the first step's inputs (and the sampling parameters when this window
+        re-sent them); every rank then replays its graph k times and advances its inputs on the device."""
+        self._sync_step(self.KIND_WINDOW, n, pad, k, self._samp_sent)
+        self.windows_synced += 1
+
+    def _sync_continuation(self, par: int, pad: int, k: int, base: int) -> None:
+        """A continuation window queued behind the running one: the grown block tables and first-step slots."""
+        self._sync_step(self.KIND_CONTINUE, pad, k, base, par)
+        self.windows_synced += 1
 
     def idle_tick(self) -> None:
         if self.tp.enabled and self.tp.rank == 0 and time.monotonic() - self._last_sync > self.HEARTBEAT_S:
@@ -157,6 +204,20 @@ class TPModelRunner(ModelRunner):
                 self._unpack(kind, a, b, d)
             if kind == self.KIND_PREFILL:
                 self._exec_prefill(a, b, c, d, True)
+            elif kind == self.KIND_WINDOW:
+                pad, k = b, c
+                self._pre_embed(pad)
+                g = self.graphs[pad]
+                for _ in range(k):
+                    g.replay()
+                self.windows_synced += 1
+            elif kind == self.KIND_CONTINUE:
+                pad, k, base = a, b, c
+                self.d_ctl[0:1].fill_(base)
+                g = self.graphs[pad]
+                for _ in range(k):
+                    g.replay()
+                self.windows_synced += 1
             else:
                 self._exec_decode(a, b)
             self.steps_synced += 1

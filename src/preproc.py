@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import asyncio
 import concurrent.futures as cf
+import os
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -124,31 +125,115 @@ def normalize_request(inputs: Any, tokenizer=None, max_model_len: Optional[int] 
                             return_text=bool(inputs.get("return_text", True)))
 
 
-def _encode_batch(texts: List[str], vocab_size: int) -> List[List[int]]:
-    tok = ByteTokenizer(vocab_size)
-    return [tok.encode(t) for t in texts]
+_POOL_TOKENIZERS: Dict[Tuple[Optional[str], int], Any] = {}
 
 
-def _decode_batch(seqs: List[List[int]], vocab_size: int) -> List[str]:
-    tok = ByteTokenizer(vocab_size)
-    return [tok.decode(s) for s in seqs]
+def _pool_tokenizer(path: Optional[str], vocab_size: int):
+    """The tokenizer of a pool process (loaded once per process and kept)."""
+    key = (path, vocab_size)
+    tok = _POOL_TOKENIZERS.get(key)
+    if tok is None:
+        tok = _POOL_TOKENIZERS[key] = load_tokenizer(path, vocab_size)
+    return tok
+
+
+def _encode_batch(texts: List[str], vocab_size: int, path: Optional[str] = None) -> Tuple[List[List[int]], int]:
+    tok = _pool_tokenizer(path, vocab_size)
+    return [list(tok.encode(t)) for t in texts], os.getpid()
+
+
+def _decode_batch(seqs: List[List[int]], vocab_size: int, path: Optional[str] = None) -> Tuple[List[str], int]:
+    tok = _pool_tokenizer(path, vocab_size)
+    return [tok.decode(s) for s in seqs], os.getpid()
+
+
+def _warm(path: Optional[str], vocab_size: int) -> int:
+    _pool_tokenizer(path, vocab_size)
+    return os.getpid()
 
 
 class PreprocPool:
-    """Tokenise / detokenise in worker processes so the serving loop never
-    spends its own time on it."""
+    """Tokenise / detokenise in separate processes so that the serving loop never spends its own time on it
+    (the reference's "pre/post-processing in a separate process", `/root/reference/README.md:15,96-98`).
 
-    def __init__(self, processes: int = 2, vocab_size: int = 128256):
+    Requests that arrive in the same event-loop turn are coalesced into ONE call to the pool (one pickle round
+    trip for a burst of prompts), up to ``max_batch`` texts per call. The processes are started with ``spawn``
+    (never ``fork``: the worker process holds a HIP context and an engine thread) and warmed at construction, so
+    the first request does not pay the interpreter start-up. ``pids`` records which processes did the work."""
+
+    def __init__(self, processes: int = 2, vocab_size: int = 128256, tokenizer_path: Optional[str] = None,
+                 max_batch: int = 64):
+        import multiprocessing as mp
+
         self.vocab_size = vocab_size
-        self._pool = cf.ProcessPoolExecutor(max_workers=processes)
+        self.path = tokenizer_path
+        self.max_batch = max_batch
+        self._pool = cf.ProcessPoolExecutor(max_workers=processes, mp_context=mp.get_context("spawn"))
+        self.pids: set = set()
+        self.calls = 0
+        self.items = 0
+        self._pending: Dict[str, List[Tuple[Any, asyncio.Future]]] = {"enc": [], "dec": []}
+        self._scheduled: Dict[str, bool] = {"enc": False, "dec": False}
+        # start every process now (and load its tokenizer): a cold spawn costs ~0.1-1 s
+        warm = [self._pool.submit(_warm, self.path, vocab_size) for _ in range(processes)]
+        for f in warm:
+            self.pids.add(f.result(timeout=120))
 
     async def encode(self, texts: List[str]) -> List[List[int]]:
         loop = asyncio.get_running_loop()
-        return await loop.run_in_executor(self._pool, _encode_batch, texts, self.vocab_size)
+        out, pid = await loop.run_in_executor(self._pool, _encode_batch, list(texts), self.vocab_size, self.path)
+        self._account(pid, len(texts))
+        return out
 
     async def decode(self, seqs: List[List[int]]) -> List[str]:
         loop = asyncio.get_running_loop()
-        return await loop.run_in_executor(self._pool, _decode_batch, seqs, self.vocab_size)
+        out, pid = await loop.run_in_executor(self._pool, _decode_batch, [list(s) for s in seqs], self.vocab_size,
+                                              self.path)
+        self._account(pid, len(seqs))
+        return out
+
+    def _account(self, pid: int, n: int) -> None:
+        self.pids.add(pid)
+        self.calls += 1
+        self.items += n
+
+    # --- coalesced single-item forms (the serving path)
+    def encode_one(self, text: str) -> "asyncio.Future":
+        return self._enqueue("enc", text)
+
+    def decode_one(self, ids: List[int]) -> "asyncio.Future":
+        return self._enqueue("dec", list(ids))
+
+    def _enqueue(self, kind: str, item: Any) -> "asyncio.Future":
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        self._pending[kind].append((item, fut))
+        if not self._scheduled[kind]:
+            self._scheduled[kind] = True
+            loop.call_soon(self._flush, kind)
+        return fut
+
+    def _flush(self, kind: str) -> None:
+        self._scheduled[kind] = False
+        batch, self._pending[kind] = self._pending[kind], []
+        for i in range(0, len(batch), self.max_batch):
+            asyncio.ensure_future(self._run(kind, batch[i:i + self.max_batch]))
+
+    async def _run(self, kind: str, batch: List[Tuple[Any, asyncio.Future]]) -> None:
+        items = [x for x, _ in batch]
+        try:
+            res = await (self.encode(items) if kind == "enc" else self.decode(items))
+        except Exception as e:  # noqa: BLE001 — every waiter of the batch gets the failure
+            for _, f in batch:
+                if not f.done():
+                    f.set_exception(e)
+            return
+        for (_, f), r in zip(batch, res):
+            if not f.done():
+                f.set_result(r)
+
+    def stats(self) -> Dict[str, Any]:
+        return {"processes": sorted(self.pids), "calls": self.calls, "items": self.items}
 
     def close(self) -> None:
         self._pool.shutdown(wait=False, cancel_futures=True)

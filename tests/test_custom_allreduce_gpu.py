@@ -128,6 +128,14 @@ def _worker(rank, world, port, q):
         gemm_ok = gemm_ok and torch.allclose(sspt.sum(0)[:m].cpu(), got.pow(2).sum(-1), rtol=1e-4, atol=1e-2)
         replay_ok.append(gemm_ok)
         out["fused_gemm"] = (gemm_ok, resid.clone().cpu())
+        # the half-LDS ring (two workgroups per CU, the 70B TP=8 shard's residency form): bit-identical result
+        resid_h = resid0.clone()
+        sspt_h = torch.zeros_like(sspt)
+        car.row_parallel_residual(xs, wsh, resid_h, sspt_h, cnt, wr, kc, sk, False, half_ring=True)
+        torch.cuda.synchronize()
+        half_ok = torch.equal(resid_h, resid) and torch.equal(sspt_h, sspt)
+        replay_ok.append(half_ok)
+        out["fused_gemm_half_ring"] = (half_ok, resid_h.cpu())
         gg2 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(gg2):
             car.row_parallel_residual(xs, wsh, resid, sspt, cnt, wr, kc, sk, False)
@@ -174,9 +182,9 @@ def test_custom_allreduce_ranks_one_gpu(world):
         assert all(replay_ok), replay_ok
         assert not err
         # one epoch per executed call (not the captures): sizes, graph warm-up, 5 replays, fused, 2 gathers,
-        # the fused GEMM eagerly and 3 replays of it
-        assert ctl[0] == len(SIZES) + 1 + 5 + 1 + 2 + 1 + 3 and ctl[1] == 0, ctl
-    for n in SIZES + ["fused_gemm", "fused_gemm_replayed"]:
+        # the fused GEMM eagerly (full and half-LDS ring) and 3 replays of it
+        assert ctl[0] == len(SIZES) + 1 + 5 + 1 + 2 + 2 + 3 and ctl[1] == 0, ctl
+    for n in SIZES + ["fused_gemm", "fused_gemm_half_ring", "fused_gemm_replayed"]:
         for r in range(1, world):
             assert (res[0][2][n] == res[r][2][n]).all()  # bit-identical on every rank
     assert all(p.exitcode == 0 for p in procs)

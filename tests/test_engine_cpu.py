@@ -340,3 +340,35 @@ def test_lm_head_argmax_candidates_are_never_left_stale():
     with pytest.raises(ValueError):
         m.compute_logits(h, argmax_parts=torch.zeros(4, 8, 2, dtype=torch.int32))
     assert m.compute_logits(h).shape == (4, m.arch.vocab_size)
+
+
+def test_decode_weight_layout_choice(monkeypatch):
+    """EngineConfig.decode_weight_layout: "auto" drops the tile-order decode weight copies when
+    the KV pool is the constraint — kv_capacity_priority (config 5), or an explicit num_kv_blocks the HBM left
+    after the copies cannot hold — and keeps them otherwise; explicit layouts win; the engine reports its choice."""
+    import src.engine.llm_engine as le
+    from src.config import EngineConfig
+    from src.models.presets import get_preset
+
+    class M:
+        arch = get_preset("llama3-8b")
+        hkv = 8
+
+        def decode_copy_bytes(self, buckets):
+            return 13 << 30
+
+    per_block = le.KVPool.bytes_per_block(32, 8, 16, 128)  # 2 MiB
+    monkeypatch.setattr(le, "plan_kv_blocks", lambda arch, model, cfg, dev: 100000)
+    cuda = torch.device("cuda")
+    choose = le.choose_decode_weight_layout
+    assert choose(M(), EngineConfig(), cuda, [32]) == "tiled"
+    assert choose(M(), EngineConfig(kv_capacity_priority=True), cuda, [32]) == "single"
+    assert choose(M(), EngineConfig(kv_capacity_priority=True, decode_weight_layout="tiled"), cuda, [32]) == "tiled"
+    assert choose(M(), EngineConfig(decode_weight_layout="single"), cuda, [32]) == "single"
+    room = 100000 - (13 << 30) // per_block
+    assert choose(M(), EngineConfig(num_kv_blocks=room), cuda, [32]) == "tiled"
+    assert choose(M(), EngineConfig(num_kv_blocks=room + 1), cuda, [32]) == "single"
+    with pytest.raises(ValueError):
+        choose(M(), EngineConfig(decode_weight_layout="bogus"), cuda, [32])
+    eng = LLMEngine.from_preset("llama-tiny", device="cpu", cfg=EngineConfig(num_kv_blocks=64), max_model_len=128)
+    assert eng.get_stats()["decode_weight_layout"] == "row-major"  # no tile-order copies off the GPU

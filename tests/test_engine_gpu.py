@@ -221,11 +221,20 @@ def _tp_gpu_worker(rank, world, port, q, preset, moe_parallel="tp", sp=False, gr
             obj.eos_token_id = None
             outs = obj.generate(TP_PROMPTS, SamplingParams(max_tokens=8))
             replayed = bool(obj.runner.graphs)
+            windows = obj.runner.windows_synced
+            if graphs:
+                # non-greedy windows: every rank samples and advances its own inputs, so they must draw the same
+                # tokens (the sampling parameters travel with the window message)
+                obj.generate(TP_PROMPTS, SamplingParams(max_tokens=12, temperature=0.9, top_k=40, top_p=0.9, seed=11))
             obj.runner.stop_followers()
+            torch.cuda.synchronize()
             fused = bool(obj.model.decode_plan(4).get("tp_fused"))
-            q.put((outs, tp.car is not None, replayed, bool(tp.car.error()) if tp.car is not None else None, fused))
+            q.put((0, (outs, tp.car is not None, replayed, bool(tp.car.error()) if tp.car is not None else None, fused,
+                       windows, obj.runner.d_tokens.cpu())))
         else:
             obj.follower_loop()
+            torch.cuda.synchronize()
+            q.put((rank, obj.d_tokens.cpu()))
     finally:
         dist.destroy_process_group()
 
@@ -260,12 +269,18 @@ def test_tensor_parallel_on_one_gpu(preset, moe_parallel, sp, world, graphs):
              for r in range(world)]
     for p in procs:
         p.start()
-    got, used_car, replayed, car_err, fused = q.get(timeout=600)
+    res = dict(q.get(timeout=600) for _ in range(world))
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
+    got, used_car, replayed, car_err, fused, windows, toks0 = res[0]
     assert used_car and car_err is False  # all-reduces / logits all-gather on the one-shot IPC kernels
     assert replayed == graphs             # graphs: decode steps replayed hipGraphs on every rank
+    # graphs: decode runs in multi-step windows, one message per window; every rank's device-side token rows
+    # (greedy then sampled windows) are identical
+    assert (windows > 0) == graphs, windows
+    for r in range(1, world):
+        assert torch.equal(res[r], toks0), r
     # dense decode: o / down as ONE launch each (the exchange in the GEMM's tile epilogue): the grids of all
     # ranks sharing the GPU fit on it at once (llama-mini: 16-128 workgroups per rank)
     assert fused == (preset == "llama-mini"), fused

@@ -897,3 +897,44 @@ def test_sample_advance_matches_sample_then_advance(dev, rows, n_real):
     ssp_ref = torch.zeros(1, ops.SSP_LD, device=dev)
     h_ref, _ = ops.embed_sumsq(a["ids"][:rows], table, ssp_ref)
     assert torch.equal(h_out, h_ref) and torch.equal(ssp_out[0, :rows], ssp_ref[0, :rows])
+
+
+@pytest.mark.parametrize("wr", [48, 96, 112])
+def test_lm_head_argmax_refuses_non_power_of_two_lanes(dev, wr):
+    """The candidate epilogue merges a row's wr / 8 lanes with xor shuffles: tiles whose lane count is not a power
+    of two (wr = 48 / 96 / 112) would mix rows, so the launcher refuses them instead of writing wrong candidates
+    (ADVICE r5)."""
+    m, n, k = 4, wr * 8, 512
+    x = torch.randn(m, k, device=dev).to(torch.bfloat16)
+    w = (torch.randn(n, k, device=dev) * 0.02).to(torch.bfloat16)
+    wt = ops.gd_pack_weights(w, wr, kc=128)
+    parts = torch.zeros(m, n // wr, 2, dtype=torch.int32, device=dev)
+    with pytest.raises(RuntimeError):
+        ops.linear_tiled_argmax(x, wt, wr, 128, parts)
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("n,k,wr,kc,sk,rows", [(8192, 1024, 32, 128, 1, 32), (8192, 3584, 32, 256, 1, 32),
+                                               (8192, 3584, 32, 256, 1, 7), (4096, 2048, 32, 128, 2, 32)])
+def test_half_ring_residual_gemm_matches_full_ring(dev, n, k, wr, kc, sk, rows):
+    """The half-LDS ring of the residual-updating decode GEMM (mode 3, two workgroups per CU: the TP exchange's
+    residency form at the 70B TP=8 shard's o / down shapes) gives bit-identical residual and statistics to the full
+    ring, and its occupancy is what the residency rule assumes (2 per CU vs 1)."""
+    assert ops.gd_occupancy(3, wr, kc, sk, 32, False) == 1
+    assert ops.gd_occupancy(3, wr, kc, sk, 32, True) >= 2
+    g = torch.Generator(device=dev).manual_seed(n + k + rows)
+    x = (torch.randn(rows, k, device=dev, generator=g) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(n, k, device=dev, generator=g) * 0.03).to(torch.bfloat16)
+    wt = ops.gd_pack_weights(w, wr, kc=kc)
+    r0 = torch.randn(rows, n, device=dev, generator=g).to(torch.bfloat16)
+    outs = []
+    for half in (False, True):
+        r = r0.clone()
+        ssp = torch.zeros(n // wr, ops.SSP_LD, device=dev)
+        cnt = torch.zeros(n // wr, dtype=torch.int32, device=dev)
+        ops.linear_slab_residual(x, wt, r, ssp, cnt, wr, sk, tiled=True, kc=kc, half_ring=half)
+        outs.append((r, ssp))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    want = r0.float() + x.float() @ w.float().t()
+    assert float((outs[1][0].float() - want).abs().max()) < 0.1
