@@ -108,10 +108,14 @@ def parse(argv=None):
     # the post-timed-region node section (configs 3 / 4 and the cross-GPU transports)
     p.add_argument("--cross-gpu", choices=["auto", "on", "off"], default="auto",
                    help="auto: on for multi-rank GPU runs; on: also on CPU (plumbing tests)")
-    p.add_argument("--cross-gpu-budget-s", type=float, default=420.0, help="watchdog for the whole node section")
+    p.add_argument("--cross-gpu-budget-s", type=float, default=720.0, help="watchdog for the whole node section")
     p.add_argument("--disagg-preset", default=None, help="config 3 model (default: --preset)")
     p.add_argument("--tp-wave-preset", default="llama3-70b", help="config 4 model")
     p.add_argument("--tp-wave-min-world", type=int, default=8, help="run the config-4 TP wave from this many ranks")
+    p.add_argument("--lb-preset", default="mixtral-8x7b", help="config 5 model (one worker per rank)")
+    p.add_argument("--lb-kv-blocks", type=int, default=2048, help="config 5: KV blocks per worker (below the working set)")
+    p.add_argument("--lb-requests-per-worker", type=int, default=32)
+    p.add_argument("--no-lb-serving", action="store_true", help="skip the config-5 part of the node section")
     p.add_argument("--node-section-only", action="store_true",
                    help="internal: the node section alone (the child run that rank 0 of a multi-rank run starts)")
     p.add_argument("--verbose", action="store_true")
@@ -282,18 +286,21 @@ def cross_gpu_section(args, rank, world, dev, on_gpu, state, progress: bool = Fa
     """Configs 3 / 4 and the transports, after the timed region. Every rank runs every part in the same order;
     ``state["part"]`` names the running part. progress (the child run's rank 0): one stdout line as each part
     starts and ends, so the parent knows what finished if the run dies or stalls."""
-    from src.parallel.node_bench import NodeBenchArgs, disagg_part, free_device_memory, tp_wave_part
+    from src.parallel.node_bench import NodeBenchArgs, disagg_part, free_device_memory, lb_serving_part, tp_wave_part
 
     free_device_memory()  # the timed replicas' weights, KV pools and graphs
     cpu = dist.new_group(list(range(world)), backend="gloo") if dist.get_backend() != "gloo" else None
     out: dict = {}
     nb = NodeBenchArgs(preset=args.disagg_preset or args.preset, tp_preset=args.tp_wave_preset, batch=args.batch,
                        prompt_len=args.prompt_len, gen_len=args.gen_len, max_model_len=args.max_model_len,
-                       max_latency_ms=args.max_latency_ms, graphs=not args.no_graph)
+                       max_latency_ms=args.max_latency_ms, graphs=not args.no_graph, lb_preset=args.lb_preset,
+                       lb_kv_blocks=args.lb_kv_blocks, lb_requests_per_worker=args.lb_requests_per_worker)
     parts = []
     if on_gpu:
         parts.append("xgpu_probe")
     parts.append("disagg")
+    if not args.no_lb_serving:
+        parts.append("lb_serving")
     if world >= args.tp_wave_min_world:
         parts.append("tp_wave")
     for part in parts:
@@ -310,6 +317,8 @@ def cross_gpu_section(args, rank, world, dev, on_gpu, state, progress: bool = Fa
                 r = xgpu_probe(rank, world, dev, rccl=not args.same_device)
             elif part == "disagg":
                 r = disagg_part(nb, rank, world, dev, cpu)
+            elif part == "lb_serving":
+                r = lb_serving_part(nb, rank, world, dev, cpu)
             else:
                 r = tp_wave_part(nb, rank, world, dev)
         except Exception as e:  # noqa: BLE001 — reported; the timed result stands on its own

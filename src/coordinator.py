@@ -163,7 +163,7 @@ class Coordinator:
         lb = self.lbs.get(key)
         if lb is None:
             lb = self.lbs[key] = LoadBalancer(strategy=self.strategy,
-                                              health_check_interval=self.health_check_interval)
+                                              health_check_interval=self.health_check_interval, model=model)
             if self.server is not None:
                 asyncio.get_event_loop().create_task(lb.start())
         return lb
@@ -359,8 +359,9 @@ class Coordinator:
                 break
             relayed = False
             try:
-                async with lb.track(wid, cost):
-                    async for frame in self.rpc.stream(addr, wmsg, timeout=self.request_timeout_s):
+                async with lb.track(wid, cost) as seq:
+                    async for frame in self.rpc.stream(addr, dict(wmsg, lb=lb.token, lb_seq=seq),
+                                                       timeout=self.request_timeout_s):
                         if isinstance(frame, dict) and frame.get("done") is False:
                             relayed = True
                             await emit(frame)
@@ -428,8 +429,9 @@ class Coordinator:
                 self.stats["retries"] += 1
             tried += 1
             try:
-                async with lb.track(wid, cost):
-                    rep = await self.rpc.call(addr, msg, timeout=min(self.request_timeout_s, left))
+                async with lb.track(wid, cost) as seq:
+                    rep = await self.rpc.call(addr, dict(msg, lb=lb.token, lb_seq=seq) if cost else msg,
+                                              timeout=min(self.request_timeout_s, left))
                     if not isinstance(rep, dict):
                         raise RPCError("malformed reply")
                     lb.observe(wid, rep.pop("engine_load", None))

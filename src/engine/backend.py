@@ -43,6 +43,8 @@ def engine_config_from(config: ModelConfig) -> EngineConfig:
         enable_prefix_caching=config.enable_prefix_caching,
         kv_block_ttl_s=ov.get("kv_block_ttl_s"),
         use_cuda_graph=config.use_cuda_graph,
+        kv_capacity_priority=bool(ov.get("kv_capacity_priority", False)),
+        decode_weight_layout=str(ov.get("decode_weight_layout", "auto")),
     )
 
 

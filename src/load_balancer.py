@@ -32,10 +32,12 @@ added on top. Workers that report nothing (mock models) keep the latency EWMA
 from __future__ import annotations
 
 import asyncio
+import collections
 import contextlib
 import logging
 import random
 import time
+import uuid
 from dataclasses import dataclass, field
 from enum import Enum
 from typing import Any, Dict, List, Optional, Tuple
@@ -63,8 +65,16 @@ class WorkerStats:
     probe_count: int = 0
     probe_latency: float = 0.0
     report: Optional[Dict[str, Any]] = None   # the worker's last engine_load (see module doc)
-    unreported_requests: int = 0              # dispatched here since that report
-    unreported_prompt_tokens: int = 0
+    # dispatches the last report does not cover yet: (sequence number, prompt tokens) in dispatch order
+    unreported: "collections.deque" = field(default_factory=collections.deque)
+
+    @property
+    def unreported_requests(self) -> int:
+        return len(self.unreported)
+
+    @property
+    def unreported_prompt_tokens(self) -> int:
+        return sum(p for _, p in self.unreported)
 
     @property
     def avg_latency(self) -> float:
@@ -81,6 +91,7 @@ class LoadBalancer:
         probe: str = "rpc",
         latency_alpha: float = 0.2,
         seed: Optional[int] = None,
+        model: Optional[str] = None,
     ):
         if isinstance(strategy, str):
             strategy = LoadBalancerStrategy(strategy)
@@ -96,7 +107,11 @@ class LoadBalancer:
         self.groups: Dict[str, str] = {}
         self._rr: Dict[Optional[str], int] = {}
         self._rng = random.Random(seed)
-        self._cost: Optional[Tuple[int, int]] = None
+        # the model this balancer serves (a multi-model worker's health answer carries one report per model) and
+        # the token + sequence numbers of its dispatches, which workers echo in their reports (observe)
+        self.model = model
+        self.token = uuid.uuid4().hex[:12]
+        self._seq = 0
         self._cost_ewma: Optional[Tuple[float, float]] = None
         self._running = False
         self._health_check_task: Optional[asyncio.Task] = None
@@ -153,8 +168,8 @@ class LoadBalancer:
     def pick(self, worker_id: Optional[str] = None, group: Optional[str] = None,
              exclude: Optional[List[str]] = None, cost: Optional[Tuple[int, int]] = None) -> Optional[Tuple[str, str]]:
         """Synchronous selection (the coordinator's hot path). ``cost``: (prompt tokens, max output tokens) of the
-        request, when known (least_latency uses it; see the module doc)."""
-        self._cost = cost
+        request, when known (least_latency uses it; see the module doc). The cost travels as an argument, never as
+        balancer state, so concurrent callers on other threads / loops cannot see each other's."""
         if not self.workers:
             return None
         if worker_id:
@@ -166,7 +181,10 @@ class LoadBalancer:
                  and (not exclude or w not in exclude)]
         if not cands:
             return None
-        wid = self._strategy_fns[self.strategy](cands, group)
+        if self.strategy is LoadBalancerStrategy.LEAST_LATENCY:
+            wid = self._least_latency(cands, group, cost)
+        else:
+            wid = self._strategy_fns[self.strategy](cands, group)
         return (wid, self.workers[wid]) if wid else None
 
     def _round_robin(self, ids: List[str], group: Optional[str] = None) -> str:
@@ -182,7 +200,8 @@ class LoadBalancer:
     def _random(self, ids: List[str], group: Optional[str] = None) -> str:
         return self._rng.choice(ids)
 
-    def _least_latency(self, ids: List[str], group: Optional[str] = None) -> str:
+    def _least_latency(self, ids: List[str], group: Optional[str] = None,
+                       cost: Optional[Tuple[int, int]] = None) -> str:
         reported = [w for w in ids if self.worker_stats[w].report is not None]
         if reported:
             # engine-state scoring over the workers that report it; a silent one (just registered, not yet
@@ -191,8 +210,8 @@ class LoadBalancer:
                       and self.worker_stats[w].active_connections == 0]
             if silent:
                 return silent[0]
-            cost = self._cost or self._default_cost()
-            return min(reported, key=lambda w: self.expected_ms(w, cost))
+            c = cost or self._default_cost()
+            return min(reported, key=lambda w: self.expected_ms(w, c))
         cold = [w for w in ids if self.worker_stats[w].ewma_latency is None
                 and self.worker_stats[w].active_connections == 0]
         if cold:
@@ -227,28 +246,48 @@ class LoadBalancer:
         return ((backlog + p) * pf + g * step * share) * kv_pen
 
     # ------------------------------------------------------ accounting
-    def acquire(self, worker_id: str, cost: Optional[Tuple[int, int]] = None) -> None:
+    def acquire(self, worker_id: str, cost: Optional[Tuple[int, int]] = None) -> int:
+        """Count a dispatch; returns its sequence number (sent with the request as ``lb_seq`` next to ``lb`` =
+        :attr:`token`, so that the worker's reports say which dispatches they cover)."""
+        self._seq += 1
         s = self.worker_stats.get(worker_id)
         if s is not None:
             s.active_connections += 1
-            s.unreported_requests += 1
-            if cost:
-                s.unreported_prompt_tokens += int(cost[0])
+            s.unreported.append((self._seq, int(cost[0]) if cost else 0))
         if cost:
             c = self._cost_ewma
             self._cost_ewma = tuple(cost) if c is None else (0.9 * c[0] + 0.1 * cost[0], 0.9 * c[1] + 0.1 * cost[1])
+        return self._seq
 
     def observe(self, worker_id: str, report: Optional[Dict[str, Any]]) -> None:
-        """A worker's engine state (``engine_load`` of a reply or a health answer): replaces the last one; what was
-        dispatched before it is in it."""
+        """A worker's engine state (``engine_load`` of a reply or a health answer) replaces the last one. It covers
+        the dispatches up to its ``lb_seen`` (the highest of this balancer's sequence numbers the worker had
+        received when it built the report): those leave the unreported list, later ones — still on the wire or not
+        yet submitted — stay counted on top (zeroing them herded bursts onto the worker that just
+        replied). A report without ``lb_seen`` (another balancer's, or an older worker) covers everything."""
         if not isinstance(report, dict):
             return
         s = self.worker_stats.get(worker_id)
         if s is None:
             return
         s.report = report
-        s.unreported_requests = 0
-        s.unreported_prompt_tokens = 0
+        seen = report.get("lb_seen")
+        if not isinstance(seen, int) or report.get("lb") not in (None, self.token):
+            s.unreported.clear()
+            return
+        q = s.unreported
+        while q and q[0][0] <= seen:
+            q.popleft()
+
+    def report_of(self, reply: Dict[str, Any]) -> Optional[Dict[str, Any]]:
+        """This balancer's model's engine report in a health answer (one per model on a multi-model worker; ADVICE
+        r5: model B's balancer must not be scored with model A's queue), else None."""
+        per = reply.get("engine_loads")
+        if isinstance(per, dict) and self.model is not None:
+            return per.get(self.model)
+        if self.model is None or reply.get("models") in (None, [self.model]):
+            return reply.get("engine_load")
+        return None
 
     def release(self, worker_id: str) -> None:
         s = self.worker_stats.get(worker_id)
@@ -257,13 +296,13 @@ class LoadBalancer:
 
     @contextlib.asynccontextmanager
     async def track(self, worker_id: str, cost: Optional[Tuple[int, int]] = None):
-        """``async with lb.track(w): ...`` — counts an active request and
-        records its outcome and latency."""
-        self.acquire(worker_id, cost)
+        """``async with lb.track(w) as seq: ...`` — counts an active request (``seq``: its dispatch sequence
+        number, see :meth:`acquire`) and records its outcome and latency."""
+        seq = self.acquire(worker_id, cost)
         t0 = time.perf_counter()
         ok = False
         try:
-            yield
+            yield seq
             ok = True
         finally:
             self.release(worker_id)
@@ -336,9 +375,10 @@ class LoadBalancer:
         if self.probe == "tcp":
             ok, lat = await tcp_connect_probe(addr, self.health_check_timeout)
         else:
-            ok, lat, reply = await self._rpc.probe(addr, self.health_check_timeout)
+            ok, lat, reply = await self._rpc.probe(addr, self.health_check_timeout,
+                                                   {"op": "health", "model": self.model, "lb": self.token})
             if ok and isinstance(reply, dict):
-                self.observe(worker_id, reply.get("engine_load"))
+                self.observe(worker_id, self.report_of(reply))
         s = self.worker_stats.get(worker_id)
         if s is None:
             return

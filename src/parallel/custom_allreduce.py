@@ -60,6 +60,11 @@ def fused_exchange_ok(n_tiles: int, grid: int, per_cu: int, ranks_per_gpu: int, 
     with the full LDS ring) fail both and take the half-LDS ring (two per CU: 256 <= 512 - 16)."""
     if not 0 < n_tiles <= SIG_BLOCKS:
         return False
+    if ranks_per_gpu > 1:
+        # ranks sharing a GPU (the one-GPU tests): another rank's next kernel (a full-LDS GEMM ring) needs a whole
+        # CU, and small-ring waiters spread one per CU would leave none — count one workgroup per CU (measured: 8
+        # ranks on one GPU with half-ring waiters on every CU stalled until the bounded spin)
+        per_cu = min(per_cu, 1)
     if grid > 0 and per_cu > 0 and grid * ranks_per_gpu <= per_cu * cus - residency_margin(cus):
         return True
     return n_tiles * ranks_per_gpu * 2 <= cus

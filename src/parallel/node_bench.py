@@ -9,6 +9,12 @@ data-parallel region (and after that region's engines are freed):
   the sequence to its continuous batch. One wave of ``batch`` x (prompt -> gen) requests per pair, timed;
   req/s, p50 latency, TTFT and how the KV travelled (``kv_path``; anything but ``direct`` on a GPU node is
   reported as a failure).
+* :func:`lb_serving_part` (config 5, N >= 2): Mixtral-8x7B, one worker per GPU (the production Worker +
+  LLMBackend) behind ONE coordinator on rank 0 whose load balancer picks a worker per request
+  (``least_latency`` on the workers' engine reports, then ``round_robin`` for comparison), config 5's
+  mixed-length workload with Zipf-shared prefixes and KV pools smaller than its working set (LRU / TTL
+  evictions): req/s, p50 / p99, TTFT, dispatches per worker, prefix hits, evictions
+  (:mod:`src.parallel.lb_serving`).
 * :func:`tp_wave_part` (config 4, N == 8 by default): Llama-3-70B tensor-parallel over every rank — Megatron
   split, one-shot IPC exchange fused into the row-parallel GEMM epilogue, RCCL for prefill-sized
   all-reduces — one wave served to completion: ms per decode step, req/s of the TP group, whether the fused
@@ -49,6 +55,10 @@ class NodeBenchArgs:
     waves: int = 1
     kv_blocks: int = 8192                # per engine (these parts never need the whole HBM)
     graphs: bool = True
+    lb_preset: str = "mixtral-8x7b"      # config 5 model
+    lb_kv_blocks: int = 2048             # per worker: below the shared-prefix working set, so the pools evict
+    lb_requests_per_worker: int = 32
+    lb_strategies: tuple = ("least_latency", "round_robin")
 
 
 def device_identity(dev: torch.device) -> Dict[str, Any]:
@@ -232,6 +242,94 @@ def _disagg_summary(recs: List[Dict[str, Any]], a: NodeBenchArgs, dev: torch.dev
                 errors.setdefault(r["rank"], f"kv_path {r.get('kv_path')!r}: the KV did not go GPU to GPU directly")
     if errors or len(ok) != len(pre) or not pre:
         out["error"] = errors or "no prefill pair completed"
+    return out
+
+
+# ------------------------------------------------------------------------------------------------ config 5
+def lb_serving_part(a: NodeBenchArgs, rank: int, world: int, dev: torch.device, cpu_group) -> Dict[str, Any]:
+    """Every rank calls this. Returns rank 0's aggregate (other ranks: their own record)."""
+    return asyncio.run(_lb_serving(a, rank, world, dev, cpu_group))
+
+
+async def _lb_serving(a: NodeBenchArgs, rank: int, world: int, dev: torch.device, cpu_group) -> Dict[str, Any]:
+    from src.config import ModelConfig
+    from src.parallel.lb_serving import LBWorkload, make_requests, serve_through_coordinator
+    from src.worker import Worker
+
+    loop = asyncio.get_running_loop()
+
+    async def coll(fn):
+        return await loop.run_in_executor(None, fn)
+
+    arch = _arch_of(a.lb_preset)
+    rec: Dict[str, Any] = {"rank": rank}
+    worker = None
+    t0 = time.perf_counter()
+    try:
+        worker = Worker(f"lb-r{rank}", host="127.0.0.1", port=0, install_signal_handlers=False)
+        cfg = ModelConfig(model_name="moe", model_path="", max_batch_size=a.batch, arch=arch, preset=a.lb_preset,
+                          max_model_len=a.max_model_len + 256, max_latency_ms=a.max_latency_ms,
+                          use_cuda_graph=a.graphs, num_kv_blocks=a.lb_kv_blocks, seed=1234,
+                          overrides={"device": str(dev), "kv_block_ttl_s": 30.0})
+        if not worker.load_model(cfg):
+            raise RuntimeError("worker model failed to load")
+        await worker.start()
+        rec["init_s"] = round(time.perf_counter() - t0, 1)
+    except Exception as e:  # noqa: BLE001 — reported through the gather below
+        rec["error"] = f"worker: {type(e).__name__}: {e}"[:300]
+        worker = None
+    addrs: List[Any] = [None] * world
+    mine = (worker.worker_id, worker.address) if worker is not None else None
+    await coll(lambda: dist.all_gather_object(addrs, mine, group=cpu_group))
+    runs: List[Dict[str, Any]] = []
+    if rank == 0:
+        try:
+            workers = {w: ad for w, ad in (x for x in addrs if x is not None)}
+            if len(workers) != world:
+                raise RuntimeError(f"only {len(workers)} of {world} workers came up")
+            vocab = worker.models["moe"].engine.arch.vocab_size
+            n = a.lb_requests_per_worker * world
+            for i, strat in enumerate(a.lb_strategies):
+                # a fresh prefix set per strategy (the previous run's cached prefixes must not favour the next)
+                # config 5's mix (128-2048 -> 32-256) at serving sizes; scaled down for small test contexts
+                big = a.max_model_len >= 1024
+                pmax = min(2048, a.max_model_len)
+                shape = dict(prompt_min=min(128, pmax // 2), prompt_max=pmax,
+                             gen_choices=(32, 64, 128, 256) if big else (4, 8, 16))
+                wl = LBWorkload(requests=n, concurrency=min(n, 8 * world), seed=100 + i, **shape)
+                warm = make_requests(LBWorkload(requests=2 * world, seed=900 + i, **shape), vocab)
+                runs.append(await serve_through_coordinator(workers, "moe", arch, strat, make_requests(wl, vocab),
+                                                            wl.concurrency, warmup=warm))
+        except Exception as e:  # noqa: BLE001
+            rec["error"] = f"{type(e).__name__}: {e}"[:300]
+    await coll(lambda: dist.barrier(group=cpu_group))  # every worker serves until rank 0's runs are done
+    if worker is not None:
+        try:
+            await worker.shutdown()
+        except Exception:  # noqa: BLE001
+            pass
+    worker = None
+    free_device_memory()
+    recs: List[Any] = [None] * world
+    await coll(lambda: dist.all_gather_object(recs, rec, group=cpu_group))
+    if rank != 0:
+        return rec
+    errors = {r["rank"]: r["error"] for r in recs if r and r.get("error")}
+    out: Dict[str, Any] = {
+        "config": "BASELINE 5: one worker per GPU behind one coordinator; the load balancer picks per request",
+        "model": a.lb_preset, "workers": world, "kv_blocks_per_worker": a.lb_kv_blocks,
+        "workload": "mixed 128-2048 -> 32-256 tokens, Zipf-shared prefixes, closed loop",
+        "runs": runs, "worker_init_s": [r.get("init_s") for r in recs if r],
+    }
+    ll = next((r for r in runs if r.get("strategy") == "least_latency"), None)
+    if ll is not None:
+        out.update({k: ll.get(k) for k in ("req_s", "p50_latency_ms", "p99_latency_ms", "ttft_p50_ms",
+                                           "prefix_hit_rate", "lru_evictions", "ttl_evictions")})
+        out["dispatched_per_worker"] = {w: p["dispatched"] for w, p in ll["per_worker"].items()}
+    if any(r.get("error_count") for r in runs):
+        errors.setdefault(0, f"request errors: {[r.get('errors') for r in runs]}"[:300])
+    if errors or not runs:
+        out["error"] = errors or "no run completed"
     return out
 
 

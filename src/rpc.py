@@ -115,7 +115,8 @@ class RPCClient:
         finally:
             conn.close()
 
-    async def probe(self, address: str, timeout: float = 2.0) -> Tuple[bool, float, Optional[Dict[str, Any]]]:
+    async def probe(self, address: str, timeout: float = 2.0,
+                    msg: Optional[Dict[str, Any]] = None) -> Tuple[bool, float, Optional[Dict[str, Any]]]:
         """Health RPC on a dedicated short-lived connection. Returns
         ``(ok, latency_s, reply)``; the latency is the probe's own round trip
         and is kept apart from request latency statistics."""
@@ -123,7 +124,7 @@ class RPCClient:
         conn = None
         try:
             conn = await self._open(address, timeout)
-            conn.writer.write(pack_frame({"op": "health"}, CODEC_JSON))
+            conn.writer.write(pack_frame(msg or {"op": "health"}, CODEC_JSON))
             await conn.writer.drain()
             reply, _ = await asyncio.wait_for(read_frame(conn.reader), timeout)
             ok = bool(reply.get("success", False)) if isinstance(reply, dict) else False

@@ -73,6 +73,7 @@ class Worker:
         self.metadata = metadata or {}
         self.install_signal_handlers = install_signal_handlers
         self.models: Dict[str, Any] = {}
+        self._lb_seen: Dict[str, int] = {}  # balancer token -> highest dispatch sequence number received
         self.server: Optional[asyncio.AbstractServer] = None
         self._stop_event = asyncio.Event()
         self._start_time = time.time()
@@ -192,8 +193,12 @@ class Worker:
         if op == "health":
             self._probe_count += 1
             failed = self.failed_models()
+            lb = msg.get("lb")
             return {"success": not failed, "worker_id": self.worker_id, "load": self.load(), "failed_models": failed,
-                    "engine_load": self.engine_load(),
+                    "engine_load": self.engine_load(msg.get("model"), lb),
+                    # one report per model: a per-model balancer scores this worker by its own model's engine
+                    "engine_loads": {n: self.engine_load(n, lb) for n in self.models
+                                     if hasattr(self.models[n], "load_report")},
                     "models": list(self.models),
                     "archs": {n: getattr(getattr(m, "config", None), "arch", "mock") for n, m in self.models.items()}}
         if op == "metrics":
@@ -221,13 +226,19 @@ class Worker:
         if op in ("infer", "infer_batch"):
             self._request_count += 1
             self._active += 1
+            lb, lb_seq = msg.get("lb"), msg.get("lb_seq")
+            if isinstance(lb, str) and isinstance(lb_seq, int):  # which of a balancer's dispatches have arrived
+                if lb_seq > self._lb_seen.get(lb, 0):
+                    if len(self._lb_seen) > 256 and lb not in self._lb_seen:
+                        self._lb_seen.clear()
+                    self._lb_seen[lb] = lb_seq
             try:
                 resp = await (self._process_batch(msg) if op == "infer_batch" else self._process_request(msg, emit))
             finally:
                 self._active -= 1
             if not resp.get("success"):
                 self._error_count += 1
-            el = self.engine_load(msg.get("model"))
+            el = self.engine_load(msg.get("model"), lb)
             if el is not None:  # piggybacked for the coordinator's load balancer (least_latency)
                 resp["engine_load"] = el
             return resp
@@ -331,15 +342,20 @@ class Worker:
         loads = [m.load() for m in self.models.values() if hasattr(m, "load")]
         return max(loads) if loads else float(self._active)
 
-    def engine_load(self, model: Optional[str] = None) -> Optional[Dict[str, Any]]:
-        """The engine-state report of ``model`` (default: the first model that has one), or None."""
+    def engine_load(self, model: Optional[str] = None, lb: Optional[str] = None) -> Optional[Dict[str, Any]]:
+        """The engine-state report of ``model`` (default: the first model that has one), or None. ``lb``: the asking
+        balancer's token — the report then says up to which of its dispatch sequence numbers it covers
+        (``lb_seen``, see LoadBalancer.observe)."""
         ms = [self.models[model]] if model in self.models else list(self.models.values())
         for m in ms:
             if hasattr(m, "load_report"):
                 try:
-                    return m.load_report()
+                    r = m.load_report()
                 except Exception:  # noqa: BLE001 - a report must never fail a request
                     return None
+                if lb is not None and lb in self._lb_seen:
+                    r = dict(r, lb=lb, lb_seen=self._lb_seen[lb])
+                return r
         return None
 
     def get_metrics(self) -> Dict[str, Any]:
@@ -394,6 +410,11 @@ def build_arg_parser():
                    help="(role=prefill) host:port of the decode worker that receives the prompt KV")
     p.add_argument("--device", default=None, help="torch device for LLM backends (default cuda:0 / cpu)")
     p.add_argument("--num-kv-blocks", type=int, default=None)
+    p.add_argument("--kv-block-ttl-s", type=float, default=None, help="TTL of cached (released) KV blocks")
+    p.add_argument("--kv-capacity-priority", action="store_true",
+                   help="the KV pool is the constraint: decode weights in one layout (EngineConfig)")
+    p.add_argument("--preproc-processes", type=int, default=0,
+                   help="tokenise / detokenise text in this many separate processes (0: inline)")
     p.add_argument("--coordinator", default=None, help="host:port to register with")
     p.add_argument("--port-file", default=None, help="write the bound port here once listening")
     return p
@@ -409,11 +430,16 @@ async def main(argv=None) -> None:
         overrides["decode_worker"] = args.decode_worker
     if args.device:
         overrides["device"] = args.device
+    if args.kv_block_ttl_s:
+        overrides["kv_block_ttl_s"] = args.kv_block_ttl_s
+    if args.kv_capacity_priority:
+        overrides["kv_capacity_priority"] = True
     cfg = ModelConfig(
         model_name=args.model, model_path=args.model_path, batch_size=min(8, args.max_batch_size),
         max_batch_size=args.max_batch_size, arch=args.arch, preset=args.preset, tp_size=args.tp_size,
         role=args.role, max_model_len=args.max_model_len, max_latency_ms=args.max_latency_ms,
         use_cuda_graph=not args.no_graph, num_kv_blocks=args.num_kv_blocks, overrides=overrides,
+        preproc_processes=args.preproc_processes,
     )
     worker = Worker(worker_id=args.worker_id or f"worker-{os.getpid()}", host=args.host, port=args.port,
                     coordinator=args.coordinator,

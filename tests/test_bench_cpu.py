@@ -118,11 +118,14 @@ def test_bench_gpus_mismatch_under_launcher_refuses():
     assert r.returncode == 2 and not [ln for ln in r.stdout.splitlines() if ln.startswith("{")], r.stdout
 
 
-def test_bench_node_section_configs_3_and_4_on_cpu():
+def test_bench_node_section_configs_3_4_5_on_cpu():
     """The post-timed-region node section over 2 CPU ranks (gloo): config 3 (prefill worker on rank 0 -> decode
-    worker on rank 1 over the RPC; on a CPU engine the KV rides the socket: kv_path 'wire') and config 4 (a TP=2
-    engine over both ranks) both serve a wave; their status reaches the top level."""
-    r = _self_launched(2, ["--cross-gpu", "on", "--tp-wave-min-world", "2", "--tp-wave-preset", "llama-tiny"])
+    worker on rank 1 over the RPC; on a CPU engine the KV rides the socket: kv_path 'wire'), config 5 (a worker per
+    rank behind one coordinator on rank 0: least_latency then round_robin, mixed lengths with shared prefixes,
+    small KV pools that evict) and config 4 (a TP=2 engine over both ranks) all serve; their status reaches the top
+    level."""
+    r = _self_launched(2, ["--cross-gpu", "on", "--tp-wave-min-world", "2", "--tp-wave-preset", "llama-tiny",
+                           "--lb-preset", "mixtral-tiny", "--lb-kv-blocks", "64", "--lb-requests-per-worker", "6"])
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert res["cross_gpu_status"] == "ok", res["notes"].get("cross_gpu")
@@ -132,6 +135,13 @@ def test_bench_node_section_configs_3_and_4_on_cpu():
     assert d["pairs"] == 1 and d["req_s_total"] > 0 and d["kv_path"] == "wire" and d["ttft_p50_ms"] > 0
     t = cross["tp_wave"]
     assert t["tp"] == 2 and t["requests"] == 4 and t["all_tokens"] and t["req_s"] > 0
+    lb = cross["lb_serving"]
+    assert lb["workers"] == 2 and [x["strategy"] for x in lb["runs"]] == ["least_latency", "round_robin"], lb
+    for run in lb["runs"]:
+        assert run["requests"] == 12 and run["error_count"] == 0 and run["req_s"] > 0, run
+        assert sum(p["dispatched"] for p in run["per_worker"].values()) == 12, run
+    assert lb["prefix_hit_rate"] is not None and lb["p99_latency_ms"] >= lb["p50_latency_ms"] > 0, lb
+    assert lb["lru_evictions"] >= 0 and lb["ttl_evictions"] >= 0 and lb["dispatched_per_worker"], lb
 
 
 def test_bench_node_section_child_run_failure_and_stall():

@@ -104,7 +104,7 @@ def _worker(rank, world, port, q):
         # layer's o / down projection in one launch): resid += bf16(sum over ranks of bf16(x_r @ w_r^T)), per-tile
         # row statistics of the new residual, bit-identical on every rank; eagerly, then under hipGraph replay
         m, n, ks = 19, 1024, 512
-        wr, kc, sk = 64, 256, 2  # 16 column tiles: every rank's waiting tiles fit beside the rest, even at 8 ranks
+        wr, kc, sk = 64, 128, 2  # 16 column tiles (a tile with a half-LDS ring form): every rank's waiting tiles fit beside the rest, even at 8 ranks
         assert car.fused_ok(n // wr), (n // wr, car.ranks_per_gpu, car.cus)
         g = torch.Generator(device="cuda").manual_seed(50 + rank)
         xs = (torch.randn(m, ks, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
@@ -134,6 +134,13 @@ def _worker(rank, world, port, q):
         car.row_parallel_residual(xs, wsh, resid_h, sspt_h, cnt, wr, kc, sk, False, half_ring=True)
         torch.cuda.synchronize()
         half_ok = torch.equal(resid_h, resid) and torch.equal(sspt_h, sspt)
+        # and at 4 rows (the 16-row activation image): against the full ring at the same rows
+        r4f, r4h = resid0[:4].clone(), resid0[:4].clone()
+        s4f, s4h = torch.zeros_like(sspt), torch.zeros_like(sspt)
+        car.row_parallel_residual(xs[:4], wsh, r4f, s4f, cnt, wr, kc, sk, False)
+        car.row_parallel_residual(xs[:4], wsh, r4h, s4h, cnt, wr, kc, sk, False, half_ring=True)
+        torch.cuda.synchronize()
+        half_ok = half_ok and torch.equal(r4f, r4h) and torch.equal(s4f, s4h)
         replay_ok.append(half_ok)
         out["fused_gemm_half_ring"] = (half_ok, resid_h.cpu())
         gg2 = torch.cuda.CUDAGraph()
@@ -183,7 +190,7 @@ def test_custom_allreduce_ranks_one_gpu(world):
         assert not err
         # one epoch per executed call (not the captures): sizes, graph warm-up, 5 replays, fused, 2 gathers,
         # the fused GEMM eagerly (full and half-LDS ring) and 3 replays of it
-        assert ctl[0] == len(SIZES) + 1 + 5 + 1 + 2 + 2 + 3 and ctl[1] == 0, ctl
+        assert ctl[0] == len(SIZES) + 1 + 5 + 1 + 2 + 4 + 3 and ctl[1] == 0, ctl
     for n in SIZES + ["fused_gemm", "fused_gemm_half_ring", "fused_gemm_replayed"]:
         for r in range(1, world):
             assert (res[0][2][n] == res[r][2][n]).all()  # bit-identical on every rank

@@ -122,7 +122,7 @@ class E2ELatencyLB(LoadBalancer):
     def observe(self, worker_id, report):
         pass
 
-    def _least_latency(self, ids, group=None):
+    def _least_latency(self, ids, group=None, cost=None):
         cold = [w for w in ids if self.worker_stats[w].ewma_latency is None
                 and self.worker_stats[w].active_connections == 0]
         if cold:
@@ -168,3 +168,63 @@ def test_expected_ms_orders_by_backlog_speed_and_size():
     assert lb.expected_ms("a", (64, 16)) > lb.expected_ms("b", (64, 16))
     lb.observe("a", dict(base))
     assert lb.worker_stats["a"].unreported_prompt_tokens == 0
+
+
+def test_reports_cover_only_the_dispatches_they_saw():
+    """a reply's engine report covers the dispatches up to the sequence number the worker had received
+    (``lb_seen``); later ones (still on the wire) stay counted, so a burst does not herd onto the worker that just
+    replied. Reports of another balancer (other token) or without a sequence number cover everything."""
+    lb = LoadBalancer(LoadBalancerStrategy.LEAST_LATENCY)
+    lb.register_worker("a", "x:1")
+    base = {"running": 0, "waiting": 0, "waiting_prompt_tokens": 0, "max_num_seqs": 32, "kv_used_frac": 0.0,
+            "step_ms": 4.0, "prefill_us_per_token": 12.0}
+    seqs = [lb.acquire("a", (1000, 16)) for _ in range(5)]
+    assert seqs == sorted(seqs) and lb.worker_stats["a"].unreported_requests == 5
+    lb.observe("a", dict(base, lb=lb.token, lb_seen=seqs[2]))
+    assert lb.worker_stats["a"].unreported_requests == 2
+    assert lb.worker_stats["a"].unreported_prompt_tokens == 2000
+    lb.observe("a", dict(base, lb="other-balancer", lb_seen=seqs[3]))
+    assert lb.worker_stats["a"].unreported_requests == 0
+    lb.acquire("a", (10, 1))
+    lb.observe("a", dict(base))
+    assert lb.worker_stats["a"].unreported_requests == 0
+
+
+def test_health_answer_per_model_reports():
+    """a multi-model worker's health answer carries one report per model; a balancer takes its own."""
+    lb_a = LoadBalancer(LoadBalancerStrategy.LEAST_LATENCY, model="a")
+    lb_b = LoadBalancer(LoadBalancerStrategy.LEAST_LATENCY, model="b")
+    reply = {"models": ["a", "b"], "engine_load": {"running": 1},
+             "engine_loads": {"a": {"running": 1}, "b": {"running": 7}}}
+    assert lb_a.report_of(reply) == {"running": 1} and lb_b.report_of(reply) == {"running": 7}
+    old = {"models": ["a", "b"], "engine_load": {"running": 1}}  # a worker without per-model reports
+    assert lb_b.report_of(old) is None
+    assert lb_a.report_of({"models": ["a"], "engine_load": {"running": 3}}) == {"running": 3}
+
+
+def test_lb_serving_bench_real_worker_processes_cpu(capsys):
+    """bench/lb_serving_bench.py on CPU: three real worker processes (src.worker, RPC) behind the coordinator, one
+    with a smaller batch cap; both strategies serve config 5's mixed, prefix-sharing workload completely, every
+    request is dispatched to some worker and the summary compares them (the GPU rehearsal is
+    tests/test_serving_gpu.py::test_lb_serving_rehearsal_one_gpu)."""
+    import importlib.util
+    import json
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench", "lb_serving_bench.py")
+    spec = importlib.util.spec_from_file_location("lb_serving_bench", path)
+    lb_serving_bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(lb_serving_bench)
+
+    rc = lb_serving_bench.main(["--preset", "llama-tiny", "--device", "cpu", "--workers", "3", "--slow", "1",
+                                "--batch", "8", "--slow-batch", "2", "--kv-blocks", "64", "--requests", "24",
+                                "--concurrency", "8", "--prompt-min", "16", "--prompt-max", "64", "--gen", "4,8"])
+    assert rc == 0
+    lines = [json.loads(x) for x in capsys.readouterr().out.splitlines() if x.startswith("{")]
+    runs = {x["strategy"]: x for x in lines if "strategy" in x}
+    assert set(runs) == {"least_latency", "round_robin"}
+    for r in runs.values():
+        assert r["requests"] == 24 and r["error_count"] == 0
+        assert sum(p["dispatched"] for p in r["per_worker"].values()) == 24
+    assert runs["round_robin"]["per_worker"]["w0"]["dispatched"] == 8  # round robin ignores the slow worker's state
+    assert lines[-1]["bench"] == "lb_serving_one_device_summary"

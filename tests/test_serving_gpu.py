@@ -226,3 +226,28 @@ def test_gpu_disaggregated_ipc_landing_zone(monkeypatch):
         except subprocess.TimeoutExpired:
             proc.kill()
 
+
+
+def test_lb_serving_rehearsal_one_gpu(capsys):
+    """Config 5's balancer on real GPU worker processes: three llama-mini workers (src.worker,
+    RPC) share cuda:0 behind the coordinator, one with a 2-sequence batch cap; least_latency (scoring each request on
+    the workers' engine reports) and round_robin both serve the mixed, prefix-sharing workload completely, and
+    least_latency sends the slow worker a smaller share of the requests than round robin's third."""
+    import importlib.util
+    import json
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench", "lb_serving_bench.py")
+    spec = importlib.util.spec_from_file_location("lb_serving_bench", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    rc = mod.main(["--preset", "llama-mini", "--device", "cuda:0", "--workers", "3", "--slow", "1", "--batch", "16",
+                   "--slow-batch", "2", "--kv-blocks", "256", "--requests", "96", "--concurrency", "24",
+                   "--prompt-min", "64", "--prompt-max", "512", "--gen", "16,32,64"])
+    assert rc == 0
+    lines = [json.loads(x) for x in capsys.readouterr().out.splitlines() if x.startswith("{")]
+    runs = {x["strategy"]: x for x in lines if "strategy" in x}
+    for r in runs.values():
+        assert r["requests"] == 96 and r["error_count"] == 0, r
+    summ = lines[-1]
+    assert summ["slow_share_ll"] < summ["slow_share_rr"], summ
