@@ -61,10 +61,11 @@ def fused_exchange_ok(n_tiles: int, grid: int, per_cu: int, ranks_per_gpu: int, 
     if not 0 < n_tiles <= SIG_BLOCKS:
         return False
     if ranks_per_gpu > 1:
-        # ranks sharing a GPU (the one-GPU tests): another rank's next kernel (a full-LDS GEMM ring) needs a whole
-        # CU, and small-ring waiters spread one per CU would leave none — count one workgroup per CU (measured: 8
-        # ranks on one GPU with half-ring waiters on every CU stalled until the bounded spin)
-        per_cu = min(per_cu, 1)
+        # ranks sharing ONE GPU (the one-GPU tests, never a node): the GPU time-slices the processes' queues and
+        # another rank's next kernel (a full-LDS GEMM ring) needs a whole CU, so small-ring waiters spread one per CU
+        # would leave none (measured: 8 ranks with half-ring waiters stalled until the bounded spin). These groups
+        # keep the round-5 rule that the one-GPU suite has validated: one workgroup per CU, no margin.
+        return (0 < grid and grid * ranks_per_gpu <= cus) or n_tiles * ranks_per_gpu * 2 <= cus
     if grid > 0 and per_cu > 0 and grid * ranks_per_gpu <= per_cu * cus - residency_margin(cus):
         return True
     return n_tiles * ranks_per_gpu * 2 <= cus

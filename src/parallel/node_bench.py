@@ -198,22 +198,46 @@ async def _disagg_waves(backend, a: NodeBenchArgs, rank: int) -> Dict[str, Any]:
 
     for _ in range(a.warmup):
         await wave(_prompts(rng, a.batch, a.prompt_len, vocab))
-    waves = [_prompts(rng, a.batch, a.prompt_len, vocab) for _ in range(a.waves)]
-    if backend.engine.device.type == "cuda":
-        torch.cuda.synchronize(backend.engine.device)
-    t0 = time.perf_counter()
-    res: List[Any] = []
-    for w in waves:
-        res += await wave(w)
-    el = time.perf_counter() - t0
-    lat = sorted(x[0] * 1e3 for x in res)
-    ttft = sorted(x[1] for x in res if x[1] is not None)
-    link = backend._decode_link.stats() if backend._decode_link is not None else {}
-    return {"requests": len(res), "elapsed_s": round(el, 4), "req_s": round(len(res) / el, 3),
-            "p50_latency_ms": round(statistics.median(lat), 2),
-            "ttft_p50_ms": round(statistics.median(ttft), 2) if ttft else None,
-            "ttft_p99_ms": round(ttft[max(0, int(0.99 * len(ttft)) - 1)], 2) if ttft else None,
-            "kv_path": link.get("kv_path"), "kv_link": link}
+
+    async def timed() -> Dict[str, Any]:
+        waves = [_prompts(rng, a.batch, a.prompt_len, vocab) for _ in range(a.waves)]
+        if backend.engine.device.type == "cuda":
+            torch.cuda.synchronize(backend.engine.device)
+        t0 = time.perf_counter()
+        res: List[Any] = []
+        for w in waves:
+            res += await wave(w)
+        el = time.perf_counter() - t0
+        lat = sorted(x[0] * 1e3 for x in res)
+        ttft = sorted(x[1] for x in res if x[1] is not None)
+        return {"requests": len(res), "elapsed_s": round(el, 4), "req_s": round(len(res) / el, 3),
+                "p50_latency_ms": round(statistics.median(lat), 2),
+                "ttft_p50_ms": round(statistics.median(ttft), 2) if ttft else None,
+                "ttft_p99_ms": round(ttft[max(0, int(0.99 * len(ttft)) - 1)], 2) if ttft else None}
+
+    link = backend._decode_link
+    out = await timed()
+    st = link.stats() if link is not None else {}
+    out.update(kv_path=st.get("kv_path"), kv_link=st)
+    # transport A/B on the same pair: the default has the prefill GPU's gather kernel store straight into
+    # the decode GPU's landing zone over xGMI (CUs do the transfer, beside the next prefill's GEMMs); the alternative
+    # gathers locally and lets the copy engines move the packet (hipMemcpyAsync peer copy, CUs left to the GEMMs)
+    ch = getattr(link, "_ipc", None) if link is not None else None
+    if ch is not None and backend.engine.device.type == "cuda":
+        kv_direct0 = backend.kv_direct
+        try:
+            backend.kv_direct, ch.dma = False, True
+            n0 = link.staged_packets
+            alt = await timed()
+            alt["staged_packets"] = link.staged_packets - n0
+            out["transport_ab"] = {"shader_stores_direct": {k: out[k] for k in ("req_s", "p50_latency_ms",
+                                                                               "ttft_p50_ms", "ttft_p99_ms")},
+                                   "copy_engine_staged": alt}
+        except Exception as e:  # noqa: BLE001 — the A/B must not cost the default result
+            out["transport_ab"] = {"error": f"{type(e).__name__}: {e}"[:200]}
+        finally:
+            backend.kv_direct, ch.dma = kv_direct0, False
+    return out
 
 
 def _disagg_summary(recs: List[Dict[str, Any]], a: NodeBenchArgs, dev: torch.device) -> Dict[str, Any]:
@@ -226,7 +250,7 @@ def _disagg_summary(recs: List[Dict[str, Any]], a: NodeBenchArgs, dev: torch.dev
         "model": a.preset, "pairs": len(pre), "batch_per_pair": a.batch, "prompt_len": a.prompt_len,
         "gen_len": a.gen_len, "timed_waves": a.waves,
         "per_pair": [{k: r.get(k) for k in ("rank", "req_s", "p50_latency_ms", "ttft_p50_ms", "ttft_p99_ms",
-                                            "kv_path")} for r in pre],
+                                            "kv_path", "transport_ab")} for r in pre],
         "decode_zones": [r.get("kv_zone") for r in recs if r and r.get("role") == "decode"],
     }
     if ok:

@@ -83,6 +83,13 @@ class TPModelRunner(ModelRunner):
         self.d_pkt = torch.zeros(cap, dtype=torch.int64, device=self.device)
         self.steps_synced = 0
         self.windows_synced = 0  # decode windows (and continuations) mirrored as one message each
+        car = getattr(model.tp, "car", None)
+        if car is not None and car.ranks_per_gpu > 4:
+            # more than 4 ranks sharing ONE GPU (tests): queued windows keep every process's queues busy at once,
+            # so the GPU time-slices them and each exchange waits for a peer's queue to be scheduled (one extra
+            # context made the 8-rank group 5-10x slower; under the test runner it stalled): single steps there.
+            # A node runs one rank per GPU.
+            self.supports_multistep = False
         # the one-shot collectives' sticky error word (custom_allreduce ctl[2]), read back with the tokens
         self.h_fault = torch.zeros(1, dtype=torch.int32, pin_memory=self.is_cuda)
 

@@ -129,7 +129,12 @@ def _fused_row_parallel(rank: int, world: int, dev, car, group=None, rccl_group=
             res[name] = {"skipped": f"K = {k}"}
             continue
         wr, kc, sk = ops.decode_tile(n, k, 3, 32)
-        if not car.fused_ok(n // wr, (n // wr) * sk):
+        half = None
+        for h in (False, True):  # the model's choice (CausalLM._tp_fused_tile): full LDS ring, else the half ring
+            if car.fused_ok(n // wr, (n // wr) * sk, ops.gd_occupancy(3, wr, kc, sk, 32, h)):
+                half = h
+                break
+        if half is None:
             res[name] = {"skipped": "fused_ok"}
             continue
         g = torch.Generator(device="cpu").manual_seed(5 + rank)
@@ -138,19 +143,34 @@ def _fused_row_parallel(rank: int, world: int, dev, car, group=None, rccl_group=
         resid = torch.zeros(32, n, dtype=torch.bfloat16, device=dev)
         ssp = torch.zeros(n // wr, ops.SSP_LD, dtype=torch.float32, device=dev)
         cnt = torch.zeros(n // wr, dtype=torch.int32, device=dev)
-        car.row_parallel_residual(x, w, resid, ssp, cnt, wr, kc, sk, tiled=False)
+        car.row_parallel_residual(x, w, resid, ssp, cnt, wr, kc, sk, tiled=False, half_ring=half)
         torch.cuda.synchronize(dev)
         ok = None
         if rccl_group is not False:
             ref = x.float() @ w.float().t()
             dist.all_reduce(ref, group=rccl_group)
             ok = bool(torch.allclose(resid.float(), ref, rtol=3e-2, atol=3e-2))
-        fused = _timed(lambda: car.row_parallel_residual(x, w, resid, ssp, cnt, wr, kc, sk, tiled=False), dev, group)
+        fused = _timed(lambda: car.row_parallel_residual(x, w, resid, ssp, cnt, wr, kc, sk, tiled=False,
+                                                         half_ring=half), dev, group)
         resid2 = torch.zeros_like(resid)
         ssp2, cnt2 = torch.zeros_like(ssp), torch.zeros_like(cnt)
-        local = _timed(lambda: ops.linear_slab_residual(x, w, resid2, ssp2, cnt2, wr, sk, kc=kc), dev, group)
-        res[name] = {"K": k, "tile": [wr, kc, sk], "fused_us": round(fused, 2), "local_us": round(local, 2),
-                     "exchange_us": round(fused - local, 2), "matches_rccl": ok}
+        local = _timed(lambda: ops.linear_slab_residual(x, w, resid2, ssp2, cnt2, wr, sk, kc=kc, half_ring=half),
+                       dev, group)
+        # the same projection with the exchange as its own launch: bf16 partial GEMM, then the one-shot all-reduce +
+        # residual + statistics kernel (what the engine runs when the residency rule refuses the fused form) ...
+        ssp1 = torch.zeros(1, ops.SSP_LD, dtype=torch.float32, device=dev)
+        sep = _timed(lambda: car.all_reduce_residual(ops.linear(x, w), resid2, ssp1), dev, group)
+        row = {"K": k, "tile": [wr, kc, sk], "half_ring": half, "fused_us": round(fused, 2),
+               "local_us": round(local, 2), "exchange_us": round(fused - local, 2),
+               "separate_one_shot_us": round(sep, 2), "matches_rccl": ok}
+        # ... and over RCCL (its ring / LL protocols over the xGMI links) for the same 32 x N message
+        if rccl_group is not False:
+            def rccl_path():
+                part = ops.linear(x, w)
+                dist.all_reduce(part, group=rccl_group)
+                ops.residual_add_sumsq(resid2, part, ssp1)
+            row["rccl_us"] = round(_timed(rccl_path, dev, group), 2)
+        res[name] = row
     return res
 
 

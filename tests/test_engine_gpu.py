@@ -202,7 +202,10 @@ def test_overlapped_layer_group_export_matches_post_step_gather(engine, monkeypa
 
 
 def _tp_gpu_worker(rank, world, port, q, preset, moe_parallel="tp", sp=False, graphs=False):
+    import faulthandler
     import os
+
+    faulthandler.dump_traceback_later(45, exit=False)  # a stuck rank names where it is
 
     import torch.distributed as dist
 
@@ -217,24 +220,28 @@ def _tp_gpu_worker(rank, world, port, q, preset, moe_parallel="tp", sp=False, gr
                            use_cuda_graph=graphs, graph_batch_sizes=[1, 2, 4])
         obj = build_tp_engine(preset, tp, "cuda:0", cfg=cfg, max_model_len=512, capture=graphs,
                               full_init=True, seed=3, moe_parallel=moe_parallel, sequence_parallel=sp)
+        print(f"[tp {world}] rank {rank} built", flush=True)
         if rank == 0:
             obj.eos_token_id = None
             outs = obj.generate(TP_PROMPTS, SamplingParams(max_tokens=8))
+            print(f"[tp {world}] greedy generate done", flush=True)
             replayed = bool(obj.runner.graphs)
             windows = obj.runner.windows_synced
             if graphs:
                 # non-greedy windows: every rank samples and advances its own inputs, so they must draw the same
                 # tokens (the sampling parameters travel with the window message)
                 obj.generate(TP_PROMPTS, SamplingParams(max_tokens=12, temperature=0.9, top_k=40, top_p=0.9, seed=11))
+            print(f"[tp {world}] sampled generate done", flush=True)
             obj.runner.stop_followers()
             torch.cuda.synchronize()
             fused = bool(obj.model.decode_plan(4).get("tp_fused"))
             q.put((0, (outs, tp.car is not None, replayed, bool(tp.car.error()) if tp.car is not None else None, fused,
-                       windows, obj.runner.d_tokens.cpu())))
+                       windows, obj.runner.d_tokens.cpu().numpy())))  # numpy: pickled by value, not a shm fd
         else:
             obj.follower_loop()
             torch.cuda.synchronize()
-            q.put((rank, obj.d_tokens.cpu()))
+            q.put((rank, obj.d_tokens.cpu().numpy()))
+            print(f"[tp {world}] follower {rank} done", flush=True)
     finally:
         dist.destroy_process_group()
 
@@ -276,11 +283,11 @@ def test_tensor_parallel_on_one_gpu(preset, moe_parallel, sp, world, graphs):
     got, used_car, replayed, car_err, fused, windows, toks0 = res[0]
     assert used_car and car_err is False  # all-reduces / logits all-gather on the one-shot IPC kernels
     assert replayed == graphs             # graphs: decode steps replayed hipGraphs on every rank
-    # graphs: decode runs in multi-step windows, one message per window; every rank's device-side token rows
-    # (greedy then sampled windows) are identical
-    assert (windows > 0) == graphs, windows
+    # graphs: decode runs in multi-step windows, one message per window (up to 4 ranks sharing the GPU: more time-
+    # slice the queues, TPModelRunner); every rank's device-side token rows (greedy then sampled) are identical
+    assert (windows > 0) == (graphs and world <= 4), windows
     for r in range(1, world):
-        assert torch.equal(res[r], toks0), r
+        assert (res[r] == toks0).all(), r
     # dense decode: o / down as ONE launch each (the exchange in the GEMM's tile epilogue): the grids of all
     # ranks sharing the GPU fit on it at once (llama-mini: 16-128 workgroups per rank)
     assert fused == (preset == "llama-mini"), fused
