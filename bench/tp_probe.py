@@ -85,6 +85,12 @@ def main(argv=None):
         "wave_ms_compute_only": round(1e3 * el / a.steps, 1),
         "req_s_per_tp_group_compute_only": round(a.batch * a.steps / el, 2),
         "rank_weight_gib": round(wbytes / 2**30, 2), "engine_init_s": round(init_s, 1),
+        "decode_windows": st.get("decode_windows", 0) - s0.get("decode_windows", 0),
+        "queued_windows": st.get("queued_windows", 0) - s0.get("queued_windows", 0),
+        "tp_fused": bool(eng.model.decode_plan(a.batch).get("tp_fused")),
+        "o_tile": list(eng.model.decode_plan(a.batch)["o"]), "o_half_ring": eng.model.decode_plan(a.batch).get("o_half"),
+        "down_tile": list(eng.model.decode_plan(a.batch)["down"] or []),
+        "down_half_ring": eng.model.decode_plan(a.batch).get("down_half"),
         "not_included": "2 all-reduces per layer + the logits all-gather (one GPU: no peers)",
     }), flush=True)
 
