@@ -42,13 +42,19 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--device", default="cuda:0", help="cpu: fp32 reference ops, for tests")
+    ap.add_argument("--decode-window", type=int, default=8, help="EngineConfig.decode_window (1: single steps, A/B)")
+    ap.add_argument("--legacy-fused", action="store_true",
+                    help="A/B: round 5's fused-exchange rule (the table tile with its full LDS ring, zero slack)")
     a = ap.parse_args(argv)
     on_gpu = a.device.startswith("cuda")
     mlen = a.prompt_len + a.gen_len + 64
     cfg = EngineConfig(max_num_seqs=a.batch, max_num_batched_tokens=max(16384, a.prompt_len), max_latency_ms=0.0,
-                       graph_batch_sizes=sorted({1, 2, 4, 8, 16, 24, 32, a.batch}))
+                       graph_batch_sizes=sorted({1, 2, 4, 8, 16, 24, 32, a.batch}), decode_window=a.decode_window)
     t0 = time.perf_counter()
-    eng = build_tp_engine(a.preset, ShardProbeTP(a.tp), a.device, cfg=cfg, max_model_len=mlen, seed=1234,
+    tp = ShardProbeTP(a.tp)
+    if a.legacy_fused:
+        tp.fused_row_parallel = lambda n_tiles, grid=0, per_cu=0: True
+    eng = build_tp_engine(a.preset, tp, a.device, cfg=cfg, max_model_len=mlen, seed=1234,
                           capture=on_gpu, dtype=torch.bfloat16 if on_gpu else torch.float32)
     eng.eos_token_id = None
     init_s = time.perf_counter() - t0
@@ -80,6 +86,7 @@ def main(argv=None):
     wbytes = eng.runner.model.weight_bytes()
     print(json.dumps({
         "bench": "tp_shard_probe", "model": a.preset, "tp": a.tp, "rank": 0, "batch": a.batch,
+        "decode_window": a.decode_window, "legacy_fused": a.legacy_fused,
         "prompt_len": a.prompt_len, "gen_len": a.gen_len, "dtype": "bf16" if on_gpu else "fp32", "weights": "random-init",
         "prefill_ms_per_wave": round(prefill_ms, 1), "decode_ms_per_step": round(decode_ms, 3),
         "wave_ms_compute_only": round(1e3 * el / a.steps, 1),
