@@ -27,8 +27,9 @@ def test_bench_node_section_rehearsal_two_ranks_one_gpu():
         env.pop(k, None)
     cmd = [sys.executable, "bench.py", "--gpus", "2", "--same-device", "--preset", "llama-mini", "--batch", "8",
            "--prompt-len", "64", "--gen-len", "16", "--max-model-len", "256", "--steps", "1", "--warmup", "1",
-           "--tp-wave-min-world", "2", "--tp-wave-preset", "llama-mini", "--cross-gpu-budget-s", "150", "--verbose"]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+           "--tp-wave-min-world", "2", "--tp-wave-preset", "llama-mini", "--lb-preset", "mixtral-tiny",
+           "--lb-kv-blocks", "64", "--lb-requests-per-worker", "8", "--cross-gpu-budget-s", "200", "--verbose"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=290)
     lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
     # a stall in the node section prints the line with the stalled part (watchdog, exit 3): show it
     assert p.returncode == 0 and len(lines) == 1, (p.returncode, p.stdout[-3000:], p.stderr[-3000:])
@@ -40,5 +41,10 @@ def test_bench_node_section_rehearsal_two_ranks_one_gpu():
     assert cross["xgpu_probe"]["kv_hop"]["per_rank"][1]["receiver_bytes_match"] is True, cross["xgpu_probe"]
     d = cross["disagg"]
     assert d["pairs"] == 1 and d["kv_path"] == "direct" and d["req_s_total"] > 0, d
+    ab = d["per_pair"][0]["transport_ab"]  # shader stores (direct) vs copy engines (staged): both served
+    assert ab["copy_engine_staged"]["req_s"] > 0 and ab["copy_engine_staged"]["staged_packets"] > 0, ab
     t = cross["tp_wave"]
     assert t["tp"] == 2 and t["all_tokens"] and t["graphs_replayed"] and t["error_word"] is False, t
+    lb = cross["lb_serving"]  # config 5: a Mixtral worker per rank behind one coordinator
+    assert lb["workers"] == 2 and [r["strategy"] for r in lb["runs"]] == ["least_latency", "round_robin"], lb
+    assert all(r["requests"] == 16 and r["error_count"] == 0 for r in lb["runs"]), lb
