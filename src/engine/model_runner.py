@@ -108,7 +108,7 @@ class ModelRunner:
         self.n_ids, self.n_temp, self.n_topk = self.h_ids.numpy(), self.h_temp.numpy(), self.h_topk.numpy()
         self.n_topp, self.n_seed, self.n_step = self.h_topp.numpy(), self.h_seed.numpy(), self.h_step.numpy()
         self._samp_key = None
-        self._samp_sent = 0
+        self._samp_dirty = False
         dev = self.device
         # device-side static buffers (graph inputs)
         self.d_ids = torch.zeros(self.max_tokens, dtype=i64, device=dev)
@@ -194,7 +194,7 @@ class ModelRunner:
         for h, d in ((self.h_temp, self.d_temp), (self.h_topk, self.d_topk), (self.h_topp, self.d_topp),
                      (self.h_seed, self.d_seed), (self.h_step, self.d_step)):
             d[:n_pad].copy_(h[:n_pad], non_blocking=nb)
-        self._samp_sent = n_pad  # rows of sampling parameters this step re-sent (TP windows mirror them)
+        self._samp_dirty = True  # the device-side parameters changed since a TP leader last mirrored them
         return greedy
 
     def _sample(self, logits: torch.Tensor, n: int, greedy: bool, out: torch.Tensor) -> torch.Tensor:
@@ -401,7 +401,6 @@ class ModelRunner:
         self.rt.build_decode_inputs([s.block_table for s in seqs], [len(s) for s in seqs], self.bs,
                                     self.h_pos.data_ptr(), self.h_slots.data_ptr(), self.h_ctx.data_ptr(),
                                     self.h_bt.data_ptr(), self.bt_width, pad)
-        self._samp_sent = 0
         self._fill_sampling(seqs, pad)
         self._h2d(pad, pad, with_cu=False)
         self._pre_embed(pad)  # the step starts from these rows when its tail launch writes the next ones

@@ -17,7 +17,8 @@ Step protocol (two messages per step):
 
 Decode windows (round 6): a k-step window is ONE such message (kind WINDOW: the
 first step's inputs, the window's [step counter, real rows] words and — when
-the leader re-sent them — the sampling parameters); a continuation window
+the leader's device copies changed since its last decode message — the
+sampling parameters); a continuation window
 queued behind the running one is another (kind CONTINUE: the grown block
 tables and first-step slots, plus its token-row base). Every rank replays its
 graph k times; the graph's tail samples from the all-gathered logits
@@ -122,8 +123,9 @@ class TPModelRunner(ModelRunner):
                    (self.d_ctx, self.h_ctx, pad), (self.d_bt, self.h_bt, pad)]
             if self.supports_multistep:  # the graph's input advance reads [step counter, real rows]
                 out.append((self.d_ctl, self.h_ctl, 2))
-            if kind == self.KIND_WINDOW and d:
-                # the window's steps advance and SAMPLE on every rank: non-greedy rows need the same parameters
+            if d:
+                # decode steps advance and SAMPLE on every rank: the followers' sampling parameters must equal the
+                # leader's whenever its device copies changed (d = rows; prefill steps rewrite them too)
                 out += [(self.d_temp, self.h_temp, d), (self.d_topk, self.h_topk, d), (self.d_topp, self.h_topp, d),
                         (self.d_seed, self.h_seed, d), (self.d_step, self.h_step, d)]
             return out
@@ -167,6 +169,12 @@ class TPModelRunner(ModelRunner):
         if not self.tp.enabled:
             return
         self._last_sync = time.monotonic()
+        if kind in (self.KIND_DECODE, self.KIND_WINDOW) and self.supports_multistep:
+            # mirror the sampling parameters whenever the leader rewrote its device copies since the last decode
+            # message (a greedy window right after a prefill or a single step of another mix must not leave the
+            # followers sampling with stale ones); d = the step's padded rows
+            d = b if self._samp_dirty else 0
+            self._samp_dirty = False
         nw = self._pack(kind, a, b, d)
         self.h_hdr.copy_(torch.tensor([kind, a, b, c, d, nw, 0, 0], dtype=torch.int64))
         self.tp.broadcast_host(self.h_hdr)
@@ -176,9 +184,9 @@ class TPModelRunner(ModelRunner):
         self.steps_synced += 1
 
     def _sync_window(self, n: int, pad: int, k: int) -> None:
-        """One message per k-step window: the first step's inputs (and the sampling parameters when this window
-        re-sent them); every rank then replays its graph k times and advances its inputs on the device."""
-        self._sync_step(self.KIND_WINDOW, n, pad, k, self._samp_sent)
+        """One message per k-step window: the first step's inputs (and the sampling parameters when the leader's
+        changed); every rank then replays its graph k times and advances its inputs on the device."""
+        self._sync_step(self.KIND_WINDOW, n, pad, k, 0)
         self.windows_synced += 1
 
     def _sync_continuation(self, par: int, pad: int, k: int, base: int) -> None:

@@ -140,3 +140,56 @@ def test_tp_plan_takes_a_residency_safe_tile(monkeypatch):
     monkeypatch.setattr(NodeTP, "fused_row_parallel", lambda self, *a, **k: False)
     p = m.decode_plan(32)
     assert not p["tp_fused"] and not p["o_half"]
+
+
+def test_tp_decode_messages_mirror_sampling_parameters():
+    """The TP step protocol with decode windows: a decode / window message carries the sampling parameters
+    whenever the leader's device copies changed since its last decode message (a prefill or an earlier step of
+    another greedy / sampled mix rewrites them), float parameters travel as their bit patterns, and a follower's
+    unpack reproduces the leader's buffers exactly; an unchanged greedy batch sends none."""
+    from src.config import EngineConfig
+    from src.engine.model_runner import KVPool
+    from src.engine.sequence import Sequence
+    from src.models.llama import CausalLM
+    from src.models.presets import get_preset
+    from src.parallel.tp import TPContext
+    from src.parallel.tp_runner import TPModelRunner
+
+    arch = get_preset("llama-tiny")
+    runners = []
+    for rank in range(2):
+        tp = TPContext(rank=rank, world_size=2)
+        m = CausalLM(arch, "cpu", dtype=torch.float32, tp=tp, seed=3, max_position=128)
+        pool = KVPool(arch.num_layers, 16, m.hkv, 16, arch.head_dim, "cpu", dtype=torch.float32)
+        r = TPModelRunner(m, pool, EngineConfig(max_num_seqs=4, max_num_batched_tokens=64, num_kv_blocks=16), 128)
+        r.supports_multistep = True  # as on the GPU (windows); CPU runners default to single steps
+        runners.append(r)
+    lead, fol = runners
+    sent = []
+    lead.tp.broadcast_host = lambda t: sent.append(t.clone()) or t
+    lead._bcast = lambda t: None
+
+    def seqs(temps):
+        out = []
+        for i, t in enumerate(temps):
+            s = Sequence(f"r{i}", [1, 2, 3], SamplingParams(max_tokens=4, temperature=t, top_k=5, top_p=0.9, seed=7 + i))
+            out.append(s)
+        return out
+
+    def send(batch, pad=4):
+        lead._fill_sampling(batch, pad)
+        lead._sync_step(lead.KIND_DECODE, len(batch), pad)
+        hdr = sent[-1].tolist()
+        fol.d_pkt[: hdr[5]].copy_(lead.d_pkt[: hdr[5]])
+        fol._unpack(hdr[0], hdr[1], hdr[2], hdr[4])
+        return hdr
+
+    hdr = send(seqs([0.7, 1.3, 0.0]))
+    assert hdr[4] == 4  # sampled rows: parameters mirrored for the padded batch
+    for name in ("d_temp", "d_topk", "d_topp", "d_seed", "d_step"):
+        assert torch.equal(getattr(fol, name)[:4], getattr(lead, name)[:4]), name
+    assert float(fol.d_temp[1]) == pytest.approx(1.3)
+    hdr = send(seqs([0.0, 0.0, 0.0]))  # greedy after sampled: the leader rewrote them -> sent again
+    assert hdr[4] == 4 and float(fol.d_temp[:4].abs().sum()) == 0.0
+    hdr = send(seqs([0.0, 0.0, 0.0]))  # the same greedy batch: nothing changed, nothing sent
+    assert hdr[4] == 0
