@@ -439,7 +439,8 @@ DECODE_SILU_SPLITK_CFG = {
 def decode_tile_silu(n: int, k: int, bucket: int = 32):
     """(wr, kc, sk) of the norm-scaled SiLU gate/up decode GEMM: a split-K tile where one was measured faster,
     else the full-K tile (sk = 1)."""
-    c = DECODE_SILU_SPLITK_CFG.get((n, k, bucket))
+    # DIE_TILE_OVERRIDE entries with mode 6 name the split-K SiLU gate/up tile (N_out, K, 6, bucket) (in-graph A/Bs)
+    c = DECODE_TILE_CFG.get((n, k, 6, bucket)) or DECODE_SILU_SPLITK_CFG.get((n, k, bucket))
     if c is not None:
         return c
     return (*decode_tile(n, k, 4, bucket)[:2], 1)
