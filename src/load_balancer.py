@@ -47,6 +47,9 @@ from src.rpc import RPCClient, tcp_connect_probe
 logger = logging.getLogger(__name__)
 
 
+UNREPORTED_MAX = 4096
+
+
 class LoadBalancerStrategy(Enum):
     ROUND_ROBIN = "round_robin"
     LEAST_CONNECTIONS = "least_connections"
@@ -65,8 +68,9 @@ class WorkerStats:
     probe_count: int = 0
     probe_latency: float = 0.0
     report: Optional[Dict[str, Any]] = None   # the worker's last engine_load (see module doc)
-    # dispatches the last report does not cover yet: (sequence number, prompt tokens) in dispatch order
-    unreported: "collections.deque" = field(default_factory=collections.deque)
+    # dispatches the last report does not cover yet: (sequence number, prompt tokens) in dispatch order; bounded
+    # (a worker that never reports — a mock model — must not grow it without end; entries that old are covered)
+    unreported: "collections.deque" = field(default_factory=lambda: collections.deque(maxlen=UNREPORTED_MAX))
 
     @property
     def unreported_requests(self) -> int:

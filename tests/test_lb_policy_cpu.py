@@ -228,3 +228,14 @@ def test_lb_serving_bench_real_worker_processes_cpu(capsys):
         assert sum(p["dispatched"] for p in r["per_worker"].values()) == 24
     assert runs["round_robin"]["per_worker"]["w0"]["dispatched"] == 8  # round robin ignores the slow worker's state
     assert lines[-1]["bench"] == "lb_serving_one_device_summary"
+
+
+def test_unreported_dispatches_are_bounded_for_silent_workers():
+    """A worker that never reports (mock models) must not grow the balancer's unreported-dispatch list without end."""
+    from src.load_balancer import UNREPORTED_MAX
+
+    lb = LoadBalancer(LoadBalancerStrategy.ROUND_ROBIN)
+    lb.register_worker("m", "x:1")
+    for _ in range(UNREPORTED_MAX + 500):
+        lb.release("m") if lb.acquire("m", (4, 1)) < 0 else lb.release("m")
+    assert lb.worker_stats["m"].unreported_requests == UNREPORTED_MAX
