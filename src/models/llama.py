@@ -596,6 +596,75 @@ class CausalLM:
         return {"qkv": qkv, "o": o, "down": down, "gate_up": gu[:2] if gu else None,
                 "gate_up_sk": gu[2] if gu else 1, "tp_fused": tp_fused, "o_half": o_half, "down_half": down_half}
 
+    @torch.inference_mode()
+    def calibrate_tp_exchange(self, iters: int = 20, force: bool = False) -> Optional[dict]:
+        """Measure, on this TP group's links, the decode layer's two row-parallel projections (o, down; 32 rows) as
+        ONE launch whose tiles carry the exchange against the separate form (bf16 partial GEMM + the one-shot
+        all-reduce / residual / statistics launch), and keep the faster for serving (``tp.fused_preferred``; every
+        rank takes the slowest rank's times, so the group agrees). Runs at engine build on a node (one rank per
+        GPU); ranks sharing one GPU contend for the same CUs, so their timing says nothing about a node (``force``:
+        tests). Every rank must call it. Returns the timings, or None when not measured."""
+        import torch.distributed as dist
+
+        tp = self.tp
+        car = getattr(tp, "car", None)
+        if not (tp.enabled and car is not None and self.device.type == "cuda" and not self.arch.is_moe):
+            return None
+        if car.ranks_per_gpu > 1 and not force:
+            return None
+        tp.fused_preferred = None
+        plan = self.decode_plan(32)
+        if not plan["tp_fused"]:
+            return None  # the residency rule already keeps the separate launch
+        h, dev = self.arch.hidden_size, self.device
+        g = torch.Generator(device=dev).manual_seed(11 + tp.rank)
+        res = {}
+        fused_t = sep_t = 0.0
+        for name, k, half in (("o", self.hq * self.head_dim, plan["o_half"]), ("down", self.inter, plan["down_half"])):
+            wr, kc, sk = plan[name]
+            x = (torch.randn(32, k, device=dev, generator=g) * 0.5).to(self.dtype)
+            w = (torch.randn(h, k, device=dev, generator=g) * 0.02).to(self.dtype)
+            resid = torch.zeros(32, h, dtype=self.dtype, device=dev)
+            ssp = torch.zeros(h // wr, ops.SSP_LD, dtype=torch.float32, device=dev)
+            ssp1 = torch.zeros(1, ops.SSP_LD, dtype=torch.float32, device=dev)
+            cnt = torch.zeros(h // wr, dtype=torch.int32, device=dev)
+
+            # both forms on tile-order weights, as served (the separate form's partial GEMM on its own mode-0 tile)
+            wt = ops.gd_pack_weights(w, wr, kc=kc)
+            wr0, kc0 = ops.decode_tile(h, k, 0, 32)[:2]
+            wt0 = ops.gd_pack_weights(w, wr0, kc=kc0)
+
+            def fused():
+                tp.row_parallel_residual(x, wt, resid, ssp, cnt, wr, kc, sk, tiled=True, half_ring=half)
+
+            def separate():
+                tp.all_reduce_residual(ops.linear_tiled(x, wt0, wr0, kc0), resid, ssp1)
+
+            times = []
+            for fn in (fused, separate):
+                for _ in range(3):
+                    fn()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize(dev)
+                e0.record()
+                for _ in range(iters):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize(dev)
+                times.append(e0.elapsed_time(e1) * 1e3 / iters)
+            res[name] = {"fused_us": round(times[0], 2), "separate_us": round(times[1], 2)}
+            fused_t += times[0]
+            sep_t += times[1]
+        t = torch.tensor([fused_t, sep_t], dtype=torch.float64)
+        grp = tp.cpu_group if tp.cpu_group is not None else tp.group
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=grp)  # the group's slowest rank decides, identically on all
+        tp.fused_preferred = bool(t[0] <= t[1])
+        res.update(fused_total_us=round(float(t[0]), 2), separate_total_us=round(float(t[1]), 2),
+                   fused_preferred=tp.fused_preferred)
+        if car.error():
+            raise RuntimeError("TP exchange calibration: a one-shot collective timed out")
+        return res
+
     def _tp_fused_tile(self, n: int, k: int, bucket: int, tile):
         """((wr, kc, sk), half_ring) of a row-parallel projection whose tiles carry the TP exchange, or None. The
         measured tile first (with its full LDS ring, then — at <= 32 rows — the half-LDS ring that puts two

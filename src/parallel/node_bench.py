@@ -408,6 +408,8 @@ def tp_wave_part(a: NodeBenchArgs, rank: int, world: int, dev: torch.device) -> 
                 "decode_ms_per_step": round(1e3 * dec / steps, 3),
                 "prefill_ms_per_wave": round(1e3 * (st["prefill_time"] - st0["prefill_time"]) / a.waves, 2),
                 "fused_exchange": bool(eng.model.decode_plan(a.batch).get("tp_fused")),
+                # the group's measured choice between the fused and the separate exchange (engine build)
+                "exchange_calibration": getattr(eng.model, "tp_exchange_calibration", None),
                 "one_shot_ipc": car is not None,
                 "error_word": bool(car.error()) if car is not None else None,
                 "graphs_replayed": bool(eng.runner.graphs),

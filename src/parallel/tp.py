@@ -39,6 +39,9 @@ class TPContext:
     # test hook: run the collectives even at world_size 1 (a one-rank RCCL group pins the RCCL branches'
     # shapes and dtypes on a one-GPU box; tests/test_rccl_gpu.py)
     force_collectives: bool = False
+    # the group's measured choice between the exchange fused into the row-parallel GEMM and the separate one-shot
+    # launch (CausalLM.calibrate_tp_exchange at engine build; None: not measured, the fused form where it may run)
+    fused_preferred: Optional[bool] = None
 
     def src_rank(self) -> int:
         """Global rank of this group's rank 0 (the ``src`` of broadcasts)."""
@@ -116,7 +119,8 @@ class TPContext:
         resident per CU) runs as ONE launch: the decode GEMM whose tiles' last arrivers exchange their partials
         one-shot and update the residual (:meth:`row_parallel_residual`), instead of GEMM + all-reduce/residual
         kernel. Needs the IPC path and the residency rule (custom_allreduce.fused_exchange_ok)."""
-        return self.enabled and self.car is not None and self.car.fused_ok(n_tiles, grid, per_cu)
+        return (self.enabled and self.car is not None and self.fused_preferred is not False
+                and self.car.fused_ok(n_tiles, grid, per_cu))
 
     def row_parallel_residual(self, x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, ssp: torch.Tensor,
                               counters: torch.Tensor, wr: int, kc: int, sk: int, tiled: bool = False,

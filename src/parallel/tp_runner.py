@@ -267,6 +267,9 @@ def build_tp_engine(preset: str, tp, device, cfg: Optional[EngineConfig] = None,
                      full_init=full_init, moe_parallel=moe_parallel, sequence_parallel=sequence_parallel)
     if ckpt:
         load_checkpoint(model, preset)  # every rank streams the shards and keeps its own slice
+    # decode's row-parallel exchange: fused into the GEMM or its own launch, whichever this node's links run faster
+    # (measured here, before the decode plan sizes the scratch and the graphs are captured)
+    model.tp_exchange_calibration = model.calibrate_tp_exchange()
     nblocks = agree_num_blocks(plan_kv_blocks(arch, model, cfg, model.device), tp)
     cfg = EngineConfig(**{**cfg.__dict__, "num_kv_blocks": nblocks})
     if tp.rank == 0:

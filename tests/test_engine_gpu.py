@@ -543,3 +543,51 @@ def test_prefix_blocks_evicted_under_pressure_then_reprefilled():
         r, m = reference_with_margins(eng.model, p, 6)
         for o in outs:
             assert agree(o, r, m), (o, r, m)
+
+
+def _calib_worker(rank, world, port, q):
+    import os
+
+    import torch.distributed as dist
+
+    from src.models.llama import CausalLM
+    from src.models.presets import get_preset
+    from src.parallel.tp import TPContext
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tp = TPContext(rank=rank, world_size=world)
+        tp.enable_custom_allreduce()
+        m = CausalLM(get_preset("llama-mini"), "cuda:0", tp=tp, seed=3, max_position=512, full_init=True)
+        res = m.calibrate_tp_exchange(force=True)
+        q.put((rank, res, tp.fused_preferred, bool(m.decode_plan(32)["tp_fused"]), bool(tp.car.error())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tp_exchange_calibration_agrees_across_ranks():
+    """CausalLM.calibrate_tp_exchange (run at TP engine build on a node): times the row-parallel projections with the
+    exchange fused into the GEMM and as a separate one-shot launch, and every rank of the group keeps the same
+    choice (the slowest rank's times); the decode plan follows it. Forced here on 2 ranks sharing the GPU."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_calib_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, rest) for r, *rest in (q.get(timeout=300) for _ in range(2)))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    (res0, pref0, fused0, err0), (res1, pref1, fused1, err1) = got[0], got[1]
+    assert res0 is not None and res0["fused_total_us"] > 0 and res0["separate_total_us"] > 0, res0
+    assert pref0 == pref1 == res0["fused_preferred"] and fused0 == fused1 == pref0
+    assert res0["fused_total_us"] == res1["fused_total_us"] and not err0 and not err1
