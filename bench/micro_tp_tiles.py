@@ -27,6 +27,10 @@ SHAPES = {  # name -> [(projection, N, K, modes)]
            ("down", 4096, 14336, (3,))],
     "8b_tp4": [("qkv", 1536, 4096, (2,)), ("o", 4096, 1024, (3,)), ("gate_up", 3584, 4096, (4, 6)),
                ("down", 4096, 3584, (3,))],
+    # Llama-3-70B on ONE GPU (TP=1): its tile-order copies do not fit beside 141 GB of weights, so decode streams the
+    # row-major weights (--row-major)
+    "70b": [("qkv", 10240, 8192, (2,)), ("o", 8192, 8192, (3,)), ("gate_up", 28672, 8192, (4, 6)),
+            ("down", 8192, 28672, (3,))],
     # the decode step's LM head (Llama-3 vocabulary): mode 0, bf16 logits; row-major weight ("tiled": False)
     # as the engine stores it today, and tile-order
     "lm_head": [("lm_head", 128256, 4096, (0,))],
@@ -41,6 +45,7 @@ def main():
     ap.add_argument("--rows", type=int, default=32)
     ap.add_argument("--proj", default="", help="comma-separated projections to sweep (default: all)")
     ap.add_argument("--splits", default="1,2,4,8", help="split-K counts to try (uneven splits allowed: 3,5,6)")
+    ap.add_argument("--row-major", action="store_true", help="time the row-major weights (no tile-order copy)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     kern = ops._kern()
@@ -59,8 +64,9 @@ def main():
             best = None
             for mode in modes:
                 sks = (1,) if mode == 4 else tuple(int(v) for v in a.splits.split(","))
-                for (wr, kc), tiled in [(t, True) for t in TILES] + ([(t, False) for t in TILES]
-                                                                      if proj == "lm_head" else []):
+                for (wr, kc), tiled in ([(t, False) for t in TILES] if a.row_major else
+                                        [(t, True) for t in TILES] + ([(t, False) for t in TILES]
+                                                                      if proj == "lm_head" else [])):
                     for sk in sks:
                         cols = wr // 2 if silu else wr
                         if n % cols or k % kc or k // kc < sk or not ops.gd_tile_valid(wr, kc, 32):
@@ -86,16 +92,16 @@ def main():
                             args = (y, x, wt, tb, wr, kc, 1, True, e, e, e, e, 0.0)
                         elif mode == 2:
                             y = torch.empty(sk, m, n, dtype=torch.float32, device=dev)
-                            args = (y, x, wt, 2 | 32, wr, kc, sk, True, e, e, e, e, 0.0)
+                            args = (y, x, wt, 2 | tb, wr, kc, sk, True, e, e, e, e, 0.0)
                         elif mode == 3:
                             y = torch.empty(sk, m, n, dtype=torch.float32, device=dev)
                             resid = torch.zeros(m, n, dtype=torch.bfloat16, device=dev)
                             sspo = torch.zeros(ntiles, 128, device=dev)
-                            args = (y, x, wt, 3 | 32, wr, kc, sk, True, resid, sspo, cnt, e, 0.0)
+                            args = (y, x, wt, 3 | tb, wr, kc, sk, True, resid, sspo, cnt, e, 0.0)
                         else:
                             y = torch.empty(m, n, dtype=torch.bfloat16, device=dev)
                             slab = torch.empty(sk * m * 2 * n, dtype=torch.float32, device=dev) if mode == 6 else e
-                            args = (y, x, wt, mode | 32, wr, kc, sk, True, e, slab, cnt if mode == 6 else e, ssp, 1e-5)
+                            args = (y, x, wt, mode | tb, wr, kc, sk, True, e, slab, cnt if mode == 6 else e, ssp, 1e-5)
                         try:
                             kern.gemm_decode(*args)
                             torch.cuda.synchronize()
