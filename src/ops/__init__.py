@@ -572,6 +572,11 @@ DECODE_TILE_CFG = {
     (7168, 4096, 4, 32): (64, 128, 1),     # 8B TP=2 gate/up 24.84 vs 25.68
     (1280, 8192, 2, 64): (32, 256, 4),     # 70B TP=8 qkv at 64 rows  13.80 vs 14.40 for (32, 128, 4)
     (8192, 1024, 3, 128): (64, 64, 2),     # 70B TP=8 o at 128 rows   17.52 vs 18.20 for (64, 128, 2)
+    # Llama-3-70B on ONE GPU (TP=1): decode streams the row-major weights (their tile-order copies do not fit beside
+    # 141 GB); round-6 sweep (bench/micro_tp_tiles.py --shapes 70b --row-major, profiles/r6_70b_tp1_tiles.jsonl, cold us)
+    (10240, 8192, 2, 32): (64, 256, 1),    # qkv            38.76 vs 43.68 for the generic (64, 256, 2)
+    (28672, 8192, 4, 32): (112, 128, 1),   # gate/up + SiLU 165.76 vs 189.88 for (64, 256, 1)
+    (8192, 28672, 3, 32): (128, 128, 4),   # down           80.68 vs 88.48 for (64, 256, 2)
 }
 
 

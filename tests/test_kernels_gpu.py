@@ -545,7 +545,8 @@ def test_rope_and_cache_slab(dev):
 @pytest.mark.parametrize("wr,sk,k,m,kc", [(64, 4, 4096, 27, None), (64, 4, 14336, 27, None), (32, 1, 2048, 27, None),
                                           (128, 2, 4096, 27, None), (64, 8, 4096, 27, None), (32, 3, 3072, 27, None),
                                           (64, 4, 4096, 100, 128), (128, 8, 4096, 128, 32), (64, 2, 14336, 64, 256),
-                                          (128, 4, 4096, 77, 64), (64, 3, 4096, 27, 256), (32, 5, 8192, 32, 256)])
+                                          (128, 4, 4096, 77, 64), (64, 3, 4096, 27, 256), (32, 5, 8192, 32, 256),
+                                          (128, 4, 28672, 32, 128)])  # Llama-3-70B TP=1 down's tile, its K
 def test_gemm_decode_residual_mode(dev, wr, sk, k, m, kc):
     """mode 3: resid += x @ w^T with the split-K reduced by the last-arriving workgroup, which
     also writes the per-tile row sums of squares of the new residual."""
@@ -604,7 +605,8 @@ def test_gemm_decode_residual_mode_is_deterministic(dev, sk):
 
 @pytest.mark.parametrize("m,inter,k,wr,t", [(32, 14336, 4096, 112, 64), (7, 2048, 1024, 64, 64),
                                            (100, 14336, 4096, 112, 64), (64, 2048, 1024, 64, 64),
-                                           (32, 3584, 8192, 64, 256), (19, 3584, 8192, 64, 200)])
+                                           (32, 3584, 8192, 64, 256), (19, 3584, 8192, 64, 200),
+                                           (32, 28672, 8192, 112, 128)])  # Llama-3-70B TP=1 gate/up tile and shape
 def test_gemm_decode_rownorm_silu(dev, m, inter, k, wr, t):
     """mode 4: RMSNorm (weight folded into W) as a per-row scale + gate/up + SiLU*mul; the statistics arrive as
     t per-tile partial sums (up to 256 tiles at <= 32 rows: a residual written by wr = 32 tiles of 8,192)."""
