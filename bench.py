@@ -100,6 +100,8 @@ def parse(argv=None):
     p.add_argument("--sequence-parallel", action="store_true", help="Megatron-SP prefill under --tp")
     p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                    help="cpu: reference-op engine over gloo (tests the multi-rank plumbing, not a measurement)")
+    p.add_argument("--decode-weights", default="auto", choices=("auto", "tiled", "single"),
+                   help="EngineConfig.decode_weight_layout (A/B: single = decode on the row-major weights)")
     p.add_argument("--kv-blocks", type=int, default=None,
                    help="KV pool blocks per replica (default: the HBM left after the weights; --same-device: enough "
                         "for one wave, so the ranks sharing the GPU do not each claim its HBM)")
@@ -201,6 +203,7 @@ def serve_timed(args, rank, world, dev, on_gpu):
                        num_kv_blocks=kv_blocks, max_latency_ms=args.max_latency_ms, use_cuda_graph=not args.no_graph,
                        graph_batch_sizes=[1, 2, 4, 8, 16, 24, 32, args.batch],
                        async_decode=not args.no_async_decode, tuned_gemm_table=not args.no_gemm_table,
+                       decode_weight_layout=args.decode_weights,
                        **({"decode_window": args.decode_window} if args.decode_window else {}))
     t_init = time.perf_counter()
     tp = None

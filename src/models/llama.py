@@ -234,7 +234,9 @@ class CausalLM:
         decode GEMM — logits are computed for the sampled rows, in <= 128-row chunks). Returns whether packed."""
         if self.lm_head_tile is not None:
             return True
-        if not (self.tiled_decode_weights and self.device.type == "cuda" and ops.native_available()):
+        # packed in place (no second copy), so even a model that keeps its layers row-major for KV capacity
+        # (EngineConfig.decode_weight_layout = single) gets the tile-order head and its greedy candidates
+        if not (self.device.type == "cuda" and ops.native_available()):
             return False
         rows, k = self.lm_head.shape
         for wr, kc in self.LM_HEAD_TILES:
@@ -576,12 +578,13 @@ class CausalLM:
         # the fused attention stages sk x (G + 2) slab rows of 512 B (+ 2 KiB) in its 27 KiB merge
         # area (V3_MERGE_BYTES): at most 50 rows
         g = max(1, self.hq // self.hkv)
-        qkv = ops.decode_tile(self.layers[0].qkv.shape[0], h, 2, b, max_sk=max(1, 50 // (g + 2)))
+        rm = not getattr(self, "tiled_decode_weights", True)  # decode streams the row-major weights by choice (KV capacity)
+        qkv = ops.decode_tile(self.layers[0].qkv.shape[0], h, 2, b, max_sk=max(1, 50 // (g + 2)), row_major=rm)
         # residual-updating split-K (mode 3); under TP the same tiles carry the one-shot exchange of each column
         # tile in their last arrivers' epilogue (one launch per row-parallel projection) where the group allows
         # it (TPContext.fused_row_parallel), else bf16 partial sums (mode 0) for a separate all-reduce launch
-        o = ops.decode_tile(h, self.hq * d, 3, b)
-        down = ops.decode_tile(h, self.inter, 3, b) if not self.arch.is_moe else None
+        o = ops.decode_tile(h, self.hq * d, 3, b, row_major=rm)
+        down = ops.decode_tile(h, self.inter, 3, b, row_major=rm) if not self.arch.is_moe else None
         tp_fused = o_half = down_half = False
         if self.tp.enabled:
             fo = self._tp_fused_tile(h, self.hq * d, b, o) if not self.arch.is_moe else None
@@ -592,7 +595,7 @@ class CausalLM:
             else:
                 o = ops.decode_tile(h, self.hq * d, 0, b)
                 down = ops.decode_tile(h, self.inter, 0, b) if not self.arch.is_moe else None
-        gu = ops.decode_tile_silu(self.inter, h, b) if not self.arch.is_moe else None
+        gu = ops.decode_tile_silu(self.inter, h, b, row_major=rm) if not self.arch.is_moe else None
         return {"qkv": qkv, "o": o, "down": down, "gate_up": gu[:2] if gu else None,
                 "gate_up_sk": gu[2] if gu else 1, "tp_fused": tp_fused, "o_half": o_half, "down_half": down_half}
 

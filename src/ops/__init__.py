@@ -436,9 +436,13 @@ DECODE_SILU_SPLITK_CFG = {
 }
 
 
-def decode_tile_silu(n: int, k: int, bucket: int = 32):
+def decode_tile_silu(n: int, k: int, bucket: int = 32, row_major: bool = False):
     """(wr, kc, sk) of the norm-scaled SiLU gate/up decode GEMM: a split-K tile where one was measured faster,
-    else the full-K tile (sk = 1)."""
+    else the full-K tile (sk = 1). ``row_major``: on weights kept row-major (DECODE_TILE_CFG_RM)."""
+    if row_major:
+        c = DECODE_TILE_CFG_RM.get((n, k, 6, bucket)) or DECODE_TILE_CFG_RM.get((n, k, 4, bucket))
+        if c is not None:
+            return c
     # DIE_TILE_OVERRIDE entries with mode 6 name the split-K SiLU gate/up tile (N_out, K, 6, bucket) (in-graph A/Bs)
     c = DECODE_TILE_CFG.get((n, k, 6, bucket)) or DECODE_SILU_SPLITK_CFG.get((n, k, bucket))
     if c is not None:
@@ -595,10 +599,21 @@ _GENERIC_TILES = ((64, 128),(128, 64), (32, 128), (64, 64), (128, 32), (64, 32),
                   (128, 128))
 
 
-def decode_tile(n: int, k: int, mode: int, bucket: int = 32, max_sk: int = 8):
+# (N, K, mode, row bucket) -> (wr, kc, sk) where the decode GEMM streams the ROW-MAJOR weights by choice
+# (EngineConfig.decode_weight_layout = single: the KV pool is the constraint, no tile-order copies), measured with
+# bench/micro_tp_tiles.py --row-major; shapes not listed fall back to the tile-order table's choice
+DECODE_TILE_CFG_RM: dict = {}
+
+
+def decode_tile(n: int, k: int, mode: int, bucket: int = 32, max_sk: int = 8, row_major: bool = False):
     """(wr, kc, sk) of the decode GEMM for an [N, K] projection in ``mode`` (0 bf16, 1 / 4 SiLU, 2 slabs,
-    3 residual update) at steps of up to ``bucket`` rows (32, 64, 128)."""
+    3 residual update) at steps of up to ``bucket`` rows (32, 64, 128); ``row_major``: on weights kept row-major."""
     import math
+
+    if row_major:
+        c = DECODE_TILE_CFG_RM.get((n, k, mode, bucket))
+        if c is not None and c[2] <= max_sk:
+            return c
 
     c = DECODE_TILE_CFG.get((n, k, mode, bucket))
     # mode 3 writes one statistics tile per wr columns; its consumers take at most 128 of them
