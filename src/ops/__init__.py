@@ -602,11 +602,10 @@ _GENERIC_TILES = ((64, 128),(128, 64), (32, 128), (64, 64), (128, 32), (64, 32),
 # (N, K, mode, row bucket) -> (wr, kc, sk) where the decode GEMM streams the ROW-MAJOR weights by choice
 # (EngineConfig.decode_weight_layout = single: the KV pool is the constraint, no tile-order copies), measured with
 # bench/micro_tp_tiles.py --row-major; shapes not listed fall back to the tile-order table's choice
-DECODE_TILE_CFG_RM: dict = {
-    # Llama-3-8B, 32 rows (profiles/r6_8b_rm_tiles.jsonl, cold us; qkv / down keep the tile-order table's choice)
-    (4096, 4096, 3, 32): (64, 256, 4),     # o              14.44 vs 15.28 for (32, 256, 2)
-    (14336, 4096, 4, 32): (64, 256, 1),    # gate/up + SiLU 48.28 vs 53.68 for (128, 128, 1)
-}
+# Round 6, Llama-3-8B at 32 rows: the cold sweep's row-major winners (o (64, 256, 4) 14.44 vs 15.28 us, gate/up
+# (64, 256, 1) 48.28 vs 53.68, profiles/r6_8b_rm_tiles.jsonl) LOST in the graph — decode 3.96 vs 3.76 ms/step,
+# profiles/r6_decode_layout_rm_tiles_negative.jsonl — so the 8B shapes keep the tile-order table's tiles.
+DECODE_TILE_CFG_RM: dict = {}
 
 
 def decode_tile(n: int, k: int, mode: int, bucket: int = 32, max_sk: int = 8, row_major: bool = False):
