@@ -173,6 +173,7 @@ class PreprocPool:
         self.calls = 0
         self.items = 0
         self._pending: Dict[str, List[Tuple[Any, asyncio.Future]]] = {"enc": [], "dec": []}
+        self._tasks: set = set()  # in-flight pool calls (the loop keeps only weak references to tasks)
         self._scheduled: Dict[str, bool] = {"enc": False, "dec": False}
         # start every process now (and load its tokenizer): a cold spawn costs ~0.1-1 s
         warm = [self._pool.submit(_warm, self.path, vocab_size) for _ in range(processes)]
@@ -217,7 +218,9 @@ class PreprocPool:
         self._scheduled[kind] = False
         batch, self._pending[kind] = self._pending[kind], []
         for i in range(0, len(batch), self.max_batch):
-            asyncio.ensure_future(self._run(kind, batch[i:i + self.max_batch]))
+            t = asyncio.ensure_future(self._run(kind, batch[i:i + self.max_batch]))
+            self._tasks.add(t)
+            t.add_done_callback(self._tasks.discard)
 
     async def _run(self, kind: str, batch: List[Tuple[Any, asyncio.Future]]) -> None:
         items = [x for x, _ in batch]
