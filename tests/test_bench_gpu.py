@@ -39,6 +39,8 @@ def test_bench_node_section_rehearsal_two_ranks_one_gpu():
     cross = n["cross_gpu"]
     assert res["cross_gpu_status"] == "ok" and cross["status"] == 0, cross
     assert cross["xgpu_probe"]["kv_hop"]["per_rank"][1]["receiver_bytes_match"] is True, cross["xgpu_probe"]
+    frp = cross["xgpu_probe"]["ipc_allreduce"]["fused_row_parallel"]["rehearsal"]  # fused vs separate one-shot
+    assert frp["fused_us"] > 0 and frp["separate_one_shot_us"] > 0 and "half_ring" in frp, frp
     d = cross["disagg"]
     assert d["pairs"] == 1 and d["kv_path"] == "direct" and d["req_s_total"] > 0, d
     ab = d["per_pair"][0]["transport_ab"]  # shader stores (direct) vs copy engines (staged): both served

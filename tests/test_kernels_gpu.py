@@ -940,3 +940,28 @@ def test_half_ring_residual_gemm_matches_full_ring(dev, n, k, wr, kc, sk, rows):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     want = r0.float() + x.float() @ w.float().t()
     assert float((outs[1][0].float() - want).abs().max()) < 0.1
+
+
+def test_tp8_shard_plan_takes_the_half_ring_on_real_occupancy():
+    """at the 70B TP=8 tile counts (N = 8,192, wr = 32, grid = 256) the fused exchange is taken only
+    under the residency rule evaluated on the real occupancy of the exact instantiation (hipOccupancy...): one
+    workgroup per CU with the full LDS ring fails it, so the plan takes the half-LDS ring (two per CU)."""
+    from src.models.llama import CausalLM
+    from src.models.presets import get_preset
+    from src.parallel.custom_allreduce import fused_exchange_ok
+    from src.parallel.tp import TPContext
+
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+
+    class NodeTP(TPContext):  # one rank per GPU, the IPC path assumed up
+        def fused_row_parallel(self, n_tiles, grid=0, per_cu=0):
+            return fused_exchange_ok(n_tiles, grid, per_cu, 1, cus)
+
+    m = object.__new__(CausalLM)
+    m.arch = get_preset("llama3-70b")
+    m.tp = NodeTP(rank=0, world_size=8)
+    m.hq, m.hkv, m.head_dim, m.inter = 8, 1, 128, 28672 // 8
+    m.layers = [type("L", (), {"qkv": torch.empty(1280, 8192, device="meta")})()]
+    assert ops.gd_occupancy(3, 32, 128, 1, 32, False) == 1 and ops.gd_occupancy(3, 32, 256, 1, 32, False) == 1
+    p = m.decode_plan(32)
+    assert p["tp_fused"] and p["o"][0] == 32 and p["down"][0] == 32 and p["o_half"] and p["down_half"], p
