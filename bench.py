@@ -94,6 +94,8 @@ def parse(argv=None):
     p.add_argument("--no-async-decode", action="store_true", help="synchronous decode windows (A/B)")
     p.add_argument("--temperature", type=float, default=0.0)
     p.add_argument("--no-gemm-table", action="store_true", help="prefill GEMMs on the library defaults (A/B)")
+    p.add_argument("--no-gemm-residual", action="store_true",
+                   help="prefill o / down written out and added by the norm pass instead of in the GEMM epilogue (A/B)")
     p.add_argument("--decode-window", type=int, default=None, help="decode steps per hipGraph window (engine default)")
     p.add_argument("--tp", type=int, default=1, help="tensor-parallel degree per replica (70B: --tp 8)")
     p.add_argument("--moe-parallel", choices=["tp", "ep"], default="tp", help="MoE layout under --tp")
@@ -227,6 +229,8 @@ def serve_timed(args, rank, world, dev, on_gpu):
     else:
         engine = LLMEngine.from_preset(args.preset, device=dev, cfg=cfg, max_model_len=args.max_model_len,
                                        seed=1234, capture=not args.no_graph)
+        if args.no_gemm_residual:
+            engine.model.prefill_gemm_residual = False
     engine.eos_token_id = None
     init_s = time.perf_counter() - t_init
     aeng = AsyncLLMEngine(engine)
@@ -528,6 +532,7 @@ def main(argv=None) -> int:
                 "weights": "random-init",
                 "hip_graph_decode": not args.no_graph,
                 "prefill_gemm_table": not args.no_gemm_table,
+                "prefill_gemm_residual": not args.no_gemm_residual,
             },
             "notes": {
                 "baseline": "reference publishes no numbers and has no GPU path (BASELINE.md); vs_baseline=null",

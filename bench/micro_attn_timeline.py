@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--ctx", type=int, default=0, help="every sequence's context (0: 512 + 4 i)")
     ap.add_argument("--max-ctx", type=int, default=2048)
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--sk", type=int, default=0, help="qkv split-K slabs the prologue sums (0: the engine's tile)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     n, bs, d = a.batch, 16, 128
@@ -42,7 +43,7 @@ def main():
     bts = [torch.arange(c * n * per_seq, (c + 1) * n * per_seq, device=dev, dtype=torch.int32).view(n, per_seq)
            for c in range(copies)]
     width = (hq + 2 * hkv) * d
-    sk = 2
+    sk = a.sk or ops.decode_tile(width, hid, 2)[2]
     slab = torch.randn(sk, n, width, device=dev) * 0.7
     ssp = torch.zeros(hid // 64, ops.SSP_LD, device=dev)
     ssp[:, :n] = float(hid) / ssp.shape[0]
@@ -83,7 +84,7 @@ def main():
     res = {k: [] for k in ("span", "first_chunk", "prologue", "stream", "merge_out", "start_skew", "tail")}
     for c in range(2, copies):
         tt = t[c]
-        used = tt[:, 4] > 0
+        used = tt[:, 3] > 0  # workgroups that ran a task (a tensor-parallel shard leaves some without one)
         tt = tt[used]
         t0 = tt[:, 0].min()
         res["span"].append(float(tt[:, 4].max() - t0) * 10e-3)
@@ -98,7 +99,8 @@ def main():
     out["us_per_call"] = round(us_call, 2)
     out["kv_TBps_call"] = round(kv_bytes / us_call / 1e6, 2)
     print(json.dumps({"bench": "attn_decode_timeline", "shape": a.shape, "batch": n, "ctx": [ctxs[0], ctxs[-1]],
-                      "max_ctx": max_ctx, **out}), flush=True)
+                      "max_ctx": max_ctx, "qkv_sk": sk, "workgroups_with_a_task": int((t[-1][:, 3] > 0).sum()),
+                      **out}), flush=True)
 
 
 if __name__ == "__main__":

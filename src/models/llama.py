@@ -119,6 +119,7 @@ class CausalLM:
         self.sequence_parallel = bool(sequence_parallel and self.tp.enabled)
         self.tiled_decode_weights = True  # decode GEMMs on tile-order copies (pack_decode_weights)
         self.lm_head_tile = None          # (wr, kc) once the LM head is re-laid in place in tile order
+        self.prefill_gemm_residual = True  # TP=1 prefill: o / down add into the residual in the GEMM (beta = 1)
         self.layers: List[LayerWeights] = []
         self._init_random(seed, init_std)
         self.cos_sin = rope_cos_sin(self.max_position, a.head_dim, a.rope_theta, self.device, a.rope_scaling)
@@ -419,6 +420,9 @@ class CausalLM:
         up. No normalised copy of the residual is written or read back: two [T, hidden] bf16 passes less per
         norm. Mixtral keeps its explicit ln2 (it also feeds the router)."""
         a, eps = self.arch, self.arch.rms_eps
+        # one GPU (no all-reduce between a projection and its residual add): o and down add into the residual in
+        # the GEMM epilogue, and the norm pass only reads the residual for its statistics
+        gemm_resid = self.prefill_gemm_residual and not self.tp.enabled and not a.is_moe
         rs = ops.rms_row_scale(residual, None, eps)
         h = None
         last = len(self.layers) - 1
@@ -430,6 +434,12 @@ class CausalLM:
             attn = self._attention(li, lw, residual, positions, meta, kv_pool, rs=rs)
             if meta.kv_hook is not None:
                 meta.kv_hook(li)
+            if gemm_resid:
+                ops.linear_residual(residual, attn, lw.o)
+                rs2 = ops.rms_row_scale(residual, None, eps)
+                act = ops.silu_and_mul(ops.linear(residual, lw.gate_up), row_scale=rs2)
+                ops.linear_residual(residual, act, lw.down)
+                continue
             o = self.tp.all_reduce(ops.linear(attn, lw.o))
             if a.is_moe:
                 x = ops.fused_add_rms_norm(o, residual, lw.ln2, eps)
@@ -438,6 +448,8 @@ class CausalLM:
                 rs2 = ops.rms_row_scale(residual, o, eps)
                 act = ops.silu_and_mul(ops.linear(residual, lw.gate_up), row_scale=rs2)
                 h = self.tp.all_reduce(ops.linear(act, lw.down))
+        if h is None:
+            return ops.rms_norm(residual, self.norm, eps)
         return ops.fused_add_rms_norm(h, residual, self.norm, eps)
 
     def _last_layer_kept_rows(self, lw: LayerWeights, x: torch.Tensor, residual: torch.Tensor,

@@ -305,11 +305,6 @@ def gemm_decode(x: torch.Tensor, w: torch.Tensor, mode: int = 0, wr: int = 64, s
     return out
 
 
-def gd_kc(wr: int) -> int:
-    """K elements per ring slot of the decode GEMM for a legacy weight-row code `wr` (gemm_decode.hip)."""
-    return gd_tile(wr)[1]
-
-
 def gd_swizzle(r: torch.Tensor, kc: int) -> torch.Tensor:
     """16-byte chunk swizzle of LDS-image row r for a K slot of kc elements (gemm_decode.hip swz())."""
     rowb = 2 * kc
@@ -664,10 +659,6 @@ def _bucket(m: int) -> int:
     return 32 if m <= 32 else (64 if m <= 64 else 128)
 
 
-def decode_slab_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    return _decode_gemm_ok(x, w) and w.shape[0] % 32 == 0 and w.shape[0] <= DECODE_GEMM_MAX_N
-
-
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = x @ w^T. Decode-sized M (<= 128 rows) runs on the weight-streaming
     gfx950 kernel (gemm_decode.hip); larger M goes to hipBLASLt."""
@@ -675,6 +666,15 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
         wr, kc, _ = decode_tile(w.shape[0], x.shape[1], 0, _bucket(x.shape[0]))
         return gemm_decode(x, w, 0, wr, 1, out, kc=kc)
     return torch.nn.functional.linear(x, w, out=out) if out is not None else torch.nn.functional.linear(x, w)
+
+
+def linear_residual(resid: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """resid += x @ w^T in place through the library GEMM's C input (beta = 1): the prefill o / down projections
+    add into the residual stream in their epilogue (fp32 accumulator + bf16 C, one rounding) instead of writing
+    a [T, hidden] output that a separate pass reads back with the residual. Same TN signature as
+    :func:`linear`, so the prefill GEMM table's solution applies. Prefill sizes only (the decode GEMM has its
+    own residual epilogue, :func:`linear_slab_residual`)."""
+    return resid.addmm_(x, w.t())
 
 
 def linear_tiled(x: torch.Tensor, w: torch.Tensor, wr: int, kc: int) -> torch.Tensor:

@@ -195,6 +195,50 @@ def test_rms_row_scale(dev, t, h, add):
     close(rs, torch.rsqrt(expect.float().pow(2).mean(-1) + 1e-5), atol=1e-5, rtol=1e-4)
 
 
+@pytest.mark.parametrize("t,n,k", [(2048, 4096, 4096), (300, 4096, 14336), (129, 1024, 512)])
+def test_linear_residual(dev, t, n, k):
+    """Prefill o / down with the residual add in the GEMM epilogue (beta = 1, in place) against fp32
+    resid + x @ w^T, rounded once."""
+    res = torch.randn(t, n, device=dev, dtype=torch.bfloat16) * 2
+    x = torch.randn(t, k, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(n, k, device=dev, dtype=torch.bfloat16) / math.sqrt(k)
+    want = res.float() + x.float() @ w.float().t()
+    ptr = res.data_ptr()
+    out = ops.linear_residual(res, x, w)
+    assert out.data_ptr() == ptr == res.data_ptr()
+    close(res, want, atol=2e-2, rtol=1e-2)
+
+
+def test_prefill_gemm_residual_matches_norm_pass_add(dev):
+    """llama-mini prefill (> 128 tokens: the row-scale path): o / down added in the GEMM epilogue vs written out
+    and added by the norm pass — the same hidden states up to one bf16 rounding per add."""
+    from src.models.llama import AttnMetadata, CausalLM
+    from src.models.presets import get_preset
+
+    m = CausalLM(get_preset("llama-mini"), "cuda:0", seed=3, max_position=1024, full_init=True)
+    assert m.norms_folded
+    t = 300
+    nb = (t + 15) // 16
+    g = torch.Generator(device="cuda:0").manual_seed(1)
+    ids = torch.randint(3, 32000, (t,), device=dev, generator=g)
+    pos = torch.arange(t, device=dev)
+    hidden, pools = {}, {}
+    for flag in (True, False):
+        m.prefill_gemm_residual = flag
+        pool = torch.zeros(m.arch.num_layers, 2, nb, m.hkv, 16, 128, dtype=m.dtype, device=dev)
+        meta = AttnMetadata(True, pos.clone(), torch.arange(nb, dtype=torch.int32, device=dev)[None],
+                            torch.tensor([t], dtype=torch.int32, device=dev),
+                            torch.tensor([0, t], dtype=torch.int32, device=dev), t)
+        assert m._prefill_row_scale(torch.empty(t, 1, device=dev), meta)
+        hidden[flag], pools[flag] = m.forward(ids, pos, meta, pool).float(), pool.float()
+    # layer 0's K / V come before any residual add: identical; later layers and the output within bf16 noise
+    assert torch.equal(pools[True][0], pools[False][0])
+    close(pools[True], pools[False], atol=6e-2, rtol=5e-2)
+    close(hidden[True], hidden[False], atol=8e-2, rtol=5e-2)
+    rel = (hidden[True] - hidden[False]).norm() / hidden[False].norm()
+    assert rel < 2e-2, rel
+
+
 def test_silu_and_mul_row_scale(dev):
     t, inter = 37, 3584
     x = torch.randn(t, 2 * inter, device=dev, dtype=torch.bfloat16) * 4
