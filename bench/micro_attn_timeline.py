@@ -43,7 +43,7 @@ def main():
     bts = [torch.arange(c * n * per_seq, (c + 1) * n * per_seq, device=dev, dtype=torch.int32).view(n, per_seq)
            for c in range(copies)]
     width = (hq + 2 * hkv) * d
-    sk = a.sk or ops.decode_tile(width, hid, 2)[2]
+    sk = a.sk or ops.decode_tile(width, hid, 2, max_sk=max(1, 50 // (g + 2)))[2]  # as CausalLM picks it
     slab = torch.randn(sk, n, width, device=dev) * 0.7
     ssp = torch.zeros(hid // 64, ops.SSP_LD, device=dev)
     ssp[:, :n] = float(hid) / ssp.shape[0]
