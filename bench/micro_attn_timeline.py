@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--ctx", type=int, default=0, help="every sequence's context (0: 512 + 4 i)")
     ap.add_argument("--max-ctx", type=int, default=2048)
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--static-parts", action="store_true", help="A/B: the static split also for few pairs")
     ap.add_argument("--sk", type=int, default=0, help="qkv split-K slabs the prologue sums (0: the engine's tile)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -54,7 +55,7 @@ def main():
     pm = torch.empty(n * hq * maxp * 2, device=dev)
     cnt = torch.zeros(n * hkv, dtype=torch.int32, device=dev)
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    ts = torch.zeros(copies, ncu * 6, dtype=torch.int64, device=dev)
+    ts = torch.zeros(copies, 2 * ncu * 6, dtype=torch.int64, device=dev)  # grids of up to 2 workgroups per CU
     kv_bytes = sum(ctxs) * hkv * d * 2 * 2
 
     def call(c):
@@ -66,6 +67,7 @@ def main():
         call(c)
     torch.cuda.synchronize()
     k_ = ops._kern()
+    k_.attn_set_few_pair_parts(not a.static_parts)
     for c in range(copies):
         k_.attn_set_timestamps(ts[c])
         call(c)
@@ -80,7 +82,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     us_call = e0.elapsed_time(e1) * 1e3 / (reps * copies)
-    t = ts.view(copies, ncu, 6).cpu().double()
+    t = ts.view(copies, 2 * ncu, 6).cpu().double()
     res = {k: [] for k in ("span", "first_chunk", "prologue", "stream", "merge_out", "start_skew", "tail")}
     for c in range(2, copies):
         tt = t[c]

@@ -25,6 +25,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+from src import ops  # noqa: E402
 from src.config import EngineConfig  # noqa: E402
 from src.parallel.tp import ShardProbeTP  # noqa: E402
 from src.parallel.tp_runner import build_tp_engine  # noqa: E402
@@ -45,9 +46,14 @@ def main(argv=None):
     ap.add_argument("--decode-window", type=int, default=8, help="EngineConfig.decode_window (1: single steps, A/B)")
     ap.add_argument("--legacy-fused", action="store_true",
                     help="A/B: round 5's fused-exchange rule (the table tile with its full LDS ring, zero slack)")
+    ap.add_argument("--attn-static-parts", action="store_true",
+                    help="A/B: decode attention split statically for few pairs too (ops.set_attn_few_pair_parts)")
+    ap.add_argument("--max-model-len", type=int, default=0, help="engine bound (0: prompt + gen + 64)")
     a = ap.parse_args(argv)
     on_gpu = a.device.startswith("cuda")
-    mlen = a.prompt_len + a.gen_len + 64
+    if a.attn_static_parts:
+        ops.set_attn_few_pair_parts(False)
+    mlen = a.max_model_len or a.prompt_len + a.gen_len + 64
     cfg = EngineConfig(max_num_seqs=a.batch, max_num_batched_tokens=max(16384, a.prompt_len), max_latency_ms=0.0,
                        graph_batch_sizes=sorted({1, 2, 4, 8, 16, 24, 32, a.batch}), decode_window=a.decode_window)
     t0 = time.perf_counter()

@@ -554,6 +554,8 @@ void gd_set_timestamps(Tensor t) {
   g_gd_ts = t.numel() ? reinterpret_cast<long long*>(t.data_ptr<int64_t>()) : nullptr;
 }
 
+void attn_set_few_pair_parts(bool on) { die::attn_set_few_pair_parts(on); }
+
 void attn_set_timestamps(Tensor t) {
   die::attn_set_timestamps(t.numel() ? reinterpret_cast<long long*>(t.data_ptr<int64_t>()) : nullptr);
 }
@@ -1043,6 +1045,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("rms_row_scale", &rms_row_scale);
   m.def("gd_set_timestamps", &gd_set_timestamps);
   m.def("attn_set_timestamps", &attn_set_timestamps);
+  m.def("attn_set_few_pair_parts", &attn_set_few_pair_parts);
   m.def("row_sumsq", &row_sumsq);
   m.def("residual_add_sumsq", &residual_add_sumsq);
   m.def("decode_advance", &decode_advance);

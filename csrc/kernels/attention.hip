@@ -789,6 +789,8 @@ hipError_t launch_attn_prefill(bf16_t* out, const bf16_t* q, int64_t q_stride, c
 
 static long long* g_attn_ts = nullptr;
 void attn_set_timestamps(long long* ts) { g_attn_ts = ts; }
+static bool g_few_pair_parts = true;
+void attn_set_few_pair_parts(bool on) { g_few_pair_parts = on; }
 
 hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* counters, const bf16_t* q,
                               int64_t q_stride, bf16_t* k_cache, bf16_t* v_cache, const int* block_tables,
@@ -811,12 +813,17 @@ hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* c
     const int pairs = num_seqs * hkv;
     const int tasks = pairs * maxp3;
     const int ncu = num_cus();
-    dim3 grid(tasks < ncu ? tasks : ncu), block(256);
-    // chunks per part, from the static max context: pairs x parts ~ the grid. (Single-chunk parts for the few
-    // pairs of a tensor-parallel shard — Llama-3-70B TP=8: 32 at batch 32, two tasks per workgroup — measured
-    // neutral: 12.69 vs 12.75 us per layer, the part's time is a chain of dependent round trips, not its
-    // CU's bandwidth; profiles/r5_tp8_attn_single_chunk_parts.txt)
-    const int cpp = std::max(1, std::min(maxp3, (maxp3 * pairs + (int)grid.x - 1) / (int)grid.x));
+    // chunks per part, from the static max context: pairs x parts ~ the grid (one task per workgroup, so a
+    // workgroup never walks on to a second task after its own).
+    // Few pairs (a tensor-parallel shard: Llama-3-70B TP=8 has 32 at batch 32) with a short static bound: one
+    // chunk per part and one workgroup per task, up to two per CU. The parts past a sequence's context are
+    // empty workgroups that exit at once, dispatched behind (or beside) the real ones, which start on the CUs
+    // the 2-chunk split left idle (96 -> 160 of 256 busy at context 576): attention 13.4 -> 12.1-12.4 us
+    // (bench/micro_attn_timeline.py). Round 5 tried single-chunk parts as TWO tasks per workgroup: neutral in the
+    // graph (12.69 vs 12.75 us), each real workgroup paid the empty second task's check before it could exit.
+    const bool few = g_few_pair_parts && pairs * 4 <= ncu && tasks <= 2 * ncu;
+    dim3 grid(few ? tasks : (tasks < ncu ? tasks : ncu)), block(256);
+    const int cpp = few ? 1 : std::max(1, std::min(maxp3, (maxp3 * pairs + (int)grid.x - 1) / (int)grid.x));
     AttnDecodeFuse none{};
     none.ts = g_attn_ts;
     AttnDecodeFuse fzc{};

@@ -59,6 +59,7 @@ struct AttnDecodeFuse {
   long long* ts = nullptr;          // diagnostics: per-workgroup phase stamps [6] (s_memrealtime) or null
 };
 void attn_set_timestamps(long long* ts);  // diagnostics: stamps for every following decode launch
+void attn_set_few_pair_parts(bool on);  // decode launch policy for few (sequence, kv head) pairs (default on)
 hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* counters, const bf16_t* q,
                               int64_t q_stride, bf16_t* k_cache, bf16_t* v_cache, const int* block_tables,
                               int bt_stride, const int* ctx_lens, int num_seqs, int max_ctx, int hq, int hkv,

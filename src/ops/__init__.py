@@ -93,6 +93,13 @@ def silu_and_mul_views(gate: torch.Tensor, up: torch.Tensor, out: torch.Tensor,
     return out
 
 
+def set_attn_few_pair_parts(on: bool) -> None:
+    """Decode attention launch policy for few (sequence, kv head) pairs (tensor-parallel shards) at a short static
+    context bound: one chunk per part, one workgroup per task (default on; off = the static split, for A/Bs)."""
+    if native_available():
+        _kern().attn_set_few_pair_parts(bool(on))
+
+
 def rms_row_scale(resid: torch.Tensor, x: Optional[torch.Tensor], eps: float,
                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Prefill RMSNorm as a row scale (norm weight folded into the consuming projection): resid += x (bf16,
