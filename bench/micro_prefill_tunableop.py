@@ -40,6 +40,9 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--models", default="8b,8b_tp2,70b_tp8,70b")
     ap.add_argument("--quick", action="store_true", help="8B at 16,384 tokens only")
+    ap.add_argument("--residual", action="store_true",
+                    help="the o / down projections only, as the one-GPU prefill runs them: resid += x @ w^T in place "
+                         "(ops.linear_residual, beta = 1)")
     a = ap.parse_args()
     import torch.cuda.tunable as tun
 
@@ -48,43 +51,52 @@ def main():
     for mdl in a.models.split(","):
         for m in (TOKENS[mdl][:1] if a.quick else TOKENS[mdl]):
             for proj, n, k in SHAPES[mdl]:
-                todo.append((mdl, proj, m, n, k))
+                if not a.residual or proj in ("o", "down"):
+                    todo.append((mdl, proj, m, n, k))
         if a.quick:
             break
+    def operands(m, n, k):
+        x = torch.randn(m, k, device=dev).to(torch.bfloat16)
+        w = (torch.randn(n, k, device=dev) * 0.02).to(torch.bfloat16)
+        r = torch.randn(m, n, device=dev).to(torch.bfloat16) if a.residual else None
+        return x, w, r
+
+    def gemm(x, w, r):
+        return r.addmm_(x, w.t()) if r is not None else torch.nn.functional.linear(x, w)
+
     base = {}
     for key in todo:
         _, _, m, n, k = key
-        x = torch.randn(m, k, device=dev).to(torch.bfloat16)
-        w = (torch.randn(n, k, device=dev) * 0.02).to(torch.bfloat16)
-        torch.nn.functional.linear(x, w)
+        x, w, r = operands(m, n, k)
+        gemm(x, w, r)
         torch.cuda.synchronize()
-        base[key] = timed(lambda: torch.nn.functional.linear(x, w))
-        del x, w
+        base[key] = timed(lambda: gemm(x, w, r))
+        del x, w, r
     tun.enable(True)
     tun.tuning_enable(True)
     tun.set_max_tuning_iterations(a.iters)
     tun.set_filename(a.out)
     for key in todo:
         _, _, m, n, k = key
-        x = torch.randn(m, k, device=dev).to(torch.bfloat16)
-        w = (torch.randn(n, k, device=dev) * 0.02).to(torch.bfloat16)
-        torch.nn.functional.linear(x, w)  # tunes this shape
+        x, w, r = operands(m, n, k)
+        gemm(x, w, r)  # tunes this shape
         torch.cuda.synchronize()
         print(json.dumps({"tuned": list(key)}), flush=True)  # progress (a long silence reads as a hang)
-        del x, w
+        del x, w, r
     tun.tuning_enable(False)
     for key in todo:
         mdl, proj, m, n, k = key
-        x = torch.randn(m, k, device=dev).to(torch.bfloat16)
-        w = (torch.randn(n, k, device=dev) * 0.02).to(torch.bfloat16)
-        t = timed(lambda: torch.nn.functional.linear(x, w))
+        x, w, r = operands(m, n, k)
+        t = timed(lambda: gemm(x, w, r))
         fl = 2 * m * n * k
         print(json.dumps({"bench": "prefill_tunableop", "model": mdl, "proj": proj, "M": m, "N": n, "K": k,
+                          "residual_beta1": a.residual,
                           "default_us": round(base[key], 1), "tuned_us": round(t, 1),
                           "default_PFs": round(fl / base[key] / 1e9, 3), "tuned_PFs": round(fl / t / 1e9, 3)}),
               flush=True)
-        del x, w
-    tun.write_file(a.out)
+        del x, w, r
+    if hasattr(tun, "write_file"):  # newer PyTorch writes the file named by set_filename at exit
+        tun.write_file(a.out)
 
 
 if __name__ == "__main__":
