@@ -22,7 +22,7 @@ def main():
     import argparse
 
     ap = argparse.ArgumentParser()
-    ap.add_argument("--shape", default="8b", choices=["8b", "70b_tp8"])
+    ap.add_argument("--shape", default="8b", choices=["8b", "70b_tp8", "8b_tp2"])
     ap.add_argument("--ctx", type=int, default=0, help="every sequence's context (0: 512 + 4 i)")
     ap.add_argument("--max-ctx", type=int, default=2048)
     ap.add_argument("--batch", type=int, default=32)
@@ -31,7 +31,7 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     n, bs, d = a.batch, 16, 128
-    hkv, g, hid = (8, 4, 4096) if a.shape == "8b" else (1, 8, 8192)
+    hkv, g, hid = {"8b": (8, 4, 4096), "70b_tp8": (1, 8, 8192), "8b_tp2": (4, 4, 4096)}[a.shape]
     hq = hkv * g
     ctxs = [a.ctx] * n if a.ctx else [512 + 4 * i for i in range(n)]
     max_ctx = a.max_ctx

@@ -821,6 +821,9 @@ hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* c
     // the 2-chunk split left idle (96 -> 160 of 256 busy at context 576): attention 13.4 -> 12.1-12.4 us
     // (bench/micro_attn_timeline.py). Round 5 tried single-chunk parts as TWO tasks per workgroup: neutral in the
     // graph (12.69 vs 12.75 us), each real workgroup paid the empty second task's check before it could exit.
+    // (Sizing the parts for two workgroups per CU below one pair per CU as well — the 8B TP=2 shard, 8B at batch 16 —
+    // was measured: neutral at the 2,048 bound, 7 % slower at 704, where it breaks the balanced 3 + 2-chunk split into
+    // 2 + 2 + 1: profiles/r6_attn_spread_negative.jsonl.)
     const bool few = g_few_pair_parts && pairs * 4 <= ncu && tasks <= 2 * ncu;
     dim3 grid(few ? tasks : (tasks < ncu ? tasks : ncu)), block(256);
     const int cpp = few ? 1 : std::max(1, std::min(maxp3, (maxp3 * pairs + (int)grid.x - 1) / (int)grid.x));
