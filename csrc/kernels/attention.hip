@@ -816,7 +816,7 @@ hipError_t launch_attn_decode(bf16_t* out, float* part_o, float* part_ml, int* c
     // chunks per part, from the static max context: pairs x parts ~ the grid (one task per workgroup, so a
     // workgroup never walks on to a second task after its own).
     // Few pairs (a tensor-parallel shard: Llama-3-70B TP=8 has 32 at batch 32) with a short static bound: one
-    // chunk per part and one workgroup per task, up to two per CU. The parts past a sequence's context are
+    // chunk per part and one workgroup per task (a grid of up to 2 x CUs; one resident per CU). The parts past a sequence's context are
     // empty workgroups that exit at once, dispatched behind (or beside) the real ones, which start on the CUs
     // the 2-chunk split left idle (96 -> 160 of 256 busy at context 576): attention 13.4 -> 12.1-12.4 us
     // (bench/micro_attn_timeline.py). Round 5 tried single-chunk parts as TWO tasks per workgroup: neutral in the
